@@ -1,0 +1,78 @@
+// Device execution plan: the step parameters the document kernels need, as a flat POD that the
+// host runtime builds from the validated pipeline config and uploads once per run.
+#pragma once
+#include "tb_common.h"
+
+namespace tb {
+
+constexpr int kMaxStageSteps = 8;
+constexpr int kMaxNgramEntries = 16;
+constexpr int kMaxStopChars = 16;
+constexpr int kMaxStopWords = 512;
+constexpr int kStopTableSize = 2048;  // power of two >= 2 * kMaxStopWords
+constexpr int kStopBlobBytes = 16384;
+
+enum DevStepKind : int32_t {
+  DK_NONE = 0,
+  DK_GOPHER_QUALITY = 1,
+  DK_GOPHER_REP = 2,
+  DK_FINEWEB = 3,
+  DK_LANGID = 4,   // featurize only (the head runs in its own kernel)
+};
+
+struct DevStep {
+  int32_t kind;
+  int32_t width;       // record width (int64 fields)
+  int64_t rec_base;    // element offset of this step's records = rec_prefix * ndocs (set per batch)
+  int32_t rec_prefix;  // sum of widths of earlier steps in the stage
+  // GopherQuality: stop-word set id (index into DevPlan::stops)
+  int32_t stop_set;
+  // GopherRepetition
+  int32_t n_top, n_dup;
+  int32_t top_n[kMaxNgramEntries];
+  int32_t dup_n[kMaxNgramEntries];
+  // FineWeb
+  int32_t n_stop_chars;
+  uint32_t stop_chars[kMaxStopChars];
+  int64_t short_line_length;
+};
+
+struct DevStopSet {
+  // open-addressing table of lowercase stop words: key (0 = empty) -> word index
+  uint64_t keys[kStopTableSize];
+  int32_t idx[kStopTableSize];
+  int32_t off[kMaxStopWords + 1];  // byte offsets into blob
+  int32_t n;
+  uint8_t blob[kStopBlobBytes];
+};
+
+struct DevC4 {
+  int32_t split_paragraph, remove_citations, filter_no_terminal_punct;
+  int32_t filter_lorem_ipsum, filter_javascript, filter_curly_bracket, filter_policy;
+  int64_t min_words_per_line, max_word_length;
+};
+
+struct DevStage {
+  int32_t n_steps;
+  int32_t width_total;  // sum of record widths
+  DevStep steps[kMaxStageSteps];
+};
+
+constexpr int kMaxStopSets = 4;
+
+struct DevPlan {
+  int32_t n_stop_sets;
+  DevStopSet stops[kMaxStopSets];
+};
+
+TB_HD uint64_t dev_key(uint64_t h, uint32_t len) {
+  uint64_t x = h ^ ((uint64_t)len * 0xD6E8FEB86659FD93ull);
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x | 1ull;
+}
+
+}  // namespace tb

@@ -1,0 +1,981 @@
+// Per-document analysis algorithms shared by the HIP kernels (WavePar) and the host emulation
+// (SeqPar). Everything a filter needs is derived from one decode + segmentation per content
+// version, with exact (byte-verified) duplicate detection:
+//
+//   decode          UTF-8 -> code points + packed properties              (reference: chars())
+//   prefix_hash     PH[i] = H(bytes[0..i)), so any substring hash is O(1)
+//   words           UAX#29 word segments, trimmed, kept iff they contain a non-PUNCTUATION,
+//                   non-whitespace char                 (reference utils/text.rs:103-181)
+//   canonicalize    smallest index with an equal element (hash table + byte verification)
+//   gopher_quality / gopher_repetition / fineweb / c4 / langid features  (reference filters)
+//
+// A 64-bit hash collision between unequal elements is never trusted: it raises DOC_NEEDS_CPU and
+// the host recomputes that document with the CPU oracle.
+#pragma once
+#include "devplan.h"
+#include "hash.h"
+#include "langid.h"
+#include "par.h"
+#include "uax29.h"
+#include "ucd.h"
+
+namespace tb {
+
+enum : uint32_t {
+  DOC_OK = 0,
+  DOC_NEEDS_CPU = 1,    // dictionary script / hash collision / scratch overflow
+  DOC_OVERFLOW = 2,
+};
+
+struct Cps {
+  uint32_t n = 0;
+  uint32_t* off = nullptr;   // [n+1] byte offset of each code point (off[n] = byte length)
+  uint32_t* cp = nullptr;    // [n]
+  uint32_t* prop = nullptr;  // [n]
+};
+
+struct CpsAcc {  // accessor for the UAX#29 rule templates over a sub-range
+  const uint32_t* prop;
+  TB_HD uint32_t p(int i) const { return prop[i]; }
+};
+
+struct Words {
+  uint32_t n = 0;
+  uint32_t* cs = nullptr;  // first code point
+  uint32_t* ce = nullptr;  // one past last code point
+  uint32_t* bs = nullptr;  // byte start
+  uint32_t* be = nullptr;  // byte end
+  uint8_t* alpha = nullptr;
+};
+
+struct Lines {  // Rust str::lines() in code point space
+  uint32_t n = 0;
+  uint32_t* ls = nullptr;  // start cp
+  uint32_t* le = nullptr;  // end cp (excludes '\n' and a '\r' right before it)
+};
+
+struct HL {
+  uint64_t h;
+  uint32_t len;
+  uint32_t pad;
+};
+
+template <class P>
+struct DocCtx {
+  P par;
+  UcdView ucd;
+  const uint64_t* pw = nullptr;  // pw[k] = B^k
+  uint32_t pw_n = 0;
+  char* scr = nullptr;
+  uint64_t cap = 0;
+  uint64_t used = 0;
+  uint32_t* flag = nullptr;  // per-document status word
+  bool overflow = false;
+
+  template <class T>
+  TB_HD T* alloc(uint64_t count) {
+    uint64_t a = (used + 15) & ~15ull;
+    uint64_t e = a + count * sizeof(T) + 16;
+    if (e > cap) {
+      overflow = true;
+      return (T*)scr;  // callers check `overflow` before using results
+    }
+    used = a + count * sizeof(T);
+    return (T*)(scr + a);
+  }
+  TB_HD void set_flag(uint32_t f) {
+    if (flag) *flag |= f;  // benign race: every writer stores the same bits
+  }
+  TB_HD uint64_t powb(uint32_t k) const { return k <= pw_n ? pw[k] : powmod61(kHashBase, k); }
+};
+
+TB_HD uint64_t sub_hash(const uint64_t* PH, const uint64_t* pw, uint32_t a, uint32_t b) {
+  uint64_t x = mulmod61(PH[a], pw[b - a]);
+  return PH[b] >= x ? PH[b] - x : PH[b] + kM61 - x;
+}
+
+TB_HD bool is_ws(uint32_t p) { return (p & P_WS) != 0; }
+TB_HD constexpr int rec_gr_fixed() { return 7; }
+
+// ---------------------------------------------------------------------------------------------
+template <class P>
+TB_HD Cps decode(DocCtx<P>& x, const uint8_t* b, uint32_t n) {
+  Cps c;
+  c.off = x.template alloc<uint32_t>(n + 1);
+  c.cp = x.template alloc<uint32_t>(n + 1);
+  c.prop = x.template alloc<uint32_t>(n + 1);
+  if (x.overflow) return c;
+  const UcdView ucd = x.ucd;
+  uint32_t* off = c.off;
+  uint32_t* cpa = c.cp;
+  uint32_t* pra = c.prop;
+  c.n = x.par.template compact<int>(
+      n, [&](uint32_t i, int&) { return utf8_is_lead(b[i]); },
+      [&](uint32_t i, uint32_t k, int&) {
+        int len;
+        uint32_t cp = utf8_decode(b, i, n, &len);
+        off[k] = i;
+        cpa[k] = cp;
+        pra[k] = ucd.props(cp);
+      });
+  const uint32_t cn = c.n;
+  x.par.single([&]() { off[cn] = n; });
+  x.par.sync();
+  return c;
+}
+
+template <class P>
+TB_HD uint64_t* prefix_hash(DocCtx<P>& x, const uint8_t* b, uint32_t n) {
+  uint64_t* PH = x.template alloc<uint64_t>(n + 1);
+  if (x.overflow) return PH;
+  const uint64_t* pw = x.pw;
+  const uint32_t pwn = x.pw_n;
+  HL tot = x.par.template scan<HL>(
+      n, HL{0, 0, 0},
+      [&](const HL& a, const HL& c) {
+        uint64_t m = c.len <= pwn ? pw[c.len] : powmod61(kHashBase, c.len);
+        return HL{addmod61(mulmod61(a.h, m), c.h), a.len + c.len, 0};
+      },
+      [&](uint32_t i) { return HL{(uint64_t)b[i] + 1, 1, 0}; },
+      [&](uint32_t i, const HL& e) { PH[i] = e.h; });
+  x.par.single([&]() { PH[n] = tot.h; });
+  x.par.sync();
+  return PH;
+}
+
+// UAX#29 word segments of code points [0, C) -> words (trimmed, with a word character).
+template <class P>
+TB_HD Words words(DocCtx<P>& x, const Cps& c) {
+  Words w;
+  const uint32_t C = c.n;
+  uint8_t* wb = x.template alloc<uint8_t>(C + 1);
+  w.cs = x.template alloc<uint32_t>(C + 1);
+  w.ce = x.template alloc<uint32_t>(C + 1);
+  w.bs = x.template alloc<uint32_t>(C + 1);
+  w.be = x.template alloc<uint32_t>(C + 1);
+  w.alpha = x.template alloc<uint8_t>(C + 1);
+  if (x.overflow) return w;
+  const uint32_t* prop = c.prop;
+  const uint32_t* off = c.off;
+  CpsAcc acc{prop};
+  x.par.for_n(C + 1, [&](uint32_t i) {
+    wb[i] = (i == 0 || i == C) ? 1 : (uint8_t)wb_break(acc, (int)C, (int)i);
+  });
+  x.par.sync();
+  struct St { uint32_t s, e; uint8_t a; };
+  uint32_t *cs = w.cs, *ce = w.ce, *bs = w.bs, *be = w.be;
+  uint8_t* al = w.alpha;
+  w.n = x.par.template compact<St>(
+      C,
+      [&](uint32_t i, St& st) {
+        if (!wb[i]) return false;
+        uint32_t e = i + 1;
+        while (!wb[e]) ++e;
+        uint32_t s = i;
+        while (s < e && is_ws(prop[s])) ++s;
+        uint32_t ee = e;
+        while (ee > s && is_ws(prop[ee - 1])) --ee;
+        bool has = false, alpha = false;
+        for (uint32_t k = s; k < ee; ++k) {
+          uint32_t p = prop[k];
+          if (!(p & P_PUNCT) && !(p & P_WS)) has = true;
+          if (p & P_ALPHA) alpha = true;
+        }
+        st.s = s;
+        st.e = ee;
+        st.a = alpha;
+        return has;
+      },
+      [&](uint32_t, uint32_t k, St& st) {
+        cs[k] = st.s;
+        ce[k] = st.e;
+        bs[k] = off[st.s];
+        be[k] = off[st.e];
+        al[k] = st.a;
+      });
+  x.par.sync();
+  return w;
+}
+
+// Rust str::lines() of the whole text, in code point space.
+template <class P>
+TB_HD Lines rust_lines(DocCtx<P>& x, const Cps& c) {
+  Lines L;
+  const uint32_t C = c.n;
+  L.ls = x.template alloc<uint32_t>(C + 1);
+  L.le = x.template alloc<uint32_t>(C + 1);
+  if (x.overflow) return L;
+  const uint32_t* cp = c.cp;
+  uint32_t* ls = L.ls;
+  uint32_t* le = L.le;
+  L.n = x.par.template compact<int>(
+      C, [&](uint32_t i, int&) { return i == 0 || cp[i - 1] == '\n'; },
+      [&](uint32_t i, uint32_t k, int&) { ls[k] = i; });
+  x.par.sync();
+  const uint32_t NL = L.n;
+  x.par.for_n(NL, [&](uint32_t k) {
+    uint32_t e = (k + 1 < NL) ? ls[k + 1] - 1 : (cp[C - 1] == '\n' ? C - 1 : C);
+    uint32_t ce = e;
+    if (e < C && ce > ls[k] && cp[ce - 1] == '\r') --ce;
+    le[k] = ce;
+  });
+  x.par.sync();
+  return L;
+}
+
+// canon[i] = smallest j with element j == element i (key() groups candidates, eq() verifies).
+template <class P, class KeyF, class EqF>
+TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t* canon) {
+  uint32_t capn = 16;
+  while (capn < 2 * n + 2) capn <<= 1;
+  const uint32_t mask = capn - 1;
+  const uint64_t mark = x.used;
+  uint64_t* keys = x.template alloc<uint64_t>(capn);
+  uint32_t* vals = x.template alloc<uint32_t>(capn);
+  if (x.overflow) return;
+  x.par.for_n(capn, [&](uint32_t i) { keys[i] = 0; vals[i] = 0xFFFFFFFFu; });
+  x.par.sync();
+  x.par.for_n(n, [&](uint32_t i) {
+    const uint64_t k = key(i);
+    uint32_t slot = (uint32_t)(k >> 17) & mask;
+    while (true) {
+      uint64_t old = P::cas64(&keys[slot], 0, k);
+      if (old == 0 || old == k) { P::min32(&vals[slot], i); break; }
+      slot = (slot + 1) & mask;
+    }
+  });
+  x.par.sync();
+  bool collided = false;
+  x.par.for_n(n, [&](uint32_t i) {
+    const uint64_t k = key(i);
+    uint32_t slot = (uint32_t)(k >> 17) & mask;
+    while (keys[slot] != k) slot = (slot + 1) & mask;
+    uint32_t c = vals[slot];
+    if (c != i && !eq(i, c)) { collided = true; c = i; }
+    canon[i] = c;
+  });
+  if (collided) x.set_flag(DOC_NEEDS_CPU);
+  x.par.sync();
+  x.used = mark;  // the table is scratch; canon[] lives in the caller's allocation
+}
+
+template <class P>
+TB_HD bool bytes_eq(const uint8_t* b, uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1) {
+  if (a1 - a0 != b1 - b0) return false;
+  for (uint32_t i = 0; i < a1 - a0; ++i) if (b[a0 + i] != b[b0 + i]) return false;
+  return true;
+}
+
+// find_duplicates over byte spans [s[i], e[i]): (#repeats, sum of repeat byte lengths).
+template <class P, class SpanF>
+TB_HD void dup_spans(DocCtx<P>& x, const uint8_t* b, const uint64_t* PH, uint32_t n, SpanF&& span,
+                     int64_t* out_elems, int64_t* out_bytes) {
+  const uint64_t mark = x.used;
+  uint32_t* canon = x.template alloc<uint32_t>(n + 1);
+  if (x.overflow) return;
+  const uint64_t* pw = x.pw;
+  canonicalize(
+      x, n,
+      [&](uint32_t i) {
+        uint32_t s, e;
+        span(i, s, e);
+        return dev_key(sub_hash(PH, pw, s, e), e - s);
+      },
+      [&](uint32_t i, uint32_t j) {
+        uint32_t s0, e0, s1, e1;
+        span(i, s0, e0);
+        span(j, s1, e1);
+        return bytes_eq<P>(b, s0, e0, s1, e1);
+      },
+      canon);
+  *out_elems = x.par.template sum<int64_t>(n, [&](uint32_t i) { return canon[i] != i ? (int64_t)1 : (int64_t)0; });
+  *out_bytes = x.par.template sum<int64_t>(n, [&](uint32_t i) {
+    if (canon[i] == i) return (int64_t)0;
+    uint32_t s, e;
+    span(i, s, e);
+    return (int64_t)(e - s);
+  });
+  x.used = mark;
+}
+
+// Lowercase (Rust str::to_lowercase on the word) hashed on the fly; optionally compared to `ref`.
+template <class F>
+TB_HD void lower_bytes(const UcdView& ucd, const uint32_t* cp, const uint32_t* prop, uint32_t s,
+                       uint32_t e, F&& push) {
+  uint8_t buf[4];
+  for (uint32_t k = s; k < e; ++k) {
+    uint32_t c = cp[k];
+    uint32_t lc;
+    if (c == 0x3A3) {
+      bool before = false, after = false;
+      for (uint32_t j = k; j > s; --j) {
+        uint32_t p = prop[j - 1];
+        if (p & P_CASE_IGN) continue;
+        before = (p & P_CASED) != 0;
+        break;
+      }
+      for (uint32_t j = k + 1; j < e; ++j) {
+        uint32_t p = prop[j];
+        if (p & P_CASE_IGN) continue;
+        after = (p & P_CASED) != 0;
+        break;
+      }
+      lc = (before && !after) ? 0x3C2 : 0x3C3;
+    } else {
+      lc = ucd.lower(c);
+    }
+    int nb = utf8_encode(lc, buf);
+    for (int q = 0; q < nb; ++q) push(buf[q]);
+    if (c == 0x130) { push(0xCC); push(0x87); }
+  }
+}
+
+TB_HD bool is_stop_word(const UcdView& ucd, const DevStopSet& ss, const uint32_t* cp,
+                        const uint32_t* prop, uint32_t s, uint32_t e) {
+  if (ss.n == 0) return false;
+  uint64_t h = 0;
+  uint32_t len = 0;
+  lower_bytes(ucd, cp, prop, s, e, [&](uint8_t v) { h = hash_push(h, v); ++len; });
+  const uint64_t key = dev_key(h, len);
+  uint32_t slot = (uint32_t)(key >> 17) & (kStopTableSize - 1);
+  while (true) {
+    const uint64_t k = ss.keys[slot];
+    if (k == 0) return false;
+    if (k == key) {
+      const int32_t w = ss.idx[slot];
+      const int32_t o0 = ss.off[w], o1 = ss.off[w + 1];
+      if ((uint32_t)(o1 - o0) != len) return false;
+      int32_t pos = o0;
+      bool ok = true;
+      lower_bytes(ucd, cp, prop, s, e, [&](uint8_t v) { ok = ok && ss.blob[pos++] == v; });
+      return ok;
+    }
+    slot = (slot + 1) & (kStopTableSize - 1);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Case-insensitive substring test as Rust `to_lowercase().contains(pat)` for an ASCII lowercase
+// pattern: ASCII letters fold, U+212A KELVIN SIGN lowercases to 'k'; no other code point
+// lowercases to a sequence that can match an ASCII-letter/space pattern.
+TB_HD bool ci_contains(const uint8_t* b, uint32_t n, const char* pat, int plen) {
+  for (uint32_t s = 0; s < n; ++s) {
+    uint32_t i = s;
+    int j = 0;
+    for (; j < plen; ++j) {
+      if (i >= n) break;
+      const char pc = pat[j];
+      uint8_t c = b[i];
+      if (c >= 'A' && c <= 'Z') c = (uint8_t)(c + 32);
+      if (c == (uint8_t)pc) { ++i; continue; }
+      if (pc == 'k' && i + 2 < n && b[i] == 0xE2 && b[i + 1] == 0x84 && b[i + 2] == 0xAA) { i += 3; continue; }
+      break;
+    }
+    if (j == plen) return true;
+  }
+  return false;
+}
+
+struct StageOut {
+  int64_t* rec;     // record buffer (all steps of the stage)
+  uint32_t ndocs;
+  uint32_t doc;
+  uint16_t* lid_vec;  // [ndocs][kLidDim] doc vectors (bf16) for the MFMA head
+  int32_t* lid_cnt;   // [ndocs] n-gram counts (0 = nothing to detect)
+};
+
+TB_HD uint64_t span_hash(uint64_t pa, uint64_t pb, uint64_t blen_pow) {
+  uint64_t x = mulmod61(pa, blen_pow);
+  return pb >= x ? pb - x : pb + kM61 - x;
+}
+
+// Sentence count of split_into_sentences() over code points [s, e) (already trimmed text).
+template <class P>
+TB_HD uint32_t count_sentences(DocCtx<P>& x, const Cps& c, uint32_t s, uint32_t e) {
+  const uint32_t m = e - s;
+  if (m == 0) return 0;
+  const uint64_t mark = x.used;
+  uint32_t* starts = x.template alloc<uint32_t>(m + 1);
+  if (x.overflow) return 0;
+  const uint32_t* prop = c.prop + s;
+  CpsAcc acc{prop};
+  const uint32_t NS = x.par.template compact<int>(
+      m, [&](uint32_t i, int&) { return i == 0 || sb_break(acc, (int)m, (int)i); },
+      [&](uint32_t i, uint32_t k, int&) { starts[k] = i; });
+  x.par.sync();
+  const uint32_t cnt = x.par.template sum<uint32_t>(NS, [&](uint32_t k) {
+    const uint32_t a = starts[k], bnd = k + 1 < NS ? starts[k + 1] : m;
+    for (uint32_t j = a; j < bnd; ++j) if (!is_ws(prop[j])) return 1u;
+    return 0u;
+  });
+  x.used = mark;
+  return cnt;
+}
+
+template <class P>
+TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, const Cps& c,
+                             const uint64_t* PH, const Words& w, int64_t* r) {
+  const uint32_t C = c.n;
+  const uint32_t* cp = c.cp;
+  const uint32_t* prop = c.prop;
+  const uint32_t* off = c.off;
+  const uint64_t* pw = x.pw;
+  const int width = ds.width;
+  const uint32_t tcs = x.par.template min<uint32_t>(C, C, [&](uint32_t i) { return is_ws(prop[i]) ? C : i; });
+  const uint32_t tce = x.par.template max<uint32_t>(C, 0u, [&](uint32_t i) { return is_ws(prop[i]) ? 0u : i + 1; });
+  if (tcs >= tce) {
+    x.par.single([&]() {
+      for (int k = 0; k < width; ++k) r[k] = 0;
+      r[0] = -1;
+    });
+    return;
+  }
+  const uint64_t mark = x.used;
+  const uint32_t span = tce - tcs;
+  uint32_t* rs = x.template alloc<uint32_t>(span + 1);
+  uint32_t* rl = x.template alloc<uint32_t>(span + 1);
+  uint32_t* prs = x.template alloc<uint32_t>(span + 1);
+  if (x.overflow) return;
+  const uint32_t NR = x.par.template compact<int>(
+      span,
+      [&](uint32_t i, int&) {
+        const uint32_t j = tcs + i;
+        return cp[j] == '\n' && cp[j - 1] != '\n';
+      },
+      [&](uint32_t i, uint32_t k, int&) {
+        uint32_t j = tcs + i, q = j;
+        while (cp[q] == '\n') ++q;
+        rs[k] = j;
+        rl[k] = q - j;
+      });
+  x.par.sync();
+  int64_t line_dup = 0, line_dup_b = 0, para_dup = 0, para_dup_b = 0;
+  dup_spans(x, b, PH, NR + 1,
+            [&](uint32_t k, uint32_t& s0, uint32_t& e0) {
+              const uint32_t cs = k == 0 ? tcs : rs[k - 1] + rl[k - 1];
+              const uint32_t ce = k == NR ? tce : rs[k];
+              s0 = off[cs];
+              e0 = off[ce];
+            },
+            &line_dup, &line_dup_b);
+  const uint32_t NPR = x.par.template compact<int>(
+      NR, [&](uint32_t k, int&) { return rl[k] >= 2; }, [&](uint32_t k, uint32_t q, int&) { prs[q] = k; });
+  x.par.sync();
+  dup_spans(x, b, PH, NPR + 1,
+            [&](uint32_t q, uint32_t& s0, uint32_t& e0) {
+              const uint32_t cs = q == 0 ? tcs : rs[prs[q - 1]] + rl[prs[q - 1]];
+              const uint32_t ce = q == NPR ? tce : rs[prs[q]];
+              s0 = off[cs];
+              e0 = off[ce];
+            },
+            &para_dup, &para_dup_b);
+  x.par.single([&]() {
+    r[0] = span;
+    r[1] = NPR + 1;
+    r[2] = para_dup;
+    r[3] = para_dup_b;
+    r[4] = NR + 1;
+    r[5] = line_dup;
+    r[6] = line_dup_b;
+  });
+  // ---- n-gram statistics over the words ----
+  const uint32_t W = w.n;
+  if (ds.n_top + ds.n_dup > 0) {
+    uint64_t* wh = x.template alloc<uint64_t>(W + 1);
+    uint32_t* wid = x.template alloc<uint32_t>(W + 1);
+    uint32_t* WL = x.template alloc<uint32_t>(W + 1);
+    uint64_t* PI = x.template alloc<uint64_t>(W + 1);
+    uint64_t* PW = x.template alloc<uint64_t>(W + 1);
+    if (x.overflow) return;
+    x.par.for_n(W, [&](uint32_t k) { wh[k] = sub_hash(PH, pw, w.bs[k], w.be[k]); });
+    x.par.sync();
+    canonicalize(
+        x, W, [&](uint32_t k) { return dev_key(wh[k], w.be[k] - w.bs[k]); },
+        [&](uint32_t i, uint32_t j) { return bytes_eq<P>(b, w.bs[i], w.be[i], w.bs[j], w.be[j]); }, wid);
+    const uint32_t totl = x.par.template scan<uint32_t>(
+        W, 0u, [](uint32_t a, uint32_t c2) { return a + c2; },
+        [&](uint32_t k) { return w.be[k] - w.bs[k]; }, [&](uint32_t k, uint32_t e) { WL[k] = e; });
+    const uint32_t pwn = x.pw_n;
+    auto hl_op = [&](const HL& a, const HL& c2) {
+      uint64_t m = c2.len <= pwn ? pw[c2.len] : powmod61(kHashBase, c2.len);
+      return HL{addmod61(mulmod61(a.h, m), c2.h), a.len + c2.len, 0};
+    };
+    HL ti = x.par.template scan<HL>(
+        W, HL{0, 0, 0}, hl_op, [&](uint32_t k) { return HL{(uint64_t)wid[k] + 1, 1, 0}; },
+        [&](uint32_t k, const HL& e) { PI[k] = e.h; });
+    HL tw = x.par.template scan<HL>(
+        W, HL{0, 0, 0}, hl_op, [&](uint32_t k) { return HL{wh[k], w.be[k] - w.bs[k], 0}; },
+        [&](uint32_t k, const HL& e) { PW[k] = e.h; });
+    x.par.single([&]() {
+      WL[W] = totl;
+      PI[W] = ti.h;
+      PW[W] = tw.h;
+    });
+    x.par.sync();
+    if (x.overflow) return;
+    for (int t = 0; t < ds.n_top; ++t) {
+      const uint32_t n = (uint32_t)ds.top_n[t];
+      int64_t res = 0;
+      if (n > 0 && W >= n) {
+        const uint32_t G = W - n + 1;
+        const uint64_t m2 = x.used;
+        uint32_t* gc = x.template alloc<uint32_t>(G);
+        uint32_t* cnt = x.template alloc<uint32_t>(G);
+        if (x.overflow) return;
+        const uint64_t pn = x.powb(n);
+        canonicalize(
+            x, G, [&](uint32_t p) { return dev_key(span_hash(PI[p], PI[p + n], pn), n); },
+            [&](uint32_t p, uint32_t q) {
+              for (uint32_t k = 0; k < n; ++k) if (wid[p + k] != wid[q + k]) return false;
+              return true;
+            },
+            gc);
+        x.par.for_n(G, [&](uint32_t p) { cnt[p] = 0; });
+        x.par.sync();
+        x.par.for_n(G, [&](uint32_t p) { P::add32(&cnt[gc[p]], 1u); });
+        x.par.sync();
+        const uint32_t maxc = x.par.template max<uint32_t>(G, 0u, [&](uint32_t p) { return cnt[p]; });
+        if (maxc > 1) {
+          const uint32_t maxlen = x.par.template max<uint32_t>(G, 0u, [&](uint32_t p) {
+            return cnt[p] == maxc ? (WL[p + n] - WL[p] + n - 1) : 0u;
+          });
+          res = (int64_t)maxlen * (int64_t)maxc;
+        }
+        x.used = m2;
+      }
+      x.par.single([&]() { r[rec_gr_fixed() + t] = res; });
+    }
+    if (ds.n_dup > 0) {
+      uint32_t* gcs[kMaxNgramEntries];
+      uint32_t* seen[kMaxNgramEntries];
+      for (int t = 0; t < ds.n_dup; ++t) {
+        const uint32_t n = (uint32_t)ds.dup_n[t];
+        gcs[t] = nullptr;
+        seen[t] = nullptr;
+        if (n == 0 || W < n) continue;
+        const uint32_t G = W - n + 1;
+        gcs[t] = x.template alloc<uint32_t>(G);
+        seen[t] = x.template alloc<uint32_t>((G + 31) / 32 + 1);
+        if (x.overflow) return;
+        uint32_t* sn = seen[t];
+        x.par.for_n((G + 31) / 32 + 1, [&](uint32_t i) { sn[i] = 0; });
+        canonicalize(
+            x, G,
+            [&](uint32_t p) {
+              const uint32_t L = WL[p + n] - WL[p];
+              return dev_key(span_hash(PW[p], PW[p + n], x.powb(L)), L);
+            },
+            [&](uint32_t p, uint32_t q) {
+              if (WL[p + n] - WL[p] != WL[q + n] - WL[q]) return false;
+              uint32_t wp = p, wq = q, bp = w.bs[p], bq = w.bs[q];
+              const uint32_t L = WL[p + n] - WL[p];
+              for (uint32_t i = 0; i < L; ++i) {
+                while (bp == w.be[wp]) { ++wp; bp = w.bs[wp]; }
+                while (bq == w.be[wq]) { ++wq; bq = w.bs[wq]; }
+                if (b[bp] != b[bq]) return false;
+                ++bp;
+                ++bq;
+              }
+              return true;
+            },
+            gcs[t]);
+      }
+      x.par.sync();
+      const int ndup = ds.n_dup;
+      x.par.for_n((uint32_t)ndup, [&](uint32_t t) {
+        const uint32_t n = (uint32_t)ds.dup_n[t];
+        int64_t rep = 0;
+        if (n > 0 && W >= n) {
+          const uint32_t* gc = gcs[t];
+          uint32_t* sn = seen[t];
+          uint32_t idx = 0;
+          while (idx + n <= W) {
+            const uint32_t g = gc[idx];
+            if ((sn[g >> 5] >> (g & 31)) & 1u) {
+              rep += (int64_t)(WL[idx + n] - WL[idx]);
+              idx += n;
+            } else {
+              sn[g >> 5] |= 1u << (g & 31);
+              ++idx;
+            }
+          }
+        }
+        r[rec_gr_fixed() + ds.n_top + t] = rep;
+      });
+      x.par.sync();
+    }
+  }
+  x.used = mark;
+}
+
+template <class P>
+TB_HD void langid_features(DocCtx<P>& x, const Cps& c, const uint16_t* emb, StageOut& out) {
+  const uint32_t lim = c.n < (uint32_t)kLidMaxCps ? c.n : (uint32_t)kLidMaxCps;
+  const uint32_t* cp = c.cp;
+  const uint32_t* prop = c.prop;
+  const UcdView ucd = x.ucd;
+  auto Lf = [&](int64_t i) -> uint32_t {
+    if (i < 0 || i >= (int64_t)lim) return 0;
+    if (!(prop[i] & P_ALPHA)) return 0;
+    uint32_t l = ucd.lower(cp[i]);
+    return l ? l : cp[i];
+  };
+  const uint64_t mark = x.used;
+  uint32_t* goff = x.template alloc<uint32_t>(lim + 2);
+  if (x.overflow) return;
+  const uint32_t K = x.par.template scan<uint32_t>(
+      lim + 1, 0u, [](uint32_t a, uint32_t b2) { return a + b2; },
+      [&](uint32_t i) { return (uint32_t)lid_grams_at(Lf((int64_t)i - 2), Lf((int64_t)i - 1), Lf(i), true, true, [](uint32_t) {}); },
+      [&](uint32_t i, uint32_t e) { goff[i] = e; });
+  uint32_t* G = x.template alloc<uint32_t>(K + 1);
+  if (x.overflow) return;
+  x.par.sync();
+  x.par.for_n(lim + 1, [&](uint32_t i) {
+    uint32_t o = goff[i];
+    lid_grams_at(Lf((int64_t)i - 2), Lf((int64_t)i - 1), Lf(i), true, true, [&](uint32_t bk) { G[o++] = bk; });
+  });
+  x.par.sync();
+  int64_t acc[kLidDim];
+  x.par.template gather_rows_fixed<kLidDim>(K, [&](uint32_t k) { return emb + (size_t)G[k] * kLidDim; }, acc);
+  const uint32_t doc = out.doc;
+  x.par.single([&]() {
+    out.lid_cnt[doc] = (int32_t)K;
+    for (int d = 0; d < kLidDim; ++d) {
+      float v = K ? (float)((double)acc[d] / (double)K / (double)kLidFixedScale) : 0.0f;
+      out.lid_vec[(size_t)doc * kLidDim + d] = f32_to_bf16(v);
+    }
+  });
+  x.used = mark;
+}
+
+// ---------------------------------------------------------------------------------------------
+// C4QualityFilter, pass A: decisions + rewritten text in scratch (reference c4_filters.rs:147-295).
+// rec: LOREM, CURLY, TOO_LONG, NO_PUNCT, TOO_FEW, SENTENCES, NEW_LEN
+// src: (byte offset of the new text in the doc's scratch, or -1 = unchanged original; length)
+TB_HD bool end_punct(uint32_t c) {
+  return c == '.' || c == '!' || c == '?' || c == '"' || c == '\'' || c == 0x201D;
+}
+
+template <class P>
+TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, int64_t* r, int64_t* src) {
+  const uint32_t lorem = c4.filter_lorem_ipsum
+      ? x.par.template sum<uint32_t>(n, [&](uint32_t s) {
+          if (b[s] != 'l' && b[s] != 'L') return 0u;
+          return ci_contains(b + s, n - s < 16 ? n - s : 16, "lorem ipsum", 11) ? 1u : 0u;
+        })
+      : 0u;
+  const uint32_t curly = c4.filter_curly_bracket
+      ? x.par.template sum<uint32_t>(n, [&](uint32_t i) { return (b[i] == '{' || b[i] == '}') ? 1u : 0u; })
+      : 0u;
+  if (lorem || curly) {
+    x.par.single([&]() {
+      r[0] = lorem > 0; r[1] = curly > 0; r[2] = r[3] = r[4] = r[5] = 0; r[6] = n;
+      src[0] = -1; src[1] = n;
+    });
+    return;
+  }
+  Cps c = decode(x, b, n);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  const uint32_t C = c.n;
+  const uint32_t* cp = c.cp;
+  const uint32_t* prop = c.prop;
+  const uint32_t* off = c.off;
+  if (x.par.template sum<uint32_t>(C, [&](uint32_t i) { return (prop[i] & P_DICT) ? 1u : 0u; })) {
+    x.set_flag(DOC_NEEDS_CPU);
+    return;
+  }
+  // ---- line spans [la, lb) in code points, trimmed ----
+  uint32_t* la = x.template alloc<uint32_t>(C + 1);
+  uint32_t* lb = x.template alloc<uint32_t>(C + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  uint32_t NLn = 0;
+  if (c4.split_paragraph) {
+    Lines L = rust_lines(x, c);
+    if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+    NLn = L.n;
+    x.par.for_n(NLn, [&](uint32_t k) {
+      uint32_t s = L.ls[k], e = L.le[k];
+      while (s < e && is_ws(prop[s])) ++s;
+      while (e > s && is_ws(prop[e - 1])) --e;
+      la[k] = s;
+      lb[k] = e;
+    });
+  } else {
+    const uint32_t tcs = x.par.template min<uint32_t>(C, C, [&](uint32_t i) { return is_ws(prop[i]) ? C : i; });
+    const uint32_t tce = x.par.template max<uint32_t>(C, 0u, [&](uint32_t i) { return is_ws(prop[i]) ? 0u : i + 1; });
+    if (tcs < tce) {
+      const uint32_t m = tce - tcs;
+      uint32_t* st = x.template alloc<uint32_t>(m + 1);
+      if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+      CpsAcc acc{prop + tcs};
+      const uint32_t NS = x.par.template compact<int>(
+          m, [&](uint32_t i, int&) { return i == 0 || sb_break(acc, (int)m, (int)i); },
+          [&](uint32_t i, uint32_t k, int&) { st[k] = i; });
+      x.par.sync();
+      struct SS { uint32_t s, e; };
+      NLn = x.par.template compact<SS>(
+          NS,
+          [&](uint32_t k, SS& ss) {
+            uint32_t s = tcs + st[k], e = tcs + (k + 1 < NS ? st[k + 1] : m);
+            while (s < e && is_ws(prop[s])) ++s;
+            while (e > s && is_ws(prop[e - 1])) --e;
+            ss.s = s;
+            ss.e = e;
+            return s < e;
+          },
+          [&](uint32_t, uint32_t q, SS& ss) { la[q] = ss.s; lb[q] = ss.e; });
+    }
+  }
+  x.par.sync();
+  // ---- citation removal -> processed line lengths ----
+  auto cite_end = [&](uint32_t j, uint32_t e) -> uint32_t {  // cp index past a citation at j, or 0
+    if (cp[j] != '[') return 0;
+    uint32_t p = j + 1;
+    if (p >= e || !(prop[p] & P_DIGIT)) return 0;
+    while (p < e && (prop[p] & P_DIGIT)) ++p;
+    while (p < e && cp[p] == ',') {
+      uint32_t q = p + 1;
+      while (q < e && (prop[q] & P_WS)) ++q;
+      if (q < e && (prop[q] & P_DIGIT)) {
+        while (q < e && (prop[q] & P_DIGIT)) ++q;
+        p = q;
+      } else {
+        break;
+      }
+    }
+    return (p < e && cp[p] == ']') ? p + 1 : 0;
+  };
+  uint32_t* plen = x.template alloc<uint32_t>(NLn + 1);
+  uint32_t* poff = x.template alloc<uint32_t>(NLn + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  const bool rmc = c4.remove_citations != 0;
+  x.par.for_n(NLn, [&](uint32_t k) {
+    uint32_t removed = 0;
+    if (rmc) {
+      for (uint32_t j = la[k]; j < lb[k];) {
+        uint32_t ce = cite_end(j, lb[k]);
+        if (ce) { removed += off[ce] - off[j]; j = ce; } else { ++j; }
+      }
+    }
+    plen[k] = off[lb[k]] - off[la[k]] - removed;
+  });
+  x.par.sync();
+  const uint32_t Ptot = x.par.template scan<uint32_t>(
+      NLn, 0u, [](uint32_t a, uint32_t b2) { return a + b2; }, [&](uint32_t k) { return plen[k] + 1; },
+      [&](uint32_t k, uint32_t e) { poff[k] = e; });
+  uint8_t* Pb = x.template alloc<uint8_t>(Ptot + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  x.par.for_n(NLn, [&](uint32_t k) {
+    uint32_t o = poff[k];
+    for (uint32_t j = la[k]; j < lb[k];) {
+      uint32_t ce = rmc ? cite_end(j, lb[k]) : 0;
+      if (ce) { j = ce; continue; }
+      for (uint32_t q = off[j]; q < off[j + 1]; ++q) Pb[o++] = b[q];
+      ++j;
+    }
+    Pb[o] = '\n';
+  });
+  x.par.single([&]() { poff[NLn] = Ptot; });
+  x.par.sync();
+  // ---- words of the processed lines ----
+  Cps pc = decode(x, Pb, Ptot);
+  Words pwd = words(x, pc);
+  uint32_t* nw = x.template alloc<uint32_t>(NLn + 1);
+  uint32_t* mx = x.template alloc<uint32_t>(NLn + 1);
+  uint8_t* code = x.template alloc<uint8_t>(NLn + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  x.par.for_n(NLn, [&](uint32_t k) { nw[k] = 0; mx[k] = 0; });
+  x.par.sync();
+  x.par.for_n(pwd.n, [&](uint32_t q) {
+    const uint32_t bs = pwd.bs[q];
+    uint32_t lo = 0, hi = NLn;  // last line with poff <= bs
+    while (hi - lo > 1) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (poff[mid] <= bs) lo = mid; else hi = mid;
+    }
+    P::add32(&nw[lo], 1u);
+    P::max32(&mx[lo], pwd.ce[q] - pwd.cs[q]);
+  });
+  x.par.sync();
+  const char* const kPol[6] = {"terms of use", "privacy policy", "cookie policy",
+                                      "uses cookies", "use of cookies", "use cookies"};
+  const int kPolLen[6] = {12, 14, 13, 12, 14, 11};
+  x.par.for_n(NLn, [&](uint32_t k) {
+    const uint8_t* lp = Pb + poff[k];
+    const uint32_t ln = plen[k];
+    uint8_t cd = 0;
+    if (c4.max_word_length > 0 && (int64_t)mx[k] > c4.max_word_length) {
+      cd = 1;
+    } else if (c4.filter_no_terminal_punct) {
+      bool term = false;
+      if (ln > 0) {
+        uint32_t st = ln - 1;
+        while (st > 0 && (lp[st] & 0xC0) == 0x80) --st;
+        int len;
+        term = end_punct(utf8_decode(lp, st, ln, &len));
+      }
+      const bool ell = ln >= 3 && lp[ln - 1] == '.' && lp[ln - 2] == '.' && lp[ln - 3] == '.';
+      if (!term || ell) cd = 2;
+    }
+    if (cd == 0 && c4.min_words_per_line > 0 && (int64_t)nw[k] < c4.min_words_per_line) cd = 3;
+    if (cd == 0 && c4.filter_javascript && ci_contains(lp, ln, "javascript", 10)) cd = 4;
+    if (cd == 0 && c4.filter_policy) {
+      for (int t = 0; t < 6; ++t)
+        if (ci_contains(lp, ln, kPol[t], kPolLen[t])) { cd = 5; break; }
+    }
+    code[k] = cd;
+  });
+  x.par.sync();
+  const int64_t s_long = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 1); });
+  const int64_t s_punct = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 2); });
+  const int64_t s_few = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 3); });
+  // ---- joined kept lines ----
+  uint32_t* joff = x.template alloc<uint32_t>(NLn + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  uint32_t Jtot = x.par.template scan<uint32_t>(
+      NLn, 0u, [](uint32_t a, uint32_t b2) { return a + b2; },
+      [&](uint32_t k) { return code[k] == 0 ? plen[k] + 1 : 0u; }, [&](uint32_t k, uint32_t e) { joff[k] = e; });
+  if (Jtot > 0) Jtot -= 1;
+  uint8_t* Jb = x.template alloc<uint8_t>(Jtot + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  x.par.for_n(NLn, [&](uint32_t k) {
+    if (code[k] != 0) return;
+    const uint32_t o = joff[k];
+    for (uint32_t q = 0; q < plen[k]; ++q) Jb[o + q] = Pb[poff[k] + q];
+    if (o + plen[k] < Jtot) Jb[o + plen[k]] = '\n';
+  });
+  x.par.sync();
+  Cps jc = decode(x, Jb, Jtot);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  const uint32_t JC = jc.n;
+  const uint32_t* jprop = jc.prop;
+  const uint32_t tcs = x.par.template min<uint32_t>(JC, JC, [&](uint32_t i) { return is_ws(jprop[i]) ? JC : i; });
+  const uint32_t tce = x.par.template max<uint32_t>(JC, 0u, [&](uint32_t i) { return is_ws(jprop[i]) ? 0u : i + 1; });
+  uint32_t nsent = 0, bstart = 0, blen = 0;
+  if (tcs < tce) {
+    nsent = count_sentences(x, jc, tcs, tce);
+    bstart = jc.off[tcs];
+    blen = jc.off[tce] - jc.off[tcs];
+  }
+  const int64_t jrel = (int64_t)((const char*)Jb - x.scr) + bstart;
+  x.par.single([&]() {
+    r[0] = 0; r[1] = 0; r[2] = s_long; r[3] = s_punct; r[4] = s_few; r[5] = nsent; r[6] = blen;
+    src[0] = jrel;
+    src[1] = blen;
+  });
+}
+
+// ---------------------------------------------------------------------------------------------
+// Stage analysis for one content version: writes the records of every step of the stage.
+
+template <class P>
+TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
+                         const uint16_t* lid_emb, const uint8_t* b, uint32_t n, StageOut& out) {
+  bool need_words = false, need_lines = false, need_ph = false, need_lid = false;
+  for (int s = 0; s < st.n_steps; ++s) {
+    const int k = st.steps[s].kind;
+    if (k == DK_GOPHER_QUALITY) need_words = need_lines = true;
+    if (k == DK_GOPHER_REP) need_words = need_ph = true;
+    if (k == DK_FINEWEB) need_words = need_lines = need_ph = true;
+    if (k == DK_LANGID) need_lid = true;
+  }
+  Cps c = decode(x, b, n);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  const uint32_t C = c.n;
+  // Documents with dictionary-segmented scripts go to the ICU path (host).
+  const uint32_t ndict = x.par.template sum<uint32_t>(C, [&](uint32_t i) { return (c.prop[i] & P_DICT) ? 1u : 0u; });
+  if (ndict) { x.set_flag(DOC_NEEDS_CPU); }
+  uint64_t* PH = nullptr;
+  if (need_ph) PH = prefix_hash(x, b, n);
+  Words w;
+  if (need_words && !ndict) w = words(x, c);
+  Lines L;
+  if (need_lines) L = rust_lines(x, c);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  const uint32_t W = w.n;
+  const uint32_t* cp = c.cp;
+  const uint32_t* prop = c.prop;
+  const uint32_t* off = c.off;
+  const uint64_t* pw = x.pw;
+
+  for (int s = 0; s < st.n_steps; ++s) {
+    const DevStep& ds = st.steps[s];
+    int64_t* r = out.rec + ds.rec_base + (int64_t)out.doc * ds.width;
+    if (ds.kind == DK_GOPHER_QUALITY) {
+      const DevStopSet& ss = plan.stops[ds.stop_set];
+      const UcdView ucd = x.ucd;
+      int64_t sum_chars = x.par.template sum<int64_t>(W, [&](uint32_t k) { return (int64_t)(w.ce[k] - w.cs[k]); });
+      int64_t alpha = x.par.template sum<int64_t>(W, [&](uint32_t k) { return (int64_t)w.alpha[k]; });
+      int64_t stop = x.par.template sum<int64_t>(W, [&](uint32_t k) {
+        return (int64_t)is_stop_word(ucd, ss, cp, prop, w.cs[k], w.ce[k]);
+      });
+      int64_t nhash = x.par.template sum<int64_t>(C, [&](uint32_t i) { return (int64_t)(cp[i] == '#'); });
+      int64_t nell = x.par.template sum<int64_t>(C, [&](uint32_t i) {
+        if (cp[i] == 0x2026) return (int64_t)1;
+        if (cp[i] != '.' || (i > 0 && cp[i - 1] == '.')) return (int64_t)0;
+        uint32_t j = i;
+        while (j < C && cp[j] == '.') ++j;
+        return (int64_t)((j - i) / 3);
+      });
+      int64_t bullet = x.par.template sum<int64_t>(L.n, [&](uint32_t k) {
+        uint32_t j = L.ls[k];
+        while (j < L.le[k] && is_ws(prop[j])) ++j;
+        return (int64_t)(j < L.le[k] && (cp[j] == 0x2022 || cp[j] == '-'));
+      });
+      int64_t ell_lines = x.par.template sum<int64_t>(L.n, [&](uint32_t k) {
+        uint32_t j = L.le[k];
+        while (j > L.ls[k] && is_ws(prop[j - 1])) --j;
+        const uint32_t E = off[j], S = off[L.ls[k]];
+        if (E - S < 3) return (int64_t)0;
+        const bool dots = b[E - 3] == '.' && b[E - 2] == '.' && b[E - 1] == '.';
+        const bool uell = b[E - 3] == 0xE2 && b[E - 2] == 0x80 && b[E - 1] == 0xA6;
+        return (int64_t)(dots || uell);
+      });
+      x.par.single([&]() {
+        r[0] = W; r[1] = sum_chars; r[2] = nhash; r[3] = nell; r[4] = L.n;
+        r[5] = bullet; r[6] = ell_lines; r[7] = alpha; r[8] = stop;
+      });
+    } else if (ds.kind == DK_GOPHER_REP) {
+      gopher_rep_record(x, ds, b, c, PH, w, r);
+    } else if (ds.kind == DK_FINEWEB) {
+      const uint64_t mark = x.used;
+      uint32_t* nb = x.template alloc<uint32_t>(L.n + 1);
+      if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+      const uint32_t NB = x.par.template compact<int>(
+          L.n,
+          [&](uint32_t k, int&) {
+            for (uint32_t j = L.ls[k]; j < L.le[k]; ++j) if (!is_ws(prop[j])) return true;
+            return false;
+          },
+          [&](uint32_t k, uint32_t q, int&) { nb[q] = k; });
+      x.par.sync();
+      int64_t stop_end = x.par.template sum<int64_t>(NB, [&](uint32_t q) {
+        uint32_t k = nb[q];
+        uint32_t j = L.le[k];
+        while (j > L.ls[k] && is_ws(prop[j - 1])) --j;
+        uint32_t last = cp[j - 1];
+        for (int t = 0; t < ds.n_stop_chars; ++t) if (ds.stop_chars[t] == last) return (int64_t)1;
+        return (int64_t)0;
+      });
+      int64_t shrt = x.par.template sum<int64_t>(NB, [&](uint32_t q) {
+        uint32_t k = nb[q];
+        return (int64_t)((int64_t)(L.le[k] - L.ls[k]) <= ds.short_line_length);
+      });
+      int64_t dup_e = 0, dup_b = 0;
+      dup_spans(x, b, PH, NB,
+                [&](uint32_t q, uint32_t& s0, uint32_t& e0) { s0 = off[L.ls[nb[q]]]; e0 = off[L.le[nb[q]]]; },
+                &dup_e, &dup_b);
+      int64_t nl = x.par.template sum<int64_t>(C, [&](uint32_t i) { return (int64_t)(cp[i] == '\n'); });
+      x.par.single([&]() {
+        r[0] = NB; r[1] = stop_end; r[2] = shrt; r[3] = dup_b; r[4] = (int64_t)C - nl; r[5] = nl; r[6] = W;
+      });
+      x.used = mark;
+    } else if (ds.kind == DK_LANGID) {
+      langid_features(x, c, lid_emb, out);
+    }
+    if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  }
+  (void)pw;
+}
+
+}  // namespace tb

@@ -1,0 +1,213 @@
+// Per-document parallel primitives.
+//
+// The document algorithms in docproc.h are written against this small interface so the same
+// source runs as a wave64 kernel on the MI355X (WavePar: one wavefront per document, lanes
+// cooperate through DPP shuffles / ballots, no LDS needed) and sequentially on the host
+// (SeqPar: used to differential-test the device algorithms against the ICU oracle on CPU, and
+// as a fast ICU-free CPU path).
+//
+// Contract for algorithm code:
+//  * for_n(n, f): f(i) for every i < n, in any order and concurrently; f must not depend on
+//    other iterations of the same call.
+//  * compact<S>(n, pred, emit): pred(i, S&) computes per-item state and says whether item i
+//    is selected; emit(i, k, S&) is then called with k = rank of i among selected items (in i
+//    order). Returns the number selected (uniform across lanes).
+//  * sum/max/min: reductions (uniform result).
+//  * scan<T>(n, id, op, in, out): out(i, exclusive prefix) for every i; returns the total.
+//  * sync(): every write before it is visible to every lane after it.
+//  * single(f): f() runs once (lane 0).
+//  * cas64/min32/add32/add64/max32: atomics on scratch memory.
+#pragma once
+#include "langid.h"
+#include "tb_common.h"
+
+namespace tb {
+
+struct SeqPar {
+  template <class F>
+  void for_n(uint32_t n, F&& f) const {
+    for (uint32_t i = 0; i < n; ++i) f(i);
+  }
+  template <class S, class Pred, class Emit>
+  uint32_t compact(uint32_t n, Pred&& pred, Emit&& emit) const {
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      S st{};
+      if (pred(i, st)) emit(i, k++, st);
+    }
+    return k;
+  }
+  template <class T, class F>
+  T sum(uint32_t n, F&& f) const {
+    T s = 0;
+    for (uint32_t i = 0; i < n; ++i) s += f(i);
+    return s;
+  }
+  template <class T, class F>
+  T max(uint32_t n, T init, F&& f) const {
+    T s = init;
+    for (uint32_t i = 0; i < n; ++i) { T v = f(i); if (v > s) s = v; }
+    return s;
+  }
+  template <class T, class F>
+  T min(uint32_t n, T init, F&& f) const {
+    T s = init;
+    for (uint32_t i = 0; i < n; ++i) { T v = f(i); if (v < s) s = v; }
+    return s;
+  }
+  template <class T, class Op, class In, class Out>
+  T scan(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
+    T acc = id;
+    for (uint32_t i = 0; i < n; ++i) {
+      out(i, acc);
+      acc = op(acc, in(i));
+    }
+    return acc;
+  }
+  void sync() const {}
+  template <class F>
+  void single(F&& f) const { f(); }
+  bool leader() const { return true; }
+  static uint64_t cas64(uint64_t* p, uint64_t cmp, uint64_t val) {
+    uint64_t old = *p;
+    if (old == cmp) *p = val;
+    return old;
+  }
+  static void min32(uint32_t* p, uint32_t v) { if (v < *p) *p = v; }
+  static void max32(uint32_t* p, uint32_t v) { if (v > *p) *p = v; }
+  static uint32_t add32(uint32_t* p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
+  // Sum of fixed-point embedding rows: acc[d] = sum_k fixed(E[rows[k]][d]), d < D.
+  template <int D, class Row>
+  void gather_rows_fixed(uint32_t K, Row&& row_ptr, int64_t* acc) const {
+    for (int d = 0; d < D; ++d) acc[d] = 0;
+    for (uint32_t k = 0; k < K; ++k) {
+      const uint16_t* r = row_ptr(k);
+      for (int d = 0; d < D; ++d) acc[d] += lid_fixed(r[d]);
+    }
+  }
+};
+
+#if defined(__HIPCC__)
+struct WavePar {
+  uint32_t lane;
+  __device__ WavePar() : lane(threadIdx.x & 63) {}
+
+  template <class F>
+  __device__ void for_n(uint32_t n, F&& f) const {
+    for (uint32_t i = lane; i < n; i += 64) f(i);
+  }
+  template <class S, class Pred, class Emit>
+  __device__ uint32_t compact(uint32_t n, Pred&& pred, Emit&& emit) const {
+    uint32_t k = 0;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t i = base + lane;
+      S st{};
+      const bool p = i < n && pred(i, st);
+      const uint64_t m = __ballot(p);
+      if (p) emit(i, k + (uint32_t)__popcll(m & lt), st);
+      k += (uint32_t)__popcll(m);
+    }
+    return k;
+  }
+  template <class T>
+  __device__ static T wave_sum(T v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+  }
+  template <class T>
+  __device__ static T wave_max(T v) {
+    for (int o = 32; o > 0; o >>= 1) { T t = __shfl_xor(v, o); v = t > v ? t : v; }
+    return v;
+  }
+  template <class T>
+  __device__ static T wave_min(T v) {
+    for (int o = 32; o > 0; o >>= 1) { T t = __shfl_xor(v, o); v = t < v ? t : v; }
+    return v;
+  }
+  template <class T, class F>
+  __device__ T sum(uint32_t n, F&& f) const {
+    T s = 0;
+    for (uint32_t i = lane; i < n; i += 64) s += f(i);
+    return wave_sum(s);
+  }
+  template <class T, class F>
+  __device__ T max(uint32_t n, T init, F&& f) const {
+    T s = init;
+    for (uint32_t i = lane; i < n; i += 64) { T v = f(i); if (v > s) s = v; }
+    return wave_max(s);
+  }
+  template <class T, class F>
+  __device__ T min(uint32_t n, T init, F&& f) const {
+    T s = init;
+    for (uint32_t i = lane; i < n; i += 64) { T v = f(i); if (v < s) s = v; }
+    return wave_min(s);
+  }
+  template <class T, class Op, class In, class Out>
+  __device__ T scan(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
+    T carry = id;
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t i = base + lane;
+      T x = i < n ? in(i) : id;
+      // inclusive Hillis-Steele scan (op is associative, not necessarily commutative)
+      for (int o = 1; o < 64; o <<= 1) {
+        T y = shfl_up_t(x, o);
+        if ((int)lane >= o) x = op(y, x);
+      }
+      T excl = shfl_up_t(x, 1);
+      if (lane == 0) excl = id;
+      if (i < n) out(i, op(carry, excl));
+      carry = op(carry, shfl_t(x, 63));
+    }
+    return carry;
+  }
+  __device__ void sync() const { __syncthreads(); }
+  template <class F>
+  __device__ void single(F&& f) const { if (lane == 0) f(); }
+  __device__ bool leader() const { return lane == 0; }
+  __device__ static uint64_t cas64(uint64_t* p, uint64_t cmp, uint64_t val) {
+    return atomicCAS((unsigned long long*)p, (unsigned long long)cmp, (unsigned long long)val);
+  }
+  __device__ static void min32(uint32_t* p, uint32_t v) { atomicMin(p, v); }
+  __device__ static void max32(uint32_t* p, uint32_t v) { atomicMax(p, v); }
+  __device__ static uint32_t add32(uint32_t* p, uint32_t v) { return atomicAdd(p, v); }
+
+  template <int D, class Row>
+  __device__ void gather_rows_fixed(uint32_t K, Row&& row_ptr, int64_t* acc) const {
+    static_assert(D == 32, "lane layout assumes 32 dims");
+    const int d = lane & 31, h = lane >> 5;
+    int64_t s = 0;
+    for (uint32_t k = h; k < K; k += 2) s += lid_fixed(row_ptr(k)[d]);
+    s += __shfl_xor(s, 32);
+    // every lane ends with its dimension's total; lanes 0..31 publish
+    for (int j = 0; j < D; ++j) acc[j] = __shfl(s, j);
+  }
+
+ private:
+  // Shuffle any POD scan element 32 bits at a time.
+  template <class T>
+  __device__ static T shfl_up_t(T v, int o) {
+    constexpr int N = (int)((sizeof(T) + 3) / 4);
+    int w[N];
+    __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+    for (int k = 0; k < N; ++k) w[k] = __shfl_up(w[k], o);
+    T r;
+    __builtin_memcpy(&r, w, sizeof(T));
+    return r;
+  }
+  template <class T>
+  __device__ static T shfl_t(T v, int src) {
+    constexpr int N = (int)((sizeof(T) + 3) / 4);
+    int w[N];
+    __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+    for (int k = 0; k < N; ++k) w[k] = __shfl(w[k], src);
+    T r;
+    __builtin_memcpy(&r, w, sizeof(T));
+    return r;
+  }
+};
+#endif
+
+}  // namespace tb

@@ -1,0 +1,149 @@
+// UAX #29 word and sentence boundary rules (Unicode 14, as tailored by ICU's default rules for
+// scripts that do not need a dictionary), written once for the host and the device.
+//
+// The reference segments with ICU4X (`WordSegmenter::new_auto`, `SentenceSegmenter::new`,
+// reference src/utils/text.rs:59-181). Documents that contain dictionary/LSTM scripts (Han,
+// Hiragana, Katakana, Thai, Lao, Khmer, Myanmar: P_DICT) are routed to the ICU4C path instead.
+//
+// The rule functions take an accessor `A` exposing `uint32_t p(int i)`: the packed property word of
+// code point i of the text being segmented, with 0 <= i < n. `wb_break(a, n, i)` answers "is there a
+// word boundary between code point i-1 and code point i" for 0 < i < n (sot/eot are boundaries).
+#pragma once
+#include "ucd.h"
+
+namespace tb {
+
+TB_HD bool wb_ign(int c) { return c == WB_Extend || c == WB_Format || c == WB_ZWJ; }
+TB_HD bool wb_nl(int c) { return c == WB_CR || c == WB_LF || c == WB_Newline; }
+TB_HD bool wb_ah(int c) { return c == WB_ALetter || c == WB_Hebrew; }
+TB_HD bool wb_midletq(int c) { return c == WB_MidLetter || c == WB_MidNumLet || c == WB_SQ; }
+TB_HD bool wb_midnumq(int c) { return c == WB_MidNum || c == WB_MidNumLet || c == WB_SQ; }
+
+// Effective previous code point index for WB4: the nearest index < i that is not
+// Extend/Format/ZWJ. Returns -1 if the run of ignorables reaches sot.
+template <class A>
+TB_HD int wb_prev_eff(const A& a, int i) {
+  int k = i - 1;
+  while (k >= 0 && wb_ign(wb_of(a.p(k)))) --k;
+  return k;
+}
+template <class A>
+TB_HD int wb_next_eff(const A& a, int n, int i) {
+  int k = i + 1;
+  while (k < n && wb_ign(wb_of(a.p(k)))) ++k;
+  return k;
+}
+
+template <class A>
+TB_HD bool wb_break(const A& a, int n, int i) {
+  const uint32_t pp = a.p(i - 1), pc = a.p(i);
+  const int cp = wb_of(pp), cc = wb_of(pc);
+  if (cp == WB_CR && cc == WB_LF) return false;            // WB3
+  if (wb_nl(cp)) return true;                              // WB3a
+  if (wb_nl(cc)) return true;                              // WB3b
+  if (cp == WB_ZWJ && (pc & P_EXTPICT)) return false;      // WB3c
+  if (cp == WB_WSegSpace && cc == WB_WSegSpace) return false;  // WB3d
+  if (wb_ign(cc)) return false;                            // WB4
+  // Effective left context (ignorables attach to the preceding non-ignorable, unless the run
+  // started at sot or right after a newline, in which case it stands alone as "Other").
+  int k = wb_prev_eff(a, i);
+  int L = WB_Other;
+  if (k >= 0) {
+    const int ck = wb_of(a.p(k));
+    if (!wb_nl(ck)) L = ck;
+  }
+  const int R = cc;
+  int LL = -1;
+  auto left2 = [&]() -> int {
+    if (k < 0 || L == WB_Other) return (int)WB_Other;
+    int k2 = wb_prev_eff(a, k);
+    return k2 >= 0 ? wb_of(a.p(k2)) : (int)WB_Other;
+  };
+  auto right2 = [&]() -> int {
+    int m = wb_next_eff(a, n, i);
+    return m < n ? wb_of(a.p(m)) : -1;
+  };
+  if (wb_ah(L) && wb_ah(R)) return false;                                   // WB5
+  if (wb_ah(L) && wb_midletq(R) && wb_ah(right2())) return false;           // WB6
+  if (wb_midletq(L) && wb_ah(R)) { LL = left2(); if (wb_ah(LL)) return false; }  // WB7
+  if (L == WB_Hebrew && R == WB_SQ) return false;                          // WB7a
+  if (L == WB_Hebrew && R == WB_DQ && right2() == WB_Hebrew) return false;  // WB7b
+  if (L == WB_DQ && R == WB_Hebrew) { if (LL < 0) LL = left2(); if (LL == WB_Hebrew) return false; }  // WB7c
+  if (L == WB_Numeric && R == WB_Numeric) return false;                    // WB8
+  if (wb_ah(L) && R == WB_Numeric) return false;                           // WB9
+  if (L == WB_Numeric && wb_ah(R)) return false;                           // WB10
+  if (wb_midnumq(L) && R == WB_Numeric) { if (LL < 0) LL = left2(); if (LL == WB_Numeric) return false; }  // WB11
+  if (L == WB_Numeric && wb_midnumq(R) && right2() == WB_Numeric) return false;  // WB12
+  if (L == WB_Katakana && R == WB_Katakana) return false;                  // WB13
+  if ((wb_ah(L) || L == WB_Numeric || L == WB_Katakana || L == WB_ExtendNumLet) &&
+      R == WB_ExtendNumLet)
+    return false;                                                          // WB13a
+  if (L == WB_ExtendNumLet && (wb_ah(R) || R == WB_Numeric || R == WB_Katakana)) return false;  // WB13b
+  if (L == WB_RI && R == WB_RI) {                                          // WB15/16
+    int cnt = 0;
+    int j = k;
+    while (j >= 0 && wb_of(a.p(j)) == WB_RI) { ++cnt; j = wb_prev_eff(a, j); }
+    return (cnt & 1) == 0;
+  }
+  return true;                                                             // WB999
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sentence boundaries.
+TB_HD bool sb_ign(int c) { return c == SB_Extend || c == SB_Format; }
+TB_HD bool sb_para(int c) { return c == SB_Sep || c == SB_CR || c == SB_LF; }
+TB_HD bool sb_sterm_or_aterm(int c) { return c == SB_ATerm || c == SB_STerm; }
+
+template <class A>
+TB_HD int sb_prev_eff(const A& a, int i) {
+  int k = i - 1;
+  while (k >= 0 && sb_ign(sb_of(a.p(k)))) --k;
+  return k;
+}
+
+template <class A>
+TB_HD bool sb_break(const A& a, int n, int i) {
+  const int cp = sb_of(a.p(i - 1)), cc = sb_of(a.p(i));
+  if (cp == SB_CR && cc == SB_LF) return false;   // SB3
+  if (sb_para(cp)) return true;                   // SB4
+  if (sb_ign(cc)) return false;                   // SB5
+  int k = sb_prev_eff(a, i);
+  int L = SB_Other;
+  if (k >= 0) {
+    const int ck = sb_of(a.p(k));
+    if (!sb_para(ck)) L = ck;
+  }
+  const int R = cc;
+  if (L == SB_ATerm && R == SB_Numeric) return false;  // SB6
+  if (L == SB_ATerm && R == SB_Upper) {               // SB7
+    int k2 = sb_prev_eff(a, k);
+    if (k2 >= 0) {
+      int c2 = sb_of(a.p(k2));
+      if (c2 == SB_Upper || c2 == SB_Lower) return false;
+    }
+  }
+  // Match  SATerm Close* Sp*  ending at the effective left context.
+  if (k < 0 || L == SB_Other) return false;  // SB998 (no terminator to the left)
+  int j = k;
+  bool saw_sp = false;
+  while (j >= 0 && sb_of(a.p(j)) == SB_Sp) { saw_sp = true; j = sb_prev_eff(a, j); }
+  while (j >= 0 && sb_of(a.p(j)) == SB_Close) { j = sb_prev_eff(a, j); }
+  if (j < 0) return false;
+  const int term = sb_of(a.p(j));
+  if (!sb_sterm_or_aterm(term)) return false;  // SB998
+  if (term == SB_ATerm) {                      // SB8
+    int m = i;
+    while (m < n) {
+      int c = sb_of(a.p(m));
+      if (c == SB_OLetter || c == SB_Upper || c == SB_Lower || sb_para(c) || sb_sterm_or_aterm(c)) break;
+      ++m;
+    }
+    if (m < n && sb_of(a.p(m)) == SB_Lower) return false;
+  }
+  if (R == SB_SContinue || sb_sterm_or_aterm(R)) return false;              // SB8a
+  if (!saw_sp && (R == SB_Close || R == SB_Sp || sb_para(R))) return false;  // SB9
+  if (R == SB_Sp || sb_para(R)) return false;                                // SB10
+  return true;                                                               // SB11
+}
+
+}  // namespace tb

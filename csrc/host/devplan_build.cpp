@@ -1,0 +1,233 @@
+// Builds the POD device plan (csrc/common/devplan.h) from step configs, and runs the device
+// document algorithms (csrc/common/docproc.h) on the host with the sequential policy.
+#include "devplan_build.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+
+#include "../common/docproc.h"
+
+namespace tb {
+
+int dev_kind_of(const StepCfg& c) {
+  switch (c.kind) {
+    case StepKind::GopherQuality: return DK_GOPHER_QUALITY;
+    case StepKind::GopherRepetition: return DK_GOPHER_REP;
+    case StepKind::FineWebQuality: return DK_FINEWEB;
+    case StepKind::LanguageDetection: return DK_LANGID;
+    default: return DK_NONE;
+  }
+}
+
+bool device_supported(const StepCfg& c, std::string* why) {
+  if (c.kind == StepKind::GopherRepetition) {
+    if (c.top_n_grams.size() > (size_t)kMaxNgramEntries || c.dup_n_grams.size() > (size_t)kMaxNgramEntries) {
+      if (why) *why = "more than 16 n-gram entries";
+      return false;
+    }
+    for (auto& e : c.top_n_grams) if (e.first > (1 << 20)) { if (why) *why = "n too large"; return false; }
+    for (auto& e : c.dup_n_grams) if (e.first > (1 << 20)) { if (why) *why = "n too large"; return false; }
+  }
+  if (c.kind == StepKind::FineWebQuality && c.stop_chars.size() > (size_t)kMaxStopChars) {
+    if (why) *why = "more than 16 stop_chars";
+    return false;
+  }
+  if (c.kind == StepKind::GopherQuality) {
+    size_t bytes = 0;
+    for (auto& w : c.stop_words) bytes += w.size();
+    if (c.stop_words.size() > (size_t)kMaxStopWords || bytes > (size_t)kStopBlobBytes) {
+      if (why) *why = "stop word list too large for the device table";
+      return false;
+    }
+  }
+  return true;
+}
+
+static int add_stop_set(DevPlan& plan, const std::vector<std::string>& words) {
+  if (plan.n_stop_sets >= kMaxStopSets) throw std::runtime_error("too many distinct stop-word sets");
+  DevStopSet& ss = plan.stops[plan.n_stop_sets];
+  std::memset(&ss, 0, sizeof(ss));
+  std::vector<std::string> uniq;
+  for (auto& w : words)
+    if (std::find(uniq.begin(), uniq.end(), w) == uniq.end()) uniq.push_back(w);
+  int32_t pos = 0;
+  for (size_t i = 0; i < uniq.size(); ++i) {
+    const std::string& w = uniq[i];
+    ss.off[i] = pos;
+    std::memcpy(ss.blob + pos, w.data(), w.size());
+    pos += (int32_t)w.size();
+    const uint64_t key = dev_key(hash_bytes((const uint8_t*)w.data(), (uint32_t)w.size()), (uint32_t)w.size());
+    uint32_t slot = (uint32_t)(key >> 17) & (kStopTableSize - 1);
+    while (ss.keys[slot] != 0) slot = (slot + 1) & (kStopTableSize - 1);
+    ss.keys[slot] = key;
+    ss.idx[slot] = (int32_t)i;
+  }
+  ss.off[uniq.size()] = pos;
+  ss.n = (int32_t)uniq.size();
+  return plan.n_stop_sets++;
+}
+
+DevStage build_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, DevPlan& plan) {
+  DevStage st;
+  std::memset(&st, 0, sizeof(st));
+  if (idx.size() > (size_t)kMaxStageSteps) throw std::runtime_error("too many steps in one device stage");
+  int prefix = 0;
+  for (size_t i = 0; i < idx.size(); ++i) {
+    const StepCfg& c = steps[idx[i]];
+    DevStep& d = st.steps[i];
+    d.kind = dev_kind_of(c);
+    if (d.kind == DK_NONE) throw std::runtime_error("step " + c.name + " has no device stage form");
+    d.width = record_width(c);
+    d.rec_prefix = prefix;
+    prefix += d.width;
+    if (c.kind == StepKind::GopherQuality) d.stop_set = add_stop_set(plan, c.stop_words);
+    if (c.kind == StepKind::GopherRepetition) {
+      d.n_top = (int32_t)c.top_n_grams.size();
+      d.n_dup = (int32_t)c.dup_n_grams.size();
+      for (int k = 0; k < d.n_top; ++k) d.top_n[k] = (int32_t)c.top_n_grams[k].first;
+      for (int k = 0; k < d.n_dup; ++k) d.dup_n[k] = (int32_t)c.dup_n_grams[k].first;
+    }
+    if (c.kind == StepKind::FineWebQuality) {
+      d.n_stop_chars = (int32_t)c.stop_chars.size();
+      for (int k = 0; k < d.n_stop_chars; ++k) d.stop_chars[k] = c.stop_chars[k];
+      d.short_line_length = c.short_line_length;
+    }
+  }
+  st.n_steps = (int32_t)idx.size();
+  st.width_total = prefix;
+  return st;
+}
+
+DevC4 build_c4(const StepCfg& c) {
+  DevC4 d;
+  std::memset(&d, 0, sizeof(d));
+  d.split_paragraph = c.split_paragraph;
+  d.remove_citations = c.remove_citations;
+  d.filter_no_terminal_punct = c.filter_no_terminal_punct;
+  d.filter_lorem_ipsum = c.filter_lorem_ipsum;
+  d.filter_javascript = c.filter_javascript;
+  d.filter_curly_bracket = c.filter_curly_bracket;
+  d.filter_policy = c.filter_policy;
+  d.min_words_per_line = c.min_words_per_line;
+  d.max_word_length = c.max_word_length;
+  return d;
+}
+
+std::vector<uint64_t> pow_table(uint32_t n) {
+  std::vector<uint64_t> pw(n + 1);
+  pw[0] = 1;
+  for (uint32_t i = 1; i <= n; ++i) pw[i] = mulmod61(pw[i - 1], kHashBase);
+  return pw;
+}
+
+uint64_t scratch_bytes_for(uint32_t doc_len) { return (uint64_t)kScratchPerByte * (doc_len + 64) + 4096; }
+
+// Head of the language model on one doc vector (host arithmetic; the device uses MFMA).
+static void lid_head_host(const LangidModel& m, const uint16_t* v, int32_t cnt, int64_t* r) {
+  if (cnt == 0) { r[0] = -1; r[1] = 0; r[2] = 0; return; }
+  float logits[kLidLangs];
+  for (int l = 0; l < kLidLangs; ++l) {
+    float s = 0.f;
+    for (int d = 0; d < kLidDim; ++d) s += bf16_to_f32(v[d]) * bf16_to_f32(m.w[d * kLidLangsPad + l]);
+    logits[l] = s + m.b[l];
+  }
+  int best = 0;
+  for (int l = 1; l < kLidLangs; ++l) if (logits[l] > logits[best]) best = l;
+  double den = 0;
+  for (int l = 0; l < kLidLangs; ++l) den += std::exp((double)logits[l] - (double)logits[best]);
+  double conf = 1.0 / den;
+  r[0] = best;
+  std::memcpy(&r[1], &conf, sizeof(double));
+  r[2] = 0;
+}
+
+void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
+                   const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
+                   std::vector<int64_t>& rec, std::vector<uint32_t>& flags) {
+  DevPlan* plan = new DevPlan();
+  std::memset(plan, 0, sizeof(DevPlan));
+  DevStage st = build_stage(steps, idx, *plan);
+  for (int s = 0; s < st.n_steps; ++s) st.steps[s].rec_base = (int64_t)st.steps[s].rec_prefix * ndocs;
+  bool has_lid = false;
+  for (int s = 0; s < st.n_steps; ++s) has_lid |= st.steps[s].kind == DK_LANGID;
+  if (has_lid && !lid) { delete plan; throw std::runtime_error("language model required"); }
+  rec.assign((size_t)st.width_total * ndocs, 0);
+  flags.assign(ndocs, 0);
+  std::vector<uint16_t> lvec(has_lid ? (size_t)ndocs * kLidDim : 1);
+  std::vector<int32_t> lcnt(has_lid ? ndocs : 1);
+  uint32_t maxlen = 0;
+  for (int64_t i = 0; i < ndocs; ++i) maxlen = std::max<uint32_t>(maxlen, (uint32_t)(off[i + 1] - off[i]));
+  std::vector<uint64_t> pw = pow_table(maxlen + 16);
+  const UcdView ucd = host_ucd();
+  parallel_for(ndocs, nthreads, [&](int64_t a, int64_t b) {
+    std::vector<char> scratch;
+    for (int64_t i = a; i < b; ++i) {
+      const uint32_t n = (uint32_t)(off[i + 1] - off[i]);
+      const uint64_t need = scratch_bytes_for(n);
+      if (scratch.size() < need) scratch.resize(need);
+      DocCtx<SeqPar> x;
+      x.ucd = ucd;
+      x.pw = pw.data();
+      x.pw_n = (uint32_t)pw.size() - 1;
+      x.scr = scratch.data();
+      x.cap = need;
+      x.flag = &flags[i];
+      StageOut out{rec.data(), (uint32_t)ndocs, (uint32_t)i, lvec.data(), lcnt.data()};
+      analyze_stage(x, st, *plan, lid ? lid->emb.data() : nullptr, (const uint8_t*)data + off[i], n, out);
+      if (has_lid) {
+        for (int s = 0; s < st.n_steps; ++s)
+          if (st.steps[s].kind == DK_LANGID)
+            lid_head_host(*lid, &lvec[(size_t)i * kLidDim], lcnt[i],
+                          rec.data() + st.steps[s].rec_base + i * st.steps[s].width);
+      }
+    }
+  });
+  delete plan;
+}
+
+void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
+                std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,
+                std::vector<uint32_t>& flags) {
+  DevC4 c4 = build_c4(step);
+  rec.assign((size_t)rec::C4_WIDTH * ndocs, 0);
+  flags.assign(ndocs, 0);
+  std::vector<std::string> outs(ndocs);
+  uint32_t maxlen = 0;
+  for (int64_t i = 0; i < ndocs; ++i) maxlen = std::max<uint32_t>(maxlen, (uint32_t)(off[i + 1] - off[i]));
+  std::vector<uint64_t> pw = pow_table(maxlen + 16);
+  const UcdView ucd = host_ucd();
+  parallel_for(ndocs, nthreads, [&](int64_t a, int64_t b) {
+    std::vector<char> scratch;
+    for (int64_t i = a; i < b; ++i) {
+      const uint32_t n = (uint32_t)(off[i + 1] - off[i]);
+      const uint64_t need = scratch_bytes_for(n);
+      if (scratch.size() < need) scratch.resize(need);
+      DocCtx<SeqPar> x;
+      x.ucd = ucd;
+      x.pw = pw.data();
+      x.pw_n = (uint32_t)pw.size() - 1;
+      x.scr = scratch.data();
+      x.cap = need;
+      x.flag = &flags[i];
+      int64_t src[2] = {-1, 0};
+      const uint8_t* b = (const uint8_t*)data + off[i];
+      c4_pass_a(x, c4, b, n, rec.data() + i * rec::C4_WIDTH, src);
+      if (flags[i] & DOC_NEEDS_CPU) continue;
+      if (src[0] < 0) outs[i].assign((const char*)b, n);
+      else outs[i].assign(scratch.data() + src[0], (size_t)src[1]);
+    }
+  });
+  new_off.assign(ndocs + 1, 0);
+  size_t tot = 0;
+  for (auto& s : outs) tot += s.size();
+  new_data.clear();
+  new_data.reserve(tot);
+  for (int64_t i = 0; i < ndocs; ++i) {
+    new_data += outs[i];
+    new_off[i + 1] = (int64_t)new_data.size();
+  }
+}
+
+}  // namespace tb

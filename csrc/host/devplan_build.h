@@ -1,0 +1,28 @@
+#pragma once
+#include <string>
+#include <vector>
+
+#include "../common/devplan.h"
+#include "filters.h"
+#include "pipeline.h"
+
+namespace tb {
+
+// Per-document device scratch: kScratchPerByte * (len + 64) + 4096 bytes.
+constexpr uint64_t kScratchPerByte = 160;
+uint64_t scratch_bytes_for(uint32_t doc_len);
+
+int dev_kind_of(const StepCfg& c);
+bool device_supported(const StepCfg& c, std::string* why);
+DevStage build_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, DevPlan& plan);
+DevC4 build_c4(const StepCfg& c);
+std::vector<uint64_t> pow_table(uint32_t n);
+
+void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
+                   const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
+                   std::vector<int64_t>& rec, std::vector<uint32_t>& flags);
+void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
+                std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,
+                std::vector<uint32_t>& flags);
+
+}  // namespace tb

@@ -1,0 +1,450 @@
+// pybind11 bindings for the host runtime (_tbhost): text primitives, the CPU pipeline, the
+// batch resolver used by the GPU path, HTML decoding and output assembly.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "../common/langid.h"
+#include "../common/ucd_tables.inc"
+#include "filters.h"
+#include "html.h"
+#include "json.h"
+#include "pipeline.h"
+#include "devplan_build.h"
+#include "rustfmt.h"
+#include "text.h"
+
+namespace py = pybind11;
+using namespace tb;
+
+template <class T>
+static py::array_t<T> to_numpy(std::vector<T>&& v) {
+  auto* heap = new std::vector<T>(std::move(v));
+  py::capsule owner(heap, [](void* p) { delete reinterpret_cast<std::vector<T>*>(p); });
+  return py::array_t<T>({(py::ssize_t)heap->size()}, {(py::ssize_t)sizeof(T)}, heap->data(), owner);
+}
+static py::array_t<uint8_t> str_to_numpy(std::string&& s) {
+  auto* heap = new std::string(std::move(s));
+  py::capsule owner(heap, [](void* p) { delete reinterpret_cast<std::string*>(p); });
+  return py::array_t<uint8_t>({(py::ssize_t)heap->size()}, {(py::ssize_t)1},
+                              (const uint8_t*)heap->data(), owner);
+}
+
+static SegBackend be_of(const std::string& s) {
+  if (s == "icu") return SegBackend::Icu;
+  if (s == "rules") return SegBackend::Rules;
+  throw std::invalid_argument("segmentation backend must be 'icu' or 'rules'");
+}
+
+template <class T>
+static std::optional<T> opt(const py::dict& d, const char* k) {
+  if (!d.contains(k) || d[k].is_none()) return std::nullopt;
+  return d[k].cast<T>();
+}
+
+static StepCfg make_step(const py::dict& d) {
+  StepCfg c;
+  std::string t = d["type"].cast<std::string>();
+  c.name = t;
+  if (t == "C4QualityFilter") {
+    c.kind = StepKind::C4Quality;
+    c.split_paragraph = d["split_paragraph"].cast<bool>();
+    c.remove_citations = d["remove_citations"].cast<bool>();
+    c.filter_no_terminal_punct = d["filter_no_terminal_punct"].cast<bool>();
+    c.min_num_sentences = d["min_num_sentences"].cast<int64_t>();
+    c.min_words_per_line = d["min_words_per_line"].cast<int64_t>();
+    c.max_word_length = d["max_word_length"].cast<int64_t>();
+    c.filter_lorem_ipsum = d["filter_lorem_ipsum"].cast<bool>();
+    c.filter_javascript = d["filter_javascript"].cast<bool>();
+    c.filter_curly_bracket = d["filter_curly_bracket"].cast<bool>();
+    c.filter_policy = d["filter_policy"].cast<bool>();
+  } else if (t == "GopherRepetitionFilter") {
+    c.kind = StepKind::GopherRepetition;
+    c.dup_line_frac = opt<double>(d, "dup_line_frac");
+    c.dup_para_frac = opt<double>(d, "dup_para_frac");
+    c.dup_line_char_frac = opt<double>(d, "dup_line_char_frac");
+    c.dup_para_char_frac = opt<double>(d, "dup_para_char_frac");
+    if (d.contains("top_n_grams")) c.top_n_grams = d["top_n_grams"].cast<std::vector<std::pair<int64_t, double>>>();
+    if (d.contains("dup_n_grams")) c.dup_n_grams = d["dup_n_grams"].cast<std::vector<std::pair<int64_t, double>>>();
+  } else if (t == "GopherQualityFilter") {
+    c.kind = StepKind::GopherQuality;
+    c.min_doc_words = opt<int64_t>(d, "min_doc_words");
+    c.max_doc_words = opt<int64_t>(d, "max_doc_words");
+    c.min_avg_word_length = opt<double>(d, "min_avg_word_length");
+    c.max_avg_word_length = opt<double>(d, "max_avg_word_length");
+    c.max_symbol_word_ratio = opt<double>(d, "max_symbol_word_ratio");
+    c.max_bullet_lines_ratio = opt<double>(d, "max_bullet_lines_ratio");
+    c.max_ellipsis_lines_ratio = opt<double>(d, "max_ellipsis_lines_ratio");
+    c.max_non_alpha_words_ratio = opt<double>(d, "max_non_alpha_words_ratio");
+    c.min_stop_words = opt<int64_t>(d, "min_stop_words");
+    c.stop_words = d["stop_words"].cast<std::vector<std::string>>();
+  } else if (t == "FineWebQualityFilter") {
+    c.kind = StepKind::FineWebQuality;
+    c.line_punct_thr = d["line_punct_thr"].cast<double>();
+    c.line_punct_exclude_zero = d["line_punct_exclude_zero"].cast<bool>();
+    c.short_line_thr = d["short_line_thr"].cast<double>();
+    c.short_line_length = d["short_line_length"].cast<int64_t>();
+    c.char_duplicates_ratio = d["char_duplicates_ratio"].cast<double>();
+    c.new_line_ratio = d["new_line_ratio"].cast<double>();
+    c.stop_chars = d["stop_chars"].cast<std::vector<uint32_t>>();
+  } else if (t == "LanguageDetectionFilter") {
+    c.kind = StepKind::LanguageDetection;
+    c.min_confidence = d["min_confidence"].cast<double>();
+    c.allowed_langs = d["allowed_langs"].cast<std::vector<int>>();
+    c.allowed_codes = d["allowed_codes"].cast<std::vector<std::string>>();
+  } else if (t == "C4BadWordsFilter") {
+    c.kind = StepKind::C4BadWords;
+    c.keep_fraction = d["keep_fraction"].cast<double>();
+    c.fail_on_missing_language = d["fail_on_missing_language"].cast<bool>();
+    c.seed = opt<uint64_t>(d, "seed");
+    c.default_language = d["default_language"].cast<std::string>();
+  } else if (t == "TokenCounter") {
+    c.kind = StepKind::TokenCounter;
+    c.tokenizer_name = d["tokenizer_name"].cast<std::string>();
+  } else {
+    throw std::invalid_argument("unknown step type " + t);
+  }
+  return c;
+}
+
+// Holds the numpy buffers a BatchState borrows so they outlive it.
+struct __attribute__((visibility("hidden"))) PyBatch {
+  std::unique_ptr<BatchState> st;
+  std::vector<py::object> keep;
+};
+
+static const char* buf_ptr(const py::array& a) { return (const char*)a.data(); }
+
+PYBIND11_MODULE(_tbhost, m) {
+  m.doc() = "textblaster_amd host runtime";
+
+  py::enum_<StepKind>(m, "StepKind")
+      .value("C4Quality", StepKind::C4Quality)
+      .value("GopherRepetition", StepKind::GopherRepetition)
+      .value("GopherQuality", StepKind::GopherQuality)
+      .value("C4BadWords", StepKind::C4BadWords)
+      .value("LanguageDetection", StepKind::LanguageDetection)
+      .value("FineWebQuality", StepKind::FineWebQuality)
+      .value("TokenCounter", StepKind::TokenCounter);
+
+  py::class_<StepCfg>(m, "StepCfg")
+      .def_readonly("kind", &StepCfg::kind)
+      .def_readonly("name", &StepCfg::name)
+      .def("record_width", [](const StepCfg& c) { return record_width(c); });
+  m.def("make_step", &make_step);
+
+  // ---- text primitives (reference utils/text.rs) ----
+  m.def("split_into_words", [](const std::string& s, const std::string& be) {
+    std::vector<std::string> out;
+    for (auto w : split_into_words(s, be_of(be))) out.emplace_back(w);
+    return out;
+  }, py::arg("text"), py::arg("backend") = "rules");
+  m.def("split_into_sentences", [](const std::string& s, const std::string& be) {
+    std::vector<std::string> out;
+    for (auto w : split_into_sentences(s, be_of(be))) out.emplace_back(w);
+    return out;
+  }, py::arg("text"), py::arg("backend") = "rules");
+  m.def("word_breaks", [](const std::string& s, const std::string& be) { return word_breaks(s, be_of(be)); },
+        py::arg("text"), py::arg("backend") = "rules");
+  m.def("sentence_breaks", [](const std::string& s, const std::string& be) { return sentence_breaks(s, be_of(be)); },
+        py::arg("text"), py::arg("backend") = "rules");
+  m.def("find_duplicates", [](const std::vector<std::string>& items) {
+    std::vector<std::string_view> v(items.begin(), items.end());
+    return find_duplicates(v);
+  });
+  m.def("find_top_duplicate", [](const std::vector<std::string>& words, size_t n) {
+    std::vector<std::string_view> v(words.begin(), words.end());
+    return find_top_duplicate_ngrams(v, n);
+  });
+  m.def("find_all_duplicate", [](const std::vector<std::string>& words, size_t n) {
+    std::vector<std::string_view> v(words.begin(), words.end());
+    return find_all_duplicate(v, n);
+  });
+  m.def("remove_citations", [](const std::string& s) { return remove_citations(s); });
+  m.def("rust_lowercase", [](const std::string& s) { return rust_lowercase(s); });
+  m.def("rust_lines", [](const std::string& s) {
+    std::vector<std::string> out;
+    for (auto l : rust_lines(s)) out.emplace_back(l);
+    return out;
+  });
+  m.def("trim", [](const std::string& s) { return std::string(trim(s)); });
+  m.def("props", [](uint32_t cp) { return host_ucd().props(cp); });
+  m.def("has_dict_script", [](const std::string& s) { return has_dict_script(s); });
+  m.def("ucd_tables", []() {
+    std::vector<uint16_t> s1(TB_UCD_PROPS_STAGE1, TB_UCD_PROPS_STAGE1 + sizeof(TB_UCD_PROPS_STAGE1) / 2);
+    std::vector<uint32_t> s2((const uint32_t*)TB_UCD_PROPS_STAGE2,
+                             (const uint32_t*)TB_UCD_PROPS_STAGE2 + sizeof(TB_UCD_PROPS_STAGE2) / 4);
+    std::vector<uint16_t> l1(TB_UCD_LOWER_STAGE1, TB_UCD_LOWER_STAGE1 + sizeof(TB_UCD_LOWER_STAGE1) / 2);
+    std::vector<int32_t> l2(TB_UCD_LOWER_STAGE2, TB_UCD_LOWER_STAGE2 + sizeof(TB_UCD_LOWER_STAGE2) / 4);
+    return py::make_tuple(to_numpy(std::move(s1)), to_numpy(std::move(s2)), to_numpy(std::move(l1)),
+                          to_numpy(std::move(l2)));
+  });
+  m.def("fmt_f64", [](double x) { return fmt_f64(x); });
+
+  // ---- per-step records and decisions ----
+  m.def("compute_record", [](const StepCfg& c, const std::string& text, const std::string& be) {
+    std::vector<int64_t> r(record_width(c), 0);
+    std::string nc;
+    compute_record(c, text, be_of(be), r.data(), &nc);
+    return py::make_tuple(r, py::bytes(nc));
+  }, py::arg("step"), py::arg("text"), py::arg("backend") = "rules");
+  m.def("decide", [](const StepCfg& c, const std::vector<int64_t>& r) {
+    Decision d;
+    decide(c, r.data(), d);
+    return py::make_tuple(d.pass, d.error, d.reason, d.meta);
+  });
+
+  // ---- metadata JSON ----
+  m.def("parse_meta_json", [](const std::string& s) -> py::object {
+    MetaMap mm;
+    if (!parse_meta_json(s, mm)) return py::none();
+    return py::cast(mm);
+  });
+  m.def("serialize_meta_json", [](const MetaMap& mm) {
+    std::string out;
+    serialize_meta_json(mm, out);
+    return out;
+  });
+
+  // ---- HTML entity decoding over a packed batch ----
+  m.def("html_decode", [](const std::string& s) {
+    std::string out;
+    if (!html_decode(s, out)) return s;
+    return out;
+  });
+  m.def("html_decode_batch", [](py::array_t<uint8_t, py::array::c_style> data,
+                                py::array_t<int64_t, py::array::c_style> off, int nthreads) -> py::object {
+    const int64_t n = (int64_t)off.size() - 1;
+    const char* d = (const char*)data.data();
+    const int64_t* o = off.data();
+    std::vector<std::string> dec(n);
+    std::vector<uint8_t> changed(n, 0);
+    {
+      py::gil_scoped_release nogil;
+      parallel_for(n, nthreads, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i)
+          changed[i] = html_decode(std::string_view(d + o[i], (size_t)(o[i + 1] - o[i])), dec[i]);
+      });
+    }
+    bool any = false;
+    for (auto c : changed) any |= c != 0;
+    if (!any) return py::none();
+    std::string out;
+    std::vector<int64_t> no(n + 1, 0);
+    {
+      py::gil_scoped_release nogil;
+      size_t tot = 0;
+      for (int64_t i = 0; i < n; ++i) tot += changed[i] ? dec[i].size() : (size_t)(o[i + 1] - o[i]);
+      out.reserve(tot);
+      for (int64_t i = 0; i < n; ++i) {
+        if (changed[i]) out += dec[i];
+        else out.append(d + o[i], (size_t)(o[i + 1] - o[i]));
+        no[i + 1] = (int64_t)out.size();
+      }
+    }
+    return py::make_tuple(str_to_numpy(std::move(out)), to_numpy(std::move(no)));
+  });
+
+  // ---- language id (CPU) ----
+  py::class_<LangidModel, std::shared_ptr<LangidModel>>(m, "LangidModel")
+      .def(py::init([](py::array_t<uint16_t, py::array::c_style> emb, py::array_t<uint16_t, py::array::c_style> w,
+                       py::array_t<float, py::array::c_style> b) {
+        auto mdl = std::make_shared<LangidModel>();
+        if ((size_t)emb.size() != (size_t)kLidBuckets * kLidDim) throw std::invalid_argument("emb shape");
+        if ((size_t)w.size() != (size_t)kLidDim * kLidLangsPad) throw std::invalid_argument("w shape");
+        if ((size_t)b.size() != (size_t)kLidLangsPad) throw std::invalid_argument("b shape");
+        mdl->emb.assign(emb.data(), emb.data() + emb.size());
+        mdl->w.assign(w.data(), w.data() + w.size());
+        mdl->b.assign(b.data(), b.data() + b.size());
+        return mdl;
+      }))
+      .def("detect", [](const LangidModel& mdl, const std::string& s) {
+        double conf = 0;
+        int l = mdl.detect(s, &conf);
+        return py::make_tuple(l, conf);
+      })
+      .def("featurize", [](const LangidModel& mdl, const std::string& s) {
+        std::vector<uint16_t> v(kLidDim, 0);
+        int c = mdl.featurize(s, v.data());
+        return py::make_tuple(c, v);
+      });
+  m.def("langid_buckets", [](const std::string& s) {
+    // The hashed n-gram bucket ids of `s` (training-time featurizer, identical to the model's).
+    std::vector<uint32_t> out;
+    const uint8_t* b = (const uint8_t*)s.data();
+    const uint32_t n = (uint32_t)s.size();
+    const UcdView& u = host_ucd();
+    uint32_t lm2 = 0, lm1 = 0;
+    int ncp = 0;
+    auto emit = [&](uint32_t k) { out.push_back(k); };
+    for (uint32_t i = 0; i < n && ncp < kLidMaxCps; ++ncp) {
+      int len;
+      uint32_t c = utf8_decode(b, i, n, &len);
+      i += len;
+      uint32_t l0 = (u.props(c) & P_ALPHA) ? u.lower(c) : 0;
+      if (l0 == 0 && (u.props(c) & P_ALPHA)) l0 = c;
+      lid_grams_at(lm2, lm1, l0, true, true, emit);
+      lm2 = lm1;
+      lm1 = l0;
+    }
+    lid_grams_at(lm2, lm1, 0, true, true, emit);
+    return out;
+  });
+  m.attr("LID_DIM") = kLidDim;
+  m.attr("LID_BUCKETS") = kLidBuckets;
+  m.attr("LID_LANGS_PAD") = kLidLangsPad;
+
+  py::class_<BadWordsModule, std::shared_ptr<BadWordsModule>>(m, "BadWordsModule")
+      .def(py::init([](const std::string& dir) {
+        auto b = std::make_shared<BadWordsModule>();
+        b->cache_dir = dir;
+        return b;
+      }))
+      .def("matches", [](BadWordsModule& b, const std::string& lang, const std::string& text) {
+        bool sup;
+        auto l = b.get(lang, &sup);
+        if (!l) return false;
+        return l->match(text);
+      });
+
+  // ---- batch state ----
+  py::class_<PyBatch>(m, "BatchState")
+      .def(py::init([](py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
+                       py::object meta_data, py::object meta_off, py::object meta_valid, int nthreads) {
+        auto pb = new PyBatch();
+        pb->keep = {data, off, meta_data, meta_off, meta_valid};
+        const char* md = nullptr;
+        const int64_t* mo = nullptr;
+        const uint8_t* mv = nullptr;
+        if (!meta_data.is_none()) {
+          md = buf_ptr(meta_data.cast<py::array>());
+          mo = (const int64_t*)meta_off.cast<py::array>().data();
+          if (!meta_valid.is_none()) mv = (const uint8_t*)meta_valid.cast<py::array>().data();
+        }
+        py::gil_scoped_release nogil;
+        pb->st = std::make_unique<BatchState>((int64_t)off.size() - 1, (const char*)data.data(), off.data(),
+                                              md, mo, mv, nthreads);
+        return pb;
+      }), py::arg("data"), py::arg("offsets"), py::arg("meta_data") = py::none(),
+          py::arg("meta_offsets") = py::none(), py::arg("meta_valid") = py::none(), py::arg("nthreads") = 8)
+      .def_property_readonly("size", [](PyBatch& b) { return b.st->size(); })
+      .def_property_readonly("meta_parse_failures", [](PyBatch& b) { return b.st->meta_parse_failures(); })
+      .def("add_version", [](PyBatch& b, py::array_t<uint8_t, py::array::c_style> data,
+                             py::array_t<int64_t, py::array::c_style> off) {
+        if ((int64_t)off.size() != b.st->size() + 1) throw std::invalid_argument("offsets length");
+        b.keep.push_back(data);
+        b.keep.push_back(off);
+        return b.st->add_version((const char*)data.data(), off.data());
+      })
+      .def("run_cpu", [](PyBatch& b, const std::vector<StepCfg>& steps, int begin, int end, const std::string& be,
+                         std::shared_ptr<LangidModel> lid, std::shared_ptr<BadWordsModule> bw) {
+        py::gil_scoped_release nogil;
+        b.st->run_cpu(steps, begin, end, be_of(be), lid.get(), bw.get());
+      }, py::arg("steps"), py::arg("begin"), py::arg("end"), py::arg("backend") = "rules",
+         py::arg("lid") = nullptr, py::arg("badwords") = nullptr)
+      .def("apply_records", [](PyBatch& b, const StepCfg& c, int step_index,
+                               py::array_t<int64_t, py::array::c_style> rec, int rewrite_version) {
+        const int w = record_width(c);
+        if ((int64_t)rec.size() != b.st->size() * w) throw std::invalid_argument("record array size");
+        py::gil_scoped_release nogil;
+        b.st->apply_records(c, step_index, rec.data(), w, rewrite_version);
+      }, py::arg("step"), py::arg("step_index"), py::arg("records"), py::arg("rewrite_version") = -1)
+      .def("apply_badwords", [](PyBatch& b, const StepCfg& c, int step_index, std::shared_ptr<BadWordsModule> bw) {
+        py::gil_scoped_release nogil;
+        b.st->apply_badwords(c, step_index, *bw);
+      })
+      .def("alive_indices", [](PyBatch& b) { return to_numpy(b.st->alive_indices()); })
+      .def("fail_step", [](PyBatch& b) { return to_numpy(std::vector<int32_t>(b.st->fail_step())); })
+      .def("status", [](PyBatch& b) { return to_numpy(std::vector<uint8_t>(b.st->status())); })
+      .def("cur_version", [](PyBatch& b) { return to_numpy(std::vector<int32_t>(b.st->cur_version())); })
+      .def("reasons", [](PyBatch& b, py::array_t<int64_t, py::array::c_style> idx) {
+        std::vector<std::string> out;
+        for (py::ssize_t k = 0; k < idx.size(); ++k) out.push_back(b.st->reason(idx.data()[k]));
+        return out;
+      })
+      .def("contents", [](PyBatch& b, py::array_t<int64_t, py::array::c_style> idx) {
+        py::list out;
+        for (py::ssize_t k = 0; k < idx.size(); ++k) {
+          auto s = b.st->content(idx.data()[k]);
+          out.append(py::str(s.data(), s.size()));
+        }
+        return out;
+      })
+      .def("assemble", [](PyBatch& b, py::array_t<int64_t, py::array::c_style> idx) {
+        std::vector<int64_t> iv(idx.data(), idx.data() + idx.size());
+        std::string td, md;
+        std::vector<int64_t> to, mo;
+        std::vector<uint8_t> mv;
+        {
+          py::gil_scoped_release nogil;
+          b.st->assemble(iv, td, to, md, mo, mv);
+        }
+        return py::make_tuple(str_to_numpy(std::move(td)), to_numpy(std::move(to)), str_to_numpy(std::move(md)),
+                              to_numpy(std::move(mo)), to_numpy(std::move(mv)));
+      });
+
+  // ---- device plan building + host emulation of the device algorithms ----
+  m.def("device_supported", [](const StepCfg& c) {
+    std::string why;
+    bool ok = device_supported(c, &why);
+    return py::make_tuple(ok, why);
+  });
+  m.def("build_device_plan", [](const std::vector<StepCfg>& steps, const std::vector<std::vector<int>>& stages) {
+    auto plan = std::make_unique<DevPlan>();
+    std::memset(plan.get(), 0, sizeof(DevPlan));
+    py::list st;
+    for (auto& idx : stages) {
+      DevStage d = build_stage(steps, idx, *plan);
+      st.append(py::bytes((const char*)&d, sizeof(d)));
+    }
+    return py::make_tuple(py::bytes((const char*)plan.get(), sizeof(DevPlan)), st);
+  });
+  m.def("build_c4", [](const StepCfg& c) {
+    DevC4 d = build_c4(c);
+    return py::bytes((const char*)&d, sizeof(d));
+  });
+  m.def("stage_layout", [](const py::bytes& b) {
+    std::string s = b;
+    DevStage d;
+    std::memcpy(&d, s.data(), sizeof(d));
+    py::list out;
+    for (int i = 0; i < d.n_steps; ++i) out.append(py::make_tuple(d.steps[i].kind, d.steps[i].width, d.steps[i].rec_prefix));
+    return py::make_tuple(d.width_total, out);
+  });
+  m.def("pow_table", [](uint32_t n) { return to_numpy(pow_table(n)); });
+  m.def("scratch_bytes_for", [](uint32_t n) { return scratch_bytes_for(n); });
+  m.attr("SIZEOF_DEV_PLAN") = sizeof(DevPlan);
+  m.attr("SIZEOF_DEV_STAGE") = sizeof(DevStage);
+  m.attr("SIZEOF_DEV_C4") = sizeof(DevC4);
+  m.attr("OFFSETOF_REC_BASE") = offsetof(DevStep, rec_base);
+  m.attr("SIZEOF_DEV_STEP") = sizeof(DevStep);
+  m.attr("OFFSETOF_STEPS") = offsetof(DevStage, steps);
+  m.def("emulate_stage", [](const std::vector<StepCfg>& steps, const std::vector<int>& idx,
+                            py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
+                            int nthreads, std::shared_ptr<LangidModel> lid) {
+    std::vector<int64_t> rec;
+    std::vector<uint32_t> flags;
+    const int64_t nd = (int64_t)off.size() - 1;
+    {
+      py::gil_scoped_release nogil;
+      emulate_stage(steps, idx, nd, (const char*)data.data(), off.data(), nthreads, lid.get(), rec, flags);
+    }
+    return py::make_tuple(to_numpy(std::move(rec)), to_numpy(std::move(flags)));
+  }, py::arg("steps"), py::arg("idx"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8,
+     py::arg("lid") = nullptr);
+  m.def("emulate_c4", [](const StepCfg& step, py::array_t<uint8_t, py::array::c_style> data,
+                         py::array_t<int64_t, py::array::c_style> off, int nthreads) {
+    std::vector<int64_t> rec, no;
+    std::vector<uint32_t> flags;
+    std::string nd;
+    const int64_t n = (int64_t)off.size() - 1;
+    {
+      py::gil_scoped_release nogil;
+      emulate_c4(step, n, (const char*)data.data(), off.data(), nthreads, rec, nd, no, flags);
+    }
+    return py::make_tuple(to_numpy(std::move(rec)), str_to_numpy(std::move(nd)), to_numpy(std::move(no)),
+                          to_numpy(std::move(flags)));
+  });
+}

@@ -1,0 +1,420 @@
+#include "pipeline.h"
+
+#include <unicode/uchar.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+#include "../common/langid.h"
+
+namespace tb {
+
+void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t, int64_t)>& fn) {
+  if (n <= 0) return;
+  if (nthreads <= 1 || n < 256) { fn(0, n); return; }
+  const int64_t chunks = std::min<int64_t>((int64_t)nthreads * 8, (n + 63) / 64);
+  std::atomic<int64_t> next{0};
+  auto worker = [&]() {
+    while (true) {
+      int64_t c = next.fetch_add(1);
+      if (c >= chunks) break;
+      int64_t a = n * c / chunks, b = n * (c + 1) / chunks;
+      fn(a, b);
+    }
+  };
+  std::vector<std::thread> ts;
+  int nt = (int)std::min<int64_t>(nthreads, chunks);
+  for (int t = 1; t < nt; ++t) ts.emplace_back(worker);
+  worker();
+  for (auto& t : ts) t.join();
+}
+
+// ------------------------------------------------------------------------------------------
+// Language identification (CPU inference with the same arithmetic as the device path).
+int LangidModel::featurize(std::string_view text, uint16_t* out_vec) const {
+  const uint8_t* b = (const uint8_t*)text.data();
+  const uint32_t n = (uint32_t)text.size();
+  const UcdView& u = host_ucd();
+  int64_t acc[kLidDim] = {0};
+  int64_t cnt = 0;
+  uint32_t lm2 = 0, lm1 = 0;
+  int ncp = 0;
+  auto emit = [&](uint32_t bucket) {
+    const uint16_t* row = &emb[(size_t)bucket * kLidDim];
+    for (int d = 0; d < kLidDim; ++d) acc[d] += lid_fixed(row[d]);
+  };
+  uint32_t i = 0;
+  for (; i < n && ncp < kLidMaxCps; ++ncp) {
+    int len;
+    uint32_t c = utf8_decode(b, i, n, &len);
+    i += len;
+    uint32_t l0 = (u.props(c) & P_ALPHA) ? u.lower(c) : 0;
+    if (l0 == 0 && (u.props(c) & P_ALPHA)) l0 = c;  // paranoia: a letter never maps to 0
+    cnt += lid_grams_at(lm2, lm1, l0, true, true, emit);
+    lm2 = lm1;
+    lm1 = l0;
+  }
+  // virtual non-letter at the cut / end of text
+  cnt += lid_grams_at(lm2, lm1, 0, true, true, emit);
+  if (cnt == 0) return 0;
+  for (int d = 0; d < kLidDim; ++d) {
+    float v = (float)((double)acc[d] / (double)cnt / (double)kLidFixedScale);
+    out_vec[d] = f32_to_bf16(v);
+  }
+  return (int)std::min<int64_t>(cnt, INT32_MAX);
+}
+
+int LangidModel::detect(std::string_view text, double* conf) const {
+  uint16_t v[kLidDim];
+  if (featurize(text, v) == 0) return -1;
+  float logits[kLidLangs];
+  for (int l = 0; l < kLidLangs; ++l) {
+    float s = 0.f;
+    for (int d = 0; d < kLidDim; ++d) s += bf16_to_f32(v[d]) * bf16_to_f32(w[d * kLidLangsPad + l]);
+    logits[l] = s + b[l];
+  }
+  int best = 0;
+  for (int l = 1; l < kLidLangs; ++l) if (logits[l] > logits[best]) best = l;
+  double den = 0;
+  for (int l = 0; l < kLidLangs; ++l) den += std::exp((double)logits[l] - (double)logits[best]);
+  *conf = 1.0 / den;
+  return best;
+}
+
+// ------------------------------------------------------------------------------------------
+// C4 bad words.
+static const char* const kBadwordsLangs[] = {
+    "ar", "cs", "da", "de", "en", "eo", "es", "fa", "fi", "fil", "fr", "fr-CA-u-sd-caqc", "hi", "hu",
+    "it", "ja", "kab", "ko", "nl", "no", "pl", "pt", "ru", "sv", "th", "tlh", "tr", "zh"};
+
+static std::vector<uint32_t> fold_cps(std::string_view s) {
+  std::vector<uint32_t> out;
+  const uint8_t* b = (const uint8_t*)s.data();
+  uint32_t n = (uint32_t)s.size();
+  for (uint32_t i = 0; i < n;) {
+    int len;
+    uint32_t c = utf8_decode(b, i, n, &len);
+    out.push_back((uint32_t)u_foldCase((UChar32)c, U_FOLD_CASE_DEFAULT));
+    i += len;
+  }
+  return out;
+}
+
+bool BadWordsLang::match(std::string_view text) const {
+  CpView v;
+  v.build(text);
+  std::vector<uint32_t> f(v.n());
+  for (int i = 0; i < v.n(); ++i) f[i] = (uint32_t)u_foldCase((UChar32)v.cp[i], U_FOLD_CASE_DEFAULT);
+  auto is_w = [&](int i) { return (v.prop[i] & P_WORDCHAR) != 0; };
+  for (int i = 0; i < v.n(); ++i) {
+    if (!cjk && i > 0 && is_w(i - 1)) continue;  // (?:\W|^)
+    int node = 0;
+    for (int j = i; j < v.n(); ++j) {
+      auto it = trie[node].next.find(f[j]);
+      if (it == trie[node].next.end()) break;
+      node = it->second;
+      if (trie[node].term && (cjk || j + 1 == v.n() || !is_w(j + 1))) return true;  // (?:\W|$)
+    }
+  }
+  return false;
+}
+
+std::shared_ptr<BadWordsLang> BadWordsModule::get(const std::string& lang, bool* supported) {
+  bool sup = false;
+  for (auto l : kBadwordsLangs) if (lang == l) sup = true;
+  *supported = sup;
+  if (!sup) return nullptr;
+  auto it = langs.find(lang);
+  if (it != langs.end()) return it->second;
+  std::string path = cache_dir + "/" + lang;
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("badwords list for '" + lang + "' not found in cache dir '" +
+                                   cache_dir + "' (no network: place the LDNOOBW list at " + path + ")");
+  std::stringstream ss;
+  ss << f.rdbuf();
+  std::string content = ss.str();
+  auto bl = std::make_shared<BadWordsLang>();
+  bl->cjk = (lang == "ja" || lang == "th" || lang == "zh");
+  bl->trie.emplace_back();
+  int nwords = 0;
+  std::string_view cv(content);
+  size_t p = 0;
+  while (p <= cv.size()) {
+    size_t q = cv.find('\n', p);
+    if (q == std::string_view::npos) q = cv.size();
+    std::string_view line = trim(cv.substr(p, q - p));
+    if (!line.empty()) {
+      auto cps = fold_cps(line);
+      int node = 0;
+      for (uint32_t c : cps) {
+        auto it = bl->trie[node].next.find(c);
+        if (it == bl->trie[node].next.end()) {
+          bl->trie.emplace_back();
+          int nn = (int)bl->trie.size() - 1;
+          bl->trie[node].next[c] = nn;
+          node = nn;
+        } else {
+          node = it->second;
+        }
+      }
+      bl->trie[node].term = true;
+      ++nwords;
+    }
+    p = q + 1;
+  }
+  std::shared_ptr<BadWordsLang> res = nwords ? bl : nullptr;
+  langs[lang] = res;
+  return res;
+}
+
+// Deterministic per-document uniform f32 in [0,1) (splitmix64 keyed by seed and row index).
+static float doc_uniform(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// ------------------------------------------------------------------------------------------
+BatchState::BatchState(int64_t n, const char* data, const int64_t* off, const char* meta_data,
+                       const int64_t* meta_off, const uint8_t* meta_valid, int nthreads)
+    : n_(n), nthreads_(std::max(1, nthreads)) {
+  versions_.emplace_back();
+  versions_[0].data = data;
+  versions_[0].off = off;
+  cur_version_.assign(n, 0);
+  fail_step_.assign(n, -1);
+  status_.assign(n, 0);
+  reason_.resize(n);
+  in_meta_.resize(n);
+  in_meta_valid_.assign(n, 0);
+  add_meta_.resize(n);
+  own_content_.resize(n);
+  if (meta_data && meta_off) {
+    std::atomic<int64_t> fails{0};
+    parallel_for(n, nthreads_, [&](int64_t a, int64_t b) {
+      int64_t f = 0;
+      for (int64_t i = a; i < b; ++i) {
+        if (meta_valid && !meta_valid[i]) continue;
+        std::string_view js(meta_data + meta_off[i], (size_t)(meta_off[i + 1] - meta_off[i]));
+        if (!parse_meta_json(js, in_meta_[i])) ++f;
+        in_meta_valid_[i] = 1;
+      }
+      fails += f;
+    });
+    meta_fail_ = fails.load();
+  }
+}
+
+std::string_view BatchState::content(int64_t i) const {
+  int v = cur_version_[i];
+  if (v < 0) return own_content_[i];
+  const Version& ver = versions_[v];
+  return std::string_view(ver.data + ver.off[i], (size_t)(ver.off[i + 1] - ver.off[i]));
+}
+
+int BatchState::add_version(const char* data, const int64_t* off) {
+  versions_.emplace_back();
+  versions_.back().data = data;
+  versions_.back().off = off;
+  return (int)versions_.size() - 1;
+}
+
+int BatchState::add_owned_version(std::string&& data, std::vector<int64_t>&& off) {
+  versions_.emplace_back();
+  Version& v = versions_.back();
+  v.own_data = std::move(data);
+  v.own_off = std::move(off);
+  v.data = v.own_data.data();
+  v.off = v.own_off.data();
+  return (int)versions_.size() - 1;
+}
+
+void BatchState::apply_decision(int64_t doc, int step_index, Decision& d) {
+  for (auto& kv : d.meta) meta_set(add_meta_[doc], kv.first, kv.second);
+  if (!d.pass) {
+    fail_step_[doc] = step_index;
+    status_[doc] = d.error ? 2 : 1;
+    reason_[doc] = std::move(d.reason);
+  }
+}
+
+void BatchState::apply_records(const StepCfg& cfg, int step_index, const int64_t* rec, int width,
+                               int rewrite_version) {
+  parallel_for(n_, nthreads_, [&](int64_t a, int64_t b) {
+    Decision d;
+    for (int64_t i = a; i < b; ++i) {
+      if (fail_step_[i] >= 0) continue;
+      const int64_t* r = rec + i * width;
+      decide(cfg, r, d);
+      if (cfg.kind == StepKind::C4Quality && rewrite_version >= 0 && !r[rec::C4_LOREM] &&
+          !r[rec::C4_CURLY])
+        cur_version_[i] = rewrite_version;
+      apply_decision(i, step_index, d);
+    }
+  });
+}
+
+void BatchState::apply_badwords(const StepCfg& cfg, int step_index, BadWordsModule& mod) {
+  // Language lists are loaded lazily on the calling thread, then matching runs in parallel.
+  std::vector<std::string> lang(n_);
+  for (int64_t i = 0; i < n_; ++i) {
+    if (fail_step_[i] >= 0) continue;
+    std::string l = cfg.default_language;
+    const MetaMap& m = add_meta_[i];
+    bool found = false;
+    for (auto& kv : m) if (kv.first == "language") { l = kv.second; found = true; }
+    if (!found)
+      for (auto& kv : in_meta_[i]) if (kv.first == "language") { l = kv.second; found = true; }
+    lang[i] = l;
+    bool sup;
+    mod.get(l, &sup);
+  }
+  parallel_for(n_, nthreads_, [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) {
+      if (fail_step_[i] >= 0) continue;
+      Decision d;
+      bool sup;
+      auto it = mod.langs.find(lang[i]);
+      std::shared_ptr<BadWordsLang> bl = it == mod.langs.end() ? nullptr : it->second;
+      sup = false;
+      for (auto l : kBadwordsLangs) if (lang[i] == l) sup = true;
+      if (!sup) {
+        if (cfg.fail_on_missing_language) {
+          d.pass = false;
+          d.reason = "There is no badwords list available for '" + lang[i] +
+                     "'. Set fail_on_missing_language=False to continue anyway.";
+          d.meta.push_back({"c4_badwords_filter_status", "filtered"});
+          d.meta.push_back({"c4_badwords_filter_reason", d.reason});
+        } else {
+          d.meta.push_back({"c4_badwords_filter_status", "passed_no_regex"});
+        }
+      } else if (!bl) {
+        d.meta.push_back({"c4_badwords_filter_status", "passed_no_regex"});
+      } else if (bl->match(content(i))) {
+        if (cfg.keep_fraction > 0.0 &&
+            doc_uniform(cfg.seed ? *cfg.seed : 0x5EEDull, (uint64_t)i) < (float)cfg.keep_fraction) {
+          d.meta.push_back({"c4_badwords_filter_status", "passed_kept_by_fraction"});
+        } else {
+          d.pass = false;
+          d.reason = "document_removed_with_badwords";
+          d.meta.push_back({"c4_badwords_filter_status", "filtered"});
+          d.meta.push_back({"c4_badwords_filter_reason", d.reason});
+        }
+      } else {
+        d.meta.push_back({"c4_badwords_filter_status", "passed"});
+      }
+      apply_decision(i, step_index, d);
+    }
+  });
+}
+
+void BatchState::run_cpu(const std::vector<StepCfg>& steps, int begin, int end, SegBackend be,
+                         const LangidModel* lid, BadWordsModule* bw) {
+  for (int s = begin; s < end; ++s) {
+    const StepCfg& cfg = steps[s];
+    if (cfg.kind == StepKind::C4BadWords) {
+      if (!bw) throw std::runtime_error("C4BadWordsFilter requires a badwords module");
+      apply_badwords(cfg, s, *bw);
+      continue;
+    }
+    if (cfg.kind == StepKind::TokenCounter)
+      throw std::runtime_error("TokenCounter records must be supplied by the host tokenizer");
+    if (cfg.kind == StepKind::LanguageDetection && !lid)
+      throw std::runtime_error("LanguageDetectionFilter requires a language-id model");
+    const int width = record_width(cfg);
+    parallel_for(n_, nthreads_, [&](int64_t a, int64_t b) {
+      std::vector<int64_t> r(width);
+      Decision d;
+      std::string nc;
+      for (int64_t i = a; i < b; ++i) {
+        if (fail_step_[i] >= 0) continue;
+        std::string_view text = content(i);
+        std::fill(r.begin(), r.end(), 0);
+        if (cfg.kind == StepKind::LanguageDetection) {
+          double conf = 0;
+          r[rec::LD_LANG] = lid->detect(text, &conf);
+          std::memcpy(&r[rec::LD_CONF_BITS], &conf, sizeof(double));
+        } else {
+          compute_record(cfg, text, be, r.data(), &nc);
+        }
+        decide(cfg, r.data(), d);
+        if (cfg.kind == StepKind::C4Quality && !r[rec::C4_LOREM] && !r[rec::C4_CURLY]) {
+          own_content_[i] = std::move(nc);
+          cur_version_[i] = -1;
+        }
+        apply_decision(i, s, d);
+      }
+    });
+  }
+}
+
+std::vector<int64_t> BatchState::alive_indices() const {
+  std::vector<int64_t> out;
+  for (int64_t i = 0; i < n_; ++i) if (fail_step_[i] < 0) out.push_back(i);
+  return out;
+}
+
+void BatchState::assemble(const std::vector<int64_t>& idx, std::string& text_data,
+                          std::vector<int64_t>& text_off, std::string& meta_data,
+                          std::vector<int64_t>& meta_off, std::vector<uint8_t>& meta_valid) const {
+  const int64_t m = (int64_t)idx.size();
+  const int nchunks = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads_ * 4, m / 256));
+  std::vector<std::string> tparts(nchunks), mparts(nchunks);
+  std::vector<std::vector<int64_t>> tlen(nchunks), mlen(nchunks);
+  meta_valid.assign(m, 0);
+  std::atomic<int> next{0};
+  auto worker = [&]() {
+    while (true) {
+      int c = next.fetch_add(1);
+      if (c >= nchunks) break;
+      int64_t a = m * c / nchunks, b = m * (c + 1) / nchunks;
+      std::string& td = tparts[c];
+      std::string& md = mparts[c];
+      MetaMap merged;
+      for (int64_t k = a; k < b; ++k) {
+        int64_t i = idx[k];
+        std::string_view t = content(i);
+        td.append(t.data(), t.size());
+        tlen[c].push_back((int64_t)t.size());
+        merged = in_meta_[i];
+        for (auto& kv : add_meta_[i]) meta_set(merged, kv.first, kv.second);
+        if (merged.empty()) {
+          mlen[c].push_back(0);
+        } else {
+          size_t before = md.size();
+          serialize_meta_json(merged, md);
+          mlen[c].push_back((int64_t)(md.size() - before));
+          meta_valid[k] = 1;
+        }
+      }
+    }
+  };
+  std::vector<std::thread> ts;
+  for (int t = 1; t < std::min(nthreads_, nchunks); ++t) ts.emplace_back(worker);
+  worker();
+  for (auto& t : ts) t.join();
+  text_off.assign(m + 1, 0);
+  meta_off.assign(m + 1, 0);
+  size_t tt = 0, mt = 0;
+  for (int c = 0; c < nchunks; ++c) { tt += tparts[c].size(); mt += mparts[c].size(); }
+  text_data.clear();
+  text_data.reserve(tt);
+  meta_data.clear();
+  meta_data.reserve(mt);
+  int64_t k = 0;
+  for (int c = 0; c < nchunks; ++c) {
+    text_data += tparts[c];
+    meta_data += mparts[c];
+    for (size_t j = 0; j < tlen[c].size(); ++j, ++k) {
+      text_off[k + 1] = text_off[k] + tlen[c][j];
+      meta_off[k + 1] = meta_off[k] + mlen[c][j];
+    }
+  }
+}
+
+}  // namespace tb

@@ -1,0 +1,105 @@
+// Batch execution state shared by the CPU path and the GPU path.
+//
+// A batch holds the documents of one Parquet read batch as packed UTF-8 (data + int64 offsets).
+// Steps are applied in pipeline order; per document the first failing step wins and later
+// steps do not run (reference executor.rs:30-57). Metadata written by executed steps is kept in
+// insertion order and merged over the input metadata when the outputs are assembled.
+#pragma once
+#include <atomic>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "filters.h"
+#include "json.h"
+
+namespace tb {
+
+void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t, int64_t)>& fn);
+
+struct LangidModel {
+  std::vector<uint16_t> emb;   // [kLidBuckets * kLidDim] bf16
+  std::vector<uint16_t> w;     // [kLidDim * kLidLangsPad] bf16
+  std::vector<float> b;        // [kLidLangsPad]
+  // Detect the language of `text`: returns lang index or -1, confidence in *conf.
+  int detect(std::string_view text, double* conf) const;
+  // Doc vector (bf16 bits) + n-gram count (for tests / training).
+  int featurize(std::string_view text, uint16_t* out_vec) const;
+};
+
+// C4 bad-words matcher for one language (reference c4_filters.rs:298-551).
+struct BadWordsLang {
+  bool cjk = false;
+  struct Node { std::unordered_map<uint32_t, int> next; bool term = false; };
+  std::vector<Node> trie;
+  bool match(std::string_view text) const;
+};
+
+struct BadWordsModule {
+  std::string cache_dir;
+  std::unordered_map<std::string, std::shared_ptr<BadWordsLang>> langs;  // nullptr = no list
+  std::shared_ptr<BadWordsLang> get(const std::string& lang, bool* supported);
+};
+
+struct Version {
+  const char* data = nullptr;
+  const int64_t* off = nullptr;
+  std::string own_data;
+  std::vector<int64_t> own_off;
+};
+
+class BatchState {
+ public:
+  BatchState(int64_t n, const char* data, const int64_t* off, const char* meta_data,
+             const int64_t* meta_off, const uint8_t* meta_valid, int nthreads);
+
+  int64_t size() const { return n_; }
+  int nthreads() const { return nthreads_; }
+  std::string_view content(int64_t i) const;
+  int add_version(const char* data, const int64_t* off);  // borrowed buffers
+  int add_owned_version(std::string&& data, std::vector<int64_t>&& off);
+
+  // Apply a step whose per-document records were computed elsewhere (GPU or CPU runner).
+  // For C4 steps `rewrite_version` is the version holding the rewritten contents.
+  void apply_records(const StepCfg& cfg, int step_index, const int64_t* rec, int width,
+                     int rewrite_version);
+  // CPU path: compute records for alive docs and apply them for steps [begin, end).
+  void run_cpu(const std::vector<StepCfg>& steps, int begin, int end, SegBackend be,
+               const LangidModel* lid, BadWordsModule* bw);
+  void apply_badwords(const StepCfg& cfg, int step_index, BadWordsModule& mod);
+
+  std::vector<int64_t> alive_indices() const;
+  const std::vector<int32_t>& fail_step() const { return fail_step_; }
+  const std::vector<uint8_t>& status() const { return status_; }  // 0 ok, 1 filtered, 2 error
+  const std::vector<int32_t>& cur_version() const { return cur_version_; }
+  const std::string& reason(int64_t i) const { return reason_[i]; }
+
+  // Output assembly for a subset of documents (indices): contents and metadata JSON.
+  void assemble(const std::vector<int64_t>& idx, std::string& text_data, std::vector<int64_t>& text_off,
+                std::string& meta_data, std::vector<int64_t>& meta_off, std::vector<uint8_t>& meta_valid) const;
+  int64_t meta_parse_failures() const { return meta_fail_; }
+
+ private:
+  void apply_decision(int64_t doc, int step_index, Decision& d);
+  const MetaMap& input_meta(int64_t i) const { return in_meta_[i]; }
+
+  int64_t n_;
+  int nthreads_;
+  std::vector<Version> versions_;
+  std::vector<int32_t> cur_version_;
+  std::vector<int32_t> fail_step_;
+  std::vector<uint8_t> status_;
+  std::vector<std::string> reason_;
+  std::vector<MetaMap> in_meta_;
+  std::vector<uint8_t> in_meta_valid_;
+  std::vector<MetaMap> add_meta_;
+  std::vector<std::string> own_content_;  // CPU path rewritten contents (cur_version == -1)
+  int64_t meta_fail_ = 0;
+};
+
+}  // namespace tb

@@ -1,0 +1,168 @@
+"""Native components: build and load.
+
+* ``_tbhost`` — pybind11 extension (g++): text primitives, the CPU pipeline, batch resolver,
+  output assembly, HTML decoding, device-plan building and the host emulation of the device
+  algorithms. Links ICU4C (the segmentation oracle).
+* ``libtbhip.so`` — HIP kernels for gfx950 (hipcc), C ABI, loaded with ctypes. Device memory
+  and streams come from PyTorch-ROCm; the library only launches kernels on the given stream.
+
+Both are built in-tree (``textblaster_amd/``) so they travel with the repository snapshot.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import sys
+import sysconfig
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from typing import List, Optional
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(REPO_DIR, "csrc")
+BUILD_DIR = os.path.join(REPO_DIR, "build")
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX")
+HOST_EXT = os.path.join(PKG_DIR, "_tbhost" + EXT_SUFFIX)
+HIP_LIB = os.path.join(PKG_DIR, "libtbhip.so")
+GPU_ARCH = os.environ.get("TB_GPU_ARCH", "gfx950")
+
+_lock = threading.Lock()
+_host = None
+_hip = None
+
+
+def _sources(sub: str, ext: str) -> List[str]:
+    d = os.path.join(CSRC, sub)
+    return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(ext))
+
+
+def _headers() -> List[str]:
+    out = []
+    for sub in ("common", "host", "hip"):
+        d = os.path.join(CSRC, sub)
+        if os.path.isdir(d):
+            out += [os.path.join(d, f) for f in os.listdir(d) if f.endswith((".h", ".inc"))]
+    return out
+
+
+def _newest(paths: List[str]) -> float:
+    return max((os.path.getmtime(p) for p in paths), default=0.0)
+
+
+def _run(cmd: List[str], verbose: bool) -> None:
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"native build failed:\n{' '.join(cmd)}\n{r.stdout}")
+
+
+def build_host(verbose: bool = False, force: bool = False) -> str:
+    import pybind11
+
+    srcs = _sources("host", ".cpp")
+    hdrs = _headers()
+    if (not force and os.path.exists(HOST_EXT)
+            and os.path.getmtime(HOST_EXT) >= _newest(srcs + hdrs)):
+        return HOST_EXT
+    os.makedirs(os.path.join(BUILD_DIR, "host"), exist_ok=True)
+    inc = ["-I" + sysconfig.get_paths()["include"], "-I" + pybind11.get_include()]
+    flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
+             "-march=x86-64-v2"]
+    objs = []
+
+    def compile_one(src: str) -> str:
+        obj = os.path.join(BUILD_DIR, "host", os.path.basename(src) + ".o")
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < _newest([src] + hdrs):
+            _run(["g++", *flags, *inc, "-c", src, "-o", obj], verbose)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    tmp = HOST_EXT + ".tmp"
+    _run(["g++", "-shared", "-o", tmp, *objs, "-licuuc", "-lpthread"], verbose)
+    os.replace(tmp, HOST_EXT)
+    return HOST_EXT
+
+
+def hipcc_path() -> Optional[str]:
+    for p in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc"):
+        if p and os.path.exists(p):
+            return p
+    return None
+
+
+def build_hip(verbose: bool = False, force: bool = False) -> str:
+    hipcc = hipcc_path()
+    if hipcc is None:
+        raise RuntimeError("hipcc not found (ROCm required to build the device library)")
+    srcs = _sources("hip", ".hip")
+    hdrs = _headers()
+    if (not force and os.path.exists(HIP_LIB)
+            and os.path.getmtime(HIP_LIB) >= _newest(srcs + hdrs)):
+        return HIP_LIB
+    os.makedirs(os.path.join(BUILD_DIR, "hip"), exist_ok=True)
+    flags = [f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffast-math",
+             "-fno-gpu-rdc", "-munsafe-fp-atomics"]
+    objs = []
+
+    def compile_one(src: str) -> str:
+        obj = os.path.join(BUILD_DIR, "hip", os.path.basename(src) + ".o")
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < _newest([src] + hdrs):
+            _run([hipcc, *flags, "-c", src, "-o", obj], verbose)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    tmp = HIP_LIB + ".tmp"
+    _run([hipcc, f"--offload-arch={GPU_ARCH}", "-shared", "-fPIC", "-o", tmp, *objs], verbose)
+    os.replace(tmp, HIP_LIB)
+    return HIP_LIB
+
+
+def build_all(verbose: bool = False) -> None:
+    build_host(verbose)
+    build_hip(verbose)
+
+
+def host():
+    """The host extension module (built on first use if missing)."""
+    global _host
+    if _host is None:
+        with _lock:
+            if _host is None:
+                if not os.path.exists(HOST_EXT):
+                    build_host()
+                from . import _tbhost  # type: ignore
+
+                _host = _tbhost
+    return _host
+
+
+def hip() -> ctypes.CDLL:
+    """The HIP kernel library (fails loudly if missing: the GPU path never silently falls back)."""
+    global _hip
+    if _hip is None:
+        with _lock:
+            if _hip is None:
+                if not os.path.exists(HIP_LIB):
+                    build_hip()
+                _hip = ctypes.CDLL(HIP_LIB, mode=ctypes.RTLD_GLOBAL)
+                _declare_hip(_hip)
+    return _hip
+
+
+def _declare_hip(lib: ctypes.CDLL) -> None:
+    from .ops import kernels
+
+    kernels.declare(lib)
+
+
+if __name__ == "__main__":  # python -m textblaster_amd.native [host|hip|all]
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what in ("host", "all"):
+        print(build_host(verbose=True, force="--force" in sys.argv))
+    if what in ("hip", "all"):
+        print(build_hip(verbose=True, force="--force" in sys.argv))

@@ -546,18 +546,20 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       x.par.single([&]() { r[rec_gr_fixed() + t] = res; });
     }
     if (ds.n_dup > 0) {
-      uint32_t* gcs[kMaxNgramEntries];
-      uint32_t* seen[kMaxNgramEntries];
+      // per-n canonical-gram arrays and visited bitmaps; their scratch offsets are kept in scratch
+      uint64_t* gofs = x.template alloc<uint64_t>(2 * kMaxNgramEntries);
+      if (x.overflow) return;
       for (int t = 0; t < ds.n_dup; ++t) {
         const uint32_t n = (uint32_t)ds.dup_n[t];
-        gcs[t] = nullptr;
-        seen[t] = nullptr;
         if (n == 0 || W < n) continue;
         const uint32_t G = W - n + 1;
-        gcs[t] = x.template alloc<uint32_t>(G);
-        seen[t] = x.template alloc<uint32_t>((G + 31) / 32 + 1);
+        uint32_t* gct = x.template alloc<uint32_t>(G);
+        uint32_t* sn = x.template alloc<uint32_t>((G + 31) / 32 + 1);
         if (x.overflow) return;
-        uint32_t* sn = seen[t];
+        x.par.single([&]() {
+          gofs[2 * t] = (uint64_t)((char*)gct - x.scr);
+          gofs[2 * t + 1] = (uint64_t)((char*)sn - x.scr);
+        });
         x.par.for_n((G + 31) / 32 + 1, [&](uint32_t i) { sn[i] = 0; });
         canonicalize(
             x, G,
@@ -578,7 +580,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
               }
               return true;
             },
-            gcs[t]);
+            gct);
       }
       x.par.sync();
       const int ndup = ds.n_dup;
@@ -586,8 +588,8 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
         const uint32_t n = (uint32_t)ds.dup_n[t];
         int64_t rep = 0;
         if (n > 0 && W >= n) {
-          const uint32_t* gc = gcs[t];
-          uint32_t* sn = seen[t];
+          const uint32_t* gc = (const uint32_t*)(x.scr + gofs[2 * t]);
+          uint32_t* sn = (uint32_t*)(x.scr + gofs[2 * t + 1]);
           uint32_t idx = 0;
           while (idx + n <= W) {
             const uint32_t g = gc[idx];
@@ -635,16 +637,15 @@ TB_HD void langid_features(DocCtx<P>& x, const Cps& c, const uint16_t* emb, Stag
     lid_grams_at(Lf((int64_t)i - 2), Lf((int64_t)i - 1), Lf(i), true, true, [&](uint32_t bk) { G[o++] = bk; });
   });
   x.par.sync();
-  int64_t acc[kLidDim];
-  x.par.template gather_rows_fixed<kLidDim>(K, [&](uint32_t k) { return emb + (size_t)G[k] * kLidDim; }, acc);
   const uint32_t doc = out.doc;
-  x.par.single([&]() {
-    out.lid_cnt[doc] = (int32_t)K;
-    for (int d = 0; d < kLidDim; ++d) {
-      float v = K ? (float)((double)acc[d] / (double)K / (double)kLidFixedScale) : 0.0f;
-      out.lid_vec[(size_t)doc * kLidDim + d] = f32_to_bf16(v);
-    }
-  });
+  uint16_t* vec = out.lid_vec + (size_t)doc * kLidDim;
+  x.par.template gather_rows_fixed<kLidDim>(
+      K, [&](uint32_t k) { return emb + (size_t)G[k] * kLidDim; },
+      [&](int d, int64_t sum) {
+        float v = K ? (float)((double)sum / (double)K / (double)kLidFixedScale) : 0.0f;
+        vec[d] = f32_to_bf16(v);
+      });
+  x.par.single([&]() { out.lid_cnt[doc] = (int32_t)K; });
   x.used = mark;
 }
 
@@ -900,7 +901,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
 
   for (int s = 0; s < st.n_steps; ++s) {
     const DevStep& ds = st.steps[s];
-    int64_t* r = out.rec + ds.rec_base + (int64_t)out.doc * ds.width;
+    int64_t* r = out.rec + (int64_t)ds.rec_prefix * out.ndocs + (int64_t)out.doc * ds.width;
     if (ds.kind == DK_GOPHER_QUALITY) {
       const DevStopSet& ss = plan.stops[ds.stop_set];
       const UcdView ucd = x.ucd;

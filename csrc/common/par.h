@@ -76,14 +76,16 @@ struct SeqPar {
   static void min32(uint32_t* p, uint32_t v) { if (v < *p) *p = v; }
   static void max32(uint32_t* p, uint32_t v) { if (v > *p) *p = v; }
   static uint32_t add32(uint32_t* p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
-  // Sum of fixed-point embedding rows: acc[d] = sum_k fixed(E[rows[k]][d]), d < D.
-  template <int D, class Row>
-  void gather_rows_fixed(uint32_t K, Row&& row_ptr, int64_t* acc) const {
+  // Sum of fixed-point embedding rows: out(d, sum_k fixed(E[rows[k]][d])) for d < D.
+  template <int D, class Row, class Out>
+  void gather_rows_fixed(uint32_t K, Row&& row_ptr, Out&& out) const {
+    int64_t acc[D];
     for (int d = 0; d < D; ++d) acc[d] = 0;
     for (uint32_t k = 0; k < K; ++k) {
       const uint16_t* r = row_ptr(k);
       for (int d = 0; d < D; ++d) acc[d] += lid_fixed(r[d]);
     }
+    for (int d = 0; d < D; ++d) out(d, acc[d]);
   }
 };
 
@@ -172,15 +174,14 @@ struct WavePar {
   __device__ static void max32(uint32_t* p, uint32_t v) { atomicMax(p, v); }
   __device__ static uint32_t add32(uint32_t* p, uint32_t v) { return atomicAdd(p, v); }
 
-  template <int D, class Row>
-  __device__ void gather_rows_fixed(uint32_t K, Row&& row_ptr, int64_t* acc) const {
+  template <int D, class Row, class Out>
+  __device__ void gather_rows_fixed(uint32_t K, Row&& row_ptr, Out&& out) const {
     static_assert(D == 32, "lane layout assumes 32 dims");
     const int d = lane & 31, h = lane >> 5;
     int64_t s = 0;
     for (uint32_t k = h; k < K; k += 2) s += lid_fixed(row_ptr(k)[d]);
     s += __shfl_xor(s, 32);
-    // every lane ends with its dimension's total; lanes 0..31 publish
-    for (int j = 0; j < D; ++j) acc[j] = __shfl(s, j);
+    if (lane < 32) out(d, s);
   }
 
  private:

@@ -1,0 +1,196 @@
+// HIP kernels for gfx950 (MI355X). C ABI, launched on a caller-provided stream (PyTorch's).
+//
+// Document kernels run one wavefront per document (block = 64 lanes = one wave64): the lanes
+// cooperate through DPP shuffles and ballots (csrc/common/par.h WavePar), per-document working
+// arrays live in a per-document slice of an HBM scratch arena (L2-resident while the wave
+// works on it). Grid = number of documents, visited through a length-sorted permutation so the
+// longest documents start first (tail-latency balance under the power-law length distribution).
+//
+//  tb_stage_analyze : decode + UAX#29 words + lines + hashes -> Gopher/FineWeb records,
+//                     language-id n-gram doc vectors
+//  tb_c4_pass_a     : C4 line filtering, citation removal, rewritten text into scratch
+//  tb_c4_pass_b     : compaction of the rewritten texts into the next content version
+//  tb_langid_head   : bf16 MFMA (v_mfma_f32_16x16x32_bf16) linear head + softmax -> records
+#include <hip/hip_runtime.h>
+
+#include "../common/docproc.h"
+
+using namespace tb;
+
+namespace {
+
+struct DevTables {
+  const uint16_t* s1;
+  const uint32_t* s2;
+  const uint16_t* l1;
+  const int32_t* l2;
+};
+
+__device__ __forceinline__ DocCtx<WavePar> make_ctx(const DevTables& t, const uint64_t* pw, uint32_t pw_n,
+                                                   char* scratch, const int64_t* scratch_off, int doc,
+                                                   uint32_t* flags) {
+  DocCtx<WavePar> x;
+  x.ucd = UcdView{t.s1, t.s2, t.l1, t.l2};
+  x.pw = pw;
+  x.pw_n = pw_n;
+  x.scr = scratch + scratch_off[doc];
+  x.cap = (uint64_t)(scratch_off[doc + 1] - scratch_off[doc]);
+  x.used = 0;
+  x.flag = flags + doc;
+  return x;
+}
+
+__global__ __launch_bounds__(64) void k_stage_analyze(
+    const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes,
+    const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,
+    const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
+    int64_t* rec, uint32_t* flags, const uint16_t* __restrict__ lid_emb, uint16_t* lid_vec, int32_t* lid_cnt) {
+  const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
+  if (doc >= ndocs) return;
+  DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags);
+  const uint8_t* b = bytes + off[doc];
+  const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
+  StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, lid_vec, lid_cnt};
+  analyze_stage(x, *stage, *plan, lid_emb, b, n, out);
+}
+
+__global__ __launch_bounds__(64) void k_c4_pass_a(
+    const DevC4* __restrict__ c4, const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
+    const int32_t* __restrict__ perm, int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off,
+    const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec, int64_t* src, uint32_t* flags) {
+  const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
+  if (doc >= ndocs) return;
+  DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags);
+  const uint8_t* b = bytes + off[doc];
+  const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
+  c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2);
+}
+
+__global__ __launch_bounds__(256) void k_c4_pass_b(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
+                                                   int32_t ndocs, const char* __restrict__ scratch,
+                                                   const int64_t* __restrict__ scratch_off,
+                                                   const int64_t* __restrict__ src, const int64_t* __restrict__ new_off,
+                                                   uint8_t* __restrict__ out) {
+  const int doc = blockIdx.x;
+  if (doc >= ndocs) return;
+  const int64_t len = new_off[doc + 1] - new_off[doc];
+  const int64_t s = src[2 * doc];
+  const uint8_t* from = s < 0 ? bytes + off[doc] : (const uint8_t*)scratch + scratch_off[doc] + s;
+  uint8_t* to = out + new_off[doc];
+  for (int64_t i = threadIdx.x; i < len; i += blockDim.x) to[i] = from[i];
+}
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// One wave = 16 documents: logits[16 x 16] = X[16 x 32] . W[32 x 16] in one MFMA.
+// A lane layout: lane l holds X[row l&15][k 8(l>>4) .. +8]; B: W[k 8(l>>4)+j][col l&15] read from
+// the transposed weights wT[col][k]; D: col = l&15, row = 4(l>>4) + i.
+__global__ __launch_bounds__(64) void k_langid_head(const uint16_t* __restrict__ vec, const int32_t* __restrict__ cnt,
+                                                    const uint16_t* __restrict__ wT, const float* __restrict__ bias,
+                                                    int32_t ndocs, int64_t* rec, int64_t rec_off, int32_t width) {
+  const int lane = threadIdx.x;
+  const int row0 = blockIdx.x * 16;
+  const int r = row0 + (lane & 15);
+  bf16x8 a;
+  if (r < ndocs) {
+    a = *reinterpret_cast<const bf16x8*>(vec + (size_t)r * kLidDim + 8 * (lane >> 4));
+  } else {
+    for (int j = 0; j < 8; ++j) a[j] = (__bf16)0.0f;
+  }
+  const bf16x8 bw = *reinterpret_cast<const bf16x8*>(wT + (size_t)(lane & 15) * kLidDim + 8 * (lane >> 4));
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw, acc, 0, 0, 0);
+  const int col = lane & 15;
+  const float bcol = bias[col];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = row0 + 4 * (lane >> 4) + i;
+    const bool valid = col < kLidLangs;
+    float v = valid ? acc[i] + bcol : -3.0e38f;
+    // arg-max over the 16 lanes of this row group (ties -> lowest column)
+    float bv = v;
+    int bc = col;
+    for (int o = 1; o < 16; o <<= 1) {
+      float ov = __shfl_xor(bv, o);
+      int oc = __shfl_xor(bc, o);
+      if (ov > bv || (ov == bv && oc < bc)) { bv = ov; bc = oc; }
+    }
+    double e = valid ? exp((double)v - (double)bv) : 0.0;
+    for (int o = 1; o < 16; o <<= 1) e += __shfl_xor(e, o);
+    if (col == 0 && row < ndocs) {
+      int64_t* rr = rec + rec_off + (int64_t)row * width;
+      if (cnt[row] == 0) {
+        rr[0] = -1;
+        rr[1] = 0;
+      } else {
+        const double conf = 1.0 / e;
+        rr[0] = bc;
+        rr[1] = __double_as_longlong(conf);
+      }
+      rr[2] = 0;
+    }
+  }
+}
+
+__global__ void k_pow_table(uint64_t* pw, uint32_t n) {
+  // pw[i] = B^i, computed independently per element (exact modular arithmetic)
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= n) pw[i] = powmod61(kHashBase, i);
+}
+
+}  // namespace
+
+extern "C" {
+
+int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, const uint8_t* bytes,
+                     const int64_t* off, const int32_t* perm, int32_t ndocs, char* scratch,
+                     const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
+                     const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
+                     const uint16_t* lid_emb, uint16_t* lid_vec, int32_t* lid_cnt) {
+  if (ndocs <= 0) return 0;
+  DevTables t{s1, s2, l1, l2};
+  hipLaunchKernelGGL(k_stage_analyze, dim3(ndocs), dim3(64), 0, stream, (const DevPlan*)plan,
+                     (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, flags,
+                     lid_emb, lid_vec, lid_cnt);
+  return (int)hipGetLastError();
+}
+
+int tb_c4_pass_a(hipStream_t stream, const void* c4, const uint8_t* bytes, const int64_t* off, const int32_t* perm,
+                 int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n,
+                 const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
+                 int64_t* src, uint32_t* flags) {
+  if (ndocs <= 0) return 0;
+  DevTables t{s1, s2, l1, l2};
+  hipLaunchKernelGGL(k_c4_pass_a, dim3(ndocs), dim3(64), 0, stream, (const DevC4*)c4, bytes, off, perm, ndocs,
+                     scratch, scratch_off, pw, pw_n, t, rec, src, flags);
+  return (int)hipGetLastError();
+}
+
+int tb_c4_pass_b(hipStream_t stream, const uint8_t* bytes, const int64_t* off, int32_t ndocs, const char* scratch,
+                 const int64_t* scratch_off, const int64_t* src, const int64_t* new_off, uint8_t* out) {
+  if (ndocs <= 0) return 0;
+  hipLaunchKernelGGL(k_c4_pass_b, dim3(ndocs), dim3(256), 0, stream, bytes, off, ndocs, scratch, scratch_off, src,
+                     new_off, out);
+  return (int)hipGetLastError();
+}
+
+int tb_langid_head(hipStream_t stream, const uint16_t* vec, const int32_t* cnt, const uint16_t* wT,
+                   const float* bias, int32_t ndocs, int64_t* rec, int64_t rec_off, int32_t width) {
+  if (ndocs <= 0) return 0;
+  hipLaunchKernelGGL(k_langid_head, dim3((ndocs + 15) / 16), dim3(64), 0, stream, vec, cnt, wT, bias, ndocs, rec,
+                     rec_off, width);
+  return (int)hipGetLastError();
+}
+
+int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
+  hipLaunchKernelGGL(k_pow_table, dim3((n + 256) / 256), dim3(256), 0, stream, pw, n);
+  return (int)hipGetLastError();
+}
+
+int tb_abi_version() { return 1; }
+size_t tb_sizeof_plan() { return sizeof(DevPlan); }
+size_t tb_sizeof_stage() { return sizeof(DevStage); }
+size_t tb_sizeof_c4() { return sizeof(DevC4); }
+
+}  // extern "C"

@@ -149,7 +149,6 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
   DevPlan* plan = new DevPlan();
   std::memset(plan, 0, sizeof(DevPlan));
   DevStage st = build_stage(steps, idx, *plan);
-  for (int s = 0; s < st.n_steps; ++s) st.steps[s].rec_base = (int64_t)st.steps[s].rec_prefix * ndocs;
   bool has_lid = false;
   for (int s = 0; s < st.n_steps; ++s) has_lid |= st.steps[s].kind == DK_LANGID;
   if (has_lid && !lid) { delete plan; throw std::runtime_error("language model required"); }
@@ -180,7 +179,7 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
         for (int s = 0; s < st.n_steps; ++s)
           if (st.steps[s].kind == DK_LANGID)
             lid_head_host(*lid, &lvec[(size_t)i * kLidDim], lcnt[i],
-                          rec.data() + st.steps[s].rec_base + i * st.steps[s].width);
+                          rec.data() + (int64_t)st.steps[s].rec_prefix * ndocs + i * st.steps[s].width);
       }
     }
   });

@@ -355,6 +355,9 @@ PYBIND11_MODULE(_tbhost, m) {
         py::gil_scoped_release nogil;
         b.st->apply_badwords(c, step_index, *bw);
       })
+      .def("delegate", [](PyBatch& b, py::array_t<int64_t, py::array::c_style> idx) {
+        b.st->delegate(idx.data(), (int64_t)idx.size());
+      })
       .def("alive_indices", [](PyBatch& b) { return to_numpy(b.st->alive_indices()); })
       .def("fail_step", [](PyBatch& b) { return to_numpy(std::vector<int32_t>(b.st->fail_step())); })
       .def("status", [](PyBatch& b) { return to_numpy(std::vector<uint8_t>(b.st->status())); })

@@ -353,6 +353,15 @@ void BatchState::run_cpu(const std::vector<StepCfg>& steps, int begin, int end, 
   }
 }
 
+void BatchState::delegate(const int64_t* idx, int64_t n) {
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t i = idx[k];
+    if (i < 0 || i >= n_) continue;
+    fail_step_[i] = 1 << 30;
+    status_[i] = 3;
+  }
+}
+
 std::vector<int64_t> BatchState::alive_indices() const {
   std::vector<int64_t> out;
   for (int64_t i = 0; i < n_; ++i) if (fail_step_[i] < 0) out.push_back(i);

@@ -73,6 +73,8 @@ class BatchState {
                const LangidModel* lid, BadWordsModule* bw);
   void apply_badwords(const StepCfg& cfg, int step_index, BadWordsModule& mod);
 
+  // Remove documents from this batch (they are processed elsewhere, e.g. the CPU oracle path).
+  void delegate(const int64_t* idx, int64_t n);
   std::vector<int64_t> alive_indices() const;
   const std::vector<int32_t>& fail_step() const { return fail_step_; }
   const std::vector<uint8_t>& status() const { return status_; }  // 0 ok, 1 filtered, 2 error

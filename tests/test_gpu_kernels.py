@@ -1,0 +1,81 @@
+"""Device kernels vs. the host emulation of the same algorithms (bit-exact records) and vs. the
+ICU oracle (end-to-end decisions). Needs an MI355X."""
+import numpy as np
+import pytest
+
+from textblaster_amd.config import load_pipeline_config
+from textblaster_amd.utils import synth
+
+pytestmark = pytest.mark.gpu
+
+EDGE = ["", "   ", "\n\n", "a", "a\r\nb\r\n", "Hello.\n\n\nHello.\n\nHello.", "x [1] y [2, 3]. z",
+        "ΣΑΣ ΣΑΣ.", "İstanbul THE the", "cooKie policy is here.", "lorem IPSUM dolor", "{ curly }",
+        "日本語のテキストです。", "mixed 日本 text. Another sentence here.", "- bullet\n- bullet\n• x...",
+        "a b a b a b a b a b a b a b", "ab c a bc ab c a bc"]
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    texts = synth.make_corpus(3000, 1024, seed=11) + EDGE
+    texts += [synth.make_doc(np.random.default_rng(7), "eng", 40000)]  # long doc
+    return texts
+
+
+@pytest.fixture(scope="module")
+def runner_parts(host):
+    import torch
+
+    assert torch.cuda.is_available()
+    from textblaster_amd.models.langid import load_default
+    from textblaster_amd.pipeline.device import DeviceRunner
+    from textblaster_amd.pipeline.plan import build_plan
+
+    cfg = load_pipeline_config("config/pipeline_config.yaml")
+    cfg.pipeline = [s for s in cfg.pipeline if s.type != "TokenCounter"]
+    steps = [host.make_step(s.native_dict()) for s in cfg.pipeline]
+    plan = build_plan(cfg)
+    lid = load_default()
+    return cfg, steps, plan, DeviceRunner(steps, plan, "cuda:0", lid), lid
+
+
+def test_device_records_match_host_emulation(host, corpus, runner_parts):
+    cfg, steps, plan, runner, lid = runner_parts
+    data, off = synth.pack(corpus)
+    res = runner.run(data, off)
+    n = len(corpus)
+    for s, idx in enumerate(plan.stages):
+        ver = plan.stage_version[s]
+        vd, vo = (data, off) if ver == 0 else res.versions[ver]
+        ref, rflags = host.emulate_stage(steps, idx, np.ascontiguousarray(vd), np.ascontiguousarray(vo), 8,
+                                         lid.native())
+        got = res.stage_recs[s]
+        width_total, layout = runner.stage_layout[s]
+        for (kind, width, prefix), step_i in zip(layout, idx):
+            a = got[prefix * n:(prefix + width) * n].reshape(n, width)
+            b = ref[prefix * n:(prefix + width) * n].reshape(n, width)
+            ok = (res.flags == 0) & (rflags == 0)
+            if kind == 4:  # language id: identical language, confidence within fp32-sum tolerance
+                assert np.array_equal(a[ok, 0], b[ok, 0]), steps[step_i].name
+                ca = a[ok, 1].view(np.float64)
+                cb = b[ok, 1].view(np.float64)
+                assert np.allclose(ca, cb, rtol=1e-5, atol=1e-6)
+            else:
+                bad = np.nonzero(~np.all(a[ok] == b[ok], axis=1))[0]
+                assert len(bad) == 0, (steps[step_i].name, bad[:5], a[ok][bad[:3]], b[ok][bad[:3]])
+    # C4 pass: records and rewritten text
+    for i in plan.c4_steps:
+        ver = plan.steps[i].version_in
+        vd, vo = (data, off) if ver == 0 else res.versions[ver]
+        rrec, rdata, roff, rflags = host.emulate_c4(steps[i], np.ascontiguousarray(vd), np.ascontiguousarray(vo), 8)
+        ok = (res.flags == 0) & (rflags == 0)
+        assert np.array_equal(res.c4_recs[i].reshape(n, 7)[ok], rrec.reshape(n, 7)[ok])
+        gd, go = res.versions[plan.steps[i].version_out]
+        for d in np.nonzero(ok)[0]:
+            assert bytes(gd[go[d]:go[d + 1]]) == bytes(rdata[roff[d]:roff[d + 1]])
+
+
+def test_dictionary_scripts_are_flagged(host, runner_parts):
+    _, _, _, runner, _ = runner_parts
+    data, off = synth.pack(["日本語のテキストです。", "plain english text here."])
+    res = runner.run(data, off)
+    assert res.flags[0] != 0 and res.flags[1] == 0

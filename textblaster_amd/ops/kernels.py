@@ -1,0 +1,107 @@
+"""ctypes bindings for libtbhip.so (csrc/hip/kernels.hip) and thin launch helpers.
+
+Device memory is owned by PyTorch (``torch.empty(..., device="cuda")``); kernels are launched on
+the caller's current PyTorch stream. Every launch checks the returned hipError_t and raises —
+there is no silent fallback on a GPU box.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+from ..errors import DeviceError
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_U32 = ctypes.c_uint32
+_I64 = ctypes.c_int64
+
+_SIGS = {
+    "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P],
+    "tb_c4_pass_b": [_P, _P, _P, _I32, _P, _P, _P, _P, _P],
+    "tb_langid_head": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I32],
+    "tb_pow_table": [_P, _P, _U32],
+    "tb_abi_version": [],
+    "tb_sizeof_plan": [],
+    "tb_sizeof_stage": [],
+    "tb_sizeof_c4": [],
+}
+
+
+def declare(lib: ctypes.CDLL) -> None:
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_size_t if name.startswith("tb_sizeof") else ctypes.c_int
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise DeviceError(f"{what} failed with hipError_t {rc}")
+
+
+def stream_handle(torch, device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class Kernels:
+    """Launch helpers bound to one device (holds the Unicode tables in HBM)."""
+
+    def __init__(self, torch, device):
+        from .. import native
+
+        self.torch = torch
+        self.device = device
+        self.lib = native.hip()
+        h = native.host()
+        if self.lib.tb_sizeof_plan() != h.SIZEOF_DEV_PLAN or self.lib.tb_sizeof_stage() != h.SIZEOF_DEV_STAGE:
+            raise DeviceError("libtbhip.so and _tbhost disagree on the device plan layout; rebuild")
+        s1, s2, l1, l2 = h.ucd_tables()
+        self.tabs = [torch.from_numpy(a).to(device) for a in (s1, s2, l1, l2)]
+        self._pw = None
+        self._pw_n = 0
+
+    def stream(self) -> int:
+        return self.torch.cuda.current_stream(self.device).cuda_stream
+
+    def pow_table(self, n: int):
+        if n > self._pw_n:
+            cap = max(n, 1 << 16)
+            cap = 1 << (cap - 1).bit_length()
+            self._pw = self.torch.empty(cap + 1, dtype=self.torch.int64, device=self.device)
+            _check(self.lib.tb_pow_table(self.stream(), self._pw.data_ptr(), cap), "tb_pow_table")
+            self._pw_n = cap
+        return self._pw, self._pw_n
+
+    def stage_analyze(self, plan, stage, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, flags,
+                      lid_emb=None, lid_vec=None, lid_cnt=None):
+        t = self.tabs
+        rc = self.lib.tb_stage_analyze(
+            self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs,
+            scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
+            t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), _ptr(lid_emb), _ptr(lid_vec),
+            _ptr(lid_cnt))
+        _check(rc, "tb_stage_analyze")
+
+    def c4_pass_a(self, c4, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags):
+        t = self.tabs
+        rc = self.lib.tb_c4_pass_a(
+            self.stream(), c4.data_ptr(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs, scratch.data_ptr(),
+            scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
+            t[3].data_ptr(), rec.data_ptr(), src.data_ptr(), flags.data_ptr())
+        _check(rc, "tb_c4_pass_a")
+
+    def c4_pass_b(self, bytes_, off, ndocs, scratch, scratch_off, src, new_off, out):
+        rc = self.lib.tb_c4_pass_b(self.stream(), bytes_.data_ptr(), off.data_ptr(), ndocs, scratch.data_ptr(),
+                                   scratch_off.data_ptr(), src.data_ptr(), new_off.data_ptr(), out.data_ptr())
+        _check(rc, "tb_c4_pass_b")
+
+    def langid_head(self, vec, cnt, wT, bias, ndocs, rec, rec_off, width):
+        rc = self.lib.tb_langid_head(self.stream(), vec.data_ptr(), cnt.data_ptr(), wT.data_ptr(), bias.data_ptr(),
+                                     ndocs, rec.data_ptr(), rec_off, width)
+        _check(rc, "tb_langid_head")

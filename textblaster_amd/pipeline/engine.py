@@ -1,0 +1,249 @@
+"""Batched pipeline engine: the in-process replacement of the reference's producer/worker loop
+(reference worker_logic.rs:140-193 + producer_logic.rs:109-196).
+
+One ``Engine`` holds a validated pipeline, its device plan and models. ``process()`` takes one
+batch of documents (packed UTF-8 + optional metadata JSON column) and returns kept / excluded
+outputs with the same per-document semantics as the reference executor: steps in YAML order,
+the first filtering step wins, metadata of every executed step is kept, C4 rewrites content.
+
+Backends:
+  * ``cuda``: record/rewrite steps on the MI355X (HIP kernels), decisions + output assembly in
+    the C++ host runtime; documents flagged by the device (dictionary scripts, hash collisions,
+    scratch overflow) are recomputed on the CPU path with the ICU oracle.
+  * ``cpu``: the C++ CPU path (multithreaded); segmentation by our UAX#29 rules ("rules") or by
+    ICU4C ("icu", the oracle).
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .. import native
+from ..config.pipeline import PipelineConfig
+from ..errors import ConfigError, Unexpected
+from .plan import ExecPlan, build_plan
+
+
+@dataclasses.dataclass
+class OutputPart:
+    rows: np.ndarray          # int64 row indices into the input batch
+    text_data: np.ndarray     # uint8
+    text_off: np.ndarray      # int64 [len(rows)+1]
+    meta_data: np.ndarray     # uint8
+    meta_off: np.ndarray      # int64
+    meta_valid: np.ndarray    # uint8 (0 -> null metadata)
+
+
+@dataclasses.dataclass
+class BatchResult:
+    n_docs: int
+    kept: List[OutputPart]
+    excluded: List[OutputPart]
+    error_rows: np.ndarray
+    fail_step: np.ndarray      # int32 per doc (-1 kept), CPU-delegated docs included
+    status: np.ndarray         # uint8 per doc: 0 kept, 1 filtered, 2 error
+    reasons: Dict[int, str]    # filled only when requested
+    timings: Dict[str, float]
+    n_delegated: int = 0
+
+    @property
+    def n_kept(self) -> int:
+        return int(sum(len(p.rows) for p in self.kept))
+
+    @property
+    def n_excluded(self) -> int:
+        return int(sum(len(p.rows) for p in self.excluded))
+
+
+def default_threads() -> int:
+    env = os.environ.get("TB_THREADS")
+    if env:
+        return max(1, int(env))
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+class Engine:
+    def __init__(self, cfg: PipelineConfig, backend: str = "auto", device: Optional[str] = None,
+                 nthreads: Optional[int] = None, segmentation: str = "rules", langid=None,
+                 tokenizer_dir: Optional[str] = None, badwords_dir: Optional[str] = None,
+                 keep_reasons: bool = False):
+        self.cfg = cfg
+        self.h = native.host()
+        self.plan: ExecPlan = build_plan(cfg)
+        self.steps = [self.h.make_step(s.native_dict()) for s in cfg.pipeline]
+        self.nthreads = nthreads or default_threads()
+        self.segmentation = segmentation
+        self.keep_reasons = keep_reasons
+        if backend == "auto":
+            backend = "cuda" if _cuda_available() else "cpu"
+        self.backend = backend
+        types = [s.type for s in cfg.pipeline]
+        self.langid = None
+        if "LanguageDetectionFilter" in types:
+            from ..models.langid import load_default
+
+            self.langid = langid or load_default()
+        self.lid_native = self.langid.native() if self.langid is not None else None
+        self.tokenizers: Dict[int, object] = {}
+        for i, s in enumerate(cfg.pipeline):
+            if s.type == "TokenCounter":
+                from ..models.tokenizer import load_tokenizer
+
+                self.tokenizers[i] = load_tokenizer(s.params.tokenizer_name, tokenizer_dir)
+        self.badwords = None
+        if "C4BadWordsFilter" in types:
+            bw_dirs = [s.params.cache_base_path for s in cfg.pipeline
+                       if s.type == "C4BadWordsFilter" and s.params.cache_base_path]
+            d = badwords_dir or (bw_dirs[0] if bw_dirs else os.path.join("data", "c4_badwords"))
+            self.badwords = self.h.BadWordsModule(d)
+        self.device_runner = None
+        if backend == "cuda":
+            for st in self.steps:
+                ok, why = self.h.device_supported(st)
+                if not ok:
+                    raise ConfigError(f"step {st.name} cannot run on the device: {why}")
+            from .device import DeviceRunner
+
+            self.device_runner = DeviceRunner(self.steps, self.plan, device or "cuda", self.langid)
+
+    # ------------------------------------------------------------------------------------------
+    def process(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None,
+                row_base: int = 0) -> BatchResult:
+        """Run the pipeline over one batch. ``meta`` = (data uint8, off int64, valid uint8) or None."""
+        t0 = time.perf_counter()
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.int64)
+        ndocs = len(off) - 1
+        md, mo, mv = meta if meta is not None else (None, None, None)
+        bs = self.h.BatchState(data, off, md, mo, mv, self.nthreads)
+        timings: Dict[str, float] = {}
+        delegated = np.zeros(0, dtype=np.int64)
+        if self.backend == "cuda":
+            res = self.device_runner.run(data, off)
+            timings.update(res.timings)
+            t1 = time.perf_counter()
+            delegated = np.nonzero(res.flags)[0].astype(np.int64)
+            if len(delegated):
+                bs.delegate(delegated)
+            vid = {0: 0}
+            for v in sorted(res.versions):
+                vd, vo = res.versions[v]
+                vid[v] = bs.add_version(np.ascontiguousarray(vd), np.ascontiguousarray(vo))
+            for sp in self.plan.steps:
+                st = self.steps[sp.index]
+                if sp.stage >= 0:
+                    width_total, layout = self.device_runner.stage_layout[sp.stage]
+                    pos = self.plan.stages[sp.stage].index(sp.index)
+                    _, width, prefix = layout[pos]
+                    rec = res.stage_recs[sp.stage][prefix * ndocs:(prefix + width) * ndocs]
+                    bs.apply_records(st, sp.index, np.ascontiguousarray(rec), -1)
+                elif sp.c4_pass >= 0:
+                    bs.apply_records(st, sp.index, res.c4_recs[sp.index], vid[sp.version_out])
+                else:
+                    self._host_step(bs, sp.index, ndocs)
+            timings["resolve"] = time.perf_counter() - t1
+        else:
+            t1 = time.perf_counter()
+            self._run_cpu_steps(bs, 0, len(self.steps), ndocs, self.segmentation)
+            timings["cpu_pipeline"] = time.perf_counter() - t1
+        t2 = time.perf_counter()
+        result = self._collect(bs, ndocs, timings)
+        if len(delegated):
+            sub = self._process_subset_cpu(data, off, meta, delegated)
+            result.kept += sub.kept
+            result.excluded += sub.excluded
+            result.error_rows = np.concatenate([result.error_rows, sub.error_rows])
+            result.fail_step[delegated] = sub.fail_step
+            result.status[delegated] = sub.status
+            result.reasons.update(sub.reasons)
+            result.n_delegated = len(delegated)
+        timings["assemble"] = time.perf_counter() - t2
+        timings["total"] = time.perf_counter() - t0
+        if row_base:
+            for p in result.kept + result.excluded:
+                p.rows = p.rows + row_base
+        return result
+
+    def _run_cpu_steps(self, bs, begin: int, end: int, ndocs: int, seg: str) -> None:
+        a = begin
+        for i in range(begin, end):
+            if self.cfg.pipeline[i].type == "TokenCounter":
+                if i > a:
+                    bs.run_cpu(self.steps, a, i, seg, self.lid_native, self.badwords)
+                self._host_step(bs, i, ndocs)
+                a = i + 1
+        if end > a:
+            bs.run_cpu(self.steps, a, end, seg, self.lid_native, self.badwords)
+
+    def _host_step(self, bs, i: int, ndocs: int) -> None:
+        st = self.steps[i]
+        t = self.cfg.pipeline[i].type
+        if t == "TokenCounter":
+            alive = bs.alive_indices()
+            rec = np.full(ndocs, -1, dtype=np.int64)
+            if len(alive):
+                texts = bs.contents(alive)
+                rec[alive] = self.tokenizers[i].count(texts)
+            bs.apply_records(st, i, rec, -1)
+        elif t == "C4BadWordsFilter":
+            bs.apply_badwords(st, i, self.badwords)
+        else:
+            raise Unexpected(f"{t} is not a host step")
+
+    def _process_subset_cpu(self, data, off, meta, rows: np.ndarray) -> BatchResult:
+        lens = off[rows + 1] - off[rows]
+        sub_off = np.zeros(len(rows) + 1, dtype=np.int64)
+        np.cumsum(lens, out=sub_off[1:])
+        sub_data = np.concatenate([data[off[r]:off[r + 1]] for r in rows]) if len(rows) else np.zeros(0, np.uint8)
+        sub_meta = None
+        if meta is not None and meta[0] is not None:
+            md, mo, mv = meta
+            ml = mo[rows + 1] - mo[rows]
+            smo = np.zeros(len(rows) + 1, dtype=np.int64)
+            np.cumsum(ml, out=smo[1:])
+            smd = np.concatenate([md[mo[r]:mo[r + 1]] for r in rows]) if len(rows) else np.zeros(0, np.uint8)
+            smv = mv[rows] if mv is not None else None
+            sub_meta = (np.ascontiguousarray(smd, dtype=np.uint8), smo, smv)
+        md2, mo2, mv2 = sub_meta if sub_meta else (None, None, None)
+        bs = self.h.BatchState(np.ascontiguousarray(sub_data, dtype=np.uint8), sub_off, md2, mo2, mv2, self.nthreads)
+        self._run_cpu_steps(bs, 0, len(self.steps), len(rows), "icu")
+        res = self._collect(bs, len(rows), {})
+        for p in res.kept + res.excluded:
+            p.rows = rows[p.rows]
+        res.error_rows = rows[res.error_rows]
+        res.reasons = {int(rows[k]): v for k, v in res.reasons.items()}
+        return res
+
+    def _collect(self, bs, ndocs: int, timings) -> BatchResult:
+        status = bs.status()
+        fail = bs.fail_step()
+        kept_rows = np.nonzero(status == 0)[0].astype(np.int64)
+        excl_rows = np.nonzero(status == 1)[0].astype(np.int64)
+        err_rows = np.nonzero(status == 2)[0].astype(np.int64)
+        parts = []
+        for rows in (kept_rows, excl_rows):
+            td, to, md, mo, mv = bs.assemble(rows)
+            parts.append(OutputPart(rows, td, to, md, mo, mv))
+        reasons = {}
+        if self.keep_reasons and len(excl_rows):
+            reasons = dict(zip(excl_rows.tolist(), bs.reasons(excl_rows)))
+        return BatchResult(ndocs, [parts[0]], [parts[1]], err_rows, fail, status, reasons, timings)
+
+    def step_names(self) -> List[str]:
+        return [s.type for s in self.cfg.pipeline]
+
+
+def _cuda_available() -> bool:
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:
+        return False

@@ -1,0 +1,100 @@
+"""Train the language-id weights (textblaster_amd/models/data/langid_v1.npz).
+
+Training text: the hand-written sentences in models/data/langid_corpus/<lang>.txt plus random
+word sequences from the synthetic-corpus vocabularies. Features come from the native featurizer
+(_tbhost.langid_buckets), so training and inference hash identically. Label smoothing keeps the
+confidence of short texts below ~0.93, like lingua's relative confidences.
+
+    python tools/train_langid.py [--epochs 30] [--out path]
+"""
+import argparse
+import os
+import random
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from textblaster_amd import native  # noqa: E402
+from textblaster_amd.models.langid import DATA_DIR, LANGS  # noqa: E402
+from textblaster_amd.utils.synth import VOCAB  # noqa: E402
+
+
+def bf16_bits(a: np.ndarray) -> np.ndarray:
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(torch.bfloat16)
+    return t.view(torch.int16).numpy().view(np.uint16)
+
+
+def samples(rng: random.Random, n_per_lang: int):
+    out = []
+    for li, lang in enumerate(LANGS):
+        sents = [s.strip() for s in open(os.path.join(DATA_DIR, "langid_corpus", f"{lang}.txt"), encoding="utf-8")
+                 if s.strip()]
+        vocab = VOCAB[lang]
+        for _ in range(n_per_lang):
+            r = rng.random()
+            if r < 0.45:
+                k = rng.randint(1, 4)
+                i = rng.randint(0, len(sents) - 1)
+                text = " ".join(sents[i:i + k])
+            elif r < 0.7:
+                s = rng.choice(sents).split()
+                a = rng.randint(0, max(0, len(s) - 2))
+                text = " ".join(s[a:a + rng.randint(2, 8)])
+            else:
+                text = " ".join(rng.choice(vocab) for _ in range(rng.randint(3, 40)))
+            if rng.random() < 0.1:
+                text = text.upper()
+            out.append((text, li))
+    rng.shuffle(out)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epochs", type=int, default=12)
+    ap.add_argument("--n", type=int, default=6000)
+    ap.add_argument("--out", default=os.path.join(DATA_DIR, "langid_v1.npz"))
+    args = ap.parse_args()
+    h = native.host()
+    rng = random.Random(1234)
+    torch.manual_seed(1234)
+    train = samples(rng, args.n)
+    feats = [np.asarray(h.langid_buckets(t), dtype=np.int64) for t, _ in train]
+    keep = [i for i, f in enumerate(feats) if len(f)]
+    feats = [feats[i] for i in keep]
+    labels = torch.tensor([train[i][1] for i in keep])
+    emb = torch.nn.EmbeddingBag(h.LID_BUCKETS, h.LID_DIM, mode="mean")
+    torch.nn.init.normal_(emb.weight, std=0.05)
+    head = torch.nn.Linear(h.LID_DIM, len(LANGS))
+    opt = torch.optim.Adam(list(emb.parameters()) + list(head.parameters()), lr=0.01)
+    lossf = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
+    bs = 256
+    for ep in range(args.epochs):
+        order = torch.randperm(len(feats))
+        tot = 0.0
+        for k in range(0, len(order), bs):
+            idx = order[k:k + bs].tolist()
+            flat = torch.from_numpy(np.concatenate([feats[i] for i in idx]))
+            offs = torch.tensor([0] + list(np.cumsum([len(feats[i]) for i in idx])[:-1]))
+            logits = head(emb(flat, offs))
+            loss = lossf(logits, labels[idx])
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            with torch.no_grad():
+                emb.weight.clamp_(-4.0, 4.0)
+            tot += loss.item() * len(idx)
+        print(f"epoch {ep} loss {tot / len(feats):.4f}", flush=True)
+    E = emb.weight.detach().numpy()
+    W = np.zeros((h.LID_DIM, h.LID_LANGS_PAD), dtype=np.float32)
+    W[:, :len(LANGS)] = head.weight.detach().numpy().T
+    b = np.zeros(h.LID_LANGS_PAD, dtype=np.float32)
+    b[:len(LANGS)] = head.bias.detach().numpy()
+    np.savez(args.out, emb=bf16_bits(E).reshape(-1), w=bf16_bits(W).reshape(-1), b=b)
+    print("saved", args.out, os.path.getsize(args.out))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,133 @@
+"""Headline benchmark: documents/sec through the full language-ID + Gopher + C4 (+FineWeb)
+pipeline (BASELINE.json metric) on N MI355X GPUs of one node, one process per GPU.
+
+    python bench.py --gpus N --steps K --warmup W
+    (N > 1 is launched by torch.distributed.run; ranks read RANK/LOCAL_RANK/WORLD_SIZE)
+
+One step = every rank pushes one batch of synthetic CommonCrawl-shaped documents (log-normal
+lengths around 1 KB, 5 languages) through the whole pipeline: H2D staging, all device stages
+(analysis kernels, C4 rewrite passes, bf16 MFMA language-id head), D2H, per-document
+first-failure resolution with reason/metadata formatting, and assembly of the kept/excluded
+text + metadata JSON columns. Parquet decode/encode is not in the timed step (the reference's
+worker docs/sec excludes it too). Weak scaling: per-GPU batch fixed as N grows; RCCL all-reduces
+the per-step document counters (the only cross-GPU traffic).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "documents/sec through full C4+Gopher+langID pipeline at 1/2/4/8 MI355X"
+# CPU baseline: this framework's CPU path (C++ with ICU4C segmentation, all cores of the box's
+# CPU share) on the same corpus, measured with `python bench.py --backend cpu`.
+CPU_BASELINE_DOCS_PER_SEC = float(os.environ.get("TB_CPU_BASELINE", "0") or 0) or None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--docs-per-step", type=int, default=65536)
+    ap.add_argument("--mean-bytes", type=int, default=1024)
+    ap.add_argument("--pool", type=int, default=16384, help="distinct synthetic docs per rank")
+    ap.add_argument("--config", default=os.path.join(ROOT, "config", "bench_pipeline.yaml"))
+    ap.add_argument("--backend", default="cuda", choices=["cuda", "cpu"])
+    ap.add_argument("--segmentation", default="icu", help="CPU backend segmentation (icu|rules)")
+    ap.add_argument("--threads", type=int, default=None)
+    args = ap.parse_args()
+
+    import torch
+
+    from textblaster_amd.config import load_pipeline_config
+    from textblaster_amd.parallel import dist
+    from textblaster_amd.pipeline.engine import Engine
+    from textblaster_amd.utils import synth
+
+    ctx = dist.init_from_env(backend="nccl" if args.backend == "cuda" else "gloo")
+    rank, world = ctx.rank, ctx.world_size
+    device = f"cuda:{ctx.local_rank}" if args.backend == "cuda" else None
+    cfg = load_pipeline_config(args.config)
+    eng = Engine(cfg, backend=args.backend, device=device, nthreads=args.threads, segmentation=args.segmentation)
+
+    # synthetic corpus: a pool of distinct docs per rank, batches are fresh permutations of it
+    texts = synth.make_corpus(args.pool, args.mean_bytes, seed=1000 + rank)
+    enc = [t.encode("utf-8") for t in texts]
+    rng = np.random.default_rng(rank)
+
+    def make_batch():
+        idx = rng.integers(0, len(enc), size=args.docs_per_step)
+        parts = [enc[i] for i in idx]
+        off = np.zeros(len(parts) + 1, dtype=np.int64)
+        np.cumsum([len(p) for p in parts], out=off[1:])
+        return np.frombuffer(b"".join(parts), dtype=np.uint8).copy(), off
+
+    batches = [make_batch() for _ in range(min(4, args.steps + args.warmup))]
+    bytes_per_step = float(np.mean([len(b[0]) for b in batches]))
+    counters = np.zeros(4, dtype=np.int64)  # docs, kept, excluded, errors
+
+    def step(i):
+        data, off = batches[i % len(batches)]
+        res = eng.process(data, off)
+        return res
+
+    for i in range(args.warmup):
+        step(i)
+    ctx.barrier()
+    if args.backend == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        res = step(i)
+        counters += [res.n_docs, res.n_kept, res.n_excluded, len(res.error_rows)]
+    if args.backend == "cuda":
+        torch.cuda.synchronize()
+    ctx.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed_max = ctx.all_reduce_max(elapsed)
+    totals = ctx.all_reduce_sum(counters)
+    docs_total = int(totals[0])
+    value = docs_total / elapsed_max
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "docs/s",
+            "n_gpus": world if args.backend == "cuda" else 0,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * elapsed_max / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / CPU_BASELINE_DOCS_PER_SEC, 3) if CPU_BASELINE_DOCS_PER_SEC else None,
+            "dtype": "bf16",
+            "data": f"synthetic CommonCrawl-shaped docs (log-normal ~{args.mean_bytes} B, 5 languages), "
+                    f"{args.docs_per_step} docs/GPU/step",
+            "config": {
+                "model": "LanguageDetection(fastText bf16 MFMA head)+GopherRepetition+GopherQuality+C4Quality+FineWeb",
+                "global_batch": args.docs_per_step * world,
+                "seq_len": int(bytes_per_step / args.docs_per_step),
+                "parallelism": f"dp{world}",
+                "backend": args.backend,
+                "pipeline_config": os.path.relpath(args.config, ROOT),
+            },
+            "kept": int(totals[1]),
+            "excluded": int(totals[2]),
+            "errors": int(totals[3]),
+            "bytes_per_sec": round(bytes_per_step * world * args.steps / elapsed_max, 1),
+            "last_step_timings": {k: round(v, 5) for k, v in res.timings.items()},
+        }
+        print(json.dumps(line), flush=True)
+    ctx.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -69,8 +69,17 @@ class DeviceRunner:
         return self._scratch
 
     def _h2d(self, arr: np.ndarray):
-        t = self.torch.from_numpy(arr)
-        return t.to(self.device, non_blocking=False)
+        # staged through a pinned host buffer so the copy is a DMA (and numpy read-only views
+        # of Arrow buffers are never handed to torch directly)
+        arr = np.ascontiguousarray(arr)
+        nb = arr.nbytes
+        if self._pinned is None or self._pinned.numel() < nb:
+            self._pinned = self.torch.empty(max(nb, 1 << 20) * 2, dtype=self.torch.uint8, pin_memory=True)
+        host = self._pinned[:nb]
+        host.numpy()[:] = arr.view(np.uint8).reshape(-1)
+        dev = self.torch.empty(nb, dtype=self.torch.uint8, device=self.device)
+        dev.copy_(host, non_blocking=False)
+        return dev.view(self.torch.from_numpy(arr[:0]).dtype) if nb else dev
 
     def run(self, data: np.ndarray, off: np.ndarray) -> DeviceResult:
         import time

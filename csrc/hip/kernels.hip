@@ -103,20 +103,24 @@ __global__ __launch_bounds__(64) void k_langid_head(const uint16_t* __restrict__
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw, acc, 0, 0, 0);
   const int col = lane & 15;
   const float bcol = bias[col];
-#pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = row0 + 4 * (lane >> 4) + i;
     const bool valid = col < kLidLangs;
-    float v = valid ? acc[i] + bcol : -3.0e38f;
-    // arg-max over the 16 lanes of this row group (ties -> lowest column)
-    float bv = v;
-    int bc = col;
+    const float v = acc[i] + bcol;
+    // arg-max over the 16 lanes of this row group as ONE integer max-reduction of an
+    // order-preserving key: (float ordering bits << 8) | (15 - col)  -> ties pick the lowest col
+    uint32_t fb = __float_as_uint(v);
+    fb = (fb & 0x80000000u) ? ~fb : (fb | 0x80000000u);
+    uint64_t key = valid ? (((uint64_t)fb << 8) | (uint64_t)(15 - col)) : 0ull;
     for (int o = 1; o < 16; o <<= 1) {
-      float ov = __shfl_xor(bv, o);
-      int oc = __shfl_xor(bc, o);
-      if (ov > bv || (ov == bv && oc < bc)) { bv = ov; bc = oc; }
+      const uint64_t ok = __shfl_xor(key, o);
+      key = ok > key ? ok : key;
     }
-    double e = valid ? exp((double)v - (double)bv) : 0.0;
+    const int best = 15 - (int)(key & 0xFF);
+    uint32_t mb = (uint32_t)(key >> 8);
+    mb = (mb & 0x80000000u) ? (mb & 0x7FFFFFFFu) : ~mb;
+    const float vmax = __uint_as_float(mb);
+    double e = valid ? exp((double)v - (double)vmax) : 0.0;
     for (int o = 1; o < 16; o <<= 1) e += __shfl_xor(e, o);
     if (col == 0 && row < ndocs) {
       int64_t* rr = rec + rec_off + (int64_t)row * width;
@@ -125,7 +129,7 @@ __global__ __launch_bounds__(64) void k_langid_head(const uint16_t* __restrict__
         rr[1] = 0;
       } else {
         const double conf = 1.0 / e;
-        rr[0] = bc;
+        rr[0] = best;
         rr[1] = __double_as_longlong(conf);
       }
       rr[2] = 0;

@@ -104,8 +104,8 @@ def build_hip(verbose: bool = False, force: bool = False) -> str:
             and os.path.getmtime(HIP_LIB) >= _newest(srcs + hdrs)):
         return HIP_LIB
     os.makedirs(os.path.join(BUILD_DIR, "hip"), exist_ok=True)
-    flags = [f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffast-math",
-             "-fno-gpu-rdc", "-munsafe-fp-atomics"]
+    # no -ffast-math: the fixed-point -> f32 -> bf16 conversions must match the host bit for bit
+    flags = [f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-fPIC", "-fno-gpu-rdc"]
     objs = []
 
     def compile_one(src: str) -> str:

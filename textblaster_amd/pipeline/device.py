@@ -20,6 +20,16 @@ from .plan import ExecPlan
 SCRATCH_ALIGN = 256
 
 
+def _torch_dtypes():
+    import torch
+
+    return {np.dtype(np.uint8).str: torch.uint8, np.dtype(np.int32).str: torch.int32,
+            np.dtype(np.int64).str: torch.int64, np.dtype(np.uint16).str: torch.int16}
+
+
+_TORCH_DTYPES = _torch_dtypes() if __import__('importlib').util.find_spec('torch') else {}
+
+
 @dataclasses.dataclass
 class DeviceResult:
     stage_recs: List[np.ndarray]            # per stage: int64 [width_total * ndocs]
@@ -79,7 +89,7 @@ class DeviceRunner:
         host.numpy()[:] = arr.view(np.uint8).reshape(-1)
         dev = self.torch.empty(nb, dtype=self.torch.uint8, device=self.device)
         dev.copy_(host, non_blocking=False)
-        return dev.view(self.torch.from_numpy(arr[:0]).dtype) if nb else dev
+        return dev.view(_TORCH_DTYPES[arr.dtype.str]) if nb else dev
 
     def run(self, data: np.ndarray, off: np.ndarray) -> DeviceResult:
         import time

@@ -60,9 +60,12 @@ class BatchResult:
 
 
 def default_threads() -> int:
-    env = os.environ.get("TB_THREADS")
-    if env:
-        return max(1, int(env))
+    # the GPU boxes expose every CPU of the host through the affinity mask but give one GPU a
+    # share of them (OMP_NUM_THREADS); honour explicit limits first
+    for var in ("TB_THREADS", "OMP_NUM_THREADS"):
+        env = os.environ.get(var)
+        if env and env.isdigit() and int(env) > 0:
+            return int(env)
     try:
         return max(1, len(os.sched_getaffinity(0)))
     except AttributeError:

@@ -88,7 +88,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // the transposed weights wT[col][k]; D: col = l&15, row = 4(l>>4) + i.
 __global__ __launch_bounds__(64) void k_langid_head(const uint16_t* __restrict__ vec, const int32_t* __restrict__ cnt,
                                                     const uint16_t* __restrict__ wT, const float* __restrict__ bias,
-                                                    int32_t ndocs, int64_t* rec, int64_t rec_off, int32_t width) {
+                                                    int32_t ndocs, int64_t* rec, int64_t rec_off, int32_t width,
+                                                    float* dbg_logits) {
   const int lane = threadIdx.x;
   const int row0 = blockIdx.x * 16;
   const int r = row0 + (lane & 15);
@@ -107,6 +108,7 @@ __global__ __launch_bounds__(64) void k_langid_head(const uint16_t* __restrict__
     const int row = row0 + 4 * (lane >> 4) + i;
     const bool valid = col < kLidLangs;
     const float v = acc[i] + bcol;
+    if (dbg_logits && row < ndocs) dbg_logits[(size_t)row * 16 + col] = v;
     // arg-max over the 16 lanes of this row group as ONE integer max-reduction of an
     // order-preserving key: (float ordering bits << 8) | (15 - col)  -> ties pick the lowest col
     uint32_t fb = __float_as_uint(v);
@@ -180,10 +182,11 @@ int tb_c4_pass_b(hipStream_t stream, const uint8_t* bytes, const int64_t* off, i
 }
 
 int tb_langid_head(hipStream_t stream, const uint16_t* vec, const int32_t* cnt, const uint16_t* wT,
-                   const float* bias, int32_t ndocs, int64_t* rec, int64_t rec_off, int32_t width) {
+                   const float* bias, int32_t ndocs, int64_t* rec, int64_t rec_off, int32_t width,
+                   float* dbg_logits) {
   if (ndocs <= 0) return 0;
   hipLaunchKernelGGL(k_langid_head, dim3((ndocs + 15) / 16), dim3(64), 0, stream, vec, cnt, wT, bias, ndocs, rec,
-                     rec_off, width);
+                     rec_off, width, dbg_logits);
   return (int)hipGetLastError();
 }
 

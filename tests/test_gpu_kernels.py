@@ -50,7 +50,7 @@ def test_device_records_match_host_emulation(host, corpus, runner_parts):
                                          lid.native())
         got = res.stage_recs[s]
         width_total, layout = runner.stage_layout[s]
-        for (kind, width, prefix), step_i in zip(layout, idx):
+        for (kind, width, prefix), step_i in sorted(zip(layout, idx), key=lambda t: t[0][0] == 4):
             a = got[prefix * n:(prefix + width) * n].reshape(n, width)
             b = ref[prefix * n:(prefix + width) * n].reshape(n, width)
             ok = (res.flags == 0) & (rflags == 0)
@@ -85,3 +85,29 @@ def test_dictionary_scripts_are_flagged(host, runner_parts):
     data, off = synth.pack(["日本語のテキストです。", "plain english text here."])
     res = runner.run(data, off)
     assert res.flags[0] != 0 and res.flags[1] == 0
+
+
+def test_langid_head_mfma_matches_numpy(host, runner_parts):
+    """The bf16 MFMA head on known inputs vs. an fp64 numpy reference (isolates the head)."""
+    import torch
+
+    _, _, _, runner, lid = runner_parts
+    rng = np.random.default_rng(0)
+    n = 200
+    vec = torch.from_numpy(rng.normal(0, 0.5, size=(n, 32)).astype(np.float32)).to(torch.bfloat16)
+    w = lid.w.copy().view(np.uint16).reshape(32, 16)
+    wf = torch.from_numpy(w.view(np.int16)).view(torch.bfloat16).float().numpy()
+    logits_ref = vec.float().numpy() @ wf + lid.b
+    dev = runner.device
+    vec_d = vec.view(torch.int16).reshape(-1).to(dev)
+    cnt_d = torch.ones(n, dtype=torch.int32, device=dev)
+    rec = torch.zeros(3 * n, dtype=torch.int64, device=dev)
+    dbg = torch.zeros(n * 16, dtype=torch.float32, device=dev)
+    runner.k.langid_head(vec_d, cnt_d, runner.lid_wT, runner.lid_b, n, rec, 0, 3, dbg)
+    torch.cuda.synchronize()
+    got_logits = dbg.cpu().numpy().reshape(n, 16)[:, :5]
+    assert np.allclose(got_logits, logits_ref[:, :5], atol=1e-4), np.abs(got_logits - logits_ref[:, :5]).max()
+    r = rec.cpu().numpy().reshape(n, 3)
+    best_ref = logits_ref[:, :5].argmax(1)
+    print("head argmax mismatches", np.nonzero(r[:, 0] != best_ref)[0][:20])
+    assert np.array_equal(r[:, 0], best_ref)

@@ -20,7 +20,7 @@ _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P],
     "tb_c4_pass_b": [_P, _P, _P, _I32, _P, _P, _P, _P, _P],
-    "tb_langid_head": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I32],
+    "tb_langid_head": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I32, _P],
     "tb_pow_table": [_P, _P, _U32],
     "tb_abi_version": [],
     "tb_sizeof_plan": [],
@@ -101,7 +101,7 @@ class Kernels:
                                    scratch_off.data_ptr(), src.data_ptr(), new_off.data_ptr(), out.data_ptr())
         _check(rc, "tb_c4_pass_b")
 
-    def langid_head(self, vec, cnt, wT, bias, ndocs, rec, rec_off, width):
+    def langid_head(self, vec, cnt, wT, bias, ndocs, rec, rec_off, width, dbg_logits=None):
         rc = self.lib.tb_langid_head(self.stream(), vec.data_ptr(), cnt.data_ptr(), wT.data_ptr(), bias.data_ptr(),
-                                     ndocs, rec.data_ptr(), rec_off, width)
+                                     ndocs, rec.data_ptr(), rec_off, width, _ptr(dbg_logits))
         _check(rc, "tb_langid_head")

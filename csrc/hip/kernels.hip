@@ -102,37 +102,36 @@ __global__ __launch_bounds__(64) void k_langid_head(const uint16_t* __restrict__
   const bf16x8 bw = *reinterpret_cast<const bf16x8*>(wT + (size_t)(lane & 15) * kLidDim + 8 * (lane >> 4));
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw, acc, 0, 0, 0);
+  // Epilogue: the 16x16 logits tile goes through LDS; one lane per document then does the
+  // arg-max (ties -> lowest index, as the host) and the softmax in f64.
+  __shared__ float tile[16][17];
   const int col = lane & 15;
   const float bcol = bias[col];
-  for (int i = 0; i < 4; ++i) {
-    const int row = row0 + 4 * (lane >> 4) + i;
-    const bool valid = col < kLidLangs;
-    const float v = acc[i] + bcol;
-    if (dbg_logits && row < ndocs) dbg_logits[(size_t)row * 16 + col] = v;
-    // arg-max over the 16 lanes of this row group as ONE integer max-reduction of an
-    // order-preserving key: (float ordering bits << 8) | (15 - col)  -> ties pick the lowest col
-    uint32_t fb = __float_as_uint(v);
-    fb = (fb & 0x80000000u) ? ~fb : (fb | 0x80000000u);
-    uint64_t key = valid ? (((uint64_t)fb << 8) | (uint64_t)(15 - col)) : 0ull;
-    for (int o = 1; o < 16; o <<= 1) {
-      const uint64_t ok = __shfl_xor(key, o);
-      key = ok > key ? ok : key;
-    }
-    const int best = 15 - (int)(key & 0xFF);
-    uint32_t mb = (uint32_t)(key >> 8);
-    mb = (mb & 0x80000000u) ? (mb & 0x7FFFFFFFu) : ~mb;
-    const float vmax = __uint_as_float(mb);
-    double e = valid ? exp((double)v - (double)vmax) : 0.0;
-    for (int o = 1; o < 16; o <<= 1) e += __shfl_xor(e, o);
-    if (col == 0 && row < ndocs) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) tile[4 * (lane >> 4) + i][col] = acc[i] + bcol;
+  __syncthreads();
+  if (lane < 16) {
+    const int row = row0 + lane;
+    if (row < ndocs) {
+      float v[kLidLangs];
+      int best = 0;
+#pragma unroll
+      for (int l = 0; l < kLidLangs; ++l) {
+        v[l] = tile[lane][l];
+        if (l > 0 && v[l] > v[best]) best = l;
+      }
+      if (dbg_logits)
+        for (int l = 0; l < 16; ++l) dbg_logits[(size_t)row * 16 + l] = tile[lane][l];
+      double den = 0.0;
+#pragma unroll
+      for (int l = 0; l < kLidLangs; ++l) den += exp((double)v[l] - (double)v[best]);
       int64_t* rr = rec + rec_off + (int64_t)row * width;
       if (cnt[row] == 0) {
         rr[0] = -1;
         rr[1] = 0;
       } else {
-        const double conf = 1.0 / e;
         rr[0] = best;
-        rr[1] = __double_as_longlong(conf);
+        rr[1] = __double_as_longlong(1.0 / den);
       }
       rr[2] = 0;
     }

@@ -111,3 +111,42 @@ def test_langid_head_mfma_matches_numpy(host, runner_parts):
     best_ref = logits_ref[:, :5].argmax(1)
     print("head argmax mismatches", np.nonzero(r[:, 0] != best_ref)[0][:20])
     assert np.array_equal(r[:, 0], best_ref)
+
+
+def test_langid_pipeline_vectors_and_head(host, corpus, runner_parts):
+    """Doc vectors from the analysis kernel are bit-exact vs. the host featurizer, and the head
+    applied to them gives the host's language."""
+    import torch
+
+    _, _, _, runner, lid = runner_parts
+    texts = corpus[:512]
+    data, off = synth.pack(texts)
+    res = runner.run(data, off)
+    vec_d, cnt_d = runner._last_lid
+    n = len(texts)
+    vec = vec_d.cpu().numpy().view(np.uint16).reshape(n, 32)
+    cnt = cnt_d.cpu().numpy()
+    m = lid.native()
+    bad_vec = []
+    for i, t in enumerate(texts):
+        c, v = m.featurize(t)
+        if c != cnt[i] or (c and list(v) != list(vec[i])):
+            bad_vec.append(i)
+    print("vector mismatches", len(bad_vec), bad_vec[:10])
+    rec2 = torch.zeros(3 * n, dtype=torch.int64, device=runner.device)
+    dbg = torch.zeros(16 * n, dtype=torch.float32, device=runner.device)
+    runner.k.langid_head(vec_d, cnt_d, runner.lid_wT, runner.lid_b, n, rec2, 0, 3, dbg)
+    rec3 = torch.zeros(3 * n, dtype=torch.int64, device=runner.device)
+    runner.k.langid_head(vec_d, cnt_d, runner.lid_wT, runner.lid_b, n, rec3, 0, 3, None)
+    torch.cuda.synchronize()
+    r1 = res.stage_recs[0][:3 * n].reshape(n, 3)
+    r2 = rec2.cpu().numpy().reshape(n, 3)
+    r3 = rec3.cpu().numpy().reshape(n, 3)
+    lg = dbg.cpu().numpy().reshape(n, 16)[:, :5]
+    cpu = np.array([m.detect(t)[0] for t in texts])
+    print("pipeline lang", r1[:12, 0], "\nhead+dbg", r2[:12, 0], "\nhead nodbg", r3[:12, 0],
+          "\nlogit argmax", lg[:12].argmax(1), "\ncpu", cpu[:12])
+    assert not bad_vec
+    assert np.array_equal(r2[:, 0], cpu)
+    assert np.array_equal(r3[:, 0], cpu)
+    assert np.array_equal(r1[:, 0], cpu)

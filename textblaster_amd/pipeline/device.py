@@ -66,6 +66,7 @@ class DeviceRunner:
             self.lid_b = torch.from_numpy(langid.b.astype(np.float32)).to(self.device)
         self._scratch = None
         self._pinned = None
+        self._last_lid = None
 
     def _to_dev(self, b: bytes):
         t = self.torch.frombuffer(bytearray(b), dtype=self.torch.uint8)
@@ -129,6 +130,7 @@ class DeviceRunner:
                     lid_cnt = torch.zeros(ndocs, dtype=torch.int32, device=self.device)
                 self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm, ndocs, scratch, d_soff, pw, pw_n,
                                      rec, flags, self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt)
+                self._last_lid = (lid_vec, lid_cnt)
                 for kind, width, prefix in layout:
                     if kind == 4:
                         self.k.langid_head(lid_vec, lid_cnt, self.lid_wT, self.lid_b, ndocs, rec, prefix * ndocs, width)

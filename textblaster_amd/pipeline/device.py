@@ -130,7 +130,8 @@ class DeviceRunner:
                     lid_cnt = torch.zeros(ndocs, dtype=torch.int32, device=self.device)
                 self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm, ndocs, scratch, d_soff, pw, pw_n,
                                      rec, flags, self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt)
-                self._last_lid = (lid_vec, lid_cnt)
+                if lid_vec is not None:
+                    self._last_lid = (lid_vec, lid_cnt)
                 for kind, width, prefix in layout:
                     if kind == 4:
                         self.k.langid_head(lid_vec, lid_cnt, self.lid_wT, self.lid_b, ndocs, rec, prefix * ndocs, width)

@@ -133,7 +133,6 @@ __global__ __launch_bounds__(64) void k_langid_head(const uint16_t* __restrict__
         rr[0] = best;
         rr[1] = __double_as_longlong(1.0 / den);
       }
-      rr[2] = 0;
     }
   }
 }

@@ -126,7 +126,7 @@ uint64_t scratch_bytes_for(uint32_t doc_len) { return (uint64_t)kScratchPerByte 
 
 // Head of the language model on one doc vector (host arithmetic; the device uses MFMA).
 static void lid_head_host(const LangidModel& m, const uint16_t* v, int32_t cnt, int64_t* r) {
-  if (cnt == 0) { r[0] = -1; r[1] = 0; r[2] = 0; return; }
+  if (cnt == 0) { r[0] = -1; r[1] = 0; return; }
   float logits[kLidLangs];
   for (int l = 0; l < kLidLangs; ++l) {
     float s = 0.f;
@@ -140,7 +140,6 @@ static void lid_head_host(const LangidModel& m, const uint16_t* v, int32_t cnt, 
   double conf = 1.0 / den;
   r[0] = best;
   std::memcpy(&r[1], &conf, sizeof(double));
-  r[2] = 0;
 }
 
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,

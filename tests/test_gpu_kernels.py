@@ -101,13 +101,13 @@ def test_langid_head_mfma_matches_numpy(host, runner_parts):
     dev = runner.device
     vec_d = vec.view(torch.int16).reshape(-1).to(dev)
     cnt_d = torch.ones(n, dtype=torch.int32, device=dev)
-    rec = torch.zeros(3 * n, dtype=torch.int64, device=dev)
+    rec = torch.zeros(2 * n, dtype=torch.int64, device=dev)
     dbg = torch.zeros(n * 16, dtype=torch.float32, device=dev)
-    runner.k.langid_head(vec_d, cnt_d, runner.lid_wT, runner.lid_b, n, rec, 0, 3, dbg)
+    runner.k.langid_head(vec_d, cnt_d, runner.lid_wT, runner.lid_b, n, rec, 0, 2, dbg)
     torch.cuda.synchronize()
     got_logits = dbg.cpu().numpy().reshape(n, 16)[:, :5]
     assert np.allclose(got_logits, logits_ref[:, :5], atol=1e-4), np.abs(got_logits - logits_ref[:, :5]).max()
-    r = rec.cpu().numpy().reshape(n, 3)
+    r = rec.cpu().numpy().reshape(n, 2)
     best_ref = logits_ref[:, :5].argmax(1)
     print("head argmax mismatches", np.nonzero(r[:, 0] != best_ref)[0][:20])
     assert np.array_equal(r[:, 0], best_ref)
@@ -133,15 +133,17 @@ def test_langid_pipeline_vectors_and_head(host, corpus, runner_parts):
         if c != cnt[i] or (c and list(v) != list(vec[i])):
             bad_vec.append(i)
     print("vector mismatches", len(bad_vec), bad_vec[:10])
-    rec2 = torch.zeros(3 * n, dtype=torch.int64, device=runner.device)
+    rec2 = torch.zeros(2 * n, dtype=torch.int64, device=runner.device)
     dbg = torch.zeros(16 * n, dtype=torch.float32, device=runner.device)
-    runner.k.langid_head(vec_d, cnt_d, runner.lid_wT, runner.lid_b, n, rec2, 0, 3, dbg)
-    rec3 = torch.zeros(3 * n, dtype=torch.int64, device=runner.device)
-    runner.k.langid_head(vec_d, cnt_d, runner.lid_wT, runner.lid_b, n, rec3, 0, 3, None)
+    runner.k.langid_head(vec_d, cnt_d, runner.lid_wT, runner.lid_b, n, rec2, 0, 2, dbg)
+    rec3 = torch.zeros(2 * n, dtype=torch.int64, device=runner.device)
+    runner.k.langid_head(vec_d, cnt_d, runner.lid_wT, runner.lid_b, n, rec3, 0, 2, None)
     torch.cuda.synchronize()
-    r1 = res.stage_recs[0][:3 * n].reshape(n, 3)
-    r2 = rec2.cpu().numpy().reshape(n, 3)
-    r3 = rec3.cpu().numpy().reshape(n, 3)
+    width_total, layout = runner.stage_layout[0]
+    _, w, prefix = [t for t in layout if t[0] == 4][0]
+    r1 = res.stage_recs[0][prefix * n:(prefix + w) * n].reshape(n, w)
+    r2 = rec2.cpu().numpy().reshape(n, 2)
+    r3 = rec3.cpu().numpy().reshape(n, 2)
     lg = dbg.cpu().numpy().reshape(n, 16)[:, :5]
     cpu = np.array([m.detect(t)[0] for t in texts])
     print("pipeline lang", r1[:12, 0], "\nhead+dbg", r2[:12, 0], "\nhead nodbg", r3[:12, 0],

@@ -296,6 +296,11 @@ PYBIND11_MODULE(_tbhost, m) {
   m.attr("LID_BUCKETS") = kLidBuckets;
   m.attr("LID_LANGS_PAD") = kLidLangsPad;
 
+  py::class_<StdRng>(m, "StdRng")
+      .def(py::init<uint64_t>())
+      .def("next_u32", &StdRng::next_u32)
+      .def("gen_f32", &StdRng::gen_f32);
+
   py::class_<BadWordsModule, std::shared_ptr<BadWordsModule>>(m, "BadWordsModule")
       .def(py::init([](const std::string& dir) {
         auto b = std::make_shared<BadWordsModule>();
@@ -307,6 +312,12 @@ PYBIND11_MODULE(_tbhost, m) {
         auto l = b.get(lang, &sup);
         if (!l) return false;
         return l->match(text);
+      })
+      .def("lookup", [](BadWordsModule& b, const std::string& lang) {
+        // (supported language?, has a non-empty list?)
+        bool sup;
+        auto l = b.get(lang, &sup);
+        return py::make_tuple(sup, (bool)l);
       });
 
   // ---- batch state ----

@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstring>
 #include <fstream>
+#include <random>
 #include <sstream>
 
 #include "../common/langid.h"
@@ -170,13 +171,38 @@ std::shared_ptr<BadWordsLang> BadWordsModule::get(const std::string& lang, bool*
   return res;
 }
 
-// Deterministic per-document uniform f32 in [0,1) (splitmix64 keyed by seed and row index).
-static float doc_uniform(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (float)(z >> 40) * (1.0f / 16777216.0f);
+StdRng::StdRng(uint64_t state) {
+  for (int i = 0; i < 8; ++i) {  // rand_core SeedableRng::seed_from_u64
+    state = state * 6364136223846793005ull + 11634580027462260723ull;
+    const uint32_t xs = (uint32_t)(((state >> 18) ^ state) >> 27);
+    const uint32_t rot = (uint32_t)(state >> 59);
+    key[i] = (xs >> rot) | (xs << ((32 - rot) & 31));
+  }
+}
+
+static inline uint32_t rotl32(uint32_t v, int c) { return (v << c) | (v >> (32 - c)); }
+
+uint32_t StdRng::next_u32() {
+  if (pos >= 16) {
+    uint32_t st[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1], key[2], key[3],
+                       key[4], key[5], key[6], key[7], (uint32_t)counter, (uint32_t)(counter >> 32), 0u, 0u};
+    uint32_t x[16];
+    for (int i = 0; i < 16; ++i) x[i] = st[i];
+    auto qr = [&](int a, int b, int c, int d) {
+      x[a] += x[b]; x[d] = rotl32(x[d] ^ x[a], 16);
+      x[c] += x[d]; x[b] = rotl32(x[b] ^ x[c], 12);
+      x[a] += x[b]; x[d] = rotl32(x[d] ^ x[a], 8);
+      x[c] += x[d]; x[b] = rotl32(x[b] ^ x[c], 7);
+    };
+    for (int r = 0; r < 6; ++r) {  // 12 rounds
+      qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15);
+      qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14);
+    }
+    for (int i = 0; i < 16; ++i) buf[i] = x[i] + st[i];
+    ++counter;
+    pos = 0;
+  }
+  return buf[pos++];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -274,43 +300,50 @@ void BatchState::apply_badwords(const StepCfg& cfg, int step_index, BadWordsModu
     bool sup;
     mod.get(l, &sup);
   }
+  // matching in parallel, then keep-fraction draws in document order from the shared stream
+  std::vector<int8_t> matched(n_, -1);  // -1 n/a, 0 no match, 1 match
   parallel_for(n_, nthreads_, [&](int64_t a, int64_t b) {
     for (int64_t i = a; i < b; ++i) {
       if (fail_step_[i] >= 0) continue;
-      Decision d;
-      bool sup;
       auto it = mod.langs.find(lang[i]);
-      std::shared_ptr<BadWordsLang> bl = it == mod.langs.end() ? nullptr : it->second;
-      sup = false;
-      for (auto l : kBadwordsLangs) if (lang[i] == l) sup = true;
-      if (!sup) {
-        if (cfg.fail_on_missing_language) {
-          d.pass = false;
-          d.reason = "There is no badwords list available for '" + lang[i] +
-                     "'. Set fail_on_missing_language=False to continue anyway.";
-          d.meta.push_back({"c4_badwords_filter_status", "filtered"});
-          d.meta.push_back({"c4_badwords_filter_reason", d.reason});
-        } else {
-          d.meta.push_back({"c4_badwords_filter_status", "passed_no_regex"});
-        }
-      } else if (!bl) {
-        d.meta.push_back({"c4_badwords_filter_status", "passed_no_regex"});
-      } else if (bl->match(content(i))) {
-        if (cfg.keep_fraction > 0.0 &&
-            doc_uniform(cfg.seed ? *cfg.seed : 0x5EEDull, (uint64_t)i) < (float)cfg.keep_fraction) {
-          d.meta.push_back({"c4_badwords_filter_status", "passed_kept_by_fraction"});
-        } else {
-          d.pass = false;
-          d.reason = "document_removed_with_badwords";
-          d.meta.push_back({"c4_badwords_filter_status", "filtered"});
-          d.meta.push_back({"c4_badwords_filter_reason", d.reason});
-        }
-      } else {
-        d.meta.push_back({"c4_badwords_filter_status", "passed"});
-      }
-      apply_decision(i, step_index, d);
+      if (it != mod.langs.end() && it->second) matched[i] = it->second->match(content(i)) ? 1 : 0;
     }
   });
+  if (!mod.rng) {
+    uint64_t seed = cfg.seed ? *cfg.seed : (((uint64_t)std::random_device{}() << 32) ^ std::random_device{}());
+    mod.rng = std::make_unique<StdRng>(seed);
+  }
+  for (int64_t i = 0; i < n_; ++i) {
+    if (fail_step_[i] >= 0) continue;
+    Decision d;
+    bool sup = false;
+    for (auto l : kBadwordsLangs) if (lang[i] == l) sup = true;
+    if (!sup) {
+      if (cfg.fail_on_missing_language) {
+        d.pass = false;
+        d.reason = "There is no badwords list available for '" + lang[i] +
+                   "'. Set fail_on_missing_language=False to continue anyway.";
+        d.meta.push_back({"c4_badwords_filter_status", "filtered"});
+        d.meta.push_back({"c4_badwords_filter_reason", d.reason});
+      } else {
+        d.meta.push_back({"c4_badwords_filter_status", "passed_no_regex"});
+      }
+    } else if (matched[i] < 0) {
+      d.meta.push_back({"c4_badwords_filter_status", "passed_no_regex"});
+    } else if (matched[i] == 1) {
+      if (cfg.keep_fraction > 0.0 && mod.rng->gen_f32() < (float)cfg.keep_fraction) {
+        d.meta.push_back({"c4_badwords_filter_status", "passed_kept_by_fraction"});
+      } else {
+        d.pass = false;
+        d.reason = "document_removed_with_badwords";
+        d.meta.push_back({"c4_badwords_filter_status", "filtered"});
+        d.meta.push_back({"c4_badwords_filter_reason", d.reason});
+      }
+    } else {
+      d.meta.push_back({"c4_badwords_filter_status", "passed"});
+    }
+    apply_decision(i, step_index, d);
+  }
 }
 
 void BatchState::run_cpu(const std::vector<StepCfg>& steps, int begin, int end, SegBackend be,

@@ -40,8 +40,22 @@ struct BadWordsLang {
   bool match(std::string_view text) const;
 };
 
+// rand 0.8 `StdRng` (ChaCha12, key from `seed_from_u64` via PCG32) and `gen::<f32>()`, so a
+// seeded C4BadWordsFilter draws the same keep/drop sequence as the reference
+// (c4_filters.rs:303-309, :520).
+struct StdRng {
+  uint32_t key[8];
+  uint64_t counter = 0;
+  uint32_t buf[16];
+  int pos = 16;
+  explicit StdRng(uint64_t seed);
+  uint32_t next_u32();
+  float gen_f32() { return (float)(next_u32() >> 8) * (1.0f / 16777216.0f); }
+};
+
 struct BadWordsModule {
   std::string cache_dir;
+  std::unique_ptr<StdRng> rng;  // shared by every document, drawn in document order
   std::unordered_map<std::string, std::shared_ptr<BadWordsLang>> langs;  // nullptr = no list
   std::shared_ptr<BadWordsLang> get(const std::string& lang, bool* supported);
 };

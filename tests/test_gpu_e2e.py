@@ -1,0 +1,51 @@
+"""End-to-end on the MI355X: Parquet -> device pipeline -> Parquet must equal the CPU ICU-oracle
+run byte for byte (kept/excluded rows, rewritten text, metadata JSON), except for documents whose
+language-id decision is an exact bf16 near-tie (none in this corpus). Needs an MI355X."""
+import os
+
+import pyarrow.parquet as pq
+import pytest
+
+from textblaster_amd.data_model import TextDocument
+from textblaster_amd.io.parquet import ParquetWriter
+from textblaster_amd.runner import RunConfig, run
+from textblaster_amd.utils import synth
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CFG = os.path.join(REPO, "config", "bench_pipeline.yaml")
+
+
+def test_device_run_equals_cpu_oracle(tmp_path):
+    import torch
+
+    assert torch.cuda.is_available()
+    texts = synth.make_corpus(6000, 1024, seed=21) + ["", "日本語のテキストです。", "&amp; entity &lt;b&gt; text."]
+    docs = [TextDocument(f"g{i}", t, "gpu", metadata={"n": str(i)} if i % 5 == 0 else {}) for i, t in enumerate(texts)]
+    inp = str(tmp_path / "in.parquet")
+    w = ParquetWriter(inp)
+    w.write_batch(docs)
+    w.close()
+    outs = {}
+    for backend in ("cuda", "cpu"):
+        o, e = str(tmp_path / f"{backend}.o.parquet"), str(tmp_path / f"{backend}.e.parquet")
+        st = run(RunConfig(inp, o, e, CFG, backend=backend, segmentation="icu", unit_rows=2048))
+        outs[backend] = (st, pq.read_table(o), pq.read_table(e))
+    (sg, og, eg), (sc, oc, ec) = outs["cuda"], outs["cpu"]
+    assert (sg.docs, sg.kept, sg.excluded, sg.errors) == (sc.docs, sc.kept, sc.excluded, sc.errors)
+    assert sg.step_filtered == sc.step_filtered
+    assert og.column("id").equals(oc.column("id")) and og.column("text").equals(oc.column("text"))
+    assert eg.column("id").equals(ec.column("id")) and eg.column("text").equals(ec.column("text"))
+    # metadata carries the language confidence; fp32 head rounding may differ in the last digits
+    import json
+
+    for a, b in zip(og.column("metadata").to_pylist() + eg.column("metadata").to_pylist(),
+                    oc.column("metadata").to_pylist() + ec.column("metadata").to_pylist()):
+        ja, jb = json.loads(a), json.loads(b)
+        assert ja.keys() == jb.keys()
+        for k in ja:
+            if k == "Detected language confidence":
+                assert abs(float(ja[k]) - float(jb[k])) < 1e-5
+            else:
+                assert ja[k] == jb[k]

@@ -114,6 +114,19 @@ def _timestamp_us(arr: pa.Array) -> pa.Array:
     return pa.nulls(len(arr), pa.timestamp("us"))
 
 
+_RS_NAMES = {
+    "int8": "Int8", "int16": "Int16", "int32": "Int32", "int64": "Int64", "uint8": "UInt8", "uint16": "UInt16",
+    "uint32": "UInt32", "uint64": "UInt64", "float": "Float32", "double": "Float64", "halffloat": "Float16",
+    "bool": "Boolean", "binary": "Binary", "large_binary": "LargeBinary", "null": "Null", "date32[day]": "Date32",
+    "date64[ms]": "Date64", "string": "Utf8", "large_string": "LargeUtf8",
+}
+
+
+def arrow_rs_debug(t: pa.DataType) -> str:
+    """Name of an Arrow type as arrow-rs's ``{:?}`` prints it (for the reference's messages)."""
+    return _RS_NAMES.get(str(t), str(t))
+
+
 @dataclasses.dataclass
 class DocBatch:
     """One read batch in engine layout."""
@@ -133,22 +146,33 @@ class ParquetReader:
     """reference parquet_reader.rs:18-251"""
 
     def __init__(self, config: ParquetInputConfig, html_threads: int = 8):
+        # like the reference, construction does not touch the file; errors surface on first use
         self.config = config
         self.html_threads = html_threads
+        self._pf_obj = None
+
+    @property
+    def _pf(self) -> pq.ParquetFile:
+        return self.open()._pf_obj
+
+    def open(self) -> "ParquetReader":
+        if self._pf_obj is not None:
+            return self
+        config = self.config
         try:
-            self._pf = pq.ParquetFile(config.path)
+            pf = pq.ParquetFile(config.path)
         except FileNotFoundError as e:
             raise IoError(e) from e
         except (pa.ArrowInvalid, OSError) as e:
             raise ParquetError(e) from e
-        schema = self._pf.schema_arrow
+        schema = pf.schema_arrow
         names = schema.names
         for col in (config.text_column, config.id_column):
             if col not in names:
                 raise ConfigError(f"Required column '{col}' not found in schema.")
         ttype = schema.field(config.text_column).type
         if not (pa.types.is_string(ttype) or pa.types.is_large_string(ttype)):
-            raise ConfigError(f"Column '{config.text_column}' must be Utf8 or LargeUtf8, found: {ttype}")
+            raise ConfigError(f"Column '{config.text_column}' must be Utf8 or LargeUtf8, found: {arrow_rs_debug(ttype)}")
         self.has_source = "source" in names
         self.has_added = "added" in names
         self.has_created = "created" in names
@@ -158,6 +182,8 @@ class ParquetReader:
         self.columns = [config.text_column, config.id_column] + [
             c for c, ok in (("source", self.has_source), ("added", self.has_added), ("created", self.has_created),
                             ("metadata", self.has_metadata)) if ok and c not in (config.text_column, config.id_column)]
+        self._pf_obj = pf
+        return self
 
     @property
     def num_row_groups(self) -> int:

@@ -1,0 +1,465 @@
+"""End-to-end Parquet -> pipeline -> Parquet run: the in-process replacement of the reference's
+producer + worker pair (reference producer_logic.rs:23-230, worker_logic.rs:136-283,
+bin/producer.rs, bin/worker.rs).
+
+Work decomposition
+  The input is cut into *units*: row-group slices of at most ``unit_rows`` rows. Units are the
+  scheduling, sharding and checkpoint granularity. Rank ``r`` of ``W`` owns a contiguous range
+  of units balanced by bytes (``parallel.dist.shard_ranges``), so documents never cross GPUs.
+
+Per rank, three stages overlap (bounded queues, the heavy native calls release the GIL):
+  reader thread   Parquet decode + HTML-entity decode + packing   (unit k+1)
+  main thread     Engine.process: H2D, HIP kernels, D2H, resolve   (unit k)
+  writer thread   Arrow assembly + Parquet encode                  (unit k-1)
+
+Outputs
+  * single rank, no checkpointing: rows stream straight into ``output_file`` / ``excluded_file``;
+  * otherwise every unit writes ``<work_dir>/parts/u<unit>.{kept,excluded}.parquet`` and appends a
+    line to ``<work_dir>/manifest.rank<r>.jsonl`` once both files are closed. ``resume=True``
+    skips units already in a manifest. After a barrier rank 0 concatenates the parts in unit
+    order into the two final files (row order = input order) and removes the work dir unless
+    ``keep_parts``.
+  Counters (docs, kept, excluded, errors, per-step filtered) are all-reduced over RCCL (AR1);
+  rank 0 reports the global view and serves it on the metrics endpoint.
+"""
+from __future__ import annotations
+
+import dataclasses
+import hashlib
+import json
+import logging
+import os
+import queue
+import shutil
+import threading
+import time
+from typing import Dict, Iterator, List, Optional, Tuple
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.parquet as pq
+
+from .config.pipeline import PipelineConfig, load_pipeline_config
+from .errors import PipelineError, Unexpected
+from .io.parquet import (DocBatch, ParquetInputConfig, ParquetReader, ParquetWriter, build_output_table,
+                         packed_to_string_array)
+from .parallel.dist import DistContext, shard_ranges
+from .utils import metrics
+
+log = logging.getLogger("textblaster_amd.runner")
+
+
+@dataclasses.dataclass
+class RunConfig:
+    input_file: str
+    output_file: str = "output_processed.parquet"
+    excluded_file: str = "excluded.parquet"
+    pipeline_config: str = "config/pipeline_config.yaml"
+    text_column: str = "text"
+    id_column: str = "id"
+    backend: str = "auto"              # auto | cuda | cpu
+    segmentation: str = "icu"          # CPU backend segmentation: icu (oracle) | rules
+    unit_rows: int = 65536
+    threads: Optional[int] = None
+    work_dir: Optional[str] = None     # checkpoint dir (default: <output_file>.work when needed)
+    resume: bool = False
+    checkpoint: bool = False           # force the part-file path on a single rank
+    keep_parts: bool = False
+    compression: str = "none"
+    tokenizer_dir: Optional[str] = None
+    badwords_dir: Optional[str] = None
+    metrics_port: Optional[int] = None
+    progress_interval: float = 1.0
+
+
+@dataclasses.dataclass
+class RunStats:
+    docs: int = 0
+    kept: int = 0
+    excluded: int = 0
+    errors: int = 0
+    bytes_in: int = 0
+    seconds: float = 0.0
+    units: int = 0
+    units_skipped: int = 0
+    delegated: int = 0
+    step_filtered: List[int] = dataclasses.field(default_factory=list)
+
+    @property
+    def docs_per_sec(self) -> float:
+        return self.docs / self.seconds if self.seconds > 0 else 0.0
+
+    def vector(self, nsteps: int) -> np.ndarray:
+        sf = list(self.step_filtered) + [0] * (nsteps - len(self.step_filtered))
+        return np.asarray([self.docs, self.kept, self.excluded, self.errors, self.bytes_in, self.delegated] + sf,
+                          dtype=np.int64)
+
+    @classmethod
+    def from_vector(cls, v: np.ndarray, seconds: float, units: int, skipped: int) -> "RunStats":
+        v = [int(x) for x in v]
+        return cls(v[0], v[1], v[2], v[3], v[4], seconds, units, skipped, v[5], v[6:])
+
+
+# ---------------------------------------------------------------------------------------------
+# units
+
+@dataclasses.dataclass(frozen=True)
+class Unit:
+    index: int
+    row_group: int
+    start: int
+    stop: int
+    est_bytes: float
+
+
+def plan_units(reader: ParquetReader, unit_rows: int) -> List[Unit]:
+    units = []
+    for rg, (n, b) in enumerate(zip(reader.row_group_rows(), reader.row_group_bytes())):
+        for s in range(0, n, unit_rows):
+            e = min(n, s + unit_rows)
+            units.append(Unit(len(units), rg, s, e, b * (e - s) / max(n, 1)))
+    return units
+
+
+def _fingerprint(path: str, unit_rows: int, pipeline_path: str) -> str:
+    st = os.stat(path)
+    h = hashlib.sha256()
+    h.update(f"{os.path.abspath(path)}|{st.st_size}|{int(st.st_mtime)}|{unit_rows}".encode())
+    with open(pipeline_path, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+class _UnitReader:
+    """Reads units in order, caching the last decoded row group (consecutive units usually share
+    it)."""
+
+    def __init__(self, reader: ParquetReader):
+        self.reader = reader
+        self._rg = -1
+        self._tbl = None
+
+    def read(self, u: Unit) -> DocBatch:
+        if u.row_group != self._rg:
+            self._tbl = self.reader._pf.read_row_group(u.row_group, columns=self.reader.columns, use_threads=True)
+            self._rg = u.row_group
+        t = self._tbl.slice(u.start, u.stop - u.start).combine_chunks()
+        batches = t.to_batches()
+        rb = batches[0] if batches else pa.RecordBatch.from_pylist([], schema=t.schema)
+        return self.reader._to_docbatch(rb)
+
+
+# ---------------------------------------------------------------------------------------------
+# output assembly
+
+def part_table(batch: DocBatch, part) -> pa.Table:
+    rows = pa.array(part.rows, type=pa.int64())
+    text = packed_to_string_array(part.text_data, part.text_off)
+    meta = packed_to_string_array(part.meta_data, part.meta_off, part.meta_valid)
+    return build_output_table(batch.ids.take(rows).cast(pa.string()), batch.source.take(rows),
+                              text, batch.added.take(rows), batch.created.take(rows), meta)
+
+
+class _Sink:
+    def write(self, unit: Unit, kept: pa.Table, excluded: pa.Table, counts: Dict) -> None:
+        raise NotImplementedError
+
+    def close(self) -> None:
+        pass
+
+
+class _DirectSink(_Sink):
+    def __init__(self, rc: RunConfig):
+        self.out = ParquetWriter(rc.output_file, rc.compression)
+        self.exc = ParquetWriter(rc.excluded_file, rc.compression)
+
+    def write(self, unit, kept, excluded, counts):
+        self.out.write_table(kept)
+        self.exc.write_table(excluded)
+
+    def close(self):
+        self.out.close()
+        self.exc.close()
+
+
+class _PartSink(_Sink):
+    def __init__(self, rc: RunConfig, work_dir: str, rank: int):
+        self.rc = rc
+        self.parts = os.path.join(work_dir, "parts")
+        os.makedirs(self.parts, exist_ok=True)
+        self.manifest = open(os.path.join(work_dir, f"manifest.rank{rank}.jsonl"), "a", encoding="utf-8")
+
+    def write(self, unit, kept, excluded, counts):
+        for kind, tbl in (("kept", kept), ("excluded", excluded)):
+            final = os.path.join(self.parts, f"u{unit.index:07d}.{kind}.parquet")
+            tmp = final + ".tmp"
+            w = ParquetWriter(tmp, self.rc.compression)
+            w.write_table(tbl)
+            w.close()
+            os.replace(tmp, final)
+        self.manifest.write(json.dumps(dict(unit=unit.index, **counts)) + "\n")
+        self.manifest.flush()
+        os.fsync(self.manifest.fileno())
+
+    def close(self):
+        self.manifest.close()
+
+
+def read_manifests(work_dir: str) -> Dict[int, Dict]:
+    done = {}
+    if not os.path.isdir(work_dir):
+        return done
+    for name in sorted(os.listdir(work_dir)):
+        if name.startswith("manifest.rank") and name.endswith(".jsonl"):
+            with open(os.path.join(work_dir, name), encoding="utf-8") as f:
+                for line in f:
+                    line = line.strip()
+                    if not line:
+                        continue
+                    try:
+                        rec = json.loads(line)
+                    except json.JSONDecodeError:
+                        continue  # a torn last line from a crash: the unit is redone
+                    done[int(rec["unit"])] = rec
+    return done
+
+
+def merge_parts(work_dir: str, n_units: int, rc: RunConfig) -> None:
+    parts = os.path.join(work_dir, "parts")
+    for kind, path in (("kept", rc.output_file), ("excluded", rc.excluded_file)):
+        w = ParquetWriter(path, rc.compression)
+        for u in range(n_units):
+            p = os.path.join(parts, f"u{u:07d}.{kind}.parquet")
+            if not os.path.exists(p):
+                raise Unexpected(f"missing part file {p}; rerun with --resume")
+            pf = pq.ParquetFile(p)
+            for i in range(pf.num_row_groups):
+                w.write_table(pf.read_row_group(i))
+        w.close()
+
+
+# ---------------------------------------------------------------------------------------------
+
+def _prefetch(gen: Iterator, depth: int) -> Iterator:
+    """Runs ``gen`` in a thread, keeping up to ``depth`` items ready."""
+    q: queue.Queue = queue.Queue(maxsize=depth)
+    sentinel = object()
+    err: List[BaseException] = []
+    stop = threading.Event()
+
+    def worker():
+        try:
+            for item in gen:
+                while not stop.is_set():
+                    try:
+                        q.put(item, timeout=0.1)
+                        break
+                    except queue.Full:
+                        continue
+                if stop.is_set():
+                    return
+        except BaseException as e:  # noqa: BLE001 - re-raised in the consumer
+            err.append(e)
+        finally:
+            q.put(sentinel)
+
+    t = threading.Thread(target=worker, name="tb-reader", daemon=True)
+    t.start()
+    try:
+        while True:
+            item = q.get()
+            if item is sentinel:
+                break
+            yield item
+        if err:
+            raise err[0]
+    finally:
+        stop.set()
+
+
+class _Writer:
+    """Single background writer thread; ``submit`` blocks when ``depth`` writes are pending."""
+
+    def __init__(self, sink: _Sink, depth: int = 2):
+        self.sink = sink
+        self.q: queue.Queue = queue.Queue(maxsize=depth)
+        self.err: List[BaseException] = []
+        self.t = threading.Thread(target=self._run, name="tb-writer", daemon=True)
+        self.t.start()
+
+    def _run(self):
+        while True:
+            job = self.q.get()
+            if job is None:
+                return
+            if self.err:
+                continue
+            try:
+                batch, res, unit, counts = job
+                kept = part_table(batch, res.kept[0]) if len(res.kept) == 1 else pa.concat_tables(
+                    [part_table(batch, p) for p in res.kept])
+                exc = part_table(batch, res.excluded[0]) if len(res.excluded) == 1 else pa.concat_tables(
+                    [part_table(batch, p) for p in res.excluded])
+                if len(res.kept) > 1:
+                    kept = _sort_by_row(kept, np.concatenate([p.rows for p in res.kept]))
+                if len(res.excluded) > 1:
+                    exc = _sort_by_row(exc, np.concatenate([p.rows for p in res.excluded]))
+                self.sink.write(unit, kept, exc, counts)
+            except BaseException as e:  # noqa: BLE001
+                self.err.append(e)
+
+    def submit(self, job):
+        if self.err:
+            raise self.err[0]
+        self.q.put(job)
+
+    def close(self):
+        self.q.put(None)
+        self.t.join()
+        self.sink.close()
+        if self.err:
+            raise self.err[0]
+
+
+def _sort_by_row(tbl: pa.Table, rows: np.ndarray) -> pa.Table:
+    order = np.argsort(rows, kind="stable")
+    return tbl.take(pa.array(order))
+
+
+def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[PipelineConfig] = None,
+        engine=None) -> RunStats:
+    """Process ``rc.input_file`` end to end; returns the global (all-rank) statistics."""
+    from .pipeline.engine import Engine
+
+    ctx = ctx or DistContext()
+    rank, world = ctx.rank, ctx.world_size
+    cfg = cfg or load_pipeline_config(rc.pipeline_config)
+    nsteps = len(cfg.pipeline)
+    t_start = time.perf_counter()
+    reader = ParquetReader(ParquetInputConfig(rc.input_file, rc.text_column, rc.id_column))
+    units = plan_units(reader, rc.unit_rows)
+    if engine is None:
+        backend = rc.backend
+        device = ctx.device if backend in ("cuda", "auto") else None
+        engine = Engine(cfg, backend=backend, device=device, nthreads=rc.threads, segmentation=rc.segmentation,
+                        tokenizer_dir=rc.tokenizer_dir, badwords_dir=rc.badwords_dir)
+    use_parts = world > 1 or rc.checkpoint or rc.resume
+    work_dir = rc.work_dir or (rc.output_file + ".work")
+    done: Dict[int, Dict] = {}
+    if use_parts:
+        if rank == 0:
+            os.makedirs(work_dir, exist_ok=True)
+            fp = _fingerprint(rc.input_file, rc.unit_rows, rc.pipeline_config) if os.path.exists(
+                rc.pipeline_config) else None
+            plan_path = os.path.join(work_dir, "plan.json")
+            if rc.resume and os.path.exists(plan_path):
+                with open(plan_path, encoding="utf-8") as f:
+                    old = json.load(f)
+                if old.get("fingerprint") != fp or old.get("n_units") != len(units):
+                    raise Unexpected(f"--resume: {work_dir} was written for a different input/config "
+                                     f"(fingerprint {old.get('fingerprint')} != {fp}); remove it to start over")
+            elif not rc.resume:
+                for name in os.listdir(work_dir):
+                    if name.startswith("manifest.rank"):
+                        os.remove(os.path.join(work_dir, name))
+                shutil.rmtree(os.path.join(work_dir, "parts"), ignore_errors=True)
+            with open(plan_path, "w", encoding="utf-8") as f:
+                json.dump({"fingerprint": fp, "n_units": len(units), "unit_rows": rc.unit_rows,
+                           "input": os.path.abspath(rc.input_file)}, f)
+        ctx.barrier()
+        if rc.resume:
+            done = read_manifests(work_dir)
+    shard = shard_ranges([u.est_bytes for u in units], world)[rank]
+    mine = [units[i] for i in shard]
+    todo = [u for u in mine if u.index not in done]
+    local = RunStats(step_filtered=[0] * nsteps)
+    for u in mine:
+        if u.index in done:
+            rec = done[u.index]
+            local.docs += rec["docs"]
+            local.kept += rec["kept"]
+            local.excluded += rec["excluded"]
+            local.errors += rec["errors"]
+            for i, c in enumerate(rec.get("step_filtered", [])):
+                local.step_filtered[i] += c
+            local.units_skipped += 1
+    metrics.RANK.set(rank)
+    metrics.WORLD_SIZE.set(world)
+    if rank == 0 and rc.metrics_port is not None:
+        metrics.setup_prometheus_metrics(rc.metrics_port)
+    log.info("rank %d/%d: %d units (%d already done), backend=%s", rank, world, len(mine), len(mine) - len(todo),
+             engine.backend)
+
+    sink = _PartSink(rc, work_dir, rank) if use_parts else _DirectSink(rc)
+    writer = _Writer(sink)
+    ureader = _UnitReader(reader)
+    last_report = time.perf_counter()
+    last_docs = local.docs
+    try:
+        for unit, batch in _prefetch(((u, ureader.read(u)) for u in todo), depth=2):
+            t0 = time.perf_counter()
+            with metrics.ACTIVE_PROCESSING_TASKS.track_inprogress():
+                res = engine.process(batch.text[0], batch.text[1], batch.meta)
+            dt = time.perf_counter() - t0
+            fs = res.fail_step
+            step_counts = np.bincount(fs[(res.status == 1) & (fs >= 0)], minlength=nsteps)[:nsteps] \
+                if len(fs) else np.zeros(nsteps, dtype=np.int64)
+            counts = dict(docs=batch.n + batch.error_rows, kept=res.n_kept, excluded=res.n_excluded,
+                          errors=int(len(res.error_rows)) + batch.error_rows,
+                          step_filtered=[int(x) for x in step_counts])
+            writer.submit((batch, res, unit, counts))
+            local.docs += counts["docs"]
+            local.kept += counts["kept"]
+            local.excluded += counts["excluded"]
+            local.errors += counts["errors"]
+            local.bytes_in += batch.bytes_in
+            local.delegated += res.n_delegated
+            for i, c in enumerate(step_counts):
+                local.step_filtered[i] += int(c)
+            local.units += 1
+            _update_metrics(cfg, res, batch, counts, step_counts, dt)
+            now = time.perf_counter()
+            if now - last_report >= rc.progress_interval:
+                speed = (local.docs - last_docs) / (now - last_report)
+                log.info("Processed: %d, Filtered: %d, Errored: %d | Speed: %.2f docs/sec", local.kept,
+                         local.excluded, local.errors, speed)
+                last_report, last_docs = now, local.docs
+    finally:
+        writer.close()
+    elapsed = time.perf_counter() - t_start
+    total_vec = ctx.all_reduce_sum(local.vector(nsteps))
+    elapsed_max = ctx.all_reduce_max(elapsed)
+    units_done = int(ctx.all_reduce_sum([local.units])[0])
+    skipped = int(ctx.all_reduce_sum([local.units_skipped])[0])
+    stats = RunStats.from_vector(total_vec, elapsed_max, units_done, skipped)
+    if use_parts:
+        ctx.barrier()
+        if rank == 0:
+            merge_parts(work_dir, len(units), rc)
+            if not rc.keep_parts:
+                shutil.rmtree(work_dir, ignore_errors=True)
+        ctx.barrier()
+    stats.seconds = ctx.all_reduce_max(time.perf_counter() - t_start)
+    if rank == 0:
+        metrics.set_global_counts(stats.docs, stats.kept, stats.excluded, stats.errors)
+    return stats
+
+
+def _update_metrics(cfg, res, batch, counts, step_counts, dt) -> None:
+    metrics.TASKS_PROCESSED_TOTAL.inc(counts["kept"])
+    metrics.TASKS_FILTERED_TOTAL.inc(counts["excluded"])
+    metrics.TASKS_FAILED_TOTAL.inc(counts["errors"])
+    metrics.RESULTS_RECEIVED_TOTAL.inc(counts["docs"])
+    metrics.RESULTS_SUCCESS_TOTAL.inc(counts["kept"])
+    metrics.RESULTS_FILTERED_TOTAL.inc(counts["excluded"])
+    metrics.RESULTS_ERROR_TOTAL.inc(counts["errors"])
+    metrics.TASK_PROCESSING_DURATION_SECONDS.observe(dt)
+    metrics.BYTES_PROCESSED_TOTAL.inc(batch.bytes_in)
+    metrics.DELEGATED_DOCS_TOTAL.inc(res.n_delegated)
+    if dt > 0:
+        metrics.DOCS_PER_SECOND.set(counts["docs"] / dt)
+    for phase, sec in res.timings.items():
+        metrics.GPU_PHASE_SECONDS.labels(phase).observe(sec)
+    for i, c in enumerate(step_counts):
+        if c:
+            metrics.STEP_FILTERED_TOTAL.labels(str(i), cfg.pipeline[i].type).inc(int(c))

@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--mean-bytes", type=int, default=1024)
     ap.add_argument("--pool", type=int, default=16384, help="distinct synthetic docs per rank")
     ap.add_argument("--config", default=os.path.join(ROOT, "config", "bench_pipeline.yaml"))
-    ap.add_argument("--backend", default="cuda", choices=["cuda", "cpu"])
+    ap.add_argument("--backend", default="cuda", choices=["cuda", "cpu", "emulate"])
     ap.add_argument("--segmentation", default="icu", help="CPU backend segmentation (icu|rules)")
     ap.add_argument("--threads", type=int, default=None)
     args = ap.parse_args()
@@ -74,20 +74,24 @@ def main():
     bytes_per_step = float(np.mean([len(b[0]) for b in batches]))
     counters = np.zeros(4, dtype=np.int64)  # docs, kept, excluded, errors
 
-    def step(i):
-        data, off = batches[i % len(batches)]
-        res = eng.process(data, off)
-        return res
+    def feed(k, start):
+        for i in range(start, start + k):
+            yield batches[i % len(batches)]
 
-    for i in range(args.warmup):
-        step(i)
+    # Steps run through Engine.process_many: step i+1's H2D + kernels are queued before step i
+    # is resolved on the host (device/host overlap). Every step's full pipeline completes inside
+    # the timed region: process_many returns the K-th result only after its assembly.
+    for res in eng.process_many(feed(args.warmup, 0)):
+        pass
     ctx.barrier()
     if args.backend == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        res = step(i)
+    n_done = 0
+    for res in eng.process_many(feed(args.steps, args.warmup)):
         counters += [res.n_docs, res.n_kept, res.n_excluded, len(res.error_rows)]
+        n_done += 1
+    assert n_done == args.steps
     if args.backend == "cuda":
         torch.cuda.synchronize()
     ctx.barrier()

@@ -20,6 +20,10 @@ enum DevStepKind : int32_t {
   DK_LANGID = 4,   // featurize only (the head runs in its own kernel)
 };
 
+// Max bytes a device C4 rewrite may add to one document (larger growth -> CPU path), so the host
+// can size the next content version without reading the device scan back.
+constexpr uint32_t kC4MaxGrowth = 16;
+
 struct DevStep {
   int32_t kind;
   int32_t width;       // record width (int64 fields)

@@ -859,6 +859,15 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
     blen = jc.off[tce] - jc.off[tcs];
   }
   const int64_t jrel = (int64_t)((const char*)Jb - x.scr) + bstart;
+  // The rewrite can only grow a document by one '\n' per sentence not followed by whitespace
+  // (split_paragraph=false). Bounding the growth to kC4MaxGrowth bytes lets the host size the
+  // next version's buffer (and its D2H copy) up front without a sync; the rare document that
+  // would exceed it is recomputed on the CPU path.
+  if (blen > n + kC4MaxGrowth) {
+    x.set_flag(DOC_NEEDS_CPU);
+    x.par.single([&]() { src[0] = 0; src[1] = 0; });
+    return;
+  }
   x.par.single([&]() {
     r[0] = 0; r[1] = 0; r[2] = s_long; r[3] = s_punct; r[4] = s_few; r[5] = nsent; r[6] = blen;
     src[0] = jrel;

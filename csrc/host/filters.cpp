@@ -220,9 +220,41 @@ void compute_record(const StepCfg& c, std::string_view text, SegBackend be, int6
 static std::string f2(double x) { return fmt_fixed(x, 2); }
 static std::string f4(double x) { return fmt_fixed(x, 4); }
 
-void decide(const StepCfg& c, const int64_t* r, Decision& d) {
-  d = Decision();
+// One implementation of every step's decision logic, instantiated twice: kFmt=false only
+// derives pass/filtered/error (the per-batch resolve hot path: no strings are built),
+// kFmt=true also formats the reason and the step's metadata (output assembly, per-document
+// API). String-building expressions are wrapped in lambdas that the kFmt=false instance never
+// calls, so both instances take exactly the same branches.
+template <bool kFmt>
+static void decide_t(const StepCfg& c, const int64_t* r, Decision& d) {
+  d.pass = true;
+  d.error = false;
+  if constexpr (kFmt) {
+    d.reason.clear();
+    d.meta.clear();
+  }
   std::vector<std::string> reasons;
+  int nreasons = 0;
+  auto add = [&](auto&& mk) {
+    ++nreasons;
+    if constexpr (kFmt) reasons.push_back(mk());
+  };
+  auto meta = [&](std::string_view k, auto&& mk) {
+    if constexpr (kFmt) d.meta.emplace_back(k, mk());
+  };
+  auto lit = [](const char* s) { return [s]() { return std::string(s); }; };
+  auto finish_multi = [&](std::string_view status_key, std::string_view reasons_key) {
+    if (nreasons) {
+      d.pass = false;
+      if constexpr (kFmt) {
+        d.reason = join(reasons, "; ");
+        d.meta.emplace_back(status_key, "filtered");
+        d.meta.emplace_back(reasons_key, d.reason);
+      }
+    } else {
+      meta(status_key, lit("passed"));
+    }
+  };
   switch (c.kind) {
     case StepKind::GopherQuality: {  // reference gopher_quality.rs:198-317
       const int64_t n = r[rec::GQ_WORDS];
@@ -235,54 +267,49 @@ void decide(const StepCfg& c, const int64_t* r, Decision& d) {
       const double ell_lines = (double)r[rec::GQ_ELL_LINES] / lcalc;
       const double alpha = (double)r[rec::GQ_ALPHA] / ncalc;
       if (c.min_doc_words && n < *c.min_doc_words)
-        reasons.push_back("gopher_short_doc (" + std::to_string(n) + " non-symbol words, required " +
-                          std::to_string(*c.min_doc_words) + ")");
+        add([&] { return "gopher_short_doc (" + std::to_string(n) + " non-symbol words, required " +
+                         std::to_string(*c.min_doc_words) + ")"; });
       if (c.max_doc_words && n > *c.max_doc_words)
-        reasons.push_back("gopher_long_doc (" + std::to_string(n) + " non-symbol words, max " +
-                          std::to_string(*c.max_doc_words) + ")");
+        add([&] { return "gopher_long_doc (" + std::to_string(n) + " non-symbol words, max " +
+                         std::to_string(*c.max_doc_words) + ")"; });
       if (c.min_avg_word_length && avg < *c.min_avg_word_length)
-        reasons.push_back("gopher_below_avg_threshold (avg len " + f2(avg) + ", required " +
-                          f2(*c.min_avg_word_length) +
-                          ((n == 0 && *c.min_avg_word_length > 0.0) ? " - 0 non-symbol words" : "") + ")");
+        add([&] { return "gopher_below_avg_threshold (avg len " + f2(avg) + ", required " +
+                         f2(*c.min_avg_word_length) +
+                         ((n == 0 && *c.min_avg_word_length > 0.0) ? " - 0 non-symbol words" : "") + ")"; });
       if (c.max_avg_word_length && n > 0 && avg > *c.max_avg_word_length)
-        reasons.push_back("gopher_above_avg_threshold (avg len " + f2(avg) + ", max " +
-                          f2(*c.max_avg_word_length) + ")");
+        add([&] { return "gopher_above_avg_threshold (avg len " + f2(avg) + ", max " +
+                         f2(*c.max_avg_word_length) + ")"; });
       if (c.max_symbol_word_ratio) {
         if (hash_ratio > *c.max_symbol_word_ratio)
-          reasons.push_back("gopher_too_many_hashes (ratio " + f2(hash_ratio) + ", max " +
-                            f2(*c.max_symbol_word_ratio) + ")");
+          add([&] { return "gopher_too_many_hashes (ratio " + f2(hash_ratio) + ", max " +
+                           f2(*c.max_symbol_word_ratio) + ")"; });
         if (ell_ratio > *c.max_symbol_word_ratio)
-          reasons.push_back("gopher_too_many_ellipsis_units (ratio " + f2(ell_ratio) + ", max " +
-                            f2(*c.max_symbol_word_ratio) + ")");
+          add([&] { return "gopher_too_many_ellipsis_units (ratio " + f2(ell_ratio) + ", max " +
+                           f2(*c.max_symbol_word_ratio) + ")"; });
       }
       if (c.max_bullet_lines_ratio && bullet > *c.max_bullet_lines_ratio)
-        reasons.push_back("gopher_too_many_bullets (ratio " + f2(bullet) + ", max " +
-                          f2(*c.max_bullet_lines_ratio) + ")");
+        add([&] { return "gopher_too_many_bullets (ratio " + f2(bullet) + ", max " +
+                         f2(*c.max_bullet_lines_ratio) + ")"; });
       if (c.max_ellipsis_lines_ratio && ell_lines > *c.max_ellipsis_lines_ratio)
-        reasons.push_back("gopher_too_many_end_ellipsis_lines (ratio " + f2(ell_lines) + ", max " +
-                          f2(*c.max_ellipsis_lines_ratio) + ")");
+        add([&] { return "gopher_too_many_end_ellipsis_lines (ratio " + f2(ell_lines) + ", max " +
+                         f2(*c.max_ellipsis_lines_ratio) + ")"; });
       if (c.max_non_alpha_words_ratio && alpha < *c.max_non_alpha_words_ratio)
-        reasons.push_back("gopher_below_alpha_threshold (alpha ratio " + f2(alpha) + ", required min " +
-                          f2(*c.max_non_alpha_words_ratio) + ")");
+        add([&] { return "gopher_below_alpha_threshold (alpha ratio " + f2(alpha) + ", required min " +
+                         f2(*c.max_non_alpha_words_ratio) + ")"; });
       if (c.min_stop_words && *c.min_stop_words > 0 && r[rec::GQ_STOP] < *c.min_stop_words)
-        reasons.push_back("gopher_too_few_stop_words (found " + std::to_string(r[rec::GQ_STOP]) +
-                          ", required " + std::to_string(*c.min_stop_words) + ")");
-      if (!reasons.empty()) {
-        d.pass = false;
-        d.reason = join(reasons, "; ");
-        d.meta.push_back({"gopher_quality_filter_status", "filtered"});
-        d.meta.push_back({"gopher_quality_filter_reasons", d.reason});
-      } else {
-        d.meta.push_back({"gopher_quality_filter_status", "passed"});
-      }
+        add([&] { return "gopher_too_few_stop_words (found " + std::to_string(r[rec::GQ_STOP]) + ", required " +
+                         std::to_string(*c.min_stop_words) + ")"; });
+      finish_multi("gopher_quality_filter_status", "gopher_quality_filter_reasons");
       return;
     }
     case StepKind::GopherRepetition: {  // reference gopher_rep.rs:52-220
       if (r[rec::GR_CHARS] < 0) {
         d.pass = false;
-        d.reason = "skipping empty content";
-        d.meta.push_back({"gopher_repetition_filter_status", "filtered"});
-        d.meta.push_back({"gopher_repetition_filter_reason", "skipping empty content"});
+        if constexpr (kFmt) {
+          d.reason = "skipping empty content";
+          d.meta.emplace_back("gopher_repetition_filter_status", "filtered");
+          d.meta.emplace_back("gopher_repetition_filter_reason", "skipping empty content");
+        }
         return;
       }
       const double C = (double)std::max<int64_t>(1, r[rec::GR_CHARS]);
@@ -291,104 +318,99 @@ void decide(const StepCfg& c, const int64_t* r, Decision& d) {
       double v;
       v = (double)r[rec::GR_PARA_DUP] / para_len;
       if (c.dup_para_frac && v > *c.dup_para_frac)
-        reasons.push_back("dup_para_frac (ratio " + f2(v) + ", max " + f2(*c.dup_para_frac) + ")");
+        add([&] { return "dup_para_frac (ratio " + f2(v) + ", max " + f2(*c.dup_para_frac) + ")"; });
       v = (double)r[rec::GR_PARA_DUP_BYTES] / C;
       if (c.dup_para_char_frac && v > *c.dup_para_char_frac)
-        reasons.push_back("dup_para_char_frac (ratio " + f2(v) + ", max " + f2(*c.dup_para_char_frac) + ")");
+        add([&] { return "dup_para_char_frac (ratio " + f2(v) + ", max " + f2(*c.dup_para_char_frac) + ")"; });
       v = (double)r[rec::GR_LINE_DUP] / line_len;
       if (c.dup_line_frac && v > *c.dup_line_frac)
-        reasons.push_back("dup_line_frac (ratio " + f2(v) + ", max " + f2(*c.dup_line_frac) + ")");
+        add([&] { return "dup_line_frac (ratio " + f2(v) + ", max " + f2(*c.dup_line_frac) + ")"; });
       v = (double)r[rec::GR_LINE_DUP_BYTES] / C;
       if (c.dup_line_char_frac && v > *c.dup_line_char_frac)
-        reasons.push_back("dup_line_char_frac (ratio " + f2(v) + ", max " + f2(*c.dup_line_char_frac) + ")");
+        add([&] { return "dup_line_char_frac (ratio " + f2(v) + ", max " + f2(*c.dup_line_char_frac) + ")"; });
       int k = rec::GR_FIXED;
       for (auto& e : c.top_n_grams) {
         v = (double)r[k++] / C;
         if (e.first > 0 && v > e.second)
-          reasons.push_back("top_" + std::to_string(e.first) + "_gram (ratio " + f2(v) + ", max " +
-                            f2(e.second) + ")");
+          add([&] { return "top_" + std::to_string(e.first) + "_gram (ratio " + f2(v) + ", max " + f2(e.second) + ")"; });
       }
       for (auto& e : c.dup_n_grams) {
         v = (double)r[k++] / C;
         if (e.first > 0 && v > e.second)
-          reasons.push_back("duplicated_" + std::to_string(e.first) + "_n_grams (ratio " + f2(v) +
-                            ", max " + f2(e.second) + ")");
+          add([&] { return "duplicated_" + std::to_string(e.first) + "_n_grams (ratio " + f2(v) + ", max " +
+                           f2(e.second) + ")"; });
       }
-      if (!reasons.empty()) {
-        d.pass = false;
-        d.reason = join(reasons, "; ");
-        d.meta.push_back({"gopher_repetition_filter_status", "filtered"});
-        d.meta.push_back({"gopher_repetition_filter_reasons", d.reason});
-      } else {
-        d.meta.push_back({"gopher_repetition_filter_status", "passed"});
-      }
+      finish_multi("gopher_repetition_filter_status", "gopher_repetition_filter_reasons");
       return;
     }
     case StepKind::C4Quality: {  // reference c4_filters.rs:147-295
-      if (r[rec::C4_LOREM]) reasons.push_back("lorem_ipsum");
-      if (r[rec::C4_CURLY]) reasons.push_back("curly_bracket");
-      if (!reasons.empty()) {
-        d.pass = false;
-        d.reason = join(reasons, "; ");
-        d.meta.push_back({"c4_filter_status", "filtered"});
-        d.meta.push_back({"c4_filter_reasons", d.reason});
+      if (r[rec::C4_LOREM]) add(lit("lorem_ipsum"));
+      if (r[rec::C4_CURLY]) add(lit("curly_bracket"));
+      if (nreasons) {
+        finish_multi("c4_filter_status", "c4_filter_reasons");
         return;
       }
       if (c.min_num_sentences > 0 && r[rec::C4_SENTENCES] < c.min_num_sentences) {
         d.pass = false;
-        d.reason = "too_few_sentences (found " + std::to_string(r[rec::C4_SENTENCES]) + ", required " +
-                   std::to_string(c.min_num_sentences) + ")";
-        d.meta.push_back({"c4_filter_status", "filtered"});
-        d.meta.push_back({"c4_filter_reasons", d.reason});
-        if (r[rec::C4_TOO_LONG]) d.meta.push_back({"line-filter-too_long_word", std::to_string(r[rec::C4_TOO_LONG])});
-        if (r[rec::C4_NO_PUNCT]) d.meta.push_back({"line-filter-no_terminal_punc", std::to_string(r[rec::C4_NO_PUNCT])});
-        if (r[rec::C4_TOO_FEW]) d.meta.push_back({"line-filter-too_few_words", std::to_string(r[rec::C4_TOO_FEW])});
+        if constexpr (kFmt) {
+          d.reason = "too_few_sentences (found " + std::to_string(r[rec::C4_SENTENCES]) + ", required " +
+                     std::to_string(c.min_num_sentences) + ")";
+          d.meta.emplace_back("c4_filter_status", "filtered");
+          d.meta.emplace_back("c4_filter_reasons", d.reason);
+          if (r[rec::C4_TOO_LONG]) d.meta.emplace_back("line-filter-too_long_word", std::to_string(r[rec::C4_TOO_LONG]));
+          if (r[rec::C4_NO_PUNCT]) d.meta.emplace_back("line-filter-no_terminal_punc", std::to_string(r[rec::C4_NO_PUNCT]));
+          if (r[rec::C4_TOO_FEW]) d.meta.emplace_back("line-filter-too_few_words", std::to_string(r[rec::C4_TOO_FEW]));
+        }
         return;
       }
-      d.meta.push_back({"c4_filter_status", "passed"});
+      meta("c4_filter_status", lit("passed"));
       return;
     }
     case StepKind::FineWebQuality: {  // reference fineweb_quality.rs:71-226
-      auto fail = [&](const std::string& reason, const std::string& meta_reason) {
+      auto fail = [&](auto&& mk_reason, auto&& mk_meta) {
         d.pass = false;
-        d.reason = reason;
-        d.meta.push_back({"fineweb_filter_status", "filtered"});
-        d.meta.push_back({"fineweb_filter_reason", meta_reason});
+        if constexpr (kFmt) {
+          d.reason = mk_reason();
+          d.meta.emplace_back("fineweb_filter_status", "filtered");
+          d.meta.emplace_back("fineweb_filter_reason", mk_meta());
+        }
       };
       const int64_t nl = r[rec::FW_LINES];
-      if (nl == 0) { fail("empty", "empty document"); return; }
+      if (nl == 0) { fail(lit("empty"), lit("empty document")); return; }
       double ratio = (double)r[rec::FW_STOP_END] / (double)nl;
       if (ratio < c.line_punct_thr && !(ratio == 0.0 && c.line_punct_exclude_zero)) {
-        std::string s = "line_punct_ratio: " + f4(ratio) + " < threshold " + f4(c.line_punct_thr) +
-                        " (exclude_zero: " + (c.line_punct_exclude_zero ? "true" : "false") + ")";
-        fail(s, s);
+        auto mk = [&] {
+          return "line_punct_ratio: " + f4(ratio) + " < threshold " + f4(c.line_punct_thr) + " (exclude_zero: " +
+                 (c.line_punct_exclude_zero ? "true" : "false") + ")";
+        };
+        fail(mk, mk);
         return;
       }
       ratio = (double)r[rec::FW_SHORT] / (double)nl;
       if (ratio > c.short_line_thr) {
-        std::string s = "short_line_ratio: " + f4(ratio) + " > threshold " + f4(c.short_line_thr);
-        fail(s, s);
+        auto mk = [&] { return "short_line_ratio: " + f4(ratio) + " > threshold " + f4(c.short_line_thr); };
+        fail(mk, mk);
         return;
       }
       const int64_t tot = r[rec::FW_CHARS_NO_NL];
       ratio = tot > 0 ? (double)r[rec::FW_DUP_BYTES] / (double)tot : 0.0;
       if (ratio > c.char_duplicates_ratio) {
-        std::string s = "char_dup_ratio: " + f4(ratio) + " > threshold " + f4(c.char_duplicates_ratio);
-        fail(s, s);
+        auto mk = [&] { return "char_dup_ratio: " + f4(ratio) + " > threshold " + f4(c.char_duplicates_ratio); };
+        fail(mk, mk);
         return;
       }
       const int64_t w = r[rec::FW_WORDS], nls = r[rec::FW_NL];
       if (w == 0) {
         if (nls > 0) {
-          std::string s = "list_ratio_no_words (newlines present but no words)";
-          fail(s, s);
+          auto mk = lit("list_ratio_no_words (newlines present but no words)");
+          fail(mk, mk);
         }
         return;
       }
       ratio = (double)nls / (double)w;
       if (ratio > c.new_line_ratio) {
-        std::string s = "list_ratio: " + f4(ratio) + " > threshold " + f4(c.new_line_ratio);
-        fail(s, s);
+        auto mk = [&] { return "list_ratio: " + f4(ratio) + " > threshold " + f4(c.new_line_ratio); };
+        fail(mk, mk);
       }
       return;
     }
@@ -396,26 +418,29 @@ void decide(const StepCfg& c, const int64_t* r, Decision& d) {
       const int64_t lang = r[rec::LD_LANG];
       if (lang < 0) {
         d.pass = false;
-        d.reason = "Language could not be confidently detected";
+        if constexpr (kFmt) d.reason = "Language could not be confidently detected";
         return;
       }
       double conf;
       std::memcpy(&conf, &r[rec::LD_CONF_BITS], sizeof(double));
-      d.meta.push_back({"Detected language", kLangNames[lang]});
-      d.meta.push_back({"Detected language confidence", fmt_f64(conf)});
+      meta("Detected language", [&] { return std::string(kLangNames[lang]); });
+      meta("Detected language confidence", [&] { return fmt_f64(conf); });
       bool allowed = std::find(c.allowed_langs.begin(), c.allowed_langs.end(), (int)lang) != c.allowed_langs.end();
       if (!allowed) {
-        std::string joined;
-        for (size_t i = 0; i < c.allowed_codes.size(); ++i) {
-          if (i) joined += "; ";
-          joined += c.allowed_codes[i];
-        }
         d.pass = false;
-        d.reason = "Document is not any of the following languages: " + fmt_debug_str(joined);
+        if constexpr (kFmt) {
+          std::string joined;
+          for (size_t i = 0; i < c.allowed_codes.size(); ++i) {
+            if (i) joined += "; ";
+            joined += c.allowed_codes[i];
+          }
+          d.reason = "Document is not any of the following languages: " + fmt_debug_str(joined);
+        }
       } else if (conf < c.min_confidence) {
         d.pass = false;
-        d.reason = "Language detection confidence is not satified: " + fmt_f64(conf) + " < " +
-                   fmt_f64(c.min_confidence);
+        if constexpr (kFmt)
+          d.reason = "Language detection confidence is not satified: " + fmt_f64(conf) + " < " +
+                     fmt_f64(c.min_confidence);
       }
       return;
     }
@@ -423,15 +448,23 @@ void decide(const StepCfg& c, const int64_t* r, Decision& d) {
       if (r[rec::TC_COUNT] < 0) {
         d.pass = false;
         d.error = true;
-        d.reason = "TokenCounter failed";
+        if constexpr (kFmt) d.reason = "TokenCounter failed";
         return;
       }
-      d.meta.push_back({"token_count", std::to_string(r[rec::TC_COUNT])});
+      meta("token_count", [&] { return std::to_string(r[rec::TC_COUNT]); });
       return;
     }
     case StepKind::C4BadWords:
       return;  // decided by the badwords module (needs per-document language strings)
   }
+}
+
+void decide(const StepCfg& c, const int64_t* r, Decision& d) { decide_t<true>(c, r, d); }
+
+uint8_t decide_status(const StepCfg& c, const int64_t* r) {
+  Decision d;
+  decide_t<false>(c, r, d);
+  return d.pass ? 0 : (d.error ? 2 : 1);
 }
 
 }  // namespace tb

@@ -97,14 +97,18 @@ enum BwStatus : int64_t {
 };
 
 // Outcome of one step on one document.
+// Metadata keys are string literals (static storage), values are formatted per document.
 struct Decision {
   bool pass = true;
   bool error = false;  // unrecoverable step error (no outcome, like the reference's None path)
   std::string reason;
-  std::vector<std::pair<std::string, std::string>> meta;  // in insertion order
+  std::vector<std::pair<std::string_view, std::string>> meta;  // in insertion order
 };
 
+// Full decision: pass/filtered/error + reason + metadata (formatting).
 void decide(const StepCfg& c, const int64_t* r, Decision& d);
+// Same branches without building any string: 0 pass, 1 filtered, 2 error.
+uint8_t decide_status(const StepCfg& c, const int64_t* r);
 
 // CPU computation of a step record on `text` (the step's input content version).
 // For C4Quality, `new_content` receives the rewritten content.

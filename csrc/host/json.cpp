@@ -87,7 +87,8 @@ void meta_set(MetaMap& m, const std::string& k, const std::string& v) {
   m.emplace_back(k, v);
 }
 
-bool parse_meta_json(std::string_view s, MetaMap& out) {
+template <class Map>
+static bool parse_into(std::string_view s, Map& out, std::string& k, std::string& v) {
   out.clear();
   Parser p{s};
   p.ws();
@@ -100,7 +101,8 @@ bool parse_meta_json(std::string_view s, MetaMap& out) {
     return p.i == s.size();
   }
   while (true) {
-    std::string k, v;
+    k.clear();
+    v.clear();
     p.ws();
     if (!p.str(k)) { out.clear(); return false; }
     p.ws();
@@ -108,7 +110,7 @@ bool parse_meta_json(std::string_view s, MetaMap& out) {
     ++p.i;
     p.ws();
     if (!p.str(v)) { out.clear(); return false; }
-    meta_set(out, k, v);
+    out.set(k, v);
     p.ws();
     if (p.i < s.size() && s[p.i] == ',') { ++p.i; continue; }
     if (p.i < s.size() && s[p.i] == '}') { ++p.i; break; }
@@ -120,10 +122,75 @@ bool parse_meta_json(std::string_view s, MetaMap& out) {
   return true;
 }
 
+namespace {
+struct MetaMapSink {
+  MetaMap& m;
+  void clear() { m.clear(); }
+  void set(const std::string& k, const std::string& v) { meta_set(m, k, v); }
+};
+}  // namespace
+
+bool parse_meta_json(std::string_view s, MetaMap& out) {
+  MetaMapSink sink{out};
+  std::string k, v;
+  return parse_into(s, sink, k, v);
+}
+
+bool parse_meta_json(std::string_view s, FlatMeta& out) {
+  thread_local std::string k, v;
+  return parse_into(s, out, k, v);
+}
+
+void FlatMeta::set(std::string_view k, std::string_view v) {
+  for (auto& x : e)
+    if (key(x) == k) {
+      x.vo = (uint32_t)arena.size();
+      x.vl = (uint32_t)v.size();
+      arena.append(v.data(), v.size());
+      return;
+    }
+  E x;
+  x.ko = (uint32_t)arena.size();
+  x.kl = (uint32_t)k.size();
+  arena.append(k.data(), k.size());
+  x.vo = (uint32_t)arena.size();
+  x.vl = (uint32_t)v.size();
+  arena.append(v.data(), v.size());
+  e.push_back(x);
+}
+
+void FlatMeta::append_json(std::string& out) const {
+  out.push_back('{');
+  for (size_t i = 0; i < e.size(); ++i) {
+    if (i) out.push_back(',');
+    json_escape_append(out, key(e[i]));
+    out.push_back(':');
+    json_escape_append(out, value(e[i]));
+  }
+  out.push_back('}');
+}
+
+std::string_view FlatMeta::get(std::string_view k) const {
+  for (auto& x : e)
+    if (key(x) == k) return value(x);
+  return std::string_view();
+}
+
+bool FlatMeta::has(std::string_view k) const {
+  for (auto& x : e)
+    if (key(x) == k) return true;
+  return false;
+}
+
 void json_escape_append(std::string& out, std::string_view s) {
   static const char* hex = "0123456789abcdef";
   out.push_back('"');
-  for (unsigned char c : s) {
+  size_t run = 0;  // start of the pending run of bytes that need no escaping
+  for (size_t i = 0; i < s.size(); ++i) {
+    const unsigned char c = (unsigned char)s[i];
+    if (c >= 0x20 && c != '"' && c != '\\') continue;
+    out.append(s.data() + run, i - run);
+    run = i + 1;
     switch (c) {
       case '"': out += "\\\""; break;
       case '\\': out += "\\\\"; break;
@@ -133,15 +200,12 @@ void json_escape_append(std::string& out, std::string_view s) {
       case '\b': out += "\\b"; break;
       case '\f': out += "\\f"; break;
       default:
-        if (c < 0x20) {
-          out += "\\u00";
-          out.push_back(hex[c >> 4]);
-          out.push_back(hex[c & 15]);
-        } else {
-          out.push_back((char)c);
-        }
+        out += "\\u00";
+        out.push_back(hex[c >> 4]);
+        out.push_back(hex[c & 15]);
     }
   }
+  out.append(s.data() + run, s.size() - run);
   out.push_back('"');
 }
 

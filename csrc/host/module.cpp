@@ -32,6 +32,17 @@ static py::array_t<uint8_t> str_to_numpy(std::string&& s) {
                               (const uint8_t*)heap->data(), owner);
 }
 
+static py::array_t<uint8_t> raw_to_numpy(RawBuf& b) {
+  auto* hold = new RawBuf(b);
+  b.p = nullptr;
+  py::capsule owner(hold, [](void* q) {
+    auto* r = reinterpret_cast<RawBuf*>(q);
+    RawBuf::release(r->p, r->cap);
+    delete r;
+  });
+  return py::array_t<uint8_t>({(py::ssize_t)hold->n}, {(py::ssize_t)1}, (const uint8_t*)hold->p, owner);
+}
+
 static SegBackend be_of(const std::string& s) {
   if (s == "icu") return SegBackend::Icu;
   if (s == "rules") return SegBackend::Rules;
@@ -359,6 +370,7 @@ PYBIND11_MODULE(_tbhost, m) {
                                py::array_t<int64_t, py::array::c_style> rec, int rewrite_version) {
         const int w = record_width(c);
         if ((int64_t)rec.size() != b.st->size() * w) throw std::invalid_argument("record array size");
+        b.keep.push_back(rec);  // records are read again at output assembly
         py::gil_scoped_release nogil;
         b.st->apply_records(c, step_index, rec.data(), w, rewrite_version);
       }, py::arg("step"), py::arg("step_index"), py::arg("records"), py::arg("rewrite_version") = -1)
@@ -388,14 +400,14 @@ PYBIND11_MODULE(_tbhost, m) {
       })
       .def("assemble", [](PyBatch& b, py::array_t<int64_t, py::array::c_style> idx) {
         std::vector<int64_t> iv(idx.data(), idx.data() + idx.size());
-        std::string td, md;
+        RawBuf td, md;
         std::vector<int64_t> to, mo;
         std::vector<uint8_t> mv;
         {
           py::gil_scoped_release nogil;
           b.st->assemble(iv, td, to, md, mo, mv);
         }
-        return py::make_tuple(str_to_numpy(std::move(td)), to_numpy(std::move(to)), str_to_numpy(std::move(md)),
+        return py::make_tuple(raw_to_numpy(td), to_numpy(std::move(to)), raw_to_numpy(md),
                               to_numpy(std::move(mo)), to_numpy(std::move(mv)));
       });
 
@@ -429,6 +441,7 @@ PYBIND11_MODULE(_tbhost, m) {
   });
   m.def("pow_table", [](uint32_t n) { return to_numpy(pow_table(n)); });
   m.def("scratch_bytes_for", [](uint32_t n) { return scratch_bytes_for(n); });
+  m.attr("C4_MAX_GROWTH") = kC4MaxGrowth;
   m.attr("SIZEOF_DEV_PLAN") = sizeof(DevPlan);
   m.attr("SIZEOF_DEV_STAGE") = sizeof(DevStage);
   m.attr("SIZEOF_DEV_C4") = sizeof(DevC4);

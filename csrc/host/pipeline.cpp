@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstring>
 #include <fstream>
+#include <mutex>
 #include <random>
 #include <sstream>
 
@@ -206,6 +207,56 @@ uint32_t StdRng::next_u32() {
 }
 
 // ------------------------------------------------------------------------------------------
+namespace {
+struct BufPool {
+  std::mutex mu;
+  std::vector<std::pair<char*, size_t>> free;  // (ptr, capacity)
+  static constexpr size_t kMin = 1 << 20;
+  static constexpr size_t kMaxFree = 8;
+};
+BufPool& buf_pool() {
+  static BufPool* p = new BufPool();  // leaked on purpose: numpy owners may outlive statics
+  return *p;
+}
+}  // namespace
+
+void RawBuf::alloc(size_t bytes) {
+  n = bytes;
+  if (bytes >= BufPool::kMin) {
+    BufPool& bp = buf_pool();
+    std::lock_guard<std::mutex> g(bp.mu);
+    int best = -1;
+    for (int i = 0; i < (int)bp.free.size(); ++i)
+      if (bp.free[i].second >= bytes && (best < 0 || bp.free[i].second < bp.free[best].second)) best = i;
+    if (best >= 0) {
+      p = bp.free[best].first;
+      cap = bp.free[best].second;
+      bp.free.erase(bp.free.begin() + best);
+      return;
+    }
+  }
+  cap = bytes < BufPool::kMin ? std::max<size_t>(bytes, 1) : bytes + bytes / 8;  // headroom for reuse
+  p = new char[cap];
+}
+
+void RawBuf::release(char* p, size_t cap) {
+  if (!p) return;
+  if (cap >= BufPool::kMin) {
+    BufPool& bp = buf_pool();
+    std::lock_guard<std::mutex> g(bp.mu);
+    if (bp.free.size() < BufPool::kMaxFree) {
+      bp.free.emplace_back(p, cap);
+      return;
+    }
+    // pool full: drop the smallest buffer (keep large ones: they serve every batch size)
+    int small = 0;
+    for (int i = 1; i < (int)bp.free.size(); ++i)
+      if (bp.free[i].second < bp.free[small].second) small = i;
+    if (bp.free[small].second < cap) std::swap(bp.free[small].first, p), std::swap(bp.free[small].second, cap);
+  }
+  delete[] p;
+}
+
 BatchState::BatchState(int64_t n, const char* data, const int64_t* off, const char* meta_data,
                        const int64_t* meta_off, const uint8_t* meta_valid, int nthreads)
     : n_(n), nthreads_(std::max(1, nthreads)) {
@@ -215,24 +266,10 @@ BatchState::BatchState(int64_t n, const char* data, const int64_t* off, const ch
   cur_version_.assign(n, 0);
   fail_step_.assign(n, -1);
   status_.assign(n, 0);
-  reason_.resize(n);
-  in_meta_.resize(n);
-  in_meta_valid_.assign(n, 0);
-  add_meta_.resize(n);
-  own_content_.resize(n);
   if (meta_data && meta_off) {
-    std::atomic<int64_t> fails{0};
-    parallel_for(n, nthreads_, [&](int64_t a, int64_t b) {
-      int64_t f = 0;
-      for (int64_t i = a; i < b; ++i) {
-        if (meta_valid && !meta_valid[i]) continue;
-        std::string_view js(meta_data + meta_off[i], (size_t)(meta_off[i + 1] - meta_off[i]));
-        if (!parse_meta_json(js, in_meta_[i])) ++f;
-        in_meta_valid_[i] = 1;
-      }
-      fails += f;
-    });
-    meta_fail_ = fails.load();
+    meta_data_ = meta_data;
+    meta_off_ = meta_off;
+    meta_valid_ = meta_valid;
   }
 }
 
@@ -260,47 +297,66 @@ int BatchState::add_owned_version(std::string&& data, std::vector<int64_t>&& off
   return (int)versions_.size() - 1;
 }
 
-void BatchState::apply_decision(int64_t doc, int step_index, Decision& d) {
-  for (auto& kv : d.meta) meta_set(add_meta_[doc], kv.first, kv.second);
-  if (!d.pass) {
+BatchState::StepRec& BatchState::step_slot(int step_index) {
+  if ((int)recs_.size() <= step_index) recs_.resize(step_index + 1);
+  if ((int)bw_.size() <= step_index) bw_.resize(step_index + 1);
+  n_applied_ = std::max(n_applied_, step_index + 1);
+  return recs_[step_index];
+}
+
+void BatchState::set_status(int64_t doc, int step_index, uint8_t st) {
+  if (st) {
     fail_step_[doc] = step_index;
-    status_[doc] = d.error ? 2 : 1;
-    reason_[doc] = std::move(d.reason);
+    status_[doc] = st;
   }
+}
+
+bool BatchState::input_meta(int64_t i, FlatMeta& out) const {
+  out.clear();
+  if (!meta_data_ || (meta_valid_ && !meta_valid_[i])) return false;
+  std::string_view js(meta_data_ + meta_off_[i], (size_t)(meta_off_[i + 1] - meta_off_[i]));
+  return parse_meta_json(js, out);
 }
 
 void BatchState::apply_records(const StepCfg& cfg, int step_index, const int64_t* rec, int width,
                                int rewrite_version) {
+  StepRec& sr = step_slot(step_index);
+  sr.cfg = std::make_unique<StepCfg>(cfg);
+  sr.rec = rec;
+  sr.width = width;
+  const bool c4_rewrite = cfg.kind == StepKind::C4Quality && rewrite_version >= 0;
   parallel_for(n_, nthreads_, [&](int64_t a, int64_t b) {
-    Decision d;
     for (int64_t i = a; i < b; ++i) {
       if (fail_step_[i] >= 0) continue;
       const int64_t* r = rec + i * width;
-      decide(cfg, r, d);
-      if (cfg.kind == StepKind::C4Quality && rewrite_version >= 0 && !r[rec::C4_LOREM] &&
-          !r[rec::C4_CURLY])
-        cur_version_[i] = rewrite_version;
-      apply_decision(i, step_index, d);
+      if (c4_rewrite && !r[rec::C4_LOREM] && !r[rec::C4_CURLY]) cur_version_[i] = rewrite_version;
+      set_status(i, step_index, decide_status(cfg, r));
     }
   });
 }
 
 void BatchState::apply_badwords(const StepCfg& cfg, int step_index, BadWordsModule& mod) {
-  // Language lists are loaded lazily on the calling thread, then matching runs in parallel.
+  step_slot(step_index);
+  auto out = std::make_unique<BwOut>();
+  out->code.assign(n_, -1);
+  out->lang.resize(n_);
+  // The document language: metadata "language" (no step writes that key, so only the input
+  // metadata can hold it), else the configured default (reference c4_filters.rs:478-486).
   std::vector<std::string> lang(n_);
+  parallel_for(n_, nthreads_, [&](int64_t a, int64_t b) {
+    FlatMeta fm;
+    for (int64_t i = a; i < b; ++i) {
+      if (fail_step_[i] >= 0) continue;
+      lang[i] = cfg.default_language;
+      if (input_meta(i, fm) && fm.has("language")) lang[i] = std::string(fm.get("language"));
+    }
+  });
+  // lists load lazily on this thread, then matching runs in parallel
   for (int64_t i = 0; i < n_; ++i) {
     if (fail_step_[i] >= 0) continue;
-    std::string l = cfg.default_language;
-    const MetaMap& m = add_meta_[i];
-    bool found = false;
-    for (auto& kv : m) if (kv.first == "language") { l = kv.second; found = true; }
-    if (!found)
-      for (auto& kv : in_meta_[i]) if (kv.first == "language") { l = kv.second; found = true; }
-    lang[i] = l;
     bool sup;
-    mod.get(l, &sup);
+    mod.get(lang[i], &sup);
   }
-  // matching in parallel, then keep-fraction draws in document order from the shared stream
   std::vector<int8_t> matched(n_, -1);  // -1 n/a, 0 no match, 1 match
   parallel_for(n_, nthreads_, [&](int64_t a, int64_t b) {
     for (int64_t i = a; i < b; ++i) {
@@ -313,37 +369,27 @@ void BatchState::apply_badwords(const StepCfg& cfg, int step_index, BadWordsModu
     uint64_t seed = cfg.seed ? *cfg.seed : (((uint64_t)std::random_device{}() << 32) ^ std::random_device{}());
     mod.rng = std::make_unique<StdRng>(seed);
   }
+  // keep-fraction draws from the shared stream, in document order
   for (int64_t i = 0; i < n_; ++i) {
     if (fail_step_[i] >= 0) continue;
-    Decision d;
     bool sup = false;
     for (auto l : kBadwordsLangs) if (lang[i] == l) sup = true;
+    int8_t code;
     if (!sup) {
-      if (cfg.fail_on_missing_language) {
-        d.pass = false;
-        d.reason = "There is no badwords list available for '" + lang[i] +
-                   "'. Set fail_on_missing_language=False to continue anyway.";
-        d.meta.push_back({"c4_badwords_filter_status", "filtered"});
-        d.meta.push_back({"c4_badwords_filter_reason", d.reason});
-      } else {
-        d.meta.push_back({"c4_badwords_filter_status", "passed_no_regex"});
-      }
+      code = cfg.fail_on_missing_language ? BW_MISSING_LANG_FAIL : BW_NO_REGEX;
+      if (code == BW_MISSING_LANG_FAIL) out->lang[i] = lang[i];
     } else if (matched[i] < 0) {
-      d.meta.push_back({"c4_badwords_filter_status", "passed_no_regex"});
+      code = BW_NO_REGEX;
     } else if (matched[i] == 1) {
-      if (cfg.keep_fraction > 0.0 && mod.rng->gen_f32() < (float)cfg.keep_fraction) {
-        d.meta.push_back({"c4_badwords_filter_status", "passed_kept_by_fraction"});
-      } else {
-        d.pass = false;
-        d.reason = "document_removed_with_badwords";
-        d.meta.push_back({"c4_badwords_filter_status", "filtered"});
-        d.meta.push_back({"c4_badwords_filter_reason", d.reason});
-      }
+      code = (cfg.keep_fraction > 0.0 && mod.rng->gen_f32() < (float)cfg.keep_fraction) ? BW_KEPT_BY_FRACTION
+                                                                                          : BW_FILTERED;
     } else {
-      d.meta.push_back({"c4_badwords_filter_status", "passed"});
+      code = BW_PASSED;
     }
-    apply_decision(i, step_index, d);
+    out->code[i] = code;
+    set_status(i, step_index, (code == BW_FILTERED || code == BW_MISSING_LANG_FAIL) ? 1 : 0);
   }
+  bw_[step_index] = std::move(out);
 }
 
 void BatchState::run_cpu(const std::vector<StepCfg>& steps, int begin, int end, SegBackend be,
@@ -360,27 +406,30 @@ void BatchState::run_cpu(const std::vector<StepCfg>& steps, int begin, int end, 
     if (cfg.kind == StepKind::LanguageDetection && !lid)
       throw std::runtime_error("LanguageDetectionFilter requires a language-id model");
     const int width = record_width(cfg);
+    StepRec& sr = step_slot(s);
+    sr.cfg = std::make_unique<StepCfg>(cfg);
+    sr.width = width;
+    sr.own.assign((size_t)n_ * width, 0);
+    sr.rec = sr.own.data();
+    if (cfg.kind == StepKind::C4Quality && own_content_.empty()) own_content_.resize(n_);
     parallel_for(n_, nthreads_, [&](int64_t a, int64_t b) {
-      std::vector<int64_t> r(width);
-      Decision d;
       std::string nc;
       for (int64_t i = a; i < b; ++i) {
         if (fail_step_[i] >= 0) continue;
         std::string_view text = content(i);
-        std::fill(r.begin(), r.end(), 0);
+        int64_t* r = sr.own.data() + i * width;
         if (cfg.kind == StepKind::LanguageDetection) {
           double conf = 0;
           r[rec::LD_LANG] = lid->detect(text, &conf);
           std::memcpy(&r[rec::LD_CONF_BITS], &conf, sizeof(double));
         } else {
-          compute_record(cfg, text, be, r.data(), &nc);
+          compute_record(cfg, text, be, r, &nc);
         }
-        decide(cfg, r.data(), d);
         if (cfg.kind == StepKind::C4Quality && !r[rec::C4_LOREM] && !r[rec::C4_CURLY]) {
           own_content_[i] = std::move(nc);
           cur_version_[i] = -1;
         }
-        apply_decision(i, s, d);
+        set_status(i, s, decide_status(cfg, r));
       }
     });
   }
@@ -401,36 +450,97 @@ std::vector<int64_t> BatchState::alive_indices() const {
   return out;
 }
 
-void BatchState::assemble(const std::vector<int64_t>& idx, std::string& text_data,
-                          std::vector<int64_t>& text_off, std::string& meta_data,
-                          std::vector<int64_t>& meta_off, std::vector<uint8_t>& meta_valid) const {
+void BatchState::step_meta(int64_t doc, int s, Decision& d) const {
+  d.pass = true;
+  d.error = false;
+  d.reason.clear();
+  d.meta.clear();
+  if (s < (int)bw_.size() && bw_[s]) {
+    const BwOut& b = *bw_[s];
+    switch (b.code[doc]) {
+      case BW_PASSED: d.meta.emplace_back("c4_badwords_filter_status", "passed"); break;
+      case BW_NO_REGEX: d.meta.emplace_back("c4_badwords_filter_status", "passed_no_regex"); break;
+      case BW_KEPT_BY_FRACTION: d.meta.emplace_back("c4_badwords_filter_status", "passed_kept_by_fraction"); break;
+      case BW_FILTERED:
+        d.pass = false;
+        d.reason = "document_removed_with_badwords";
+        d.meta.emplace_back("c4_badwords_filter_status", "filtered");
+        d.meta.emplace_back("c4_badwords_filter_reason", d.reason);
+        break;
+      case BW_MISSING_LANG_FAIL:
+        d.pass = false;
+        d.reason = "There is no badwords list available for '" + b.lang[doc] +
+                   "'. Set fail_on_missing_language=False to continue anyway.";
+        d.meta.emplace_back("c4_badwords_filter_status", "filtered");
+        d.meta.emplace_back("c4_badwords_filter_reason", d.reason);
+        break;
+      default: break;
+    }
+    return;
+  }
+  if (s >= (int)recs_.size() || !recs_[s].cfg) return;
+  const StepRec& sr = recs_[s];
+  decide(*sr.cfg, sr.rec + doc * sr.width, d);
+}
+
+std::string BatchState::reason(int64_t i) const {
+  const int s = fail_step_[i];
+  if (s < 0 || s >= n_applied_) return std::string();
+  Decision d;
+  step_meta(i, s, d);
+  return d.reason;
+}
+
+void BatchState::assemble(const std::vector<int64_t>& idx, RawBuf& text_data, std::vector<int64_t>& text_off,
+                          RawBuf& meta_data, std::vector<int64_t>& meta_off,
+                          std::vector<uint8_t>& meta_valid) const {
   const int64_t m = (int64_t)idx.size();
-  const int nchunks = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads_ * 4, m / 256));
-  std::vector<std::string> tparts(nchunks), mparts(nchunks);
-  std::vector<std::vector<int64_t>> tlen(nchunks), mlen(nchunks);
+  // text: sizes are known up front -> offsets, then one parallel gather into the final buffer
+  text_off.assign(m + 1, 0);
+  for (int64_t k = 0; k < m; ++k) {
+    const int64_t i = idx[k];
+    int64_t len;
+    const int v = cur_version_[i];
+    if (v < 0) len = (int64_t)own_content_[i].size();
+    else len = versions_[v].off[i + 1] - versions_[v].off[i];
+    text_off[k + 1] = text_off[k] + len;
+  }
+  text_data.alloc((size_t)text_off[m]);
+  // metadata: formatted per chunk (sizes unknown), then concatenated
+  const int nchunks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)nthreads_ * 4, m / 256));
+  std::vector<std::string> mparts(nchunks);
+  meta_off.assign(m + 1, 0);
   meta_valid.assign(m, 0);
   std::atomic<int> next{0};
   auto worker = [&]() {
+    FlatMeta fm;
+    Decision d;
     while (true) {
-      int c = next.fetch_add(1);
+      const int c = next.fetch_add(1);
       if (c >= nchunks) break;
-      int64_t a = m * c / nchunks, b = m * (c + 1) / nchunks;
-      std::string& td = tparts[c];
+      const int64_t a = m * c / nchunks, b = m * (c + 1) / nchunks;
       std::string& md = mparts[c];
-      MetaMap merged;
+      md.reserve((size_t)(b - a) * 192);
       for (int64_t k = a; k < b; ++k) {
-        int64_t i = idx[k];
+        const int64_t i = idx[k];
         std::string_view t = content(i);
-        td.append(t.data(), t.size());
-        tlen[c].push_back((int64_t)t.size());
-        merged = in_meta_[i];
-        for (auto& kv : add_meta_[i]) meta_set(merged, kv.first, kv.second);
-        if (merged.empty()) {
-          mlen[c].push_back(0);
+        if (!t.empty()) std::memcpy(text_data.p + text_off[k], t.data(), t.size());
+        if (meta_data_ && (!meta_valid_ || meta_valid_[i])) {
+          if (!input_meta(i, fm)) meta_fail_.fetch_add(1, std::memory_order_relaxed);
         } else {
-          size_t before = md.size();
-          serialize_meta_json(merged, md);
-          mlen[c].push_back((int64_t)(md.size() - before));
+          fm.clear();
+        }
+        const int last = status_[i] == 0 ? n_applied_ - 1 : std::min(fail_step_[i], n_applied_ - 1);
+        for (int s = 0; s <= last; ++s) {
+          step_meta(i, s, d);
+          for (auto& kv : d.meta) fm.set(kv.first, kv.second);
+        }
+        if (fm.empty()) {
+          meta_off[k + 1] = 0;  // length; prefix-summed below
+        } else {
+          const size_t before = md.size();
+          fm.append_json(md);
+          meta_off[k + 1] = (int64_t)(md.size() - before);
           meta_valid[k] = 1;
         }
       }
@@ -440,23 +550,14 @@ void BatchState::assemble(const std::vector<int64_t>& idx, std::string& text_dat
   for (int t = 1; t < std::min(nthreads_, nchunks); ++t) ts.emplace_back(worker);
   worker();
   for (auto& t : ts) t.join();
-  text_off.assign(m + 1, 0);
-  meta_off.assign(m + 1, 0);
-  size_t tt = 0, mt = 0;
-  for (int c = 0; c < nchunks; ++c) { tt += tparts[c].size(); mt += mparts[c].size(); }
-  text_data.clear();
-  text_data.reserve(tt);
-  meta_data.clear();
-  meta_data.reserve(mt);
-  int64_t k = 0;
-  for (int c = 0; c < nchunks; ++c) {
-    text_data += tparts[c];
-    meta_data += mparts[c];
-    for (size_t j = 0; j < tlen[c].size(); ++j, ++k) {
-      text_off[k + 1] = text_off[k] + tlen[c][j];
-      meta_off[k + 1] = meta_off[k] + mlen[c][j];
-    }
-  }
+  for (int64_t k = 0; k < m; ++k) meta_off[k + 1] += meta_off[k];
+  meta_data.alloc((size_t)meta_off[m]);
+  std::vector<size_t> base(nchunks + 1, 0);
+  for (int c = 0; c < nchunks; ++c) base[c + 1] = base[c] + mparts[c].size();
+  parallel_for(nchunks, std::min(nthreads_, nchunks), [&](int64_t a, int64_t b) {
+    for (int64_t c = a; c < b; ++c)
+      if (!mparts[c].empty()) std::memcpy(meta_data.p + base[c], mparts[c].data(), mparts[c].size());
+  });
 }
 
 }  // namespace tb

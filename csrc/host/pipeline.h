@@ -67,6 +67,24 @@ struct Version {
   std::vector<int64_t> own_off;
 };
 
+// Output column buffer handed to Python without a copy. Large buffers come from a small
+// recycling pool (released by the numpy owner), so steady-state batches reuse already-faulted
+// pages instead of paying mmap + first-touch faults + munmap for ~100 MB per batch.
+struct RawBuf {
+  char* p = nullptr;
+  size_t n = 0;
+  size_t cap = 0;
+  void alloc(size_t bytes);
+  static void release(char* p, size_t cap);
+};
+
+// Per-batch resolver. Hot-path design (one batch = up to ~1e5 documents):
+//   * applying a step only derives each alive document's status from its record
+//     (decide_status: no strings), records stay where they were produced (device D2H buffers
+//     or owned CPU-path arrays);
+//   * reasons and metadata are formatted once, at output assembly, by re-running the shared
+//     decision code over the records of the steps each document executed;
+//   * no per-document heap objects survive a step, so building and dropping a batch is cheap.
 class BatchState {
  public:
   BatchState(int64_t n, const char* data, const int64_t* off, const char* meta_data,
@@ -78,8 +96,9 @@ class BatchState {
   int add_version(const char* data, const int64_t* off);  // borrowed buffers
   int add_owned_version(std::string&& data, std::vector<int64_t>&& off);
 
-  // Apply a step whose per-document records were computed elsewhere (GPU or CPU runner).
-  // For C4 steps `rewrite_version` is the version holding the rewritten contents.
+  // Apply a step whose per-document records were computed elsewhere (GPU, host tokenizer).
+  // `rec` is borrowed and must outlive the batch. For C4 steps `rewrite_version` is the
+  // version holding the rewritten contents.
   void apply_records(const StepCfg& cfg, int step_index, const int64_t* rec, int width,
                      int rewrite_version);
   // CPU path: compute records for alive docs and apply them for steps [begin, end).
@@ -91,31 +110,46 @@ class BatchState {
   void delegate(const int64_t* idx, int64_t n);
   std::vector<int64_t> alive_indices() const;
   const std::vector<int32_t>& fail_step() const { return fail_step_; }
-  const std::vector<uint8_t>& status() const { return status_; }  // 0 ok, 1 filtered, 2 error
+  const std::vector<uint8_t>& status() const { return status_; }  // 0 ok, 1 filtered, 2 error, 3 delegated
   const std::vector<int32_t>& cur_version() const { return cur_version_; }
-  const std::string& reason(int64_t i) const { return reason_[i]; }
+  std::string reason(int64_t i) const;
 
   // Output assembly for a subset of documents (indices): contents and metadata JSON.
-  void assemble(const std::vector<int64_t>& idx, std::string& text_data, std::vector<int64_t>& text_off,
-                std::string& meta_data, std::vector<int64_t>& meta_off, std::vector<uint8_t>& meta_valid) const;
-  int64_t meta_parse_failures() const { return meta_fail_; }
+  void assemble(const std::vector<int64_t>& idx, RawBuf& text_data, std::vector<int64_t>& text_off,
+                RawBuf& meta_data, std::vector<int64_t>& meta_off, std::vector<uint8_t>& meta_valid) const;
+  int64_t meta_parse_failures() const { return meta_fail_.load(); }
 
  private:
-  void apply_decision(int64_t doc, int step_index, Decision& d);
-  const MetaMap& input_meta(int64_t i) const { return in_meta_[i]; }
+  struct StepRec {
+    std::unique_ptr<StepCfg> cfg;  // own copy: callers may pass temporaries
+    const int64_t* rec = nullptr;
+    int width = 0;
+    std::vector<int64_t> own;
+  };
+  // C4BadWordsFilter outcome per document (decided with the shared RNG stream in doc order).
+  struct BwOut {
+    std::vector<int8_t> code;           // BwStatus or -1 (not executed)
+    std::vector<std::string> lang;      // only for BW_MISSING_LANG_FAIL reasons
+  };
+  StepRec& step_slot(int step_index);
+  void set_status(int64_t doc, int step_index, uint8_t st);
+  bool input_meta(int64_t i, FlatMeta& out) const;
+  void step_meta(int64_t doc, int s, Decision& d) const;  // metadata of step s for doc
 
   int64_t n_;
   int nthreads_;
+  int n_applied_ = 0;  // steps [0, n_applied_) have been applied (in order)
   std::vector<Version> versions_;
   std::vector<int32_t> cur_version_;
   std::vector<int32_t> fail_step_;
   std::vector<uint8_t> status_;
-  std::vector<std::string> reason_;
-  std::vector<MetaMap> in_meta_;
-  std::vector<uint8_t> in_meta_valid_;
-  std::vector<MetaMap> add_meta_;
-  std::vector<std::string> own_content_;  // CPU path rewritten contents (cur_version == -1)
-  int64_t meta_fail_ = 0;
+  const char* meta_data_ = nullptr;
+  const int64_t* meta_off_ = nullptr;
+  const uint8_t* meta_valid_ = nullptr;
+  std::vector<StepRec> recs_;                 // by step index
+  std::vector<std::unique_ptr<BwOut>> bw_;    // by step index (nullptr unless bad-words step)
+  std::vector<std::string> own_content_;      // CPU path rewritten contents (cur_version == -1)
+  mutable std::atomic<int64_t> meta_fail_{0};
 };
 
 }  // namespace tb

@@ -1,0 +1,56 @@
+"""The GPU backend's resolve path (records -> statuses -> lazily formatted metadata), driven by
+the host port of the device kernels (``backend="emulate"``), must produce exactly the CPU ICU
+oracle's outputs. Runs without a GPU."""
+import numpy as np
+import pytest
+
+from textblaster_amd.config import load_pipeline_config
+from textblaster_amd.pipeline.engine import Engine
+from textblaster_amd.utils import synth
+
+EDGE = ["", "   ", "\n\n", "a", "a\r\nb\r\n", "Hello.\n\n\nHello.\n\nHello.", "x [1] y [2, 3]. z",
+        "ΣΑΣ ΣΑΣ.", "İstanbul THE the", "cooKie policy is here.", "lorem IPSUM dolor", "{ curly }",
+        "日本語のテキストです。", "mixed 日本 text. Another sentence here.", "- bullet\n- bullet\n• x...",
+        "Hi?There!Again.Yes" * 3]
+
+
+def outputs(res):
+    out = {}
+    for kind, parts in (("kept", res.kept), ("excluded", res.excluded)):
+        for p in parts:
+            for k, r in enumerate(p.rows):
+                t = bytes(p.text_data[p.text_off[k]:p.text_off[k + 1]])
+                m = bytes(p.meta_data[p.meta_off[k]:p.meta_off[k + 1]]) if p.meta_valid[k] else None
+                out[int(r)] = (kind, t, m)
+    return out
+
+
+@pytest.mark.parametrize("cfg_path", ["config/bench_pipeline.yaml", "tests/config/test_pipeline_config.yaml"])
+def test_emulated_device_path_equals_cpu_oracle(cfg_path):
+    cfg = load_pipeline_config(cfg_path)
+    texts = synth.make_corpus(1500, 900, seed=17) + EDGE
+    data, off = synth.pack(texts)
+    meta = [b'{"src":"x"}' if i % 3 == 0 else b"" for i in range(len(texts))]
+    md = np.frombuffer(b"".join(meta), np.uint8).copy()
+    mo = np.zeros(len(meta) + 1, np.int64)
+    np.cumsum([len(m) for m in meta], out=mo[1:])
+    mv = np.array([1 if m else 0 for m in meta], np.uint8)
+    a = Engine(cfg, backend="emulate", nthreads=4, keep_reasons=True).process(data, off, (md, mo, mv))
+    b = Engine(cfg, backend="cpu", segmentation="icu", nthreads=4, keep_reasons=True).process(data, off, (md, mo, mv))
+    assert (a.n_kept, a.n_excluded) == (b.n_kept, b.n_excluded)
+    np.testing.assert_array_equal(a.status, b.status)
+    np.testing.assert_array_equal(a.fail_step, b.fail_step)
+    assert a.reasons == b.reasons
+    oa, ob = outputs(a), outputs(b)
+    assert oa.keys() == ob.keys()
+    diff = [k for k in oa if oa[k] != ob[k]]
+    assert not diff, (diff[:3], [oa[k] for k in diff[:1]], [ob[k] for k in diff[:1]])
+
+
+def test_pipelined_equals_sequential():
+    cfg = load_pipeline_config("config/bench_pipeline.yaml")
+    eng = Engine(cfg, backend="emulate", nthreads=4)
+    batches = [synth.pack(synth.make_corpus(300, 700, seed=s)) for s in range(4)]
+    seq = [outputs(eng.process(d, o)) for d, o in batches]
+    pip = [outputs(r) for r in eng.process_many(batches)]
+    assert seq == pip

@@ -39,7 +39,54 @@ class DeviceResult:
     timings: Dict[str, float]
 
 
+class _Slot:
+    """Per in-flight batch resources: pinned input staging buffer and device scratch arena.
+    Two slots alternate, so batch k+1 can be staged and launched while batch k's results are
+    still being resolved on the host."""
+
+    def __init__(self):
+        self.pinned = None
+        self.scratch = None
+        self.h2d_done = None  # event: the pinned staging buffer may be rewritten after it
+
+
+class PendingBatch:
+    """A submitted batch: kernels and D2H copies are queued on the stream; ``wait()`` blocks on
+    the completion event and returns host views of the results."""
+
+    def __init__(self, runner, ndocs, event, stage_recs, c4_recs, versions, flags, t_submit, keep):
+        self.runner = runner
+        self.ndocs = ndocs
+        self.event = event
+        self._stage_recs = stage_recs
+        self._c4_recs = c4_recs
+        self._versions = versions
+        self._flags = flags
+        self._t_submit = t_submit
+        self._keep = keep  # device tensors that must stay alive until the event completes
+
+    def wait(self) -> DeviceResult:
+        import time
+
+        t0 = time.perf_counter()
+        self.event.synchronize()
+        t1 = time.perf_counter()
+        stage_recs = [r.numpy() if r is not None else None for r in self._stage_recs]
+        c4_recs = {i: r.numpy() for i, r in self._c4_recs.items()}
+        host_versions = {}
+        for ver, (vb, vo) in self._versions.items():
+            o = vo.numpy()
+            host_versions[ver] = (vb.numpy()[: int(o[-1])], o)
+        fl = self._flags.numpy().view(np.uint32)
+        self._keep = None
+        timings = dict(self._t_submit)
+        timings["gpu_wait"] = t1 - t0
+        return DeviceResult(stage_recs, c4_recs, host_versions, fl, timings)
+
+
 class DeviceRunner:
+    N_SLOTS = 2
+
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None):
         import torch
 
@@ -64,40 +111,64 @@ class DeviceRunner:
             wT = np.ascontiguousarray(langid.w.reshape(h.LID_DIM, h.LID_LANGS_PAD).T)  # [16][32]
             self.lid_wT = torch.from_numpy(wT).to(self.device)
             self.lid_b = torch.from_numpy(langid.b.astype(np.float32)).to(self.device)
-        self._scratch = None
-        self._pinned = None
+        self.c4_growth = int(h.C4_MAX_GROWTH)
+        self.slots = [_Slot() for _ in range(self.N_SLOTS)]
+        self._next_slot = 0
         self._last_lid = None
 
     def _to_dev(self, b: bytes):
         t = self.torch.frombuffer(bytearray(b), dtype=self.torch.uint8)
         return t.to(self.device)
 
-    def _scratch_for(self, nbytes: int):
-        if self._scratch is None or self._scratch.numel() < nbytes:
-            self._scratch = None
-            self._scratch = self.torch.empty(int(nbytes * 1.25) + (1 << 20), dtype=self.torch.uint8,
-                                             device=self.device)
-        return self._scratch
+    def _pinned(self, nbytes: int, dtype):
+        t = self.torch.empty(max(nbytes, 8), dtype=self.torch.uint8, pin_memory=True)
+        return t[:nbytes].view(dtype) if nbytes else t[:0].view(dtype)
 
-    def _h2d(self, arr: np.ndarray):
-        # staged through a pinned host buffer so the copy is a DMA (and numpy read-only views
-        # of Arrow buffers are never handed to torch directly)
-        arr = np.ascontiguousarray(arr)
-        nb = arr.nbytes
-        if self._pinned is None or self._pinned.numel() < nb:
-            self._pinned = self.torch.empty(max(nb, 1 << 20) * 2, dtype=self.torch.uint8, pin_memory=True)
-        host = self._pinned[:nb]
-        host.numpy()[:] = arr.view(np.uint8).reshape(-1)
-        dev = self.torch.empty(nb, dtype=self.torch.uint8, device=self.device)
-        dev.copy_(host, non_blocking=False)
-        return dev.view(_TORCH_DTYPES[arr.dtype.str]) if nb else dev
+    def _stage_inputs(self, slot: _Slot, arrays):
+        """One H2D transfer for all per-batch inputs: arrays are packed at 256-byte aligned
+        offsets into the slot's pinned buffer, copied with one DMA, and returned as typed views
+        of the device buffer."""
+        torch = self.torch
+        offs, total = [], 0
+        for a in arrays:
+            offs.append(total)
+            total += (a.nbytes + SCRATCH_ALIGN - 1) // SCRATCH_ALIGN * SCRATCH_ALIGN
+        total = max(total, SCRATCH_ALIGN)
+        if slot.h2d_done is not None:
+            slot.h2d_done.synchronize()  # the previous DMA out of this buffer has finished
+        if slot.pinned is None or slot.pinned.numel() < total:
+            slot.pinned = torch.empty(int(total * 1.25), dtype=torch.uint8, pin_memory=True)
+        hv = slot.pinned.numpy()
+        for a, o in zip(arrays, offs):
+            if a.nbytes:
+                hv[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+        dev = torch.empty(total, dtype=torch.uint8, device=self.device)
+        dev.copy_(slot.pinned[:total], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        slot.h2d_done = ev
+        out = []
+        for a, o in zip(arrays, offs):
+            dt = _TORCH_DTYPES[np.dtype(a.dtype).str]
+            out.append(dev[o:o + a.nbytes].view(dt) if a.nbytes else dev[o:o].view(dt))
+        return out, dev
 
-    def run(self, data: np.ndarray, off: np.ndarray) -> DeviceResult:
+    def _scratch_for(self, slot: _Slot, nbytes: int):
+        if slot.scratch is None or slot.scratch.numel() < nbytes:
+            slot.scratch = None
+            slot.scratch = self.torch.empty(int(nbytes * 1.25) + (1 << 20), dtype=self.torch.uint8,
+                                            device=self.device)
+        return slot.scratch
+
+    def submit(self, data: np.ndarray, off: np.ndarray) -> PendingBatch:
+        """Stage inputs, enqueue every device stage and the D2H copies; returns immediately."""
         import time
 
         torch = self.torch
         h = native.host()
         t0 = time.perf_counter()
+        slot = self.slots[self._next_slot]
+        self._next_slot = (self._next_slot + 1) % self.N_SLOTS
         ndocs = len(off) - 1
         lens = np.diff(off)
         perm = np.argsort(-lens, kind="stable").astype(np.int32)
@@ -105,18 +176,17 @@ class DeviceRunner:
         per_doc = (per_doc + SCRATCH_ALIGN - 1) // SCRATCH_ALIGN * SCRATCH_ALIGN
         scratch_off = np.zeros(ndocs + 1, dtype=np.int64)
         np.cumsum(per_doc, out=scratch_off[1:])
-        scratch = self._scratch_for(int(scratch_off[-1]))
         maxlen = int(lens.max()) if ndocs else 0
+        (d_bytes, d_off, d_perm, d_soff), staged = self._stage_inputs(
+            slot, [data if len(data) else np.zeros(1, np.uint8), off, perm, scratch_off])
+        scratch = self._scratch_for(slot, int(scratch_off[-1]))
         pw, pw_n = self.k.pow_table(2 * maxlen + 64)
-        d_bytes = self._h2d(data if len(data) else np.zeros(1, np.uint8))
-        d_off = self._h2d(off)
-        d_perm = self._h2d(perm)
-        d_soff = self._h2d(scratch_off)
         flags = torch.zeros(ndocs, dtype=torch.int32, device=self.device)
         t1 = time.perf_counter()
         versions = {0: (d_bytes, d_off, len(data))}
-        stage_recs_d = []
+        stage_recs_d: List = [None] * len(self.plan.stages)
         c4_recs_d = {}
+        keep = [staged, scratch]
         for ver in range(self.plan.n_versions):
             vb, vo, vlen = versions[ver]
             for s, sv in enumerate(self.plan.stage_version):
@@ -135,7 +205,7 @@ class DeviceRunner:
                 for kind, width, prefix in layout:
                     if kind == 4:
                         self.k.langid_head(lid_vec, lid_cnt, self.lid_wT, self.lid_b, ndocs, rec, prefix * ndocs, width)
-                stage_recs_d.append((s, rec))
+                stage_recs_d[s] = rec
             c4_here = [i for i in self.plan.c4_steps if self.plan.steps[i].version_in == ver]
             for i in c4_here:
                 rec = torch.zeros(7 * ndocs, dtype=torch.int64, device=self.device)
@@ -143,23 +213,73 @@ class DeviceRunner:
                 self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm, ndocs, scratch, d_soff, pw, pw_n, rec, src, flags)
                 new_off = torch.zeros(ndocs + 1, dtype=torch.int64, device=self.device)
                 torch.cumsum(src.view(ndocs, 2)[:, 1], 0, out=new_off[1:])
-                cap = 2 * vlen + ndocs + 16
+                cap = vlen + self.c4_growth * ndocs + 16  # device rewrites never grow more (kC4MaxGrowth)
                 out = torch.empty(cap, dtype=torch.uint8, device=self.device)
                 self.k.c4_pass_b(vb, vo, ndocs, scratch, d_soff, src, new_off, out)
                 versions[ver + 1] = (out, new_off, cap)
                 c4_recs_d[i] = rec
-        torch.cuda.synchronize(self.device)
-        t2 = time.perf_counter()
-        stage_recs = [None] * len(self.plan.stages)
-        for s, rec in stage_recs_d:
-            stage_recs[s] = rec.cpu().numpy()
-        c4_recs = {i: r.cpu().numpy() for i, r in c4_recs_d.items()}
-        host_versions = {}
+                keep.append(src)
+        # D2H into pinned host buffers, all on the stream, then one completion event
+        def d2h(t):
+            ht = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            ht.copy_(t, non_blocking=True)
+            return ht
+
+        h_stage = [d2h(r) if r is not None else None for r in stage_recs_d]
+        h_c4 = {i: d2h(r) for i, r in c4_recs_d.items()}
+        h_versions = {}
         for ver in range(1, self.plan.n_versions):
             vb, vo, _ = versions[ver]
-            o = vo.cpu().numpy()
-            host_versions[ver] = (vb[: int(o[-1])].cpu().numpy(), o)
-        fl = flags.cpu().numpy().view(np.uint32)
-        t3 = time.perf_counter()
-        return DeviceResult(stage_recs, c4_recs, host_versions, fl,
-                            {"h2d": t1 - t0, "kernels": t2 - t1, "d2h": t3 - t2})
+            h_versions[ver] = (d2h(vb), d2h(vo))
+        h_flags = d2h(flags)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        keep += [stage_recs_d, c4_recs_d, versions, flags]
+        t2 = time.perf_counter()
+        return PendingBatch(self, ndocs, ev, h_stage, h_c4, h_versions, h_flags,
+                            {"stage_h2d": t1 - t0, "launch": t2 - t1}, keep)
+
+    def run(self, data: np.ndarray, off: np.ndarray) -> DeviceResult:
+        return self.submit(data, off).wait()
+
+
+class EmulatedRunner:
+    """Host emulation of :class:`DeviceRunner` (same records, versions and flags, computed by the
+    C++ port of the device algorithms). Drives the exact resolve path of the GPU backend on a
+    machine without a GPU (``Engine(backend="emulate")``): used by CPU tests and for profiling
+    the host side of the device pipeline."""
+
+    def __init__(self, steps_native, plan: ExecPlan, langid=None, nthreads: int = 8):
+        h = native.host()
+        self.steps = steps_native
+        self.plan = plan
+        self.nthreads = nthreads
+        self.lid = langid.native() if langid is not None else None
+        _, stage_bs = h.build_device_plan(steps_native, plan.stages)
+        self.stage_layout = [h.stage_layout(b) for b in stage_bs]
+
+    def run(self, data: np.ndarray, off: np.ndarray) -> DeviceResult:
+        import time
+
+        h = native.host()
+        t0 = time.perf_counter()
+        ndocs = len(off) - 1
+        flags = np.zeros(ndocs, dtype=np.uint32)
+        versions = {0: (data, off)}
+        stage_recs: List[Optional[np.ndarray]] = [None] * len(self.plan.stages)
+        c4_recs = {}
+        for ver in range(self.plan.n_versions):
+            vd, vo = versions[ver]
+            for s, sv in enumerate(self.plan.stage_version):
+                if sv == ver:
+                    rec, fl = h.emulate_stage(self.steps, self.plan.stages[s], vd, vo, self.nthreads, self.lid)
+                    stage_recs[s] = rec
+                    flags |= fl
+            for i in self.plan.c4_steps:
+                if self.plan.steps[i].version_in == ver:
+                    rec, nd, no, fl = h.emulate_c4(self.steps[i], vd, vo, self.nthreads)
+                    c4_recs[i] = rec
+                    flags |= fl
+                    versions[ver + 1] = (nd, no)
+        host_versions = {v: versions[v] for v in range(1, self.plan.n_versions)}
+        return DeviceResult(stage_recs, c4_recs, host_versions, flags, {"emulate": time.perf_counter() - t0})

@@ -10,6 +10,8 @@ Backends:
   * ``cuda``: record/rewrite steps on the MI355X (HIP kernels), decisions + output assembly in
     the C++ host runtime; documents flagged by the device (dictionary scripts, hash collisions,
     scratch overflow) are recomputed on the CPU path with the ICU oracle.
+  * ``emulate``: the ``cuda`` resolve path with device records computed by the host port of
+    the kernels (no GPU needed; tests and profiling).
   * ``cpu``: the C++ CPU path (multithreaded); segmentation by our UAX#29 rules ("rules") or by
     ICU4C ("icu", the oracle).
 """
@@ -18,7 +20,7 @@ from __future__ import annotations
 import dataclasses
 import os
 import time
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -107,6 +109,10 @@ class Engine:
             d = badwords_dir or (bw_dirs[0] if bw_dirs else os.path.join("data", "c4_badwords"))
             self.badwords = self.h.BadWordsModule(d)
         self.device_runner = None
+        if backend == "emulate":
+            from .device import EmulatedRunner
+
+            self.device_runner = EmulatedRunner(self.steps, self.plan, self.langid, self.nthreads)
         if backend == "cuda":
             for st in self.steps:
                 ok, why = self.h.device_supported(st)
@@ -120,16 +126,42 @@ class Engine:
     def process(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None,
                 row_base: int = 0) -> BatchResult:
         """Run the pipeline over one batch. ``meta`` = (data uint8, off int64, valid uint8) or None."""
+        return self.finish(self.submit(data, off, meta, row_base))
+
+    def process_many(self, batches: Iterable) -> Iterator[BatchResult]:
+        """Pipelined processing of an iterable of ``(data, off, meta)`` batches: batch k+1 is
+        staged and its kernels queued on the GPU before batch k is resolved and assembled on the
+        host, so device work and host work overlap. Results are yielded in input order."""
+        pending = None
+        for item in batches:
+            data, off = item[0], item[1]
+            meta = item[2] if len(item) > 2 else None
+            cur = self.submit(data, off, meta)
+            if pending is not None:
+                yield self.finish(pending)
+            pending = cur
+        if pending is not None:
+            yield self.finish(pending)
+
+    def submit(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None, row_base: int = 0):
         t0 = time.perf_counter()
         data = np.ascontiguousarray(data, dtype=np.uint8)
         off = np.ascontiguousarray(off, dtype=np.int64)
+        dev = None
+        if self.backend in ("cuda", "emulate"):
+            submit = getattr(self.device_runner, "submit", None)
+            dev = submit(data, off) if submit is not None else self.device_runner.run(data, off)
+        return _Submitted(data, off, meta, row_base, dev, t0)
+
+    def finish(self, sub: "_Submitted") -> BatchResult:
+        data, off, meta, row_base, t0 = sub.data, sub.off, sub.meta, sub.row_base, sub.t0
         ndocs = len(off) - 1
         md, mo, mv = meta if meta is not None else (None, None, None)
         bs = self.h.BatchState(data, off, md, mo, mv, self.nthreads)
         timings: Dict[str, float] = {}
         delegated = np.zeros(0, dtype=np.int64)
-        if self.backend == "cuda":
-            res = self.device_runner.run(data, off)
+        if sub.dev is not None:
+            res = sub.dev.wait() if hasattr(sub.dev, "wait") else sub.dev
             timings.update(res.timings)
             t1 = time.perf_counter()
             delegated = np.nonzero(res.flags)[0].astype(np.int64)
@@ -159,13 +191,13 @@ class Engine:
         t2 = time.perf_counter()
         result = self._collect(bs, ndocs, timings)
         if len(delegated):
-            sub = self._process_subset_cpu(data, off, meta, delegated)
-            result.kept += sub.kept
-            result.excluded += sub.excluded
-            result.error_rows = np.concatenate([result.error_rows, sub.error_rows])
-            result.fail_step[delegated] = sub.fail_step
-            result.status[delegated] = sub.status
-            result.reasons.update(sub.reasons)
+            sub2 = self._process_subset_cpu(data, off, meta, delegated)
+            result.kept += sub2.kept
+            result.excluded += sub2.excluded
+            result.error_rows = np.concatenate([result.error_rows, sub2.error_rows])
+            result.fail_step[delegated] = sub2.fail_step
+            result.status[delegated] = sub2.status
+            result.reasons.update(sub2.reasons)
             result.n_delegated = len(delegated)
         timings["assemble"] = time.perf_counter() - t2
         timings["total"] = time.perf_counter() - t0
@@ -241,6 +273,16 @@ class Engine:
 
     def step_names(self) -> List[str]:
         return [s.type for s in self.cfg.pipeline]
+
+
+@dataclasses.dataclass
+class _Submitted:
+    data: np.ndarray
+    off: np.ndarray
+    meta: Optional[Tuple]
+    row_base: int
+    dev: object          # PendingBatch / DeviceResult / None (cpu)
+    t0: float
 
 
 def _cuda_available() -> bool:

@@ -7,9 +7,10 @@ Work decomposition
   scheduling, sharding and checkpoint granularity. Rank ``r`` of ``W`` owns a contiguous range
   of units balanced by bytes (``parallel.dist.shard_ranges``), so documents never cross GPUs.
 
-Per rank, three stages overlap (bounded queues, the heavy native calls release the GIL):
-  reader thread   Parquet decode + HTML-entity decode + packing   (unit k+1)
-  main thread     Engine.process: H2D, HIP kernels, D2H, resolve   (unit k)
+Per rank, four stages overlap (bounded queues, the heavy native calls release the GIL):
+  reader thread   Parquet decode + HTML-entity decode + packing    (unit k+2)
+  GPU stream      H2D, HIP kernels, D2H (Engine.process_many)      (unit k+1)
+  main thread     resolve + output assembly                        (unit k)
   writer thread   Arrow assembly + Parquet encode                  (unit k-1)
 
 Outputs
@@ -24,6 +25,7 @@ Outputs
 """
 from __future__ import annotations
 
+import collections
 import dataclasses
 import hashlib
 import json
@@ -395,12 +397,19 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     ureader = _UnitReader(reader)
     last_report = time.perf_counter()
     last_docs = local.docs
-    try:
+    inflight: collections.deque = collections.deque()
+
+    def feed():
         for unit, batch in _prefetch(((u, ureader.read(u)) for u in todo), depth=2):
-            t0 = time.perf_counter()
-            with metrics.ACTIVE_PROCESSING_TASKS.track_inprogress():
-                res = engine.process(batch.text[0], batch.text[1], batch.meta)
-            dt = time.perf_counter() - t0
+            inflight.append((unit, batch))
+            yield batch.text[0], batch.text[1], batch.meta
+
+    try:
+        t_prev = time.perf_counter()
+        for res in engine.process_many(feed()):
+            unit, batch = inflight.popleft()
+            now = time.perf_counter()
+            dt, t_prev = now - t_prev, now
             fs = res.fail_step
             step_counts = np.bincount(fs[(res.status == 1) & (fs >= 0)], minlength=nsteps)[:nsteps] \
                 if len(fs) else np.zeros(nsteps, dtype=np.int64)

@@ -1,0 +1,81 @@
+"""End-to-end file benchmark: synthetic CommonCrawl-shaped Parquet -> `run` -> Parquet.
+
+Unlike bench.py (which times the in-memory pipeline step), this includes Parquet decode, HTML
+entity decoding, output assembly and Parquet encode — the full CLI path.
+
+    python tools/e2e_bench.py --docs 1000000 --backend cuda [--backend cpu] [--out gpurun_out/e2e]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.parquet as pq
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def make_input(path: str, ndocs: int, mean_bytes: int, pool: int, row_group: int) -> int:
+    from textblaster_amd.utils import synth
+
+    texts = synth.make_corpus(pool, mean_bytes, seed=5)
+    rng = np.random.default_rng(5)
+    w = None
+    total = 0
+    for start in range(0, ndocs, row_group):
+        n = min(row_group, ndocs - start)
+        idx = rng.integers(0, len(texts), size=n)
+        tbl = pa.table({
+            "id": pa.array([f"doc-{start + i}" for i in range(n)]),
+            "text": pa.array([texts[i] for i in idx]),
+            "source": pa.array(["s3://commoncrawl/synthetic"] * n),
+            "metadata": pa.array(['{"url":"https://example.com/%d"}' % (start + i) for i in range(n)]),
+        })
+        total += sum(len(texts[i].encode()) for i in idx[:1000]) * n // min(n, 1000)
+        if w is None:
+            w = pq.ParquetWriter(path, tbl.schema, compression="snappy")
+        w.write_table(tbl)
+    w.close()
+    return total
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--docs", type=int, default=1_000_000)
+    ap.add_argument("--mean-bytes", type=int, default=1024)
+    ap.add_argument("--pool", type=int, default=50_000)
+    ap.add_argument("--row-group", type=int, default=100_000)
+    ap.add_argument("--unit-rows", type=int, default=65536)
+    ap.add_argument("--backend", action="append", default=None)
+    ap.add_argument("--config", default=os.path.join(ROOT, "config", "bench_pipeline.yaml"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "e2e"))
+    args = ap.parse_args()
+    os.makedirs(args.out, exist_ok=True)
+    inp = os.path.join(args.out, "input.parquet")
+    t = time.perf_counter()
+    make_input(inp, args.docs, args.mean_bytes, args.pool, args.row_group)
+    print(f"input: {args.docs} docs, {os.path.getsize(inp) / 1e6:.1f} MB in {time.perf_counter() - t:.1f}s",
+          flush=True)
+    from textblaster_amd.runner import RunConfig, run
+
+    for backend in args.backend or ["cuda"]:
+        o = os.path.join(args.out, f"{backend}.out.parquet")
+        e = os.path.join(args.out, f"{backend}.excluded.parquet")
+        st = run(RunConfig(inp, o, e, args.config, backend=backend, unit_rows=args.unit_rows))
+        line = {"backend": backend, "docs": st.docs, "kept": st.kept, "excluded": st.excluded, "errors": st.errors,
+                "seconds": round(st.seconds, 3), "docs_per_sec": round(st.docs_per_sec, 1),
+                "step_filtered": st.step_filtered, "delegated": st.delegated}
+        print(json.dumps(line), flush=True)
+        for p in (o, e):
+            os.remove(p)
+    os.remove(inp)
+
+
+if __name__ == "__main__":
+    main()

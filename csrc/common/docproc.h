@@ -66,14 +66,35 @@ struct DocCtx {
   UcdView ucd;
   const uint64_t* pw = nullptr;  // pw[k] = B^k
   uint32_t pw_n = 0;
-  char* scr = nullptr;
+  char* scr = nullptr;       // global (HBM) scratch arena of this document
   uint64_t cap = 0;
   uint64_t used = 0;
+  char* lds = nullptr;       // optional fast arena (the wave's LDS slice on the device)
+  uint32_t lcap = 0;
+  uint32_t lused = 0;
   uint32_t* flag = nullptr;  // per-document status word
   bool overflow = false;
 
+  struct Mark { uint64_t g; uint32_t l; };
+  TB_HD Mark mark() const { return Mark{used, lused}; }
+  TB_HD void reset(Mark m) { used = m.g; lused = m.l; }
+
+  // Working arrays go to LDS while it has room (addressed through generic pointers, so the
+  // algorithm code is the same for both arenas), then to the HBM scratch arena.
   template <class T>
   TB_HD T* alloc(uint64_t count) {
+    if (lds) {
+      const uint64_t a = (lused + 15u) & ~15u;
+      const uint64_t e = a + count * sizeof(T);
+      if (e <= lcap) {
+        lused = (uint32_t)e;
+        return (T*)(lds + a);
+      }
+    }
+    return alloc_global<T>(count);
+  }
+  template <class T>
+  TB_HD T* alloc_global(uint64_t count) {
     uint64_t a = (used + 15) & ~15ull;
     uint64_t e = a + count * sizeof(T) + 16;
     if (e > cap) {
@@ -229,7 +250,7 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
   uint32_t capn = 16;
   while (capn < 2 * n + 2) capn <<= 1;
   const uint32_t mask = capn - 1;
-  const uint64_t mark = x.used;
+  const auto mark = x.mark();
   uint64_t* keys = x.template alloc<uint64_t>(capn);
   uint32_t* vals = x.template alloc<uint32_t>(capn);
   if (x.overflow) return;
@@ -256,7 +277,7 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
   });
   if (collided) x.set_flag(DOC_NEEDS_CPU);
   x.par.sync();
-  x.used = mark;  // the table is scratch; canon[] lives in the caller's allocation
+  x.reset(mark);  // the table is scratch; canon[] lives in the caller's allocation
 }
 
 template <class P>
@@ -270,7 +291,7 @@ TB_HD bool bytes_eq(const uint8_t* b, uint32_t a0, uint32_t a1, uint32_t b0, uin
 template <class P, class SpanF>
 TB_HD void dup_spans(DocCtx<P>& x, const uint8_t* b, const uint64_t* PH, uint32_t n, SpanF&& span,
                      int64_t* out_elems, int64_t* out_bytes) {
-  const uint64_t mark = x.used;
+  const auto mark = x.mark();
   uint32_t* canon = x.template alloc<uint32_t>(n + 1);
   if (x.overflow) return;
   const uint64_t* pw = x.pw;
@@ -295,7 +316,7 @@ TB_HD void dup_spans(DocCtx<P>& x, const uint8_t* b, const uint64_t* PH, uint32_
     span(i, s, e);
     return (int64_t)(e - s);
   });
-  x.used = mark;
+  x.reset(mark);
 }
 
 // Lowercase (Rust str::to_lowercase on the word) hashed on the fly; optionally compared to `ref`.
@@ -394,7 +415,7 @@ template <class P>
 TB_HD uint32_t count_sentences(DocCtx<P>& x, const Cps& c, uint32_t s, uint32_t e) {
   const uint32_t m = e - s;
   if (m == 0) return 0;
-  const uint64_t mark = x.used;
+  const auto mark = x.mark();
   uint32_t* starts = x.template alloc<uint32_t>(m + 1);
   if (x.overflow) return 0;
   const uint32_t* prop = c.prop + s;
@@ -408,7 +429,7 @@ TB_HD uint32_t count_sentences(DocCtx<P>& x, const Cps& c, uint32_t s, uint32_t 
     for (uint32_t j = a; j < bnd; ++j) if (!is_ws(prop[j])) return 1u;
     return 0u;
   });
-  x.used = mark;
+  x.reset(mark);
   return cnt;
 }
 
@@ -430,7 +451,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     });
     return;
   }
-  const uint64_t mark = x.used;
+  const auto mark = x.mark();
   const uint32_t span = tce - tcs;
   uint32_t* rs = x.template alloc<uint32_t>(span + 1);
   uint32_t* rl = x.template alloc<uint32_t>(span + 1);
@@ -518,7 +539,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       int64_t res = 0;
       if (n > 0 && W >= n) {
         const uint32_t G = W - n + 1;
-        const uint64_t m2 = x.used;
+        const auto m2 = x.mark();
         uint32_t* gc = x.template alloc<uint32_t>(G);
         uint32_t* cnt = x.template alloc<uint32_t>(G);
         if (x.overflow) return;
@@ -541,7 +562,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
           });
           res = (int64_t)maxlen * (int64_t)maxc;
         }
-        x.used = m2;
+        x.reset(m2);
       }
       x.par.single([&]() { r[rec_gr_fixed() + t] = res; });
     }
@@ -557,8 +578,8 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
         uint32_t* sn = x.template alloc<uint32_t>((G + 31) / 32 + 1);
         if (x.overflow) return;
         x.par.single([&]() {
-          gofs[2 * t] = (uint64_t)((char*)gct - x.scr);
-          gofs[2 * t + 1] = (uint64_t)((char*)sn - x.scr);
+          gofs[2 * t] = (uint64_t)(uintptr_t)gct;  // generic pointers (LDS or HBM)
+          gofs[2 * t + 1] = (uint64_t)(uintptr_t)sn;
         });
         x.par.for_n((G + 31) / 32 + 1, [&](uint32_t i) { sn[i] = 0; });
         canonicalize(
@@ -588,8 +609,8 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
         const uint32_t n = (uint32_t)ds.dup_n[t];
         int64_t rep = 0;
         if (n > 0 && W >= n) {
-          const uint32_t* gc = (const uint32_t*)(x.scr + gofs[2 * t]);
-          uint32_t* sn = (uint32_t*)(x.scr + gofs[2 * t + 1]);
+          const uint32_t* gc = (const uint32_t*)(uintptr_t)gofs[2 * t];
+          uint32_t* sn = (uint32_t*)(uintptr_t)gofs[2 * t + 1];
           uint32_t idx = 0;
           while (idx + n <= W) {
             const uint32_t g = gc[idx];
@@ -607,7 +628,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       x.par.sync();
     }
   }
-  x.used = mark;
+  x.reset(mark);
 }
 
 template <class P>
@@ -622,7 +643,7 @@ TB_HD void langid_features(DocCtx<P>& x, const Cps& c, const uint16_t* emb, Stag
     uint32_t l = ucd.lower(cp[i]);
     return l ? l : cp[i];
   };
-  const uint64_t mark = x.used;
+  const auto mark = x.mark();
   uint32_t* goff = x.template alloc<uint32_t>(lim + 2);
   if (x.overflow) return;
   const uint32_t K = x.par.template scan<uint32_t>(
@@ -646,7 +667,7 @@ TB_HD void langid_features(DocCtx<P>& x, const Cps& c, const uint16_t* emb, Stag
         vec[d] = f32_to_bf16(v);
       });
   x.par.single([&]() { out.lid_cnt[doc] = (int32_t)K; });
-  x.used = mark;
+  x.reset(mark);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -837,7 +858,7 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
       NLn, 0u, [](uint32_t a, uint32_t b2) { return a + b2; },
       [&](uint32_t k) { return code[k] == 0 ? plen[k] + 1 : 0u; }, [&](uint32_t k, uint32_t e) { joff[k] = e; });
   if (Jtot > 0) Jtot -= 1;
-  uint8_t* Jb = x.template alloc<uint8_t>(Jtot + 1);
+  uint8_t* Jb = x.template alloc_global<uint8_t>(Jtot + 1);  // read back by pass B: HBM
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   x.par.for_n(NLn, [&](uint32_t k) {
     if (code[k] != 0) return;
@@ -948,7 +969,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
     } else if (ds.kind == DK_GOPHER_REP) {
       gopher_rep_record(x, ds, b, c, PH, w, r);
     } else if (ds.kind == DK_FINEWEB) {
-      const uint64_t mark = x.used;
+      const auto mark = x.mark();
       uint32_t* nb = x.template alloc<uint32_t>(L.n + 1);
       if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
       const uint32_t NB = x.par.template compact<int>(
@@ -979,7 +1000,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
       x.par.single([&]() {
         r[0] = NB; r[1] = stop_end; r[2] = shrt; r[3] = dup_b; r[4] = (int64_t)C - nl; r[5] = nl; r[6] = W;
       });
-      x.used = mark;
+      x.reset(mark);
     } else if (ds.kind == DK_LANGID) {
       langid_features(x, c, lid_emb, out);
     }

@@ -19,6 +19,8 @@ using namespace tb;
 
 namespace {
 
+constexpr uint32_t kMaxLdsPerDoc = 160 * 1024;
+
 struct DevTables {
   const uint16_t* s1;
   const uint32_t* s2;
@@ -26,10 +28,17 @@ struct DevTables {
   const int32_t* l2;
 };
 
+// Dynamic LDS: each workgroup (= one wave = one document) gets `lds_bytes` of fast arena; the
+// document's working arrays are carved from it first and spill to its HBM scratch slice.
+extern __shared__ __attribute__((aligned(16))) char g_lds_arena[];
+
 __device__ __forceinline__ DocCtx<WavePar> make_ctx(const DevTables& t, const uint64_t* pw, uint32_t pw_n,
                                                    char* scratch, const int64_t* scratch_off, int doc,
-                                                   uint32_t* flags) {
+                                                   uint32_t* flags, uint32_t lds_bytes) {
   DocCtx<WavePar> x;
+  x.lds = lds_bytes ? (char*)g_lds_arena : nullptr;
+  x.lcap = lds_bytes;
+  x.lused = 0;
   x.ucd = UcdView{t.s1, t.s2, t.l1, t.l2};
   x.pw = pw;
   x.pw_n = pw_n;
@@ -44,10 +53,11 @@ __global__ __launch_bounds__(64) void k_stage_analyze(
     const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes,
     const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,
     const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
-    int64_t* rec, uint32_t* flags, const uint16_t* __restrict__ lid_emb, uint16_t* lid_vec, int32_t* lid_cnt) {
+    int64_t* rec, uint32_t* flags, const uint16_t* __restrict__ lid_emb, uint16_t* lid_vec, int32_t* lid_cnt,
+    uint32_t lds_bytes) {
   const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
   if (doc >= ndocs) return;
-  DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags);
+  DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, lid_vec, lid_cnt};
@@ -57,10 +67,11 @@ __global__ __launch_bounds__(64) void k_stage_analyze(
 __global__ __launch_bounds__(64) void k_c4_pass_a(
     const DevC4* __restrict__ c4, const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
     const int32_t* __restrict__ perm, int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off,
-    const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec, int64_t* src, uint32_t* flags) {
+    const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec, int64_t* src, uint32_t* flags,
+    uint32_t lds_bytes) {
   const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
   if (doc >= ndocs) return;
-  DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags);
+  DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2);
@@ -151,23 +162,29 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
                      const int64_t* off, const int32_t* perm, int32_t ndocs, char* scratch,
                      const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                      const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
-                     const uint16_t* lid_emb, uint16_t* lid_vec, int32_t* lid_cnt) {
+                     const uint16_t* lid_emb, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes) {
   if (ndocs <= 0) return 0;
+  if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
-  hipLaunchKernelGGL(k_stage_analyze, dim3(ndocs), dim3(64), 0, stream, (const DevPlan*)plan,
+  if (lds_bytes > 65536)
+    (void)hipFuncSetAttribute((const void*)k_stage_analyze, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  hipLaunchKernelGGL(k_stage_analyze, dim3(ndocs), dim3(64), lds_bytes, stream, (const DevPlan*)plan,
                      (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, flags,
-                     lid_emb, lid_vec, lid_cnt);
+                     lid_emb, lid_vec, lid_cnt, lds_bytes);
   return (int)hipGetLastError();
 }
 
 int tb_c4_pass_a(hipStream_t stream, const void* c4, const uint8_t* bytes, const int64_t* off, const int32_t* perm,
                  int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n,
                  const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
-                 int64_t* src, uint32_t* flags) {
+                 int64_t* src, uint32_t* flags, uint32_t lds_bytes) {
   if (ndocs <= 0) return 0;
+  if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
-  hipLaunchKernelGGL(k_c4_pass_a, dim3(ndocs), dim3(64), 0, stream, (const DevC4*)c4, bytes, off, perm, ndocs,
-                     scratch, scratch_off, pw, pw_n, t, rec, src, flags);
+  if (lds_bytes > 65536)
+    (void)hipFuncSetAttribute((const void*)k_c4_pass_a, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  hipLaunchKernelGGL(k_c4_pass_a, dim3(ndocs), dim3(64), lds_bytes, stream, (const DevC4*)c4, bytes, off, perm, ndocs,
+                     scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes);
   return (int)hipGetLastError();
 }
 

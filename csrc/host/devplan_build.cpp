@@ -144,7 +144,7 @@ static void lid_head_host(const LangidModel& m, const uint16_t* v, int32_t cnt, 
 
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
-                   std::vector<int64_t>& rec, std::vector<uint32_t>& flags) {
+                   std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes) {
   DevPlan* plan = new DevPlan();
   std::memset(plan, 0, sizeof(DevPlan));
   DevStage st = build_stage(steps, idx, *plan);
@@ -161,6 +161,7 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
   const UcdView ucd = host_ucd();
   parallel_for(ndocs, nthreads, [&](int64_t a, int64_t b) {
     std::vector<char> scratch;
+    std::vector<char> lds(lds_bytes + 16);  // stands in for the wave's LDS slice
     for (int64_t i = a; i < b; ++i) {
       const uint32_t n = (uint32_t)(off[i + 1] - off[i]);
       const uint64_t need = scratch_bytes_for(n);
@@ -171,6 +172,8 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
       x.pw_n = (uint32_t)pw.size() - 1;
       x.scr = scratch.data();
       x.cap = need;
+      x.lds = lds_bytes ? lds.data() : nullptr;
+      x.lcap = lds_bytes;
       x.flag = &flags[i];
       StageOut out{rec.data(), (uint32_t)ndocs, (uint32_t)i, lvec.data(), lcnt.data()};
       analyze_stage(x, st, *plan, lid ? lid->emb.data() : nullptr, (const uint8_t*)data + off[i], n, out);
@@ -187,7 +190,7 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
 
 void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
                 std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,
-                std::vector<uint32_t>& flags) {
+                std::vector<uint32_t>& flags, uint32_t lds_bytes) {
   DevC4 c4 = build_c4(step);
   rec.assign((size_t)rec::C4_WIDTH * ndocs, 0);
   flags.assign(ndocs, 0);
@@ -198,6 +201,7 @@ void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int6
   const UcdView ucd = host_ucd();
   parallel_for(ndocs, nthreads, [&](int64_t a, int64_t b) {
     std::vector<char> scratch;
+    std::vector<char> lds(lds_bytes + 16);  // stands in for the wave's LDS slice
     for (int64_t i = a; i < b; ++i) {
       const uint32_t n = (uint32_t)(off[i + 1] - off[i]);
       const uint64_t need = scratch_bytes_for(n);
@@ -208,6 +212,8 @@ void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int6
       x.pw_n = (uint32_t)pw.size() - 1;
       x.scr = scratch.data();
       x.cap = need;
+      x.lds = lds_bytes ? lds.data() : nullptr;
+      x.lcap = lds_bytes;
       x.flag = &flags[i];
       int64_t src[2] = {-1, 0};
       const uint8_t* b = (const uint8_t*)data + off[i];

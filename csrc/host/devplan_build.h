@@ -20,9 +20,9 @@ std::vector<uint64_t> pow_table(uint32_t n);
 
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
-                   std::vector<int64_t>& rec, std::vector<uint32_t>& flags);
+                   std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes = 0);
 void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
                 std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,
-                std::vector<uint32_t>& flags);
+                std::vector<uint32_t>& flags, uint32_t lds_bytes = 0);
 
 }  // namespace tb

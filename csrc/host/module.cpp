@@ -450,28 +450,28 @@ PYBIND11_MODULE(_tbhost, m) {
   m.attr("OFFSETOF_STEPS") = offsetof(DevStage, steps);
   m.def("emulate_stage", [](const std::vector<StepCfg>& steps, const std::vector<int>& idx,
                             py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
-                            int nthreads, std::shared_ptr<LangidModel> lid) {
+                            int nthreads, std::shared_ptr<LangidModel> lid, uint32_t lds_bytes) {
     std::vector<int64_t> rec;
     std::vector<uint32_t> flags;
     const int64_t nd = (int64_t)off.size() - 1;
     {
       py::gil_scoped_release nogil;
-      emulate_stage(steps, idx, nd, (const char*)data.data(), off.data(), nthreads, lid.get(), rec, flags);
+      emulate_stage(steps, idx, nd, (const char*)data.data(), off.data(), nthreads, lid.get(), rec, flags, lds_bytes);
     }
     return py::make_tuple(to_numpy(std::move(rec)), to_numpy(std::move(flags)));
   }, py::arg("steps"), py::arg("idx"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8,
-     py::arg("lid") = nullptr);
+     py::arg("lid") = nullptr, py::arg("lds_bytes") = 0);
   m.def("emulate_c4", [](const StepCfg& step, py::array_t<uint8_t, py::array::c_style> data,
-                         py::array_t<int64_t, py::array::c_style> off, int nthreads) {
+                         py::array_t<int64_t, py::array::c_style> off, int nthreads, uint32_t lds_bytes) {
     std::vector<int64_t> rec, no;
     std::vector<uint32_t> flags;
     std::string nd;
     const int64_t n = (int64_t)off.size() - 1;
     {
       py::gil_scoped_release nogil;
-      emulate_c4(step, n, (const char*)data.data(), off.data(), nthreads, rec, nd, no, flags);
+      emulate_c4(step, n, (const char*)data.data(), off.data(), nthreads, rec, nd, no, flags, lds_bytes);
     }
     return py::make_tuple(to_numpy(std::move(rec)), str_to_numpy(std::move(nd)), to_numpy(std::move(no)),
                           to_numpy(std::move(flags)));
-  });
+  }, py::arg("step"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8, py::arg("lds_bytes") = 0);
 }

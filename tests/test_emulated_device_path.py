@@ -54,3 +54,29 @@ def test_pipelined_equals_sequential():
     seq = [outputs(eng.process(d, o)) for d, o in batches]
     pip = [outputs(r) for r in eng.process_many(batches)]
     assert seq == pip
+
+
+@pytest.mark.parametrize("lds", [256, 4096, 16384])
+def test_lds_arena_does_not_change_results(host, lds):
+    """Device working arrays are carved from a per-wave LDS slice first and spill to HBM scratch;
+    the host emulation runs the same allocator over a stand-in buffer: records, flags and
+    rewritten texts must not depend on the slice size."""
+    from textblaster_amd.models.langid import load_default
+    from textblaster_amd.pipeline.plan import build_plan
+
+    cfg = load_pipeline_config("config/bench_pipeline.yaml")
+    steps = [host.make_step(s.native_dict()) for s in cfg.pipeline]
+    plan = build_plan(cfg)
+    lid = load_default().native()
+    texts = synth.make_corpus(400, 1200, seed=23) + EDGE
+    data, off = synth.pack(texts)
+    for idx in plan.stages:
+        r0, f0 = host.emulate_stage(steps, idx, data, off, 4, lid, 0)
+        r1, f1 = host.emulate_stage(steps, idx, data, off, 4, lid, lds)
+        np.testing.assert_array_equal(r0, r1)
+        np.testing.assert_array_equal(f0, f1)
+    for i in plan.c4_steps:
+        a = host.emulate_c4(steps[i], data, off, 4, 0)
+        b = host.emulate_c4(steps[i], data, off, 4, lds)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)

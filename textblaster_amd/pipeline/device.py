@@ -86,6 +86,7 @@ class PendingBatch:
 
 class DeviceRunner:
     N_SLOTS = 2
+    DEFAULT_LDS_BYTES = 12288
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None):
         import torch
@@ -112,6 +113,11 @@ class DeviceRunner:
             self.lid_wT = torch.from_numpy(wT).to(self.device)
             self.lid_b = torch.from_numpy(langid.b.astype(np.float32)).to(self.device)
         self.c4_growth = int(h.C4_MAX_GROWTH)
+        # LDS arena per document (one wave per workgroup); TB_LDS_BYTES overrides for tuning
+        import os
+
+        self.lds_bytes = int(os.environ.get("TB_LDS_BYTES", str(self.DEFAULT_LDS_BYTES)))
+        self.lds_bytes_c4 = int(os.environ.get("TB_LDS_BYTES_C4", str(self.lds_bytes)))
         self.slots = [_Slot() for _ in range(self.N_SLOTS)]
         self._next_slot = 0
         self._last_lid = None
@@ -199,7 +205,8 @@ class DeviceRunner:
                     lid_vec = torch.zeros(ndocs * h.LID_DIM, dtype=torch.int16, device=self.device)
                     lid_cnt = torch.zeros(ndocs, dtype=torch.int32, device=self.device)
                 self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm, ndocs, scratch, d_soff, pw, pw_n,
-                                     rec, flags, self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt)
+                                     rec, flags, self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
+                                     self.lds_bytes)
                 if lid_vec is not None:
                     self._last_lid = (lid_vec, lid_cnt)
                 for kind, width, prefix in layout:
@@ -210,7 +217,8 @@ class DeviceRunner:
             for i in c4_here:
                 rec = torch.zeros(7 * ndocs, dtype=torch.int64, device=self.device)
                 src = torch.zeros(2 * ndocs, dtype=torch.int64, device=self.device)
-                self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm, ndocs, scratch, d_soff, pw, pw_n, rec, src, flags)
+                self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm, ndocs, scratch, d_soff, pw, pw_n, rec, src, flags,
+                                 self.lds_bytes_c4)
                 new_off = torch.zeros(ndocs + 1, dtype=torch.int64, device=self.device)
                 torch.cumsum(src.view(ndocs, 2)[:, 1], 0, out=new_off[1:])
                 cap = vlen + self.c4_growth * ndocs + 16  # device rewrites never grow more (kC4MaxGrowth)

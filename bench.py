@@ -130,6 +130,9 @@ def main():
             "last_step_timings": {k: round(v, 5) for k, v in res.timings.items()},
         }
         print(json.dumps(line), flush=True)
+        dr = getattr(eng, "device_runner", None)
+        if dr is not None and getattr(dr, "phase_prof", False):
+            print(dr.phase_report(), file=sys.stderr, flush=True)
     ctx.destroy()
 
 

@@ -21,6 +21,14 @@
 
 namespace tb {
 
+// Phase ids for DocCtx::stamp (profiling only).
+enum : int {
+  PH_START = 0, PH_DECODE, PH_DICT, PH_PREFIX_HASH, PH_WORDS, PH_LINES, PH_GQ, PH_GR_LINES, PH_GR_WORDS,
+  PH_GR_TOP, PH_GR_DUP, PH_FW, PH_LID,
+  PH_C4_LOREM = 16, PH_C4_DECODE, PH_C4_LINES, PH_C4_CITE, PH_C4_WORDS, PH_C4_CODES, PH_C4_JOIN, PH_C4_SENT,
+  kPhaseSlots = 32
+};
+
 enum : uint32_t {
   DOC_OK = 0,
   DOC_NEEDS_CPU = 1,    // dictionary script / hash collision / scratch overflow
@@ -74,6 +82,16 @@ struct DocCtx {
   uint32_t lused = 0;
   uint32_t* flag = nullptr;  // per-document status word
   bool overflow = false;
+  uint64_t* prof = nullptr;  // optional per-document phase cycle counters (kPhaseSlots)
+  uint64_t t_last = 0;
+
+  // Phase timing (profiling builds of a run): cycles since the previous stamp go to `id`.
+  TB_HD void stamp(int id) {
+    if (!prof) return;
+    const uint64_t t = P::clock();
+    if (t_last && par.leader()) prof[id] += t - t_last;
+    t_last = t;
+  }
 
   struct Mark { uint64_t g; uint32_t l; };
   TB_HD Mark mark() const { return Mark{used, lused}; }
@@ -490,6 +508,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
               e0 = off[ce];
             },
             &para_dup, &para_dup_b);
+  x.stamp(PH_GR_LINES);
   x.par.single([&]() {
     r[0] = span;
     r[1] = NPR + 1;
@@ -534,6 +553,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     });
     x.par.sync();
     if (x.overflow) return;
+    x.stamp(PH_GR_WORDS);
     for (int t = 0; t < ds.n_top; ++t) {
       const uint32_t n = (uint32_t)ds.top_n[t];
       int64_t res = 0;
@@ -566,6 +586,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       }
       x.par.single([&]() { r[rec_gr_fixed() + t] = res; });
     }
+    x.stamp(PH_GR_TOP);
     if (ds.n_dup > 0) {
       // per-n canonical-gram arrays and visited bitmaps; their scratch offsets are kept in scratch
       uint64_t* gofs = x.template alloc<uint64_t>(2 * kMaxNgramEntries);
@@ -626,6 +647,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
         r[rec_gr_fixed() + ds.n_top + t] = rep;
       });
       x.par.sync();
+      x.stamp(PH_GR_DUP);
     }
   }
   x.reset(mark);
@@ -680,6 +702,7 @@ TB_HD bool end_punct(uint32_t c) {
 
 template <class P>
 TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, int64_t* r, int64_t* src) {
+  x.stamp(PH_START);
   const uint32_t lorem = c4.filter_lorem_ipsum
       ? x.par.template sum<uint32_t>(n, [&](uint32_t s) {
           if (b[s] != 'l' && b[s] != 'L') return 0u;
@@ -696,8 +719,10 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
     });
     return;
   }
+  x.stamp(PH_C4_LOREM);
   Cps c = decode(x, b, n);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  x.stamp(PH_C4_DECODE);
   const uint32_t C = c.n;
   const uint32_t* cp = c.cp;
   const uint32_t* prop = c.prop;
@@ -749,6 +774,7 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
     }
   }
   x.par.sync();
+  x.stamp(PH_C4_LINES);
   // ---- citation removal -> processed line lengths ----
   auto cite_end = [&](uint32_t j, uint32_t e) -> uint32_t {  // cp index past a citation at j, or 0
     if (cp[j] != '[') return 0;
@@ -799,6 +825,7 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   });
   x.par.single([&]() { poff[NLn] = Ptot; });
   x.par.sync();
+  x.stamp(PH_C4_CITE);
   // ---- words of the processed lines ----
   Cps pc = decode(x, Pb, Ptot);
   Words pwd = words(x, pc);
@@ -819,6 +846,7 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
     P::max32(&mx[lo], pwd.ce[q] - pwd.cs[q]);
   });
   x.par.sync();
+  x.stamp(PH_C4_WORDS);
   const char* const kPol[6] = {"terms of use", "privacy policy", "cookie policy",
                                       "uses cookies", "use of cookies", "use cookies"};
   const int kPolLen[6] = {12, 14, 13, 12, 14, 11};
@@ -851,6 +879,7 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   const int64_t s_long = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 1); });
   const int64_t s_punct = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 2); });
   const int64_t s_few = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 3); });
+  x.stamp(PH_C4_CODES);
   // ---- joined kept lines ----
   uint32_t* joff = x.template alloc<uint32_t>(NLn + 1);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
@@ -867,6 +896,7 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
     if (o + plen[k] < Jtot) Jb[o + plen[k]] = '\n';
   });
   x.par.sync();
+  x.stamp(PH_C4_JOIN);
   Cps jc = decode(x, Jb, Jtot);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   const uint32_t JC = jc.n;
@@ -879,6 +909,7 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
     bstart = jc.off[tcs];
     blen = jc.off[tce] - jc.off[tcs];
   }
+  x.stamp(PH_C4_SENT);
   const int64_t jrel = (int64_t)((const char*)Jb - x.scr) + bstart;
   // The rewrite can only grow a document by one '\n' per sentence not followed by whitespace
   // (split_paragraph=false). Bounding the growth to kC4MaxGrowth bytes lets the host size the
@@ -910,18 +941,24 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
     if (k == DK_FINEWEB) need_words = need_lines = need_ph = true;
     if (k == DK_LANGID) need_lid = true;
   }
+  x.stamp(PH_START);
   Cps c = decode(x, b, n);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  x.stamp(PH_DECODE);
   const uint32_t C = c.n;
   // Documents with dictionary-segmented scripts go to the ICU path (host).
   const uint32_t ndict = x.par.template sum<uint32_t>(C, [&](uint32_t i) { return (c.prop[i] & P_DICT) ? 1u : 0u; });
   if (ndict) { x.set_flag(DOC_NEEDS_CPU); }
+  x.stamp(PH_DICT);
   uint64_t* PH = nullptr;
   if (need_ph) PH = prefix_hash(x, b, n);
+  x.stamp(PH_PREFIX_HASH);
   Words w;
   if (need_words && !ndict) w = words(x, c);
+  x.stamp(PH_WORDS);
   Lines L;
   if (need_lines) L = rust_lines(x, c);
+  x.stamp(PH_LINES);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   const uint32_t W = w.n;
   const uint32_t* cp = c.cp;
@@ -966,6 +1003,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
         r[0] = W; r[1] = sum_chars; r[2] = nhash; r[3] = nell; r[4] = L.n;
         r[5] = bullet; r[6] = ell_lines; r[7] = alpha; r[8] = stop;
       });
+      x.stamp(PH_GQ);
     } else if (ds.kind == DK_GOPHER_REP) {
       gopher_rep_record(x, ds, b, c, PH, w, r);
     } else if (ds.kind == DK_FINEWEB) {
@@ -1001,8 +1039,10 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
         r[0] = NB; r[1] = stop_end; r[2] = shrt; r[3] = dup_b; r[4] = (int64_t)C - nl; r[5] = nl; r[6] = W;
       });
       x.reset(mark);
+      x.stamp(PH_FW);
     } else if (ds.kind == DK_LANGID) {
       langid_features(x, c, lid_emb, out);
+      x.stamp(PH_LID);
     }
     if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   }

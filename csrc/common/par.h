@@ -65,6 +65,7 @@ struct SeqPar {
     return acc;
   }
   void sync() const {}
+  static uint64_t clock() { return 0; }
   template <class F>
   void single(F&& f) const { f(); }
   bool leader() const { return true; }
@@ -164,6 +165,7 @@ struct WavePar {
     return carry;
   }
   __device__ void sync() const { __syncthreads(); }
+  __device__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
   template <class F>
   __device__ void single(F&& f) const { if (lane == 0) f(); }
   __device__ bool leader() const { return lane == 0; }

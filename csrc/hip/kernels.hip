@@ -34,8 +34,9 @@ extern __shared__ __attribute__((aligned(16))) char g_lds_arena[];
 
 __device__ __forceinline__ DocCtx<WavePar> make_ctx(const DevTables& t, const uint64_t* pw, uint32_t pw_n,
                                                    char* scratch, const int64_t* scratch_off, int doc,
-                                                   uint32_t* flags, uint32_t lds_bytes) {
+                                                   uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
   DocCtx<WavePar> x;
+  x.prof = prof ? prof + (size_t)doc * kPhaseSlots : nullptr;
   x.lds = lds_bytes ? (char*)g_lds_arena : nullptr;
   x.lcap = lds_bytes;
   x.lused = 0;
@@ -54,10 +55,10 @@ __global__ __launch_bounds__(64) void k_stage_analyze(
     const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,
     const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
     int64_t* rec, uint32_t* flags, const uint16_t* __restrict__ lid_emb, uint16_t* lid_vec, int32_t* lid_cnt,
-    uint32_t lds_bytes) {
+    uint32_t lds_bytes, uint64_t* prof) {
   const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
   if (doc >= ndocs) return;
-  DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes);
+  DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, lid_vec, lid_cnt};
@@ -68,10 +69,10 @@ __global__ __launch_bounds__(64) void k_c4_pass_a(
     const DevC4* __restrict__ c4, const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
     const int32_t* __restrict__ perm, int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off,
     const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec, int64_t* src, uint32_t* flags,
-    uint32_t lds_bytes) {
+    uint32_t lds_bytes, uint64_t* prof) {
   const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
   if (doc >= ndocs) return;
-  DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes);
+  DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2);
@@ -162,7 +163,8 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
                      const int64_t* off, const int32_t* perm, int32_t ndocs, char* scratch,
                      const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                      const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
-                     const uint16_t* lid_emb, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes) {
+                     const uint16_t* lid_emb, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes,
+                     uint64_t* prof) {
   if (ndocs <= 0) return 0;
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
@@ -170,21 +172,21 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
     (void)hipFuncSetAttribute((const void*)k_stage_analyze, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(k_stage_analyze, dim3(ndocs), dim3(64), lds_bytes, stream, (const DevPlan*)plan,
                      (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, flags,
-                     lid_emb, lid_vec, lid_cnt, lds_bytes);
+                     lid_emb, lid_vec, lid_cnt, lds_bytes, prof);
   return (int)hipGetLastError();
 }
 
 int tb_c4_pass_a(hipStream_t stream, const void* c4, const uint8_t* bytes, const int64_t* off, const int32_t* perm,
                  int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n,
                  const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
-                 int64_t* src, uint32_t* flags, uint32_t lds_bytes) {
+                 int64_t* src, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
   if (ndocs <= 0) return 0;
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k_c4_pass_a, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(k_c4_pass_a, dim3(ndocs), dim3(64), lds_bytes, stream, (const DevC4*)c4, bytes, off, perm, ndocs,
-                     scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes);
+                     scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof);
   return (int)hipGetLastError();
 }
 
@@ -209,6 +211,8 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
   hipLaunchKernelGGL(k_pow_table, dim3((n + 256) / 256), dim3(256), 0, stream, pw, n);
   return (int)hipGetLastError();
 }
+
+int tb_phase_slots() { return kPhaseSlots; }
 
 int tb_abi_version() { return 1; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }

@@ -17,12 +17,13 @@ _U32 = ctypes.c_uint32
 _I64 = ctypes.c_int64
 
 _SIGS = {
-    "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32],
-    "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32],
+    "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
+    "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
     "tb_c4_pass_b": [_P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "tb_langid_head": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I32, _P],
     "tb_pow_table": [_P, _P, _U32],
     "tb_abi_version": [],
+    "tb_phase_slots": [],
     "tb_sizeof_plan": [],
     "tb_sizeof_stage": [],
     "tb_sizeof_c4": [],
@@ -79,21 +80,22 @@ class Kernels:
         return self._pw, self._pw_n
 
     def stage_analyze(self, plan, stage, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, flags,
-                      lid_emb=None, lid_vec=None, lid_cnt=None, lds_bytes=0):
+                      lid_emb=None, lid_vec=None, lid_cnt=None, lds_bytes=0, prof=None):
         t = self.tabs
         rc = self.lib.tb_stage_analyze(
             self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs,
             scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
             t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), _ptr(lid_emb), _ptr(lid_vec),
-            _ptr(lid_cnt), lds_bytes)
+            _ptr(lid_cnt), lds_bytes, _ptr(prof))
         _check(rc, "tb_stage_analyze")
 
-    def c4_pass_a(self, c4, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags, lds_bytes=0):
+    def c4_pass_a(self, c4, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags, lds_bytes=0,
+                  prof=None):
         t = self.tabs
         rc = self.lib.tb_c4_pass_a(
             self.stream(), c4.data_ptr(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs, scratch.data_ptr(),
             scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
-            t[3].data_ptr(), rec.data_ptr(), src.data_ptr(), flags.data_ptr(), lds_bytes)
+            t[3].data_ptr(), rec.data_ptr(), src.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof))
         _check(rc, "tb_c4_pass_a")
 
     def c4_pass_b(self, bytes_, off, ndocs, scratch, scratch_off, src, new_off, out):

@@ -78,6 +78,8 @@ class PendingBatch:
             o = vo.numpy()
             host_versions[ver] = (vb.numpy()[: int(o[-1])], o)
         fl = self._flags.numpy().view(np.uint32)
+        if self.runner.phase_prof:
+            self.runner.collect_phase_prof(self._keep)
         self._keep = None
         timings = dict(self._t_submit)
         timings["gpu_wait"] = t1 - t0
@@ -118,6 +120,10 @@ class DeviceRunner:
 
         self.lds_bytes = int(os.environ.get("TB_LDS_BYTES", str(self.DEFAULT_LDS_BYTES)))
         self.lds_bytes_c4 = int(os.environ.get("TB_LDS_BYTES_C4", str(self.lds_bytes)))
+        # TB_PHASE_PROF=1: per-document phase cycle counters (s_memtime stamps) for profiling
+        self.phase_prof = os.environ.get("TB_PHASE_PROF", "") not in ("", "0")
+        self.phase_totals: Dict[str, np.ndarray] = {}
+        self.phase_docs: Dict[str, int] = {}
         self.slots = [_Slot() for _ in range(self.N_SLOTS)]
         self._next_slot = 0
         self._last_lid = None
@@ -166,6 +172,35 @@ class DeviceRunner:
                                             device=self.device)
         return slot.scratch
 
+    def _prof_buf(self, ndocs, keep, name):
+        if not self.phase_prof:
+            return None
+        t = self.torch.zeros(ndocs * 32, dtype=self.torch.int64, device=self.device)
+        keep.append(("prof", name, t))
+        return t
+
+    def collect_phase_prof(self, keep) -> None:
+        for item in keep:
+            if isinstance(item, tuple) and len(item) == 3 and item[0] == "prof":
+                _, name, t = item
+                a = t.view(-1, 32).sum(0).cpu().numpy()
+                self.phase_totals[name] = self.phase_totals.get(name, 0) + a
+                self.phase_docs[name] = self.phase_docs.get(name, 0) + t.numel() // 32
+
+    def phase_report(self) -> str:
+        names = {0: "start", 1: "decode", 2: "dict", 3: "prefix_hash", 4: "words", 5: "lines", 6: "gopher_quality",
+                 7: "gr_lines_paras", 8: "gr_word_hash", 9: "gr_top_ngrams", 10: "gr_dup_ngrams", 11: "fineweb",
+                 12: "langid", 16: "c4_lorem", 17: "c4_decode", 18: "c4_lines", 19: "c4_cite", 20: "c4_words",
+                 21: "c4_codes", 22: "c4_join", 23: "c4_sentences"}
+        lines = []
+        for k, tot in self.phase_totals.items():
+            nd = max(1, self.phase_docs[k])
+            allc = float(np.sum(tot))
+            lines.append(f"{k}: {allc / nd:,.0f} cycles/doc (wave lifetime, summed phases)")
+            for i in np.nonzero(tot)[0]:
+                lines.append(f"   {names.get(int(i), i):>16}: {tot[i] / nd:>12,.0f}  ({100 * tot[i] / allc:5.1f}%)")
+        return "\n".join(lines)
+
     def submit(self, data: np.ndarray, off: np.ndarray) -> PendingBatch:
         """Stage inputs, enqueue every device stage and the D2H copies; returns immediately."""
         import time
@@ -204,9 +239,10 @@ class DeviceRunner:
                 if any(kind == 4 for kind, _, _ in layout):
                     lid_vec = torch.zeros(ndocs * h.LID_DIM, dtype=torch.int16, device=self.device)
                     lid_cnt = torch.zeros(ndocs, dtype=torch.int32, device=self.device)
+                prof = self._prof_buf(ndocs, keep, f"stage{s}")
                 self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm, ndocs, scratch, d_soff, pw, pw_n,
                                      rec, flags, self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
-                                     self.lds_bytes)
+                                     self.lds_bytes, prof)
                 if lid_vec is not None:
                     self._last_lid = (lid_vec, lid_cnt)
                 for kind, width, prefix in layout:
@@ -217,8 +253,9 @@ class DeviceRunner:
             for i in c4_here:
                 rec = torch.zeros(7 * ndocs, dtype=torch.int64, device=self.device)
                 src = torch.zeros(2 * ndocs, dtype=torch.int64, device=self.device)
+                prof = self._prof_buf(ndocs, keep, f"c4_step{i}")
                 self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm, ndocs, scratch, d_soff, pw, pw_n, rec, src, flags,
-                                 self.lds_bytes_c4)
+                                 self.lds_bytes_c4, prof)
                 new_off = torch.zeros(ndocs + 1, dtype=torch.int64, device=self.device)
                 torch.cumsum(src.view(ndocs, 2)[:, 1], 0, out=new_off[1:])
                 cap = vlen + self.c4_growth * ndocs + 16  # device rewrites never grow more (kC4MaxGrowth)

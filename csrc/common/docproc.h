@@ -97,10 +97,14 @@ struct DocCtx {
   TB_HD Mark mark() const { return Mark{used, lused}; }
   TB_HD void reset(Mark m) { used = m.g; lused = m.l; }
 
-  // Working arrays go to LDS while it has room (addressed through generic pointers, so the
-  // algorithm code is the same for both arenas), then to the HBM scratch arena.
+  // Placement: big streaming per-code-point arrays live in the HBM scratch arena (alloc);
+  // small randomly-accessed ones (hash tables, per-word / per-n-gram arrays, reduction
+  // buffers) go to the wave's LDS slice while it has room (alloc_hot), then to HBM. Both are
+  // addressed through generic pointers, so algorithm code is the same for either arena.
   template <class T>
-  TB_HD T* alloc(uint64_t count) {
+  TB_HD T* alloc(uint64_t count) { return alloc_global<T>(count); }
+  template <class T>
+  TB_HD T* alloc_hot(uint64_t count) {
     if (lds) {
       const uint64_t a = (lused + 15u) & ~15u;
       const uint64_t e = a + count * sizeof(T);
@@ -269,8 +273,8 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
   while (capn < 2 * n + 2) capn <<= 1;
   const uint32_t mask = capn - 1;
   const auto mark = x.mark();
-  uint64_t* keys = x.template alloc<uint64_t>(capn);
-  uint32_t* vals = x.template alloc<uint32_t>(capn);
+  uint64_t* keys = x.template alloc_hot<uint64_t>(capn);
+  uint32_t* vals = x.template alloc_hot<uint32_t>(capn);
   if (x.overflow) return;
   x.par.for_n(capn, [&](uint32_t i) { keys[i] = 0; vals[i] = 0xFFFFFFFFu; });
   x.par.sync();
@@ -310,7 +314,7 @@ template <class P, class SpanF>
 TB_HD void dup_spans(DocCtx<P>& x, const uint8_t* b, const uint64_t* PH, uint32_t n, SpanF&& span,
                      int64_t* out_elems, int64_t* out_bytes) {
   const auto mark = x.mark();
-  uint32_t* canon = x.template alloc<uint32_t>(n + 1);
+  uint32_t* canon = x.template alloc_hot<uint32_t>(n + 1);
   if (x.overflow) return;
   const uint64_t* pw = x.pw;
   canonicalize(
@@ -521,11 +525,11 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
   // ---- n-gram statistics over the words ----
   const uint32_t W = w.n;
   if (ds.n_top + ds.n_dup > 0) {
+    uint32_t* wid = x.template alloc_hot<uint32_t>(W + 1);
+    uint32_t* WL = x.template alloc_hot<uint32_t>(W + 1);
+    uint64_t* PI = x.template alloc_hot<uint64_t>(W + 1);
+    uint64_t* PW = x.template alloc_hot<uint64_t>(W + 1);
     uint64_t* wh = x.template alloc<uint64_t>(W + 1);
-    uint32_t* wid = x.template alloc<uint32_t>(W + 1);
-    uint32_t* WL = x.template alloc<uint32_t>(W + 1);
-    uint64_t* PI = x.template alloc<uint64_t>(W + 1);
-    uint64_t* PW = x.template alloc<uint64_t>(W + 1);
     if (x.overflow) return;
     x.par.for_n(W, [&](uint32_t k) { wh[k] = sub_hash(PH, pw, w.bs[k], w.be[k]); });
     x.par.sync();
@@ -560,8 +564,8 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       if (n > 0 && W >= n) {
         const uint32_t G = W - n + 1;
         const auto m2 = x.mark();
-        uint32_t* gc = x.template alloc<uint32_t>(G);
-        uint32_t* cnt = x.template alloc<uint32_t>(G);
+        uint32_t* gc = x.template alloc_hot<uint32_t>(G);
+        uint32_t* cnt = x.template alloc_hot<uint32_t>(G);
         if (x.overflow) return;
         const uint64_t pn = x.powb(n);
         canonicalize(
@@ -589,14 +593,14 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     x.stamp(PH_GR_TOP);
     if (ds.n_dup > 0) {
       // per-n canonical-gram arrays and visited bitmaps; their scratch offsets are kept in scratch
-      uint64_t* gofs = x.template alloc<uint64_t>(2 * kMaxNgramEntries);
+      uint64_t* gofs = x.template alloc_hot<uint64_t>(2 * kMaxNgramEntries);
       if (x.overflow) return;
       for (int t = 0; t < ds.n_dup; ++t) {
         const uint32_t n = (uint32_t)ds.dup_n[t];
         if (n == 0 || W < n) continue;
         const uint32_t G = W - n + 1;
-        uint32_t* gct = x.template alloc<uint32_t>(G);
-        uint32_t* sn = x.template alloc<uint32_t>((G + 31) / 32 + 1);
+        uint32_t* gct = x.template alloc_hot<uint32_t>(G);
+        uint32_t* sn = x.template alloc_hot<uint32_t>((G + 31) / 32 + 1);
         if (x.overflow) return;
         x.par.single([&]() {
           gofs[2 * t] = (uint64_t)(uintptr_t)gct;  // generic pointers (LDS or HBM)
@@ -653,42 +657,72 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
   x.reset(mark);
 }
 
+// Language-id features straight from the UTF-8 bytes: every code point position (a UTF-8 lead
+// byte, as decode() defines them) of the first kLidMaxCps code points, plus the virtual end
+// position, emits the 1..3-grams ending there (lid_grams_at); their embedding rows are summed
+// in exact fixed point. Neighbouring letters are found by stepping back to the previous lead
+// bytes, so no per-code-point arrays are needed: this runs as its own small kernel on the
+// device (k_langid_features) and inside the stage emulation on the host.
+TB_HD uint32_t lid_letter(const UcdView& ucd, const uint8_t* b, uint32_t n, int64_t s) {
+  if (s < 0) return 0;
+  int len;
+  const uint32_t c = utf8_decode(b, (uint32_t)s, n, &len);
+  if (!(ucd.props(c) & P_ALPHA)) return 0;
+  const uint32_t l = ucd.lower(c);
+  return l ? l : c;
+}
+TB_HD int64_t prev_lead(const uint8_t* b, int64_t s) {
+  int64_t k = s - 1;
+  while (k >= 0 && !utf8_is_lead(b[k])) --k;
+  return k;
+}
+
 template <class P>
-TB_HD void langid_features(DocCtx<P>& x, const Cps& c, const uint16_t* emb, StageOut& out) {
-  const uint32_t lim = c.n < (uint32_t)kLidMaxCps ? c.n : (uint32_t)kLidMaxCps;
-  const uint32_t* cp = c.cp;
-  const uint32_t* prop = c.prop;
+TB_HD void langid_features_bytes(DocCtx<P>& x, const uint8_t* b, uint32_t n, const uint16_t* emb,
+                                 uint16_t* vec, int32_t* cnt_out) {
   const UcdView ucd = x.ucd;
-  auto Lf = [&](int64_t i) -> uint32_t {
-    if (i < 0 || i >= (int64_t)lim) return 0;
-    if (!(prop[i] & P_ALPHA)) return 0;
-    uint32_t l = ucd.lower(cp[i]);
-    return l ? l : cp[i];
-  };
   const auto mark = x.mark();
-  uint32_t* goff = x.template alloc<uint32_t>(lim + 2);
+  constexpr int D = kLidDim + 1;  // 32 embedding dims + the n-gram count
+  int32_t* tmp = x.template alloc_hot<int32_t>(64 * D);
+  int64_t* sums = x.template alloc_hot<int64_t>(D);
+  uint32_t* limb = x.template alloc_hot<uint32_t>(1);
   if (x.overflow) return;
-  const uint32_t K = x.par.template scan<uint32_t>(
-      lim + 1, 0u, [](uint32_t a, uint32_t b2) { return a + b2; },
-      [&](uint32_t i) { return (uint32_t)lid_grams_at(Lf((int64_t)i - 2), Lf((int64_t)i - 1), Lf(i), true, true, [](uint32_t) {}); },
-      [&](uint32_t i, uint32_t e) { goff[i] = e; });
-  uint32_t* G = x.template alloc<uint32_t>(K + 1);
-  if (x.overflow) return;
+  // byte offset of code point kLidMaxCps (the cut), or n
+  x.par.single([&]() { *limb = n; });
   x.par.sync();
-  x.par.for_n(lim + 1, [&](uint32_t i) {
-    uint32_t o = goff[i];
-    lid_grams_at(Lf((int64_t)i - 2), Lf((int64_t)i - 1), Lf(i), true, true, [&](uint32_t bk) { G[o++] = bk; });
+  if (n > (uint32_t)kLidMaxCps) {
+    x.par.template compact<int>(
+        n, [&](uint32_t i, int&) { return utf8_is_lead(b[i]); },
+        [&](uint32_t i, uint32_t k, int&) { if (k == (uint32_t)kLidMaxCps) *limb = i; });
+    x.par.sync();
+  }
+  const uint32_t lim = *limb;
+  // A lane visits ceil((lim + 1) / 64) <= 257 byte positions (lim <= 4 * kLidMaxCps) with at most
+  // 3 grams each, and |fixed(e)| < 2^21 (|e| < 32, checked at model load): int32 partials
+  // cannot overflow.
+  x.par.template accum_rows<D>(
+      lim + 1,
+      [&](uint32_t s, int32_t* part) {
+        if (s < lim && !utf8_is_lead(b[s])) return;
+        const uint32_t l0 = s < lim ? lid_letter(ucd, b, n, s) : 0u;
+        const int64_t p1 = prev_lead(b, s);
+        const uint32_t lm1 = lid_letter(ucd, b, n, p1);
+        const uint32_t lm2 = p1 >= 0 ? lid_letter(ucd, b, n, prev_lead(b, p1)) : 0u;
+        lid_grams_at(lm2, lm1, l0, true, true, [&](uint32_t bk) {
+          const uint16_t* row = emb + (size_t)bk * kLidDim;
+#pragma unroll
+          for (int d = 0; d < kLidDim; ++d) part[d] += lid_fixed(row[d]);
+          part[kLidDim] += 1;
+        });
+      },
+      tmp, sums);
+  const int64_t K = sums[kLidDim];
+  x.par.for_n((uint32_t)kLidDim, [&](uint32_t d) {
+    float v = K ? (float)((double)sums[d] / (double)K / (double)kLidFixedScale) : 0.0f;
+    vec[d] = f32_to_bf16(v);
   });
+  x.par.single([&]() { *cnt_out = (int32_t)K; });
   x.par.sync();
-  const uint32_t doc = out.doc;
-  uint16_t* vec = out.lid_vec + (size_t)doc * kLidDim;
-  x.par.template gather_rows_fixed<kLidDim>(
-      K, [&](uint32_t k) { return emb + (size_t)G[k] * kLidDim; },
-      [&](int d, int64_t sum) {
-        float v = K ? (float)((double)sum / (double)K / (double)kLidFixedScale) : 0.0f;
-        vec[d] = f32_to_bf16(v);
-      });
-  x.par.single([&]() { out.lid_cnt[doc] = (int32_t)K; });
   x.reset(mark);
 }
 
@@ -930,7 +964,7 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
 // ---------------------------------------------------------------------------------------------
 // Stage analysis for one content version: writes the records of every step of the stage.
 
-template <class P>
+template <class P, bool kWithLid = true>
 TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
                          const uint16_t* lid_emb, const uint8_t* b, uint32_t n, StageOut& out) {
   bool need_words = false, need_lines = false, need_ph = false, need_lid = false;
@@ -1041,7 +1075,9 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
       x.reset(mark);
       x.stamp(PH_FW);
     } else if (ds.kind == DK_LANGID) {
-      langid_features(x, c, lid_emb, out);
+      // on the device this runs as a separate kernel (k_langid_features): lid_emb == nullptr
+      if constexpr (kWithLid)
+        if (lid_emb) langid_features_bytes(x, b, n, lid_emb, out.lid_vec + (size_t)out.doc * kLidDim, out.lid_cnt + out.doc);
       x.stamp(PH_LID);
     }
     if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }

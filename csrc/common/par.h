@@ -77,6 +77,21 @@ struct SeqPar {
   static void min32(uint32_t* p, uint32_t v) { if (v < *p) *p = v; }
   static void max32(uint32_t* p, uint32_t v) { if (v > *p) *p = v; }
   static uint32_t add32(uint32_t* p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
+  // Integer accumulation over items: f(i, part) adds item i's contribution into part[0..D)
+  // (int32 partials); sums[d] receives the exact int64 total. tmp is unused on the host.
+  template <int D, class F>
+  void accum_rows(uint32_t n, F&& f, int32_t* tmp, int64_t* sums) const {
+    (void)tmp;
+    int64_t acc[D];
+    int32_t part[D];
+    for (int d = 0; d < D; ++d) acc[d] = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      for (int d = 0; d < D; ++d) part[d] = 0;
+      f(i, part);
+      for (int d = 0; d < D; ++d) acc[d] += part[d];
+    }
+    for (int d = 0; d < D; ++d) sums[d] = acc[d];
+  }
   // Sum of fixed-point embedding rows: out(d, sum_k fixed(E[rows[k]][d])) for d < D.
   template <int D, class Row, class Out>
   void gather_rows_fixed(uint32_t K, Row&& row_ptr, Out&& out) const {
@@ -176,6 +191,26 @@ struct WavePar {
   __device__ static void max32(uint32_t* p, uint32_t v) { atomicMax(p, v); }
   __device__ static uint32_t add32(uint32_t* p, uint32_t v) { return atomicAdd(p, v); }
 
+  // Each lane accumulates its items (i = lane, lane+64, ...) in D int32 registers, so the
+  // item loads of one lane are independent of the other lanes' and of each other; the 64 x D
+  // partials then go through `tmp` (64*D int32, LDS when available) and lane d sums column d
+  // in int64. Callers bound the per-lane magnitude so int32 partials cannot overflow.
+  template <int D, class F>
+  __device__ void accum_rows(uint32_t n, F&& f, int32_t* tmp, int64_t* sums) const {
+    int32_t part[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) part[d] = 0;
+    for (uint32_t i = lane; i < n; i += 64) f(i, part);
+#pragma unroll
+    for (int d = 0; d < D; ++d) tmp[lane * D + d] = part[d];
+    __syncthreads();
+    for (int d = (int)lane; d < D; d += 64) {
+      int64_t s = 0;
+      for (int r = 0; r < 64; ++r) s += tmp[r * D + d];
+      sums[d] = s;
+    }
+    __syncthreads();
+  }
   template <int D, class Row, class Out>
   __device__ void gather_rows_fixed(uint32_t K, Row&& row_ptr, Out&& out) const {
     static_assert(D == 32, "lane layout assumes 32 dims");

@@ -62,7 +62,25 @@ __global__ __launch_bounds__(64) void k_stage_analyze(
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, lid_vec, lid_cnt};
-  analyze_stage(x, *stage, *plan, lid_emb, b, n, out);
+  analyze_stage<WavePar, false>(x, *stage, *plan, lid_emb, b, n, out);  // LD features: k_langid_features
+}
+
+// Language-id n-gram bag of one document per wave (own kernel: its 33 accumulators per lane
+// would otherwise set the register budget, and so the occupancy, of the whole stage kernel).
+__global__ __launch_bounds__(64) void k_langid_features(
+    const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off, const int32_t* __restrict__ perm,
+    int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off, DevTables tabs,
+    const uint16_t* __restrict__ emb, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t* flags, uint32_t lds_bytes,
+    uint64_t* prof) {
+  const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
+  if (doc >= ndocs) return;
+  DocCtx<WavePar> x = make_ctx(tabs, nullptr, 0, scratch, scratch_off, doc, flags, lds_bytes, prof);
+  const uint8_t* b = bytes + off[doc];
+  const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
+  x.stamp(PH_START);
+  langid_features_bytes(x, b, n, emb, lid_vec + (size_t)doc * kLidDim, lid_cnt + doc);
+  x.stamp(PH_LID);
+  if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
 }
 
 __global__ __launch_bounds__(64) void k_c4_pass_a(
@@ -176,6 +194,21 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
   return (int)hipGetLastError();
 }
 
+int tb_langid_features(hipStream_t stream, const uint8_t* bytes, const int64_t* off, const int32_t* perm,
+                       int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint16_t* s1,
+                       const uint32_t* s2, const uint16_t* l1, const int32_t* l2, const uint16_t* emb,
+                       uint16_t* lid_vec, int32_t* lid_cnt, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
+  if (ndocs <= 0) return 0;
+  if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
+  DevTables t{s1, s2, l1, l2};
+  if (lds_bytes > 65536)
+    (void)hipFuncSetAttribute((const void*)k_langid_features, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds_bytes);
+  hipLaunchKernelGGL(k_langid_features, dim3(ndocs), dim3(64), lds_bytes, stream, bytes, off, perm, ndocs, scratch,
+                     scratch_off, t, emb, lid_vec, lid_cnt, flags, lds_bytes, prof);
+  return (int)hipGetLastError();
+}
+
 int tb_c4_pass_a(hipStream_t stream, const void* c4, const uint8_t* bytes, const int64_t* off, const int32_t* perm,
                  int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n,
                  const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
@@ -214,7 +247,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 
 int tb_phase_slots() { return kPhaseSlots; }
 
-int tb_abi_version() { return 1; }
+int tb_abi_version() { return 2; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

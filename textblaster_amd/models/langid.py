@@ -51,6 +51,11 @@ def load(path: str) -> LangidWeights:
     h = native.host()
     if emb.size != h.LID_BUCKETS * h.LID_DIM or w.size != h.LID_DIM * h.LID_LANGS_PAD or b.size != h.LID_LANGS_PAD:
         raise ValueError(f"language model {path} has the wrong shape")
+    # the device accumulates n-gram rows in int32 fixed point per lane (docproc.h
+    # langid_features_bytes): |e| < 32 keeps every partial sum below 2^31
+    emax = float(np.abs((emb.astype(np.uint32) << 16).view(np.float32)).max()) if emb.size else 0.0
+    if not emax < 32.0:
+        raise ValueError(f"language model {path}: embedding magnitude {emax} out of range (< 32)")
     return LangidWeights(emb, w, b)
 
 

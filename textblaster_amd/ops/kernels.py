@@ -19,6 +19,7 @@ _I64 = ctypes.c_int64
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
     "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
+    "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
     "tb_c4_pass_b": [_P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "tb_langid_head": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I32, _P],
     "tb_pow_table": [_P, _P, _U32],
@@ -88,6 +89,15 @@ class Kernels:
             t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), _ptr(lid_emb), _ptr(lid_vec),
             _ptr(lid_cnt), lds_bytes, _ptr(prof))
         _check(rc, "tb_stage_analyze")
+
+    def langid_features(self, bytes_, off, perm, ndocs, scratch, scratch_off, emb, vec, cnt, flags, lds_bytes=0,
+                        prof=None):
+        t = self.tabs
+        rc = self.lib.tb_langid_features(
+            self.stream(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs, scratch.data_ptr(),
+            scratch_off.data_ptr(), t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), emb.data_ptr(),
+            vec.data_ptr(), cnt.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof))
+        _check(rc, "tb_langid_features")
 
     def c4_pass_a(self, c4, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags, lds_bytes=0,
                   prof=None):

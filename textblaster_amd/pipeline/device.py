@@ -120,6 +120,7 @@ class DeviceRunner:
 
         self.lds_bytes = int(os.environ.get("TB_LDS_BYTES", str(self.DEFAULT_LDS_BYTES)))
         self.lds_bytes_c4 = int(os.environ.get("TB_LDS_BYTES_C4", str(self.lds_bytes)))
+        self.lds_bytes_lid = int(os.environ.get("TB_LDS_BYTES_LID", "9216"))  # 64x33 int32 partials + sums
         # TB_PHASE_PROF=1: per-document phase cycle counters (s_memtime stamps) for profiling
         self.phase_prof = os.environ.get("TB_PHASE_PROF", "") not in ("", "0")
         self.phase_totals: Dict[str, np.ndarray] = {}
@@ -239,6 +240,9 @@ class DeviceRunner:
                 if any(kind == 4 for kind, _, _ in layout):
                     lid_vec = torch.zeros(ndocs * h.LID_DIM, dtype=torch.int16, device=self.device)
                     lid_cnt = torch.zeros(ndocs, dtype=torch.int32, device=self.device)
+                if lid_vec is not None:
+                    self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec, lid_cnt,
+                                           flags, self.lds_bytes_lid, self._prof_buf(ndocs, keep, f"langid{s}"))
                 prof = self._prof_buf(ndocs, keep, f"stage{s}")
                 self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm, ndocs, scratch, d_soff, pw, pw_n,
                                      rec, flags, self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,

@@ -734,13 +734,33 @@ TB_HD bool end_punct(uint32_t c) {
   return c == '.' || c == '!' || c == '?' || c == '"' || c == '\'' || c == 0x201D;
 }
 
+// Case-insensitive prefix test with the same folding as ci_contains (ASCII letters, and
+// U+212A KELVIN SIGN as 'k'): does `pat` start at b[0] within n bytes?
+TB_HD bool ci_starts_with(const uint8_t* b, uint32_t n, const char* pat, int plen) {
+  uint32_t i = 0;
+  for (int j = 0; j < plen; ++j) {
+    if (i >= n) return false;
+    const char pc = pat[j];
+    uint8_t c = b[i];
+    if (c >= 'A' && c <= 'Z') c = (uint8_t)(c + 32);
+    if (c == (uint8_t)pc) { ++i; continue; }
+    if (pc == 'k' && i + 2 < n && b[i] == 0xE2 && b[i + 1] == 0x84 && b[i + 2] == 0xAA) { i += 3; continue; }
+    return false;
+  }
+  return true;
+}
+
+// Bits of the per-line pattern flags (c4_pass_a)
+enum : uint32_t { C4F_JS = 1, C4F_POLICY = 2 };
+
 template <class P>
 TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, int64_t* r, int64_t* src) {
   x.stamp(PH_START);
+  // lowercase().contains("lorem ipsum") == the pattern starts (case-folded) at some 'l'/'L'
   const uint32_t lorem = c4.filter_lorem_ipsum
       ? x.par.template sum<uint32_t>(n, [&](uint32_t s) {
           if (b[s] != 'l' && b[s] != 'L') return 0u;
-          return ci_contains(b + s, n - s < 16 ? n - s : 16, "lorem ipsum", 11) ? 1u : 0u;
+          return ci_starts_with(b + s, n - s, "lorem ipsum", 11) ? 1u : 0u;
         })
       : 0u;
   const uint32_t curly = c4.filter_curly_bracket
@@ -809,7 +829,27 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   }
   x.par.sync();
   x.stamp(PH_C4_LINES);
-  // ---- citation removal -> processed line lengths ----
+  // ---- citation removal -> processed lines Pb (every step parallel over code points) ----
+  // lid[j]: the line whose trimmed span holds code point j (kNoLine otherwise), by a max-scan
+  // of line-start markers (lines are ordered and disjoint).
+  constexpr uint32_t kNoLine = 0xFFFFFFFFu;
+  uint32_t* lid = x.template alloc<uint32_t>(C + 1);
+  uint32_t* Pw = x.template alloc<uint32_t>(C + 1);   // exclusive prefix of kept bytes
+  uint8_t* rm = x.template alloc<uint8_t>(C + 1);     // inside a removed citation
+  uint32_t* plen = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* poff = x.template alloc_hot<uint32_t>(NLn + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  x.par.for_n(C, [&](uint32_t j) { lid[j] = 0; rm[j] = 0; });
+  x.par.sync();
+  x.par.for_n(NLn, [&](uint32_t k) { if (la[k] < lb[k]) lid[la[k]] = k + 1; });
+  x.par.sync();
+  x.par.template scan<uint32_t>(
+      C, 0u, [](uint32_t a, uint32_t b2) { return a > b2 ? a : b2; }, [&](uint32_t j) { return lid[j]; },
+      [&](uint32_t j, uint32_t e) {
+        const uint32_t cur = e > lid[j] ? e : lid[j];  // inclusive max
+        lid[j] = (cur > 0 && j < lb[cur - 1]) ? cur - 1 : kNoLine;
+      });
+  x.par.sync();
   auto cite_end = [&](uint32_t j, uint32_t e) -> uint32_t {  // cp index past a citation at j, or 0
     if (cp[j] != '[') return 0;
     uint32_t p = j + 1;
@@ -827,63 +867,88 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
     }
     return (p < e && cp[p] == ']') ? p + 1 : 0;
   };
-  uint32_t* plen = x.template alloc<uint32_t>(NLn + 1);
-  uint32_t* poff = x.template alloc<uint32_t>(NLn + 1);
-  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   const bool rmc = c4.remove_citations != 0;
-  x.par.for_n(NLn, [&](uint32_t k) {
-    uint32_t removed = 0;
-    if (rmc) {
-      for (uint32_t j = la[k]; j < lb[k];) {
-        uint32_t ce = cite_end(j, lb[k]);
-        if (ce) { removed += off[ce] - off[j]; j = ce; } else { ++j; }
-      }
-    }
-    plen[k] = off[lb[k]] - off[la[k]] - removed;
-  });
+  if (rmc) {
+    // a citation holds only digits, commas, whitespace and ']': no '[' inside one, so every
+    // '[' can be tested independently (same result as the left-to-right scan)
+    x.par.for_n(C, [&](uint32_t j) {
+      if (cp[j] != '[' || lid[j] == kNoLine) return;
+      const uint32_t ce = cite_end(j, lb[lid[j]]);
+      for (uint32_t q = j; q < ce; ++q) rm[q] = 1;
+    });
+    x.par.sync();
+  }
+  auto kept_bytes = [&](uint32_t j) -> uint32_t {
+    return (lid[j] != kNoLine && !rm[j]) ? off[j + 1] - off[j] : 0u;
+  };
+  const uint32_t Ktot = x.par.template scan<uint32_t>(
+      C, 0u, [](uint32_t a, uint32_t b2) { return a + b2; }, kept_bytes, [&](uint32_t j, uint32_t e) { Pw[j] = e; });
+  x.par.single([&]() { Pw[C] = Ktot; });
   x.par.sync();
-  const uint32_t Ptot = x.par.template scan<uint32_t>(
-      NLn, 0u, [](uint32_t a, uint32_t b2) { return a + b2; }, [&](uint32_t k) { return plen[k] + 1; },
-      [&](uint32_t k, uint32_t e) { poff[k] = e; });
+  x.par.for_n(NLn, [&](uint32_t k) {
+    plen[k] = Pw[lb[k]] - Pw[la[k]];
+    poff[k] = Pw[la[k]] + k;  // kept bytes of the earlier lines + one '\n' per earlier line
+  });
+  const uint32_t Ptot = Ktot + NLn;
   uint8_t* Pb = x.template alloc<uint8_t>(Ptot + 1);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
-  x.par.for_n(NLn, [&](uint32_t k) {
-    uint32_t o = poff[k];
-    for (uint32_t j = la[k]; j < lb[k];) {
-      uint32_t ce = rmc ? cite_end(j, lb[k]) : 0;
-      if (ce) { j = ce; continue; }
-      for (uint32_t q = off[j]; q < off[j + 1]; ++q) Pb[o++] = b[q];
-      ++j;
-    }
-    Pb[o] = '\n';
+  x.par.sync();
+  x.par.for_n(C, [&](uint32_t j) {
+    const uint32_t nb = kept_bytes(j);
+    if (!nb) return;
+    uint8_t* d = Pb + Pw[j] + lid[j];
+    for (uint32_t q = 0; q < nb; ++q) d[q] = b[off[j] + q];
   });
+  x.par.for_n(NLn, [&](uint32_t k) { Pb[poff[k] + plen[k]] = '\n'; });
   x.par.single([&]() { poff[NLn] = Ptot; });
   x.par.sync();
   x.stamp(PH_C4_CITE);
   // ---- words of the processed lines ----
   Cps pc = decode(x, Pb, Ptot);
   Words pwd = words(x, pc);
-  uint32_t* nw = x.template alloc<uint32_t>(NLn + 1);
-  uint32_t* mx = x.template alloc<uint32_t>(NLn + 1);
-  uint8_t* code = x.template alloc<uint8_t>(NLn + 1);
+  uint32_t* nw = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* mx = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* pf = x.template alloc_hot<uint32_t>(NLn + 1);  // pattern flags per line
+  uint8_t* code = x.template alloc_hot<uint8_t>(NLn + 1);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
-  x.par.for_n(NLn, [&](uint32_t k) { nw[k] = 0; mx[k] = 0; });
+  x.par.for_n(NLn, [&](uint32_t k) { nw[k] = 0; mx[k] = 0; pf[k] = 0; });
   x.par.sync();
-  x.par.for_n(pwd.n, [&](uint32_t q) {
-    const uint32_t bs = pwd.bs[q];
-    uint32_t lo = 0, hi = NLn;  // last line with poff <= bs
+  auto line_of_byte = [&](uint32_t bs) {  // last line with poff <= bs
+    uint32_t lo = 0, hi = NLn;
     while (hi - lo > 1) {
       uint32_t mid = (lo + hi) >> 1;
       if (poff[mid] <= bs) lo = mid; else hi = mid;
     }
+    return lo;
+  };
+  x.par.for_n(pwd.n, [&](uint32_t q) {
+    const uint32_t lo = line_of_byte(pwd.bs[q]);
     P::add32(&nw[lo], 1u);
     P::max32(&mx[lo], pwd.ce[q] - pwd.cs[q]);
   });
-  x.par.sync();
   x.stamp(PH_C4_WORDS);
-  const char* const kPol[6] = {"terms of use", "privacy policy", "cookie policy",
-                                      "uses cookies", "use of cookies", "use cookies"};
-  const int kPolLen[6] = {12, 14, 13, 12, 14, 11};
+  // javascript / policy phrases: to_lowercase().contains() per line == a case-folded match
+  // starting at some byte of the line; every byte position is tested in parallel.
+  if (c4.filter_javascript || c4.filter_policy) {
+    const char* const kPol[6] = {"terms of use", "privacy policy", "cookie policy",
+                                 "uses cookies", "use of cookies", "use cookies"};
+    const int kPolLen[6] = {12, 14, 13, 12, 14, 11};
+    x.par.for_n(Ptot, [&](uint32_t s) {
+      uint8_t c0 = Pb[s];
+      if (c0 >= 'A' && c0 <= 'Z') c0 = (uint8_t)(c0 + 32);
+      if (c0 != 'j' && c0 != 't' && c0 != 'p' && c0 != 'c' && c0 != 'u') return;
+      const uint32_t k = line_of_byte(s);
+      const uint32_t lend = poff[k] + plen[k];
+      if (s >= lend) return;
+      uint32_t bits = 0;
+      if (c4.filter_javascript && c0 == 'j' && ci_starts_with(Pb + s, lend - s, "javascript", 10)) bits |= C4F_JS;
+      if (c4.filter_policy)
+        for (int t = 0; t < 6; ++t)
+          if (kPol[t][0] == (char)c0 && ci_starts_with(Pb + s, lend - s, kPol[t], kPolLen[t])) { bits |= C4F_POLICY; break; }
+      if (bits) P::or32(&pf[k], bits);
+    });
+  }
+  x.par.sync();
   x.par.for_n(NLn, [&](uint32_t k) {
     const uint8_t* lp = Pb + poff[k];
     const uint32_t ln = plen[k];
@@ -902,11 +967,8 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
       if (!term || ell) cd = 2;
     }
     if (cd == 0 && c4.min_words_per_line > 0 && (int64_t)nw[k] < c4.min_words_per_line) cd = 3;
-    if (cd == 0 && c4.filter_javascript && ci_contains(lp, ln, "javascript", 10)) cd = 4;
-    if (cd == 0 && c4.filter_policy) {
-      for (int t = 0; t < 6; ++t)
-        if (ci_contains(lp, ln, kPol[t], kPolLen[t])) { cd = 5; break; }
-    }
+    if (cd == 0 && c4.filter_javascript && (pf[k] & C4F_JS)) cd = 4;
+    if (cd == 0 && c4.filter_policy && (pf[k] & C4F_POLICY)) cd = 5;
     code[k] = cd;
   });
   x.par.sync();
@@ -914,20 +976,25 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   const int64_t s_punct = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 2); });
   const int64_t s_few = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 3); });
   x.stamp(PH_C4_CODES);
-  // ---- joined kept lines ----
-  uint32_t* joff = x.template alloc<uint32_t>(NLn + 1);
+  // ---- joined kept lines (HBM: read back by pass B), scattered per code point ----
+  uint32_t* joff = x.template alloc_hot<uint32_t>(NLn + 1);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   uint32_t Jtot = x.par.template scan<uint32_t>(
       NLn, 0u, [](uint32_t a, uint32_t b2) { return a + b2; },
       [&](uint32_t k) { return code[k] == 0 ? plen[k] + 1 : 0u; }, [&](uint32_t k, uint32_t e) { joff[k] = e; });
   if (Jtot > 0) Jtot -= 1;
-  uint8_t* Jb = x.template alloc_global<uint8_t>(Jtot + 1);  // read back by pass B: HBM
+  uint8_t* Jb = x.template alloc_global<uint8_t>(Jtot + 1);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  x.par.sync();
+  x.par.for_n(C, [&](uint32_t j) {
+    const uint32_t nb = kept_bytes(j);
+    if (!nb || code[lid[j]] != 0) return;
+    const uint32_t k = lid[j];
+    uint8_t* d = Jb + joff[k] + (Pw[j] - Pw[la[k]]);
+    for (uint32_t q = 0; q < nb; ++q) d[q] = b[off[j] + q];
+  });
   x.par.for_n(NLn, [&](uint32_t k) {
-    if (code[k] != 0) return;
-    const uint32_t o = joff[k];
-    for (uint32_t q = 0; q < plen[k]; ++q) Jb[o + q] = Pb[poff[k] + q];
-    if (o + plen[k] < Jtot) Jb[o + plen[k]] = '\n';
+    if (code[k] == 0 && joff[k] + plen[k] < Jtot) Jb[joff[k] + plen[k]] = '\n';
   });
   x.par.sync();
   x.stamp(PH_C4_JOIN);

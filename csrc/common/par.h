@@ -59,8 +59,9 @@ struct SeqPar {
   T scan(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
     T acc = id;
     for (uint32_t i = 0; i < n; ++i) {
+      const T v = in(i);  // read before out(i) may overwrite what in(i) reads (as on the device)
       out(i, acc);
-      acc = op(acc, in(i));
+      acc = op(acc, v);
     }
     return acc;
   }
@@ -77,6 +78,7 @@ struct SeqPar {
   static void min32(uint32_t* p, uint32_t v) { if (v < *p) *p = v; }
   static void max32(uint32_t* p, uint32_t v) { if (v > *p) *p = v; }
   static uint32_t add32(uint32_t* p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
+  static void or32(uint32_t* p, uint32_t v) { *p |= v; }
   // Integer accumulation over items: f(i, part) adds item i's contribution into part[0..D)
   // (int32 partials); sums[d] receives the exact int64 total. tmp is unused on the host.
   template <int D, class F>
@@ -190,6 +192,7 @@ struct WavePar {
   __device__ static void min32(uint32_t* p, uint32_t v) { atomicMin(p, v); }
   __device__ static void max32(uint32_t* p, uint32_t v) { atomicMax(p, v); }
   __device__ static uint32_t add32(uint32_t* p, uint32_t v) { return atomicAdd(p, v); }
+  __device__ static void or32(uint32_t* p, uint32_t v) { atomicOr(p, v); }
 
   // Each lane accumulates its items (i = lane, lane+64, ...) in D int32 registers, so the
   // item loads of one lane are independent of the other lanes' and of each other; the 64 x D

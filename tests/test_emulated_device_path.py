@@ -11,7 +11,11 @@ from textblaster_amd.utils import synth
 EDGE = ["", "   ", "\n\n", "a", "a\r\nb\r\n", "Hello.\n\n\nHello.\n\nHello.", "x [1] y [2, 3]. z",
         "ΣΑΣ ΣΑΣ.", "İstanbul THE the", "cooKie policy is here.", "lorem IPSUM dolor", "{ curly }",
         "日本語のテキストです。", "mixed 日本 text. Another sentence here.", "- bullet\n- bullet\n• x...",
-        "Hi?There!Again.Yes" * 3]
+        "Hi?There!Again.Yes" * 3,
+        "Use of coo\u212Aies here, for all.\nJavaScript is needed. Yes it is.\n[1] [2,3] [4, 5, 6] text [a] [12\n"
+        "Terms of USE apply to all lines here.\nA normal line that is fine. Another one.\nPRIVACY policy.",
+        "Line one [1, 2 ,3] cites [99].\n\n  Indented line with words in it.  \nEnds with ellipsis...\nok.",
+        "text with LOREM IPSUM inside"]
 
 
 def outputs(res):

@@ -615,6 +615,11 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
             },
             [&](uint32_t p, uint32_t q) {
               if (WL[p + n] - WL[p] != WL[q + n] - WL[q]) return false;
+              // same canonical word sequence => same concatenation (the common case); only
+              // different word splits of equal-hash text need the byte comparison
+              bool same = true;
+              for (uint32_t k = 0; k < n && same; ++k) same = wid[p + k] == wid[q + k];
+              if (same) return true;
               uint32_t wp = p, wq = q, bp = w.bs[p], bq = w.bs[q];
               const uint32_t L = WL[p + n] - WL[p];
               for (uint32_t i = 0; i < L; ++i) {

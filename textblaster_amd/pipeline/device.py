@@ -88,7 +88,10 @@ class PendingBatch:
 
 class DeviceRunner:
     N_SLOTS = 2
-    DEFAULT_LDS_BYTES = 12288
+    # per-wave LDS slices: the stage kernel runs at 3 waves/SIMD (VGPR-bound) = 12 waves/CU, so
+    # 13 KB each costs no occupancy; the C4 kernel (7 waves/SIMD) only keeps per-line arrays there
+    DEFAULT_LDS_BYTES = 13312
+    DEFAULT_LDS_BYTES_C4 = 2048
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None):
         import torch
@@ -119,7 +122,7 @@ class DeviceRunner:
         import os
 
         self.lds_bytes = int(os.environ.get("TB_LDS_BYTES", str(self.DEFAULT_LDS_BYTES)))
-        self.lds_bytes_c4 = int(os.environ.get("TB_LDS_BYTES_C4", str(self.lds_bytes)))
+        self.lds_bytes_c4 = int(os.environ.get("TB_LDS_BYTES_C4", str(self.DEFAULT_LDS_BYTES_C4)))
         self.lds_bytes_lid = int(os.environ.get("TB_LDS_BYTES_LID", "9216"))  # 64x33 int32 partials + sums
         # TB_PHASE_PROF=1: per-document phase cycle counters (s_memtime stamps) for profiling
         self.phase_prof = os.environ.get("TB_PHASE_PROF", "") not in ("", "0")

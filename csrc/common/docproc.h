@@ -173,7 +173,7 @@ TB_HD uint64_t* prefix_hash(DocCtx<P>& x, const uint8_t* b, uint32_t n) {
   if (x.overflow) return PH;
   const uint64_t* pw = x.pw;
   const uint32_t pwn = x.pw_n;
-  HL tot = x.par.template scan<HL>(
+  HL tot = x.par.template scan_blocked<16, HL>(
       n, HL{0, 0, 0},
       [&](const HL& a, const HL& c) {
         uint64_t m = c.len <= pwn ? pw[c.len] : powmod61(kHashBase, c.len);
@@ -187,11 +187,26 @@ TB_HD uint64_t* prefix_hash(DocCtx<P>& x, const uint8_t* b, uint32_t n) {
 }
 
 // UAX#29 word segments of code points [0, C) -> words (trimmed, with a word character).
+// Segments are aggregated with one segmented scan over the code points (no per-lane walk over a
+// segment): a segment's first code point carries the reset flag, the running element ORs the
+// word-character / alphabetic bits and tracks the first and last non-whitespace code point.
+struct WSeg {
+  uint32_t bits;   // bit0: segment start (reset), bit1: has a word char, bit2: alphabetic
+  uint32_t first;  // first non-whitespace cp (0xFFFFFFFF if none)
+  uint32_t last;   // one past the last non-whitespace cp
+};
+TB_HD WSeg wseg_op(const WSeg& a, const WSeg& b) {
+  if (b.bits & 1u) return b;
+  return WSeg{a.bits | (b.bits & 6u), a.first < b.first ? a.first : b.first, a.last > b.last ? a.last : b.last};
+}
+
 template <class P>
 TB_HD Words words(DocCtx<P>& x, const Cps& c) {
   Words w;
   const uint32_t C = c.n;
   uint8_t* wb = x.template alloc<uint8_t>(C + 1);
+  uint32_t* sf = x.template alloc<uint32_t>(C + 1);  // per segment end: first non-ws cp
+  uint32_t* sl = x.template alloc<uint32_t>(C + 1);  // per segment end: last non-ws cp + 1 | flags
   w.cs = x.template alloc<uint32_t>(C + 1);
   w.ce = x.template alloc<uint32_t>(C + 1);
   w.bs = x.template alloc<uint32_t>(C + 1);
@@ -205,36 +220,34 @@ TB_HD Words words(DocCtx<P>& x, const Cps& c) {
     wb[i] = (i == 0 || i == C) ? 1 : (uint8_t)wb_break(acc, (int)C, (int)i);
   });
   x.par.sync();
-  struct St { uint32_t s, e; uint8_t a; };
+  auto elem = [&](uint32_t j) {
+    const uint32_t p = prop[j];
+    const bool ws = is_ws(p);
+    WSeg e;
+    e.bits = (wb[j] ? 1u : 0u) | ((!(p & P_PUNCT) && !ws) ? 2u : 0u) | ((p & P_ALPHA) ? 4u : 0u);
+    e.first = ws ? 0xFFFFFFFFu : j;
+    e.last = ws ? 0u : j + 1;
+    return e;
+  };
+  x.par.template scan<WSeg>(
+      C, WSeg{0u, 0xFFFFFFFFu, 0u} /* two-sided identity */, wseg_op, elem, [&](uint32_t j, const WSeg& ex) {
+        if (!wb[j + 1]) return;  // not the last code point of its segment
+        const WSeg in = wseg_op(ex, elem(j));
+        sf[j] = in.first;
+        sl[j] = (in.bits & 2u) ? (in.last | ((in.bits & 4u) ? 0x80000000u : 0u)) : 0xFFFFFFFFu;
+      });
+  x.par.sync();
   uint32_t *cs = w.cs, *ce = w.ce, *bs = w.bs, *be = w.be;
   uint8_t* al = w.alpha;
-  w.n = x.par.template compact<St>(
-      C,
-      [&](uint32_t i, St& st) {
-        if (!wb[i]) return false;
-        uint32_t e = i + 1;
-        while (!wb[e]) ++e;
-        uint32_t s = i;
-        while (s < e && is_ws(prop[s])) ++s;
-        uint32_t ee = e;
-        while (ee > s && is_ws(prop[ee - 1])) --ee;
-        bool has = false, alpha = false;
-        for (uint32_t k = s; k < ee; ++k) {
-          uint32_t p = prop[k];
-          if (!(p & P_PUNCT) && !(p & P_WS)) has = true;
-          if (p & P_ALPHA) alpha = true;
-        }
-        st.s = s;
-        st.e = ee;
-        st.a = alpha;
-        return has;
-      },
-      [&](uint32_t, uint32_t k, St& st) {
-        cs[k] = st.s;
-        ce[k] = st.e;
-        bs[k] = off[st.s];
-        be[k] = off[st.e];
-        al[k] = st.a;
+  w.n = x.par.template compact<int>(
+      C, [&](uint32_t j, int&) { return wb[j + 1] && sl[j] != 0xFFFFFFFFu; },
+      [&](uint32_t j, uint32_t k, int&) {
+        const uint32_t s0 = sf[j], e0 = sl[j] & 0x7FFFFFFFu;
+        cs[k] = s0;
+        ce[k] = e0;
+        bs[k] = off[s0];
+        be[k] = off[e0];
+        al[k] = (sl[j] >> 31) ? 1 : 0;
       });
   x.par.sync();
   return w;

@@ -65,6 +65,10 @@ struct SeqPar {
     }
     return acc;
   }
+  template <int K, class T, class Op, class In, class Out>
+  T scan_blocked(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
+    return scan(n, id, op, in, out);
+  }
   void sync() const {}
   static uint64_t clock() { return 0; }
   template <class F>
@@ -177,6 +181,40 @@ struct WavePar {
       T excl = shfl_up_t(x, 1);
       if (lane == 0) excl = id;
       if (i < n) out(i, op(carry, excl));
+      carry = op(carry, shfl_t(x, 63));
+    }
+    return carry;
+  }
+  // Same contract as scan(), for expensive ops over long inputs: each lane folds K consecutive
+  // items sequentially in registers, only the 64 block totals go through the cross-lane scan,
+  // then each lane replays its block to emit the prefixes (op evaluated ~2x per item instead of
+  // log2(64) = 6x, and K-fold fewer shuffles).
+  template <int K, class T, class Op, class In, class Out>
+  __device__ T scan_blocked(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
+    T carry = id;
+    for (uint32_t base = 0; base < n; base += 64u * K) {
+      const uint32_t start = base + lane * K;
+      T tot = id;
+      for (int k = 0; k < K; ++k) {
+        const uint32_t i = start + k;
+        if (i < n) tot = op(tot, in(i));
+      }
+      T x = tot;
+      for (int o = 1; o < 64; o <<= 1) {
+        T y = shfl_up_t(x, o);
+        if ((int)lane >= o) x = op(y, x);
+      }
+      T excl = shfl_up_t(x, 1);
+      if (lane == 0) excl = id;
+      T run = op(carry, excl);
+      for (int k = 0; k < K; ++k) {
+        const uint32_t i = start + k;
+        if (i < n) {
+          const T v = in(i);
+          out(i, run);
+          run = op(run, v);
+        }
+      }
       carry = op(carry, shfl_t(x, 63));
     }
     return carry;

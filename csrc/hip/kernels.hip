@@ -50,20 +50,29 @@ __device__ __forceinline__ DocCtx<WavePar> make_ctx(const DevTables& t, const ui
   return x;
 }
 
-__global__ __launch_bounds__(64) void k_stage_analyze(
-    const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes,
-    const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,
-    const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
-    int64_t* rec, uint32_t* flags, const uint16_t* __restrict__ lid_emb, uint16_t* lid_vec, int32_t* lid_cnt,
-    uint32_t lds_bytes, uint64_t* prof) {
-  const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
-  if (doc >= ndocs) return;
-  DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);
-  const uint8_t* b = bytes + off[doc];
-  const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
-  StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, lid_vec, lid_cnt};
-  analyze_stage<WavePar, false>(x, *stage, *plan, lid_emb, b, n, out);  // LD features: k_langid_features
-}
+// The stage kernel is register-bound (occupancy = waves/SIMD the VGPR budget allows). Variants
+// with a forced waves-per-EU budget trade spills for occupancy; tb_stage_analyze picks one by
+// its `waves` argument (0 = compiler default).
+#define TB_STAGE_KERNEL(NAME, ATTR)                                                                   \
+  __global__ __launch_bounds__(64) ATTR void NAME(                                                   \
+      const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes, \
+      const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,        \
+      const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, \
+      int64_t* rec, uint32_t* flags, const uint16_t* __restrict__ lid_emb, uint16_t* lid_vec, int32_t* lid_cnt, \
+      uint32_t lds_bytes, uint64_t* prof) {                                                          \
+    const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;                                        \
+    if (doc >= ndocs) return;                                                                         \
+    DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);   \
+    const uint8_t* b = bytes + off[doc];                                                              \
+    const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);                                           \
+    StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, lid_vec, lid_cnt};                              \
+    analyze_stage<WavePar, false>(x, *stage, *plan, lid_emb, b, n, out); /* LD: k_langid_features */  \
+  }
+
+TB_STAGE_KERNEL(k_stage_analyze, )
+TB_STAGE_KERNEL(k_stage_analyze_w4, __attribute__((amdgpu_waves_per_eu(4, 8))))
+TB_STAGE_KERNEL(k_stage_analyze_w5, __attribute__((amdgpu_waves_per_eu(5, 8))))
+TB_STAGE_KERNEL(k_stage_analyze_w6, __attribute__((amdgpu_waves_per_eu(6, 8))))
 
 // Language-id n-gram bag of one document per wave (own kernel: its 33 accumulators per lane
 // would otherwise set the register budget, and so the occupancy, of the whole stage kernel).
@@ -182,13 +191,15 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
                      const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                      const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
                      const uint16_t* lid_emb, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes,
-                     uint64_t* prof) {
+                     uint64_t* prof, int32_t waves) {
   if (ndocs <= 0) return 0;
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
+  auto kern = waves == 4 ? k_stage_analyze_w4 : waves == 5 ? k_stage_analyze_w5 : waves == 6 ? k_stage_analyze_w6
+                                                                                              : k_stage_analyze;
   if (lds_bytes > 65536)
-    (void)hipFuncSetAttribute((const void*)k_stage_analyze, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-  hipLaunchKernelGGL(k_stage_analyze, dim3(ndocs), dim3(64), lds_bytes, stream, (const DevPlan*)plan,
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  hipLaunchKernelGGL(kern, dim3(ndocs), dim3(64), lds_bytes, stream, (const DevPlan*)plan,
                      (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, flags,
                      lid_emb, lid_vec, lid_cnt, lds_bytes, prof);
   return (int)hipGetLastError();

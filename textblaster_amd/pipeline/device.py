@@ -92,6 +92,7 @@ class DeviceRunner:
     # 13 KB each costs no occupancy; the C4 kernel (7 waves/SIMD) only keeps per-line arrays there
     DEFAULT_LDS_BYTES = 13312
     DEFAULT_LDS_BYTES_C4 = 2048
+    DEFAULT_STAGE_WAVES = 0  # stage kernel occupancy variant (0 = compiler default)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None):
         import torch
@@ -123,6 +124,7 @@ class DeviceRunner:
 
         self.lds_bytes = int(os.environ.get("TB_LDS_BYTES", str(self.DEFAULT_LDS_BYTES)))
         self.lds_bytes_c4 = int(os.environ.get("TB_LDS_BYTES_C4", str(self.DEFAULT_LDS_BYTES_C4)))
+        self.stage_waves = int(os.environ.get("TB_STAGE_WAVES", str(self.DEFAULT_STAGE_WAVES)))
         self.lds_bytes_lid = int(os.environ.get("TB_LDS_BYTES_LID", "9216"))  # 64x33 int32 partials + sums
         # TB_PHASE_PROF=1: per-document phase cycle counters (s_memtime stamps) for profiling
         self.phase_prof = os.environ.get("TB_PHASE_PROF", "") not in ("", "0")
@@ -249,7 +251,7 @@ class DeviceRunner:
                 prof = self._prof_buf(ndocs, keep, f"stage{s}")
                 self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm, ndocs, scratch, d_soff, pw, pw_n,
                                      rec, flags, self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
-                                     self.lds_bytes, prof)
+                                     self.lds_bytes, prof, self.stage_waves)
                 if lid_vec is not None:
                     self._last_lid = (lid_vec, lid_cnt)
                 for kind, width, prefix in layout:

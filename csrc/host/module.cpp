@@ -331,6 +331,24 @@ PYBIND11_MODULE(_tbhost, m) {
         return py::make_tuple(sup, (bool)l);
       });
 
+  // Multi-threaded memcpy into a (pinned) staging buffer: dst[dst_off : dst_off + src.nbytes] = src.
+  m.def("parallel_copy", [](py::array dst, int64_t dst_off, py::array src, int nthreads) {
+    if (!(dst.flags() & py::array::c_style) || !(src.flags() & py::array::c_style))
+      throw std::invalid_argument("parallel_copy needs contiguous arrays");
+    const int64_t nb = (int64_t)src.nbytes();
+    if (dst_off < 0 || dst_off + nb > (int64_t)dst.nbytes()) throw std::invalid_argument("parallel_copy out of range");
+    char* d = (char*)dst.mutable_data() + dst_off;
+    const char* sp = (const char*)src.data();
+    py::gil_scoped_release nogil;
+    const int64_t chunk = 1 << 20;
+    parallel_for((nb + chunk - 1) / chunk, nb >= (8 << 20) ? nthreads : 1, [&](int64_t a, int64_t b) {
+      for (int64_t c = a; c < b; ++c) {
+        const int64_t o = c * chunk, len = std::min<int64_t>(chunk, nb - o);
+        std::memcpy(d + o, sp + o, (size_t)len);
+      }
+    });
+  }, py::arg("dst"), py::arg("dst_off"), py::arg("src"), py::arg("nthreads") = 8);
+
   // ---- batch state ----
   py::class_<PyBatch>(m, "BatchState")
       .def(py::init([](py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,

@@ -131,6 +131,9 @@ class DeviceRunner:
         self.phase_totals: Dict[str, np.ndarray] = {}
         self.phase_docs: Dict[str, int] = {}
         self.slots = [_Slot() for _ in range(self.N_SLOTS)]
+        self.h2d_stream = torch.cuda.Stream(self.device)
+        self.d2h_stream = torch.cuda.Stream(self.device)
+        self.copy_threads = int(os.environ.get("TB_COPY_THREADS", "8"))
         self._next_slot = 0
         self._last_lid = None
 
@@ -157,14 +160,20 @@ class DeviceRunner:
         if slot.pinned is None or slot.pinned.numel() < total:
             slot.pinned = torch.empty(int(total * 1.25), dtype=torch.uint8, pin_memory=True)
         hv = slot.pinned.numpy()
+        h = native.host()
         for a, o in zip(arrays, offs):
             if a.nbytes:
-                hv[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
-        dev = torch.empty(total, dtype=torch.uint8, device=self.device)
-        dev.copy_(slot.pinned[:total], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
+                h.parallel_copy(hv, o, np.ascontiguousarray(a).view(np.uint8).reshape(-1), self.copy_threads)
+        # H2D on its own stream: batch k+1's upload overlaps batch k's kernels
+        with torch.cuda.stream(self.h2d_stream):
+            dev = torch.empty(total, dtype=torch.uint8, device=self.device)
+            dev.copy_(slot.pinned[:total], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.h2d_stream)
         slot.h2d_done = ev
+        compute = torch.cuda.current_stream(self.device)
+        compute.wait_event(ev)
+        dev.record_stream(compute)
         out = []
         for a, o in zip(arrays, offs):
             dt = _TORCH_DTYPES[np.dtype(a.dtype).str]
@@ -273,21 +282,32 @@ class DeviceRunner:
                 versions[ver + 1] = (out, new_off, cap)
                 c4_recs_d[i] = rec
                 keep.append(src)
-        # D2H into pinned host buffers, all on the stream, then one completion event
+        # D2H into pinned host buffers on the download stream (overlaps the next batch's
+        # kernels), then one completion event
+        done = torch.cuda.Event()
+        done.record(torch.cuda.current_stream(self.device))
+        self.d2h_stream.wait_event(done)
+
         def d2h(t):
             ht = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
             ht.copy_(t, non_blocking=True)
+            t.record_stream(self.d2h_stream)
             return ht
 
-        h_stage = [d2h(r) if r is not None else None for r in stage_recs_d]
-        h_c4 = {i: d2h(r) for i, r in c4_recs_d.items()}
-        h_versions = {}
-        for ver in range(1, self.plan.n_versions):
-            vb, vo, _ = versions[ver]
-            h_versions[ver] = (d2h(vb), d2h(vo))
-        h_flags = d2h(flags)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.d2h_stream):
+            h_stage = [d2h(r) if r is not None else None for r in stage_recs_d]
+            h_c4 = {i: d2h(r) for i, r in c4_recs_d.items()}
+            h_versions = {}
+            for ver in range(1, self.plan.n_versions):
+                vb, vo, _ = versions[ver]
+                h_versions[ver] = (d2h(vb), d2h(vo))
+            h_flags = d2h(flags)
+            if self.phase_prof:
+                for item in keep:
+                    if isinstance(item, tuple) and len(item) == 3 and item[0] == "prof":
+                        item[2].record_stream(self.d2h_stream)
+            ev = torch.cuda.Event()
+            ev.record(self.d2h_stream)
         keep += [stage_recs_d, c4_recs_d, versions, flags]
         t2 = time.perf_counter()
         return PendingBatch(self, ndocs, ev, h_stage, h_c4, h_versions, h_flags,

@@ -88,11 +88,11 @@ class PendingBatch:
 
 class DeviceRunner:
     N_SLOTS = 2
-    # per-wave LDS slices: the stage kernel runs at 3 waves/SIMD (VGPR-bound) = 12 waves/CU, so
-    # 13 KB each costs no occupancy; the C4 kernel (7 waves/SIMD) only keeps per-line arrays there
-    DEFAULT_LDS_BYTES = 13312
+    # per-wave LDS slices: the stage kernel is built for 4 waves/SIMD (128 VGPRs) = 16 waves/CU, so
+    # 10 KB each costs no occupancy; the C4 kernel (7 waves/SIMD) only keeps per-line arrays there
+    DEFAULT_LDS_BYTES = 10240
     DEFAULT_LDS_BYTES_C4 = 2048
-    DEFAULT_STAGE_WAVES = 0  # stage kernel occupancy variant (0 = compiler default)
+    DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; sweep: tools/occ_sweep.sh)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None):
         import torch

@@ -84,3 +84,17 @@ def test_lds_arena_does_not_change_results(host, lds):
         b = host.emulate_c4(steps[i], data, off, 4, lds)
         for x, y in zip(a, b):
             np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("spec", ["kernel@2", "oom@1"])
+def test_failed_batch_is_recovered(spec):
+    """A failing device batch is re-run in halves (then on the CPU path) and the run continues
+    with identical outputs (fault injection, emulated device backend)."""
+    cfg = load_pipeline_config("config/bench_pipeline.yaml")
+    batches = [synth.pack(synth.make_corpus(200, 600, seed=s)) for s in range(3)]
+    ref = [outputs(r) for r in Engine(cfg, backend="emulate", nthreads=2).process_many(batches)]
+    eng = Engine(cfg, backend="emulate", nthreads=2, fault_inject=spec)
+    got = [outputs(r) for r in eng.process_many(batches, on_error="recover")]
+    assert got == ref
+    with pytest.raises(Exception, match="injected"):
+        list(Engine(cfg, backend="emulate", nthreads=2, fault_inject=spec).process_many(batches))

@@ -49,3 +49,20 @@ def test_device_run_equals_cpu_oracle(tmp_path):
                 assert abs(float(ja[k]) - float(jb[k])) < 1e-5
             else:
                 assert ja[k] == jb[k]
+
+
+def test_device_fault_recovery(tmp_path):
+    """An injected device failure on the 2nd batch is recovered (halves, then CPU) and the run's
+    outputs are unchanged."""
+    texts = synth.make_corpus(3000, 800, seed=5)
+    inp = str(tmp_path / "in.parquet")
+    w = ParquetWriter(inp)
+    w.write_batch([TextDocument(f"f{i}", t, "gpu") for i, t in enumerate(texts)])
+    w.close()
+    res = {}
+    for tag, fault in (("ok", None), ("fault", "kernel@2")):
+        o, e = str(tmp_path / f"{tag}.o.parquet"), str(tmp_path / f"{tag}.e.parquet")
+        st = run(RunConfig(inp, o, e, CFG, backend="cuda", unit_rows=1000, fault_inject=fault))
+        res[tag] = (st.kept, st.excluded, pq.read_table(o).column("id"), pq.read_table(e).column("id"))
+    assert res["ok"][:2] == res["fault"][:2]
+    assert res["ok"][2].equals(res["fault"][2]) and res["ok"][3].equals(res["fault"][3])

@@ -45,7 +45,8 @@ def setup_logging(log_dir: Optional[str], name: str, console_level: str = "WARNI
     (reference: tracing console=warn, daily JSON file ./log/<name>.log)."""
     root = logging.getLogger()
     root.handlers.clear()
-    root.setLevel(os.environ.get("TB_LOG", "INFO").upper())
+    level = (os.environ.get("TB_LOG") or os.environ.get("RUST_LOG") or "INFO").upper()
+    root.setLevel(level if level in ("DEBUG", "INFO", "WARNING", "WARN", "ERROR", "CRITICAL") else "INFO")
     con = logging.StreamHandler(sys.stderr)
     con.setLevel(console_level)
     con.setFormatter(logging.Formatter("%(levelname)s %(name)s: %(message)s"))
@@ -89,9 +90,11 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("--metrics-port", type=_u16, default=None)
         p.add_argument("-c", "--pipeline-config", default=DEFAULT_CONFIG)
         _queue_flags(p)
-        p.add_argument("--gpus", type=int, default=None,
+        p.add_argument("--gpus", "--devices", dest="gpus", type=int, default=None,
                        help="number of local GPUs (one process each); default: all visible GPUs")
         p.add_argument("--backend", default="auto", choices=["auto", "cuda", "cpu"])
+        p.add_argument("--cpu", dest="backend", action="store_const", const="cpu",
+                       help="run the CPU oracle path (same as --backend cpu)")
         p.add_argument("--segmentation", default="icu", choices=["icu", "rules"],
                        help="UAX#29 implementation of the CPU backend")
         p.add_argument("--unit-rows", type=int, default=65536, help="rows per processing/checkpoint unit")
@@ -102,6 +105,9 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("--keep-parts", action="store_true")
         p.add_argument("--compression", default="none", help="Parquet codec (none, snappy, zstd, ...)")
         p.add_argument("--tokenizer-dir", default=None, help="local dir holding <name>/tokenizer.json")
+        p.add_argument("--tokenizer-file", default=None, help="tokenizer.json used by every TokenCounter step")
+        p.add_argument("--langid-model", default=None, help="language-id weights (.npz); default: bundled model")
+        p.add_argument("--fault-inject", default=None, help="debug: kernel@N or oom@N (fail the N-th batch once)")
         p.add_argument("--badwords-dir", default=None, help="dir holding the C4 bad-words lists (<lang> files)")
         p.add_argument("--log-dir", default="./log")
 
@@ -189,13 +195,15 @@ def run_cmd(args, argv: List[str]) -> int:
     log.info("Producer started.")
     log.info("Input file: %s", args.input_file)
     log.info("Output File: %s", args.output_file)
+    if args.langid_model:
+        os.environ["TB_LANGID_MODEL"] = args.langid_model
     rc = RunConfig(
         input_file=args.input_file, output_file=args.output_file, excluded_file=args.excluded_file,
         pipeline_config=args.pipeline_config, text_column=args.text_column, id_column=args.id_column,
         backend=backend, segmentation=args.segmentation, unit_rows=args.unit_rows, threads=args.threads,
         work_dir=args.work_dir, resume=args.resume, checkpoint=args.checkpoint, keep_parts=args.keep_parts,
         compression=args.compression, tokenizer_dir=args.tokenizer_dir, badwords_dir=args.badwords_dir,
-        metrics_port=args.metrics_port)
+        metrics_port=args.metrics_port, tokenizer_file=args.tokenizer_file, fault_inject=args.fault_inject)
     try:
         stats = run(rc, ctx)
     except PipelineError as e:

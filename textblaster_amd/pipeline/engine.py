@@ -26,7 +26,7 @@ import numpy as np
 
 from .. import native
 from ..config.pipeline import PipelineConfig
-from ..errors import ConfigError, Unexpected
+from ..errors import ConfigError, DeviceError, Unexpected
 from .plan import ExecPlan, build_plan
 
 
@@ -78,8 +78,12 @@ class Engine:
     def __init__(self, cfg: PipelineConfig, backend: str = "auto", device: Optional[str] = None,
                  nthreads: Optional[int] = None, segmentation: str = "rules", langid=None,
                  tokenizer_dir: Optional[str] = None, badwords_dir: Optional[str] = None,
-                 keep_reasons: bool = False):
+                 keep_reasons: bool = False, tokenizer_file: Optional[str] = None,
+                 fault_inject: Optional[str] = None, tokenizers=None, badwords=None):
         self.cfg = cfg
+        self._cpu_engine = None
+        self._n_submitted = 0
+        self._fault = _parse_fault(fault_inject or os.environ.get("TB_FAULT_INJECT", ""))
         self.h = native.host()
         self.plan: ExecPlan = build_plan(cfg)
         self.steps = [self.h.make_step(s.native_dict()) for s in cfg.pipeline]
@@ -96,14 +100,14 @@ class Engine:
 
             self.langid = langid or load_default()
         self.lid_native = self.langid.native() if self.langid is not None else None
-        self.tokenizers: Dict[int, object] = {}
+        self.tokenizers: Dict[int, object] = dict(tokenizers or {})
         for i, s in enumerate(cfg.pipeline):
-            if s.type == "TokenCounter":
+            if s.type == "TokenCounter" and i not in self.tokenizers:
                 from ..models.tokenizer import load_tokenizer
 
-                self.tokenizers[i] = load_tokenizer(s.params.tokenizer_name, tokenizer_dir)
-        self.badwords = None
-        if "C4BadWordsFilter" in types:
+                self.tokenizers[i] = load_tokenizer(tokenizer_file or s.params.tokenizer_name, tokenizer_dir)
+        self.badwords = badwords
+        if "C4BadWordsFilter" in types and self.badwords is None:
             bw_dirs = [s.params.cache_base_path for s in cfg.pipeline
                        if s.type == "C4BadWordsFilter" and s.params.cache_base_path]
             d = badwords_dir or (bw_dirs[0] if bw_dirs else os.path.join("data", "c4_badwords"))
@@ -128,23 +132,73 @@ class Engine:
         """Run the pipeline over one batch. ``meta`` = (data uint8, off int64, valid uint8) or None."""
         return self.finish(self.submit(data, off, meta, row_base))
 
-    def process_many(self, batches: Iterable) -> Iterator[BatchResult]:
+    def process_many(self, batches: Iterable, on_error: str = "raise") -> Iterator[BatchResult]:
         """Pipelined processing of an iterable of ``(data, off, meta)`` batches: batch k+1 is
         staged and its kernels queued on the GPU before batch k is resolved and assembled on the
-        host, so device work and host work overlap. Results are yielded in input order."""
+        host, so device work and host work overlap. Results are yielded in input order.
+
+        ``on_error="recover"``: a batch whose device work fails (HIP error, out of memory, an
+        injected fault) is re-run split in two halves, and if that fails too, on the CPU oracle
+        path; the failure is logged and counted, the run continues."""
         pending = None
         for item in batches:
-            data, off = item[0], item[1]
-            meta = item[2] if len(item) > 2 else None
-            cur = self.submit(data, off, meta)
+            try:
+                cur = (item, self.submit(item[0], item[1], item[2] if len(item) > 2 else None))
+            except Exception as e:  # noqa: BLE001 - handled per on_error
+                cur = (item, e)
             if pending is not None:
-                yield self.finish(pending)
+                yield self._finish_or_recover(pending, on_error)
             pending = cur
         if pending is not None:
-            yield self.finish(pending)
+            yield self._finish_or_recover(pending, on_error)
+
+    def _finish_or_recover(self, pending, on_error: str) -> BatchResult:
+        item, sub = pending
+        if not isinstance(sub, Exception):
+            try:
+                return self.finish(sub)
+            except Exception as e:  # noqa: BLE001
+                sub = e
+        if on_error != "recover":
+            raise sub
+        return self.recover(item[0], item[1], item[2] if len(item) > 2 else None, sub)
+
+    def recover(self, data, off, meta, err: BaseException) -> BatchResult:
+        """Re-run a failed batch: halves on the same backend, then the CPU oracle path."""
+        import logging
+
+        from ..utils import metrics
+
+        log = logging.getLogger("textblaster_amd.engine")
+        n = len(off) - 1
+        log.warning("batch of %d docs failed on %s (%s: %s); recovering", n, self.backend, type(err).__name__, err)
+        metrics.BATCH_FAILURES_TOTAL.labels(type(err).__name__).inc()
+        if self.backend != "cpu" and n > 1 and not _is_sticky(err):
+            try:
+                h = n // 2
+                parts = [self.process(*_slice_batch(data, off, meta, 0, h)),
+                         self.process(*_slice_batch(data, off, meta, h, n))]
+                return _concat_results(parts, [0, h])
+            except Exception as e2:  # noqa: BLE001
+                log.warning("split retry failed too (%s: %s); using the CPU path", type(e2).__name__, e2)
+        metrics.CPU_FALLBACK_DOCS_TOTAL.inc(n)
+        return self._cpu_fallback().process(data, off, meta)
+
+    def _cpu_fallback(self) -> "Engine":
+        if self._cpu_engine is None:
+            self._cpu_engine = Engine(self.cfg, backend="cpu", nthreads=self.nthreads, segmentation="icu",
+                                      langid=self.langid, keep_reasons=self.keep_reasons,
+                                      tokenizers=self.tokenizers, badwords=self.badwords)
+        return self._cpu_engine
 
     def submit(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None, row_base: int = 0):
         t0 = time.perf_counter()
+        self._n_submitted += 1
+        if self._fault is not None and not self._fault.get("fired") and self._n_submitted == self._fault["batch"]:
+            self._fault["fired"] = True
+            if self._fault["kind"] == "oom":
+                raise MemoryError("injected device out-of-memory (TB_FAULT_INJECT)")
+            raise DeviceError("injected kernel fault (TB_FAULT_INJECT)")
         data = np.ascontiguousarray(data, dtype=np.uint8)
         off = np.ascontiguousarray(off, dtype=np.int64)
         dev = None
@@ -273,6 +327,54 @@ class Engine:
 
     def step_names(self) -> List[str]:
         return [s.type for s in self.cfg.pipeline]
+
+
+def _parse_fault(spec: str):
+    """``kind@batch`` (kind: kernel | oom, batch: 1-based submit counter), e.g. ``kernel@3``."""
+    if not spec:
+        return None
+    kind, _, at = spec.partition("@")
+    if kind not in ("kernel", "oom") or not at.isdigit():
+        raise ConfigError(f"bad fault injection spec {spec!r} (expected kernel@N or oom@N)")
+    return {"kind": kind, "batch": int(at), "fired": False}
+
+
+def _is_sticky(err: BaseException) -> bool:
+    """A GPU memory access fault poisons the HIP context; retrying on the device is pointless."""
+    msg = str(err).lower()
+    return "illegal" in msg or "memory access fault" in msg or "hiperrorlaunchfailure" in msg
+
+
+def _slice_batch(data, off, meta, a: int, b: int):
+    o = off[a:b + 1]
+    d = data[o[0]:o[-1]]
+    o = o - o[0]
+    m = None
+    if meta is not None and meta[0] is not None:
+        md, mo, mv = meta
+        mo2 = mo[a:b + 1]
+        m = (md[mo2[0]:mo2[-1]], mo2 - mo2[0], mv[a:b] if mv is not None else None)
+    return np.ascontiguousarray(d), np.ascontiguousarray(o), m
+
+
+def _concat_results(parts: List[BatchResult], bases: List[int]) -> BatchResult:
+    kept, excluded, errs, reasons = [], [], [], {}
+    for r, base in zip(parts, bases):
+        for p in r.kept:
+            p.rows = p.rows + base
+            kept.append(p)
+        for p in r.excluded:
+            p.rows = p.rows + base
+            excluded.append(p)
+        errs.append(r.error_rows + base)
+        reasons.update({k + base: v for k, v in r.reasons.items()})
+    timings: Dict[str, float] = {}
+    for r in parts:
+        for k, v in r.timings.items():
+            timings[k] = timings.get(k, 0.0) + v
+    return BatchResult(sum(r.n_docs for r in parts), kept, excluded, np.concatenate(errs),
+                       np.concatenate([r.fail_step for r in parts]), np.concatenate([r.status for r in parts]),
+                       reasons, timings, sum(r.n_delegated for r in parts))
 
 
 @dataclasses.dataclass

@@ -72,6 +72,8 @@ class RunConfig:
     badwords_dir: Optional[str] = None
     metrics_port: Optional[int] = None
     progress_interval: float = 1.0
+    tokenizer_file: Optional[str] = None
+    fault_inject: Optional[str] = None   # debug: "kernel@N" / "oom@N" (N = 1-based batch)
 
 
 @dataclasses.dataclass
@@ -344,7 +346,8 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
         backend = rc.backend
         device = ctx.device if backend in ("cuda", "auto") else None
         engine = Engine(cfg, backend=backend, device=device, nthreads=rc.threads, segmentation=rc.segmentation,
-                        tokenizer_dir=rc.tokenizer_dir, badwords_dir=rc.badwords_dir)
+                        tokenizer_dir=rc.tokenizer_dir, badwords_dir=rc.badwords_dir,
+                        tokenizer_file=rc.tokenizer_file, fault_inject=rc.fault_inject)
     use_parts = world > 1 or rc.checkpoint or rc.resume
     work_dir = rc.work_dir or (rc.output_file + ".work")
     done: Dict[int, Dict] = {}
@@ -406,7 +409,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
 
     try:
         t_prev = time.perf_counter()
-        for res in engine.process_many(feed()):
+        for res in engine.process_many(feed(), on_error="recover"):
             unit, batch = inflight.popleft()
             now = time.perf_counter()
             dt, t_prev = now - t_prev, now

@@ -65,6 +65,10 @@ GPU_PHASE_SECONDS = Histogram("tb_gpu_phase_seconds", "Per-batch time by phase."
 DELEGATED_DOCS_TOTAL = Counter("tb_cpu_delegated_docs_total",
                                "Documents recomputed on the CPU oracle path (dictionary scripts, collisions).",
                                registry=REGISTRY)
+BATCH_FAILURES_TOTAL = Counter("tb_batch_failures_total", "Batches whose device work failed (then recovered).",
+                               ["error"], registry=REGISTRY)
+CPU_FALLBACK_DOCS_TOTAL = Counter("tb_cpu_fallback_docs_total",
+                                  "Documents re-run on the CPU oracle path after a device failure.", registry=REGISTRY)
 RANK = Gauge("tb_rank", "Data-parallel rank of this process.", registry=REGISTRY)
 WORLD_SIZE = Gauge("tb_world_size", "Number of data-parallel ranks.", registry=REGISTRY)
 GLOBAL_DOCS = Gauge("tb_global_docs_total", "All-reduced document counters (rank 0).", ["kind"],

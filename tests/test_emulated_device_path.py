@@ -98,3 +98,15 @@ def test_failed_batch_is_recovered(spec):
     assert got == ref
     with pytest.raises(Exception, match="injected"):
         list(Engine(cfg, backend="emulate", nthreads=2, fault_inject=spec).process_many(batches))
+
+
+def test_byte_budget_split_batches():
+    """Batches above the device byte budget run as sub-batches; results are merged back in order."""
+    cfg = load_pipeline_config("config/bench_pipeline.yaml")
+    batches = [synth.pack(synth.make_corpus(300, 700, seed=s)) for s in range(2)]
+    ref = [outputs(r) for r in Engine(cfg, backend="emulate", nthreads=2).process_many(batches)]
+    eng = Engine(cfg, backend="emulate", nthreads=2)
+    eng.max_batch_bytes = 20000
+    res = list(eng.process_many(batches))
+    assert [outputs(r) for r in res] == ref
+    assert [r.n_docs for r in res] == [300, 300]

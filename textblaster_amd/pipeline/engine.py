@@ -84,6 +84,8 @@ class Engine:
         self._cpu_engine = None
         self._n_submitted = 0
         self._fault = _parse_fault(fault_inject or os.environ.get("TB_FAULT_INJECT", ""))
+        # text bytes per device batch (scratch ~160 B per text byte per in-flight slot)
+        self.max_batch_bytes = int(os.environ.get("TB_MAX_BATCH_BYTES", str(192 << 20)))
         self.h = native.host()
         self.plan: ExecPlan = build_plan(cfg)
         self.steps = [self.h.make_step(s.native_dict()) for s in cfg.pipeline]
@@ -140,17 +142,60 @@ class Engine:
         ``on_error="recover"``: a batch whose device work fails (HIP error, out of memory, an
         injected fault) is re-run split in two halves, and if that fails too, on the CPU oracle
         path; the failure is logged and counted, the run continues."""
+        # Device batches are bounded in bytes (the per-document scratch arena is ~160x the text):
+        # a large input batch runs as several sub-batches whose results are merged back.
+        groups: Dict[int, List] = {}
+        sizes: Dict[int, int] = {}
+
+        def expand():
+            for g, item in enumerate(batches):
+                subs = self._split_by_bytes(item)
+                sizes[g] = len(subs)
+                groups[g] = []
+                for base, sub in subs:
+                    yield g, base, sub
+
         pending = None
-        for item in batches:
+        for g, base, item in expand():
             try:
-                cur = (item, self.submit(item[0], item[1], item[2] if len(item) > 2 else None))
+                cur = (g, base, item, self.submit(item[0], item[1], item[2] if len(item) > 2 else None))
             except Exception as e:  # noqa: BLE001 - handled per on_error
-                cur = (item, e)
+                cur = (g, base, item, e)
             if pending is not None:
-                yield self._finish_or_recover(pending, on_error)
+                out = self._collect_group(pending, on_error, groups, sizes)
+                if out is not None:
+                    yield out
             pending = cur
         if pending is not None:
-            yield self._finish_or_recover(pending, on_error)
+            out = self._collect_group(pending, on_error, groups, sizes)
+            if out is not None:
+                yield out
+
+    def _split_by_bytes(self, item):
+        data, off = item[0], item[1]
+        meta = item[2] if len(item) > 2 else None
+        n = len(off) - 1
+        if self.backend == "cpu" or n <= 1 or int(off[-1]) - int(off[0]) <= self.max_batch_bytes:
+            return [(0, item)]
+        out, a = [], 0
+        while a < n:
+            # largest b with off[b] - off[a] <= budget (at least one document)
+            b = int(np.searchsorted(off, off[a] + self.max_batch_bytes, side="right")) - 1
+            b = min(n, max(b, a + 1))
+            out.append((a, _slice_batch(data, off, meta, a, b)))
+            a = b
+        return out
+
+    def _collect_group(self, pending, on_error, groups, sizes):
+        g, base, item, sub = pending
+        res = self._finish_or_recover((item, sub), on_error)
+        groups[g].append((base, res))
+        if len(groups[g]) < sizes[g]:
+            return None
+        parts = groups.pop(g)
+        if len(parts) == 1:
+            return parts[0][1]
+        return _concat_results([r for _, r in parts], [b for b, _ in parts])
 
     def _finish_or_recover(self, pending, on_error: str) -> BatchResult:
         item, sub = pending

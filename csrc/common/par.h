@@ -112,6 +112,41 @@ struct SeqPar {
 };
 
 #if defined(__HIPCC__)
+namespace pardetail {
+// Shuffle any POD element 32 bits at a time.
+template <class T>
+__device__ inline T shfl_up_t(T v, int o) {
+  constexpr int N = (int)((sizeof(T) + 3) / 4);
+  int w[N];
+  __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+  for (int k = 0; k < N; ++k) w[k] = __shfl_up(w[k], o);
+  T r;
+  __builtin_memcpy(&r, w, sizeof(T));
+  return r;
+}
+template <class T>
+__device__ inline T shfl_t(T v, int src) {
+  constexpr int N = (int)((sizeof(T) + 3) / 4);
+  int w[N];
+  __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+  for (int k = 0; k < N; ++k) w[k] = __shfl(w[k], src);
+  T r;
+  __builtin_memcpy(&r, w, sizeof(T));
+  return r;
+}
+// Inclusive wave scan (Hillis-Steele; op associative, not necessarily commutative).
+template <class T, class Op>
+__device__ inline T wave_incl_scan(T x, uint32_t lane, Op&& op) {
+  for (int o = 1; o < 64; o <<= 1) {
+    T y = shfl_up_t(x, o);
+    if ((int)lane >= o) x = op(y, x);
+  }
+  return x;
+}
+}  // namespace pardetail
+
 struct WavePar {
   uint32_t lane;
   __device__ WavePar() : lane(threadIdx.x & 63) {}
@@ -175,13 +210,13 @@ struct WavePar {
       T x = i < n ? in(i) : id;
       // inclusive Hillis-Steele scan (op is associative, not necessarily commutative)
       for (int o = 1; o < 64; o <<= 1) {
-        T y = shfl_up_t(x, o);
+        T y = pardetail::shfl_up_t(x, o);
         if ((int)lane >= o) x = op(y, x);
       }
-      T excl = shfl_up_t(x, 1);
+      T excl = pardetail::shfl_up_t(x, 1);
       if (lane == 0) excl = id;
       if (i < n) out(i, op(carry, excl));
-      carry = op(carry, shfl_t(x, 63));
+      carry = op(carry, pardetail::shfl_t(x, 63));
     }
     return carry;
   }
@@ -201,10 +236,10 @@ struct WavePar {
       }
       T x = tot;
       for (int o = 1; o < 64; o <<= 1) {
-        T y = shfl_up_t(x, o);
+        T y = pardetail::shfl_up_t(x, o);
         if ((int)lane >= o) x = op(y, x);
       }
-      T excl = shfl_up_t(x, 1);
+      T excl = pardetail::shfl_up_t(x, 1);
       if (lane == 0) excl = id;
       T run = op(carry, excl);
       for (int k = 0; k < K; ++k) {
@@ -215,7 +250,7 @@ struct WavePar {
           run = op(run, v);
         }
       }
-      carry = op(carry, shfl_t(x, 63));
+      carry = op(carry, pardetail::shfl_t(x, 63));
     }
     return carry;
   }
@@ -262,30 +297,148 @@ struct WavePar {
     if (lane < 32) out(d, s);
   }
 
- private:
-  // Shuffle any POD scan element 32 bits at a time.
-  template <class T>
-  __device__ static T shfl_up_t(T v, int o) {
-    constexpr int N = (int)((sizeof(T) + 3) / 4);
-    int w[N];
-    __builtin_memcpy(w, &v, sizeof(T));
-#pragma unroll
-    for (int k = 0; k < N; ++k) w[k] = __shfl_up(w[k], o);
-    T r;
-    __builtin_memcpy(&r, w, sizeof(T));
+};
+
+// One workgroup of NT threads (NT/64 waves) per document, for long documents: the same
+// contract as WavePar with block-wide results. Cross-wave exchange goes through `xs`, a small
+// LDS buffer the kernel provides (>= 16 * NT/64 bytes). Every primitive ends with a barrier, so
+// `xs` can be reused by the next call.
+template <int NT>
+struct BlockPar {
+  static_assert(NT % 64 == 0 && NT >= 128 && NT <= 1024, "block of whole waves");
+  static constexpr int NW = NT / 64;
+  uint32_t tid, lane, wid;
+  char* xs = nullptr;
+  __device__ BlockPar() : tid(threadIdx.x), lane(threadIdx.x & 63), wid(threadIdx.x >> 6) {}
+
+  template <class F>
+  __device__ void for_n(uint32_t n, F&& f) const {
+    for (uint32_t i = tid; i < n; i += NT) f(i);
+  }
+  template <class S, class Pred, class Emit>
+  __device__ uint32_t compact(uint32_t n, Pred&& pred, Emit&& emit) const {
+    uint32_t k = 0;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t* cnt = (uint32_t*)xs;
+    for (uint32_t base = 0; base < n; base += NT) {
+      const uint32_t i = base + tid;
+      S st{};
+      const bool p = i < n && pred(i, st);
+      const uint64_t m = __ballot(p);
+      if (lane == 0) cnt[wid] = (uint32_t)__popcll(m);
+      __syncthreads();
+      uint32_t before = 0, tot = 0;
+      for (int w = 0; w < NW; ++w) {
+        const uint32_t c = cnt[w];
+        if (w < (int)wid) before += c;
+        tot += c;
+      }
+      if (p) emit(i, k + before + (uint32_t)__popcll(m & lt), st);
+      k += tot;
+      __syncthreads();
+    }
+    return k;
+  }
+  template <class T, class Op>
+  __device__ T block_reduce(T v, Op&& op) const {
+    for (int o = 32; o > 0; o >>= 1) v = op(v, pardetail::shfl_t(v, (int)(lane ^ o)));
+    T* t = (T*)xs;
+    if (lane == 0) t[wid] = v;
+    __syncthreads();
+    T r = t[0];
+    for (int w = 1; w < NW; ++w) r = op(r, t[w]);
+    __syncthreads();
     return r;
   }
-  template <class T>
-  __device__ static T shfl_t(T v, int src) {
-    constexpr int N = (int)((sizeof(T) + 3) / 4);
-    int w[N];
-    __builtin_memcpy(w, &v, sizeof(T));
-#pragma unroll
-    for (int k = 0; k < N; ++k) w[k] = __shfl(w[k], src);
-    T r;
-    __builtin_memcpy(&r, w, sizeof(T));
-    return r;
+  template <class T, class F>
+  __device__ T sum(uint32_t n, F&& f) const {
+    T s = 0;
+    for (uint32_t i = tid; i < n; i += NT) s += f(i);
+    return block_reduce(s, [](T a, T b) { return a + b; });
   }
+  template <class T, class F>
+  __device__ T max(uint32_t n, T init, F&& f) const {
+    T s = init;
+    for (uint32_t i = tid; i < n; i += NT) { T v = f(i); if (v > s) s = v; }
+    return block_reduce(s, [](T a, T b) { return a > b ? a : b; });
+  }
+  template <class T, class F>
+  __device__ T min(uint32_t n, T init, F&& f) const {
+    T s = init;
+    for (uint32_t i = tid; i < n; i += NT) { T v = f(i); if (v < s) s = v; }
+    return block_reduce(s, [](T a, T b) { return a < b ? a : b; });
+  }
+  // Exclusive prefix of this wave's inclusive totals across waves (in wave order).
+  template <class T, class Op>
+  __device__ void cross_wave(T wave_incl_last, T id, Op&& op, T& before, T& total) const {
+    T* t = (T*)xs;
+    if (lane == 63) t[wid] = wave_incl_last;
+    __syncthreads();
+    before = id;
+    total = id;
+    for (int w = 0; w < NW; ++w) {
+      const T v = t[w];
+      if (w < (int)wid) before = op(before, v);
+      total = op(total, v);
+    }
+    __syncthreads();
+  }
+  template <class T, class Op, class In, class Out>
+  __device__ T scan(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
+    T carry = id;
+    for (uint32_t base = 0; base < n; base += NT) {
+      const uint32_t i = base + tid;
+      T x = i < n ? in(i) : id;
+      x = pardetail::wave_incl_scan(x, lane, op);
+      T excl = pardetail::shfl_up_t(x, 1);
+      if (lane == 0) excl = id;
+      T before, total;
+      cross_wave(pardetail::shfl_t(x, 63), id, op, before, total);
+      if (i < n) out(i, op(carry, op(before, excl)));
+      carry = op(carry, total);
+    }
+    return carry;
+  }
+  template <int K, class T, class Op, class In, class Out>
+  __device__ T scan_blocked(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
+    T carry = id;
+    for (uint32_t base = 0; base < n; base += (uint32_t)NT * K) {
+      const uint32_t start = base + tid * K;
+      T tot = id;
+      for (int k = 0; k < K; ++k) {
+        const uint32_t i = start + k;
+        if (i < n) tot = op(tot, in(i));
+      }
+      T x = pardetail::wave_incl_scan(tot, lane, op);
+      T excl = pardetail::shfl_up_t(x, 1);
+      if (lane == 0) excl = id;
+      T before, total;
+      cross_wave(pardetail::shfl_t(x, 63), id, op, before, total);
+      T run = op(carry, op(before, excl));
+      for (int k = 0; k < K; ++k) {
+        const uint32_t i = start + k;
+        if (i < n) {
+          const T v = in(i);
+          out(i, run);
+          run = op(run, v);
+        }
+      }
+      carry = op(carry, total);
+    }
+    return carry;
+  }
+  __device__ void sync() const { __syncthreads(); }
+  __device__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
+  template <class F>
+  __device__ void single(F&& f) const { if (tid == 0) f(); }
+  __device__ bool leader() const { return tid == 0; }
+  __device__ static uint64_t cas64(uint64_t* p, uint64_t cmp, uint64_t val) {
+    return atomicCAS((unsigned long long*)p, (unsigned long long)cmp, (unsigned long long)val);
+  }
+  __device__ static void min32(uint32_t* p, uint32_t v) { atomicMin(p, v); }
+  __device__ static void max32(uint32_t* p, uint32_t v) { atomicMax(p, v); }
+  __device__ static uint32_t add32(uint32_t* p, uint32_t v) { return atomicAdd(p, v); }
+  __device__ static void or32(uint32_t* p, uint32_t v) { atomicOr(p, v); }
 };
 #endif
 

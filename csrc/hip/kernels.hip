@@ -32,10 +32,11 @@ struct DevTables {
 // document's working arrays are carved from it first and spill to its HBM scratch slice.
 extern __shared__ __attribute__((aligned(16))) char g_lds_arena[];
 
-__device__ __forceinline__ DocCtx<WavePar> make_ctx(const DevTables& t, const uint64_t* pw, uint32_t pw_n,
-                                                   char* scratch, const int64_t* scratch_off, int doc,
-                                                   uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
-  DocCtx<WavePar> x;
+template <class P = WavePar>
+__device__ __forceinline__ DocCtx<P> make_ctx(const DevTables& t, const uint64_t* pw, uint32_t pw_n,
+                                             char* scratch, const int64_t* scratch_off, int doc,
+                                             uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
+  DocCtx<P> x;
   x.prof = prof ? prof + (size_t)doc * kPhaseSlots : nullptr;
   x.lds = lds_bytes ? (char*)g_lds_arena : nullptr;
   x.lcap = lds_bytes;
@@ -74,6 +75,27 @@ TB_STAGE_KERNEL(k_stage_analyze_w4, __attribute__((amdgpu_waves_per_eu(4, 8))))
 TB_STAGE_KERNEL(k_stage_analyze_w5, __attribute__((amdgpu_waves_per_eu(5, 8))))
 TB_STAGE_KERNEL(k_stage_analyze_w6, __attribute__((amdgpu_waves_per_eu(6, 8))))
 
+// Long documents: one workgroup of kBlockThreads (4 waves) per document (BlockPar), launched
+// over the long prefix of the length-sorted permutation.
+constexpr int kBlockThreads = 256;
+__shared__ __attribute__((aligned(16))) char g_block_xs[16 * (kBlockThreads / 64) + 64];
+
+__global__ __launch_bounds__(kBlockThreads) void k_stage_analyze_blk(
+    const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes,
+    const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,
+    const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
+    int64_t* rec, uint32_t* flags, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes, uint64_t* prof) {
+  const int doc = perm[blockIdx.x];
+  if (doc >= ndocs) return;
+  DocCtx<BlockPar<kBlockThreads>> x =
+      make_ctx<BlockPar<kBlockThreads>>(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);
+  x.par.xs = g_block_xs;
+  const uint8_t* b = bytes + off[doc];
+  const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
+  StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, lid_vec, lid_cnt};
+  analyze_stage<BlockPar<kBlockThreads>, false>(x, *stage, *plan, nullptr, b, n, out);
+}
+
 // Language-id n-gram bag of one document per wave (own kernel: its 33 accumulators per lane
 // would otherwise set the register budget, and so the occupancy, of the whole stage kernel).
 __global__ __launch_bounds__(64) void k_langid_features(
@@ -100,6 +122,21 @@ __global__ __launch_bounds__(64) void k_c4_pass_a(
   const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
   if (doc >= ndocs) return;
   DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);
+  const uint8_t* b = bytes + off[doc];
+  const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
+  c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2);
+}
+
+__global__ __launch_bounds__(kBlockThreads) void k_c4_pass_a_blk(
+    const DevC4* __restrict__ c4, const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
+    const int32_t* __restrict__ perm, int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off,
+    const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec, int64_t* src, uint32_t* flags,
+    uint32_t lds_bytes, uint64_t* prof) {
+  const int doc = perm[blockIdx.x];
+  if (doc >= ndocs) return;
+  DocCtx<BlockPar<kBlockThreads>> x =
+      make_ctx<BlockPar<kBlockThreads>>(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);
+  x.par.xs = g_block_xs;
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2);
@@ -191,19 +228,57 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
                      const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                      const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
                      const uint16_t* lid_emb, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes,
-                     uint64_t* prof, int32_t waves) {
+                     uint64_t* prof, int32_t waves, int32_t nblocks) {
   if (ndocs <= 0) return 0;
+  if (nblocks <= 0) nblocks = ndocs;  // grid: docs perm[0 .. nblocks)
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
   auto kern = waves == 4 ? k_stage_analyze_w4 : waves == 5 ? k_stage_analyze_w5 : waves == 6 ? k_stage_analyze_w6
                                                                                               : k_stage_analyze;
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-  hipLaunchKernelGGL(kern, dim3(ndocs), dim3(64), lds_bytes, stream, (const DevPlan*)plan,
+  hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64), lds_bytes, stream, (const DevPlan*)plan,
                      (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, flags,
                      lid_emb, lid_vec, lid_cnt, lds_bytes, prof);
   return (int)hipGetLastError();
 }
+
+// Long-document variants: `perm` must point at the long prefix of the length-sorted
+// permutation, `nblocks` documents, one workgroup each.
+int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage, const uint8_t* bytes,
+                         const int64_t* off, const int32_t* perm, int32_t nblocks, int32_t ndocs, char* scratch,
+                         const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
+                         const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
+                         uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes, uint64_t* prof) {
+  if (nblocks <= 0) return 0;
+  if (!perm || lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
+  DevTables t{s1, s2, l1, l2};
+  if (lds_bytes > 65536)
+    (void)hipFuncSetAttribute((const void*)k_stage_analyze_blk, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds_bytes);
+  hipLaunchKernelGGL(k_stage_analyze_blk, dim3(nblocks), dim3(kBlockThreads), lds_bytes, stream,
+                     (const DevPlan*)plan, (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw,
+                     pw_n, t, rec, flags, lid_vec, lid_cnt, lds_bytes, prof);
+  return (int)hipGetLastError();
+}
+
+int tb_c4_pass_a_blk(hipStream_t stream, const void* c4, const uint8_t* bytes, const int64_t* off,
+                     const int32_t* perm, int32_t nblocks, int32_t ndocs, char* scratch, const int64_t* scratch_off,
+                     const uint64_t* pw, uint32_t pw_n, const uint16_t* s1, const uint32_t* s2, const uint16_t* l1,
+                     const int32_t* l2, int64_t* rec, int64_t* src, uint32_t* flags, uint32_t lds_bytes,
+                     uint64_t* prof) {
+  if (nblocks <= 0) return 0;
+  if (!perm || lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
+  DevTables t{s1, s2, l1, l2};
+  if (lds_bytes > 65536)
+    (void)hipFuncSetAttribute((const void*)k_c4_pass_a_blk, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds_bytes);
+  hipLaunchKernelGGL(k_c4_pass_a_blk, dim3(nblocks), dim3(kBlockThreads), lds_bytes, stream, (const DevC4*)c4,
+                     bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof);
+  return (int)hipGetLastError();
+}
+
+int tb_block_threads() { return kBlockThreads; }
 
 int tb_langid_features(hipStream_t stream, const uint8_t* bytes, const int64_t* off, const int32_t* perm,
                        int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint16_t* s1,
@@ -223,13 +298,14 @@ int tb_langid_features(hipStream_t stream, const uint8_t* bytes, const int64_t* 
 int tb_c4_pass_a(hipStream_t stream, const void* c4, const uint8_t* bytes, const int64_t* off, const int32_t* perm,
                  int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n,
                  const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
-                 int64_t* src, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
+                 int64_t* src, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, int32_t nblocks) {
   if (ndocs <= 0) return 0;
+  if (nblocks <= 0) nblocks = ndocs;
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k_c4_pass_a, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-  hipLaunchKernelGGL(k_c4_pass_a, dim3(ndocs), dim3(64), lds_bytes, stream, (const DevC4*)c4, bytes, off, perm, ndocs,
+  hipLaunchKernelGGL(k_c4_pass_a, dim3(nblocks), dim3(64), lds_bytes, stream, (const DevC4*)c4, bytes, off, perm, ndocs,
                      scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof);
   return (int)hipGetLastError();
 }

@@ -17,7 +17,14 @@ EDGE = ["", "   ", "\n\n", "a", "a\r\nb\r\n", "Hello.\n\n\nHello.\n\nHello.", "x
 @pytest.fixture(scope="module")
 def corpus():
     texts = synth.make_corpus(3000, 1024, seed=11) + EDGE
-    texts += [synth.make_doc(np.random.default_rng(7), "eng", 40000)]  # long doc
+    rng = np.random.default_rng(7)
+    # long documents run one workgroup each (BlockPar kernels): a spread of sizes and languages,
+    # plus long C4-heavy text (citations, policy lines, javascript, ellipses)
+    langs = ["eng", "dan", "swe", "nob", "nno"]
+    texts += [synth.make_doc(rng, langs[k % 5], int(s)) for k, s in enumerate(np.geomspace(4500, 90000, 24))]
+    c4ish = ("A line with a citation [1] and another [2, 3] here. Read our privacy policy today.\n"
+             "JavaScript must be enabled. Short one...\nThe quick brown fox jumps over the lazy dog.\n") * 200
+    texts += [c4ish, c4ish.replace("\n", " ")]
     return texts
 
 

@@ -17,8 +17,12 @@ _U32 = ctypes.c_uint32
 _I64 = ctypes.c_int64
 
 _SIGS = {
-    "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32],
-    "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
+    "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32],
+    "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32],
+    "tb_stage_analyze_blk": [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P,
+                             _U32, _P],
+    "tb_c4_pass_a_blk": [_P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
+    "tb_block_threads": [],
     "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
     "tb_c4_pass_b": [_P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "tb_langid_head": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I32, _P],
@@ -81,14 +85,33 @@ class Kernels:
         return self._pw, self._pw_n
 
     def stage_analyze(self, plan, stage, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, flags,
-                      lid_emb=None, lid_vec=None, lid_cnt=None, lds_bytes=0, prof=None, waves=0):
+                      lid_emb=None, lid_vec=None, lid_cnt=None, lds_bytes=0, prof=None, waves=0, nblocks=0):
         t = self.tabs
         rc = self.lib.tb_stage_analyze(
             self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs,
             scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
             t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), _ptr(lid_emb), _ptr(lid_vec),
-            _ptr(lid_cnt), lds_bytes, _ptr(prof), waves)
+            _ptr(lid_cnt), lds_bytes, _ptr(prof), waves, nblocks)
         _check(rc, "tb_stage_analyze")
+
+    def stage_analyze_blk(self, plan, stage, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n,
+                          rec, flags, lid_vec=None, lid_cnt=None, lds_bytes=0, prof=None):
+        t = self.tabs
+        rc = self.lib.tb_stage_analyze_blk(
+            self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), perm_long.data_ptr(),
+            nlong, ndocs, scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(),
+            t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), _ptr(lid_vec),
+            _ptr(lid_cnt), lds_bytes, _ptr(prof))
+        _check(rc, "tb_stage_analyze_blk")
+
+    def c4_pass_a_blk(self, c4, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags,
+                      lds_bytes=0, prof=None):
+        t = self.tabs
+        rc = self.lib.tb_c4_pass_a_blk(
+            self.stream(), c4.data_ptr(), bytes_.data_ptr(), off.data_ptr(), perm_long.data_ptr(), nlong, ndocs,
+            scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
+            t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), src.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof))
+        _check(rc, "tb_c4_pass_a_blk")
 
     def langid_features(self, bytes_, off, perm, ndocs, scratch, scratch_off, emb, vec, cnt, flags, lds_bytes=0,
                         prof=None):
@@ -100,12 +123,12 @@ class Kernels:
         _check(rc, "tb_langid_features")
 
     def c4_pass_a(self, c4, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags, lds_bytes=0,
-                  prof=None):
+                  prof=None, nblocks=0):
         t = self.tabs
         rc = self.lib.tb_c4_pass_a(
             self.stream(), c4.data_ptr(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs, scratch.data_ptr(),
             scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
-            t[3].data_ptr(), rec.data_ptr(), src.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof))
+            t[3].data_ptr(), rec.data_ptr(), src.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof), nblocks)
         _check(rc, "tb_c4_pass_a")
 
     def c4_pass_b(self, bytes_, off, ndocs, scratch, scratch_off, src, new_off, out):

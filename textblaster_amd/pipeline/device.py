@@ -92,6 +92,7 @@ class DeviceRunner:
     # 10 KB each costs no occupancy; the C4 kernel (7 waves/SIMD) only keeps per-line arrays there
     DEFAULT_LDS_BYTES = 10240
     DEFAULT_LDS_BYTES_C4 = 2048
+    DEFAULT_LONG_DOC_BYTES = 4096
     DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; sweep: tools/occ_sweep.sh)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None):
@@ -125,6 +126,9 @@ class DeviceRunner:
         self.lds_bytes = int(os.environ.get("TB_LDS_BYTES", str(self.DEFAULT_LDS_BYTES)))
         self.lds_bytes_c4 = int(os.environ.get("TB_LDS_BYTES_C4", str(self.DEFAULT_LDS_BYTES_C4)))
         self.stage_waves = int(os.environ.get("TB_STAGE_WAVES", str(self.DEFAULT_STAGE_WAVES)))
+        # documents longer than this run one workgroup (4 waves) each instead of one wave
+        self.long_doc_bytes = int(os.environ.get("TB_LONG_DOC_BYTES", str(self.DEFAULT_LONG_DOC_BYTES)))
+        self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", "32768"))
         self.lds_bytes_lid = int(os.environ.get("TB_LDS_BYTES_LID", "9216"))  # 64x33 int32 partials + sums
         # TB_PHASE_PROF=1: per-document phase cycle counters (s_memtime stamps) for profiling
         self.phase_prof = os.environ.get("TB_PHASE_PROF", "") not in ("", "0")
@@ -233,6 +237,7 @@ class DeviceRunner:
         scratch_off = np.zeros(ndocs + 1, dtype=np.int64)
         np.cumsum(per_doc, out=scratch_off[1:])
         maxlen = int(lens.max()) if ndocs else 0
+        n_long = int(np.count_nonzero(lens > self.long_doc_bytes)) if self.long_doc_bytes > 0 else 0
         (d_bytes, d_off, d_perm, d_soff), staged = self._stage_inputs(
             slot, [data if len(data) else np.zeros(1, np.uint8), off, perm, scratch_off])
         scratch = self._scratch_for(slot, int(scratch_off[-1]))
@@ -258,9 +263,17 @@ class DeviceRunner:
                     self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec, lid_cnt,
                                            flags, self.lds_bytes_lid, self._prof_buf(ndocs, keep, f"langid{s}"))
                 prof = self._prof_buf(ndocs, keep, f"stage{s}")
-                self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm, ndocs, scratch, d_soff, pw, pw_n,
-                                     rec, flags, self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
-                                     self.lds_bytes, prof, self.stage_waves)
+                # long documents (a length-sorted prefix of perm): one workgroup each; the rest:
+                # one wave each
+                if n_long:
+                    self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[:n_long], n_long, ndocs,
+                                             scratch, d_soff, pw, pw_n, rec, flags, lid_vec, lid_cnt,
+                                             self.lds_bytes_blk, prof)
+                if n_long < ndocs:
+                    self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,
+                                         scratch, d_soff, pw, pw_n, rec, flags,
+                                         self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
+                                         self.lds_bytes, prof, self.stage_waves, ndocs - n_long)
                 if lid_vec is not None:
                     self._last_lid = (lid_vec, lid_cnt)
                 for kind, width, prefix in layout:
@@ -272,8 +285,12 @@ class DeviceRunner:
                 rec = torch.zeros(7 * ndocs, dtype=torch.int64, device=self.device)
                 src = torch.zeros(2 * ndocs, dtype=torch.int64, device=self.device)
                 prof = self._prof_buf(ndocs, keep, f"c4_step{i}")
-                self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm, ndocs, scratch, d_soff, pw, pw_n, rec, src, flags,
-                                 self.lds_bytes_c4, prof)
+                if n_long:
+                    self.k.c4_pass_a_blk(self.c4_ts[i], vb, vo, d_perm[:n_long], n_long, ndocs, scratch, d_soff, pw,
+                                         pw_n, rec, src, flags, self.lds_bytes_blk, prof)
+                if n_long < ndocs:
+                    self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm[n_long:], ndocs, scratch, d_soff, pw,
+                                     pw_n, rec, src, flags, self.lds_bytes_c4, prof, ndocs - n_long)
                 new_off = torch.zeros(ndocs + 1, dtype=torch.int64, device=self.device)
                 torch.cumsum(src.view(ndocs, 2)[:, 1], 0, out=new_off[1:])
                 cap = vlen + self.c4_growth * ndocs + 16  # device rewrites never grow more (kC4MaxGrowth)

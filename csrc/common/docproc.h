@@ -605,15 +605,19 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     }
     x.stamp(PH_GR_TOP);
     if (ds.n_dup > 0) {
-      // per-n canonical-gram arrays and visited bitmaps; their scratch offsets are kept in scratch
+      // per-n canonical-gram arrays and visited bitmaps (pointers kept in scratch). The bitmaps
+      // (W bits each) are allocated first so they stay in LDS even for long documents: the
+      // sequential greedy walk probes them once per step.
+      const uint32_t SW = (W + 31) / 32 + 1;
+      uint32_t* sn_all = x.template alloc_hot<uint32_t>((uint64_t)SW * ds.n_dup);
       uint64_t* gofs = x.template alloc_hot<uint64_t>(2 * kMaxNgramEntries);
       if (x.overflow) return;
       for (int t = 0; t < ds.n_dup; ++t) {
         const uint32_t n = (uint32_t)ds.dup_n[t];
         if (n == 0 || W < n) continue;
         const uint32_t G = W - n + 1;
+        uint32_t* sn = sn_all + (size_t)t * SW;
         uint32_t* gct = x.template alloc_hot<uint32_t>(G);
-        uint32_t* sn = x.template alloc_hot<uint32_t>((G + 31) / 32 + 1);
         if (x.overflow) return;
         x.par.single([&]() {
           gofs[2 * t] = (uint64_t)(uintptr_t)gct;  // generic pointers (LDS or HBM)
@@ -648,13 +652,32 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       }
       x.par.sync();
       const int ndup = ds.n_dup;
+      // Skip the walk's duplicate-free prefix: before the first repeated gram p0 (gc[p] != p) the
+      // walk advances one position at a time and marks every gram p < p0 (each its own first
+      // occurrence), so it can start at p0 with bits [0, p0) set; no repeat at all -> 0.
+      uint32_t* p0s = x.template alloc_hot<uint32_t>(kMaxNgramEntries);
+      if (x.overflow) return;
+      for (int t = 0; t < ndup; ++t) {
+        const uint32_t n = (uint32_t)ds.dup_n[t];
+        if (n == 0 || W < n) continue;
+        const uint32_t G = W - n + 1;
+        const uint32_t* gc = (const uint32_t*)(uintptr_t)gofs[2 * t];
+        uint32_t* sn = (uint32_t*)(uintptr_t)gofs[2 * t + 1];
+        const uint32_t p0 = x.par.template min<uint32_t>(G, G, [&](uint32_t p) { return gc[p] != p ? p : G; });
+        x.par.for_n((p0 + 31) / 32, [&](uint32_t i) {
+          const uint32_t lo = i * 32;
+          sn[i] = (p0 - lo >= 32) ? 0xFFFFFFFFu : ((1u << (p0 - lo)) - 1u);
+        });
+        x.par.single([&]() { p0s[t] = p0; });
+      }
+      x.par.sync();
       x.par.for_n((uint32_t)ndup, [&](uint32_t t) {
         const uint32_t n = (uint32_t)ds.dup_n[t];
         int64_t rep = 0;
-        if (n > 0 && W >= n) {
+        if (n > 0 && W >= n && p0s[t] < W - n + 1) {
           const uint32_t* gc = (const uint32_t*)(uintptr_t)gofs[2 * t];
           uint32_t* sn = (uint32_t*)(uintptr_t)gofs[2 * t + 1];
-          uint32_t idx = 0;
+          uint32_t idx = p0s[t];
           while (idx + n <= W) {
             const uint32_t g = gc[idx];
             if ((sn[g >> 5] >> (g & 31)) & 1u) {

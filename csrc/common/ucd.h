@@ -47,6 +47,7 @@ struct UcdView {
   }
   // Simple (1:1) lowercase mapping; U+0130 additionally emits U+0307 (see lower_utf8).
   TB_HD uint32_t lower(uint32_t cp) const {
+    if (cp < 128) return (cp - 'A' < 26u) ? cp + 32 : cp;  // ASCII: no table round trip
     if (cp > 0x10FFFF) return cp;
     return (uint32_t)((int32_t)cp + lower_s2[((uint32_t)lower_s1[cp >> 7] << 7) | (cp & 127)]);
   }

@@ -231,7 +231,10 @@ class DeviceRunner:
         self._next_slot = (self._next_slot + 1) % self.N_SLOTS
         ndocs = len(off) - 1
         lens = np.diff(off)
-        perm = np.argsort(-lens, kind="stable").astype(np.int32)
+        # longest first (coarse 16-byte buckets are enough for scheduling): a stable radix sort
+        # on 16-bit keys instead of a comparison sort of int64 lengths
+        keys = (65535 - np.minimum(lens >> 4, 65535)).astype(np.uint16)
+        perm = np.argsort(keys, kind="stable").astype(np.int32)
         per_doc = (h.scratch_bytes_for(0) - 64 * 160) + 160 * (lens + 64)
         per_doc = (per_doc + SCRATCH_ALIGN - 1) // SCRATCH_ALIGN * SCRATCH_ALIGN
         scratch_off = np.zeros(ndocs + 1, dtype=np.int64)

@@ -142,11 +142,13 @@ TB_HD constexpr int rec_gr_fixed() { return 7; }
 
 // ---------------------------------------------------------------------------------------------
 template <class P>
-TB_HD Cps decode(DocCtx<P>& x, const uint8_t* b, uint32_t n) {
+TB_HD Cps decode(DocCtx<P>& x, const uint8_t* b, uint32_t n, bool hot_props = false) {
   Cps c;
+  // prop[] is read by every rule evaluation (UAX#29 look-around, trims, classes): with
+  // hot_props it goes to the LDS slice when the document is small enough
+  c.prop = hot_props ? x.template alloc_hot<uint32_t>(n + 1) : x.template alloc<uint32_t>(n + 1);
   c.off = x.template alloc<uint32_t>(n + 1);
   c.cp = x.template alloc<uint32_t>(n + 1);
-  c.prop = x.template alloc<uint32_t>(n + 1);
   if (x.overflow) return c;
   const UcdView ucd = x.ucd;
   uint32_t* off = c.off;
@@ -1072,6 +1074,11 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
 // ---------------------------------------------------------------------------------------------
 // Stage analysis for one content version: writes the records of every step of the stage.
 
+#ifndef TB_HOT_PROPS
+#define TB_HOT_PROPS 1
+#endif
+constexpr bool kHotProps = TB_HOT_PROPS != 0;
+
 template <class P, bool kWithLid = true>
 TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
                          const uint16_t* lid_emb, const uint8_t* b, uint32_t n, StageOut& out) {
@@ -1084,7 +1091,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
     if (k == DK_LANGID) need_lid = true;
   }
   x.stamp(PH_START);
-  Cps c = decode(x, b, n);
+  Cps c = decode(x, b, n, kHotProps);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   x.stamp(PH_DECODE);
   const uint32_t C = c.n;

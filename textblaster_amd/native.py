@@ -26,6 +26,8 @@ BUILD_DIR = os.path.join(REPO_DIR, "build")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX")
 HOST_EXT = os.path.join(PKG_DIR, "_tbhost" + EXT_SUFFIX)
 HIP_LIB = os.path.join(PKG_DIR, "libtbhip.so")
+# A/B experiments: TB_HIP_LIB points at an alternative build of the kernels (tools/build_variant.sh)
+_HIP_LIB_OVERRIDE = os.environ.get("TB_HIP_LIB")
 GPU_ARCH = os.environ.get("TB_GPU_ARCH", "gfx950")
 
 _lock = threading.Lock()
@@ -147,9 +149,10 @@ def hip() -> ctypes.CDLL:
     if _hip is None:
         with _lock:
             if _hip is None:
-                if not os.path.exists(HIP_LIB):
+                path = _HIP_LIB_OVERRIDE or HIP_LIB
+                if not _HIP_LIB_OVERRIDE and not os.path.exists(HIP_LIB):
                     build_hip()
-                _hip = ctypes.CDLL(HIP_LIB, mode=ctypes.RTLD_GLOBAL)
+                _hip = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
                 _declare_hip(_hip)
     return _hip
 

@@ -127,7 +127,7 @@ struct DocCtx {
     return (T*)(scr + a);
   }
   TB_HD void set_flag(uint32_t f) {
-    if (flag) *flag |= f;  // benign race: every writer stores the same bits
+    if (flag) P::or32(flag, f);  // atomic: kernels of different steps may run concurrently
   }
   TB_HD uint64_t powb(uint32_t k) const { return k <= pw_n ? pw[k] : powmod61(kHashBase, k); }
 };

@@ -47,6 +47,7 @@ class _Slot:
     def __init__(self):
         self.pinned = None
         self.scratch = None
+        self.scratch_c4 = None
         self.h2d_done = None  # event: the pinned staging buffer may be rewritten after it
 
 
@@ -130,6 +131,10 @@ class DeviceRunner:
         self.long_doc_bytes = int(os.environ.get("TB_LONG_DOC_BYTES", str(self.DEFAULT_LONG_DOC_BYTES)))
         self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", "32768"))
         self.lds_bytes_lid = int(os.environ.get("TB_LDS_BYTES_LID", "9216"))  # 64x33 int32 partials + sums
+        if self.lds_bytes_lid < 9216:
+            # the language-id kernel runs concurrently with the stage kernels and must not touch
+            # their HBM scratch arena: its working set has to fit its LDS slice
+            raise DeviceError("TB_LDS_BYTES_LID must be >= 9216")
         # TB_PHASE_PROF=1: per-document phase cycle counters (s_memtime stamps) for profiling
         self.phase_prof = os.environ.get("TB_PHASE_PROF", "") not in ("", "0")
         self.phase_totals: Dict[str, np.ndarray] = {}
@@ -137,6 +142,9 @@ class DeviceRunner:
         self.slots = [_Slot() for _ in range(self.N_SLOTS)]
         self.h2d_stream = torch.cuda.Stream(self.device)
         self.d2h_stream = torch.cuda.Stream(self.device)
+        self.s_lid = torch.cuda.Stream(self.device)
+        self.s_blk = torch.cuda.Stream(self.device)
+        self.s_c4 = torch.cuda.Stream(self.device)
         self.copy_threads = int(os.environ.get("TB_COPY_THREADS", "8"))
         self._next_slot = 0
         self._last_lid = None
@@ -184,12 +192,19 @@ class DeviceRunner:
             out.append(dev[o:o + a.nbytes].view(dt) if a.nbytes else dev[o:o].view(dt))
         return out, dev
 
-    def _scratch_for(self, slot: _Slot, nbytes: int):
-        if slot.scratch is None or slot.scratch.numel() < nbytes:
-            slot.scratch = None
-            slot.scratch = self.torch.empty(int(nbytes * 1.25) + (1 << 20), dtype=self.torch.uint8,
-                                            device=self.device)
-        return slot.scratch
+    def _scratch_for(self, slot: _Slot, nbytes: int, which: str = "stage"):
+        attr = "scratch" if which == "stage" else "scratch_c4"
+        cur = getattr(slot, attr)
+        if cur is None or cur.numel() < nbytes:
+            setattr(slot, attr, None)
+            cur = self.torch.empty(int(nbytes * 1.25) + (1 << 20), dtype=self.torch.uint8, device=self.device)
+            setattr(slot, attr, cur)
+        return cur
+
+    def _record(self, stream):
+        ev = self.torch.cuda.Event()
+        ev.record(stream)
+        return ev
 
     def _prof_buf(self, ndocs, keep, name):
         if not self.phase_prof:
@@ -251,8 +266,17 @@ class DeviceRunner:
         stage_recs_d: List = [None] * len(self.plan.stages)
         c4_recs_d = {}
         keep = [staged, scratch]
+        # Independent work runs concurrently on side streams (events order the dependencies):
+        #   language-id bag (s_lid) | long-doc workgroup kernels (s_blk) | wave kernels (main)
+        #   | C4 pass A/B of the same content version (s_c4, own scratch arena)
+        # Block and wave kernels touch disjoint documents, so they share the stage arena.
+        main = torch.cuda.current_stream(self.device)
+        ready = {0: self._record(main)}
+        tails = []
+        c4_scratch = None
         for ver in range(self.plan.n_versions):
             vb, vo, vlen = versions[ver]
+            main.wait_event(ready[ver])
             for s, sv in enumerate(self.plan.stage_version):
                 if sv != ver:
                     continue
@@ -262,16 +286,23 @@ class DeviceRunner:
                 if any(kind == 4 for kind, _, _ in layout):
                     lid_vec = torch.zeros(ndocs * h.LID_DIM, dtype=torch.int16, device=self.device)
                     lid_cnt = torch.zeros(ndocs, dtype=torch.int32, device=self.device)
+                ev_pre = self._record(main)  # rec / lid buffers zeroed
+                ev_lid = ev_blk = None
                 if lid_vec is not None:
-                    self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec, lid_cnt,
-                                           flags, self.lds_bytes_lid, self._prof_buf(ndocs, keep, f"langid{s}"))
+                    self.s_lid.wait_event(ev_pre)
+                    with torch.cuda.stream(self.s_lid):
+                        self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec,
+                                               lid_cnt, flags, self.lds_bytes_lid,
+                                               self._prof_buf(ndocs, keep, f"langid{s}"))
+                        ev_lid = self._record(self.s_lid)
                 prof = self._prof_buf(ndocs, keep, f"stage{s}")
-                # long documents (a length-sorted prefix of perm): one workgroup each; the rest:
-                # one wave each
                 if n_long:
-                    self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[:n_long], n_long, ndocs,
-                                             scratch, d_soff, pw, pw_n, rec, flags, lid_vec, lid_cnt,
-                                             self.lds_bytes_blk, prof)
+                    self.s_blk.wait_event(ev_pre)
+                    with torch.cuda.stream(self.s_blk):
+                        self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[:n_long], n_long,
+                                                 ndocs, scratch, d_soff, pw, pw_n, rec, flags, lid_vec, lid_cnt,
+                                                 self.lds_bytes_blk, prof)
+                        ev_blk = self._record(self.s_blk)
                 if n_long < ndocs:
                     self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,
                                          scratch, d_soff, pw, pw_n, rec, flags,
@@ -279,29 +310,43 @@ class DeviceRunner:
                                          self.lds_bytes, prof, self.stage_waves, ndocs - n_long)
                 if lid_vec is not None:
                     self._last_lid = (lid_vec, lid_cnt)
+                    main.wait_event(ev_lid)
+                if ev_blk is not None:
+                    main.wait_event(ev_blk)
                 for kind, width, prefix in layout:
                     if kind == 4:
                         self.k.langid_head(lid_vec, lid_cnt, self.lid_wT, self.lid_b, ndocs, rec, prefix * ndocs, width)
                 stage_recs_d[s] = rec
             c4_here = [i for i in self.plan.c4_steps if self.plan.steps[i].version_in == ver]
             for i in c4_here:
+                if c4_scratch is None:
+                    c4_scratch = self._scratch_for(slot, int(scratch_off[-1]), which="c4")
+                    keep.append(c4_scratch)
                 rec = torch.zeros(7 * ndocs, dtype=torch.int64, device=self.device)
                 src = torch.zeros(2 * ndocs, dtype=torch.int64, device=self.device)
-                prof = self._prof_buf(ndocs, keep, f"c4_step{i}")
-                if n_long:
-                    self.k.c4_pass_a_blk(self.c4_ts[i], vb, vo, d_perm[:n_long], n_long, ndocs, scratch, d_soff, pw,
-                                         pw_n, rec, src, flags, self.lds_bytes_blk, prof)
-                if n_long < ndocs:
-                    self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm[n_long:], ndocs, scratch, d_soff, pw,
-                                     pw_n, rec, src, flags, self.lds_bytes_c4, prof, ndocs - n_long)
                 new_off = torch.zeros(ndocs + 1, dtype=torch.int64, device=self.device)
-                torch.cumsum(src.view(ndocs, 2)[:, 1], 0, out=new_off[1:])
                 cap = vlen + self.c4_growth * ndocs + 16  # device rewrites never grow more (kC4MaxGrowth)
                 out = torch.empty(cap, dtype=torch.uint8, device=self.device)
-                self.k.c4_pass_b(vb, vo, ndocs, scratch, d_soff, src, new_off, out)
+                self.s_c4.wait_event(self._record(main))
+                self.s_c4.wait_event(ready[ver])
+                with torch.cuda.stream(self.s_c4):
+                    prof = self._prof_buf(ndocs, keep, f"c4_step{i}")
+                    if n_long:
+                        self.k.c4_pass_a_blk(self.c4_ts[i], vb, vo, d_perm[:n_long], n_long, ndocs, c4_scratch,
+                                             d_soff, pw, pw_n, rec, src, flags, self.lds_bytes_blk, prof)
+                    if n_long < ndocs:
+                        self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm[n_long:], ndocs, c4_scratch, d_soff, pw,
+                                         pw_n, rec, src, flags, self.lds_bytes_c4, prof, ndocs - n_long)
+                    torch.cumsum(src.view(ndocs, 2)[:, 1], 0, out=new_off[1:])
+                    self.k.c4_pass_b(vb, vo, ndocs, c4_scratch, d_soff, src, new_off, out)
+                    ev = self._record(self.s_c4)
                 versions[ver + 1] = (out, new_off, cap)
+                ready[ver + 1] = ev
+                tails.append(ev)
                 c4_recs_d[i] = rec
                 keep.append(src)
+        for ev in tails:
+            main.wait_event(ev)
         # D2H into pinned host buffers on the download stream (overlaps the next batch's
         # kernels), then one completion event
         done = torch.cuda.Event()

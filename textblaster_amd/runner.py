@@ -88,6 +88,7 @@ class RunStats:
     units_skipped: int = 0
     delegated: int = 0
     step_filtered: List[int] = dataclasses.field(default_factory=list)
+    phase_seconds: Dict[str, float] = dataclasses.field(default_factory=dict)  # rank 0's own view
 
     @property
     def docs_per_sec(self) -> float:
@@ -142,8 +143,16 @@ class _UnitReader:
         self.reader = reader
         self._rg = -1
         self._tbl = None
+        self.seconds = 0.0
 
     def read(self, u: Unit) -> DocBatch:
+        t0 = time.perf_counter()
+        try:
+            return self._read(u)
+        finally:
+            self.seconds += time.perf_counter() - t0
+
+    def _read(self, u: Unit) -> DocBatch:
         if u.row_group != self._rg:
             self._tbl = self.reader._pf.read_row_group(u.row_group, columns=self.reader.columns, use_threads=True)
             self._rg = u.row_group
@@ -288,6 +297,7 @@ class _Writer:
         self.sink = sink
         self.q: queue.Queue = queue.Queue(maxsize=depth)
         self.err: List[BaseException] = []
+        self.seconds = 0.0
         self.t = threading.Thread(target=self._run, name="tb-writer", daemon=True)
         self.t.start()
 
@@ -298,6 +308,7 @@ class _Writer:
                 return
             if self.err:
                 continue
+            t0 = time.perf_counter()
             try:
                 batch, res, unit, counts = job
                 kept = part_table(batch, res.kept[0]) if len(res.kept) == 1 else pa.concat_tables(
@@ -311,6 +322,7 @@ class _Writer:
                 self.sink.write(unit, kept, exc, counts)
             except BaseException as e:  # noqa: BLE001
                 self.err.append(e)
+            self.seconds += time.perf_counter() - t0
 
     def submit(self, job):
         if self.err:
@@ -407,6 +419,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
             inflight.append((unit, batch))
             yield batch.text[0], batch.text[1], batch.meta
 
+    t_loop = time.perf_counter()
     try:
         t_prev = time.perf_counter()
         for res in engine.process_many(feed(), on_error="recover"):
@@ -438,12 +451,15 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
                 last_report, last_docs = now, local.docs
     finally:
         writer.close()
+    phase = {"read": ureader.seconds, "write": writer.seconds, "main_loop": time.perf_counter() - t_loop}
+    log.info("rank %d phases: %s", rank, {k: round(v, 3) for k, v in phase.items()})
     elapsed = time.perf_counter() - t_start
     total_vec = ctx.all_reduce_sum(local.vector(nsteps))
     elapsed_max = ctx.all_reduce_max(elapsed)
     units_done = int(ctx.all_reduce_sum([local.units])[0])
     skipped = int(ctx.all_reduce_sum([local.units_skipped])[0])
     stats = RunStats.from_vector(total_vec, elapsed_max, units_done, skipped)
+    stats.phase_seconds = phase
     if use_parts:
         ctx.barrier()
         if rank == 0:

@@ -70,7 +70,8 @@ def main():
         st = run(RunConfig(inp, o, e, args.config, backend=backend, unit_rows=args.unit_rows))
         line = {"backend": backend, "docs": st.docs, "kept": st.kept, "excluded": st.excluded, "errors": st.errors,
                 "seconds": round(st.seconds, 3), "docs_per_sec": round(st.docs_per_sec, 1),
-                "step_filtered": st.step_filtered, "delegated": st.delegated}
+                "step_filtered": st.step_filtered, "delegated": st.delegated,
+                "phase_seconds": {k: round(v, 3) for k, v in st.phase_seconds.items()}}
         print(json.dumps(line), flush=True)
         for p in (o, e):
             os.remove(p)

@@ -73,6 +73,7 @@ class RunConfig:
     metrics_port: Optional[int] = None
     progress_interval: float = 1.0
     tokenizer_file: Optional[str] = None
+    read_threads: int = int(os.environ.get("TB_READ_THREADS", "3"))  # row groups decoded concurrently
     fault_inject: Optional[str] = None   # debug: "kernel@N" / "oom@N" (N = 1-based batch)
 
 
@@ -139,11 +140,13 @@ class _UnitReader:
     """Reads units in order, caching the last decoded row group (consecutive units usually share
     it)."""
 
-    def __init__(self, reader: ParquetReader):
+    def __init__(self, reader: ParquetReader, own_file: bool = False):
         self.reader = reader
         self._rg = -1
         self._tbl = None
         self.seconds = 0.0
+        # worker threads open their own ParquetFile (a reader object is not shared across threads)
+        self._pf = pq.ParquetFile(reader.config.path) if own_file else None
 
     def read(self, u: Unit) -> DocBatch:
         t0 = time.perf_counter()
@@ -154,7 +157,8 @@ class _UnitReader:
 
     def _read(self, u: Unit) -> DocBatch:
         if u.row_group != self._rg:
-            self._tbl = self.reader._pf.read_row_group(u.row_group, columns=self.reader.columns, use_threads=True)
+            pf = self._pf if self._pf is not None else self.reader._pf
+            self._tbl = pf.read_row_group(u.row_group, columns=self.reader.columns, use_threads=True)
             self._rg = u.row_group
         t = self._tbl.slice(u.start, u.stop - u.start).combine_chunks()
         batches = t.to_batches()
@@ -290,6 +294,44 @@ def _prefetch(gen: Iterator, depth: int) -> Iterator:
         stop.set()
 
 
+def _read_units(reader: ParquetReader, units: List[Unit], nthreads: int, timer: _UnitReader):
+    """Yields (unit, DocBatch) in order. Row groups are decoded by up to ``nthreads`` worker
+    threads at once (Parquet decompression + HTML-entity decoding dominate the input side);
+    each row group is read once and sliced into its units."""
+    import concurrent.futures as cf
+
+    groups: List[List[Unit]] = []
+    for u in units:
+        if groups and groups[-1][0].row_group == u.row_group:
+            groups[-1].append(u)
+        else:
+            groups.append([u])
+
+    def load(group: List[Unit]):
+        r = _UnitReader(reader, own_file=nthreads > 1)
+        out = [(u, r.read(u)) for u in group]
+        timer.seconds += r.seconds
+        return out
+
+    if nthreads <= 1:
+        for g in groups:
+            yield from load(g)
+        return
+    with cf.ThreadPoolExecutor(max_workers=nthreads, thread_name_prefix="tb-reader") as ex:
+        pending: collections.deque = collections.deque()
+        it = iter(groups)
+        for g in it:
+            pending.append(ex.submit(load, g))
+            if len(pending) >= nthreads + 1:
+                break
+        while pending:
+            fut = pending.popleft()
+            nxt = next(it, None)
+            if nxt is not None:
+                pending.append(ex.submit(load, nxt))
+            yield from fut.result()
+
+
 class _Writer:
     """Single background writer thread; ``submit`` blocks when ``depth`` writes are pending."""
 
@@ -415,7 +457,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     inflight: collections.deque = collections.deque()
 
     def feed():
-        for unit, batch in _prefetch(((u, ureader.read(u)) for u in todo), depth=2):
+        for unit, batch in _read_units(reader, todo, rc.read_threads, ureader):
             inflight.append((unit, batch))
             yield batch.text[0], batch.text[1], batch.meta
 

@@ -142,6 +142,80 @@ __global__ __launch_bounds__(kBlockThreads) void k_c4_pass_a_blk(
   c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2);
 }
 
+// C4 bad words (reference c4_filters.rs:431-441,516): does any list entry occur, case-folded,
+// with \W (or text edge) on both sides (no boundary requirement for CJK lists)? One wave per
+// document; every code point position (UTF-8 lead byte) starts an automaton walk in parallel;
+// the wave stops at the first 64-position chunk that contains a match.
+struct BwAutomaton {
+  const int32_t* first_edge;
+  const uint32_t* edge_cp;
+  const int32_t* edge_to;
+  const uint8_t* term;
+};
+
+__device__ __forceinline__ int32_t bw_next(const BwAutomaton& a, int32_t node, uint32_t c) {
+  int32_t lo = a.first_edge[node], hi = a.first_edge[node + 1];
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    const uint32_t v = a.edge_cp[mid];
+    if (v == c) return a.edge_to[mid];
+    if (v < c) lo = mid + 1; else hi = mid;
+  }
+  return -1;
+}
+
+__global__ __launch_bounds__(64) void k_badwords_match(const uint8_t* __restrict__ bytes,
+                                                       const int64_t* __restrict__ off, int32_t ndocs,
+                                                       const int32_t* __restrict__ root,
+                                                       const uint8_t* __restrict__ cjk, BwAutomaton a,
+                                                       DevTables tabs, const uint16_t* __restrict__ f1,
+                                                       const int32_t* __restrict__ f2, int8_t* matched) {
+  const int doc = blockIdx.x;
+  if (doc >= ndocs) return;
+  const int32_t r0 = root[doc];
+  if (r0 < 0) return;
+  const uint8_t* b = bytes + off[doc];
+  const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
+  const UcdView ucd{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
+  const bool any_edge = cjk[doc] != 0;
+  const uint32_t lane = threadIdx.x;
+  auto fold = [&](uint32_t c) -> uint32_t {
+    if (c > 0x10FFFF) return c;
+    return (uint32_t)((int32_t)c + f2[((uint32_t)f1[c >> 7] << 7) | (c & 127)]);
+  };
+  auto wordchar_at = [&](uint32_t s) {  // code point starting at byte s
+    int len;
+    return (ucd.props(utf8_decode(b, s, n, &len)) & P_WORDCHAR) != 0;
+  };
+  bool found = false;
+  for (uint32_t base = 0; base < n; base += 64) {
+    const uint32_t s = base + lane;
+    if (s < n && utf8_is_lead(b[s])) {
+      bool ok = any_edge || s == 0;
+      if (!ok) {
+        int64_t p = (int64_t)s - 1;
+        while (p >= 0 && !utf8_is_lead(b[p])) --p;
+        ok = p < 0 || !wordchar_at((uint32_t)p);
+      }
+      if (ok) {
+        int32_t node = r0;
+        uint32_t j = s;
+        while (j < n) {
+          int len;
+          const uint32_t c = utf8_decode(b, j, n, &len);
+          node = bw_next(a, node, fold(c));
+          if (node < 0) break;
+          j += (uint32_t)len;
+          if (a.term[node] && (any_edge || j >= n || !wordchar_at(j))) { found = true; break; }
+        }
+      }
+    }
+    if (__ballot(found)) break;
+  }
+  const bool anyf = __ballot(found) != 0;
+  if (lane == 0) matched[doc] = anyf ? 1 : 0;
+}
+
 __global__ __launch_bounds__(256) void k_c4_pass_b(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
                                                    int32_t ndocs, const char* __restrict__ scratch,
                                                    const int64_t* __restrict__ scratch_off,
@@ -279,6 +353,18 @@ int tb_c4_pass_a_blk(hipStream_t stream, const void* c4, const uint8_t* bytes, c
 }
 
 int tb_block_threads() { return kBlockThreads; }
+
+int tb_badwords_match(hipStream_t stream, const uint8_t* bytes, const int64_t* off, int32_t ndocs, const int32_t* root,
+                      const uint8_t* cjk, const int32_t* first_edge, const uint32_t* edge_cp, const int32_t* edge_to,
+                      const uint8_t* term, const uint16_t* s1, const uint32_t* s2, const uint16_t* l1,
+                      const int32_t* l2, const uint16_t* f1, const int32_t* f2, int8_t* matched) {
+  if (ndocs <= 0) return 0;
+  DevTables t{s1, s2, l1, l2};
+  BwAutomaton a{first_edge, edge_cp, edge_to, term};
+  hipLaunchKernelGGL(k_badwords_match, dim3(ndocs), dim3(64), 0, stream, bytes, off, ndocs, root, cjk, a, t, f1, f2,
+                     matched);
+  return (int)hipGetLastError();
+}
 
 int tb_langid_features(hipStream_t stream, const uint8_t* bytes, const int64_t* off, const int32_t* perm,
                        int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint16_t* s1,

@@ -183,6 +183,11 @@ PYBIND11_MODULE(_tbhost, m) {
   m.def("trim", [](const std::string& s) { return std::string(trim(s)); });
   m.def("props", [](uint32_t cp) { return host_ucd().props(cp); });
   m.def("has_dict_script", [](const std::string& s) { return has_dict_script(s); });
+  m.def("ucd_fold_tables", []() {
+    std::vector<uint16_t> f1(TB_UCD_FOLD_STAGE1, TB_UCD_FOLD_STAGE1 + sizeof(TB_UCD_FOLD_STAGE1) / 2);
+    std::vector<int32_t> f2(TB_UCD_FOLD_STAGE2, TB_UCD_FOLD_STAGE2 + sizeof(TB_UCD_FOLD_STAGE2) / 4);
+    return py::make_tuple(to_numpy(std::move(f1)), to_numpy(std::move(f2)));
+  });
   m.def("ucd_tables", []() {
     std::vector<uint16_t> s1(TB_UCD_PROPS_STAGE1, TB_UCD_PROPS_STAGE1 + sizeof(TB_UCD_PROPS_STAGE1) / 2);
     std::vector<uint32_t> s2((const uint32_t*)TB_UCD_PROPS_STAGE2,
@@ -324,6 +329,14 @@ PYBIND11_MODULE(_tbhost, m) {
         if (!l) return false;
         return l->match(text);
       })
+      .def("flatten", [](BadWordsModule& b) {
+        BadWordsAutomaton a = b.flatten();
+        py::dict roots, cjk;
+        for (auto& kv : a.root) roots[py::str(kv.first)] = kv.second;
+        for (auto& kv : a.cjk) cjk[py::str(kv.first)] = kv.second;
+        return py::make_tuple(to_numpy(std::move(a.first_edge)), to_numpy(std::move(a.edge_cp)),
+                              to_numpy(std::move(a.edge_to)), to_numpy(std::move(a.term)), roots, cjk);
+      })
       .def("lookup", [](BadWordsModule& b, const std::string& lang) {
         // (supported language?, has a non-empty list?)
         bool sup;
@@ -395,6 +408,32 @@ PYBIND11_MODULE(_tbhost, m) {
       .def("apply_badwords", [](PyBatch& b, const StepCfg& c, int step_index, std::shared_ptr<BadWordsModule> bw) {
         py::gil_scoped_release nogil;
         b.st->apply_badwords(c, step_index, *bw);
+      })
+      .def("badwords_languages", [](PyBatch& b, const StepCfg& c, std::shared_ptr<BadWordsModule> bw) {
+        std::vector<std::string> out;
+        {
+          py::gil_scoped_release nogil;
+          out = b.st->badwords_languages(c, *bw);
+        }
+        return out;
+      })
+      .def("apply_badwords_matched", [](PyBatch& b, const StepCfg& c, int step_index, std::shared_ptr<BadWordsModule> bw,
+                                        py::array_t<int8_t, py::array::c_style> matched,
+                                        const std::vector<std::string>& langs) {
+        if ((int64_t)matched.size() != b.st->size() || (int64_t)langs.size() != b.st->size())
+          throw std::invalid_argument("matched/langs length");
+        py::gil_scoped_release nogil;
+        b.st->apply_badwords_matched(c, step_index, *bw, matched.data(), langs);
+      })
+      .def("gather", [](PyBatch& b, py::array_t<int64_t, py::array::c_style> idx) {
+        std::vector<int64_t> iv(idx.data(), idx.data() + idx.size());
+        RawBuf d;
+        std::vector<int64_t> o;
+        {
+          py::gil_scoped_release nogil;
+          b.st->gather(iv, d, o);
+        }
+        return py::make_tuple(raw_to_numpy(d), to_numpy(std::move(o)));
       })
       .def("delegate", [](PyBatch& b, py::array_t<int64_t, py::array::c_style> idx) {
         b.st->delegate(idx.data(), (int64_t)idx.size());

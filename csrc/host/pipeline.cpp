@@ -172,6 +172,45 @@ std::shared_ptr<BadWordsLang> BadWordsModule::get(const std::string& lang, bool*
   return res;
 }
 
+BadWordsAutomaton BadWordsModule::flatten() const {
+  BadWordsAutomaton a;
+  a.first_edge.push_back(0);
+  std::vector<std::string> names;
+  for (auto& kv : langs) names.push_back(kv.first);
+  std::sort(names.begin(), names.end());
+  for (const auto& name : names) {
+    const auto& bl = langs.at(name);
+    if (!bl) continue;
+    const int32_t base = (int32_t)a.term.size();
+    a.root[name] = base;
+    a.cjk[name] = bl->cjk;
+    for (const auto& node : bl->trie) {
+      std::vector<std::pair<uint32_t, int>> edges(node.next.begin(), node.next.end());
+      std::sort(edges.begin(), edges.end());
+      for (auto& e : edges) {
+        a.edge_cp.push_back(e.first);
+        a.edge_to.push_back(base + e.second);
+      }
+      a.first_edge.push_back((int32_t)a.edge_cp.size());
+      a.term.push_back(node.term ? 1 : 0);
+    }
+  }
+  return a;
+}
+
+void BatchState::gather(const std::vector<int64_t>& idx, RawBuf& data, std::vector<int64_t>& off) const {
+  const int64_t m = (int64_t)idx.size();
+  off.assign(m + 1, 0);
+  for (int64_t k = 0; k < m; ++k) off[k + 1] = off[k] + (int64_t)content(idx[k]).size();
+  data.alloc((size_t)off[m]);
+  parallel_for(m, nthreads_, [&](int64_t a, int64_t b) {
+    for (int64_t k = a; k < b; ++k) {
+      std::string_view t = content(idx[k]);
+      if (!t.empty()) std::memcpy(data.p + off[k], t.data(), t.size());
+    }
+  });
+}
+
 StdRng::StdRng(uint64_t state) {
   for (int i = 0; i < 8; ++i) {  // rand_core SeedableRng::seed_from_u64
     state = state * 6364136223846793005ull + 11634580027462260723ull;
@@ -335,11 +374,7 @@ void BatchState::apply_records(const StepCfg& cfg, int step_index, const int64_t
   });
 }
 
-void BatchState::apply_badwords(const StepCfg& cfg, int step_index, BadWordsModule& mod) {
-  step_slot(step_index);
-  auto out = std::make_unique<BwOut>();
-  out->code.assign(n_, -1);
-  out->lang.resize(n_);
+std::vector<std::string> BatchState::badwords_languages(const StepCfg& cfg, BadWordsModule& mod) const {
   // The document language: metadata "language" (no step writes that key, so only the input
   // metadata can hold it), else the configured default (reference c4_filters.rs:478-486).
   std::vector<std::string> lang(n_);
@@ -351,12 +386,17 @@ void BatchState::apply_badwords(const StepCfg& cfg, int step_index, BadWordsModu
       if (input_meta(i, fm) && fm.has("language")) lang[i] = std::string(fm.get("language"));
     }
   });
-  // lists load lazily on this thread, then matching runs in parallel
+  // word lists load lazily, on this thread
   for (int64_t i = 0; i < n_; ++i) {
     if (fail_step_[i] >= 0) continue;
     bool sup;
     mod.get(lang[i], &sup);
   }
+  return lang;
+}
+
+void BatchState::apply_badwords(const StepCfg& cfg, int step_index, BadWordsModule& mod) {
+  const std::vector<std::string> lang = badwords_languages(cfg, mod);
   std::vector<int8_t> matched(n_, -1);  // -1 n/a, 0 no match, 1 match
   parallel_for(n_, nthreads_, [&](int64_t a, int64_t b) {
     for (int64_t i = a; i < b; ++i) {
@@ -365,6 +405,15 @@ void BatchState::apply_badwords(const StepCfg& cfg, int step_index, BadWordsModu
       if (it != mod.langs.end() && it->second) matched[i] = it->second->match(content(i)) ? 1 : 0;
     }
   });
+  apply_badwords_matched(cfg, step_index, mod, matched.data(), lang);
+}
+
+void BatchState::apply_badwords_matched(const StepCfg& cfg, int step_index, BadWordsModule& mod,
+                                        const int8_t* matched, const std::vector<std::string>& lang) {
+  step_slot(step_index);
+  auto out = std::make_unique<BwOut>();
+  out->code.assign(n_, -1);
+  out->lang.resize(n_);
   if (!mod.rng) {
     uint64_t seed = cfg.seed ? *cfg.seed : (((uint64_t)std::random_device{}() << 32) ^ std::random_device{}());
     mod.rng = std::make_unique<StdRng>(seed);

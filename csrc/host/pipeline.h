@@ -53,8 +53,20 @@ struct StdRng {
   float gen_f32() { return (float)(next_u32() >> 8) * (1.0f / 16777216.0f); }
 };
 
+// All loaded bad-words tries flattened for the device matcher (k_badwords_match): per node a
+// sorted edge list (folded code point -> node) and a terminal flag; per language a root node.
+struct BadWordsAutomaton {
+  std::vector<int32_t> first_edge;  // [nodes + 1]
+  std::vector<uint32_t> edge_cp;    // [edges], sorted per node
+  std::vector<int32_t> edge_to;     // [edges]
+  std::vector<uint8_t> term;        // [nodes]
+  std::unordered_map<std::string, int32_t> root;
+  std::unordered_map<std::string, bool> cjk;
+};
+
 struct BadWordsModule {
   std::string cache_dir;
+  BadWordsAutomaton flatten() const;
   std::unique_ptr<StdRng> rng;  // shared by every document, drawn in document order
   std::unordered_map<std::string, std::shared_ptr<BadWordsLang>> langs;  // nullptr = no list
   std::shared_ptr<BadWordsLang> get(const std::string& lang, bool* supported);
@@ -105,6 +117,14 @@ class BatchState {
   void run_cpu(const std::vector<StepCfg>& steps, int begin, int end, SegBackend be,
                const LangidModel* lid, BadWordsModule* bw);
   void apply_badwords(const StepCfg& cfg, int step_index, BadWordsModule& mod);
+  // Device path of the bad-words step: languages per alive document (lists loaded), then the
+  // decisions from externally computed matches (-1 n/a, 0, 1), drawing the keep-fraction RNG
+  // in document order exactly like apply_badwords.
+  std::vector<std::string> badwords_languages(const StepCfg& cfg, BadWordsModule& mod) const;
+  void apply_badwords_matched(const StepCfg& cfg, int step_index, BadWordsModule& mod, const int8_t* matched,
+                              const std::vector<std::string>& lang);
+  // Current contents of documents idx, packed (for device steps that run after the resolve).
+  void gather(const std::vector<int64_t>& idx, RawBuf& data, std::vector<int64_t>& off) const;
 
   // Remove documents from this batch (they are processed elsewhere, e.g. the CPU oracle path).
   void delegate(const int64_t* idx, int64_t n);

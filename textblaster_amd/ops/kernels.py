@@ -23,6 +23,7 @@ _SIGS = {
                              _U32, _P],
     "tb_c4_pass_a_blk": [_P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
     "tb_block_threads": [],
+    "tb_badwords_match": [_P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
     "tb_c4_pass_b": [_P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "tb_langid_head": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I32, _P],
@@ -112,6 +113,16 @@ class Kernels:
             scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
             t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), src.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof))
         _check(rc, "tb_c4_pass_a_blk")
+
+    def badwords_match(self, bytes_, off, ndocs, root, cjk, automaton, fold, matched):
+        t = self.tabs
+        fe, ec, et, term = automaton
+        f1, f2 = fold
+        rc = self.lib.tb_badwords_match(
+            self.stream(), bytes_.data_ptr(), off.data_ptr(), ndocs, root.data_ptr(), cjk.data_ptr(), fe.data_ptr(),
+            ec.data_ptr(), et.data_ptr(), term.data_ptr(), t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
+            t[3].data_ptr(), f1.data_ptr(), f2.data_ptr(), matched.data_ptr())
+        _check(rc, "tb_badwords_match")
 
     def langid_features(self, bytes_, off, perm, ndocs, scratch, scratch_off, emb, vec, cnt, flags, lds_bytes=0,
                         prof=None):

@@ -148,6 +148,43 @@ class DeviceRunner:
         self.copy_threads = int(os.environ.get("TB_COPY_THREADS", "8"))
         self._next_slot = 0
         self._last_lid = None
+        self.s_bw = torch.cuda.Stream(self.device)
+        self._bw_auto = None  # (key, device tensors) of the flattened bad-words automaton
+        self._bw_fold = None
+
+    def badwords_match(self, key, automaton, data: np.ndarray, off: np.ndarray, roots: np.ndarray,
+                       cjk: np.ndarray) -> np.ndarray:
+        """C4 bad-words matching of post-resolve contents on the device (k_badwords_match): one
+        wave per document walks the flattened word-list tries from every code point. ``roots``:
+        per document the root node of its language's trie. Returns 1 (match) / 0 per document."""
+        torch = self.torch
+        n = len(off) - 1
+        if n == 0:
+            return np.zeros(0, dtype=np.int8)
+        if roots.shape != (n,) or cjk.shape != (n,) or int(off[-1]) > len(data):
+            raise DeviceError("badwords_match: operand shapes")
+        if self._bw_fold is None:
+            f1, f2 = native.host().ucd_fold_tables()
+            self._bw_fold = (torch.from_numpy(f1).to(self.device), torch.from_numpy(f2).to(self.device))
+        if self._bw_auto is None or self._bw_auto[0] != key:
+            fe, ec, et, term = automaton
+            nodes = len(term)
+            if len(fe) != nodes + 1 or len(ec) != len(et) or int(fe[-1]) != len(ec):
+                raise DeviceError("badwords automaton is malformed")
+            if nodes and (int(roots.max()) >= nodes or (len(et) and (int(et.min()) < 0 or int(et.max()) >= nodes))):
+                raise DeviceError("badwords automaton node index out of range")
+            dev = tuple(torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+                        for a in (fe, ec.view(np.int32), et, np.ascontiguousarray(term, dtype=np.uint8)))
+            self._bw_auto = (key, dev)
+        with torch.cuda.stream(self.s_bw):
+            d_bytes = torch.from_numpy(np.ascontiguousarray(data, dtype=np.uint8)).to(self.device, non_blocking=False)
+            d_off = torch.from_numpy(np.ascontiguousarray(off, dtype=np.int64)).to(self.device)
+            d_root = torch.from_numpy(np.ascontiguousarray(roots, dtype=np.int32)).to(self.device)
+            d_cjk = torch.from_numpy(np.ascontiguousarray(cjk, dtype=np.uint8)).to(self.device)
+            out = torch.zeros(n, dtype=torch.int8, device=self.device)
+            self.k.badwords_match(d_bytes, d_off, n, d_root, d_cjk, self._bw_auto[1], self._bw_fold, out)
+            res = out.cpu().numpy()
+        return res
 
     def _to_dev(self, b: bytes):
         t = self.torch.frombuffer(bytearray(b), dtype=self.torch.uint8)

@@ -327,9 +327,45 @@ class Engine:
                 rec[alive] = self.tokenizers[i].count(texts)
             bs.apply_records(st, i, rec, -1)
         elif t == "C4BadWordsFilter":
-            bs.apply_badwords(st, i, self.badwords)
+            if self.backend == "cuda":
+                self._badwords_device(bs, st, i, ndocs)
+            else:
+                bs.apply_badwords(st, i, self.badwords)
         else:
             raise Unexpected(f"{t} is not a host step")
+
+    def _badwords_automaton(self, needed) -> Tuple:
+        """Flattened tries of every loaded bad-words list (re-flattened when a batch needs a
+        language whose list was loaded since)."""
+        a = getattr(self, "_bw_flat", None)
+        if a is None or any(l not in a[4] and l not in self._bw_nolist for l in needed):
+            for l in needed:
+                if not self.badwords.lookup(l)[1]:
+                    self._bw_nolist.add(l)
+            fe, ec, et, term, roots, cjk = self.badwords.flatten()
+            self._bw_gen = getattr(self, "_bw_gen", 0) + 1
+            a = self._bw_flat = (fe, ec, et, term, roots, cjk, self._bw_gen)
+        return a
+
+    def _badwords_device(self, bs, st, i: int, ndocs: int) -> None:
+        """C4BadWordsFilter with the matching on the GPU: languages and keep-fraction draws
+        stay on the host (document order), the regex-equivalent search runs in k_badwords_match."""
+        if not hasattr(self, "_bw_nolist"):
+            self._bw_nolist = set()
+        langs = bs.badwords_languages(st, self.badwords)  # loads lists as needed
+        alive = bs.alive_indices()
+        matched = np.full(ndocs, -1, dtype=np.int8)
+        if len(alive):
+            alangs = [langs[j] for j in alive.tolist()]
+            fe, ec, et, term, roots, cjk, gen = self._badwords_automaton(set(alangs))
+            r = np.fromiter((roots.get(l, -1) for l in alangs), dtype=np.int32, count=len(alangs))
+            c = np.fromiter((cjk.get(l, False) for l in alangs), dtype=np.uint8, count=len(alangs))
+            sel = r >= 0
+            if sel.any():
+                idx = alive[sel]
+                d, o = bs.gather(idx)
+                matched[idx] = self.device_runner.badwords_match(gen, (fe, ec, et, term), d, o, r[sel], c[sel])
+        bs.apply_badwords_matched(st, i, self.badwords, matched, langs)
 
     def _process_subset_cpu(self, data, off, meta, rows: np.ndarray) -> BatchResult:
         lens = off[rows + 1] - off[rows]

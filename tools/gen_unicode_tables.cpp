@@ -118,7 +118,9 @@ int main() {
 
   std::vector<uint32_t> props(N);
   std::vector<int32_t> lower(N);
+  std::vector<int32_t> fold(N);  // simple case folding (u_foldCase, default): C4 bad-words matching
   for (uint32_t c = 0; c < N; ++c) {
+    fold[c] = (int32_t)u_foldCase((UChar32)c, U_FOLD_CASE_DEFAULT) - (int32_t)c;
     uint32_t p = 0;
     p |= (uint32_t)map_wb(u_getIntPropertyValue(c, UCHAR_WORD_BREAK)) << P_WB_SHIFT;
     p |= (uint32_t)map_sb(u_getIntPropertyValue(c, UCHAR_SENTENCE_BREAK)) << P_SB_SHIFT;
@@ -180,5 +182,7 @@ int main() {
   emit_two_stage("TB_UCD_PROPS", props, "uint32_t");
   std::vector<uint32_t> lv(lower.begin(), lower.end());
   emit_two_stage("TB_UCD_LOWER", lv, "int32_t");
+  std::vector<uint32_t> fv(fold.begin(), fold.end());
+  emit_two_stage("TB_UCD_FOLD", fv, "int32_t");
   return 0;
 }

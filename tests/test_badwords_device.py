@@ -41,7 +41,7 @@ def corpus(n, seed):
 
 def cfg_yaml(d, default_language, keep_fraction=0.0, with_c4=False):
     c4 = ("  - {type: C4QualityFilter, split_paragraph: true, remove_citations: true, filter_no_terminal_punct: "
-          "false, min_num_sentences: 0, min_words_per_line: 0, max_word_length: 1000, filter_lorem_ipsum: true, "
+          "false, min_num_sentences: 1, min_words_per_line: 1, max_word_length: 1000, filter_lorem_ipsum: true, "
           "filter_javascript: true, filter_curly_bracket: true, filter_policy: true}\n") if with_c4 else ""
     return (f"pipeline:\n{c4}  - {{type: C4BadWordsFilter, keep_fraction: {keep_fraction}, fail_on_missing_language: "
             f"false, default_language: {default_language}, seed: 7}}\n")

@@ -148,7 +148,16 @@ def test_device_badwords_equals_cpu(tmp_path, keep_fraction):
         b = Engine(cfg, backend="cpu", segmentation="icu", **kw).process(data, off, (md, mo, mv))
         np.testing.assert_array_equal(a.status, b.status)
         assert a.reasons == b.reasons
-        for pa_, pb_ in zip(a.kept + a.excluded, b.kept + b.excluded):
-            np.testing.assert_array_equal(pa_.rows, pb_.rows)
-            assert bytes(pa_.meta_data) == bytes(pb_.meta_data)
-            assert bytes(pa_.text_data) == bytes(pb_.text_data)
+        assert rows_out(a) == rows_out(b)
+
+
+def rows_out(res):
+    """row -> (kept?, text, metadata); a batch result may hold several parts (delegated rows)."""
+    out = {}
+    for kind, parts in (("kept", res.kept), ("excluded", res.excluded)):
+        for p in parts:
+            for k, r in enumerate(p.rows):
+                t = bytes(p.text_data[p.text_off[k]:p.text_off[k + 1]])
+                m = bytes(p.meta_data[p.meta_off[k]:p.meta_off[k + 1]]) if p.meta_valid[k] else None
+                out[int(r)] = (kind, t, m)
+    return out

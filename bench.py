@@ -118,7 +118,8 @@ def main():
             "data": f"synthetic CommonCrawl-shaped docs (log-normal ~{args.mean_bytes} B, 5 languages), "
                     f"{args.docs_per_step} docs/GPU/step",
             "config": {
-                "model": "LanguageDetection(fastText bf16 MFMA head)+GopherRepetition+GopherQuality+C4Quality+FineWeb",
+                "model": "+".join(s.type.replace("LanguageDetectionFilter", "LanguageDetection(fastText bf16 MFMA head)")
+                                  .replace("Filter", "") for s in cfg.pipeline),
                 "global_batch": args.docs_per_step * world,
                 "seq_len": int(bytes_per_step / args.docs_per_step),
                 "parallelism": f"dp{world}",

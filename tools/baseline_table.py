@@ -1,0 +1,53 @@
+"""Markdown table of the BASELINE configurations from tools/baseline_table.sh output.
+
+    python tools/baseline_table.py gpurun_out/baseline > profiles/r1_baseline_table.md
+"""
+import json
+import os
+import sys
+
+
+def last_json(path):
+    try:
+        lines = [l for l in open(path) if l.startswith("{")]
+    except OSError:
+        return None
+    return [json.loads(l) for l in lines] if lines else None
+
+
+def main(d):
+    g = lambda n: last_json(os.path.join(d, n + ".json"))  # noqa: E731
+    rows = []
+
+    def fmt(v):
+        return f"{v:,.0f}" if v is not None else "—"
+
+    c1f = {r["backend"]: r for r in (g("c1_file") or [])}
+    c1c, c1g = g("c1_cpu"), g("c1_gpu")
+    rows.append(("1. C4QualityFilter only", "1k-row Parquet, CLI path (incl. startup)",
+                 c1f.get("cpu", {}).get("docs_per_sec"), c1f.get("cuda", {}).get("docs_per_sec")))
+    rows.append(("1. C4QualityFilter only", "65,536 ~1.1 KB docs/step, in memory",
+                 c1c and c1c[-1]["value"], c1g and c1g[-1]["value"]))
+    c2c, c2g = g("c2_cpu"), g("c2_gpu")
+    rows.append(("2. C4 + GopherQuality + GopherRepetition", "10M ~1.1 KB docs (153 steps x 65,536)",
+                 c2c and c2c[-1]["value"], c2g and c2g[-1]["value"]))
+    c3c, c3g = g("c3_cpu"), g("c3_gpu")
+    rows.append(("3. + LanguageDetection (bf16 MFMA head) + FineWeb", "65,536 ~1.1 KB docs/step (bench.py)",
+                 c3c and c3c[-1]["value"], c3g and c3g[-1]["value"]))
+    c4 = g("c4_file")
+    rows.append(("4. CommonCrawl-shaped Parquet, CLI path (1-GPU point)", "4M docs: read+decode+filter+write",
+                 None, c4 and c4[-1]["docs_per_sec"]))
+    c5c, c5g = g("c5_cpu"), g("c5_gpu")
+    rows.append(("5. GopherRepetition 2..10-gram", "~50 KB docs, 4,096 docs/step",
+                 c5c and c5c[-1]["value"], c5g and c5g[-1]["value"]))
+    print("| Config | Workload | CPU path (16 threads) docs/s | 1x MI355X docs/s | speed-up |")
+    print("|---|---|---|---|---|")
+    for name, wl, c, gv in rows:
+        sp = f"{gv / c:.1f}x" if c and gv else "—"
+        print(f"| {name} | {wl} | {fmt(c)} | {fmt(gv)} | {sp} |")
+    if c5g:
+        print(f"\nConfig 5 on the GPU: {c5g[-1]['bytes_per_sec'] / 1e9:.2f} GB/s of text.")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/baseline")

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../common/docproc.h"
+#include "../common/gate.h"
 
 using namespace tb;
 
@@ -60,9 +61,9 @@ __device__ __forceinline__ DocCtx<P> make_ctx(const DevTables& t, const uint64_t
       const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,        \
       const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, \
       int64_t* rec, uint32_t* flags, const uint16_t* __restrict__ lid_emb, uint16_t* lid_vec, int32_t* lid_cnt, \
-      uint32_t lds_bytes, uint64_t* prof) {                                                          \
+      uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead) {                         \
     const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;                                        \
-    if (doc >= ndocs) return;                                                                         \
+    if (doc >= ndocs || (dead && dead[doc])) return;                                                  \
     DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);   \
     const uint8_t* b = bytes + off[doc];                                                              \
     const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);                                           \
@@ -84,9 +85,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_stage_analyze_blk(
     const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes,
     const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,
     const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
-    int64_t* rec, uint32_t* flags, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes, uint64_t* prof) {
+    int64_t* rec, uint32_t* flags, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes, uint64_t* prof,
+    const uint8_t* __restrict__ dead) {
   const int doc = perm[blockIdx.x];
-  if (doc >= ndocs) return;
+  if (doc >= ndocs || (dead && dead[doc])) return;
   DocCtx<BlockPar<kBlockThreads>> x =
       make_ctx<BlockPar<kBlockThreads>>(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);
   x.par.xs = g_block_xs;
@@ -118,9 +120,9 @@ __global__ __launch_bounds__(64) void k_c4_pass_a(
     const DevC4* __restrict__ c4, const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
     const int32_t* __restrict__ perm, int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off,
     const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec, int64_t* src, uint32_t* flags,
-    uint32_t lds_bytes, uint64_t* prof) {
+    uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead) {
   const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
-  if (doc >= ndocs) return;
+  if (doc >= ndocs || (dead && dead[doc])) return;  // skipped: record zeros, rewritten length 0
   DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
@@ -131,9 +133,9 @@ __global__ __launch_bounds__(kBlockThreads) void k_c4_pass_a_blk(
     const DevC4* __restrict__ c4, const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
     const int32_t* __restrict__ perm, int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off,
     const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec, int64_t* src, uint32_t* flags,
-    uint32_t lds_bytes, uint64_t* prof) {
+    uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead) {
   const int doc = perm[blockIdx.x];
-  if (doc >= ndocs) return;
+  if (doc >= ndocs || (dead && dead[doc])) return;
   DocCtx<BlockPar<kBlockThreads>> x =
       make_ctx<BlockPar<kBlockThreads>>(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);
   x.par.xs = g_block_xs;
@@ -287,6 +289,24 @@ __global__ __launch_bounds__(64) void k_langid_head(const uint16_t* __restrict__
   }
 }
 
+// Step gate (csrc/common/gate.h): one thread per document. A live document that a step of the
+// just-finished pass filters (or that a kernel flagged for the CPU path) gets `code`: later
+// passes skip it. Codes are written once, so dead[doc] = the first pass the document skipped.
+__global__ __launch_bounds__(256) void k_gate(const DevGate* __restrict__ gate, GateRecs recs, int32_t ndocs,
+                                              const uint32_t* __restrict__ flags, uint8_t* dead, uint8_t code) {
+  const int doc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (doc >= ndocs || dead[doc]) return;
+  bool fail = flags[doc] != 0;
+  const int ns = gate->n_steps;
+  for (int s = 0; s < ns && !fail; ++s) {
+    const DevGateStep& g = gate->steps[s];
+    if (g.kind == GK_NONE) continue;
+    const int64_t* r = recs.p[g.slot] + (int64_t)g.prefix * ndocs + (int64_t)doc * g.width;
+    fail = gate_fails(g, r);
+  }
+  if (fail) dead[doc] = code;
+}
+
 __global__ void k_pow_table(uint64_t* pw, uint32_t n) {
   // pw[i] = B^i, computed independently per element (exact modular arithmetic)
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -302,7 +322,7 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
                      const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                      const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
                      const uint16_t* lid_emb, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes,
-                     uint64_t* prof, int32_t waves, int32_t nblocks) {
+                     uint64_t* prof, int32_t waves, int32_t nblocks, const uint8_t* dead) {
   if (ndocs <= 0) return 0;
   if (nblocks <= 0) nblocks = ndocs;  // grid: docs perm[0 .. nblocks)
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
@@ -313,7 +333,7 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64), lds_bytes, stream, (const DevPlan*)plan,
                      (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, flags,
-                     lid_emb, lid_vec, lid_cnt, lds_bytes, prof);
+                     lid_emb, lid_vec, lid_cnt, lds_bytes, prof, dead);
   return (int)hipGetLastError();
 }
 
@@ -323,7 +343,8 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
                          const int64_t* off, const int32_t* perm, int32_t nblocks, int32_t ndocs, char* scratch,
                          const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                          const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
-                         uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes, uint64_t* prof) {
+                         uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes, uint64_t* prof,
+                         const uint8_t* dead) {
   if (nblocks <= 0) return 0;
   if (!perm || lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
@@ -332,7 +353,7 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
                               (int)lds_bytes);
   hipLaunchKernelGGL(k_stage_analyze_blk, dim3(nblocks), dim3(kBlockThreads), lds_bytes, stream,
                      (const DevPlan*)plan, (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw,
-                     pw_n, t, rec, flags, lid_vec, lid_cnt, lds_bytes, prof);
+                     pw_n, t, rec, flags, lid_vec, lid_cnt, lds_bytes, prof, dead);
   return (int)hipGetLastError();
 }
 
@@ -340,7 +361,7 @@ int tb_c4_pass_a_blk(hipStream_t stream, const void* c4, const uint8_t* bytes, c
                      const int32_t* perm, int32_t nblocks, int32_t ndocs, char* scratch, const int64_t* scratch_off,
                      const uint64_t* pw, uint32_t pw_n, const uint16_t* s1, const uint32_t* s2, const uint16_t* l1,
                      const int32_t* l2, int64_t* rec, int64_t* src, uint32_t* flags, uint32_t lds_bytes,
-                     uint64_t* prof) {
+                     uint64_t* prof, const uint8_t* dead) {
   if (nblocks <= 0) return 0;
   if (!perm || lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
@@ -348,7 +369,7 @@ int tb_c4_pass_a_blk(hipStream_t stream, const void* c4, const uint8_t* bytes, c
     (void)hipFuncSetAttribute((const void*)k_c4_pass_a_blk, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds_bytes);
   hipLaunchKernelGGL(k_c4_pass_a_blk, dim3(nblocks), dim3(kBlockThreads), lds_bytes, stream, (const DevC4*)c4,
-                     bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof);
+                     bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof, dead);
   return (int)hipGetLastError();
 }
 
@@ -384,7 +405,8 @@ int tb_langid_features(hipStream_t stream, const uint8_t* bytes, const int64_t* 
 int tb_c4_pass_a(hipStream_t stream, const void* c4, const uint8_t* bytes, const int64_t* off, const int32_t* perm,
                  int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n,
                  const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
-                 int64_t* src, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, int32_t nblocks) {
+                 int64_t* src, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, int32_t nblocks,
+                 const uint8_t* dead) {
   if (ndocs <= 0) return 0;
   if (nblocks <= 0) nblocks = ndocs;
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
@@ -392,7 +414,7 @@ int tb_c4_pass_a(hipStream_t stream, const void* c4, const uint8_t* bytes, const
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k_c4_pass_a, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(k_c4_pass_a, dim3(nblocks), dim3(64), lds_bytes, stream, (const DevC4*)c4, bytes, off, perm, ndocs,
-                     scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof);
+                     scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof, dead);
   return (int)hipGetLastError();
 }
 
@@ -413,6 +435,19 @@ int tb_langid_head(hipStream_t stream, const uint16_t* vec, const int32_t* cnt, 
   return (int)hipGetLastError();
 }
 
+int tb_gate(hipStream_t stream, const void* gate, const int64_t* const* recs, int32_t nrecs, int32_t ndocs,
+            const uint32_t* flags, uint8_t* dead, int32_t code) {
+  if (ndocs <= 0) return 0;
+  if (nrecs < 0 || nrecs > kMaxGateSteps || code <= 0 || code > 255) return (int)hipErrorInvalidValue;
+  GateRecs r{};
+  for (int i = 0; i < nrecs; ++i) r.p[i] = recs[i];
+  hipLaunchKernelGGL(k_gate, dim3((ndocs + 255) / 256), dim3(256), 0, stream, (const DevGate*)gate, r, ndocs, flags,
+                     dead, (uint8_t)code);
+  return (int)hipGetLastError();
+}
+
+size_t tb_sizeof_gate() { return sizeof(DevGate); }
+
 int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
   hipLaunchKernelGGL(k_pow_table, dim3((n + 256) / 256), dim3(256), 0, stream, pw, n);
   return (int)hipGetLastError();
@@ -420,7 +455,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 
 int tb_phase_slots() { return kPhaseSlots; }
 
-int tb_abi_version() { return 2; }
+int tb_abi_version() { return 3; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

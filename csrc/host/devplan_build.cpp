@@ -3,6 +3,7 @@
 #include "devplan_build.h"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -115,6 +116,100 @@ DevC4 build_c4(const StepCfg& c) {
   return d;
 }
 
+DevGateStep build_gate_step(const StepCfg& c, int slot, int prefix) {
+  DevGateStep g;
+  std::memset(&g, 0, sizeof(g));
+  g.slot = slot;
+  g.prefix = prefix;
+  g.width = record_width(c);
+  auto opt_d = [&](const std::optional<double>& v, int bit, int k) {
+    if (v) { g.has |= 1u << bit; g.d[k] = *v; }
+  };
+  auto opt_i = [&](const std::optional<int64_t>& v, int bit, int k) {
+    if (v) { g.has |= 1u << bit; g.i[k] = *v; }
+  };
+  switch (c.kind) {
+    case StepKind::GopherQuality:
+      g.kind = GK_GOPHER_QUALITY;
+      opt_i(c.min_doc_words, GQ_T_MIN_WORDS, 0);
+      opt_i(c.max_doc_words, GQ_T_MAX_WORDS, 1);
+      opt_d(c.min_avg_word_length, GQ_T_MIN_AVG, 0);
+      opt_d(c.max_avg_word_length, GQ_T_MAX_AVG, 1);
+      opt_d(c.max_symbol_word_ratio, GQ_T_SYMBOL, 2);
+      opt_d(c.max_bullet_lines_ratio, GQ_T_BULLET, 3);
+      opt_d(c.max_ellipsis_lines_ratio, GQ_T_ELL_LINES, 4);
+      opt_d(c.max_non_alpha_words_ratio, GQ_T_ALPHA, 5);
+      opt_i(c.min_stop_words, GQ_T_MIN_STOP, 2);
+      break;
+    case StepKind::GopherRepetition:
+      if (c.top_n_grams.size() > (size_t)kMaxGateNgrams || c.dup_n_grams.size() > (size_t)kMaxGateNgrams)
+        return DevGateStep{};  // GK_NONE: never gates
+      g.kind = GK_GOPHER_REP;
+      opt_d(c.dup_para_frac, GR_T_PARA, 0);
+      opt_d(c.dup_para_char_frac, GR_T_PARA_CHAR, 1);
+      opt_d(c.dup_line_frac, GR_T_LINE, 2);
+      opt_d(c.dup_line_char_frac, GR_T_LINE_CHAR, 3);
+      g.n_top = (int32_t)c.top_n_grams.size();
+      g.n_dup = (int32_t)c.dup_n_grams.size();
+      for (int k = 0; k < g.n_top; ++k) { g.top_n[k] = c.top_n_grams[k].first; g.top_thr[k] = c.top_n_grams[k].second; }
+      for (int k = 0; k < g.n_dup; ++k) { g.dup_n[k] = c.dup_n_grams[k].first; g.dup_thr[k] = c.dup_n_grams[k].second; }
+      break;
+    case StepKind::FineWebQuality:
+      g.kind = GK_FINEWEB;
+      g.d[0] = c.line_punct_thr;
+      g.d[1] = c.short_line_thr;
+      g.d[2] = c.char_duplicates_ratio;
+      g.d[3] = c.new_line_ratio;
+      g.flag = c.line_punct_exclude_zero ? 1 : 0;
+      break;
+    case StepKind::LanguageDetection:
+      g.kind = GK_LANGID;
+      for (int l : c.allowed_langs)
+        if (l >= 0 && l < 32) g.has |= 1u << l;
+      g.d[0] = c.min_confidence;
+      break;
+    case StepKind::C4Quality:
+      g.kind = GK_C4;
+      g.i[0] = c.min_num_sentences;
+      break;
+    default:
+      g.kind = GK_NONE;  // host-only steps are never evaluated on the device
+      break;
+  }
+  return g;
+}
+
+DevGate build_gate(const std::vector<StepCfg>& steps, const std::vector<std::array<int, 3>>& entries) {
+  DevGate gate;
+  std::memset(&gate, 0, sizeof(gate));
+  if (entries.size() > (size_t)kMaxGateSteps) throw std::runtime_error("too many steps in one device gate");
+  for (size_t k = 0; k < entries.size(); ++k) {
+    const auto& e = entries[k];
+    if (e[0] < 0 || e[0] >= (int)steps.size() || e[1] < 0 || e[1] >= kMaxGateSteps)
+      throw std::runtime_error("device gate entry out of range");
+    gate.steps[k] = build_gate_step(steps[e[0]], e[1], e[2]);
+  }
+  gate.n_steps = (int32_t)entries.size();
+  return gate;
+}
+
+void gate_host(const DevGate& g, const std::vector<const int64_t*>& recs, int64_t ndocs, const uint32_t* flags,
+               uint8_t* dead, uint8_t code) {
+  for (int s = 0; s < g.n_steps; ++s)
+    if (g.steps[s].kind != GK_NONE && (g.steps[s].slot < 0 || g.steps[s].slot >= (int)recs.size()))
+      throw std::runtime_error("gate record slot out of range");
+  for (int64_t doc = 0; doc < ndocs; ++doc) {  // same loop body as k_gate
+    if (dead[doc]) continue;
+    bool fail = flags && flags[doc] != 0;
+    for (int s = 0; s < g.n_steps && !fail; ++s) {
+      const DevGateStep& st = g.steps[s];
+      if (st.kind == GK_NONE) continue;
+      fail = gate_fails(st, recs[st.slot] + (int64_t)st.prefix * ndocs + doc * st.width);
+    }
+    if (fail) dead[doc] = code;
+  }
+}
+
 std::vector<uint64_t> pow_table(uint32_t n) {
   std::vector<uint64_t> pw(n + 1);
   pw[0] = 1;
@@ -144,7 +239,7 @@ static void lid_head_host(const LangidModel& m, const uint16_t* v, int32_t cnt, 
 
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
-                   std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes) {
+                   std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes, const uint8_t* dead) {
   DevPlan* plan = new DevPlan();
   std::memset(plan, 0, sizeof(DevPlan));
   DevStage st = build_stage(steps, idx, *plan);
@@ -163,6 +258,7 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
     std::vector<char> scratch;
     std::vector<char> lds(lds_bytes + 16);  // stands in for the wave's LDS slice
     for (int64_t i = a; i < b; ++i) {
+      if (dead && dead[i]) continue;  // skipped by the device gate: record stays zero
       const uint32_t n = (uint32_t)(off[i + 1] - off[i]);
       const uint64_t need = scratch_bytes_for(n);
       if (scratch.size() < need) scratch.resize(need);
@@ -190,7 +286,7 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
 
 void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
                 std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,
-                std::vector<uint32_t>& flags, uint32_t lds_bytes) {
+                std::vector<uint32_t>& flags, uint32_t lds_bytes, const uint8_t* dead) {
   DevC4 c4 = build_c4(step);
   rec.assign((size_t)rec::C4_WIDTH * ndocs, 0);
   flags.assign(ndocs, 0);
@@ -203,6 +299,7 @@ void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int6
     std::vector<char> scratch;
     std::vector<char> lds(lds_bytes + 16);  // stands in for the wave's LDS slice
     for (int64_t i = a; i < b; ++i) {
+      if (dead && dead[i]) continue;  // skipped: record zeros, empty rewrite
       const uint32_t n = (uint32_t)(off[i + 1] - off[i]);
       const uint64_t need = scratch_bytes_for(n);
       if (scratch.size() < need) scratch.resize(need);

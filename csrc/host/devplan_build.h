@@ -1,8 +1,10 @@
 #pragma once
+#include <array>
 #include <string>
 #include <vector>
 
 #include "../common/devplan.h"
+#include "../common/gate.h"
 #include "filters.h"
 #include "pipeline.h"
 
@@ -16,13 +18,20 @@ int dev_kind_of(const StepCfg& c);
 bool device_supported(const StepCfg& c, std::string* why);
 DevStage build_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, DevPlan& plan);
 DevC4 build_c4(const StepCfg& c);
+// Gate (csrc/common/gate.h) over steps: entries = (step index, record slot, record prefix).
+DevGateStep build_gate_step(const StepCfg& c, int slot, int prefix);
+DevGate build_gate(const std::vector<StepCfg>& steps, const std::vector<std::array<int, 3>>& entries);
 std::vector<uint64_t> pow_table(uint32_t n);
 
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
-                   std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes = 0);
+                   std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes = 0,
+                   const uint8_t* dead = nullptr);
 void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
                 std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,
-                std::vector<uint32_t>& flags, uint32_t lds_bytes = 0);
+                std::vector<uint32_t>& flags, uint32_t lds_bytes = 0, const uint8_t* dead = nullptr);
+// Host run of k_gate (same loop body): dead[doc] = code for live docs that a gated step filters.
+void gate_host(const DevGate& g, const std::vector<const int64_t*>& recs, int64_t ndocs, const uint32_t* flags,
+               uint8_t* dead, uint8_t code);
 
 }  // namespace tb

@@ -5,6 +5,7 @@
 #include <pybind11/stl.h>
 
 #include <cstring>
+#include <optional>
 
 #include "../common/langid.h"
 #include "../common/ucd_tables.inc"
@@ -488,6 +489,22 @@ PYBIND11_MODULE(_tbhost, m) {
     DevC4 d = build_c4(c);
     return py::bytes((const char*)&d, sizeof(d));
   });
+  m.def("build_gate", [](const std::vector<StepCfg>& steps, const std::vector<std::array<int, 3>>& entries) {
+    DevGate g = build_gate(steps, entries);
+    return py::bytes((const char*)&g, sizeof(g));
+  });
+  // Device gate decision on one record (host evaluation of the same TB_HD code; tests compare it
+  // with decide_status over the step's whole decision space).
+  m.def("gate_fails", [](const StepCfg& c, const std::vector<int64_t>& r) {
+    if ((int)r.size() < record_width(c)) throw std::runtime_error("record too short");
+    DevGateStep g = build_gate_step(c, 0, 0);
+    return gate_fails(g, r.data());
+  });
+  m.def("decide_status", [](const StepCfg& c, const std::vector<int64_t>& r) {
+    if ((int)r.size() < record_width(c)) throw std::runtime_error("record too short");
+    return (int)decide_status(c, r.data());
+  });
+  m.attr("SIZEOF_DEV_GATE") = sizeof(DevGate);
   m.def("stage_layout", [](const py::bytes& b) {
     std::string s = b;
     DevStage d;
@@ -507,28 +524,56 @@ PYBIND11_MODULE(_tbhost, m) {
   m.attr("OFFSETOF_STEPS") = offsetof(DevStage, steps);
   m.def("emulate_stage", [](const std::vector<StepCfg>& steps, const std::vector<int>& idx,
                             py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
-                            int nthreads, std::shared_ptr<LangidModel> lid, uint32_t lds_bytes) {
+                            int nthreads, std::shared_ptr<LangidModel> lid, uint32_t lds_bytes,
+                            std::optional<py::array_t<uint8_t, py::array::c_style>> dead) {
     std::vector<int64_t> rec;
     std::vector<uint32_t> flags;
     const int64_t nd = (int64_t)off.size() - 1;
+    if (dead && (int64_t)dead->size() < nd) throw std::runtime_error("dead mask too short");
+    const uint8_t* dp = dead ? dead->data() : nullptr;
     {
       py::gil_scoped_release nogil;
-      emulate_stage(steps, idx, nd, (const char*)data.data(), off.data(), nthreads, lid.get(), rec, flags, lds_bytes);
+      emulate_stage(steps, idx, nd, (const char*)data.data(), off.data(), nthreads, lid.get(), rec, flags, lds_bytes,
+                    dp);
     }
     return py::make_tuple(to_numpy(std::move(rec)), to_numpy(std::move(flags)));
   }, py::arg("steps"), py::arg("idx"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8,
-     py::arg("lid") = nullptr, py::arg("lds_bytes") = 0);
+     py::arg("lid") = nullptr, py::arg("lds_bytes") = 0, py::arg("dead") = py::none());
+  m.def("gate_host", [](const py::bytes& gate, const std::vector<py::array_t<int64_t, py::array::c_style>>& recs,
+                        int64_t ndocs, py::array_t<uint32_t, py::array::c_style> flags,
+                        py::array_t<uint8_t, py::array::c_style> dead, int code) {
+    std::string gs = gate;
+    if (gs.size() != sizeof(DevGate)) throw std::runtime_error("bad gate blob");
+    if (code <= 0 || code > 255) throw std::runtime_error("gate code out of range");
+    if ((int64_t)dead.size() < ndocs || (int64_t)flags.size() < ndocs) throw std::runtime_error("gate: operand shapes");
+    DevGate g;
+    std::memcpy(&g, gs.data(), sizeof(g));
+    std::vector<const int64_t*> rp;
+    for (int s = 0; s < g.n_steps; ++s) {
+      const DevGateStep& st = g.steps[s];
+      if (st.kind == GK_NONE) continue;
+      if (st.slot < 0 || st.slot >= (int)recs.size()) throw std::runtime_error("gate slot out of range");
+      if ((int64_t)recs[st.slot].size() < ((int64_t)st.prefix + st.width) * ndocs)
+        throw std::runtime_error("gate record buffer too short");
+    }
+    for (auto& r : recs) rp.push_back(r.data());
+    gate_host(g, rp, ndocs, flags.data(), dead.mutable_data(), (uint8_t)code);
+  });
   m.def("emulate_c4", [](const StepCfg& step, py::array_t<uint8_t, py::array::c_style> data,
-                         py::array_t<int64_t, py::array::c_style> off, int nthreads, uint32_t lds_bytes) {
+                         py::array_t<int64_t, py::array::c_style> off, int nthreads, uint32_t lds_bytes,
+                         std::optional<py::array_t<uint8_t, py::array::c_style>> dead) {
     std::vector<int64_t> rec, no;
     std::vector<uint32_t> flags;
     std::string nd;
     const int64_t n = (int64_t)off.size() - 1;
+    if (dead && (int64_t)dead->size() < n) throw std::runtime_error("dead mask too short");
+    const uint8_t* dp = dead ? dead->data() : nullptr;
     {
       py::gil_scoped_release nogil;
-      emulate_c4(step, n, (const char*)data.data(), off.data(), nthreads, rec, nd, no, flags, lds_bytes);
+      emulate_c4(step, n, (const char*)data.data(), off.data(), nthreads, rec, nd, no, flags, lds_bytes, dp);
     }
     return py::make_tuple(to_numpy(std::move(rec)), str_to_numpy(std::move(nd)), to_numpy(std::move(no)),
                           to_numpy(std::move(flags)));
-  }, py::arg("step"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8, py::arg("lds_bytes") = 0);
+  }, py::arg("step"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8, py::arg("lds_bytes") = 0,
+     py::arg("dead") = py::none());
 }

@@ -50,6 +50,11 @@ def test_device_records_match_host_emulation(host, corpus, runner_parts):
     data, off = synth.pack(corpus)
     res = runner.run(data, off)
     n = len(corpus)
+    # documents a gate skipped in a pass (csrc/common/gate.h) have zero records there
+    def live(step_i):
+        p = runner.pass_of_step[step_i]
+        return ~((res.dead != 0) & (res.dead <= p)) if res.dead is not None else np.ones(n, bool)
+
     for s, idx in enumerate(plan.stages):
         ver = plan.stage_version[s]
         vd, vo = (data, off) if ver == 0 else res.versions[ver]
@@ -60,7 +65,7 @@ def test_device_records_match_host_emulation(host, corpus, runner_parts):
         for (kind, width, prefix), step_i in sorted(zip(layout, idx), key=lambda t: t[0][0] == 4):
             a = got[prefix * n:(prefix + width) * n].reshape(n, width)
             b = ref[prefix * n:(prefix + width) * n].reshape(n, width)
-            ok = (res.flags == 0) & (rflags == 0)
+            ok = (res.flags == 0) & (rflags == 0) & live(step_i)
             if kind == 4:
                 # language id: the doc vectors are bit-exact (fixed-point bag); the head sums 32
                 # bf16 products in MFMA order vs. sequential fp32 on the host, so only exact
@@ -80,11 +85,27 @@ def test_device_records_match_host_emulation(host, corpus, runner_parts):
         ver = plan.steps[i].version_in
         vd, vo = (data, off) if ver == 0 else res.versions[ver]
         rrec, rdata, roff, rflags = host.emulate_c4(steps[i], np.ascontiguousarray(vd), np.ascontiguousarray(vo), 8)
-        ok = (res.flags == 0) & (rflags == 0)
+        ok = (res.flags == 0) & (rflags == 0) & live(i)
         assert np.array_equal(res.c4_recs[i].reshape(n, 7)[ok], rrec.reshape(n, 7)[ok])
         gd, go = res.versions[plan.steps[i].version_out]
         for d in np.nonzero(ok)[0]:
             assert bytes(gd[go[d]:go[d + 1]]) == bytes(rdata[roff[d]:roff[d + 1]])
+
+
+def test_device_gate_matches_host_gate(host, corpus, runner_parts):
+    """The gate kernel marks the same documents dead as the host run of the same code over the
+    emulated records (language-id near-ties aside), and it does skip work."""
+    from textblaster_amd.pipeline.device import EmulatedRunner
+
+    cfg, steps, plan, runner, lid = runner_parts
+    data, off = synth.pack(corpus)
+    res = runner.run(data, off)
+    emu = EmulatedRunner(steps, plan, lid, 8).run(data, off)
+    assert res.dead is not None and emu.dead is not None
+    assert np.count_nonzero(res.dead) > len(corpus) // 10
+    ok = (res.flags == 0) & (emu.flags == 0)
+    diff = np.nonzero(ok & (res.dead != emu.dead))[0]
+    assert len(diff) <= max(2, len(corpus) // 500), diff[:10]
 
 
 def test_dictionary_scripts_are_flagged(host, runner_parts):

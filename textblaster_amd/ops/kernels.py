@@ -17,11 +17,14 @@ _U32 = ctypes.c_uint32
 _I64 = ctypes.c_int64
 
 _SIGS = {
-    "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32],
-    "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32],
+    "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32,
+                         _P],
+    "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _P],
     "tb_stage_analyze_blk": [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P,
-                             _U32, _P],
-    "tb_c4_pass_a_blk": [_P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
+                             _U32, _P, _P],
+    "tb_c4_pass_a_blk": [_P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _P],
+    "tb_gate": [_P, _P, _P, _I32, _I32, _P, _P, _I32],
+    "tb_sizeof_gate": [],
     "tb_block_threads": [],
     "tb_badwords_match": [_P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
@@ -66,7 +69,8 @@ class Kernels:
         self.device = device
         self.lib = native.hip()
         h = native.host()
-        if self.lib.tb_sizeof_plan() != h.SIZEOF_DEV_PLAN or self.lib.tb_sizeof_stage() != h.SIZEOF_DEV_STAGE:
+        if (self.lib.tb_sizeof_plan() != h.SIZEOF_DEV_PLAN or self.lib.tb_sizeof_stage() != h.SIZEOF_DEV_STAGE
+                or self.lib.tb_sizeof_gate() != h.SIZEOF_DEV_GATE):
             raise DeviceError("libtbhip.so and _tbhost disagree on the device plan layout; rebuild")
         s1, s2, l1, l2 = h.ucd_tables()
         self.tabs = [torch.from_numpy(a).to(device) for a in (s1, s2, l1, l2)]
@@ -86,32 +90,33 @@ class Kernels:
         return self._pw, self._pw_n
 
     def stage_analyze(self, plan, stage, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, flags,
-                      lid_emb=None, lid_vec=None, lid_cnt=None, lds_bytes=0, prof=None, waves=0, nblocks=0):
+                      lid_emb=None, lid_vec=None, lid_cnt=None, lds_bytes=0, prof=None, waves=0, nblocks=0, dead=None):
         t = self.tabs
         rc = self.lib.tb_stage_analyze(
             self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs,
             scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
             t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), _ptr(lid_emb), _ptr(lid_vec),
-            _ptr(lid_cnt), lds_bytes, _ptr(prof), waves, nblocks)
+            _ptr(lid_cnt), lds_bytes, _ptr(prof), waves, nblocks, _ptr(dead))
         _check(rc, "tb_stage_analyze")
 
     def stage_analyze_blk(self, plan, stage, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n,
-                          rec, flags, lid_vec=None, lid_cnt=None, lds_bytes=0, prof=None):
+                          rec, flags, lid_vec=None, lid_cnt=None, lds_bytes=0, prof=None, dead=None):
         t = self.tabs
         rc = self.lib.tb_stage_analyze_blk(
             self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), perm_long.data_ptr(),
             nlong, ndocs, scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(),
             t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), _ptr(lid_vec),
-            _ptr(lid_cnt), lds_bytes, _ptr(prof))
+            _ptr(lid_cnt), lds_bytes, _ptr(prof), _ptr(dead))
         _check(rc, "tb_stage_analyze_blk")
 
     def c4_pass_a_blk(self, c4, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags,
-                      lds_bytes=0, prof=None):
+                      lds_bytes=0, prof=None, dead=None):
         t = self.tabs
         rc = self.lib.tb_c4_pass_a_blk(
             self.stream(), c4.data_ptr(), bytes_.data_ptr(), off.data_ptr(), perm_long.data_ptr(), nlong, ndocs,
             scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
-            t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), src.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof))
+            t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), src.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof),
+            _ptr(dead))
         _check(rc, "tb_c4_pass_a_blk")
 
     def badwords_match(self, bytes_, off, ndocs, root, cjk, automaton, fold, matched):
@@ -134,18 +139,30 @@ class Kernels:
         _check(rc, "tb_langid_features")
 
     def c4_pass_a(self, c4, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags, lds_bytes=0,
-                  prof=None, nblocks=0):
+                  prof=None, nblocks=0, dead=None):
         t = self.tabs
         rc = self.lib.tb_c4_pass_a(
             self.stream(), c4.data_ptr(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs, scratch.data_ptr(),
             scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
-            t[3].data_ptr(), rec.data_ptr(), src.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof), nblocks)
+            t[3].data_ptr(), rec.data_ptr(), src.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof), nblocks,
+            _ptr(dead))
         _check(rc, "tb_c4_pass_a")
 
     def c4_pass_b(self, bytes_, off, ndocs, scratch, scratch_off, src, new_off, out):
         rc = self.lib.tb_c4_pass_b(self.stream(), bytes_.data_ptr(), off.data_ptr(), ndocs, scratch.data_ptr(),
                                    scratch_off.data_ptr(), src.data_ptr(), new_off.data_ptr(), out.data_ptr())
         _check(rc, "tb_c4_pass_b")
+
+    def gate(self, gate, recs, ndocs, flags, dead, code, max_slot):
+        """k_gate: mark documents that a step of the finished pass filtered (dead[doc] = code)."""
+        if not 0 < code <= 255:
+            raise DeviceError("gate code out of range")
+        if max_slot >= len(recs) or len(recs) > 8 or dead.numel() < ndocs or flags.numel() < ndocs:
+            raise DeviceError("gate: operand shapes")
+        arr = (ctypes.c_void_p * 8)(*([r.data_ptr() for r in recs] + [None] * (8 - len(recs))))
+        rc = self.lib.tb_gate(self.stream(), gate.data_ptr(), ctypes.cast(arr, ctypes.c_void_p), len(recs), ndocs,
+                              flags.data_ptr(), dead.data_ptr(), code)
+        _check(rc, "tb_gate")
 
     def langid_head(self, vec, cnt, wT, bias, ndocs, rec, rec_off, width, dbg_logits=None):
         rc = self.lib.tb_langid_head(self.stream(), vec.data_ptr(), cnt.data_ptr(), wT.data_ptr(), bias.data_ptr(),

@@ -37,6 +37,10 @@ class DeviceResult:
     versions: Dict[int, Tuple[np.ndarray, np.ndarray]]  # v >= 1 -> (bytes, offsets)
     flags: np.ndarray                       # uint32 [ndocs]; nonzero -> recompute on the CPU path
     timings: Dict[str, float]
+    # Step gating (csrc/common/gate.h): dead[doc] = k > 0 -> passes >= k skipped the document
+    # (a step of pass k-1 or earlier filtered it on the device); pass_of_step: step -> pass index
+    dead: Optional[np.ndarray] = None
+    pass_of_step: Optional[Dict[int, int]] = None
 
 
 class _Slot:
@@ -55,7 +59,7 @@ class PendingBatch:
     """A submitted batch: kernels and D2H copies are queued on the stream; ``wait()`` blocks on
     the completion event and returns host views of the results."""
 
-    def __init__(self, runner, ndocs, event, stage_recs, c4_recs, versions, flags, t_submit, keep):
+    def __init__(self, runner, ndocs, event, stage_recs, c4_recs, versions, flags, t_submit, keep, dead=None):
         self.runner = runner
         self.ndocs = ndocs
         self.event = event
@@ -63,6 +67,7 @@ class PendingBatch:
         self._c4_recs = c4_recs
         self._versions = versions
         self._flags = flags
+        self._dead = dead
         self._t_submit = t_submit
         self._keep = keep  # device tensors that must stay alive until the event completes
 
@@ -79,12 +84,36 @@ class PendingBatch:
             o = vo.numpy()
             host_versions[ver] = (vb.numpy()[: int(o[-1])], o)
         fl = self._flags.numpy().view(np.uint32)
+        dead = self._dead.numpy() if self._dead is not None else None
         if self.runner.phase_prof:
             self.runner.collect_phase_prof(self._keep)
         self._keep = None
         timings = dict(self._t_submit)
         timings["gpu_wait"] = t1 - t0
-        return DeviceResult(stage_recs, c4_recs, host_versions, fl, timings)
+        return DeviceResult(stage_recs, c4_recs, host_versions, fl, timings, dead, self.runner.pass_of_step)
+
+
+def plan_passes(plan: ExecPlan, stage_layout, steps_native, gating: bool):
+    """Device passes in execution order (stages and C4 rewrites, by content version), the pass of
+    every device step, and per pass (except the last) the gate blob over the steps it produced
+    records for."""
+    h = native.host()
+    passes = []
+    for ver in range(plan.n_versions):
+        passes += [("stage", s) for s, sv in enumerate(plan.stage_version) if sv == ver]
+        passes += [("c4", i) for i in plan.c4_steps if plan.steps[i].version_in == ver]
+    pass_of_step: Dict[int, int] = {}
+    gates: Dict[int, bytes] = {}
+    for p, (kind, x) in enumerate(passes):
+        if kind == "stage":
+            entries = [(j, 0, prefix) for j, (_, _, prefix) in zip(plan.stages[x], stage_layout[x][1])]
+        else:
+            entries = [(x, 0, 0)]
+        for j, _, _ in entries:
+            pass_of_step[j] = p
+        if gating and p + 1 < len(passes) and p + 1 <= 255:
+            gates[p] = h.build_gate(steps_native, entries)
+    return passes, pass_of_step, gates
 
 
 class DeviceRunner:
@@ -121,6 +150,12 @@ class DeviceRunner:
             self.lid_wT = torch.from_numpy(wT).to(self.device)
             self.lid_b = torch.from_numpy(langid.b.astype(np.float32)).to(self.device)
         self.c4_growth = int(h.C4_MAX_GROWTH)
+        # TB_GATE=0 disables step gating (every pass runs over every document)
+        import os as _os
+
+        self.gating = _os.environ.get("TB_GATE", "1") not in ("", "0")
+        self.passes, self.pass_of_step, gates = plan_passes(plan, self.stage_layout, steps_native, self.gating)
+        self.gate_ts = {p: self._to_dev(b) for p, b in gates.items()}
         # LDS arena per document (one wave per workgroup); TB_LDS_BYTES overrides for tuning
         import os
 
@@ -298,6 +333,8 @@ class DeviceRunner:
         scratch = self._scratch_for(slot, int(scratch_off[-1]))
         pw, pw_n = self.k.pow_table(2 * maxlen + 64)
         flags = torch.zeros(ndocs, dtype=torch.int32, device=self.device)
+        dead = torch.zeros(ndocs, dtype=torch.uint8, device=self.device) if self.gate_ts else None
+        pass_idx = 0
         t1 = time.perf_counter()
         versions = {0: (d_bytes, d_off, len(data))}
         stage_recs_d: List = [None] * len(self.plan.stages)
@@ -333,18 +370,19 @@ class DeviceRunner:
                                                self._prof_buf(ndocs, keep, f"langid{s}"))
                         ev_lid = self._record(self.s_lid)
                 prof = self._prof_buf(ndocs, keep, f"stage{s}")
+                skip = dead if pass_idx > 0 else None
                 if n_long:
                     self.s_blk.wait_event(ev_pre)
                     with torch.cuda.stream(self.s_blk):
                         self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[:n_long], n_long,
                                                  ndocs, scratch, d_soff, pw, pw_n, rec, flags, lid_vec, lid_cnt,
-                                                 self.lds_bytes_blk, prof)
+                                                 self.lds_bytes_blk, prof, skip)
                         ev_blk = self._record(self.s_blk)
                 if n_long < ndocs:
                     self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,
                                          scratch, d_soff, pw, pw_n, rec, flags,
                                          self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
-                                         self.lds_bytes, prof, self.stage_waves, ndocs - n_long)
+                                         self.lds_bytes, prof, self.stage_waves, ndocs - n_long, skip)
                 if lid_vec is not None:
                     self._last_lid = (lid_vec, lid_cnt)
                     main.wait_event(ev_lid)
@@ -353,6 +391,9 @@ class DeviceRunner:
                 for kind, width, prefix in layout:
                     if kind == 4:
                         self.k.langid_head(lid_vec, lid_cnt, self.lid_wT, self.lid_b, ndocs, rec, prefix * ndocs, width)
+                if pass_idx in self.gate_ts:
+                    self.k.gate(self.gate_ts[pass_idx], [rec], ndocs, flags, dead, pass_idx + 1, 0)
+                pass_idx += 1
                 stage_recs_d[s] = rec
             c4_here = [i for i in self.plan.c4_steps if self.plan.steps[i].version_in == ver]
             for i in c4_here:
@@ -366,17 +407,21 @@ class DeviceRunner:
                 out = torch.empty(cap, dtype=torch.uint8, device=self.device)
                 self.s_c4.wait_event(self._record(main))
                 self.s_c4.wait_event(ready[ver])
+                skip = dead if pass_idx > 0 else None
                 with torch.cuda.stream(self.s_c4):
                     prof = self._prof_buf(ndocs, keep, f"c4_step{i}")
                     if n_long:
                         self.k.c4_pass_a_blk(self.c4_ts[i], vb, vo, d_perm[:n_long], n_long, ndocs, c4_scratch,
-                                             d_soff, pw, pw_n, rec, src, flags, self.lds_bytes_blk, prof)
+                                             d_soff, pw, pw_n, rec, src, flags, self.lds_bytes_blk, prof, skip)
                     if n_long < ndocs:
                         self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm[n_long:], ndocs, c4_scratch, d_soff, pw,
-                                         pw_n, rec, src, flags, self.lds_bytes_c4, prof, ndocs - n_long)
+                                         pw_n, rec, src, flags, self.lds_bytes_c4, prof, ndocs - n_long, skip)
                     torch.cumsum(src.view(ndocs, 2)[:, 1], 0, out=new_off[1:])
                     self.k.c4_pass_b(vb, vo, ndocs, c4_scratch, d_soff, src, new_off, out)
+                    if pass_idx in self.gate_ts:
+                        self.k.gate(self.gate_ts[pass_idx], [rec], ndocs, flags, dead, pass_idx + 1, 0)
                     ev = self._record(self.s_c4)
+                pass_idx += 1
                 versions[ver + 1] = (out, new_off, cap)
                 ready[ver + 1] = ev
                 tails.append(ev)
@@ -404,16 +449,17 @@ class DeviceRunner:
                 vb, vo, _ = versions[ver]
                 h_versions[ver] = (d2h(vb), d2h(vo))
             h_flags = d2h(flags)
+            h_dead = d2h(dead) if dead is not None else None
             if self.phase_prof:
                 for item in keep:
                     if isinstance(item, tuple) and len(item) == 3 and item[0] == "prof":
                         item[2].record_stream(self.d2h_stream)
             ev = torch.cuda.Event()
             ev.record(self.d2h_stream)
-        keep += [stage_recs_d, c4_recs_d, versions, flags]
+        keep += [stage_recs_d, c4_recs_d, versions, flags, dead]
         t2 = time.perf_counter()
         return PendingBatch(self, ndocs, ev, h_stage, h_c4, h_versions, h_flags,
-                            {"stage_h2d": t1 - t0, "launch": t2 - t1}, keep)
+                            {"stage_h2d": t1 - t0, "launch": t2 - t1}, keep, h_dead)
 
     def run(self, data: np.ndarray, off: np.ndarray) -> DeviceResult:
         return self.submit(data, off).wait()
@@ -425,7 +471,10 @@ class EmulatedRunner:
     machine without a GPU (``Engine(backend="emulate")``): used by CPU tests and for profiling
     the host side of the device pipeline."""
 
-    def __init__(self, steps_native, plan: ExecPlan, langid=None, nthreads: int = 8):
+    def __init__(self, steps_native, plan: ExecPlan, langid=None, nthreads: int = 8, gating: Optional[bool] = None,
+                 gate_corrupt: int = 0):
+        import os
+
         h = native.host()
         self.steps = steps_native
         self.plan = plan
@@ -433,6 +482,12 @@ class EmulatedRunner:
         self.lid = langid.native() if langid is not None else None
         _, stage_bs = h.build_device_plan(steps_native, plan.stages)
         self.stage_layout = [h.stage_layout(b) for b in stage_bs]
+        if gating is None:
+            gating = os.environ.get("TB_GATE", "1") not in ("", "0")
+        self.passes, self.pass_of_step, self.gates = plan_passes(plan, self.stage_layout, steps_native, gating)
+        # test hook: additionally mark every k-th document dead after the first pass (a wrong
+        # device gate), to exercise the resolver's recovery path
+        self.gate_corrupt = gate_corrupt
 
     def run(self, data: np.ndarray, off: np.ndarray) -> DeviceResult:
         import time
@@ -444,18 +499,24 @@ class EmulatedRunner:
         versions = {0: (data, off)}
         stage_recs: List[Optional[np.ndarray]] = [None] * len(self.plan.stages)
         c4_recs = {}
-        for ver in range(self.plan.n_versions):
-            vd, vo = versions[ver]
-            for s, sv in enumerate(self.plan.stage_version):
-                if sv == ver:
-                    rec, fl = h.emulate_stage(self.steps, self.plan.stages[s], vd, vo, self.nthreads, self.lid)
-                    stage_recs[s] = rec
-                    flags |= fl
-            for i in self.plan.c4_steps:
-                if self.plan.steps[i].version_in == ver:
-                    rec, nd, no, fl = h.emulate_c4(self.steps[i], vd, vo, self.nthreads)
-                    c4_recs[i] = rec
-                    flags |= fl
-                    versions[ver + 1] = (nd, no)
+        dead = np.zeros(ndocs, dtype=np.uint8) if self.gates else None
+        for p, (kind, x) in enumerate(self.passes):
+            skip = dead if p > 0 else None
+            if kind == "stage":
+                vd, vo = versions[self.plan.stage_version[x]]
+                rec, fl = h.emulate_stage(self.steps, self.plan.stages[x], vd, vo, self.nthreads, self.lid, 0, skip)
+                stage_recs[x] = rec
+            else:
+                vd, vo = versions[self.plan.steps[x].version_in]
+                rec, nd, no, fl = h.emulate_c4(self.steps[x], vd, vo, self.nthreads, 0, skip)
+                c4_recs[x] = rec
+                versions[self.plan.steps[x].version_out] = (nd, no)
+            flags |= fl
+            if p in self.gates:
+                h.gate_host(self.gates[p], [rec], ndocs, flags, dead, p + 1)
+                if p == 0 and self.gate_corrupt > 0:
+                    extra = np.arange(0, ndocs, self.gate_corrupt)
+                    dead[extra[dead[extra] == 0]] = 1
         host_versions = {v: versions[v] for v in range(1, self.plan.n_versions)}
-        return DeviceResult(stage_recs, c4_recs, host_versions, flags, {"emulate": time.perf_counter() - t0})
+        return DeviceResult(stage_recs, c4_recs, host_versions, flags, {"emulate": time.perf_counter() - t0}, dead,
+                            self.pass_of_step)

@@ -61,17 +61,34 @@ class BatchResult:
         return int(sum(len(p.rows) for p in self.excluded))
 
 
+def _gate_mismatch(n: int, p: int) -> None:
+    import logging
+
+    from ..utils import metrics
+
+    logging.getLogger("textblaster_amd.engine").warning(
+        "device gate skipped %d document(s) in pass %d that the resolver finds alive; recomputing them on the CPU path",
+        n, p)
+    metrics.GATE_MISMATCH_DOCS_TOTAL.inc(n)
+
+
 def default_threads() -> int:
     # the GPU boxes expose every CPU of the host through the affinity mask but give one GPU a
     # share of them (OMP_NUM_THREADS); honour explicit limits first
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)
     for var in ("TB_THREADS", "OMP_NUM_THREADS"):
         env = os.environ.get(var)
         if env and env.isdigit() and int(env) > 0:
+            # torch.distributed.run exports OMP_NUM_THREADS=1 to every rank when it was unset;
+            # that is its default for math libraries, not a CPU budget for our host runtime
+            if var == "OMP_NUM_THREADS" and int(env) == 1 and local_world > 1:
+                continue
             return int(env)
     try:
-        return max(1, len(os.sched_getaffinity(0)))
+        ncpu = max(1, len(os.sched_getaffinity(0)))
     except AttributeError:
-        return os.cpu_count() or 1
+        ncpu = os.cpu_count() or 1
+    return max(1, min(32, ncpu // max(1, local_world))) if local_world > 1 else ncpu
 
 
 class Engine:
@@ -270,8 +287,20 @@ class Engine:
             for v in sorted(res.versions):
                 vd, vo = res.versions[v]
                 vid[v] = bs.add_version(np.ascontiguousarray(vd), np.ascontiguousarray(vo))
+            dead = getattr(res, "dead", None)
+            gate_checked = set()
             for sp in self.plan.steps:
                 st = self.steps[sp.index]
+                p = res.pass_of_step.get(sp.index, 0) if dead is not None else 0
+                if p > 0 and p not in gate_checked:
+                    # documents the device skipped in this pass must already be filtered here;
+                    # any that are still alive (a gate disagreement) go to the CPU path
+                    gate_checked.add(p)
+                    bad = np.nonzero((dead != 0) & (dead <= p) & (bs.fail_step() < 0))[0].astype(np.int64)
+                    if len(bad):
+                        _gate_mismatch(len(bad), p)
+                        bs.delegate(bad)
+                        delegated = np.union1d(delegated, bad).astype(np.int64)
                 if sp.stage >= 0:
                     width_total, layout = self.device_runner.stage_layout[sp.stage]
                     pos = self.plan.stages[sp.stage].index(sp.index)

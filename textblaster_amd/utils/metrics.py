@@ -69,6 +69,9 @@ BATCH_FAILURES_TOTAL = Counter("tb_batch_failures_total", "Batches whose device 
                                ["error"], registry=REGISTRY)
 CPU_FALLBACK_DOCS_TOTAL = Counter("tb_cpu_fallback_docs_total",
                                   "Documents re-run on the CPU oracle path after a device failure.", registry=REGISTRY)
+GATE_MISMATCH_DOCS_TOTAL = Counter("tb_gate_mismatch_docs_total",
+                                   "Documents a device step gate skipped that the host resolver found alive "
+                                   "(recomputed on the CPU path; expected 0).", registry=REGISTRY)
 RANK = Gauge("tb_rank", "Data-parallel rank of this process.", registry=REGISTRY)
 WORLD_SIZE = Gauge("tb_world_size", "Number of data-parallel ranks.", registry=REGISTRY)
 GLOBAL_DOCS = Gauge("tb_global_docs_total", "All-reduced document counters (rank 0).", ["kind"],

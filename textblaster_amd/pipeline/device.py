@@ -180,12 +180,20 @@ class DeviceRunner:
         self.s_lid = torch.cuda.Stream(self.device)
         self.s_blk = torch.cuda.Stream(self.device)
         self.s_c4 = torch.cuda.Stream(self.device)
+        if os.environ.get("TB_SERIAL_STREAMS", "") not in ("", "0"):
+            # profiling aid: every kernel of a batch on the compute stream (exclusive durations)
+            self.s_lid = self.s_blk = self.s_c4 = torch.cuda.current_stream(self.device)
         self.copy_threads = int(os.environ.get("TB_COPY_THREADS", "8"))
         self._next_slot = 0
         self._last_lid = None
         self.s_bw = torch.cuda.Stream(self.device)
         self._bw_auto = None  # (key, device tensors) of the flattened bad-words automaton
         self._bw_fold = None
+
+    def bind_thread(self) -> None:
+        """Make this runner's GPU the current device of the calling thread (HIP's current device
+        is per thread; helper threads that launch work for this runner call this first)."""
+        self.torch.cuda.set_device(self.device)
 
     def badwords_match(self, key, automaton, data: np.ndarray, off: np.ndarray, roots: np.ndarray,
                        cjk: np.ndarray) -> np.ndarray:

@@ -101,6 +101,11 @@ class Engine:
         self._cpu_engine = None
         self._n_submitted = 0
         self._fault = _parse_fault(fault_inject or os.environ.get("TB_FAULT_INJECT", ""))
+        import threading
+
+        self._submit_lock = threading.RLock()
+        # process_many on the GPU backend submits from a helper thread (TB_PREFETCH_THREAD=0: off)
+        self.prefetch_threads = os.environ.get("TB_PREFETCH_THREAD", "1") not in ("", "0")
         # text bytes per device batch (scratch ~160 B per text byte per in-flight slot)
         self.max_batch_bytes = int(os.environ.get("TB_MAX_BATCH_BYTES", str(192 << 20)))
         self.h = native.host()
@@ -172,12 +177,18 @@ class Engine:
                 for base, sub in subs:
                     yield g, base, sub
 
+        def submit_item(g, base, item):
+            try:
+                return (g, base, item, self.submit(item[0], item[1], item[2] if len(item) > 2 else None))
+            except Exception as e:  # noqa: BLE001 - handled per on_error
+                return (g, base, item, e)
+
+        if self.prefetch_threads and self.backend in ("cuda", "emulate"):
+            yield from self._process_threaded(expand(), submit_item, on_error, groups, sizes)
+            return
         pending = None
         for g, base, item in expand():
-            try:
-                cur = (g, base, item, self.submit(item[0], item[1], item[2] if len(item) > 2 else None))
-            except Exception as e:  # noqa: BLE001 - handled per on_error
-                cur = (g, base, item, e)
+            cur = submit_item(g, base, item)
             if pending is not None:
                 out = self._collect_group(pending, on_error, groups, sizes)
                 if out is not None:
@@ -187,6 +198,53 @@ class Engine:
             out = self._collect_group(pending, on_error, groups, sizes)
             if out is not None:
                 yield out
+
+    def _process_threaded(self, items, submit_item, on_error, groups, sizes):
+        """process_many with a submitter thread: input staging (pinned copy + H2D) and kernel
+        launches of the next batches run on their own thread while this thread resolves and
+        assembles the current one, so the host critical path is max(staging, resolve+assemble)
+        instead of their sum. At most two batches wait in the hand-off queue."""
+        import queue
+        import threading
+
+        q: "queue.Queue" = queue.Queue(maxsize=1)
+        stop = threading.Event()
+        _END = object()
+
+        def producer():
+            try:
+                bind = getattr(self.device_runner, "bind_thread", None)
+                if bind is not None:
+                    bind()
+                for g, base, item in items:
+                    if stop.is_set():
+                        break
+                    q.put(submit_item(g, base, item))
+            except BaseException as e:  # noqa: BLE001 - re-raised on the consumer thread
+                q.put(("__error__", e))
+            finally:
+                q.put(_END)
+
+        th = threading.Thread(target=producer, name="tb-submit", daemon=True)
+        th.start()
+        try:
+            while True:
+                x = q.get()
+                if x is _END:
+                    break
+                if x[0] == "__error__":
+                    raise x[1]
+                out = self._collect_group(x, on_error, groups, sizes)
+                if out is not None:
+                    yield out
+        finally:
+            stop.set()
+            while th.is_alive():
+                try:
+                    q.get(timeout=0.05)
+                except queue.Empty:
+                    pass
+            th.join()
 
     def _split_by_bytes(self, item):
         data, off = item[0], item[1]
@@ -254,6 +312,10 @@ class Engine:
         return self._cpu_engine
 
     def submit(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None, row_base: int = 0):
+        with self._submit_lock:  # the submitter thread and batch recovery may both submit
+            return self._submit(data, off, meta, row_base)
+
+    def _submit(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None, row_base: int = 0):
         t0 = time.perf_counter()
         self._n_submitted += 1
         if self._fault is not None and not self._fault.get("fired") and self._n_submitted == self._fault["batch"]:

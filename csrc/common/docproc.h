@@ -282,33 +282,43 @@ TB_HD Lines rust_lines(DocCtx<P>& x, const Cps& c) {
 }
 
 // canon[i] = smallest j with element j == element i (key() groups candidates, eq() verifies).
+// Open-addressing table of ~1.5 n packed 64-bit slots (fingerprint = high 32 bits of the key,
+// low 32 bits = smallest index + 1; 0 = empty), small enough to stay in the wave's LDS slice for
+// typical documents. An element joins the group whose slot holds its fingerprint (one 64-bit
+// atomic min keeps the smallest index) and remembers the slot in canon[] until the lookup pass;
+// every non-trivial member is then verified against its representative with eq(), so a
+// fingerprint collision between unequal elements sends the document to the CPU oracle.
 template <class P, class KeyF, class EqF>
 TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t* canon) {
-  uint32_t capn = 16;
-  while (capn < 2 * n + 2) capn <<= 1;
-  const uint32_t mask = capn - 1;
+  const uint32_t capn = n + (n >> 1) + 2;
   const auto mark = x.mark();
-  uint64_t* keys = x.template alloc_hot<uint64_t>(capn);
-  uint32_t* vals = x.template alloc_hot<uint32_t>(capn);
+  uint64_t* tab = x.template alloc_hot<uint64_t>(capn);
   if (x.overflow) return;
-  x.par.for_n(capn, [&](uint32_t i) { keys[i] = 0; vals[i] = 0xFFFFFFFFu; });
+  x.par.for_n(capn, [&](uint32_t i) { tab[i] = 0; });
   x.par.sync();
   x.par.for_n(n, [&](uint32_t i) {
     const uint64_t k = key(i);
-    uint32_t slot = (uint32_t)(k >> 17) & mask;
+    const uint64_t fp = (k >> 32) | 1ull;
+    const uint64_t mine = (fp << 32) | (uint64_t)(i + 1);
+    uint32_t slot = (uint32_t)(((k & 0xFFFFFFFFull) * capn) >> 32);
     while (true) {
-      uint64_t old = P::cas64(&keys[slot], 0, k);
-      if (old == 0 || old == k) { P::min32(&vals[slot], i); break; }
-      slot = (slot + 1) & mask;
+      uint64_t cur = tab[slot];
+      if (cur == 0) {
+        cur = P::cas64(&tab[slot], 0, mine);
+        if (cur == 0) break;
+      }
+      if ((cur >> 32) == fp) {
+        P::min64(&tab[slot], mine);
+        break;
+      }
+      if (++slot == capn) slot = 0;
     }
+    canon[i] = slot;
   });
   x.par.sync();
   bool collided = false;
   x.par.for_n(n, [&](uint32_t i) {
-    const uint64_t k = key(i);
-    uint32_t slot = (uint32_t)(k >> 17) & mask;
-    while (keys[slot] != k) slot = (slot + 1) & mask;
-    uint32_t c = vals[slot];
+    uint32_t c = (uint32_t)(tab[canon[i]] & 0xFFFFFFFFull) - 1u;
     if (c != i && !eq(i, c)) { collided = true; c = i; }
     canon[i] = c;
   });
@@ -654,40 +664,59 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       }
       x.par.sync();
       const int ndup = ds.n_dup;
-      // Skip the walk's duplicate-free prefix: before the first repeated gram p0 (gc[p] != p) the
-      // walk advances one position at a time and marks every gram p < p0 (each its own first
-      // occurrence), so it can start at p0 with bits [0, p0) set; no repeat at all -> 0.
-      uint32_t* p0s = x.template alloc_hot<uint32_t>(kMaxNgramEntries);
+      // The greedy walk only has to stop at *repeated* grams (canonical id shared with another
+      // position). At a gram that occurs once the walk marks its id as seen (an id no other
+      // position has) and advances by one, so those positions are skipped without bookkeeping:
+      // per n a bitmap R of repeated positions (p with gc[p] != p, and their first occurrence
+      // gc[p]) lets the walking lane jump from one repeated position to the next.
+      uint32_t* R_all = x.template alloc_hot<uint32_t>((uint64_t)SW * ndup);
       if (x.overflow) return;
+      x.par.for_n(SW * (uint32_t)ndup, [&](uint32_t i) { R_all[i] = 0; });
+      x.par.sync();
       for (int t = 0; t < ndup; ++t) {
         const uint32_t n = (uint32_t)ds.dup_n[t];
         if (n == 0 || W < n) continue;
         const uint32_t G = W - n + 1;
         const uint32_t* gc = (const uint32_t*)(uintptr_t)gofs[2 * t];
-        uint32_t* sn = (uint32_t*)(uintptr_t)gofs[2 * t + 1];
-        const uint32_t p0 = x.par.template min<uint32_t>(G, G, [&](uint32_t p) { return gc[p] != p ? p : G; });
-        x.par.for_n((p0 + 31) / 32, [&](uint32_t i) {
-          const uint32_t lo = i * 32;
-          sn[i] = (p0 - lo >= 32) ? 0xFFFFFFFFu : ((1u << (p0 - lo)) - 1u);
+        uint32_t* R = R_all + (size_t)t * SW;
+        x.par.for_n(G, [&](uint32_t p) {
+          const uint32_t g = gc[p];
+          if (g != p) {
+            P::or32(&R[p >> 5], 1u << (p & 31));
+            P::or32(&R[g >> 5], 1u << (g & 31));
+          }
         });
-        x.par.single([&]() { p0s[t] = p0; });
       }
       x.par.sync();
       x.par.for_n((uint32_t)ndup, [&](uint32_t t) {
         const uint32_t n = (uint32_t)ds.dup_n[t];
         int64_t rep = 0;
-        if (n > 0 && W >= n && p0s[t] < W - n + 1) {
+        if (n > 0 && W >= n) {
+          const uint32_t G = W - n + 1;
+          const uint32_t nw = (G + 31) >> 5;
           const uint32_t* gc = (const uint32_t*)(uintptr_t)gofs[2 * t];
           uint32_t* sn = (uint32_t*)(uintptr_t)gofs[2 * t + 1];
-          uint32_t idx = p0s[t];
-          while (idx + n <= W) {
+          const uint32_t* R = R_all + (size_t)t * SW;
+          auto next_rep = [&](uint32_t from) -> uint32_t {  // first repeated position >= from, or G
+            if (from >= G) return G;
+            uint32_t wi = from >> 5;
+            uint32_t bits = R[wi] & (~0u << (from & 31));
+            while (!bits) {
+              if (++wi >= nw) return G;
+              bits = R[wi];
+            }
+            const uint32_t q = (wi << 5) + (uint32_t)__builtin_ctz(bits);
+            return q < G ? q : G;
+          };
+          uint32_t idx = next_rep(0);
+          while (idx < G) {
             const uint32_t g = gc[idx];
             if ((sn[g >> 5] >> (g & 31)) & 1u) {
               rep += (int64_t)(WL[idx + n] - WL[idx]);
-              idx += n;
+              idx = next_rep(idx + n);
             } else {
               sn[g >> 5] |= 1u << (g & 31);
-              ++idx;
+              idx = next_rep(idx + 1);
             }
           }
         }

@@ -16,10 +16,15 @@
 //  * scan<T>(n, id, op, in, out): out(i, exclusive prefix) for every i; returns the total.
 //  * sync(): every write before it is visible to every lane after it.
 //  * single(f): f() runs once (lane 0).
-//  * cas64/min32/add32/add64/max32: atomics on scratch memory.
+//  * cas64/min32/min64/add32/add64/max32: atomics on scratch memory.
 #pragma once
 #include "langid.h"
 #include "tb_common.h"
+
+// Chunks of 64 items whose loads a wave issues together in the latency-bound passes (WavePar).
+#ifndef TB_UNROLL
+#define TB_UNROLL 2
+#endif
 
 namespace tb {
 
@@ -80,6 +85,7 @@ struct SeqPar {
     return old;
   }
   static void min32(uint32_t* p, uint32_t v) { if (v < *p) *p = v; }
+  static void min64(uint64_t* p, uint64_t v) { if (v < *p) *p = v; }
   static void max32(uint32_t* p, uint32_t v) { if (v > *p) *p = v; }
   static uint32_t add32(uint32_t* p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
   static void or32(uint32_t* p, uint32_t v) { *p |= v; }
@@ -152,71 +158,124 @@ struct WavePar {
   __device__ WavePar() : lane(threadIdx.x & 63) {}
 
   template <class F>
-  __device__ void for_n(uint32_t n, F&& f) const {
+  __device__ __forceinline__ void for_n(uint32_t n, F&& f) const {
     for (uint32_t i = lane; i < n; i += 64) f(i);
   }
+  // The per-document passes are bound by memory latency (scratch arrays mostly miss L2), so
+  // the pure parts of a pass (predicates, scan inputs, reduction terms) are evaluated for
+  // kUnroll chunks of 64 items before any of them is consumed: each lane keeps kUnroll
+  // independent loads in flight instead of one. Results are unchanged (chunk order is kept,
+  // integer reductions are exact in any order).
+  static constexpr uint32_t kU = TB_UNROLL;
   template <class S, class Pred, class Emit>
-  __device__ uint32_t compact(uint32_t n, Pred&& pred, Emit&& emit) const {
+  __device__ __forceinline__ uint32_t compact(uint32_t n, Pred&& pred, Emit&& emit) const {
     uint32_t k = 0;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t base = 0; base < n; base += 64) {
-      const uint32_t i = base + lane;
-      S st{};
-      const bool p = i < n && pred(i, st);
-      const uint64_t m = __ballot(p);
-      if (p) emit(i, k + (uint32_t)__popcll(m & lt), st);
-      k += (uint32_t)__popcll(m);
+    for (uint32_t base = 0; base < n; base += 64 * kU) {
+      S st[kU];
+      bool p[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t i = base + 64 * u + lane;
+        st[u] = S{};
+        p[u] = i < n && pred(i, st[u]);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t i = base + 64 * u + lane;
+        const uint64_t m = __ballot(p[u]);
+        if (p[u]) emit(i, k + (uint32_t)__popcll(m & lt), st[u]);
+        k += (uint32_t)__popcll(m);
+      }
     }
     return k;
   }
   template <class T>
-  __device__ static T wave_sum(T v) {
+  __device__ __forceinline__ static T wave_sum(T v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
   }
   template <class T>
-  __device__ static T wave_max(T v) {
+  __device__ __forceinline__ static T wave_max(T v) {
     for (int o = 32; o > 0; o >>= 1) { T t = __shfl_xor(v, o); v = t > v ? t : v; }
     return v;
   }
   template <class T>
-  __device__ static T wave_min(T v) {
+  __device__ __forceinline__ static T wave_min(T v) {
     for (int o = 32; o > 0; o >>= 1) { T t = __shfl_xor(v, o); v = t < v ? t : v; }
     return v;
   }
   template <class T, class F>
-  __device__ T sum(uint32_t n, F&& f) const {
-    T s = 0;
-    for (uint32_t i = lane; i < n; i += 64) s += f(i);
-    return wave_sum(s);
+  __device__ __forceinline__ T sum(uint32_t n, F&& f) const {
+    T s[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) s[u] = 0;
+    uint32_t i = lane;
+    for (; i + 64 * (kU - 1) < n; i += 64 * kU) {
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) s[u] += f(i + 64 * u);
+    }
+    for (; i < n; i += 64) s[0] += f(i);
+#pragma unroll
+    for (uint32_t u = 1; u < kU; ++u) s[0] += s[u];
+    return wave_sum(s[0]);
   }
   template <class T, class F>
-  __device__ T max(uint32_t n, T init, F&& f) const {
-    T s = init;
-    for (uint32_t i = lane; i < n; i += 64) { T v = f(i); if (v > s) s = v; }
-    return wave_max(s);
+  __device__ __forceinline__ T max(uint32_t n, T init, F&& f) const {
+    T s[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) s[u] = init;
+    uint32_t i = lane;
+    for (; i + 64 * (kU - 1) < n; i += 64 * kU) {
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) { T v = f(i + 64 * u); if (v > s[u]) s[u] = v; }
+    }
+    for (; i < n; i += 64) { T v = f(i); if (v > s[0]) s[0] = v; }
+#pragma unroll
+    for (uint32_t u = 1; u < kU; ++u) if (s[u] > s[0]) s[0] = s[u];
+    return wave_max(s[0]);
   }
   template <class T, class F>
-  __device__ T min(uint32_t n, T init, F&& f) const {
-    T s = init;
-    for (uint32_t i = lane; i < n; i += 64) { T v = f(i); if (v < s) s = v; }
-    return wave_min(s);
+  __device__ __forceinline__ T min(uint32_t n, T init, F&& f) const {
+    T s[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) s[u] = init;
+    uint32_t i = lane;
+    for (; i + 64 * (kU - 1) < n; i += 64 * kU) {
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) { T v = f(i + 64 * u); if (v < s[u]) s[u] = v; }
+    }
+    for (; i < n; i += 64) { T v = f(i); if (v < s[0]) s[0] = v; }
+#pragma unroll
+    for (uint32_t u = 1; u < kU; ++u) if (s[u] < s[0]) s[0] = s[u];
+    return wave_min(s[0]);
   }
   template <class T, class Op, class In, class Out>
-  __device__ T scan(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
+  __device__ __forceinline__ T scan(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
     T carry = id;
-    for (uint32_t base = 0; base < n; base += 64) {
-      const uint32_t i = base + lane;
-      T x = i < n ? in(i) : id;
-      // inclusive Hillis-Steele scan (op is associative, not necessarily commutative)
-      for (int o = 1; o < 64; o <<= 1) {
-        T y = pardetail::shfl_up_t(x, o);
-        if ((int)lane >= o) x = op(y, x);
+    for (uint32_t base0 = 0; base0 < n; base0 += 64 * kU) {
+      T xs[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t i = base0 + 64 * u + lane;
+        xs[u] = i < n ? in(i) : id;
       }
-      T excl = pardetail::shfl_up_t(x, 1);
-      if (lane == 0) excl = id;
-      if (i < n) out(i, op(carry, excl));
-      carry = op(carry, pardetail::shfl_t(x, 63));
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t base = base0 + 64 * u;
+        if (base >= n) break;
+        const uint32_t i = base + lane;
+        T x = xs[u];
+        // inclusive Hillis-Steele scan (op is associative, not necessarily commutative)
+        for (int o = 1; o < 64; o <<= 1) {
+          T y = pardetail::shfl_up_t(x, o);
+          if ((int)lane >= o) x = op(y, x);
+        }
+        T excl = pardetail::shfl_up_t(x, 1);
+        if (lane == 0) excl = id;
+        if (i < n) out(i, op(carry, excl));
+        carry = op(carry, pardetail::shfl_t(x, 63));
+      }
     }
     return carry;
   }
@@ -225,7 +284,7 @@ struct WavePar {
   // then each lane replays its block to emit the prefixes (op evaluated ~2x per item instead of
   // log2(64) = 6x, and K-fold fewer shuffles).
   template <int K, class T, class Op, class In, class Out>
-  __device__ T scan_blocked(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
+  __device__ __forceinline__ T scan_blocked(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
     T carry = id;
     for (uint32_t base = 0; base < n; base += 64u * K) {
       const uint32_t start = base + lane * K;
@@ -254,25 +313,28 @@ struct WavePar {
     }
     return carry;
   }
-  __device__ void sync() const { __syncthreads(); }
-  __device__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ void sync() const { __syncthreads(); }
+  __device__ __forceinline__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
   template <class F>
-  __device__ void single(F&& f) const { if (lane == 0) f(); }
-  __device__ bool leader() const { return lane == 0; }
-  __device__ static uint64_t cas64(uint64_t* p, uint64_t cmp, uint64_t val) {
+  __device__ __forceinline__ void single(F&& f) const { if (lane == 0) f(); }
+  __device__ __forceinline__ bool leader() const { return lane == 0; }
+  __device__ __forceinline__ static uint64_t cas64(uint64_t* p, uint64_t cmp, uint64_t val) {
     return atomicCAS((unsigned long long*)p, (unsigned long long)cmp, (unsigned long long)val);
   }
-  __device__ static void min32(uint32_t* p, uint32_t v) { atomicMin(p, v); }
-  __device__ static void max32(uint32_t* p, uint32_t v) { atomicMax(p, v); }
-  __device__ static uint32_t add32(uint32_t* p, uint32_t v) { return atomicAdd(p, v); }
-  __device__ static void or32(uint32_t* p, uint32_t v) { atomicOr(p, v); }
+  __device__ __forceinline__ static void min32(uint32_t* p, uint32_t v) { atomicMin(p, v); }
+  __device__ __forceinline__ static void min64(uint64_t* p, uint64_t v) {
+    atomicMin((unsigned long long*)p, (unsigned long long)v);
+  }
+  __device__ __forceinline__ static void max32(uint32_t* p, uint32_t v) { atomicMax(p, v); }
+  __device__ __forceinline__ static uint32_t add32(uint32_t* p, uint32_t v) { return atomicAdd(p, v); }
+  __device__ __forceinline__ static void or32(uint32_t* p, uint32_t v) { atomicOr(p, v); }
 
   // Each lane accumulates its items (i = lane, lane+64, ...) in D int32 registers, so the
   // item loads of one lane are independent of the other lanes' and of each other; the 64 x D
   // partials then go through `tmp` (64*D int32, LDS when available) and lane d sums column d
   // in int64. Callers bound the per-lane magnitude so int32 partials cannot overflow.
   template <int D, class F>
-  __device__ void accum_rows(uint32_t n, F&& f, int32_t* tmp, int64_t* sums) const {
+  __device__ __forceinline__ void accum_rows(uint32_t n, F&& f, int32_t* tmp, int64_t* sums) const {
     int32_t part[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) part[d] = 0;
@@ -288,7 +350,7 @@ struct WavePar {
     __syncthreads();
   }
   template <int D, class Row, class Out>
-  __device__ void gather_rows_fixed(uint32_t K, Row&& row_ptr, Out&& out) const {
+  __device__ __forceinline__ void gather_rows_fixed(uint32_t K, Row&& row_ptr, Out&& out) const {
     static_assert(D == 32, "lane layout assumes 32 dims");
     const int d = lane & 31, h = lane >> 5;
     int64_t s = 0;
@@ -312,11 +374,11 @@ struct BlockPar {
   __device__ BlockPar() : tid(threadIdx.x), lane(threadIdx.x & 63), wid(threadIdx.x >> 6) {}
 
   template <class F>
-  __device__ void for_n(uint32_t n, F&& f) const {
+  __device__ __forceinline__ void for_n(uint32_t n, F&& f) const {
     for (uint32_t i = tid; i < n; i += NT) f(i);
   }
   template <class S, class Pred, class Emit>
-  __device__ uint32_t compact(uint32_t n, Pred&& pred, Emit&& emit) const {
+  __device__ __forceinline__ uint32_t compact(uint32_t n, Pred&& pred, Emit&& emit) const {
     uint32_t k = 0;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t* cnt = (uint32_t*)xs;
@@ -340,7 +402,7 @@ struct BlockPar {
     return k;
   }
   template <class T, class Op>
-  __device__ T block_reduce(T v, Op&& op) const {
+  __device__ __forceinline__ T block_reduce(T v, Op&& op) const {
     for (int o = 32; o > 0; o >>= 1) v = op(v, pardetail::shfl_t(v, (int)(lane ^ o)));
     T* t = (T*)xs;
     if (lane == 0) t[wid] = v;
@@ -351,26 +413,26 @@ struct BlockPar {
     return r;
   }
   template <class T, class F>
-  __device__ T sum(uint32_t n, F&& f) const {
+  __device__ __forceinline__ T sum(uint32_t n, F&& f) const {
     T s = 0;
     for (uint32_t i = tid; i < n; i += NT) s += f(i);
     return block_reduce(s, [](T a, T b) { return a + b; });
   }
   template <class T, class F>
-  __device__ T max(uint32_t n, T init, F&& f) const {
+  __device__ __forceinline__ T max(uint32_t n, T init, F&& f) const {
     T s = init;
     for (uint32_t i = tid; i < n; i += NT) { T v = f(i); if (v > s) s = v; }
     return block_reduce(s, [](T a, T b) { return a > b ? a : b; });
   }
   template <class T, class F>
-  __device__ T min(uint32_t n, T init, F&& f) const {
+  __device__ __forceinline__ T min(uint32_t n, T init, F&& f) const {
     T s = init;
     for (uint32_t i = tid; i < n; i += NT) { T v = f(i); if (v < s) s = v; }
     return block_reduce(s, [](T a, T b) { return a < b ? a : b; });
   }
   // Exclusive prefix of this wave's inclusive totals across waves (in wave order).
   template <class T, class Op>
-  __device__ void cross_wave(T wave_incl_last, T id, Op&& op, T& before, T& total) const {
+  __device__ __forceinline__ void cross_wave(T wave_incl_last, T id, Op&& op, T& before, T& total) const {
     T* t = (T*)xs;
     if (lane == 63) t[wid] = wave_incl_last;
     __syncthreads();
@@ -384,7 +446,7 @@ struct BlockPar {
     __syncthreads();
   }
   template <class T, class Op, class In, class Out>
-  __device__ T scan(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
+  __device__ __forceinline__ T scan(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
     T carry = id;
     for (uint32_t base = 0; base < n; base += NT) {
       const uint32_t i = base + tid;
@@ -400,7 +462,7 @@ struct BlockPar {
     return carry;
   }
   template <int K, class T, class Op, class In, class Out>
-  __device__ T scan_blocked(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
+  __device__ __forceinline__ T scan_blocked(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
     T carry = id;
     for (uint32_t base = 0; base < n; base += (uint32_t)NT * K) {
       const uint32_t start = base + tid * K;
@@ -427,18 +489,21 @@ struct BlockPar {
     }
     return carry;
   }
-  __device__ void sync() const { __syncthreads(); }
-  __device__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ void sync() const { __syncthreads(); }
+  __device__ __forceinline__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
   template <class F>
-  __device__ void single(F&& f) const { if (tid == 0) f(); }
-  __device__ bool leader() const { return tid == 0; }
-  __device__ static uint64_t cas64(uint64_t* p, uint64_t cmp, uint64_t val) {
+  __device__ __forceinline__ void single(F&& f) const { if (tid == 0) f(); }
+  __device__ __forceinline__ bool leader() const { return tid == 0; }
+  __device__ __forceinline__ static uint64_t cas64(uint64_t* p, uint64_t cmp, uint64_t val) {
     return atomicCAS((unsigned long long*)p, (unsigned long long)cmp, (unsigned long long)val);
   }
-  __device__ static void min32(uint32_t* p, uint32_t v) { atomicMin(p, v); }
-  __device__ static void max32(uint32_t* p, uint32_t v) { atomicMax(p, v); }
-  __device__ static uint32_t add32(uint32_t* p, uint32_t v) { return atomicAdd(p, v); }
-  __device__ static void or32(uint32_t* p, uint32_t v) { atomicOr(p, v); }
+  __device__ __forceinline__ static void min32(uint32_t* p, uint32_t v) { atomicMin(p, v); }
+  __device__ __forceinline__ static void min64(uint64_t* p, uint64_t v) {
+    atomicMin((unsigned long long*)p, (unsigned long long)v);
+  }
+  __device__ __forceinline__ static void max32(uint32_t* p, uint32_t v) { atomicMax(p, v); }
+  __device__ __forceinline__ static uint32_t add32(uint32_t* p, uint32_t v) { return atomicAdd(p, v); }
+  __device__ __forceinline__ static void or32(uint32_t* p, uint32_t v) { atomicOr(p, v); }
 };
 #endif
 

@@ -110,3 +110,31 @@ def test_byte_budget_split_batches():
     res = list(eng.process_many(batches))
     assert [outputs(r) for r in res] == ref
     assert [r.n_docs for r in res] == [300, 300]
+
+
+def test_gopher_repetition_records_equal_oracle_on_repetitive_text(host):
+    """Device GopherRepetition records (host port of the kernel: canonical n-grams, repeated-
+    position bitmaps, greedy duplicate walk) equal the ICU oracle's records field by field, on
+    text with many repeated n-grams (different word splits of equal text included)."""
+    cfg = load_pipeline_config("config/bench_pipeline.yaml")
+    steps = [host.make_step(s.native_dict()) for s in cfg.pipeline]
+    gi = [i for i, s in enumerate(cfg.pipeline) if s.type == "GopherRepetitionFilter"][0]
+    rng = np.random.default_rng(3)
+    texts = synth.make_corpus(300, 900, seed=41)
+    words = "the cat sat on the mat and the dog ran".split()
+    for _ in range(200):
+        k = int(rng.integers(2, 10))
+        texts.append(" ".join(rng.choice(words[:k], size=int(rng.integers(20, 400)))))
+    texts += ["ab c a bc ab c a bc " * 20, "a b a b a b a b a b a b a b a b", "x y z\n\nx y z\nx y z"] + EDGE
+    data, off = synth.pack(texts)
+    rec, fl = host.emulate_stage(steps, [gi], data, off, 4, None, 0)
+    w = steps[gi].record_width()
+    rec = rec.reshape(len(texts), w)
+    with_dups = 0
+    for i, t in enumerate(texts):
+        if fl[i]:
+            continue
+        ref = list(host.compute_record(steps[gi], t, "icu")[0])
+        with_dups += any(ref[7 + 3:])
+        assert ref == list(rec[i]), (i, t[:80], ref, list(rec[i]))
+    assert with_dups > 100

@@ -130,6 +130,8 @@ class DeviceRunner:
 
         self.torch = torch
         self.device = torch.device(device)
+        if self.device.index is None:  # "cuda" -> the current device, explicitly (helper threads bind to it)
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.plan = plan
         self.steps = steps_native
         h = native.host()

@@ -79,7 +79,8 @@ struct DocCtx {
   uint64_t used = 0;
   char* lds = nullptr;       // optional fast arena (the wave's LDS slice on the device)
   uint32_t lcap = 0;
-  uint32_t lused = 0;
+  uint32_t lused = 0;        // bytes allocated from the bottom of the LDS slice
+  uint32_t lhi = 0;          // bytes allocated from the top (temporaries, releasable props)
   uint32_t* flag = nullptr;  // per-document status word
   bool overflow = false;
   uint64_t* prof = nullptr;  // optional per-document phase cycle counters (kPhaseSlots)
@@ -93,9 +94,9 @@ struct DocCtx {
     t_last = t;
   }
 
-  struct Mark { uint64_t g; uint32_t l; };
-  TB_HD Mark mark() const { return Mark{used, lused}; }
-  TB_HD void reset(Mark m) { used = m.g; lused = m.l; }
+  struct Mark { uint64_t g; uint32_t l, h; };
+  TB_HD Mark mark() const { return Mark{used, lused, lhi}; }
+  TB_HD void reset(Mark m) { used = m.g; lused = m.l; lhi = m.h; }
 
   // Placement: big streaming per-code-point arrays live in the HBM scratch arena (alloc);
   // small randomly-accessed ones (hash tables, per-word / per-n-gram arrays, reduction
@@ -108,13 +109,29 @@ struct DocCtx {
     if (lds) {
       const uint64_t a = (lused + 15u) & ~15u;
       const uint64_t e = a + count * sizeof(T);
-      if (e <= lcap) {
+      if (e + lhi <= lcap) {
         lused = (uint32_t)e;
         return (T*)(lds + a);
       }
     }
     return alloc_global<T>(count);
   }
+  // Same, from the top of the LDS slice: short-lived tables (released by reset()) and the
+  // property array, which the n-gram statistics no longer need (release_hi()), so the space
+  // they held goes back to the hash tables of the later phases.
+  template <class T>
+  TB_HD T* alloc_hot_hi(uint64_t count) {
+    if (lds) {
+      const uint64_t bytes = (count * sizeof(T) + 15u) & ~15ull;
+      const uint64_t lo = (lused + 15u) & ~15u;
+      if (lo + lhi + bytes <= lcap) {
+        lhi += (uint32_t)bytes;
+        return (T*)(lds + (lcap - lhi));
+      }
+    }
+    return alloc_global<T>(count);
+  }
+  TB_HD void release_hi() { lhi = 0; }
   template <class T>
   TB_HD T* alloc_global(uint64_t count) {
     uint64_t a = (used + 15) & ~15ull;
@@ -146,7 +163,7 @@ TB_HD Cps decode(DocCtx<P>& x, const uint8_t* b, uint32_t n, bool hot_props = fa
   Cps c;
   // prop[] is read by every rule evaluation (UAX#29 look-around, trims, classes): with
   // hot_props it goes to the LDS slice when the document is small enough
-  c.prop = hot_props ? x.template alloc_hot<uint32_t>(n + 1) : x.template alloc<uint32_t>(n + 1);
+  c.prop = hot_props ? x.template alloc_hot_hi<uint32_t>(n + 1) : x.template alloc<uint32_t>(n + 1);
   c.off = x.template alloc<uint32_t>(n + 1);
   c.cp = x.template alloc<uint32_t>(n + 1);
   if (x.overflow) return c;
@@ -292,7 +309,7 @@ template <class P, class KeyF, class EqF>
 TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t* canon) {
   const uint32_t capn = n + (n >> 1) + 2;
   const auto mark = x.mark();
-  uint64_t* tab = x.template alloc_hot<uint64_t>(capn);
+  uint64_t* tab = x.template alloc_hot_hi<uint64_t>(capn);
   if (x.overflow) return;
   x.par.for_n(capn, [&](uint32_t i) { tab[i] = 0; });
   x.par.sync();
@@ -482,7 +499,7 @@ TB_HD uint32_t count_sentences(DocCtx<P>& x, const Cps& c, uint32_t s, uint32_t 
 
 template <class P>
 TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, const Cps& c,
-                             const uint64_t* PH, const Words& w, int64_t* r) {
+                             const uint64_t* PH, const Words& w, int64_t* r, bool release_props = false) {
   const uint32_t C = c.n;
   const uint32_t* cp = c.cp;
   const uint32_t* prop = c.prop;
@@ -538,6 +555,9 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
             },
             &para_dup, &para_dup_b);
   x.stamp(PH_GR_LINES);
+  // the n-gram statistics below read words, bytes and offsets only: the property array's LDS
+  // (top of the slice) goes to their hash tables
+  if (release_props) x.release_hi();
   x.par.single([&]() {
     r[0] = span;
     r[1] = NPR + 1;
@@ -1144,8 +1164,15 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
   const uint32_t* off = c.off;
   const uint64_t* pw = x.pw;
 
-  for (int s = 0; s < st.n_steps; ++s) {
+  // Records are independent: GopherRepetition runs after the other steps so that its n-gram
+  // phase (the last user of the code point properties) can hand their LDS to its hash tables.
+  int n_gr = 0;
+  for (int s = 0; s < st.n_steps; ++s) n_gr += st.steps[s].kind == DK_GOPHER_REP;
+  int gr_seen = 0;
+  for (int so = 0; so < 2 * st.n_steps; ++so) {
+    const int s = so % st.n_steps;
     const DevStep& ds = st.steps[s];
+    if ((so < st.n_steps) == (ds.kind == DK_GOPHER_REP)) continue;
     int64_t* r = out.rec + (int64_t)ds.rec_prefix * out.ndocs + (int64_t)out.doc * ds.width;
     if (ds.kind == DK_GOPHER_QUALITY) {
       const DevStopSet& ss = plan.stops[ds.stop_set];
@@ -1183,7 +1210,8 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
       });
       x.stamp(PH_GQ);
     } else if (ds.kind == DK_GOPHER_REP) {
-      gopher_rep_record(x, ds, b, c, PH, w, r);
+      ++gr_seen;
+      gopher_rep_record(x, ds, b, c, PH, w, r, kHotProps && gr_seen == n_gr);
     } else if (ds.kind == DK_FINEWEB) {
       const auto mark = x.mark();
       uint32_t* nb = x.template alloc<uint32_t>(L.n + 1);

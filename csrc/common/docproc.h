@@ -637,25 +637,28 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     }
     x.stamp(PH_GR_TOP);
     if (ds.n_dup > 0) {
-      // per-n canonical-gram arrays and visited bitmaps (pointers kept in scratch). The bitmaps
-      // (W bits each) are allocated first so they stay in LDS even for long documents: the
-      // sequential greedy walk probes them once per step.
+      // One n at a time (its canonical-gram array, visited and repeated-position bitmaps and
+      // hash table are scratch for this n only, so they fit the LDS slice):
+      //   canonicalize the n-gram concatenations, mark repeated positions in R (p with
+      //   gc[p] != p, and their first occurrence gc[p]), then one lane runs the greedy walk.
+      // The walk only has to stop at repeated grams: at a gram that occurs once it would mark an
+      // id no other position has and advance by one, so it jumps from one set bit of R to the
+      // next instead (reference find_all_duplicate, utils/text.rs:241-259).
       const uint32_t SW = (W + 31) / 32 + 1;
-      uint32_t* sn_all = x.template alloc_hot<uint32_t>((uint64_t)SW * ds.n_dup);
-      uint64_t* gofs = x.template alloc_hot<uint64_t>(2 * kMaxNgramEntries);
-      if (x.overflow) return;
       for (int t = 0; t < ds.n_dup; ++t) {
         const uint32_t n = (uint32_t)ds.dup_n[t];
-        if (n == 0 || W < n) continue;
+        int64_t* rt = &r[rec_gr_fixed() + ds.n_top + t];
+        if (n == 0 || W < n) {
+          x.par.single([&]() { *rt = 0; });
+          continue;
+        }
         const uint32_t G = W - n + 1;
-        uint32_t* sn = sn_all + (size_t)t * SW;
-        uint32_t* gct = x.template alloc_hot<uint32_t>(G);
+        const auto m3 = x.mark();
+        uint32_t* sn = x.template alloc_hot<uint32_t>(2 * (uint64_t)SW);
+        uint32_t* R = sn + SW;
+        uint32_t* gc = x.template alloc_hot<uint32_t>(G);
         if (x.overflow) return;
-        x.par.single([&]() {
-          gofs[2 * t] = (uint64_t)(uintptr_t)gct;  // generic pointers (LDS or HBM)
-          gofs[2 * t + 1] = (uint64_t)(uintptr_t)sn;
-        });
-        x.par.for_n((G + 31) / 32 + 1, [&](uint32_t i) { sn[i] = 0; });
+        x.par.for_n(2 * SW, [&](uint32_t i) { sn[i] = 0; });
         canonicalize(
             x, G,
             [&](uint32_t p) {
@@ -680,25 +683,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
               }
               return true;
             },
-            gct);
-      }
-      x.par.sync();
-      const int ndup = ds.n_dup;
-      // The greedy walk only has to stop at *repeated* grams (canonical id shared with another
-      // position). At a gram that occurs once the walk marks its id as seen (an id no other
-      // position has) and advances by one, so those positions are skipped without bookkeeping:
-      // per n a bitmap R of repeated positions (p with gc[p] != p, and their first occurrence
-      // gc[p]) lets the walking lane jump from one repeated position to the next.
-      uint32_t* R_all = x.template alloc_hot<uint32_t>((uint64_t)SW * ndup);
-      if (x.overflow) return;
-      x.par.for_n(SW * (uint32_t)ndup, [&](uint32_t i) { R_all[i] = 0; });
-      x.par.sync();
-      for (int t = 0; t < ndup; ++t) {
-        const uint32_t n = (uint32_t)ds.dup_n[t];
-        if (n == 0 || W < n) continue;
-        const uint32_t G = W - n + 1;
-        const uint32_t* gc = (const uint32_t*)(uintptr_t)gofs[2 * t];
-        uint32_t* R = R_all + (size_t)t * SW;
+            gc);
         x.par.for_n(G, [&](uint32_t p) {
           const uint32_t g = gc[p];
           if (g != p) {
@@ -706,17 +691,9 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
             P::or32(&R[g >> 5], 1u << (g & 31));
           }
         });
-      }
-      x.par.sync();
-      x.par.for_n((uint32_t)ndup, [&](uint32_t t) {
-        const uint32_t n = (uint32_t)ds.dup_n[t];
-        int64_t rep = 0;
-        if (n > 0 && W >= n) {
-          const uint32_t G = W - n + 1;
+        x.par.sync();
+        x.par.single([&]() {
           const uint32_t nw = (G + 31) >> 5;
-          const uint32_t* gc = (const uint32_t*)(uintptr_t)gofs[2 * t];
-          uint32_t* sn = (uint32_t*)(uintptr_t)gofs[2 * t + 1];
-          const uint32_t* R = R_all + (size_t)t * SW;
           auto next_rep = [&](uint32_t from) -> uint32_t {  // first repeated position >= from, or G
             if (from >= G) return G;
             uint32_t wi = from >> 5;
@@ -728,6 +705,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
             const uint32_t q = (wi << 5) + (uint32_t)__builtin_ctz(bits);
             return q < G ? q : G;
           };
+          int64_t rep = 0;
           uint32_t idx = next_rep(0);
           while (idx < G) {
             const uint32_t g = gc[idx];
@@ -739,10 +717,11 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
               idx = next_rep(idx + 1);
             }
           }
-        }
-        r[rec_gr_fixed() + ds.n_top + t] = rep;
-      });
-      x.par.sync();
+          *rt = rep;
+        });
+        x.par.sync();
+        x.reset(m3);
+      }
       x.stamp(PH_GR_DUP);
     }
   }
@@ -1177,33 +1156,57 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
     if (ds.kind == DK_GOPHER_QUALITY) {
       const DevStopSet& ss = plan.stops[ds.stop_set];
       const UcdView ucd = x.ucd;
-      int64_t sum_chars = x.par.template sum<int64_t>(W, [&](uint32_t k) { return (int64_t)(w.ce[k] - w.cs[k]); });
-      int64_t alpha = x.par.template sum<int64_t>(W, [&](uint32_t k) { return (int64_t)w.alpha[k]; });
-      int64_t stop = x.par.template sum<int64_t>(W, [&](uint32_t k) {
-        return (int64_t)is_stop_word(ucd, ss, cp, prop, w.cs[k], w.ce[k]);
+      // Counts are packed two per 64-bit sum (each < 2^32: a document is < 4 GiB), so the seven
+      // statistics take one pass over the words, one over the code points and one over the lines.
+      auto lo32 = [](uint64_t v) { return (int64_t)(v & 0xFFFFFFFFull); };
+      auto hi32 = [](uint64_t v) { return (int64_t)(v >> 32); };
+      int64_t sum_chars = 0;
+      const uint64_t as = x.par.template sum<uint64_t>(W, [&](uint32_t k) {
+        const uint32_t a = w.cs[k], e = w.ce[k];
+        return ((uint64_t)(e - a) << 32) | ((uint64_t)w.alpha[k] << 16) |
+               (uint64_t)is_stop_word(ucd, ss, cp, prop, a, e);
       });
-      int64_t nhash = x.par.template sum<int64_t>(C, [&](uint32_t i) { return (int64_t)(cp[i] == '#'); });
-      int64_t nell = x.par.template sum<int64_t>(C, [&](uint32_t i) {
-        if (cp[i] == 0x2026) return (int64_t)1;
-        if (cp[i] != '.' || (i > 0 && cp[i - 1] == '.')) return (int64_t)0;
+      // fields: chars (bits 32..63, <= C), alphabetic words (16..31) and stop words (0..15), both
+      // <= W; documents with 2^16 words or more are counted field by field
+      int64_t alpha, stop;
+      if (W < 65536u) {
+        sum_chars = hi32(as);
+        alpha = (int64_t)((as >> 16) & 0xFFFFull);
+        stop = (int64_t)(as & 0xFFFFull);
+      } else {
+        sum_chars = x.par.template sum<int64_t>(W, [&](uint32_t k) { return (int64_t)(w.ce[k] - w.cs[k]); });
+        alpha = x.par.template sum<int64_t>(W, [&](uint32_t k) { return (int64_t)w.alpha[k]; });
+        stop = x.par.template sum<int64_t>(W, [&](uint32_t k) {
+          return (int64_t)is_stop_word(ucd, ss, cp, prop, w.cs[k], w.ce[k]);
+        });
+      }
+      const uint64_t he = x.par.template sum<uint64_t>(C, [&](uint32_t i) {
+        const uint32_t c0 = cp[i];
+        if (c0 == '#') return (uint64_t)1 << 32;
+        if (c0 == 0x2026) return (uint64_t)1;
+        if (c0 != '.' || (i > 0 && cp[i - 1] == '.')) return (uint64_t)0;
         uint32_t j = i;
         while (j < C && cp[j] == '.') ++j;
-        return (int64_t)((j - i) / 3);
+        return (uint64_t)((j - i) / 3);
       });
-      int64_t bullet = x.par.template sum<int64_t>(L.n, [&](uint32_t k) {
-        uint32_t j = L.ls[k];
-        while (j < L.le[k] && is_ws(prop[j])) ++j;
-        return (int64_t)(j < L.le[k] && (cp[j] == 0x2022 || cp[j] == '-'));
+      const int64_t nhash = hi32(he), nell = lo32(he);
+      const uint64_t be = x.par.template sum<uint64_t>(L.n, [&](uint32_t k) {
+        const uint32_t ls = L.ls[k], le = L.le[k];
+        uint32_t j = ls;
+        while (j < le && is_ws(prop[j])) ++j;
+        const uint64_t bul = (j < le && (cp[j] == 0x2022 || cp[j] == '-')) ? 1 : 0;
+        j = le;
+        while (j > ls && is_ws(prop[j - 1])) --j;
+        const uint32_t E = off[j], S = off[ls];
+        uint64_t ell = 0;
+        if (E - S >= 3) {
+          const bool dots = b[E - 3] == '.' && b[E - 2] == '.' && b[E - 1] == '.';
+          const bool uell = b[E - 3] == 0xE2 && b[E - 2] == 0x80 && b[E - 1] == 0xA6;
+          ell = (dots || uell) ? 1 : 0;
+        }
+        return (bul << 32) | ell;
       });
-      int64_t ell_lines = x.par.template sum<int64_t>(L.n, [&](uint32_t k) {
-        uint32_t j = L.le[k];
-        while (j > L.ls[k] && is_ws(prop[j - 1])) --j;
-        const uint32_t E = off[j], S = off[L.ls[k]];
-        if (E - S < 3) return (int64_t)0;
-        const bool dots = b[E - 3] == '.' && b[E - 2] == '.' && b[E - 1] == '.';
-        const bool uell = b[E - 3] == 0xE2 && b[E - 2] == 0x80 && b[E - 1] == 0xA6;
-        return (int64_t)(dots || uell);
-      });
+      const int64_t bullet = hi32(be), ell_lines = lo32(be);
       x.par.single([&]() {
         r[0] = W; r[1] = sum_chars; r[2] = nhash; r[3] = nell; r[4] = L.n;
         r[5] = bullet; r[6] = ell_lines; r[7] = alpha; r[8] = stop;

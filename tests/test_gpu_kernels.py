@@ -180,3 +180,21 @@ def test_langid_pipeline_vectors_and_head(host, corpus, runner_parts):
     assert np.array_equal(r2[:, 0], cpu)
     assert np.array_equal(r3[:, 0], cpu)
     assert np.array_equal(r1[:, 0], cpu)
+
+
+def test_device_run_is_deterministic(host, corpus, runner_parts):
+    """Run-twice check: records, flags, gate codes and rewritten texts are
+    bitwise identical across runs, whatever the wave scheduling and the LDS atomics order."""
+    _, _, plan, runner, _ = runner_parts
+    data, off = synth.pack(corpus)
+    a = runner.run(data, off)
+    b = runner.run(data, off)
+    for x, y in zip(a.stage_recs, b.stage_recs):
+        np.testing.assert_array_equal(x, y)
+    for i in a.c4_recs:
+        np.testing.assert_array_equal(a.c4_recs[i], b.c4_recs[i])
+    np.testing.assert_array_equal(a.flags, b.flags)
+    np.testing.assert_array_equal(a.dead, b.dead)
+    for v in a.versions:
+        np.testing.assert_array_equal(a.versions[v][0], b.versions[v][0])
+        np.testing.assert_array_equal(a.versions[v][1], b.versions[v][1])

@@ -246,3 +246,13 @@ def test_cli_run_and_worker(tmp_path, capsys):
     outs = [json.loads(l) for l in r.stdout.splitlines()]
     assert [next(iter(o)) for o in outs] == ["Success", "Filtered", "Success"]
     assert outs[1]["Filtered"]["document"]["id"] == "doc2_fr"
+
+
+def test_run_twice_is_byte_identical(corpus, tmp_path):
+    """Determinism: two runs over the same input write identical Parquet files."""
+    outs = []
+    for k in range(2):
+        o, e = str(tmp_path / f"o{k}.parquet"), str(tmp_path / f"e{k}.parquet")
+        run(RunConfig(corpus, o, e, DEFAULT_CFG, backend="emulate", unit_rows=700, threads=2, tokenizer_dir=TOK))
+        outs.append((open(o, "rb").read(), open(e, "rb").read()))
+    assert outs[0] == outs[1]

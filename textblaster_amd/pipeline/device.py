@@ -15,6 +15,7 @@ import numpy as np
 
 from .. import native
 from ..errors import DeviceError
+from ..utils import tracing
 from .plan import ExecPlan
 
 SCRATCH_ALIGN = 256
@@ -75,7 +76,8 @@ class PendingBatch:
         import time
 
         t0 = time.perf_counter()
-        self.event.synchronize()
+        with tracing.trace_range("tb.gpu_wait"):
+            self.event.synchronize()
         t1 = time.perf_counter()
         stage_recs = [r.numpy() if r is not None else None for r in self._stage_recs]
         c4_recs = {i: r.numpy() for i, r in self._c4_recs.items()}
@@ -338,8 +340,9 @@ class DeviceRunner:
         np.cumsum(per_doc, out=scratch_off[1:])
         maxlen = int(lens.max()) if ndocs else 0
         n_long = int(np.count_nonzero(lens > self.long_doc_bytes)) if self.long_doc_bytes > 0 else 0
-        (d_bytes, d_off, d_perm, d_soff), staged = self._stage_inputs(
-            slot, [data if len(data) else np.zeros(1, np.uint8), off, perm, scratch_off])
+        with tracing.trace_range("tb.stage_h2d"):
+            (d_bytes, d_off, d_perm, d_soff), staged = self._stage_inputs(
+                slot, [data if len(data) else np.zeros(1, np.uint8), off, perm, scratch_off])
         scratch = self._scratch_for(slot, int(scratch_off[-1]))
         pw, pw_n = self.k.pow_table(2 * maxlen + 64)
         flags = torch.zeros(ndocs, dtype=torch.int32, device=self.device)

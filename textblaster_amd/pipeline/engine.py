@@ -27,6 +27,7 @@ import numpy as np
 from .. import native
 from ..config.pipeline import PipelineConfig
 from ..errors import ConfigError, DeviceError, Unexpected
+from ..utils import tracing
 from .plan import ExecPlan, build_plan
 
 
@@ -312,7 +313,7 @@ class Engine:
         return self._cpu_engine
 
     def submit(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None, row_base: int = 0):
-        with self._submit_lock:  # the submitter thread and batch recovery may both submit
+        with self._submit_lock, tracing.trace_range("tb.submit"):  # submitter thread and recovery may both submit
             return self._submit(data, off, meta, row_base)
 
     def _submit(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None, row_base: int = 0):
@@ -332,6 +333,10 @@ class Engine:
         return _Submitted(data, off, meta, row_base, dev, t0)
 
     def finish(self, sub: "_Submitted") -> BatchResult:
+        with tracing.trace_range("tb.finish"):
+            return self._finish(sub)
+
+    def _finish(self, sub: "_Submitted") -> BatchResult:
         data, off, meta, row_base, t0 = sub.data, sub.off, sub.meta, sub.row_base, sub.t0
         ndocs = len(off) - 1
         md, mo, mv = meta if meta is not None else (None, None, None)
@@ -379,7 +384,8 @@ class Engine:
             self._run_cpu_steps(bs, 0, len(self.steps), ndocs, self.segmentation)
             timings["cpu_pipeline"] = time.perf_counter() - t1
         t2 = time.perf_counter()
-        result = self._collect(bs, ndocs, timings)
+        with tracing.trace_range("tb.assemble"):
+            result = self._collect(bs, ndocs, timings)
         if len(delegated):
             sub2 = self._process_subset_cpu(data, off, meta, delegated)
             result.kept += sub2.kept

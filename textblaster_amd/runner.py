@@ -46,7 +46,7 @@ from .errors import PipelineError, Unexpected
 from .io.parquet import (DocBatch, ParquetInputConfig, ParquetReader, ParquetWriter, build_output_table,
                          packed_to_string_array)
 from .parallel.dist import DistContext, shard_ranges
-from .utils import metrics
+from .utils import metrics, tracing
 
 log = logging.getLogger("textblaster_amd.runner")
 
@@ -151,7 +151,8 @@ class _UnitReader:
     def read(self, u: Unit) -> DocBatch:
         t0 = time.perf_counter()
         try:
-            return self._read(u)
+            with tracing.trace_range("tb.read"):
+                return self._read(u)
         finally:
             self.seconds += time.perf_counter() - t0
 
@@ -361,7 +362,8 @@ class _Writer:
                     kept = _sort_by_row(kept, np.concatenate([p.rows for p in res.kept]))
                 if len(res.excluded) > 1:
                     exc = _sort_by_row(exc, np.concatenate([p.rows for p in res.excluded]))
-                self.sink.write(unit, kept, exc, counts)
+                with tracing.trace_range("tb.write"):
+                    self.sink.write(unit, kept, exc, counts)
             except BaseException as e:  # noqa: BLE001
                 self.err.append(e)
             self.seconds += time.perf_counter() - t0

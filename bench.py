@@ -38,7 +38,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--docs-per-step", type=int, default=65536)
+    ap.add_argument("--docs-per-step", type=int, default=262144,
+                    help="documents per GPU per step (~290 MB of text: device batches sized for 288 GB HBM)")
     ap.add_argument("--mean-bytes", type=int, default=1024)
     ap.add_argument("--pool", type=int, default=16384, help="distinct synthetic docs per rank")
     ap.add_argument("--config", default=os.path.join(ROOT, "config", "bench_pipeline.yaml"))

@@ -76,9 +76,12 @@ TB_STAGE_KERNEL(k_stage_analyze_w4, __attribute__((amdgpu_waves_per_eu(4, 8))))
 TB_STAGE_KERNEL(k_stage_analyze_w5, __attribute__((amdgpu_waves_per_eu(5, 8))))
 TB_STAGE_KERNEL(k_stage_analyze_w6, __attribute__((amdgpu_waves_per_eu(6, 8))))
 
-// Long documents: one workgroup of kBlockThreads (4 waves) per document (BlockPar), launched
+// Long documents: one workgroup of kBlockThreads (8 waves by default) per document (BlockPar), launched
 // over the long prefix of the length-sorted permutation.
-constexpr int kBlockThreads = 256;
+#ifndef TB_BLOCK_THREADS
+#define TB_BLOCK_THREADS 512
+#endif
+constexpr int kBlockThreads = TB_BLOCK_THREADS;
 __shared__ __attribute__((aligned(16))) char g_block_xs[16 * (kBlockThreads / 64) + 64];
 
 __global__ __launch_bounds__(kBlockThreads) void k_stage_analyze_blk(

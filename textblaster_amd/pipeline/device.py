@@ -410,9 +410,10 @@ class DeviceRunner:
                 stage_recs_d[s] = rec
             c4_here = [i for i in self.plan.c4_steps if self.plan.steps[i].version_in == ver]
             for i in c4_here:
-                if c4_scratch is None:
-                    c4_scratch = self._scratch_for(slot, int(scratch_off[-1]), which="c4")
-                    keep.append(c4_scratch)
+                # The C4 pass reuses the stage arena: it starts after every stage kernel of its
+                # content version (it waits for the gate on the compute stream), and the stages of
+                # the next version start after its pass B (ready event).
+                c4_scratch = scratch
                 rec = torch.zeros(7 * ndocs, dtype=torch.int64, device=self.device)
                 src = torch.zeros(2 * ndocs, dtype=torch.int64, device=self.device)
                 new_off = torch.zeros(ndocs + 1, dtype=torch.int64, device=self.device)

@@ -54,6 +54,10 @@ class _Slot:
         self.scratch = None
         self.scratch_c4 = None
         self.h2d_done = None  # event: the pinned staging buffer may be rewritten after it
+        # per-slot streams (compute, language-id bag, long-document kernels, C4 wave / long):
+        # a batch's kernels only order against the batch that used the slot before it, so batch
+        # k+1 starts while batch k's tail (long documents, C4, FineWeb, D2H) still runs
+        self.main = self.s_lid = self.s_blk = self.s_c4 = self.s_c4blk = None
 
 
 class PendingBatch:
@@ -181,12 +185,25 @@ class DeviceRunner:
         self.slots = [_Slot() for _ in range(self.N_SLOTS)]
         self.h2d_stream = torch.cuda.Stream(self.device)
         self.d2h_stream = torch.cuda.Stream(self.device)
-        self.s_lid = torch.cuda.Stream(self.device)
-        self.s_blk = torch.cuda.Stream(self.device)
-        self.s_c4 = torch.cuda.Stream(self.device)
-        if os.environ.get("TB_SERIAL_STREAMS", "") not in ("", "0"):
-            # profiling aid: every kernel of a batch on the compute stream (exclusive durations)
-            self.s_lid = self.s_blk = self.s_c4 = torch.cuda.current_stream(self.device)
+        # The long-document workgroup kernels are the tail of every stage (few, long-lived
+        # workgroups): their stream gets the highest priority so they are dispatched before the
+        # wave kernels that run next to them (TB_BLK_PRIORITY=0 disables).
+        blk_prio = int(os.environ.get("TB_BLK_PRIORITY", "-1"))
+        serial = os.environ.get("TB_SERIAL_STREAMS", "") not in ("", "0")
+        for sl in self.slots:
+            if serial:
+                # profiling aid: every kernel on one stream (exclusive durations, no overlap)
+                sl.main = sl.s_lid = sl.s_blk = sl.s_c4 = sl.s_c4blk = torch.cuda.current_stream(self.device)
+                continue
+            sl.main = torch.cuda.Stream(self.device)
+            sl.s_lid = torch.cuda.Stream(self.device)
+            sl.s_blk = torch.cuda.Stream(self.device, priority=blk_prio)
+            sl.s_c4 = torch.cuda.Stream(self.device)
+            sl.s_c4blk = torch.cuda.Stream(self.device, priority=blk_prio)
+        # B^k for the hashes, shared read-only by both slots: allocated once (longer spans fall
+        # back to powmod61 in the kernels)
+        self.k.pow_table(1 << 22)
+        torch.cuda.synchronize(self.device)  # uploads and the table are complete before any slot stream reads them
         self.copy_threads = int(os.environ.get("TB_COPY_THREADS", "8"))
         self._next_slot = 0
         self._last_lid = None
@@ -328,6 +345,14 @@ class DeviceRunner:
         t0 = time.perf_counter()
         slot = self.slots[self._next_slot]
         self._next_slot = (self._next_slot + 1) % self.N_SLOTS
+        with torch.cuda.stream(slot.main):
+            return self._submit_on(slot, data, off, t0)
+
+    def _submit_on(self, slot: "_Slot", data: np.ndarray, off: np.ndarray, t0: float) -> PendingBatch:
+        import time
+
+        torch = self.torch
+        h = native.host()
         ndocs = len(off) - 1
         lens = np.diff(off)
         # longest first (coarse 16-byte buckets are enough for scheduling): a stable radix sort
@@ -344,6 +369,8 @@ class DeviceRunner:
             (d_bytes, d_off, d_perm, d_soff), staged = self._stage_inputs(
                 slot, [data if len(data) else np.zeros(1, np.uint8), off, perm, scratch_off])
         scratch = self._scratch_for(slot, int(scratch_off[-1]))
+        # grows (new tensor, on this slot's stream) only for documents over 2 MB; the batch keeps a
+        # reference to the table it used, so the other slot's kernels never see it freed
         pw, pw_n = self.k.pow_table(2 * maxlen + 64)
         flags = torch.zeros(ndocs, dtype=torch.int32, device=self.device)
         dead = torch.zeros(ndocs, dtype=torch.uint8, device=self.device) if self.gate_ts else None
@@ -352,7 +379,7 @@ class DeviceRunner:
         versions = {0: (d_bytes, d_off, len(data))}
         stage_recs_d: List = [None] * len(self.plan.stages)
         c4_recs_d = {}
-        keep = [staged, scratch]
+        keep = [staged, scratch, pw]
         # Independent work runs concurrently on side streams (events order the dependencies):
         #   language-id bag (s_lid) | long-doc workgroup kernels (s_blk) | wave kernels (main)
         #   | C4 pass A/B of the same content version (s_c4, own scratch arena)
@@ -376,21 +403,21 @@ class DeviceRunner:
                 ev_pre = self._record(main)  # rec / lid buffers zeroed
                 ev_lid = ev_blk = None
                 if lid_vec is not None:
-                    self.s_lid.wait_event(ev_pre)
-                    with torch.cuda.stream(self.s_lid):
+                    slot.s_lid.wait_event(ev_pre)
+                    with torch.cuda.stream(slot.s_lid):
                         self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec,
                                                lid_cnt, flags, self.lds_bytes_lid,
                                                self._prof_buf(ndocs, keep, f"langid{s}"))
-                        ev_lid = self._record(self.s_lid)
+                        ev_lid = self._record(slot.s_lid)
                 prof = self._prof_buf(ndocs, keep, f"stage{s}")
                 skip = dead if pass_idx > 0 else None
                 if n_long:
-                    self.s_blk.wait_event(ev_pre)
-                    with torch.cuda.stream(self.s_blk):
+                    slot.s_blk.wait_event(ev_pre)
+                    with torch.cuda.stream(slot.s_blk):
                         self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[:n_long], n_long,
                                                  ndocs, scratch, d_soff, pw, pw_n, rec, flags, lid_vec, lid_cnt,
                                                  self.lds_bytes_blk, prof, skip)
-                        ev_blk = self._record(self.s_blk)
+                        ev_blk = self._record(slot.s_blk)
                 if n_long < ndocs:
                     self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,
                                          scratch, d_soff, pw, pw_n, rec, flags,
@@ -419,22 +446,29 @@ class DeviceRunner:
                 new_off = torch.zeros(ndocs + 1, dtype=torch.int64, device=self.device)
                 cap = vlen + self.c4_growth * ndocs + 16  # device rewrites never grow more (kC4MaxGrowth)
                 out = torch.empty(cap, dtype=torch.uint8, device=self.device)
-                self.s_c4.wait_event(self._record(main))
-                self.s_c4.wait_event(ready[ver])
+                slot.s_c4.wait_event(self._record(main))
+                slot.s_c4.wait_event(ready[ver])
                 skip = dead if pass_idx > 0 else None
-                with torch.cuda.stream(self.s_c4):
-                    prof = self._prof_buf(ndocs, keep, f"c4_step{i}")
-                    if n_long:
+                prof = self._prof_buf(ndocs, keep, f"c4_step{i}")
+                ev_c4blk = None
+                if n_long:
+                    # long documents (workgroup kernel) next to the wave kernel: disjoint docs
+                    slot.s_c4blk.wait_event(self._record(slot.s_c4))
+                    with torch.cuda.stream(slot.s_c4blk):
                         self.k.c4_pass_a_blk(self.c4_ts[i], vb, vo, d_perm[:n_long], n_long, ndocs, c4_scratch,
                                              d_soff, pw, pw_n, rec, src, flags, self.lds_bytes_blk, prof, skip)
+                        ev_c4blk = self._record(slot.s_c4blk)
+                with torch.cuda.stream(slot.s_c4):
                     if n_long < ndocs:
                         self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm[n_long:], ndocs, c4_scratch, d_soff, pw,
                                          pw_n, rec, src, flags, self.lds_bytes_c4, prof, ndocs - n_long, skip)
+                    if ev_c4blk is not None:
+                        slot.s_c4.wait_event(ev_c4blk)
                     torch.cumsum(src.view(ndocs, 2)[:, 1], 0, out=new_off[1:])
                     self.k.c4_pass_b(vb, vo, ndocs, c4_scratch, d_soff, src, new_off, out)
                     if pass_idx in self.gate_ts:
                         self.k.gate(self.gate_ts[pass_idx], [rec], ndocs, flags, dead, pass_idx + 1, 0)
-                    ev = self._record(self.s_c4)
+                    ev = self._record(slot.s_c4)
                 pass_idx += 1
                 versions[ver + 1] = (out, new_off, cap)
                 ready[ver + 1] = ev

@@ -315,7 +315,10 @@ class Engine:
 
     def submit(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None, row_base: int = 0):
         with self._submit_lock, tracing.trace_range("tb.submit"):  # submitter thread and recovery may both submit
-            return self._submit(data, off, meta, row_base)
+            ts = time.perf_counter()
+            sub = self._submit(data, off, meta, row_base)
+            sub.submit_s = time.perf_counter() - ts
+            return sub
 
     def _submit(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None, row_base: int = 0):
         t0 = time.perf_counter()
@@ -341,13 +344,16 @@ class Engine:
         data, off, meta, row_base, t0 = sub.data, sub.off, sub.meta, sub.row_base, sub.t0
         ndocs = len(off) - 1
         md, mo, mv = meta if meta is not None else (None, None, None)
+        tf = time.perf_counter()
         bs = self.h.BatchState(data, off, md, mo, mv, self.nthreads)
-        timings: Dict[str, float] = {}
+        timings: Dict[str, float] = {"batch_state": time.perf_counter() - tf}
         delegated = np.zeros(0, dtype=np.int64)
         if sub.dev is not None:
+            tw = time.perf_counter()
             res = sub.dev.wait() if hasattr(sub.dev, "wait") else sub.dev
             timings.update(res.timings)
             t1 = time.perf_counter()
+            timings["wait_total"] = t1 - tw
             delegated = np.nonzero(res.flags)[0].astype(np.int64)
             if len(delegated):
                 bs.delegate(delegated)
@@ -397,6 +403,8 @@ class Engine:
             result.reasons.update(sub2.reasons)
             result.n_delegated = len(delegated)
         timings["assemble"] = time.perf_counter() - t2
+        timings["finish"] = time.perf_counter() - tf
+        timings["submit"] = sub.submit_s
         timings["total"] = time.perf_counter() - t0
         if row_base:
             for p in result.kept + result.excluded:
@@ -564,6 +572,7 @@ class _Submitted:
     row_base: int
     dev: object          # PendingBatch / DeviceResult / None (cpu)
     t0: float
+    submit_s: float = 0.0
 
 
 def _cuda_available() -> bool:

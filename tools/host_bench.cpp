@@ -72,15 +72,15 @@ int main(int argc, char** argv) {
   double best = 1e9;
   size_t meta_bytes = 0;
   int64_t kept = 0, excl = 0;
+  BatchState bs(ndocs, data.data(), off.data(), nullptr, nullptr, nullptr, 1);
+  int prefix = 0;
+  for (int s = 0; s < 3; ++s) {
+    bs.apply_records(st[s], s, rec.data() + (int64_t)prefix * ndocs, record_width(st[s]), -1);
+    prefix += record_width(st[s]);
+  }
+  std::vector<int64_t> k, e;
+  for (int64_t i = 0; i < ndocs; ++i) (bs.status()[i] == 0 ? k : e).push_back(i);
   for (int r = 0; r < reps; ++r) {
-    BatchState bs(ndocs, data.data(), off.data(), nullptr, nullptr, nullptr, 1);
-    int prefix = 0;
-    for (int s = 0; s < 3; ++s) {
-      bs.apply_records(st[s], s, rec.data() + (int64_t)prefix * ndocs, record_width(st[s]), -1);
-      prefix += record_width(st[s]);
-    }
-    std::vector<int64_t> k, e;
-    for (int64_t i = 0; i < ndocs; ++i) (bs.status()[i] == 0 ? k : e).push_back(i);
     const auto t0 = std::chrono::steady_clock::now();
     RawBuf td, md;
     std::vector<int64_t> to, mo;

@@ -35,7 +35,7 @@ extern __shared__ __attribute__((aligned(16))) char g_lds_arena[];
 
 template <class P = WavePar>
 __device__ __forceinline__ DocCtx<P> make_ctx(const DevTables& t, const uint64_t* pw, uint32_t pw_n,
-                                             char* scratch, const int64_t* scratch_off, int doc,
+                                             char* scratch, const int64_t* scratch_off, int doc, int k,
                                              uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
   DocCtx<P> x;
   x.prof = prof ? prof + (size_t)doc * kPhaseSlots : nullptr;
@@ -45,11 +45,20 @@ __device__ __forceinline__ DocCtx<P> make_ctx(const DevTables& t, const uint64_t
   x.ucd = UcdView{t.s1, t.s2, t.l1, t.l2};
   x.pw = pw;
   x.pw_n = pw_n;
-  x.scr = scratch + scratch_off[doc];
-  x.cap = (uint64_t)(scratch_off[doc + 1] - scratch_off[doc]);
+  // scratch slices are laid out in dispatch order (k = position in the launched permutation), so
+  // the waves resident at the same time work in one contiguous window of the arena
+  x.scr = scratch + scratch_off[k];
+  x.cap = (uint64_t)(scratch_off[k + 1] - scratch_off[k]);
   x.used = 0;
   x.flag = flags + doc;
   return x;
+}
+
+// C4 pass A leaves src[0] relative to the document's scratch slice (the convention the host
+// emulation shares); pass B copies straight out of the arena, so the leader makes it absolute.
+template <class P>
+__device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int64_t slice_begin) {
+  if (x.par.leader() && src[0] >= 0) src[0] += slice_begin;
 }
 
 // The stage kernel is register-bound (occupancy = waves/SIMD the VGPR budget allows). Variants
@@ -64,7 +73,7 @@ __device__ __forceinline__ DocCtx<P> make_ctx(const DevTables& t, const uint64_t
       uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead) {                         \
     const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;                                        \
     if (doc >= ndocs || (dead && dead[doc])) return;                                                  \
-    DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);   \
+    DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);   \
     const uint8_t* b = bytes + off[doc];                                                              \
     const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);                                           \
     StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, lid_vec, lid_cnt};                              \
@@ -93,7 +102,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_stage_analyze_blk(
   const int doc = perm[blockIdx.x];
   if (doc >= ndocs || (dead && dead[doc])) return;
   DocCtx<BlockPar<kBlockThreads>> x =
-      make_ctx<BlockPar<kBlockThreads>>(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);
+      make_ctx<BlockPar<kBlockThreads>>(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
   x.par.xs = g_block_xs;
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
@@ -110,7 +119,7 @@ __global__ __launch_bounds__(64) void k_langid_features(
     uint64_t* prof) {
   const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
   if (doc >= ndocs) return;
-  DocCtx<WavePar> x = make_ctx(tabs, nullptr, 0, scratch, scratch_off, doc, flags, lds_bytes, prof);
+  DocCtx<WavePar> x = make_ctx(tabs, nullptr, 0, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   x.stamp(PH_START);
@@ -126,10 +135,11 @@ __global__ __launch_bounds__(64) void k_c4_pass_a(
     uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead) {
   const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
   if (doc >= ndocs || (dead && dead[doc])) return;  // skipped: record zeros, rewritten length 0
-  DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);
+  DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2);
+  c4_src_absolute(x, src + (int64_t)doc * 2, scratch_off[blockIdx.x]);
 }
 
 __global__ __launch_bounds__(kBlockThreads) void k_c4_pass_a_blk(
@@ -140,11 +150,12 @@ __global__ __launch_bounds__(kBlockThreads) void k_c4_pass_a_blk(
   const int doc = perm[blockIdx.x];
   if (doc >= ndocs || (dead && dead[doc])) return;
   DocCtx<BlockPar<kBlockThreads>> x =
-      make_ctx<BlockPar<kBlockThreads>>(tabs, pw, pw_n, scratch, scratch_off, doc, flags, lds_bytes, prof);
+      make_ctx<BlockPar<kBlockThreads>>(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
   x.par.xs = g_block_xs;
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2);
+  c4_src_absolute(x, src + (int64_t)doc * 2, scratch_off[blockIdx.x]);
 }
 
 // C4 bad words (reference c4_filters.rs:431-441,516): does any list entry occur, case-folded,
@@ -230,7 +241,8 @@ __global__ __launch_bounds__(256) void k_c4_pass_b(const uint8_t* __restrict__ b
   if (doc >= ndocs) return;
   const int64_t len = new_off[doc + 1] - new_off[doc];
   const int64_t s = src[2 * doc];
-  const uint8_t* from = s < 0 ? bytes + off[doc] : (const uint8_t*)scratch + scratch_off[doc] + s;
+  (void)scratch_off;  // src holds absolute arena offsets (c4_src_absolute)
+  const uint8_t* from = s < 0 ? bytes + off[doc] : (const uint8_t*)scratch + s;
   uint8_t* to = out + new_off[doc];
   for (int64_t i = threadIdx.x; i < len; i += blockDim.x) to[i] = from[i];
 }

@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--segmentation", default="icu", help="CPU backend segmentation (icu|rules)")
     ap.add_argument("--threads", type=int, default=None)
     args = ap.parse_args()
+    if args.steps < 1 or args.warmup < 0 or args.docs_per_step < 1:
+        ap.error("--steps must be >= 1, --warmup >= 0 and --docs-per-step >= 1")
 
     import torch
 
@@ -91,8 +93,11 @@ def main():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     n_done = 0
+    tsum: dict = {}
     for res in eng.process_many(feed(args.steps, args.warmup)):
         counters += [res.n_docs, res.n_kept, res.n_excluded, len(res.error_rows)]
+        for k, v in res.timings.items():
+            tsum[k] = tsum.get(k, 0.0) + v
         n_done += 1
     assert n_done == args.steps
     if args.backend == "cuda":
@@ -132,6 +137,9 @@ def main():
             "errors": int(totals[3]),
             "bytes_per_sec": round(bytes_per_step * world * args.steps / elapsed_max, 1),
             "last_step_timings": {k: round(v, 5) for k, v in res.timings.items()},
+            # host seconds per phase averaged over the K timed steps (phases of consecutive
+            # steps overlap, so they do not add up to ms_per_step)
+            "mean_step_timings": {k: round(v / n_done, 5) for k, v in tsum.items()},
         }
         print(json.dumps(line), flush=True)
         dr = getattr(eng, "device_runner", None)

@@ -26,13 +26,19 @@ def main(d):
     c1c, c1g = g("c1_cpu"), g("c1_gpu")
     rows.append(("1. C4QualityFilter only", "1k-row Parquet, CLI path (incl. startup)",
                  c1f.get("cpu", {}).get("docs_per_sec"), c1f.get("cuda", {}).get("docs_per_sec")))
-    rows.append(("1. C4QualityFilter only", "65,536 ~1.1 KB docs/step, in memory",
+    def batch(r):
+        return f"{r[-1]['config']['global_batch']:,}" if r else "?"
+
+    rows.append(("1. C4QualityFilter only", f"{batch(c1g)} ~1.1 KB docs/step, in memory",
                  c1c and c1c[-1]["value"], c1g and c1g[-1]["value"]))
     c2c, c2g = g("c2_cpu"), g("c2_gpu")
-    rows.append(("2. C4 + GopherQuality + GopherRepetition", "10M ~1.1 KB docs (153 steps x 65,536)",
+    steps2 = c2g[-1]["steps"] if c2g else 0
+    rows.append(("2. C4 + GopherQuality + GopherRepetition",
+                 f"{steps2 * (c2g[-1]['config']['global_batch'] if c2g else 0) / 1e6:.1f}M ~1.1 KB docs "
+                 f"({steps2} steps x {batch(c2g)})",
                  c2c and c2c[-1]["value"], c2g and c2g[-1]["value"]))
     c3c, c3g = g("c3_cpu"), g("c3_gpu")
-    rows.append(("3. + LanguageDetection (bf16 MFMA head) + FineWeb", "65,536 ~1.1 KB docs/step (bench.py)",
+    rows.append(("3. + LanguageDetection (bf16 MFMA head) + FineWeb", f"{batch(c3g)} ~1.1 KB docs/step (bench.py)",
                  c3c and c3c[-1]["value"], c3g and c3g[-1]["value"]))
     c4 = g("c4_file")
     rows.append(("4. CommonCrawl-shaped Parquet, CLI path (1-GPU point)", "4M docs: read+decode+filter+write",

@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=0, help="timed bench steps at the end of the trace")
+    ap.add_argument("--copies", default=None, help="rocprofv3 memory_copy_trace.csv")
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     tot = defaultdict(lambda: [0, 0])
@@ -54,6 +55,34 @@ def main():
     nstage = sum(1 for _, _, k in iv if k.startswith("k_langid_features"))
     if nstage:
         print(f"steps in trace (langid launches): {nstage}; GPU busy per step: {busy / nstage / 1e6:.2f} ms")
+        # per-step timeline: a step starts at its langid launch; busy = union of kernel time until the next
+        starts = [a for a, _, k in iv if k.startswith("k_langid_features")]
+        print(f"\n{'step':>4} {'start ms':>10} {'gap ms':>8} {'busy ms':>8} {'kernels':>8}")
+        for j, s0 in enumerate(starts):
+            s1 = starts[j + 1] if j + 1 < len(starts) else iv[-1][1] + 1
+            seg = [(max(a, s0), min(b, s1)) for a, b, _ in iv if b > s0 and a < s1]
+            ub, ca, cb = 0, None, None
+            for a, b in sorted(seg):
+                if cb is None or a > cb:
+                    if cb is not None:
+                        ub += cb - ca
+                    ca, cb = a, b
+                else:
+                    cb = max(cb, b)
+            if cb is not None:
+                ub += cb - ca
+            print(f"{j:>4} {(s0 - starts[0]) / 1e6:>10.2f} {(s1 - s0) / 1e6:>8.2f} {ub / 1e6:>8.2f} {len(seg):>8}")
+    if args.copies:
+        rows = list(csv.DictReader(open(args.copies)))
+        agg = defaultdict(lambda: [0, 0, 0])
+        for r in rows:
+            d = r.get("Direction") or r.get("Operation") or "?"
+            agg[d][0] += 1
+            agg[d][1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            agg[d][2] += int(r.get("Bytes") or 0)
+        print(f"\n{'copy':<28} {'calls':>6} {'total ms':>10} {'MB':>10} {'GB/s':>8}")
+        for d, (c, ns, by) in sorted(agg.items()):
+            print(f"{d:<28} {c:>6} {ns / 1e6:>10.2f} {by / 1e6:>10.1f} {by / max(1, ns):>8.1f}")
 
 
 if __name__ == "__main__":

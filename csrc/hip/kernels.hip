@@ -110,8 +110,92 @@ __global__ __launch_bounds__(kBlockThreads) void k_stage_analyze_blk(
   analyze_stage<BlockPar<kBlockThreads>, false>(x, *stage, *plan, nullptr, b, n, out);
 }
 
-// Language-id n-gram bag of one document per wave (own kernel: its 33 accumulators per lane
-// would otherwise set the register budget, and so the occupancy, of the whole stage kernel).
+// Language-id n-gram bag, one wave per document, with cooperative row gathers.
+// Same result as langid_features_bytes (docproc.h; the fixed-point sum is exact, so the order
+// of the terms does not matter), different memory schedule: there every lane gathered the
+// whole 64-byte embedding row of each of its grams with 4 dwordx4 loads, so one load
+// instruction touched 64 distinct cache lines and the kernel was bound by the per-line rate of
+// the vector memory pipeline. Here each lane first derives the (up to 3) bucket ids of its byte
+// position; then, for each gram slot, 4 lanes share one row: lane (4*src + q) loads 16 bytes
+// (dims 8q..8q+7) of the row of lane j*16+src's gram, so an instruction covers 16 whole rows
+// (16 lines instead of 64) and each lane keeps 8 accumulators instead of 33.
+__device__ __forceinline__ void langid_features_coop(DocCtx<WavePar>& x, const uint8_t* b, uint32_t n,
+                                                     const uint16_t* __restrict__ emb, uint16_t* vec,
+                                                     int32_t* cnt_out) {
+  const UcdView ucd = x.ucd;
+  const auto mark = x.mark();
+  uint32_t* limb = x.template alloc_hot<uint32_t>(1);
+  if (x.overflow) return;
+  x.par.single([&]() { *limb = n; });
+  x.par.sync();
+  if (n > (uint32_t)kLidMaxCps) {
+    x.par.template compact<int>(
+        n, [&](uint32_t i, int&) { return utf8_is_lead(b[i]); },
+        [&](uint32_t i, uint32_t k, int&) { if (k == (uint32_t)kLidMaxCps) *limb = i; });
+    x.par.sync();
+  }
+  const uint32_t lim = *limb;
+  const uint32_t lane = x.par.lane, q = lane & 3u, src = lane >> 2;
+  int64_t acc[8];
+#pragma unroll
+  for (int d = 0; d < 8; ++d) acc[d] = 0;
+  uint32_t cnt = 0;
+  for (uint32_t base = 0; base <= lim; base += 64) {  // wave-uniform trip count
+    const uint32_t s = base + lane;
+    int32_t g[3] = {-1, -1, -1};
+    if (s <= lim && (s == lim || utf8_is_lead(b[s]))) {
+      const uint32_t l0 = s < lim ? lid_letter(ucd, b, n, s) : 0u;
+      const int64_t p1 = prev_lead(b, s);
+      const uint32_t lm1 = lid_letter(ucd, b, n, p1);
+      const uint32_t lm2 = p1 >= 0 ? lid_letter(ucd, b, n, prev_lead(b, p1)) : 0u;
+      int k = 0;
+      lid_grams_at(lm2, lm1, l0, true, true, [&](uint32_t bk) { g[k++] = (int32_t)bk; });
+      cnt += (uint32_t)k;
+    }
+    // |fixed(e)| < 2^21 and a lane adds at most 12 rows per chunk: int32 partials cannot overflow
+    int32_t part[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) part[d] = 0;
+#pragma unroll
+    for (int slot = 0; slot < 3; ++slot) {
+      if (__ballot(g[slot] >= 0) == 0) break;  // slots fill in order: later ones are empty too
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int32_t bk = __shfl(g[slot], j * 16 + (int)src);
+        if (bk >= 0) {
+          const uint4 w = *(const uint4*)(emb + (size_t)bk * kLidDim + q * 8u);
+          const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            part[2 * h] += lid_fixed((uint16_t)(ws[h] & 0xffffu));
+            part[2 * h + 1] += lid_fixed((uint16_t)(ws[h] >> 16));
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < 8; ++d) acc[d] += part[d];
+  }
+  // lanes with the same q hold partial sums of the same 8 dims
+#pragma unroll
+  for (int d = 0; d < 8; ++d)
+    for (int o = 4; o < 64; o <<= 1) acc[d] += pardetail::shfl_t(acc[d], (int)(lane ^ (uint32_t)o));
+  for (int o = 1; o < 64; o <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, o);
+  const int64_t K = cnt;
+  if (lane < 4) {
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      const float v = K ? (float)((double)acc[d] / (double)K / (double)kLidFixedScale) : 0.0f;
+      vec[q * 8u + d] = f32_to_bf16(v);
+    }
+  }
+  x.par.single([&]() { *cnt_out = (int32_t)K; });
+  x.par.sync();
+  x.reset(mark);
+}
+
+// Language-id n-gram bag of one document per wave (own kernel: it would otherwise set the
+// register budget, and so the occupancy, of the whole stage kernel).
 __global__ __launch_bounds__(64) void k_langid_features(
     const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off, const int32_t* __restrict__ perm,
     int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off, DevTables tabs,
@@ -123,7 +207,7 @@ __global__ __launch_bounds__(64) void k_langid_features(
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   x.stamp(PH_START);
-  langid_features_bytes(x, b, n, emb, lid_vec + (size_t)doc * kLidDim, lid_cnt + doc);
+  langid_features_coop(x, b, n, emb, lid_vec + (size_t)doc * kLidDim, lid_cnt + doc);
   x.stamp(PH_LID);
   if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
 }

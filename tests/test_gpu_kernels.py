@@ -182,6 +182,33 @@ def test_langid_pipeline_vectors_and_head(host, corpus, runner_parts):
     assert np.array_equal(r1[:, 0], cpu)
 
 
+def test_langid_bag_edge_cases_bit_exact(host, runner_parts):
+    """Cooperative-gather bag kernel (csrc/hip/kernels.hip langid_features_coop) vs. the host
+    featurizer on the cases its chunking has to get right: empty and letter-free documents, a
+    word cut at the 4096-code-point limit, multibyte letters across 64-byte chunk edges, and
+    long documents (which take the workgroup stage kernel but the wave bag kernel)."""
+    rng = np.random.default_rng(7)
+    words = ["blåbærgrød", "æblet", "Øresund", "straße", "the", "och", "kærlighed", "ÆØÅ", "naïve"]
+    texts = ["", "1234 5678 !!!", "a", "Å", " \n\n ", "x" * 5000, ("ø" * 4095) + "abc def",
+             ("z" * 4094) + " qq"]
+    for k in (63, 64, 65, 127, 128, 129, 4095, 4096, 4097, 9000):
+        t = " ".join(rng.choice(words) for _ in range(k // 4 + 1))
+        texts.append(t[:k])
+    _, _, _, runner, lid = runner_parts
+    data, off = synth.pack(texts)
+    runner.run(data, off)
+    vec_d, cnt_d = runner._last_lid
+    n = len(texts)
+    vec = vec_d.cpu().numpy().view(np.uint16).reshape(n, 32)
+    cnt = cnt_d.cpu().numpy()
+    m = lid.native()
+    for i, t in enumerate(texts):
+        c, v = m.featurize(t)
+        assert c == cnt[i], (i, c, cnt[i])
+        if c:
+            assert list(v) == list(vec[i]), i
+
+
 def test_device_run_is_deterministic(host, corpus, runner_parts):
     """Run-twice check: records, flags, gate codes and rewritten texts are
     bitwise identical across runs, whatever the wave scheduling and the LDS atomics order."""

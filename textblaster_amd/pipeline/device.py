@@ -173,11 +173,12 @@ class DeviceRunner:
         # documents longer than this run one workgroup (4 waves) each instead of one wave
         self.long_doc_bytes = int(os.environ.get("TB_LONG_DOC_BYTES", str(self.DEFAULT_LONG_DOC_BYTES)))
         self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", "32768"))
-        self.lds_bytes_lid = int(os.environ.get("TB_LDS_BYTES_LID", "9216"))  # 64x33 int32 partials + sums
-        if self.lds_bytes_lid < 9216:
+        # the cooperative-gather bag keeps its sums in registers; LDS holds only the cut offset
+        self.lds_bytes_lid = int(os.environ.get("TB_LDS_BYTES_LID", "256"))
+        if self.lds_bytes_lid < 16:
             # the language-id kernel runs concurrently with the stage kernels and must not touch
             # their HBM scratch arena: its working set has to fit its LDS slice
-            raise DeviceError("TB_LDS_BYTES_LID must be >= 9216")
+            raise DeviceError("TB_LDS_BYTES_LID must be >= 16")
         # TB_PHASE_PROF=1: per-document phase cycle counters (s_memtime stamps) for profiling
         self.phase_prof = os.environ.get("TB_PHASE_PROF", "") not in ("", "0")
         self.phase_totals: Dict[str, np.ndarray] = {}

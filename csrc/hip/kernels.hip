@@ -143,11 +143,23 @@ __device__ __forceinline__ void langid_features_coop(DocCtx<WavePar>& x, const u
   for (uint32_t base = 0; base <= lim; base += 64) {  // wave-uniform trip count
     const uint32_t s = base + lane;
     int32_t g[3] = {-1, -1, -1};
-    if (s <= lim && (s == lim || utf8_is_lead(b[s]))) {
-      const uint32_t l0 = s < lim ? lid_letter(ucd, b, n, s) : 0u;
-      const int64_t p1 = prev_lead(b, s);
-      const uint32_t lm1 = lid_letter(ucd, b, n, p1);
-      const uint32_t lm2 = p1 >= 0 ? lid_letter(ucd, b, n, prev_lead(b, p1)) : 0u;
+    // Each lane decodes only its own code point; the letters of the two previous code points
+    // come from the lanes holding their lead bytes when those are in this chunk (all but the
+    // first few lanes), so a position costs one decode + property lookup instead of three.
+    const bool act = s <= lim && (s == lim || utf8_is_lead(b[s]));
+    const uint32_t l0 = act && s < lim ? lid_letter(ucd, b, n, s) : 0u;
+    const int64_t p1 = act ? prev_lead(b, s) : -1;
+    const int src1 = p1 >= (int64_t)base ? (int)(p1 - base) : (int)lane;
+    const uint32_t lm1_sh = (uint32_t)__shfl((int)l0, src1);
+    const int64_t p2_sh = pardetail::shfl_t(p1, src1);
+    const int src2 = p1 >= (int64_t)base && p2_sh >= (int64_t)base ? (int)(p2_sh - base) : (int)lane;
+    const uint32_t lm2_sh = (uint32_t)__shfl((int)l0, src2);
+    if (act) {
+      const uint32_t lm1 = p1 >= (int64_t)base ? lm1_sh : lid_letter(ucd, b, n, p1);
+      uint32_t lm2;
+      if (p1 < 0) lm2 = 0u;
+      else if (p1 >= (int64_t)base && p2_sh >= (int64_t)base) lm2 = lm2_sh;
+      else lm2 = lid_letter(ucd, b, n, p1 >= (int64_t)base ? p2_sh : prev_lead(b, p1));
       int k = 0;
       lid_grams_at(lm2, lm1, l0, true, true, [&](uint32_t bk) { g[k++] = (int32_t)bk; });
       cnt += (uint32_t)k;

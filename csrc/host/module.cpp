@@ -11,6 +11,7 @@
 #include "../common/ucd_tables.inc"
 #include "filters.h"
 #include "html.h"
+#include "html_entities.inc"
 #include "json.h"
 #include "pipeline.h"
 #include "devplan_build.h"
@@ -230,6 +231,19 @@ PYBIND11_MODULE(_tbhost, m) {
     std::string out;
     if (!html_decode(s, out)) return s;
     return out;
+  });
+  m.def("html_entity_table", []() {
+    // The named-reference table (sorted bytewise) packed for the device decoder (csrc/hip/html.hip):
+    // (names, name offsets, UTF-8 values, value offsets).
+    std::string names, vals;
+    std::vector<int32_t> no{0}, vo{0};
+    for (int k = 0; k < kHtmlEntityCount; ++k) {
+      names += kHtmlEntities[k].name;
+      vals += kHtmlEntities[k].utf8;
+      no.push_back((int32_t)names.size());
+      vo.push_back((int32_t)vals.size());
+    }
+    return py::make_tuple(py::bytes(names), no, py::bytes(vals), vo);
   });
   m.def("html_decode_batch", [](py::array_t<uint8_t, py::array::c_style> data,
                                 py::array_t<int64_t, py::array::c_style> off, int nthreads) -> py::object {

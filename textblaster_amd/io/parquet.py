@@ -145,10 +145,12 @@ class DocBatch:
 class ParquetReader:
     """reference parquet_reader.rs:18-251"""
 
-    def __init__(self, config: ParquetInputConfig, html_threads: int = 8):
+    def __init__(self, config: ParquetInputConfig, html_threads: int = 8, html_decoder=None):
         # like the reference, construction does not touch the file; errors surface on first use
         self.config = config
         self.html_threads = html_threads
+        # optional device decoder (ops.html.HtmlDecoder, K17); default: the host C++ decoder
+        self.html_decoder = html_decoder
         self._pf_obj = None
 
     @property
@@ -222,8 +224,11 @@ class ParquetReader:
             ids = rb.column(cfg.id_column)
         n = rb.num_rows
         data, off, _ = string_column_buffers(text)
-        dec = native.host().html_decode_batch(np.ascontiguousarray(data), np.ascontiguousarray(off),
-                                              self.html_threads)
+        if self.html_decoder is not None:
+            dec = self.html_decoder.decode_host(data, off)
+        else:
+            dec = native.host().html_decode_batch(np.ascontiguousarray(data), np.ascontiguousarray(off),
+                                                  self.html_threads)
         if dec is not None:
             data, off = dec
         if not (pa.types.is_string(ids.type) or pa.types.is_large_string(ids.type)):

@@ -1,0 +1,78 @@
+"""K17: HTML character-reference decoding of a packed text batch on the GPU (csrc/hip/html.hip).
+
+The reference reader decodes every text cell with ``html_escape::decode_html_entities``
+(reference src/data/readers/parquet_reader.rs:177-179). The host reader does the same with the
+C++ decoder (csrc/host/html.cpp); this op is the device version of that decoder, bit-identical
+to it (tests/test_gpu_html.py), for batches that are already packed as UTF-8 bytes + int64
+offsets. Two launches, one wave per document: output sizes, then an on-device exclusive scan
+of the sizes and the scatter of the decoded bytes.
+"""
+from __future__ import annotations
+
+import threading
+from typing import Tuple
+
+import numpy as np
+
+from .. import native
+from .kernels import _check
+
+
+class HtmlDecoder:
+    """Holds the entity table on one device; ``decode`` works on device tensors."""
+
+    def __init__(self, device="cuda:0"):
+        import torch
+
+        self.torch = torch
+        self.device = torch.device(device)
+        self.lib = native.hip()
+        names, noff, vals, voff = native.host().html_entity_table()
+        dev = self.device
+        self.names = torch.from_numpy(np.frombuffer(names, dtype=np.uint8).copy()).to(dev)
+        self.name_off = torch.tensor(noff, dtype=torch.int32, device=dev)
+        self.vals = torch.from_numpy(np.frombuffer(vals, dtype=np.uint8).copy()).to(dev)
+        self.val_off = torch.tensor(voff, dtype=torch.int32, device=dev)
+        self.nent = len(noff) - 1
+        self._lock = threading.Lock()  # the reader pool calls decode_host from several threads
+
+    def _stream(self) -> int:
+        return self.torch.cuda.current_stream(self.device).cuda_stream
+
+    def decode(self, data, off) -> Tuple["torch.Tensor", "torch.Tensor"]:  # noqa: F821
+        """data: uint8[N], off: int64[B+1] (CUDA tensors) -> decoded (data', off')."""
+        torch = self.torch
+        if data.dtype != torch.uint8 or off.dtype != torch.int64 or off.dim() != 1:
+            raise ValueError("html decode needs uint8 data and int64 offsets")
+        if data.device != self.device or off.device != self.device:
+            raise ValueError("html decode inputs must live on " + str(self.device))
+        ndocs = off.numel() - 1
+        if ndocs <= 0:
+            return data[:0], off.clone()
+        data = data.contiguous()
+        off = off.contiguous()
+        lens = torch.empty(ndocs, dtype=torch.int64, device=self.device)
+        _check(self.lib.tb_html_sizes(self._stream(), data.data_ptr(), off.data_ptr(), ndocs, self.names.data_ptr(),
+                                      self.name_off.data_ptr(), self.vals.data_ptr(), self.val_off.data_ptr(),
+                                      self.nent, lens.data_ptr()), "tb_html_sizes")
+        out_off = torch.zeros(ndocs + 1, dtype=torch.int64, device=self.device)
+        torch.cumsum(lens, 0, out=out_off[1:])
+        total = int(out_off[-1].item())
+        out = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
+        _check(self.lib.tb_html_scatter(self._stream(), data.data_ptr(), off.data_ptr(), ndocs,
+                                        self.names.data_ptr(), self.name_off.data_ptr(), self.vals.data_ptr(),
+                                        self.val_off.data_ptr(), self.nent, out_off.data_ptr(), out.data_ptr()),
+               "tb_html_scatter")
+        return out[:total], out_off
+
+    def decode_host(self, data: np.ndarray, off: np.ndarray):
+        """Host arrays in, host arrays out (H2D, the two kernels, D2H); None when no document
+        changes, like the host decoder's html_decode_batch."""
+        torch = self.torch
+        if data.size == 0 or not np.any(data == ord("&")):
+            return None
+        with self._lock, torch.cuda.device(self.device):
+            d = torch.from_numpy(np.ascontiguousarray(data)).to(self.device)
+            o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.int64)).to(self.device)
+            od, oo = self.decode(d, o)
+            return od.cpu().numpy(), oo.cpu().numpy()

@@ -70,6 +70,7 @@ class RunConfig:
     compression: str = "none"
     tokenizer_dir: Optional[str] = None
     badwords_dir: Optional[str] = None
+    html_decode: str = "cpu"           # input HTML entity decoding: cpu (C++ host) | gpu (K17 kernels)
     metrics_port: Optional[int] = None
     progress_interval: float = 1.0
     tokenizer_file: Optional[str] = None
@@ -396,7 +397,16 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     cfg = cfg or load_pipeline_config(rc.pipeline_config)
     nsteps = len(cfg.pipeline)
     t_start = time.perf_counter()
-    reader = ParquetReader(ParquetInputConfig(rc.input_file, rc.text_column, rc.id_column))
+    html_dec = None
+    if rc.html_decode == "gpu":
+        if ctx.device is None:
+            raise PipelineError("--html-decode gpu needs a GPU rank")
+        from .ops.html import HtmlDecoder
+
+        html_dec = HtmlDecoder(ctx.device)
+    elif rc.html_decode != "cpu":
+        raise PipelineError(f"unknown html decode backend {rc.html_decode!r} (cpu | gpu)")
+    reader = ParquetReader(ParquetInputConfig(rc.input_file, rc.text_column, rc.id_column), html_decoder=html_dec)
     units = plan_units(reader, rc.unit_rows)
     if engine is None:
         backend = rc.backend

@@ -1,7 +1,7 @@
 // K17: HTML character-reference decoding of packed input text on the MI355X (the reference
 // reader runs html_escape::decode_html_entities on every text cell, parquet_reader.rs:177-179).
 // Same semantics as the host decoder csrc/host/html.cpp (the oracle its tests compare against):
-//   &name;  HTML5 named references (sorted table, binary search)
+//   &name;  HTML5 named references (hashed lookup table built by ops/html.py)
 //   &#DDD; / &#xHHH;  numeric references denoting a Unicode scalar value (NUL included)
 //   anything else is copied verbatim.
 //
@@ -24,6 +24,8 @@ struct HtmlTab {
   const uint8_t* vals;      // concatenated UTF-8 replacements
   const int32_t* val_off;   // [nent + 1]
   int32_t nent;
+  const int32_t* slots;     // open-addressing name hash -> entity index (-1 = empty), pow2 size
+  uint32_t slot_mask;
 };
 
 __device__ __forceinline__ bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
@@ -44,15 +46,22 @@ __device__ int cmp_name(const HtmlTab& t, int k, const uint8_t* s, uint32_t len)
   return la == len ? 0 : (la > len ? 1 : -1);
 }
 
+// FNV-1a of the name; must equal html_name_hash in textblaster_amd/ops/html.py (table builder)
+__device__ __forceinline__ uint32_t name_hash(const uint8_t* s, uint32_t len) {
+  uint32_t h = 2166136261u;
+  for (uint32_t i = 0; i < len; ++i) h = (h ^ s[i]) * 16777619u;
+  return h;
+}
+
+// One probe (plus linear probing on collisions) instead of a binary search of dependent loads.
 __device__ int find_entity(const HtmlTab& t, const uint8_t* s, uint32_t len) {
-  int lo = 0, hi = t.nent - 1;
-  while (lo <= hi) {
-    const int mid = (lo + hi) >> 1;
-    const int c = cmp_name(t, mid, s, len);
-    if (c == 0) return mid;
-    if (c < 0) lo = mid + 1; else hi = mid - 1;
+  uint32_t k = name_hash(s, len) & t.slot_mask;
+  for (;;) {
+    const int e = t.slots[k];
+    if (e < 0) return -1;
+    if (cmp_name(t, e, s, len) == 0) return e;
+    k = (k + 1) & t.slot_mask;
   }
-  return -1;
 }
 
 // Decides the reference starting at the '&' at b[p]. On a match: *end = one past its ';',
@@ -186,18 +195,19 @@ extern "C" {
 
 int tb_html_sizes(hipStream_t stream, const uint8_t* bytes, const int64_t* off, int32_t ndocs, const uint8_t* names,
                   const int32_t* name_off, const uint8_t* vals, const int32_t* val_off, int32_t nent,
-                  int64_t* out_len) {
+                  const int32_t* slots, uint32_t slot_mask, int64_t* out_len) {
   if (ndocs <= 0) return 0;
-  HtmlTab t{names, name_off, vals, val_off, nent};
+  HtmlTab t{names, name_off, vals, val_off, nent, slots, slot_mask};
   hipLaunchKernelGGL(k_html_sizes, dim3(ndocs), dim3(64), 0, stream, bytes, off, ndocs, t, out_len);
   return (int)hipGetLastError();
 }
 
 int tb_html_scatter(hipStream_t stream, const uint8_t* bytes, const int64_t* off, int32_t ndocs,
                     const uint8_t* names, const int32_t* name_off, const uint8_t* vals, const int32_t* val_off,
-                    int32_t nent, const int64_t* out_off, uint8_t* out) {
+                    int32_t nent, const int32_t* slots, uint32_t slot_mask, const int64_t* out_off,
+                    uint8_t* out) {
   if (ndocs <= 0) return 0;
-  HtmlTab t{names, name_off, vals, val_off, nent};
+  HtmlTab t{names, name_off, vals, val_off, nent, slots, slot_mask};
   hipLaunchKernelGGL(k_html_scatter, dim3(ndocs), dim3(64), 0, stream, bytes, off, ndocs, t, out_off, out);
   return (int)hipGetLastError();
 }

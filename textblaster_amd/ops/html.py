@@ -4,7 +4,8 @@ The reference reader decodes every text cell with ``html_escape::decode_html_ent
 (reference src/data/readers/parquet_reader.rs:177-179). The host reader does the same with the
 C++ decoder (csrc/host/html.cpp); this op is the device version of that decoder, bit-identical
 to it (tests/test_gpu_html.py), for batches that are already packed as UTF-8 bytes + int64
-offsets. Two launches, one wave per document: output sizes, then an on-device exclusive scan
+offsets. Named references are found with one hashed probe (table built here). Two
+launches, one wave per document: output sizes, then an on-device exclusive scan
 of the sizes and the scatter of the decoded bytes.
 """
 from __future__ import annotations
@@ -16,6 +17,29 @@ import numpy as np
 
 from .. import native
 from .kernels import _check
+
+
+def html_name_hash(name: bytes) -> int:
+    """FNV-1a, the hash the device lookup uses (csrc/hip/html.hip name_hash)."""
+    h = 2166136261
+    for c in name:
+        h = ((h ^ c) * 16777619) & 0xFFFFFFFF
+    return h
+
+
+def build_slots(names: bytes, noff) -> np.ndarray:
+    """Open-addressing table (load factor <= 1/4, linear probing) of entity indices by name."""
+    n = len(noff) - 1
+    size = 1
+    while size < 4 * n:
+        size <<= 1
+    slots = np.full(size, -1, dtype=np.int32)
+    for e in range(n):
+        k = html_name_hash(names[noff[e]:noff[e + 1]]) & (size - 1)
+        while slots[k] >= 0:
+            k = (k + 1) & (size - 1)
+        slots[k] = e
+    return slots
 
 
 class HtmlDecoder:
@@ -34,6 +58,10 @@ class HtmlDecoder:
         self.vals = torch.from_numpy(np.frombuffer(vals, dtype=np.uint8).copy()).to(dev)
         self.val_off = torch.tensor(voff, dtype=torch.int32, device=dev)
         self.nent = len(noff) - 1
+        slots = build_slots(names, noff)
+        assert (slots < 0).any(), "the device probe loop needs an empty slot"
+        self.slots = torch.from_numpy(slots).to(dev)
+        self.slot_mask = len(slots) - 1
         self._lock = threading.Lock()  # the reader pool calls decode_host from several threads
 
     def _stream(self) -> int:
@@ -54,14 +82,16 @@ class HtmlDecoder:
         lens = torch.empty(ndocs, dtype=torch.int64, device=self.device)
         _check(self.lib.tb_html_sizes(self._stream(), data.data_ptr(), off.data_ptr(), ndocs, self.names.data_ptr(),
                                       self.name_off.data_ptr(), self.vals.data_ptr(), self.val_off.data_ptr(),
-                                      self.nent, lens.data_ptr()), "tb_html_sizes")
+                                      self.nent, self.slots.data_ptr(), self.slot_mask, lens.data_ptr()),
+               "tb_html_sizes")
         out_off = torch.zeros(ndocs + 1, dtype=torch.int64, device=self.device)
         torch.cumsum(lens, 0, out=out_off[1:])
         total = int(out_off[-1].item())
         out = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
         _check(self.lib.tb_html_scatter(self._stream(), data.data_ptr(), off.data_ptr(), ndocs,
                                         self.names.data_ptr(), self.name_off.data_ptr(), self.vals.data_ptr(),
-                                        self.val_off.data_ptr(), self.nent, out_off.data_ptr(), out.data_ptr()),
+                                        self.val_off.data_ptr(), self.nent, self.slots.data_ptr(), self.slot_mask,
+                                        out_off.data_ptr(), out.data_ptr()),
                "tb_html_scatter")
         return out[:total], out_off
 

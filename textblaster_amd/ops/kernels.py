@@ -31,8 +31,8 @@ _SIGS = {
     "tb_c4_pass_b": [_P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "tb_langid_head": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I32, _P],
     "tb_pow_table": [_P, _P, _U32],
-    "tb_html_sizes": [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _P],
-    "tb_html_scatter": [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _P, _P],
+    "tb_html_sizes": [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _P, _U32, _P],
+    "tb_html_scatter": [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _P, _U32, _P, _P],
     "tb_abi_version": [],
     "tb_phase_slots": [],
     "tb_sizeof_plan": [],

@@ -128,7 +128,7 @@ class DeviceRunner:
     # 10 KB each costs no occupancy; the C4 kernel (7 waves/SIMD) only keeps per-line arrays there
     DEFAULT_LDS_BYTES = 10240
     DEFAULT_LDS_BYTES_C4 = 2048
-    DEFAULT_LONG_DOC_BYTES = 4096
+    DEFAULT_LONG_DOC_BYTES = 8192
     DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; sweep: tools/occ_sweep.sh)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None):
@@ -172,7 +172,7 @@ class DeviceRunner:
         self.stage_waves = int(os.environ.get("TB_STAGE_WAVES", str(self.DEFAULT_STAGE_WAVES)))
         # documents longer than this run one workgroup (4 waves) each instead of one wave
         self.long_doc_bytes = int(os.environ.get("TB_LONG_DOC_BYTES", str(self.DEFAULT_LONG_DOC_BYTES)))
-        self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", "32768"))
+        self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", "65536"))
         # the cooperative-gather bag keeps its sums in registers; LDS holds only the cut offset
         self.lds_bytes_lid = int(os.environ.get("TB_LDS_BYTES_LID", "256"))
         if self.lds_bytes_lid < 16:

@@ -256,3 +256,23 @@ def test_run_twice_is_byte_identical(corpus, tmp_path):
         run(RunConfig(corpus, o, e, DEFAULT_CFG, backend="emulate", unit_rows=700, threads=2, tokenizer_dir=TOK))
         outs.append((open(o, "rb").read(), open(e, "rb").read()))
     assert outs[0] == outs[1]
+
+
+def test_html_decode_backend_is_validated(tmp_path):
+    """`run --html-decode` accepts cpu | gpu only; an unknown value is a PipelineError (the GPU
+    decoder itself is covered by tests/test_gpu_html.py)."""
+    import pytest as _pytest
+
+    from textblaster_amd.data_model import TextDocument as _Doc
+    from textblaster_amd.errors import PipelineError
+    from textblaster_amd.io.parquet import ParquetWriter as _W
+    from textblaster_amd.runner import RunConfig as _RC, run as _run
+
+    inp = str(tmp_path / "in.parquet")
+    w = _W(inp)
+    w.write_batch([_Doc("a", "x &amp; y", "s")])
+    w.close()
+    cfg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "config", "bench_pipeline.yaml")
+    with _pytest.raises(PipelineError):
+        _run(_RC(inp, str(tmp_path / "o.parquet"), str(tmp_path / "e.parquet"), cfg, backend="cpu",
+                 html_decode="bogus"))

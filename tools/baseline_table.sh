@@ -23,7 +23,7 @@ run c1_file 300 python tools/e2e_bench.py --docs 1000 --row-group 1000 --unit-ro
     --backend cpu --backend cuda --out /tmp/tb_c1
 run c1_cpu 300 python bench.py --config $C/c4_only.yaml --backend cpu --steps 5 --warmup 1
 run c1_gpu 300 python bench.py --config $C/c4_only.yaml --steps 20 --warmup 3
-# 2. C4 + GopherQuality + GopherRepetition, 10M ~1 KB docs (153 x 65,536)
+# 2. C4 + GopherQuality + GopherRepetition, >= 10M ~1 KB docs (153 steps x the bench batch, 262,144 docs)
 run c2_gpu 600 python bench.py --config $C/c4_gopher.yaml --steps 153 --warmup 3
 run c2_cpu 300 python bench.py --config $C/c4_gopher.yaml --backend cpu --steps 3 --warmup 1
 # 3. + LanguageDetectionFilter (bench.py default config)

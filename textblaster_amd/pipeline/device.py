@@ -173,6 +173,11 @@ class DeviceRunner:
         # documents longer than this run one workgroup (4 waves) each instead of one wave
         self.long_doc_bytes = int(os.environ.get("TB_LONG_DOC_BYTES", str(self.DEFAULT_LONG_DOC_BYTES)))
         self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", "65536"))
+        if not 0 <= self.lds_bytes_blk <= 131072:
+            # the workgroup kernels also hold static LDS (cross-wave exchange buffers): a 160 KB
+            # dynamic slice does not fit the CU's 160 KB and the launch fails with
+            # HSA_STATUS_ERROR_INVALID_ALLOCATION (measured), so cap it here
+            raise DeviceError("TB_LDS_BYTES_BLK must be in [0, 131072]")
         # the cooperative-gather bag keeps its sums in registers; LDS holds only the cut offset
         self.lds_bytes_lid = int(os.environ.get("TB_LDS_BYTES_LID", "256"))
         if self.lds_bytes_lid < 16:

@@ -47,8 +47,20 @@ def main():
     ap.add_argument("--segmentation", default="icu", help="CPU backend segmentation (icu|rules)")
     ap.add_argument("--threads", type=int, default=None)
     args = ap.parse_args()
-    if args.steps < 1 or args.warmup < 0 or args.docs_per_step < 1:
-        ap.error("--steps must be >= 1, --warmup >= 0 and --docs-per-step >= 1")
+    if args.steps < 1 or args.warmup < 0 or args.docs_per_step < 1 or args.gpus < 1:
+        ap.error("--steps must be >= 1, --warmup >= 0, --docs-per-step >= 1 and --gpus >= 1")
+
+    from textblaster_amd.parallel import launch
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: start torch.distributed.run as a child before any HIP call
+        if args.backend == "cuda":
+            have = launch.visible_gpu_count()
+            if have < args.gpus:
+                print(f"bench.py: --gpus {args.gpus} requested but only {have} GPU(s) are visible",
+                      file=sys.stderr)
+                sys.exit(2)
+        sys.exit(launch.spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
 
     import torch
 
@@ -57,6 +69,15 @@ def main():
     from textblaster_amd.pipeline.engine import Engine
     from textblaster_amd.utils import synth
 
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
+        sys.exit(2)
+    if args.backend == "cuda":
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} requested but only {have} GPU(s) are visible", file=sys.stderr)
+            sys.exit(2)
     ctx = dist.init_from_env(backend="nccl" if args.backend == "cuda" else "gloo")
     rank, world = ctx.rank, ctx.world_size
     device = f"cuda:{ctx.local_rank}" if args.backend == "cuda" else None
@@ -94,11 +115,20 @@ def main():
     t0 = time.perf_counter()
     n_done = 0
     tsum: dict = {}
+    ar1 = None
     for res in eng.process_many(feed(args.steps, args.warmup)):
-        counters += [res.n_docs, res.n_kept, res.n_excluded, len(res.error_rows)]
+        step = np.asarray([res.n_docs, res.n_kept, res.n_excluded, len(res.error_rows)], dtype=np.int64)
+        counters += step
+        # AR1 once per step: the global counter vector (what rank 0's /metrics serves), reduced
+        # over RCCL while the next step runs; waited one step later
+        if ar1 is not None:
+            ar1.wait()
+        ar1 = ctx.all_reduce_sum_async(step)
         for k, v in res.timings.items():
             tsum[k] = tsum.get(k, 0.0) + v
         n_done += 1
+    if ar1 is not None:
+        ar1.wait()
     assert n_done == args.steps
     if args.backend == "cuda":
         torch.cuda.synchronize()
@@ -113,7 +143,7 @@ def main():
             "metric": METRIC,
             "value": round(value, 1),
             "unit": "docs/s",
-            "n_gpus": world if args.backend == "cuda" else 0,
+            "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1000 * elapsed_max / args.steps, 3),

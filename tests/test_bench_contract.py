@@ -58,6 +58,30 @@ def test_bench_two_ranks_contract():
     _check(line, 2, 1, 2)
 
 
+def test_bench_spawns_ranks_itself():
+    """``bench.py --gpus N`` without an outer launcher starts N ranks (gloo here) as a child
+    torch.distributed.run and reports the whole job."""
+    line = _run([sys.executable, "bench.py", "--gpus", "3", "--steps", "2", "--warmup", "1"] + ARGS,
+                {"TB_MASTER_PORT": str(_free_port())})
+    _check(line, 2, 1, 3)
+    assert line["n_gpus"] == 3
+
+
+def test_bench_refuses_missing_gpus():
+    """More GPUs than visible fails loudly instead of silently running one rank."""
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="0")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert p.returncode != 0 and "--gpus 2" in p.stderr
+
+
+def test_bench_world_mismatch_fails():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1"] + ARGS, cwd=ROOT,
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr
+
+
 def test_bench_rejects_zero_steps():
     p = subprocess.run([sys.executable, "bench.py", "--steps", "0"] + ARGS, cwd=ROOT, capture_output=True,
                        text=True, timeout=300)

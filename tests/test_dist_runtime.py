@@ -1,0 +1,174 @@
+"""Multi-rank runtime pieces on the CPU (gloo): byte-level Parquet concatenation, the live
+counter heartbeat (AR1 while ranks own unequal work) and rank-failure detection, the
+``run --gpus N`` launcher, and resume after an injected rank failure."""
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.parquet as pq
+import pytest
+
+from textblaster_amd.io import pqconcat
+from textblaster_amd.parallel.launch import free_port, strip_flag
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOK = os.path.join(REPO, "tests", "fixtures", "tokenizers")
+DEFAULT_CFG = os.path.join(REPO, "config", "pipeline_config.yaml")
+
+
+def test_pqconcat_roundtrip(tmp_path):
+    rng = np.random.default_rng(0)
+    sch = pa.schema([("id", pa.string()), ("text", pa.string()), ("v", pa.int64()), ("m", pa.string())])
+    paths, tabs = [], []
+    for k, n in enumerate([0, 3, 1000, 17, 40000]):
+        t = pa.table({"id": [f"d{k}-{i}" for i in range(n)],
+                      "text": ["x" * int(rng.integers(0, 60)) + str(i % 7) for i in range(n)],
+                      "v": pa.array(rng.integers(0, 5, n)),
+                      "m": [None if i % 3 else "{}" for i in range(n)]}, schema=sch)
+        p = str(tmp_path / f"p{k}.parquet")
+        pq.write_table(t, p, row_group_size=15000, compression="snappy" if k % 2 else "none")
+        paths.append(p)
+        tabs.append(t)
+    out = str(tmp_path / "all.parquet")
+    assert pqconcat.concat(paths, out) == 41020
+    got = pq.read_table(out)
+    assert got.equals(pa.concat_tables(tabs))
+    md = pq.ParquetFile(out).metadata
+    assert md.num_rows == 41020
+    assert md.num_row_groups == sum(pq.ParquetFile(p).metadata.num_row_groups for p in paths)
+    # statistics survive (offsets shifted, the rest of the footer verbatim)
+    assert md.row_group(md.num_row_groups - 1).column(0).statistics.max == "d4-39999"
+
+
+def test_pqconcat_rejects_schema_mismatch(tmp_path):
+    a, b = str(tmp_path / "a.parquet"), str(tmp_path / "b.parquet")
+    pq.write_table(pa.table({"x": [1]}), a)
+    pq.write_table(pa.table({"y": [1]}), b)
+    with pytest.raises(pqconcat.ThriftError, match="schema differs"):
+        pqconcat.concat([a, b], str(tmp_path / "c.parquet"))
+
+
+def test_thrift_compact_codec_roundtrip(tmp_path):
+    p = str(tmp_path / "z.parquet")
+    pq.write_table(pa.table({"a": list(range(100)), "b": [str(i) for i in range(100)]}), p)
+    size, start, fmd = pqconcat.read_footer(p)
+    with open(p, "rb") as f:
+        f.seek(start)
+        raw = f.read(size - 8 - start)
+    assert pqconcat.encode_struct(fmd) == raw
+
+
+def test_strip_flag():
+    assert strip_flag(["run", "--gpus", "4", "-i", "x", "--gpus=2"], "--gpus") == ["run", "-i", "x"]
+
+
+_HB_WORKER = r'''
+import os, sys, time
+import numpy as np
+import torch.distributed as td
+sys.path.insert(0, os.environ["REPO"])
+from textblaster_amd.parallel import dist
+from textblaster_amd.parallel.heartbeat import Heartbeat, RankFailure
+ctx = dist.init_from_env(backend="gloo")
+seen = []
+hb = Heartbeat(ctx, 2, interval=0.05, on_global=lambda v: seen.append(v.copy()))
+n = 3 + 4 * ctx.rank            # unequal work per rank
+for i in range(n):
+    hb.update([i + 1, 10 * (i + 1)])
+    time.sleep(0.03)
+    if os.environ.get("DIE") == str(ctx.rank) and i == 1:
+        os._exit(9)
+try:
+    g = hb.finish([n, 10 * n])
+except RankFailure as e:
+    print("RANKFAIL", ctx.rank, flush=True)
+    os._exit(3)
+print("GLOBAL", ctx.rank, int(g[0]), int(g[1]), len(seen) > 0, flush=True)
+ctx.destroy()
+'''
+
+
+def _spawn_hb(tmp_path, extra_env=None):
+    script = tmp_path / "hb.py"
+    script.write_text(_HB_WORKER)
+    env = dict(os.environ, REPO=REPO, TB_HEARTBEAT_TIMEOUT="20", TB_COLLECTIVE_TIMEOUT="30", **(extra_env or {}))
+    # plain processes (no torch.distributed.run agent, which would kill the survivors itself)
+    port = free_port()
+    procs = []
+    for r in range(2):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=e, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=120)
+        outs.append((p.returncode, o, e))
+    return outs
+
+
+def test_heartbeat_global_counts_unequal_work(tmp_path):
+    outs = _spawn_hb(tmp_path)
+    for rc, o, e in outs:
+        assert rc == 0, e[-2000:]
+        # rank 0 did 3 units, rank 1 did 7: the final global vector is the sum
+        assert "GLOBAL" in o and " 10 100 True" in o, o
+
+
+def test_heartbeat_detects_dead_rank(tmp_path):
+    t0 = time.time()
+    outs = _spawn_hb(tmp_path, {"DIE": "1"})
+    assert outs[1][0] == 9
+    assert outs[0][0] == 3 and "RANKFAIL 0" in outs[0][1], outs[0]
+    assert time.time() - t0 < 100
+
+
+def _corpus(tmp_path):
+    from textblaster_amd.data_model import TextDocument
+    from textblaster_amd.io.parquet import ParquetWriter
+    from textblaster_amd.utils import synth
+
+    texts = synth.make_corpus(2000, 600, seed=11)
+    p = str(tmp_path / "in.parquet")
+    w = ParquetWriter(p)
+    w.write_batch([TextDocument(f"r{i}", t, "syn", metadata={"i": str(i)} if i % 2 else {})
+                   for i, t in enumerate(texts)])
+    w.close()
+    return p
+
+
+def _cli(tmp_path, inp, tag, *extra, ok=True):
+    out, exc = str(tmp_path / f"{tag}.o.parquet"), str(tmp_path / f"{tag}.e.parquet")
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="2", TB_MASTER_PORT=str(free_port()),
+               TB_HEARTBEAT_TIMEOUT="30")
+    cmd = [sys.executable, "-m", "textblaster_amd", "run", "-i", inp, "-o", out, "-e", exc, "-c", DEFAULT_CFG,
+           "--cpu", "--unit-rows", "250", "--tokenizer-dir", TOK, "--log-dir", str(tmp_path / "log")] + list(extra)
+    r = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
+    if ok:
+        assert r.returncode == 0, r.stderr[-3000:]
+    return r, out, exc
+
+
+def test_run_gpus_flag_spawns_ranks_and_merges_in_order(tmp_path):
+    inp = _corpus(tmp_path)
+    _, o1, e1 = _cli(tmp_path, inp, "one")
+    r, o4, e4 = _cli(tmp_path, inp, "four", "--gpus", "4")
+    assert "Ranks: 4 (cpu)" in r.stdout and "Documents Read: 2000" in r.stdout
+    assert pq.read_table(o4).equals(pq.read_table(o1)) and pq.read_table(e4).equals(pq.read_table(e1))
+    # one row group per unit: the parts were concatenated, not re-encoded into new groups
+    assert pq.ParquetFile(o4).metadata.num_row_groups == 8
+
+
+def test_rank_failure_then_resume(tmp_path):
+    inp = _corpus(tmp_path)
+    _, o1, e1 = _cli(tmp_path, inp, "ref")
+    work = str(tmp_path / "work")
+    r, _, _ = _cli(tmp_path, inp, "ft", "--gpus", "2", "--work-dir", work, "--fault-inject", "rank@2:1", ok=False)
+    assert r.returncode != 0
+    done = [l for n in os.listdir(work) if n.startswith("manifest") for l in open(os.path.join(work, n))]
+    assert 0 < len(done) < 8
+    r2, o2, e2 = _cli(tmp_path, inp, "ft", "--gpus", "2", "--work-dir", work, "--resume")
+    assert "resumed" in r2.stdout
+    assert pq.read_table(o2).equals(pq.read_table(o1)) and pq.read_table(e2).equals(pq.read_table(e1))

@@ -20,7 +20,6 @@ import argparse
 import json
 import logging
 import os
-import subprocess
 import sys
 import time
 from typing import List, Optional
@@ -107,7 +106,7 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("--tokenizer-dir", default=None, help="local dir holding <name>/tokenizer.json")
         p.add_argument("--tokenizer-file", default=None, help="tokenizer.json used by every TokenCounter step")
         p.add_argument("--langid-model", default=None, help="language-id weights (.npz); default: bundled model")
-        p.add_argument("--fault-inject", default=None, help="debug: kernel@N or oom@N (fail the N-th batch once)")
+        p.add_argument("--fault-inject", default=None, help="debug: kernel@N or oom@N (fail the N-th batch once), rank@N[:R] (rank R dies after N units)")
         p.add_argument("--badwords-dir", default=None, help="dir holding the C4 bad-words lists (<lang> files)")
         p.add_argument("--html-decode", choices=("cpu", "gpu"), default="cpu",
                        help="decode HTML entities of the input text on the host (default) or the GPU")
@@ -141,49 +140,37 @@ def validate_config_cmd(path: str) -> int:
 
 
 def _visible_gpus() -> int:
-    try:
-        import torch
+    from .parallel.launch import visible_gpu_count
 
-        return torch.cuda.device_count()
-    except Exception:  # noqa: BLE001
-        return 0
+    return visible_gpu_count()
 
 
 def _relaunch_distributed(n: int, argv: List[str]) -> int:
     """Start ``n`` ranks via torch.distributed.run as a child process (never exec)."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr=127.0.0.1", f"--master-port={os.environ.get('TB_MASTER_PORT', '29517')}",
-           "-m", "textblaster_amd"] + argv
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.call(cmd, env=env)
+    from .parallel.launch import spawn_ranks
+
+    return spawn_ranks(n, ["-m", "textblaster_amd"] + argv)
 
 
 def run_cmd(args, argv: List[str]) -> int:
     from .errors import PipelineError
     from .parallel import dist
+    from .parallel.heartbeat import RankFailure
     from .runner import RunConfig, run
 
     under_launcher = "WORLD_SIZE" in os.environ
     if args.backend == "cpu":
-        ngpu = 0
+        ngpu = args.gpus or 0       # CPU ranks (gloo) when --gpus is given with --cpu
     else:
         ngpu = args.gpus if args.gpus is not None else _visible_gpus()
     if not under_launcher and ngpu > 1:
+        from .parallel.launch import strip_flag
+
+        if args.backend != "cpu" and args.gpus is not None and _visible_gpus() < ngpu:
+            print(f"Error: --gpus {ngpu} requested but only {_visible_gpus()} GPU(s) are visible", file=sys.stderr)
+            return 2
         # strip --gpus so the children do not relaunch
-        child = []
-        skip = False
-        for a in argv:
-            if skip:
-                skip = False
-                continue
-            if a == "--gpus":
-                skip = True
-                continue
-            if a.startswith("--gpus="):
-                continue
-            child.append(a)
-        return _relaunch_distributed(ngpu, child)
+        return _relaunch_distributed(ngpu, strip_flag(strip_flag(argv, "--gpus"), "--devices"))
 
     backend = args.backend
     if backend == "auto":
@@ -208,6 +195,12 @@ def run_cmd(args, argv: List[str]) -> int:
         html_decode=args.html_decode, metrics_port=args.metrics_port, tokenizer_file=args.tokenizer_file, fault_inject=args.fault_inject)
     try:
         stats = run(rc, ctx)
+    except RankFailure as e:
+        # a peer is gone: collective teardown could block on it, so leave right away
+        log.error("Run failed: %s", e)
+        print(f"Error: {e}", file=sys.stderr, flush=True)
+        logging.shutdown()
+        os._exit(3)
     except PipelineError as e:
         log.error("Run failed: %s", e)
         print(f"Error: {e}", file=sys.stderr)

@@ -63,6 +63,15 @@ class DistContext:
         td.all_reduce(t, op=td.ReduceOp.SUM)
         return t.cpu().numpy()
 
+    def all_reduce_sum_async(self, arr) -> "PendingReduce":
+        """Non-blocking all_reduce(SUM) of a small int64 vector (AR1); ``.wait()`` returns it."""
+        a = np.asarray(arr, dtype=np.int64)
+        if not self.initialized:
+            return PendingReduce(None, a.copy())
+        _, td = self._torch()
+        t = self._tensor(a)
+        return PendingReduce(td.all_reduce(t, op=td.ReduceOp.SUM, async_op=True), t)
+
     def all_reduce_max(self, x: float) -> float:
         if not self.initialized:
             return float(x)
@@ -88,6 +97,19 @@ class DistContext:
             self.backend = None
 
 
+class PendingReduce:
+    def __init__(self, work, tensor):
+        self.work = work
+        self.tensor = tensor
+
+    def wait(self) -> np.ndarray:
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+            self.tensor = self.tensor.cpu().numpy()
+        return self.tensor
+
+
 def init_from_env(backend: str = "nccl") -> DistContext:
     """Initialise from torchrun's env (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,8 +124,11 @@ def init_from_env(backend: str = "nccl") -> DistContext:
     if world > 1:
         import torch.distributed as td
 
+        import datetime
+
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        kwargs = {}
+        # a dead or hung peer turns into an error after this long instead of a silent hang
+        kwargs = {"timeout": datetime.timedelta(seconds=float(os.environ.get("TB_COLLECTIVE_TIMEOUT", "600")))}
         if backend == "nccl":
             import torch
 

@@ -17,11 +17,15 @@ Outputs
   * single rank, no checkpointing: rows stream straight into ``output_file`` / ``excluded_file``;
   * otherwise every unit writes ``<work_dir>/parts/u<unit>.{kept,excluded}.parquet`` and appends a
     line to ``<work_dir>/manifest.rank<r>.jsonl`` once both files are closed. ``resume=True``
-    skips units already in a manifest. After a barrier rank 0 concatenates the parts in unit
-    order into the two final files (row order = input order) and removes the work dir unless
+    skips units already in a manifest. At the end the parts are concatenated in unit order
+    (row order = input order) into the two final files *without re-encoding*: every rank
+    copies its own parts' column-chunk bytes at an offset from an all-gather of sizes (AG1),
+    rank 0 writes the rewritten footers (io/pqconcat.py); the work dir is removed unless
     ``keep_parts``.
-  Counters (docs, kept, excluded, errors, per-step filtered) are all-reduced over RCCL (AR1);
-  rank 0 reports the global view and serves it on the metrics endpoint.
+  Counters (docs, kept, excluded, errors, per-step filtered) are all-reduced while the job
+  runs by a heartbeat thread (parallel/heartbeat.py; it also turns a dead peer into a
+  non-zero exit) and once more over RCCL at the end (AR1); rank 0 serves the global view on
+  the metrics endpoint.
 """
 from __future__ import annotations
 
@@ -46,6 +50,7 @@ from .errors import PipelineError, Unexpected
 from .io.parquet import (DocBatch, ParquetInputConfig, ParquetReader, ParquetWriter, build_output_table,
                          packed_to_string_array)
 from .parallel.dist import DistContext, shard_ranges
+from .parallel.heartbeat import Heartbeat
 from .utils import metrics, tracing
 
 log = logging.getLogger("textblaster_amd.runner")
@@ -243,18 +248,74 @@ def read_manifests(work_dir: str) -> Dict[int, Dict]:
     return done
 
 
-def merge_parts(work_dir: str, n_units: int, rc: RunConfig) -> None:
+def merge_parts(work_dir: str, my_units: List[int], rc: RunConfig, ctx: Optional[DistContext] = None) -> None:
+    """Concatenates the part files into the two final files without re-encoding them
+    (io/pqconcat.py). Every rank copies the parts of its own (contiguous) unit range at an
+    offset from an all-gather of body sizes (AG1); rank 0 then writes the footers. Row order
+    is unit order = input order."""
+    from .io import pqconcat
+
+    ctx = ctx or DistContext()
+    rank, world = ctx.rank, ctx.world_size
     parts = os.path.join(work_dir, "parts")
-    for kind, path in (("kept", rc.output_file), ("excluded", rc.excluded_file)):
-        w = ParquetWriter(path, rc.compression)
-        for u in range(n_units):
-            p = os.path.join(parts, f"u{u:07d}.{kind}.parquet")
+    outs = (("kept", rc.output_file), ("excluded", rc.excluded_file))
+    lays = []
+    for kind, _ in outs:
+        paths = [os.path.join(parts, f"u{u:07d}.{kind}.parquet") for u in my_units]
+        for p in paths:
             if not os.path.exists(p):
                 raise Unexpected(f"missing part file {p}; rerun with --resume")
-            pf = pq.ParquetFile(p)
-            for i in range(pf.num_row_groups):
-                w.write_table(pf.read_row_group(i))
-        w.close()
+        lays.append(pqconcat.part_layout(paths))
+    sizes = ctx.all_gather_counts([lay.body_bytes for lay in lays])          # AG1: [world, 2]
+    if rank == 0:
+        for _, path in outs:
+            d = os.path.dirname(os.path.abspath(path))
+            os.makedirs(d, exist_ok=True)
+            os.close(os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644))
+    ctx.barrier()
+    for k, ((kind, path), lay) in enumerate(zip(outs, lays)):
+        base = 4 + int(sizes[:rank, k].sum())
+        fd = os.open(path, os.O_WRONLY)
+        try:
+            pqconcat.write_bodies(fd, lay, base)
+        finally:
+            os.close(fd)
+        for rg in lay.row_groups:
+            pqconcat.shift_row_group(rg, base)
+        rec = [[1, pqconcat.T_LIST, (pqconcat.T_STRUCT, lay.row_groups)],
+               [2, pqconcat.T_I64, lay.num_rows],
+               [3, pqconcat.T_BINARY, pqconcat.encode_struct(lay.template) if lay.template else b""]]
+        with open(os.path.join(work_dir, f"footer.{kind}.rank{rank}.bin"), "wb") as f:
+            f.write(pqconcat.encode_struct(rec))
+    ctx.barrier()
+    if rank == 0:
+        for k, (kind, path) in enumerate(outs):
+            rgs, rows, template, schema = [], 0, None, None
+            for r in range(world):
+                with open(os.path.join(work_dir, f"footer.{kind}.rank{r}.bin"), "rb") as f:
+                    rec = pqconcat.decode_struct(f.read())
+                fields = {fid: v for fid, _, v in rec}
+                rgs += fields[1][1]
+                rows += fields[2]
+                if fields[3]:
+                    t = pqconcat.decode_struct(fields[3])
+                    sch = pqconcat.encode_struct([x for x in t if x[0] == pqconcat.FMD_SCHEMA])
+                    if template is None:
+                        template, schema = t, sch
+                    elif sch != schema:
+                        raise Unexpected(f"rank {r} wrote {kind} parts with a different schema")
+            fd = os.open(path, os.O_WRONLY)
+            try:
+                if template is None:       # no unit anywhere: a valid empty file
+                    os.close(fd)
+                    fd = -1
+                    ParquetWriter(path, rc.compression).close()
+                else:
+                    pqconcat.finish(fd, 4 + int(sizes[:, k].sum()), template, rgs, rows)
+            finally:
+                if fd >= 0:
+                    os.close(fd)
+    ctx.barrier()
 
 
 # ---------------------------------------------------------------------------------------------
@@ -397,6 +458,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     cfg = cfg or load_pipeline_config(rc.pipeline_config)
     nsteps = len(cfg.pipeline)
     t_start = time.perf_counter()
+    rank_fault = _parse_rank_fault(rc.fault_inject, world)
     html_dec = None
     if rc.html_decode == "gpu":
         if ctx.device is None:
@@ -413,7 +475,8 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
         device = ctx.device if backend in ("cuda", "auto") else None
         engine = Engine(cfg, backend=backend, device=device, nthreads=rc.threads, segmentation=rc.segmentation,
                         tokenizer_dir=rc.tokenizer_dir, badwords_dir=rc.badwords_dir,
-                        tokenizer_file=rc.tokenizer_file, fault_inject=rc.fault_inject)
+                        tokenizer_file=rc.tokenizer_file,
+                        fault_inject=None if rank_fault is not None else rc.fault_inject)
     use_parts = world > 1 or rc.checkpoint or rc.resume
     work_dir = rc.work_dir or (rc.output_file + ".work")
     done: Dict[int, Dict] = {}
@@ -461,6 +524,9 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     log.info("rank %d/%d: %d units (%d already done), backend=%s", rank, world, len(mine), len(mine) - len(todo),
              engine.backend)
 
+    hb = Heartbeat(ctx, len(local.vector(nsteps)), interval=rc.progress_interval,
+                   on_global=_publish_global if rank == 0 else None)
+    hb.update(local.vector(nsteps))
     sink = _PartSink(rc, work_dir, rank) if use_parts else _DirectSink(rc)
     writer = _Writer(sink)
     ureader = _UnitReader(reader)
@@ -497,6 +563,13 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
                 local.step_filtered[i] += int(c)
             local.units += 1
             _update_metrics(cfg, res, batch, counts, step_counts, dt)
+            hb.update(local.vector(nsteps))
+            hb.check()
+            if rank_fault is not None and rank_fault[1] == rank and local.units == rank_fault[0]:
+                log.error("rank %d: injected rank failure after %d unit(s) (--fault-inject rank@...)", rank,
+                          local.units)
+                logging.shutdown()
+                os._exit(17)
             now = time.perf_counter()
             if now - last_report >= rc.progress_interval:
                 speed = (local.docs - last_docs) / (now - last_report)
@@ -505,6 +578,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
                 last_report, last_docs = now, local.docs
     finally:
         writer.close()
+    hb.finish(local.vector(nsteps))
     phase = {"read": ureader.seconds, "write": writer.seconds, "main_loop": time.perf_counter() - t_loop}
     log.info("rank %d phases: %s", rank, {k: round(v, 3) for k, v in phase.items()})
     elapsed = time.perf_counter() - t_start
@@ -516,15 +590,30 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     stats.phase_seconds = phase
     if use_parts:
         ctx.barrier()
-        if rank == 0:
-            merge_parts(work_dir, len(units), rc)
-            if not rc.keep_parts:
-                shutil.rmtree(work_dir, ignore_errors=True)
+        t_merge = time.perf_counter()
+        merge_parts(work_dir, [u.index for u in mine], rc, ctx)
+        phase["merge"] = time.perf_counter() - t_merge
+        if rank == 0 and not rc.keep_parts:
+            shutil.rmtree(work_dir, ignore_errors=True)
         ctx.barrier()
     stats.seconds = ctx.all_reduce_max(time.perf_counter() - t_start)
     if rank == 0:
         metrics.set_global_counts(stats.docs, stats.kept, stats.excluded, stats.errors)
     return stats
+
+
+def _publish_global(v: np.ndarray) -> None:
+    metrics.set_global_counts(int(v[0]), int(v[1]), int(v[2]), int(v[3]))
+
+
+def _parse_rank_fault(spec: Optional[str], world: int) -> Optional[Tuple[int, int]]:
+    """``rank@N[:R]``: rank R (default: the last rank) dies after its N-th unit (debug)."""
+    if not spec or not spec.startswith("rank@"):
+        return None
+    at, _, r = spec[5:].partition(":")
+    if not at.isdigit() or (r and not r.isdigit()):
+        raise PipelineError(f"bad fault injection spec {spec!r} (expected rank@N or rank@N:R)")
+    return int(at), int(r) if r else world - 1
 
 
 def _update_metrics(cfg, res, batch, counts, step_counts, dt) -> None:

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-2 opening GPU session: tests + smoke, bench, serialized kernel profile + phase cycles,
+# PMC passes on the tuned kernels. Every step time-limited; first failure ends the script.
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+bash tools/gpu_check.sh || exit $?
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.log 2>&1 || { echo "bench failed rc=$?"; tail -20 gpurun_out/bench.log; exit 1; }
+tail -2 gpurun_out/bench.log
+bash tools/prof_current.sh || exit 1
+TB_PROF_STEPS=2 bash tools/profile_pmc.sh || exit 1

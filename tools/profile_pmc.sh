@@ -15,8 +15,9 @@ run_pass() {
   return $rc
 }
 run_pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU &&
-run_pass mem SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM TCC_HIT_sum TCC_MISS_sum &&
-run_pass hbm FETCH_SIZE SQ_INSTS_VALU SQ_INSTS_BRANCH
+run_pass mem SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum &&
+run_pass hbm FETCH_SIZE SQ_INSTS_VALU SQ_INSTS_BRANCH &&
+run_pass wr WRITE_SIZE SQ_INSTS_VMEM_WR
 rc=$?
 find "$OUT" -name "*counter_collection*.csv" | head
 exit $rc

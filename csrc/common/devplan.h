@@ -47,6 +47,7 @@ struct DevStopSet {
   int32_t idx[kStopTableSize];
   int32_t off[kMaxStopWords + 1];  // byte offsets into blob
   int32_t n;
+  int32_t max_len;  // longest entry in bytes: a word of more code points cannot match
   uint8_t blob[kStopBlobBytes];
 };
 

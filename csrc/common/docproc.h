@@ -2,10 +2,11 @@
 // (SeqPar). Everything a filter needs is derived from one decode + segmentation per content
 // version, with exact (byte-verified) duplicate detection:
 //
-//   decode          UTF-8 -> code points + packed properties              (reference: chars())
-//   prefix_hash     PH[i] = H(bytes[0..i)), so any substring hash is O(1)
+//   decode          UTF-8 -> code point byte offsets + 16-bit properties  (reference: chars())
+//   prefix_hash8    PH8[k] = H(bytes[0..8k)): any substring hash is <= 14 Horner steps + 1 power
 //   words           UAX#29 word segments, trimmed, kept iff they contain a non-PUNCTUATION,
-//                   non-whitespace char                 (reference utils/text.rs:103-181)
+//                   non-whitespace char; break bitmask + one fused scan/compaction pass
+//                                                       (reference utils/text.rs:103-181)
 //   canonicalize    smallest index with an equal element (hash table + byte verification)
 //   gopher_quality / gopher_repetition / fineweb / c4 / langid features  (reference filters)
 //
@@ -24,7 +25,7 @@ namespace tb {
 // Phase ids for DocCtx::stamp (profiling only).
 enum : int {
   PH_START = 0, PH_DECODE, PH_DICT, PH_PREFIX_HASH, PH_WORDS, PH_LINES, PH_GQ, PH_GR_LINES, PH_GR_WORDS,
-  PH_GR_TOP, PH_GR_DUP, PH_FW, PH_LID,
+  PH_GR_TOP, PH_GR_DUP, PH_FW, PH_LID, PH_GR_DUP_WALK, PH_GR_DUP_CANON, PH_GR_TOP_CANON,
   PH_C4_LOREM = 16, PH_C4_DECODE, PH_C4_LINES, PH_C4_CITE, PH_C4_WORDS, PH_C4_CODES, PH_C4_JOIN, PH_C4_SENT,
   kPhaseSlots = 32
 };
@@ -35,16 +36,71 @@ enum : uint32_t {
   DOC_OVERFLOW = 2,
 };
 
+// Code points of a text: byte offsets and compact properties. The code point values themselves
+// are not stored: ASCII tests read the lead byte (b[off[i]], equal to the code point below 0x80
+// and >= 0xC0 otherwise), the rest re-decode from the bytes.
+//
+// Compact property layout (16 bits): the UCD word bits 0..13 and 15 (WB class, SB class, WS,
+// ALPHA, PUNCT, EXTPICT, DIGIT, CASED) unchanged; bit 14 carries CASE_IGN (bit 16 of the full
+// word). P_DICT is consumed while decoding (decode() reports it) and not kept.
+constexpr uint32_t P16_CASE_IGN = 1u << 14;
+TB_HD uint16_t compact_prop(uint32_t p) {
+  return (uint16_t)((p & 0xBFFFu) | ((p & P_CASE_IGN) ? P16_CASE_IGN : 0u));
+}
+
+// Per-code-point arrays. Texts under 64 KiB keep one packed u32 per code point (byte offset in
+// the low half, compact properties in the high half: 4 bytes, one load); longer ones (workgroup
+// path) keep a u32 offset array and a u16 property array. The accessors below hide the layout
+// (the choice is uniform per document, so the branch is a scalar one).
+struct PropArr {
+  const uint32_t* ent = nullptr;
+  const uint16_t* p16 = nullptr;
+  TB_HD uint32_t operator[](uint32_t i) const { return ent ? (ent[i] >> 16) : (uint32_t)p16[i]; }
+  TB_HD PropArr operator+(uint32_t s) const { return PropArr{ent ? ent + s : nullptr, ent ? nullptr : p16 + s}; }
+};
+struct OffArr {
+  const uint32_t* ent = nullptr;
+  const uint32_t* o32 = nullptr;
+  TB_HD uint32_t operator[](uint32_t i) const { return ent ? (ent[i] & 0xFFFFu) : o32[i]; }
+};
+
 struct Cps {
   uint32_t n = 0;
-  uint32_t* off = nullptr;   // [n+1] byte offset of each code point (off[n] = byte length)
-  uint32_t* cp = nullptr;    // [n]
-  uint32_t* prop = nullptr;  // [n]
+  uint32_t* ent = nullptr;    // packed [n+1] (texts < 64 KiB) ...
+  uint32_t* off = nullptr;    // ... or [n+1] byte offsets (off[n] = byte length)
+  uint16_t* prop = nullptr;   //     and [n+1] compact properties
+  const uint8_t* b = nullptr; // the text
+  uint32_t nb = 0;            // its byte length
+  TB_HD PropArr props() const { return PropArr{ent, prop}; }
+  TB_HD OffArr offs() const { return OffArr{ent, off}; }
+  TB_HD uint32_t o(uint32_t i) const { return ent ? (ent[i] & 0xFFFFu) : off[i]; }
+  TB_HD uint32_t p(uint32_t i) const { return ent ? (ent[i] >> 16) : (uint32_t)prop[i]; }
+  TB_HD uint8_t lead(uint32_t i) const { return b[o(i)]; }
+  TB_HD uint32_t cp(uint32_t i) const {
+    int len;
+    return utf8_decode(b, o(i), nb, &len);
+  }
 };
 
 struct CpsAcc {  // accessor for the UAX#29 rule templates over a sub-range
-  const uint32_t* prop;
-  TB_HD uint32_t p(int i) const { return prop[i]; }
+  PropArr prop;
+  TB_HD uint32_t p(int i) const { return prop[(uint32_t)i]; }
+};
+
+// Prefix hashes of a text kept at every 8th byte only (PH8[k] = H(b[0..8k)), PHn = H(b)): a
+// prefix at any position is at most 7 Horner steps away, so the table costs 1 byte per text byte
+// (LDS-resident for typical documents) instead of 8.
+struct PHView {
+  const uint64_t* ph8 = nullptr;
+  uint64_t phn = 0;
+  const uint8_t* b = nullptr;
+  uint32_t n = 0;
+  TB_HD uint64_t at(uint32_t x) const {
+    if (x >= n) return phn;
+    uint64_t h = ph8[x >> 3];
+    for (uint32_t j = x & ~7u; j < x; ++j) h = hash_push(h, b[j]);
+    return h;
+  }
 };
 
 struct Words {
@@ -72,8 +128,10 @@ template <class P>
 struct DocCtx {
   P par;
   UcdView ucd;
-  const uint64_t* pw = nullptr;  // pw[k] = B^k
+  const uint64_t* pw = nullptr;  // pw[k] = B^k, k <= pw_n; followed by ipw
+  const uint64_t* ipw = nullptr; // ipw[k] = B^-k, k <= pw_n
   uint32_t pw_n = 0;
+  const uint32_t* asc = nullptr; // UCD properties of code points < 128 (LDS copy), or null
   char* scr = nullptr;       // global (HBM) scratch arena of this document
   uint64_t cap = 0;
   uint64_t used = 0;
@@ -147,62 +205,109 @@ struct DocCtx {
     if (flag) P::or32(flag, f);  // atomic: kernels of different steps may run concurrently
   }
   TB_HD uint64_t powb(uint32_t k) const { return k <= pw_n ? pw[k] : powmod61(kHashBase, k); }
+  TB_HD uint64_t ipowb(uint32_t k) const { return (ipw && k <= pw_n) ? ipw[k] : powmod61(kHashBaseInv, k); }
+  // `count` elements from the bottom of the LDS slice, or nullptr when they do not fit
+  template <class T>
+  TB_HD T* try_lds(uint64_t count) {
+    if (!lds) return nullptr;
+    const uint64_t a = (lused + 15u) & ~15u;
+    const uint64_t e = a + count * sizeof(T);
+    if (e + lhi > lcap) return nullptr;
+    lused = (uint32_t)e;
+    return (T*)(lds + a);
+  }
 };
-
-TB_HD uint64_t sub_hash(const uint64_t* PH, const uint64_t* pw, uint32_t a, uint32_t b) {
-  uint64_t x = mulmod61(PH[a], pw[b - a]);
-  return PH[b] >= x ? PH[b] - x : PH[b] + kM61 - x;
-}
 
 TB_HD bool is_ws(uint32_t p) { return (p & P_WS) != 0; }
 TB_HD constexpr int rec_gr_fixed() { return 7; }
 
 // ---------------------------------------------------------------------------------------------
 template <class P>
-TB_HD Cps decode(DocCtx<P>& x, const uint8_t* b, uint32_t n, bool hot_props = false) {
+TB_HD Cps decode(DocCtx<P>& x, const uint8_t* b, uint32_t n, bool hot = false, uint32_t* dict = nullptr) {
   Cps c;
-  // prop[] is read by every rule evaluation (UAX#29 look-around, trims, classes): with
-  // hot_props it goes to the LDS slice when the document is small enough
-  c.prop = hot_props ? x.template alloc_hot_hi<uint32_t>(n + 1) : x.template alloc<uint32_t>(n + 1);
-  c.off = x.template alloc<uint32_t>(n + 1);
-  c.cp = x.template alloc<uint32_t>(n + 1);
+  c.b = b;
+  c.nb = n;
+  // read by every later pass (rule look-around, trims, spans): with `hot` they go to the top of
+  // the LDS slice when the document is small enough (released before the n-gram statistics)
+  const bool packed = n < 65536u;
+  if (packed) {
+    c.ent = hot ? x.template alloc_hot_hi<uint32_t>(n + 1) : x.template alloc<uint32_t>(n + 1);
+  } else {
+    c.prop = hot ? x.template alloc_hot_hi<uint16_t>(n + 1) : x.template alloc<uint16_t>(n + 1);
+    c.off = hot ? x.template alloc_hot_hi<uint32_t>(n + 1) : x.template alloc<uint32_t>(n + 1);
+  }
   if (x.overflow) return c;
   const UcdView ucd = x.ucd;
+  const uint32_t* asc = x.asc;
+  uint32_t* ent = c.ent;
   uint32_t* off = c.off;
-  uint32_t* cpa = c.cp;
-  uint32_t* pra = c.prop;
+  uint16_t* pra = c.prop;
+  uint32_t dl = 0;
   c.n = x.par.template compact<int>(
       n, [&](uint32_t i, int&) { return utf8_is_lead(b[i]); },
       [&](uint32_t i, uint32_t k, int&) {
-        int len;
-        uint32_t cp = utf8_decode(b, i, n, &len);
-        off[k] = i;
-        cpa[k] = cp;
-        pra[k] = ucd.props(cp);
+        uint32_t p;
+        if (b[i] < 0x80 && asc) {
+          p = asc[b[i]];
+        } else {
+          int len;
+          p = ucd.props(utf8_decode(b, i, n, &len));
+        }
+        const uint16_t cpk = compact_prop(p);
+        if (packed) {
+          ent[k] = i | ((uint32_t)cpk << 16);
+        } else {
+          off[k] = i;
+          pra[k] = cpk;
+        }
+        dl |= (p & P_DICT) ? 1u : 0u;
       });
   const uint32_t cn = c.n;
-  x.par.single([&]() { off[cn] = n; });
+  x.par.single([&]() {
+    if (packed) ent[cn] = n;
+    else { off[cn] = n; pra[cn] = 0; }
+  });
+  if (dict) *dict = x.par.reduce_or(dl);
   x.par.sync();
   return c;
 }
 
 template <class P>
-TB_HD uint64_t* prefix_hash(DocCtx<P>& x, const uint8_t* b, uint32_t n) {
-  uint64_t* PH = x.template alloc<uint64_t>(n + 1);
-  if (x.overflow) return PH;
+TB_HD uint64_t span_hash8(const DocCtx<P>& x, const PHView& v, uint32_t s, uint32_t e) {
+  const uint64_t hs = v.at(s), he = v.at(e);
+  const uint64_t t = mulmod61(hs, x.powb(e - s));
+  return he >= t ? he - t : he + kM61 - t;
+}
+
+template <class P>
+TB_HD PHView prefix_hash8(DocCtx<P>& x, const uint8_t* b, uint32_t n) {
+  PHView v;
+  v.b = b;
+  v.n = n;
+  const uint32_t nblk = (n + 7) >> 3;
+  // top of the slice: released with the code point arrays before the n-gram statistics
+  uint64_t* ph8 = x.template alloc_hot_hi<uint64_t>(nblk + 1);
+  if (x.overflow) return v;
   const uint64_t* pw = x.pw;
   const uint32_t pwn = x.pw_n;
-  HL tot = x.par.template scan_blocked<16, HL>(
-      n, HL{0, 0, 0},
+  HL tot = x.par.template scan<HL>(
+      nblk, HL{0, 0, 0},
       [&](const HL& a, const HL& c) {
         uint64_t m = c.len <= pwn ? pw[c.len] : powmod61(kHashBase, c.len);
         return HL{addmod61(mulmod61(a.h, m), c.h), a.len + c.len, 0};
       },
-      [&](uint32_t i) { return HL{(uint64_t)b[i] + 1, 1, 0}; },
-      [&](uint32_t i, const HL& e) { PH[i] = e.h; });
-  x.par.single([&]() { PH[n] = tot.h; });
+      [&](uint32_t k) {
+        const uint32_t s0 = k << 3, e0 = s0 + 8 < n ? s0 + 8 : n;
+        uint64_t h = 0;
+        for (uint32_t j = s0; j < e0; ++j) h = hash_push(h, b[j]);
+        return HL{h, e0 - s0, 0};
+      },
+      [&](uint32_t k, const HL& e) { ph8[k] = e.h; });
+  x.par.single([&]() { ph8[nblk] = tot.h; });
   x.par.sync();
-  return PH;
+  v.ph8 = ph8;
+  v.phn = tot.h;
+  return v;
 }
 
 // UAX#29 word segments of code points [0, C) -> words (trimmed, with a word character).
@@ -223,52 +328,45 @@ template <class P>
 TB_HD Words words(DocCtx<P>& x, const Cps& c) {
   Words w;
   const uint32_t C = c.n;
-  uint8_t* wb = x.template alloc<uint8_t>(C + 1);
-  uint32_t* sf = x.template alloc<uint32_t>(C + 1);  // per segment end: first non-ws cp
-  uint32_t* sl = x.template alloc<uint32_t>(C + 1);  // per segment end: last non-ws cp + 1 | flags
   w.cs = x.template alloc<uint32_t>(C + 1);
   w.ce = x.template alloc<uint32_t>(C + 1);
   w.bs = x.template alloc<uint32_t>(C + 1);
   w.be = x.template alloc<uint32_t>(C + 1);
   w.alpha = x.template alloc<uint8_t>(C + 1);
+  const auto mark = x.mark();
+  // word-break positions as a bitmask (C/8 bytes, LDS): one rule evaluation per position, no
+  // per-code-point arrays; the segment scan and the word compaction run in one fused pass
+  uint32_t* wbm = x.template alloc_hot_hi<uint32_t>(mask_words(C + 1));
   if (x.overflow) return w;
-  const uint32_t* prop = c.prop;
-  const uint32_t* off = c.off;
+  const PropArr prop = c.props();
+  const OffArr off = c.offs();
   CpsAcc acc{prop};
-  x.par.for_n(C + 1, [&](uint32_t i) {
-    wb[i] = (i == 0 || i == C) ? 1 : (uint8_t)wb_break(acc, (int)C, (int)i);
-  });
+  x.par.mask_bits(C + 1, [&](uint32_t i) { return i == 0 || i == C || wb_break(acc, (int)C, (int)i); }, wbm);
   x.par.sync();
-  auto elem = [&](uint32_t j) {
-    const uint32_t p = prop[j];
-    const bool ws = is_ws(p);
-    WSeg e;
-    e.bits = (wb[j] ? 1u : 0u) | ((!(p & P_PUNCT) && !ws) ? 2u : 0u) | ((p & P_ALPHA) ? 4u : 0u);
-    e.first = ws ? 0xFFFFFFFFu : j;
-    e.last = ws ? 0u : j + 1;
-    return e;
-  };
-  x.par.template scan<WSeg>(
-      C, WSeg{0u, 0xFFFFFFFFu, 0u} /* two-sided identity */, wseg_op, elem, [&](uint32_t j, const WSeg& ex) {
-        if (!wb[j + 1]) return;  // not the last code point of its segment
-        const WSeg in = wseg_op(ex, elem(j));
-        sf[j] = in.first;
-        sl[j] = (in.bits & 2u) ? (in.last | ((in.bits & 4u) ? 0x80000000u : 0u)) : 0xFFFFFFFFu;
-      });
-  x.par.sync();
+  auto bit = [&](uint32_t i) { return (wbm[i >> 5] >> (i & 31)) & 1u; };
   uint32_t *cs = w.cs, *ce = w.ce, *bs = w.bs, *be = w.be;
   uint8_t* al = w.alpha;
-  w.n = x.par.template compact<int>(
-      C, [&](uint32_t j, int&) { return wb[j + 1] && sl[j] != 0xFFFFFFFFu; },
-      [&](uint32_t j, uint32_t k, int&) {
-        const uint32_t s0 = sf[j], e0 = sl[j] & 0x7FFFFFFFu;
-        cs[k] = s0;
-        ce[k] = e0;
-        bs[k] = off[s0];
-        be[k] = off[e0];
-        al[k] = (sl[j] >> 31) ? 1 : 0;
+  w.n = x.par.template scan_compact<WSeg>(
+      C, WSeg{0u, 0xFFFFFFFFu, 0u} /* two-sided identity */, wseg_op,
+      [&](uint32_t j) {
+        const uint32_t p = prop[j];
+        const bool ws = is_ws(p);
+        WSeg e;
+        e.bits = bit(j) | ((!(p & P_PUNCT) && !ws) ? 2u : 0u) | ((p & P_ALPHA) ? 4u : 0u);
+        e.first = ws ? 0xFFFFFFFFu : j;
+        e.last = ws ? 0u : j + 1;
+        return e;
+      },
+      [&](uint32_t j, const WSeg& in) { return bit(j + 1) && (in.bits & 2u); },
+      [&](uint32_t, uint32_t k, const WSeg& in) {
+        cs[k] = in.first;
+        ce[k] = in.last;
+        bs[k] = off[in.first];
+        be[k] = off[in.last];
+        al[k] = (in.bits & 4u) ? 1 : 0;
       });
   x.par.sync();
+  x.reset(mark);
   return w;
 }
 
@@ -280,18 +378,17 @@ TB_HD Lines rust_lines(DocCtx<P>& x, const Cps& c) {
   L.ls = x.template alloc<uint32_t>(C + 1);
   L.le = x.template alloc<uint32_t>(C + 1);
   if (x.overflow) return L;
-  const uint32_t* cp = c.cp;
   uint32_t* ls = L.ls;
   uint32_t* le = L.le;
   L.n = x.par.template compact<int>(
-      C, [&](uint32_t i, int&) { return i == 0 || cp[i - 1] == '\n'; },
+      C, [&](uint32_t i, int&) { return i == 0 || c.lead(i - 1) == '\n'; },
       [&](uint32_t i, uint32_t k, int&) { ls[k] = i; });
   x.par.sync();
   const uint32_t NL = L.n;
   x.par.for_n(NL, [&](uint32_t k) {
-    uint32_t e = (k + 1 < NL) ? ls[k + 1] - 1 : (cp[C - 1] == '\n' ? C - 1 : C);
+    uint32_t e = (k + 1 < NL) ? ls[k + 1] - 1 : (c.lead(C - 1) == '\n' ? C - 1 : C);
     uint32_t ce = e;
-    if (e < C && ce > ls[k] && cp[ce - 1] == '\r') --ce;
+    if (e < C && ce > ls[k] && c.lead(ce - 1) == '\r') --ce;
     le[k] = ce;
   });
   x.par.sync();
@@ -299,16 +396,49 @@ TB_HD Lines rust_lines(DocCtx<P>& x, const Cps& c) {
 }
 
 // canon[i] = smallest j with element j == element i (key() groups candidates, eq() verifies).
-// Open-addressing table of ~1.5 n packed 64-bit slots (fingerprint = high 32 bits of the key,
-// low 32 bits = smallest index + 1; 0 = empty), small enough to stay in the wave's LDS slice for
-// typical documents. An element joins the group whose slot holds its fingerprint (one 64-bit
-// atomic min keeps the smallest index) and remembers the slot in canon[] until the lookup pass;
-// every non-trivial member is then verified against its representative with eq(), so a
-// fingerprint collision between unequal elements sends the document to the CPU oracle.
+//
+// Up to 65534 elements (every wave-path document): open addressing over ~1.5 n packed 32-bit
+// slots (16-bit fingerprint from the key's high bits | smallest index + 1; 0 = empty), half the
+// LDS of 64-bit slots, so the table stays on chip. An element joins a slot whose fingerprint
+// matches only after eq() against the slot's member says they are equal (a fingerprint
+// collision keeps probing), so the grouping is exact and no document is sent to the CPU for it;
+// a 32-bit atomic min keeps the smallest index. Larger inputs (workgroup path) use 64-bit slots
+// with a 32-bit fingerprint and a verification pass, where a collision between unequal elements
+// sends the document to the CPU oracle.
 template <class P, class KeyF, class EqF>
 TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t* canon) {
   const uint32_t capn = n + (n >> 1) + 2;
   const auto mark = x.mark();
+  if (n < 65535u) {
+    uint32_t* tab = x.template alloc_hot_hi<uint32_t>(capn);
+    if (x.overflow) return;
+    x.par.for_n(capn, [&](uint32_t i) { tab[i] = 0; });
+    x.par.sync();
+    x.par.for_n(n, [&](uint32_t i) {
+      const uint64_t k = key(i);
+      const uint32_t fp = (uint32_t)(k >> 48);
+      const uint32_t mine = (fp << 16) | (i + 1);
+      uint32_t slot = (uint32_t)(((k & 0xFFFFFFFFull) * capn) >> 32);
+      while (true) {
+        uint32_t cur = tab[slot];
+        if (cur == 0) {
+          cur = P::cas32(&tab[slot], 0u, mine);
+          if (cur == 0) break;
+        }
+        if ((cur >> 16) == fp && eq(i, (cur & 0xFFFFu) - 1u)) {
+          P::min32(&tab[slot], mine);
+          break;
+        }
+        if (++slot == capn) slot = 0;
+      }
+      canon[i] = slot;
+    });
+    x.par.sync();
+    x.par.for_n(n, [&](uint32_t i) { canon[i] = (tab[canon[i]] & 0xFFFFu) - 1u; });
+    x.par.sync();
+    x.reset(mark);
+    return;
+  }
   uint64_t* tab = x.template alloc_hot_hi<uint64_t>(capn);
   if (x.overflow) return;
   x.par.for_n(capn, [&](uint32_t i) { tab[i] = 0; });
@@ -353,18 +483,17 @@ TB_HD bool bytes_eq(const uint8_t* b, uint32_t a0, uint32_t a1, uint32_t b0, uin
 
 // find_duplicates over byte spans [s[i], e[i]): (#repeats, sum of repeat byte lengths).
 template <class P, class SpanF>
-TB_HD void dup_spans(DocCtx<P>& x, const uint8_t* b, const uint64_t* PH, uint32_t n, SpanF&& span,
+TB_HD void dup_spans(DocCtx<P>& x, const uint8_t* b, const PHView& ph, uint32_t n, SpanF&& span,
                      int64_t* out_elems, int64_t* out_bytes) {
   const auto mark = x.mark();
   uint32_t* canon = x.template alloc_hot<uint32_t>(n + 1);
   if (x.overflow) return;
-  const uint64_t* pw = x.pw;
   canonicalize(
       x, n,
       [&](uint32_t i) {
         uint32_t s, e;
         span(i, s, e);
-        return dev_key(sub_hash(PH, pw, s, e), e - s);
+        return dev_key(span_hash8(x, ph, s, e), e - s);
       },
       [&](uint32_t i, uint32_t j) {
         uint32_t s0, e0, s1, e1;
@@ -385,23 +514,23 @@ TB_HD void dup_spans(DocCtx<P>& x, const uint8_t* b, const uint64_t* PH, uint32_
 
 // Lowercase (Rust str::to_lowercase on the word) hashed on the fly; optionally compared to `ref`.
 template <class F>
-TB_HD void lower_bytes(const UcdView& ucd, const uint32_t* cp, const uint32_t* prop, uint32_t s,
-                       uint32_t e, F&& push) {
+TB_HD void lower_bytes(const UcdView& ucd, const Cps& cv, uint32_t s, uint32_t e, F&& push) {
   uint8_t buf[4];
+  const PropArr prop = cv.props();
   for (uint32_t k = s; k < e; ++k) {
-    uint32_t c = cp[k];
+    uint32_t c = cv.cp(k);
     uint32_t lc;
     if (c == 0x3A3) {
       bool before = false, after = false;
       for (uint32_t j = k; j > s; --j) {
         uint32_t p = prop[j - 1];
-        if (p & P_CASE_IGN) continue;
+        if (p & P16_CASE_IGN) continue;
         before = (p & P_CASED) != 0;
         break;
       }
       for (uint32_t j = k + 1; j < e; ++j) {
         uint32_t p = prop[j];
-        if (p & P_CASE_IGN) continue;
+        if (p & P16_CASE_IGN) continue;
         after = (p & P_CASED) != 0;
         break;
       }
@@ -415,12 +544,12 @@ TB_HD void lower_bytes(const UcdView& ucd, const uint32_t* cp, const uint32_t* p
   }
 }
 
-TB_HD bool is_stop_word(const UcdView& ucd, const DevStopSet& ss, const uint32_t* cp,
-                        const uint32_t* prop, uint32_t s, uint32_t e) {
-  if (ss.n == 0) return false;
+TB_HD bool is_stop_word(const UcdView& ucd, const DevStopSet& ss, const Cps& cv, uint32_t s, uint32_t e) {
+  // every code point lowercases to at least one byte
+  if (ss.n == 0 || (int32_t)(e - s) > ss.max_len) return false;
   uint64_t h = 0;
   uint32_t len = 0;
-  lower_bytes(ucd, cp, prop, s, e, [&](uint8_t v) { h = hash_push(h, v); ++len; });
+  lower_bytes(ucd, cv, s, e, [&](uint8_t v) { h = hash_push(h, v); ++len; });
   const uint64_t key = dev_key(h, len);
   uint32_t slot = (uint32_t)(key >> 17) & (kStopTableSize - 1);
   while (true) {
@@ -432,7 +561,7 @@ TB_HD bool is_stop_word(const UcdView& ucd, const DevStopSet& ss, const uint32_t
       if ((uint32_t)(o1 - o0) != len) return false;
       int32_t pos = o0;
       bool ok = true;
-      lower_bytes(ucd, cp, prop, s, e, [&](uint8_t v) { ok = ok && ss.blob[pos++] == v; });
+      lower_bytes(ucd, cv, s, e, [&](uint8_t v) { ok = ok && ss.blob[pos++] == v; });
       return ok;
     }
     slot = (slot + 1) & (kStopTableSize - 1);
@@ -482,7 +611,7 @@ TB_HD uint32_t count_sentences(DocCtx<P>& x, const Cps& c, uint32_t s, uint32_t 
   const auto mark = x.mark();
   uint32_t* starts = x.template alloc<uint32_t>(m + 1);
   if (x.overflow) return 0;
-  const uint32_t* prop = c.prop + s;
+  const PropArr prop = c.props() + s;
   CpsAcc acc{prop};
   const uint32_t NS = x.par.template compact<int>(
       m, [&](uint32_t i, int&) { return i == 0 || sb_break(acc, (int)m, (int)i); },
@@ -499,12 +628,10 @@ TB_HD uint32_t count_sentences(DocCtx<P>& x, const Cps& c, uint32_t s, uint32_t 
 
 template <class P>
 TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, const Cps& c,
-                             const uint64_t* PH, const Words& w, int64_t* r, bool release_props = false) {
+                             const PHView& ph, const Words& w, int64_t* r, bool release_props = false) {
   const uint32_t C = c.n;
-  const uint32_t* cp = c.cp;
-  const uint32_t* prop = c.prop;
-  const uint32_t* off = c.off;
-  const uint64_t* pw = x.pw;
+  const PropArr prop = c.props();
+  const OffArr off = c.offs();
   const int width = ds.width;
   const uint32_t tcs = x.par.template min<uint32_t>(C, C, [&](uint32_t i) { return is_ws(prop[i]) ? C : i; });
   const uint32_t tce = x.par.template max<uint32_t>(C, 0u, [&](uint32_t i) { return is_ws(prop[i]) ? 0u : i + 1; });
@@ -525,17 +652,17 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       span,
       [&](uint32_t i, int&) {
         const uint32_t j = tcs + i;
-        return cp[j] == '\n' && cp[j - 1] != '\n';
+        return c.lead(j) == '\n' && c.lead(j - 1) != '\n';
       },
       [&](uint32_t i, uint32_t k, int&) {
         uint32_t j = tcs + i, q = j;
-        while (cp[q] == '\n') ++q;
+        while (c.lead(q) == '\n') ++q;
         rs[k] = j;
         rl[k] = q - j;
       });
   x.par.sync();
   int64_t line_dup = 0, line_dup_b = 0, para_dup = 0, para_dup_b = 0;
-  dup_spans(x, b, PH, NR + 1,
+  dup_spans(x, b, ph, NR + 1,
             [&](uint32_t k, uint32_t& s0, uint32_t& e0) {
               const uint32_t cs = k == 0 ? tcs : rs[k - 1] + rl[k - 1];
               const uint32_t ce = k == NR ? tce : rs[k];
@@ -546,7 +673,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
   const uint32_t NPR = x.par.template compact<int>(
       NR, [&](uint32_t k, int&) { return rl[k] >= 2; }, [&](uint32_t k, uint32_t q, int&) { prs[q] = k; });
   x.par.sync();
-  dup_spans(x, b, PH, NPR + 1,
+  dup_spans(x, b, ph, NPR + 1,
             [&](uint32_t q, uint32_t& s0, uint32_t& e0) {
               const uint32_t cs = q == 0 ? tcs : rs[prs[q - 1]] + rl[prs[q - 1]];
               const uint32_t ce = q == NPR ? tce : rs[prs[q]];
@@ -555,9 +682,6 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
             },
             &para_dup, &para_dup_b);
   x.stamp(PH_GR_LINES);
-  // the n-gram statistics below read words, bytes and offsets only: the property array's LDS
-  // (top of the slice) goes to their hash tables
-  if (release_props) x.release_hi();
   x.par.single([&]() {
     r[0] = span;
     r[1] = NPR + 1;
@@ -568,15 +692,29 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     r[6] = line_dup_b;
   });
   // ---- n-gram statistics over the words ----
+  // Word-level arrays (LDS while they fit): wid = canonical word id (smallest index of an equal
+  // word), WL = byte prefix of word lengths, and for concatenation hashes of any word run
+  //   K[k] = sum_{j<k} H(word j) * B^-WL[j+1],  PB[k] = B^WL[k]
+  //   H(words p .. p+n-1 concatenated) = PB[p+n] * (K[p+n] - K[p])
+  // (the Horner hash of the concatenation), so a run costs one multiplication and no power
+  // lookup; the powers are read once per word instead of once per (n, position). They are built
+  // while the prefix hashes are still on chip; then the code point arrays and prefix hashes (top
+  // of the LDS slice) are released, so the n-gram tables get that space.
   const uint32_t W = w.n;
-  if (ds.n_top + ds.n_dup > 0) {
-    uint32_t* wid = x.template alloc_hot<uint32_t>(W + 1);
-    uint32_t* WL = x.template alloc_hot<uint32_t>(W + 1);
-    uint64_t* PI = x.template alloc_hot<uint64_t>(W + 1);
-    uint64_t* PW = x.template alloc_hot<uint64_t>(W + 1);
-    uint64_t* wh = x.template alloc<uint64_t>(W + 1);
+  const bool ngrams = ds.n_top + ds.n_dup > 0;
+  uint32_t* wid = nullptr;
+  uint32_t* WL = nullptr;
+  uint64_t* K = nullptr;
+  uint64_t* PB = nullptr;
+  if (ngrams) {
+    wid = x.template alloc_hot<uint32_t>(W + 1);
+    WL = x.template alloc_hot<uint32_t>(W + 1);
+    K = x.template alloc_hot<uint64_t>(W + 1);
+    PB = x.template alloc_hot<uint64_t>(W + 1);
+    const auto mw = x.mark();
+    uint64_t* wh = x.template alloc_hot_hi<uint64_t>(W + 1);
     if (x.overflow) return;
-    x.par.for_n(W, [&](uint32_t k) { wh[k] = sub_hash(PH, pw, w.bs[k], w.be[k]); });
+    x.par.for_n(W, [&](uint32_t k) { wh[k] = span_hash8(x, ph, w.bs[k], w.be[k]); });
     x.par.sync();
     canonicalize(
         x, W, [&](uint32_t k) { return dev_key(wh[k], w.be[k] - w.bs[k]); },
@@ -584,56 +722,74 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     const uint32_t totl = x.par.template scan<uint32_t>(
         W, 0u, [](uint32_t a, uint32_t c2) { return a + c2; },
         [&](uint32_t k) { return w.be[k] - w.bs[k]; }, [&](uint32_t k, uint32_t e) { WL[k] = e; });
-    const uint32_t pwn = x.pw_n;
-    auto hl_op = [&](const HL& a, const HL& c2) {
-      uint64_t m = c2.len <= pwn ? pw[c2.len] : powmod61(kHashBase, c2.len);
-      return HL{addmod61(mulmod61(a.h, m), c2.h), a.len + c2.len, 0};
-    };
-    HL ti = x.par.template scan<HL>(
-        W, HL{0, 0, 0}, hl_op, [&](uint32_t k) { return HL{(uint64_t)wid[k] + 1, 1, 0}; },
-        [&](uint32_t k, const HL& e) { PI[k] = e.h; });
-    HL tw = x.par.template scan<HL>(
-        W, HL{0, 0, 0}, hl_op, [&](uint32_t k) { return HL{wh[k], w.be[k] - w.bs[k], 0}; },
-        [&](uint32_t k, const HL& e) { PW[k] = e.h; });
-    x.par.single([&]() {
-      WL[W] = totl;
-      PI[W] = ti.h;
-      PW[W] = tw.h;
-    });
+    x.par.single([&]() { WL[W] = totl; });
     x.par.sync();
+    x.par.for_n(W + 1, [&](uint32_t k) { PB[k] = x.powb(WL[k]); });
+    const uint64_t ktot = x.par.template scan<uint64_t>(
+        W, 0ull, [](uint64_t a, uint64_t c2) { return addmod61(a, c2); },
+        [&](uint32_t j) { return mulmod61(wh[j], x.ipowb(WL[j + 1])); }, [&](uint32_t k, uint64_t e) { K[k] = e; });
+    x.par.single([&]() { K[W] = ktot; });
+    x.par.sync();
+    x.reset(mw);  // wh
     if (x.overflow) return;
-    x.stamp(PH_GR_WORDS);
-    for (int t = 0; t < ds.n_top; ++t) {
-      const uint32_t n = (uint32_t)ds.top_n[t];
-      int64_t res = 0;
-      if (n > 0 && W >= n) {
+  }
+  x.stamp(PH_GR_WORDS);
+  // the n-gram statistics read words, bytes and the arrays above only: the top of the LDS slice
+  // (code point arrays, prefix hashes) goes to their hash tables
+  if (release_props) x.release_hi();
+  if (ngrams) {
+    auto run_hash = [&](uint32_t p, uint32_t n) {
+      const uint64_t d = K[p + n] >= K[p] ? K[p + n] - K[p] : K[p + n] + kM61 - K[p];
+      return mulmod61(PB[p + n], d);
+    };
+    // Top n-grams (space-joined grams: equal iff their word sequences are equal). Canonical ids
+    // of the n-grams are built incrementally: the n-gram at p is the pair (id of the (n-1)-gram
+    // at p, id of word p+n-1), so each order is one exact pair canonicalisation (O(1) equality,
+    // no hashing of the gram text).
+    if (ds.n_top > 0) {
+      int max_top = 0;
+      for (int t = 0; t < ds.n_top; ++t) max_top = ds.top_n[t] > max_top ? ds.top_n[t] : max_top;
+      const auto m2 = x.mark();
+      // two id arrays in turn; the counts of order n go to the one the (n-1)-gram ids used
+      uint32_t* ga = x.template alloc_hot<uint32_t>(W + 1);
+      uint32_t* gb = x.template alloc_hot<uint32_t>(W + 1);
+      if (x.overflow) return;
+      x.par.single([&]() { for (int t = 0; t < ds.n_top; ++t) r[rec_gr_fixed() + t] = 0; });
+      const uint32_t* gprev = wid;
+      for (uint32_t n = 1; n <= (uint32_t)max_top && W >= n; ++n) {
         const uint32_t G = W - n + 1;
-        const auto m2 = x.mark();
-        uint32_t* gc = x.template alloc_hot<uint32_t>(G);
-        uint32_t* cnt = x.template alloc_hot<uint32_t>(G);
-        if (x.overflow) return;
-        const uint64_t pn = x.powb(n);
-        canonicalize(
-            x, G, [&](uint32_t p) { return dev_key(span_hash(PI[p], PI[p + n], pn), n); },
-            [&](uint32_t p, uint32_t q) {
-              for (uint32_t k = 0; k < n; ++k) if (wid[p + k] != wid[q + k]) return false;
-              return true;
-            },
-            gc);
+        const uint32_t* gc = wid;
+        uint32_t* cnt = (n == 1 || !(n & 1)) ? ga : gb;
+        if (n > 1) {
+          uint32_t* gcur = (n & 1) ? ga : gb;
+          canonicalize(
+              x, G, [&](uint32_t p) { return mix64(((uint64_t)gprev[p] << 32) ^ (uint64_t)wid[p + n - 1] ^ ((uint64_t)n << 60)); },
+              [&](uint32_t p, uint32_t q) { return gprev[p] == gprev[q] && wid[p + n - 1] == wid[q + n - 1]; }, gcur);
+          gc = gcur;
+          gprev = gcur;
+          x.stamp(PH_GR_TOP_CANON);
+        }
+        bool wanted = false;
+        for (int t = 0; t < ds.n_top; ++t) wanted |= ds.top_n[t] == (int32_t)n;
+        if (!wanted) continue;
         x.par.for_n(G, [&](uint32_t p) { cnt[p] = 0; });
         x.par.sync();
         x.par.for_n(G, [&](uint32_t p) { P::add32(&cnt[gc[p]], 1u); });
         x.par.sync();
         const uint32_t maxc = x.par.template max<uint32_t>(G, 0u, [&](uint32_t p) { return cnt[p]; });
+        int64_t v = 0;
         if (maxc > 1) {
           const uint32_t maxlen = x.par.template max<uint32_t>(G, 0u, [&](uint32_t p) {
             return cnt[p] == maxc ? (WL[p + n] - WL[p] + n - 1) : 0u;
           });
-          res = (int64_t)maxlen * (int64_t)maxc;
+          v = (int64_t)maxlen * (int64_t)maxc;
         }
-        x.reset(m2);
+        x.par.single([&]() {
+          for (int t = 0; t < ds.n_top; ++t) if (ds.top_n[t] == (int32_t)n) r[rec_gr_fixed() + t] = v;
+        });
+        x.par.sync();
       }
-      x.par.single([&]() { r[rec_gr_fixed() + t] = res; });
+      x.reset(m2);
     }
     x.stamp(PH_GR_TOP);
     if (ds.n_dup > 0) {
@@ -660,11 +816,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
         if (x.overflow) return;
         x.par.for_n(2 * SW, [&](uint32_t i) { sn[i] = 0; });
         canonicalize(
-            x, G,
-            [&](uint32_t p) {
-              const uint32_t L = WL[p + n] - WL[p];
-              return dev_key(span_hash(PW[p], PW[p + n], x.powb(L)), L);
-            },
+            x, G, [&](uint32_t p) { return dev_key(run_hash(p, n), WL[p + n] - WL[p]); },
             [&](uint32_t p, uint32_t q) {
               if (WL[p + n] - WL[p] != WL[q + n] - WL[q]) return false;
               // same canonical word sequence => same concatenation (the common case); only
@@ -684,6 +836,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
               return true;
             },
             gc);
+        x.stamp(PH_GR_DUP_CANON);
         x.par.for_n(G, [&](uint32_t p) {
           const uint32_t g = gc[p];
           if (g != p) {
@@ -720,6 +873,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
           *rt = rep;
         });
         x.par.sync();
+        x.stamp(PH_GR_DUP_WALK);
         x.reset(m3);
       }
       x.stamp(PH_GR_DUP);
@@ -845,14 +999,14 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
     return;
   }
   x.stamp(PH_C4_LOREM);
-  Cps c = decode(x, b, n);
+  uint32_t dict = 0;
+  Cps c = decode(x, b, n, false, &dict);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   x.stamp(PH_C4_DECODE);
   const uint32_t C = c.n;
-  const uint32_t* cp = c.cp;
-  const uint32_t* prop = c.prop;
-  const uint32_t* off = c.off;
-  if (x.par.template sum<uint32_t>(C, [&](uint32_t i) { return (prop[i] & P_DICT) ? 1u : 0u; })) {
+  const PropArr prop = c.props();
+  const OffArr off = c.offs();
+  if (dict) {
     x.set_flag(DOC_NEEDS_CPU);
     return;
   }
@@ -922,11 +1076,11 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
       });
   x.par.sync();
   auto cite_end = [&](uint32_t j, uint32_t e) -> uint32_t {  // cp index past a citation at j, or 0
-    if (cp[j] != '[') return 0;
+    if (c.lead(j) != '[') return 0;
     uint32_t p = j + 1;
     if (p >= e || !(prop[p] & P_DIGIT)) return 0;
     while (p < e && (prop[p] & P_DIGIT)) ++p;
-    while (p < e && cp[p] == ',') {
+    while (p < e && c.lead(p) == ',') {
       uint32_t q = p + 1;
       while (q < e && (prop[q] & P_WS)) ++q;
       if (q < e && (prop[q] & P_DIGIT)) {
@@ -936,14 +1090,14 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
         break;
       }
     }
-    return (p < e && cp[p] == ']') ? p + 1 : 0;
+    return (p < e && c.lead(p) == ']') ? p + 1 : 0;
   };
   const bool rmc = c4.remove_citations != 0;
   if (rmc) {
     // a citation holds only digits, commas, whitespace and ']': no '[' inside one, so every
     // '[' can be tested independently (same result as the left-to-right scan)
     x.par.for_n(C, [&](uint32_t j) {
-      if (cp[j] != '[' || lid[j] == kNoLine) return;
+      if (c.lead(j) != '[' || lid[j] == kNoLine) return;
       const uint32_t ce = cite_end(j, lb[lid[j]]);
       for (uint32_t q = j; q < ce; ++q) rm[q] = 1;
     });
@@ -1072,14 +1226,14 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   Cps jc = decode(x, Jb, Jtot);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   const uint32_t JC = jc.n;
-  const uint32_t* jprop = jc.prop;
+  const PropArr jprop = jc.props();
   const uint32_t tcs = x.par.template min<uint32_t>(JC, JC, [&](uint32_t i) { return is_ws(jprop[i]) ? JC : i; });
   const uint32_t tce = x.par.template max<uint32_t>(JC, 0u, [&](uint32_t i) { return is_ws(jprop[i]) ? 0u : i + 1; });
   uint32_t nsent = 0, bstart = 0, blen = 0;
   if (tcs < tce) {
     nsent = count_sentences(x, jc, tcs, tce);
-    bstart = jc.off[tcs];
-    blen = jc.off[tce] - jc.off[tcs];
+    bstart = jc.o(tcs);
+    blen = jc.o(tce) - jc.o(tcs);
   }
   x.stamp(PH_C4_SENT);
   const int64_t jrel = (int64_t)((const char*)Jb - x.scr) + bstart;
@@ -1119,29 +1273,31 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
     if (k == DK_LANGID) need_lid = true;
   }
   x.stamp(PH_START);
-  Cps c = decode(x, b, n, kHotProps);
+  uint32_t ndict = 0;
+  Cps c = decode(x, b, n, kHotProps, &ndict);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   x.stamp(PH_DECODE);
   const uint32_t C = c.n;
-  // Documents with dictionary-segmented scripts go to the ICU path (host).
-  const uint32_t ndict = x.par.template sum<uint32_t>(C, [&](uint32_t i) { return (c.prop[i] & P_DICT) ? 1u : 0u; });
-  if (ndict) { x.set_flag(DOC_NEEDS_CPU); }
+  // Documents with dictionary-segmented scripts go to the ICU path (host): their records are
+  // recomputed there, so nothing else is analysed on the device.
+  if (ndict) {
+    x.set_flag(DOC_NEEDS_CPU);
+    return;
+  }
   x.stamp(PH_DICT);
-  uint64_t* PH = nullptr;
-  if (need_ph) PH = prefix_hash(x, b, n);
+  PHView ph;
+  if (need_ph) ph = prefix_hash8(x, b, n);
   x.stamp(PH_PREFIX_HASH);
   Words w;
-  if (need_words && !ndict) w = words(x, c);
+  if (need_words) w = words(x, c);
   x.stamp(PH_WORDS);
   Lines L;
   if (need_lines) L = rust_lines(x, c);
   x.stamp(PH_LINES);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   const uint32_t W = w.n;
-  const uint32_t* cp = c.cp;
-  const uint32_t* prop = c.prop;
-  const uint32_t* off = c.off;
-  const uint64_t* pw = x.pw;
+  const PropArr prop = c.props();
+  const OffArr off = c.offs();
 
   // Records are independent: GopherRepetition runs after the other steps so that its n-gram
   // phase (the last user of the code point properties) can hand their LDS to its hash tables.
@@ -1164,7 +1320,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
       const uint64_t as = x.par.template sum<uint64_t>(W, [&](uint32_t k) {
         const uint32_t a = w.cs[k], e = w.ce[k];
         return ((uint64_t)(e - a) << 32) | ((uint64_t)w.alpha[k] << 16) |
-               (uint64_t)is_stop_word(ucd, ss, cp, prop, a, e);
+               (uint64_t)is_stop_word(ucd, ss, c, a, e);
       });
       // fields: chars (bits 32..63, <= C), alphabetic words (16..31) and stop words (0..15), both
       // <= W; documents with 2^16 words or more are counted field by field
@@ -1177,16 +1333,16 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
         sum_chars = x.par.template sum<int64_t>(W, [&](uint32_t k) { return (int64_t)(w.ce[k] - w.cs[k]); });
         alpha = x.par.template sum<int64_t>(W, [&](uint32_t k) { return (int64_t)w.alpha[k]; });
         stop = x.par.template sum<int64_t>(W, [&](uint32_t k) {
-          return (int64_t)is_stop_word(ucd, ss, cp, prop, w.cs[k], w.ce[k]);
+          return (int64_t)is_stop_word(ucd, ss, c, w.cs[k], w.ce[k]);
         });
       }
       const uint64_t he = x.par.template sum<uint64_t>(C, [&](uint32_t i) {
-        const uint32_t c0 = cp[i];
+        const uint32_t c0 = c.lead(i);
         if (c0 == '#') return (uint64_t)1 << 32;
-        if (c0 == 0x2026) return (uint64_t)1;
-        if (c0 != '.' || (i > 0 && cp[i - 1] == '.')) return (uint64_t)0;
+        if (c0 == 0xE2) return (uint64_t)(c.cp(i) == 0x2026);
+        if (c0 != '.' || (i > 0 && c.lead(i - 1) == '.')) return (uint64_t)0;
         uint32_t j = i;
-        while (j < C && cp[j] == '.') ++j;
+        while (j < C && c.lead(j) == '.') ++j;
         return (uint64_t)((j - i) / 3);
       });
       const int64_t nhash = hi32(he), nell = lo32(he);
@@ -1194,7 +1350,8 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
         const uint32_t ls = L.ls[k], le = L.le[k];
         uint32_t j = ls;
         while (j < le && is_ws(prop[j])) ++j;
-        const uint64_t bul = (j < le && (cp[j] == 0x2022 || cp[j] == '-')) ? 1 : 0;
+        const uint32_t l0 = j < le ? c.lead(j) : 0u;
+        const uint64_t bul = (l0 == '-' || (l0 == 0xE2 && c.cp(j) == 0x2022)) ? 1 : 0;
         j = le;
         while (j > ls && is_ws(prop[j - 1])) --j;
         const uint32_t E = off[j], S = off[ls];
@@ -1214,7 +1371,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
       x.stamp(PH_GQ);
     } else if (ds.kind == DK_GOPHER_REP) {
       ++gr_seen;
-      gopher_rep_record(x, ds, b, c, PH, w, r, kHotProps && gr_seen == n_gr);
+      gopher_rep_record(x, ds, b, c, ph, w, r, kHotProps && gr_seen == n_gr);
     } else if (ds.kind == DK_FINEWEB) {
       const auto mark = x.mark();
       uint32_t* nb = x.template alloc<uint32_t>(L.n + 1);
@@ -1231,7 +1388,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
         uint32_t k = nb[q];
         uint32_t j = L.le[k];
         while (j > L.ls[k] && is_ws(prop[j - 1])) --j;
-        uint32_t last = cp[j - 1];
+        uint32_t last = c.cp(j - 1);
         for (int t = 0; t < ds.n_stop_chars; ++t) if (ds.stop_chars[t] == last) return (int64_t)1;
         return (int64_t)0;
       });
@@ -1240,10 +1397,10 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
         return (int64_t)((int64_t)(L.le[k] - L.ls[k]) <= ds.short_line_length);
       });
       int64_t dup_e = 0, dup_b = 0;
-      dup_spans(x, b, PH, NB,
+      dup_spans(x, b, ph, NB,
                 [&](uint32_t q, uint32_t& s0, uint32_t& e0) { s0 = off[L.ls[nb[q]]]; e0 = off[L.le[nb[q]]]; },
                 &dup_e, &dup_b);
-      int64_t nl = x.par.template sum<int64_t>(C, [&](uint32_t i) { return (int64_t)(cp[i] == '\n'); });
+      int64_t nl = x.par.template sum<int64_t>(C, [&](uint32_t i) { return (int64_t)(c.lead(i) == '\n'); });
       x.par.single([&]() {
         r[0] = NB; r[1] = stop_end; r[2] = shrt; r[3] = dup_b; r[4] = (int64_t)C - nl; r[5] = nl; r[6] = W;
       });
@@ -1257,7 +1414,6 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
     }
     if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   }
-  (void)pw;
 }
 
 }  // namespace tb

@@ -11,6 +11,7 @@ namespace tb {
 
 constexpr uint64_t kM61 = (1ull << 61) - 1;
 constexpr uint64_t kHashBase = 0x1F3A5C7D9B2E4F61ull % kM61;
+constexpr uint64_t kHashBaseInv = 0x0BD8A5E56DEDF53Eull;  // kHashBase^(p-2) mod p: B * B^-1 = 1
 
 TB_HD uint64_t mulmod61(uint64_t a, uint64_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -14,6 +14,10 @@
 //    order). Returns the number selected (uniform across lanes).
 //  * sum/max/min: reductions (uniform result).
 //  * scan<T>(n, id, op, in, out): out(i, exclusive prefix) for every i; returns the total.
+//  * mask_bits(n, pred, bits): bit i of the u32 array = pred(i) (mask_words(n) words written).
+//  * scan_compact<T>(n, id, op, in, sel, emit): inclusive scan fused with a compaction that
+//    selects items by their inclusive prefix; emit(i, k, incl). Returns the number selected.
+//  * reduce_or(v): OR of a per-lane value over the document's lanes (uniform result).
 //  * sync(): every write before it is visible to every lane after it.
 //  * single(f): f() runs once (lane 0).
 //  * cas64/min32/min64/add32/add64/max32: atomics on scratch memory.
@@ -27,6 +31,9 @@
 #endif
 
 namespace tb {
+
+// u32 words mask_bits() writes for n items (whole 64-bit chunks).
+TB_HD constexpr uint32_t mask_words(uint32_t n) { return ((n + 63) / 64) * 2; }
 
 struct SeqPar {
   template <class F>
@@ -74,6 +81,27 @@ struct SeqPar {
   T scan_blocked(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
     return scan(n, id, op, in, out);
   }
+  // bits[i >> 5] bit (i & 31) = pred(i) for i < n; words up to the next multiple of 64 bits
+  // are written (callers size `bits` as mask_words(n)).
+  template <class Pred>
+  void mask_bits(uint32_t n, Pred&& pred, uint32_t* bits) const {
+    const uint32_t nw = ((n + 63) / 64) * 2;
+    for (uint32_t w = 0; w < nw; ++w) bits[w] = 0;
+    for (uint32_t i = 0; i < n; ++i) if (pred(i)) bits[i >> 5] |= 1u << (i & 31);
+  }
+  // Inclusive scan fused with a compaction: sel(i, incl) picks items given their inclusive
+  // prefix, emit(i, k, incl) gets the rank k among picked items. Returns the number picked.
+  template <class T, class Op, class In, class Sel, class Emit>
+  uint32_t scan_compact(uint32_t n, T id, Op&& op, In&& in, Sel&& sel, Emit&& emit) const {
+    T acc = id;
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      acc = op(acc, in(i));
+      if (sel(i, acc)) emit(i, k++, acc);
+    }
+    return k;
+  }
+  uint32_t reduce_or(uint32_t v) const { return v; }
   void sync() const {}
   static uint64_t clock() { return 0; }
   template <class F>
@@ -81,6 +109,11 @@ struct SeqPar {
   bool leader() const { return true; }
   static uint64_t cas64(uint64_t* p, uint64_t cmp, uint64_t val) {
     uint64_t old = *p;
+    if (old == cmp) *p = val;
+    return old;
+  }
+  static uint32_t cas32(uint32_t* p, uint32_t cmp, uint32_t val) {
+    uint32_t old = *p;
     if (old == cmp) *p = val;
     return old;
   }
@@ -142,13 +175,44 @@ __device__ inline T shfl_t(T v, int src) {
   __builtin_memcpy(&r, w, sizeof(T));
   return r;
 }
-// Inclusive wave scan (Hillis-Steele; op associative, not necessarily commutative).
+// Cross-lane moves by DPP (a VALU operand modifier: a few cycles, no LDS crossbar round trip
+// like ds_bpermute), one 32-bit word at a time for any POD element.
+template <int CTRL, class T>
+__device__ __forceinline__ T dpp_mov_t(T v) {
+  constexpr int N = (int)((sizeof(T) + 3) / 4);
+  int w[N] = {};
+  __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+  for (int k = 0; k < N; ++k) w[k] = __builtin_amdgcn_mov_dpp(w[k], CTRL, 0xF, 0xF, false);
+  T r;
+  __builtin_memcpy(&r, w, sizeof(T));
+  return r;
+}
+// Lane 63's value in every lane (scalar read-lane per word).
+template <class T>
+__device__ __forceinline__ T bcast63(T v) {
+  constexpr int N = (int)((sizeof(T) + 3) / 4);
+  int w[N] = {};
+  __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+  for (int k = 0; k < N; ++k) w[k] = __builtin_amdgcn_readlane(w[k], 63);
+  T r;
+  __builtin_memcpy(&r, w, sizeof(T));
+  return r;
+}
+// Inclusive wave64 scan (op associative, not necessarily commutative): Hillis-Steele inside
+// each row of 16 lanes with row_shr:1/2/4/8, then row_bcast:15 and row_bcast:31 carry the row
+// totals across rows (the rocPRIM warp_scan_dpp schedule): 6 DPP moves instead of 6
+// ds_bpermute round trips.
 template <class T, class Op>
-__device__ inline T wave_incl_scan(T x, uint32_t lane, Op&& op) {
-  for (int o = 1; o < 64; o <<= 1) {
-    T y = shfl_up_t(x, o);
-    if ((int)lane >= o) x = op(y, x);
-  }
+__device__ __forceinline__ T wave_incl_scan(T x, uint32_t lane, Op&& op) {
+  const uint32_t rl = lane & 15u;
+  { const T t = dpp_mov_t<0x111>(x); if (rl >= 1u) x = op(t, x); }
+  { const T t = dpp_mov_t<0x112>(x); if (rl >= 2u) x = op(t, x); }
+  { const T t = dpp_mov_t<0x114>(x); if (rl >= 4u) x = op(t, x); }
+  { const T t = dpp_mov_t<0x118>(x); if (rl >= 8u) x = op(t, x); }
+  { const T t = dpp_mov_t<0x142>(x); if ((lane & 31u) >= 16u) x = op(t, x); }
+  { const T t = dpp_mov_t<0x143>(x); if (lane >= 32u) x = op(t, x); }
   return x;
 }
 }  // namespace pardetail
@@ -191,19 +255,16 @@ struct WavePar {
     return k;
   }
   template <class T>
-  __device__ __forceinline__ static T wave_sum(T v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+  __device__ __forceinline__ T wave_sum(T v) const {
+    return pardetail::bcast63(pardetail::wave_incl_scan(v, lane, [](T a, T b) { return a + b; }));
   }
   template <class T>
-  __device__ __forceinline__ static T wave_max(T v) {
-    for (int o = 32; o > 0; o >>= 1) { T t = __shfl_xor(v, o); v = t > v ? t : v; }
-    return v;
+  __device__ __forceinline__ T wave_max(T v) const {
+    return pardetail::bcast63(pardetail::wave_incl_scan(v, lane, [](T a, T b) { return a > b ? a : b; }));
   }
   template <class T>
-  __device__ __forceinline__ static T wave_min(T v) {
-    for (int o = 32; o > 0; o >>= 1) { T t = __shfl_xor(v, o); v = t < v ? t : v; }
-    return v;
+  __device__ __forceinline__ T wave_min(T v) const {
+    return pardetail::bcast63(pardetail::wave_incl_scan(v, lane, [](T a, T b) { return a < b ? a : b; }));
   }
   template <class T, class F>
   __device__ __forceinline__ T sum(uint32_t n, F&& f) const {
@@ -265,16 +326,11 @@ struct WavePar {
         const uint32_t base = base0 + 64 * u;
         if (base >= n) break;
         const uint32_t i = base + lane;
-        T x = xs[u];
-        // inclusive Hillis-Steele scan (op is associative, not necessarily commutative)
-        for (int o = 1; o < 64; o <<= 1) {
-          T y = pardetail::shfl_up_t(x, o);
-          if ((int)lane >= o) x = op(y, x);
-        }
+        const T x = pardetail::wave_incl_scan(xs[u], lane, op);
         T excl = pardetail::shfl_up_t(x, 1);
         if (lane == 0) excl = id;
         if (i < n) out(i, op(carry, excl));
-        carry = op(carry, pardetail::shfl_t(x, 63));
+        carry = op(carry, pardetail::bcast63(x));
       }
     }
     return carry;
@@ -293,11 +349,7 @@ struct WavePar {
         const uint32_t i = start + k;
         if (i < n) tot = op(tot, in(i));
       }
-      T x = tot;
-      for (int o = 1; o < 64; o <<= 1) {
-        T y = pardetail::shfl_up_t(x, o);
-        if ((int)lane >= o) x = op(y, x);
-      }
+      const T x = pardetail::wave_incl_scan(tot, lane, op);
       T excl = pardetail::shfl_up_t(x, 1);
       if (lane == 0) excl = id;
       T run = op(carry, excl);
@@ -309,9 +361,59 @@ struct WavePar {
           run = op(run, v);
         }
       }
-      carry = op(carry, pardetail::shfl_t(x, 63));
+      carry = op(carry, pardetail::bcast63(x));
     }
     return carry;
+  }
+  __device__ __forceinline__ uint32_t reduce_or(uint32_t v) const {
+    for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o);
+    return v;
+  }
+  template <class Pred>
+  __device__ __forceinline__ void mask_bits(uint32_t n, Pred&& pred, uint32_t* bits) const {
+    for (uint32_t base = 0; base < n; base += 64 * kU) {
+      bool p[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t i = base + 64 * u + lane;
+        p[u] = i < n && pred(i);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t b0 = base + 64 * u;
+        const uint64_t m = __ballot(p[u]);
+        if (b0 < n && lane < 2) bits[(b0 >> 5) + lane] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+      }
+    }
+  }
+  template <class T, class Op, class In, class Sel, class Emit>
+  __device__ __forceinline__ uint32_t scan_compact(uint32_t n, T id, Op&& op, In&& in, Sel&& sel,
+                                                   Emit&& emit) const {
+    T carry = id;
+    uint32_t k = 0;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t base0 = 0; base0 < n; base0 += 64 * kU) {
+      T xs[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t i = base0 + 64 * u + lane;
+        xs[u] = i < n ? in(i) : id;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t base = base0 + 64 * u;
+        if (base >= n) break;
+        const uint32_t i = base + lane;
+        const T x = pardetail::wave_incl_scan(xs[u], lane, op);
+        const T incl = op(carry, x);
+        const bool p = i < n && sel(i, incl);
+        const uint64_t m = __ballot(p);
+        if (p) emit(i, k + (uint32_t)__popcll(m & lt), incl);
+        k += (uint32_t)__popcll(m);
+        carry = op(carry, pardetail::bcast63(x));
+      }
+    }
+    return k;
   }
   __device__ __forceinline__ void sync() const { __syncthreads(); }
   __device__ __forceinline__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
@@ -320,6 +422,9 @@ struct WavePar {
   __device__ __forceinline__ bool leader() const { return lane == 0; }
   __device__ __forceinline__ static uint64_t cas64(uint64_t* p, uint64_t cmp, uint64_t val) {
     return atomicCAS((unsigned long long*)p, (unsigned long long)cmp, (unsigned long long)val);
+  }
+  __device__ __forceinline__ static uint32_t cas32(uint32_t* p, uint32_t cmp, uint32_t val) {
+    return atomicCAS(p, cmp, val);
   }
   __device__ __forceinline__ static void min32(uint32_t* p, uint32_t v) { atomicMin(p, v); }
   __device__ __forceinline__ static void min64(uint64_t* p, uint64_t v) {
@@ -455,7 +560,7 @@ struct BlockPar {
       T excl = pardetail::shfl_up_t(x, 1);
       if (lane == 0) excl = id;
       T before, total;
-      cross_wave(pardetail::shfl_t(x, 63), id, op, before, total);
+      cross_wave(pardetail::bcast63(x), id, op, before, total);
       if (i < n) out(i, op(carry, op(before, excl)));
       carry = op(carry, total);
     }
@@ -475,7 +580,7 @@ struct BlockPar {
       T excl = pardetail::shfl_up_t(x, 1);
       if (lane == 0) excl = id;
       T before, total;
-      cross_wave(pardetail::shfl_t(x, 63), id, op, before, total);
+      cross_wave(pardetail::bcast63(x), id, op, before, total);
       T run = op(carry, op(before, excl));
       for (int k = 0; k < K; ++k) {
         const uint32_t i = start + k;
@@ -489,6 +594,48 @@ struct BlockPar {
     }
     return carry;
   }
+  __device__ __forceinline__ uint32_t reduce_or(uint32_t v) const {
+    return block_reduce(v, [](uint32_t a, uint32_t b) { return a | b; });
+  }
+  template <class Pred>
+  __device__ __forceinline__ void mask_bits(uint32_t n, Pred&& pred, uint32_t* bits) const {
+    for (uint32_t base = wid * 64; base < n; base += NT) {
+      const uint32_t i = base + lane;
+      const uint64_t m = __ballot(i < n && pred(i));
+      if (lane < 2) bits[(base >> 5) + lane] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
+    }
+  }
+  template <class T, class Op, class In, class Sel, class Emit>
+  __device__ __forceinline__ uint32_t scan_compact(uint32_t n, T id, Op&& op, In&& in, Sel&& sel,
+                                                   Emit&& emit) const {
+    T carry = id;
+    uint32_t k = 0;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t* cnt = (uint32_t*)(xs + 16 * NW);  // past cross_wave's slots (T <= 16 bytes); xs has 64 B slack
+    for (uint32_t base = 0; base < n; base += NT) {
+      const uint32_t i = base + tid;
+      T x = i < n ? in(i) : id;
+      x = pardetail::wave_incl_scan(x, lane, op);
+      T before, total;
+      cross_wave(pardetail::bcast63(x), id, op, before, total);
+      const T incl = op(carry, op(before, x));
+      const bool p = i < n && sel(i, incl);
+      const uint64_t m = __ballot(p);
+      if (lane == 0) cnt[wid] = (uint32_t)__popcll(m);
+      __syncthreads();
+      uint32_t pre = 0, tot = 0;
+      for (int w = 0; w < NW; ++w) {
+        const uint32_t c = cnt[w];
+        if (w < (int)wid) pre += c;
+        tot += c;
+      }
+      if (p) emit(i, k + pre + (uint32_t)__popcll(m & lt), incl);
+      k += tot;
+      carry = op(carry, total);
+      __syncthreads();
+    }
+    return k;
+  }
   __device__ __forceinline__ void sync() const { __syncthreads(); }
   __device__ __forceinline__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
   template <class F>
@@ -496,6 +643,9 @@ struct BlockPar {
   __device__ __forceinline__ bool leader() const { return tid == 0; }
   __device__ __forceinline__ static uint64_t cas64(uint64_t* p, uint64_t cmp, uint64_t val) {
     return atomicCAS((unsigned long long*)p, (unsigned long long)cmp, (unsigned long long)val);
+  }
+  __device__ __forceinline__ static uint32_t cas32(uint32_t* p, uint32_t cmp, uint32_t val) {
+    return atomicCAS(p, cmp, val);
   }
   __device__ __forceinline__ static void min32(uint32_t* p, uint32_t v) { atomicMin(p, v); }
   __device__ __forceinline__ static void min64(uint64_t* p, uint64_t v) {

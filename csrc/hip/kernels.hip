@@ -45,6 +45,7 @@ __device__ __forceinline__ DocCtx<P> make_ctx(const DevTables& t, const uint64_t
   x.ucd = UcdView{t.s1, t.s2, t.l1, t.l2};
   x.pw = pw;
   x.pw_n = pw_n;
+  x.ipw = pw ? pw + pw_n + 1 : nullptr;
   // scratch slices are laid out in dispatch order (k = position in the launched permutation), so
   // the waves resident at the same time work in one contiguous window of the arena
   x.scr = scratch + scratch_off[k];
@@ -52,6 +53,33 @@ __device__ __forceinline__ DocCtx<P> make_ctx(const DevTables& t, const uint64_t
   x.used = 0;
   x.flag = flags + doc;
   return x;
+}
+
+// Per-wave LDS copies that turn the hottest global reads into LDS reads: the UCD properties of
+// the 128 ASCII code points (every decode looks one up) and, for wave-path documents, the text
+// itself (read by every pass: lead bytes, decoding, hashing, byte verification). The text copy
+// moves whole dwords (the batch buffers are padded, so the up to 3 bytes read past a document's
+// end stay inside the allocation).
+template <class P>
+__device__ __forceinline__ void lds_ascii_props(DocCtx<P>& x) {
+  uint32_t* asc = x.template try_lds<uint32_t>(128);
+  if (!asc) return;
+  x.par.for_n(128, [&](uint32_t c) { asc[c] = x.ucd.props(c); });
+  x.par.sync();
+  x.asc = asc;
+}
+
+template <class P>
+__device__ __forceinline__ const uint8_t* lds_text(DocCtx<P>& x, const uint8_t* b, uint32_t n) {
+  const uintptr_t a0 = (uintptr_t)b & ~(uintptr_t)3;
+  const uint32_t head = (uint32_t)((uintptr_t)b - a0);
+  const uint32_t nd = (head + n + 3) >> 2;
+  uint32_t* d = x.template try_lds<uint32_t>(nd + 1);
+  if (!d) return b;
+  const uint32_t* src = (const uint32_t*)a0;
+  x.par.for_n(nd, [&](uint32_t k) { d[k] = src[k]; });
+  x.par.sync();
+  return (const uint8_t*)d + head;
 }
 
 // C4 pass A leaves src[0] relative to the document's scratch slice (the convention the host
@@ -74,8 +102,9 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
     const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;                                        \
     if (doc >= ndocs || (dead && dead[doc])) return;                                                  \
     DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);   \
-    const uint8_t* b = bytes + off[doc];                                                              \
     const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);                                           \
+    lds_ascii_props(x);                                                                               \
+    const uint8_t* b = lds_text(x, bytes + off[doc], n);                                              \
     StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, lid_vec, lid_cnt};                              \
     analyze_stage<WavePar, false>(x, *stage, *plan, lid_emb, b, n, out); /* LD: k_langid_features */  \
   }
@@ -104,6 +133,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_stage_analyze_blk(
   DocCtx<BlockPar<kBlockThreads>> x =
       make_ctx<BlockPar<kBlockThreads>>(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
   x.par.xs = g_block_xs;
+  lds_ascii_props(x);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, lid_vec, lid_cnt};
@@ -232,6 +262,7 @@ __global__ __launch_bounds__(64) void k_c4_pass_a(
   const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
   if (doc >= ndocs || (dead && dead[doc])) return;  // skipped: record zeros, rewritten length 0
   DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
+  lds_ascii_props(x);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2);
@@ -248,6 +279,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_c4_pass_a_blk(
   DocCtx<BlockPar<kBlockThreads>> x =
       make_ctx<BlockPar<kBlockThreads>>(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
   x.par.xs = g_block_xs;
+  lds_ascii_props(x);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2);
@@ -419,9 +451,13 @@ __global__ __launch_bounds__(256) void k_gate(const DevGate* __restrict__ gate, 
 }
 
 __global__ void k_pow_table(uint64_t* pw, uint32_t n) {
-  // pw[i] = B^i, computed independently per element (exact modular arithmetic)
+  // pw[i] = B^i and pw[n + 1 + i] = B^-i, computed independently per element (exact modular
+  // arithmetic); the buffer holds 2n + 2 entries
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i <= n) pw[i] = powmod61(kHashBase, i);
+  if (i <= n) {
+    pw[i] = powmod61(kHashBase, i);
+    pw[n + 1 + i] = powmod61(kHashBaseInv, i);
+  }
 }
 
 }  // namespace

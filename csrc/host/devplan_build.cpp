@@ -67,6 +67,7 @@ static int add_stop_set(DevPlan& plan, const std::vector<std::string>& words) {
   }
   ss.off[uniq.size()] = pos;
   ss.n = (int32_t)uniq.size();
+  for (auto& w : uniq) ss.max_len = std::max<int32_t>(ss.max_len, (int32_t)w.size());
   return plan.n_stop_sets++;
 }
 
@@ -211,9 +212,14 @@ void gate_host(const DevGate& g, const std::vector<const int64_t*>& recs, int64_
 }
 
 std::vector<uint64_t> pow_table(uint32_t n) {
-  std::vector<uint64_t> pw(n + 1);
+  // [0, n]: B^i, then [n + 1, 2n + 1]: B^-i (the layout tb_pow_table writes on the device)
+  std::vector<uint64_t> pw(2 * (size_t)n + 2);
   pw[0] = 1;
-  for (uint32_t i = 1; i <= n; ++i) pw[i] = mulmod61(pw[i - 1], kHashBase);
+  pw[n + 1] = 1;
+  for (uint32_t i = 1; i <= n; ++i) {
+    pw[i] = mulmod61(pw[i - 1], kHashBase);
+    pw[n + 1 + i] = mulmod61(pw[n + i], kHashBaseInv);
+  }
   return pw;
 }
 
@@ -265,7 +271,8 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
       DocCtx<SeqPar> x;
       x.ucd = ucd;
       x.pw = pw.data();
-      x.pw_n = (uint32_t)pw.size() - 1;
+      x.pw_n = (uint32_t)(pw.size() / 2 - 1);
+      x.ipw = pw.data() + x.pw_n + 1;
       x.scr = scratch.data();
       x.cap = need;
       x.lds = lds_bytes ? lds.data() : nullptr;
@@ -306,7 +313,8 @@ void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int6
       DocCtx<SeqPar> x;
       x.ucd = ucd;
       x.pw = pw.data();
-      x.pw_n = (uint32_t)pw.size() - 1;
+      x.pw_n = (uint32_t)(pw.size() / 2 - 1);
+      x.ipw = pw.data() + x.pw_n + 1;
       x.scr = scratch.data();
       x.cap = need;
       x.lds = lds_bytes ? lds.data() : nullptr;

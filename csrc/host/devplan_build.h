@@ -21,7 +21,7 @@ DevC4 build_c4(const StepCfg& c);
 // Gate (csrc/common/gate.h) over steps: entries = (step index, record slot, record prefix).
 DevGateStep build_gate_step(const StepCfg& c, int slot, int prefix);
 DevGate build_gate(const std::vector<StepCfg>& steps, const std::vector<std::array<int, 3>>& entries);
-std::vector<uint64_t> pow_table(uint32_t n);
+std::vector<uint64_t> pow_table(uint32_t n);  // B^0..B^n followed by B^-0..B^-n
 
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,

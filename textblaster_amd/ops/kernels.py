@@ -86,7 +86,8 @@ class Kernels:
         if n > self._pw_n:
             cap = max(n, 1 << 16)
             cap = 1 << (cap - 1).bit_length()
-            self._pw = self.torch.empty(cap + 1, dtype=self.torch.int64, device=self.device)
+            # B^0..B^cap followed by B^-0..B^-cap (k_pow_table)
+            self._pw = self.torch.empty(2 * cap + 2, dtype=self.torch.int64, device=self.device)
             _check(self.lib.tb_pow_table(self.stream(), self._pw.data_ptr(), cap), "tb_pow_table")
             self._pw_n = cap
         return self._pw, self._pw_n

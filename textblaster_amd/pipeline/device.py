@@ -127,7 +127,7 @@ class DeviceRunner:
     # per-wave LDS slices: the stage kernel is built for 4 waves/SIMD (128 VGPRs) = 16 waves/CU, so
     # 10 KB each costs no occupancy; the C4 kernel (7 waves/SIMD) only keeps per-line arrays there
     DEFAULT_LDS_BYTES = 10240
-    DEFAULT_LDS_BYTES_C4 = 2048
+    DEFAULT_LDS_BYTES_C4 = 2560
     DEFAULT_LONG_DOC_BYTES = 8192
     DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; sweep: tools/occ_sweep.sh)
 
@@ -331,7 +331,7 @@ class DeviceRunner:
     def phase_report(self) -> str:
         names = {0: "start", 1: "decode", 2: "dict", 3: "prefix_hash", 4: "words", 5: "lines", 6: "gopher_quality",
                  7: "gr_lines_paras", 8: "gr_word_hash", 9: "gr_top_ngrams", 10: "gr_dup_ngrams", 11: "fineweb",
-                 12: "langid", 16: "c4_lorem", 17: "c4_decode", 18: "c4_lines", 19: "c4_cite", 20: "c4_words",
+                 12: "langid", 13: "gr_dup_walk", 14: "gr_dup_canon", 15: "gr_top_canon", 16: "c4_lorem", 17: "c4_decode", 18: "c4_lines", 19: "c4_cite", 20: "c4_words",
                  21: "c4_codes", 22: "c4_join", 23: "c4_sentences"}
         lines = []
         for k, tot in self.phase_totals.items():

@@ -4,6 +4,7 @@
 #include <cstring>
 #include <unordered_set>
 
+#include "json.h"
 #include "rustfmt.h"
 
 namespace tb {
@@ -217,42 +218,138 @@ void compute_record(const StepCfg& c, std::string_view text, SegBackend be, int6
 }
 
 // ------------------------------------------------------------------------------------------
-static std::string f2(double x) { return fmt_fixed(x, 2); }
-static std::string f4(double x) { return fmt_fixed(x, 4); }
+// ------------------------------------------------------------------------------------------
+// Decisions. One implementation of every step's decision logic (decide_t), instantiated with
+// three sinks:
+//   StatusSink    pass / filtered / error only (the per-batch resolve hot path: no text at all)
+//   DecisionSink  + reason string and metadata pairs (per-document API, host steps)
+//   JsonSink      + the step's metadata appended as JSON members straight into the output
+//                 column buffer (output assembly: no per-document allocations)
+// Reasons and values are built by appending into reusable buffers with the allocation-free
+// Rust formatters of rustfmt.h; the sinks decide what is kept. Every instance takes exactly the
+// same branches, so status, reasons and metadata cannot disagree.
 
-// One implementation of every step's decision logic, instantiated twice: kFmt=false only
-// derives pass/filtered/error (the per-batch resolve hot path: no strings are built),
-// kFmt=true also formats the reason and the step's metadata (output assembly, per-document
-// API). String-building expressions are wrapped in lambdas that the kFmt=false instance never
-// calls, so both instances take exactly the same branches.
-template <bool kFmt>
-static void decide_t(const StepCfg& c, const int64_t* r, Decision& d) {
-  d.pass = true;
-  d.error = false;
-  if constexpr (kFmt) {
-    d.reason.clear();
-    d.meta.clear();
+namespace {
+
+struct Arg {  // one piece of a formatted message
+  enum K { S, I, F2, F4, F64 } k;
+  std::string_view s;
+  int64_t i = 0;
+  double d = 0;
+};
+inline Arg A(std::string_view s) { return Arg{Arg::S, s}; }
+inline Arg A(const char* s) { return Arg{Arg::S, std::string_view(s)}; }
+inline Arg A(int64_t v) { Arg a{Arg::I, {}}; a.i = v; return a; }
+inline Arg F2(double v) { Arg a{Arg::F2, {}}; a.d = v; return a; }
+inline Arg F4(double v) { Arg a{Arg::F4, {}}; a.d = v; return a; }
+inline Arg F64(double v) { Arg a{Arg::F64, {}}; a.d = v; return a; }
+
+inline void put(CharBuf& out, const Arg& a) {
+  switch (a.k) {
+    case Arg::S: out.append(a.s.data(), a.s.size()); break;
+    case Arg::I: append_i64(out, a.i); break;
+    case Arg::F2: append_fixed(out, a.d, 2); break;
+    case Arg::F4: append_fixed(out, a.d, 4); break;
+    case Arg::F64: append_f64(out, a.d); break;
   }
-  std::vector<std::string> reasons;
-  int nreasons = 0;
-  auto add = [&](auto&& mk) {
-    ++nreasons;
-    if constexpr (kFmt) reasons.push_back(mk());
+}
+inline void cat(CharBuf& out, std::initializer_list<Arg> args) {
+  for (const Arg& a : args) put(out, a);
+}
+
+struct StatusSink {
+  static constexpr bool kFmt = false;
+  bool pass = true, error = false;
+  void fail() { pass = false; }
+  void fail_error() { pass = false; error = true; }
+  void reason(std::initializer_list<Arg>) {}
+  void set_reason(std::initializer_list<Arg>) {}
+  void meta(std::string_view, std::initializer_list<Arg>) {}
+  void meta_reasons(std::string_view) {}
+};
+
+// Shared by the formatting sinks: reasons joined with "; ".
+struct ReasonBuf {
+  CharBuf r;
+  bool any = false;
+  void add(std::initializer_list<Arg> args) {
+    if (any) r.append("; ", 2);
+    any = true;
+    cat(r, args);
+  }
+  void set(std::initializer_list<Arg> args) {
+    r.clear();
+    any = true;
+    cat(r, args);
+  }
+};
+
+struct DecisionSink {
+  static constexpr bool kFmt = true;
+  Decision& d;
+  ReasonBuf rb;
+  CharBuf tmp;
+  explicit DecisionSink(Decision& dd) : d(dd) {}
+  void fail() { d.pass = false; }
+  void fail_error() { d.pass = false; d.error = true; }
+  void reason(std::initializer_list<Arg> args) { rb.add(args); }
+  void set_reason(std::initializer_list<Arg> args) { rb.set(args); }
+  void meta(std::string_view k, std::initializer_list<Arg> args) {
+    tmp.clear();
+    cat(tmp, args);
+    d.meta.emplace_back(k, std::string(tmp.view()));
+  }
+  void meta_reasons(std::string_view k) { d.meta.emplace_back(k, std::string(rb.r.view())); }
+  void finish() { d.reason = std::string(rb.r.view()); }
+};
+
+struct JsonSink {
+  static constexpr bool kFmt = true;
+  CharBuf& out;
+  bool& first;
+  ReasonBuf& rb;
+  CharBuf& tmp;
+  bool pass = true, error = false;
+  void fail() { pass = false; }
+  void fail_error() { pass = false; error = true; }
+  void reason(std::initializer_list<Arg> args) { rb.add(args); }
+  void set_reason(std::initializer_list<Arg> args) { rb.set(args); }
+  void member(std::string_view k, std::string_view v) {
+    // keys are literals of this file (plain ASCII, nothing to escape)
+    out.reserve(k.size() + 5);
+    if (!first) out.p[out.n++] = ',';
+    first = false;
+    out.p[out.n++] = '"';
+    std::memcpy(out.p + out.n, k.data(), k.size());
+    out.n += k.size();
+    out.p[out.n++] = '"';
+    out.p[out.n++] = ':';
+    json_escape_append(out, v);
+  }
+  void meta(std::string_view k, std::initializer_list<Arg> args) {
+    tmp.clear();
+    cat(tmp, args);
+    member(k, tmp.view());
+  }
+  void meta_reasons(std::string_view k) { member(k, rb.r.view()); }
+};
+
+}  // namespace
+
+template <class Sink>
+static void decide_t(const StepCfg& c, const int64_t* r, Sink& k) {
+  bool any = false;  // at least one reason
+  auto add = [&](std::initializer_list<Arg> args) {
+    any = true;
+    k.reason(args);
   };
-  auto meta = [&](std::string_view k, auto&& mk) {
-    if constexpr (kFmt) d.meta.emplace_back(k, mk());
-  };
-  auto lit = [](const char* s) { return [s]() { return std::string(s); }; };
   auto finish_multi = [&](std::string_view status_key, std::string_view reasons_key) {
-    if (nreasons) {
-      d.pass = false;
-      if constexpr (kFmt) {
-        d.reason = join(reasons, "; ");
-        d.meta.emplace_back(status_key, "filtered");
-        d.meta.emplace_back(reasons_key, d.reason);
-      }
+    if (any) {
+      k.fail();
+      k.meta(status_key, {A("filtered")});
+      k.meta_reasons(reasons_key);
     } else {
-      meta(status_key, lit("passed"));
+      k.meta(status_key, {A("passed")});
     }
   };
   switch (c.kind) {
@@ -267,49 +364,41 @@ static void decide_t(const StepCfg& c, const int64_t* r, Decision& d) {
       const double ell_lines = (double)r[rec::GQ_ELL_LINES] / lcalc;
       const double alpha = (double)r[rec::GQ_ALPHA] / ncalc;
       if (c.min_doc_words && n < *c.min_doc_words)
-        add([&] { return "gopher_short_doc (" + std::to_string(n) + " non-symbol words, required " +
-                         std::to_string(*c.min_doc_words) + ")"; });
+        add({A("gopher_short_doc ("), A(n), A(" non-symbol words, required "), A(*c.min_doc_words), A(")")});
       if (c.max_doc_words && n > *c.max_doc_words)
-        add([&] { return "gopher_long_doc (" + std::to_string(n) + " non-symbol words, max " +
-                         std::to_string(*c.max_doc_words) + ")"; });
+        add({A("gopher_long_doc ("), A(n), A(" non-symbol words, max "), A(*c.max_doc_words), A(")")});
       if (c.min_avg_word_length && avg < *c.min_avg_word_length)
-        add([&] { return "gopher_below_avg_threshold (avg len " + f2(avg) + ", required " +
-                         f2(*c.min_avg_word_length) +
-                         ((n == 0 && *c.min_avg_word_length > 0.0) ? " - 0 non-symbol words" : "") + ")"; });
+        add({A("gopher_below_avg_threshold (avg len "), F2(avg), A(", required "), F2(*c.min_avg_word_length),
+             A((n == 0 && *c.min_avg_word_length > 0.0) ? " - 0 non-symbol words" : ""), A(")")});
       if (c.max_avg_word_length && n > 0 && avg > *c.max_avg_word_length)
-        add([&] { return "gopher_above_avg_threshold (avg len " + f2(avg) + ", max " +
-                         f2(*c.max_avg_word_length) + ")"; });
+        add({A("gopher_above_avg_threshold (avg len "), F2(avg), A(", max "), F2(*c.max_avg_word_length), A(")")});
       if (c.max_symbol_word_ratio) {
         if (hash_ratio > *c.max_symbol_word_ratio)
-          add([&] { return "gopher_too_many_hashes (ratio " + f2(hash_ratio) + ", max " +
-                           f2(*c.max_symbol_word_ratio) + ")"; });
+          add({A("gopher_too_many_hashes (ratio "), F2(hash_ratio), A(", max "), F2(*c.max_symbol_word_ratio), A(")")});
         if (ell_ratio > *c.max_symbol_word_ratio)
-          add([&] { return "gopher_too_many_ellipsis_units (ratio " + f2(ell_ratio) + ", max " +
-                           f2(*c.max_symbol_word_ratio) + ")"; });
+          add({A("gopher_too_many_ellipsis_units (ratio "), F2(ell_ratio), A(", max "), F2(*c.max_symbol_word_ratio),
+               A(")")});
       }
       if (c.max_bullet_lines_ratio && bullet > *c.max_bullet_lines_ratio)
-        add([&] { return "gopher_too_many_bullets (ratio " + f2(bullet) + ", max " +
-                         f2(*c.max_bullet_lines_ratio) + ")"; });
+        add({A("gopher_too_many_bullets (ratio "), F2(bullet), A(", max "), F2(*c.max_bullet_lines_ratio), A(")")});
       if (c.max_ellipsis_lines_ratio && ell_lines > *c.max_ellipsis_lines_ratio)
-        add([&] { return "gopher_too_many_end_ellipsis_lines (ratio " + f2(ell_lines) + ", max " +
-                         f2(*c.max_ellipsis_lines_ratio) + ")"; });
+        add({A("gopher_too_many_end_ellipsis_lines (ratio "), F2(ell_lines), A(", max "),
+             F2(*c.max_ellipsis_lines_ratio), A(")")});
       if (c.max_non_alpha_words_ratio && alpha < *c.max_non_alpha_words_ratio)
-        add([&] { return "gopher_below_alpha_threshold (alpha ratio " + f2(alpha) + ", required min " +
-                         f2(*c.max_non_alpha_words_ratio) + ")"; });
+        add({A("gopher_below_alpha_threshold (alpha ratio "), F2(alpha), A(", required min "),
+             F2(*c.max_non_alpha_words_ratio), A(")")});
       if (c.min_stop_words && *c.min_stop_words > 0 && r[rec::GQ_STOP] < *c.min_stop_words)
-        add([&] { return "gopher_too_few_stop_words (found " + std::to_string(r[rec::GQ_STOP]) + ", required " +
-                         std::to_string(*c.min_stop_words) + ")"; });
+        add({A("gopher_too_few_stop_words (found "), A(r[rec::GQ_STOP]), A(", required "), A(*c.min_stop_words),
+             A(")")});
       finish_multi("gopher_quality_filter_status", "gopher_quality_filter_reasons");
       return;
     }
     case StepKind::GopherRepetition: {  // reference gopher_rep.rs:52-220
       if (r[rec::GR_CHARS] < 0) {
-        d.pass = false;
-        if constexpr (kFmt) {
-          d.reason = "skipping empty content";
-          d.meta.emplace_back("gopher_repetition_filter_status", "filtered");
-          d.meta.emplace_back("gopher_repetition_filter_reason", "skipping empty content");
-        }
+        k.fail();
+        k.set_reason({A("skipping empty content")});
+        k.meta("gopher_repetition_filter_status", {A("filtered")});
+        k.meta("gopher_repetition_filter_reason", {A("skipping empty content")});
         return;
       }
       const double C = (double)std::max<int64_t>(1, r[rec::GR_CHARS]);
@@ -318,140 +407,135 @@ static void decide_t(const StepCfg& c, const int64_t* r, Decision& d) {
       double v;
       v = (double)r[rec::GR_PARA_DUP] / para_len;
       if (c.dup_para_frac && v > *c.dup_para_frac)
-        add([&] { return "dup_para_frac (ratio " + f2(v) + ", max " + f2(*c.dup_para_frac) + ")"; });
+        add({A("dup_para_frac (ratio "), F2(v), A(", max "), F2(*c.dup_para_frac), A(")")});
       v = (double)r[rec::GR_PARA_DUP_BYTES] / C;
       if (c.dup_para_char_frac && v > *c.dup_para_char_frac)
-        add([&] { return "dup_para_char_frac (ratio " + f2(v) + ", max " + f2(*c.dup_para_char_frac) + ")"; });
+        add({A("dup_para_char_frac (ratio "), F2(v), A(", max "), F2(*c.dup_para_char_frac), A(")")});
       v = (double)r[rec::GR_LINE_DUP] / line_len;
       if (c.dup_line_frac && v > *c.dup_line_frac)
-        add([&] { return "dup_line_frac (ratio " + f2(v) + ", max " + f2(*c.dup_line_frac) + ")"; });
+        add({A("dup_line_frac (ratio "), F2(v), A(", max "), F2(*c.dup_line_frac), A(")")});
       v = (double)r[rec::GR_LINE_DUP_BYTES] / C;
       if (c.dup_line_char_frac && v > *c.dup_line_char_frac)
-        add([&] { return "dup_line_char_frac (ratio " + f2(v) + ", max " + f2(*c.dup_line_char_frac) + ")"; });
-      int k = rec::GR_FIXED;
+        add({A("dup_line_char_frac (ratio "), F2(v), A(", max "), F2(*c.dup_line_char_frac), A(")")});
+      int kk = rec::GR_FIXED;
       for (auto& e : c.top_n_grams) {
-        v = (double)r[k++] / C;
+        v = (double)r[kk++] / C;
         if (e.first > 0 && v > e.second)
-          add([&] { return "top_" + std::to_string(e.first) + "_gram (ratio " + f2(v) + ", max " + f2(e.second) + ")"; });
+          add({A("top_"), A(e.first), A("_gram (ratio "), F2(v), A(", max "), F2(e.second), A(")")});
       }
       for (auto& e : c.dup_n_grams) {
-        v = (double)r[k++] / C;
+        v = (double)r[kk++] / C;
         if (e.first > 0 && v > e.second)
-          add([&] { return "duplicated_" + std::to_string(e.first) + "_n_grams (ratio " + f2(v) + ", max " +
-                           f2(e.second) + ")"; });
+          add({A("duplicated_"), A(e.first), A("_n_grams (ratio "), F2(v), A(", max "), F2(e.second), A(")")});
       }
       finish_multi("gopher_repetition_filter_status", "gopher_repetition_filter_reasons");
       return;
     }
     case StepKind::C4Quality: {  // reference c4_filters.rs:147-295
-      if (r[rec::C4_LOREM]) add(lit("lorem_ipsum"));
-      if (r[rec::C4_CURLY]) add(lit("curly_bracket"));
-      if (nreasons) {
+      if (r[rec::C4_LOREM]) add({A("lorem_ipsum")});
+      if (r[rec::C4_CURLY]) add({A("curly_bracket")});
+      if (any) {
         finish_multi("c4_filter_status", "c4_filter_reasons");
         return;
       }
       if (c.min_num_sentences > 0 && r[rec::C4_SENTENCES] < c.min_num_sentences) {
-        d.pass = false;
-        if constexpr (kFmt) {
-          d.reason = "too_few_sentences (found " + std::to_string(r[rec::C4_SENTENCES]) + ", required " +
-                     std::to_string(c.min_num_sentences) + ")";
-          d.meta.emplace_back("c4_filter_status", "filtered");
-          d.meta.emplace_back("c4_filter_reasons", d.reason);
-          if (r[rec::C4_TOO_LONG]) d.meta.emplace_back("line-filter-too_long_word", std::to_string(r[rec::C4_TOO_LONG]));
-          if (r[rec::C4_NO_PUNCT]) d.meta.emplace_back("line-filter-no_terminal_punc", std::to_string(r[rec::C4_NO_PUNCT]));
-          if (r[rec::C4_TOO_FEW]) d.meta.emplace_back("line-filter-too_few_words", std::to_string(r[rec::C4_TOO_FEW]));
-        }
+        k.fail();
+        k.set_reason({A("too_few_sentences (found "), A(r[rec::C4_SENTENCES]), A(", required "),
+                      A(c.min_num_sentences), A(")")});
+        k.meta("c4_filter_status", {A("filtered")});
+        k.meta_reasons("c4_filter_reasons");
+        if (r[rec::C4_TOO_LONG]) k.meta("line-filter-too_long_word", {A(r[rec::C4_TOO_LONG])});
+        if (r[rec::C4_NO_PUNCT]) k.meta("line-filter-no_terminal_punc", {A(r[rec::C4_NO_PUNCT])});
+        if (r[rec::C4_TOO_FEW]) k.meta("line-filter-too_few_words", {A(r[rec::C4_TOO_FEW])});
         return;
       }
-      meta("c4_filter_status", lit("passed"));
+      k.meta("c4_filter_status", {A("passed")});
       return;
     }
     case StepKind::FineWebQuality: {  // reference fineweb_quality.rs:71-226
-      auto fail = [&](auto&& mk_reason, auto&& mk_meta) {
-        d.pass = false;
-        if constexpr (kFmt) {
-          d.reason = mk_reason();
-          d.meta.emplace_back("fineweb_filter_status", "filtered");
-          d.meta.emplace_back("fineweb_filter_reason", mk_meta());
-        }
+      auto fail = [&](std::initializer_list<Arg> reason, std::initializer_list<Arg> meta_value) {
+        k.fail();
+        k.set_reason(reason);
+        k.meta("fineweb_filter_status", {A("filtered")});
+        k.meta("fineweb_filter_reason", meta_value);
       };
       const int64_t nl = r[rec::FW_LINES];
-      if (nl == 0) { fail(lit("empty"), lit("empty document")); return; }
+      if (nl == 0) { fail({A("empty")}, {A("empty document")}); return; }
       double ratio = (double)r[rec::FW_STOP_END] / (double)nl;
       if (ratio < c.line_punct_thr && !(ratio == 0.0 && c.line_punct_exclude_zero)) {
-        auto mk = [&] {
-          return "line_punct_ratio: " + f4(ratio) + " < threshold " + f4(c.line_punct_thr) + " (exclude_zero: " +
-                 (c.line_punct_exclude_zero ? "true" : "false") + ")";
-        };
-        fail(mk, mk);
+        const std::initializer_list<Arg> m = {A("line_punct_ratio: "), F4(ratio), A(" < threshold "),
+                                              F4(c.line_punct_thr), A(" (exclude_zero: "),
+                                              A(c.line_punct_exclude_zero ? "true" : "false"), A(")")};
+        fail(m, m);
         return;
       }
       ratio = (double)r[rec::FW_SHORT] / (double)nl;
       if (ratio > c.short_line_thr) {
-        auto mk = [&] { return "short_line_ratio: " + f4(ratio) + " > threshold " + f4(c.short_line_thr); };
-        fail(mk, mk);
+        const std::initializer_list<Arg> m = {A("short_line_ratio: "), F4(ratio), A(" > threshold "),
+                                              F4(c.short_line_thr)};
+        fail(m, m);
         return;
       }
       const int64_t tot = r[rec::FW_CHARS_NO_NL];
       ratio = tot > 0 ? (double)r[rec::FW_DUP_BYTES] / (double)tot : 0.0;
       if (ratio > c.char_duplicates_ratio) {
-        auto mk = [&] { return "char_dup_ratio: " + f4(ratio) + " > threshold " + f4(c.char_duplicates_ratio); };
-        fail(mk, mk);
+        const std::initializer_list<Arg> m = {A("char_dup_ratio: "), F4(ratio), A(" > threshold "),
+                                              F4(c.char_duplicates_ratio)};
+        fail(m, m);
         return;
       }
       const int64_t w = r[rec::FW_WORDS], nls = r[rec::FW_NL];
       if (w == 0) {
         if (nls > 0) {
-          auto mk = lit("list_ratio_no_words (newlines present but no words)");
-          fail(mk, mk);
+          const std::initializer_list<Arg> m = {A("list_ratio_no_words (newlines present but no words)")};
+          fail(m, m);
         }
         return;
       }
       ratio = (double)nls / (double)w;
       if (ratio > c.new_line_ratio) {
-        auto mk = [&] { return "list_ratio: " + f4(ratio) + " > threshold " + f4(c.new_line_ratio); };
-        fail(mk, mk);
+        const std::initializer_list<Arg> m = {A("list_ratio: "), F4(ratio), A(" > threshold "), F4(c.new_line_ratio)};
+        fail(m, m);
       }
       return;
     }
     case StepKind::LanguageDetection: {  // reference language_filter.rs:35-93
       const int64_t lang = r[rec::LD_LANG];
       if (lang < 0) {
-        d.pass = false;
-        if constexpr (kFmt) d.reason = "Language could not be confidently detected";
+        k.fail();
+        k.set_reason({A("Language could not be confidently detected")});
         return;
       }
       double conf;
       std::memcpy(&conf, &r[rec::LD_CONF_BITS], sizeof(double));
-      meta("Detected language", [&] { return std::string(kLangNames[lang]); });
-      meta("Detected language confidence", [&] { return fmt_f64(conf); });
+      k.meta("Detected language", {A(kLangNames[lang])});
+      k.meta("Detected language confidence", {F64(conf)});
       bool allowed = std::find(c.allowed_langs.begin(), c.allowed_langs.end(), (int)lang) != c.allowed_langs.end();
       if (!allowed) {
-        d.pass = false;
-        if constexpr (kFmt) {
+        k.fail();
+        if constexpr (Sink::kFmt) {
           std::string joined;
           for (size_t i = 0; i < c.allowed_codes.size(); ++i) {
             if (i) joined += "; ";
             joined += c.allowed_codes[i];
           }
-          d.reason = "Document is not any of the following languages: " + fmt_debug_str(joined);
+          const std::string dbg = fmt_debug_str(joined);
+          k.set_reason({A("Document is not any of the following languages: "), A(std::string_view(dbg))});
         }
       } else if (conf < c.min_confidence) {
-        d.pass = false;
-        if constexpr (kFmt)
-          d.reason = "Language detection confidence is not satified: " + fmt_f64(conf) + " < " +
-                     fmt_f64(c.min_confidence);
+        k.fail();
+        k.set_reason({A("Language detection confidence is not satified: "), F64(conf), A(" < "),
+                      F64(c.min_confidence)});
       }
       return;
     }
     case StepKind::TokenCounter: {  // reference token_counter.rs:31-42
       if (r[rec::TC_COUNT] < 0) {
-        d.pass = false;
-        d.error = true;
-        if constexpr (kFmt) d.reason = "TokenCounter failed";
+        k.fail_error();
+        k.set_reason({A("TokenCounter failed")});
         return;
       }
-      meta("token_count", [&] { return std::to_string(r[rec::TC_COUNT]); });
+      k.meta("token_count", {A(r[rec::TC_COUNT])});
       return;
     }
     case StepKind::C4BadWords:
@@ -459,12 +543,29 @@ static void decide_t(const StepCfg& c, const int64_t* r, Decision& d) {
   }
 }
 
-void decide(const StepCfg& c, const int64_t* r, Decision& d) { decide_t<true>(c, r, d); }
+void decide(const StepCfg& c, const int64_t* r, Decision& d) {
+  d.pass = true;
+  d.error = false;
+  d.reason.clear();
+  d.meta.clear();
+  DecisionSink k(d);
+  decide_t(c, r, k);
+  k.finish();
+}
 
 uint8_t decide_status(const StepCfg& c, const int64_t* r) {
-  Decision d;
-  decide_t<false>(c, r, d);
-  return d.pass ? 0 : (d.error ? 2 : 1);
+  StatusSink k;
+  decide_t(c, r, k);
+  return k.pass ? 0 : (k.error ? 2 : 1);
+}
+
+void decide_meta_json(const StepCfg& c, const int64_t* r, CharBuf& out, bool& first) {
+  thread_local ReasonBuf rb;
+  thread_local CharBuf tmp;
+  rb.r.clear();
+  rb.any = false;
+  JsonSink k{out, first, rb, tmp};
+  decide_t(c, r, k);
 }
 
 }  // namespace tb

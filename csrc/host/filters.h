@@ -12,6 +12,7 @@
 #include <utility>
 #include <vector>
 
+#include "rustfmt.h"
 #include "text.h"
 
 namespace tb {
@@ -109,6 +110,9 @@ struct Decision {
 void decide(const StepCfg& c, const int64_t* r, Decision& d);
 // Same branches without building any string: 0 pass, 1 filtered, 2 error.
 uint8_t decide_status(const StepCfg& c, const int64_t* r);
+// Same branches; appends the step's metadata as JSON object members ("k":"v", comma-separated,
+// `first` tracks the leading comma) to `out` without per-call allocations (output assembly).
+void decide_meta_json(const StepCfg& c, const int64_t* r, CharBuf& out, bool& first);
 
 // CPU computation of a step record on `text` (the step's input content version).
 // For C4Quality, `new_content` receives the rewritten content.

@@ -1,6 +1,7 @@
 #include "json.h"
 
 #include <cstdint>
+#include <cstring>
 
 namespace tb {
 
@@ -180,33 +181,6 @@ bool FlatMeta::has(std::string_view k) const {
   for (auto& x : e)
     if (key(x) == k) return true;
   return false;
-}
-
-void json_escape_append(std::string& out, std::string_view s) {
-  static const char* hex = "0123456789abcdef";
-  out.push_back('"');
-  size_t run = 0;  // start of the pending run of bytes that need no escaping
-  for (size_t i = 0; i < s.size(); ++i) {
-    const unsigned char c = (unsigned char)s[i];
-    if (c >= 0x20 && c != '"' && c != '\\') continue;
-    out.append(s.data() + run, i - run);
-    run = i + 1;
-    switch (c) {
-      case '"': out += "\\\""; break;
-      case '\\': out += "\\\\"; break;
-      case '\n': out += "\\n"; break;
-      case '\r': out += "\\r"; break;
-      case '\t': out += "\\t"; break;
-      case '\b': out += "\\b"; break;
-      case '\f': out += "\\f"; break;
-      default:
-        out += "\\u00";
-        out.push_back(hex[c >> 4]);
-        out.push_back(hex[c & 15]);
-    }
-  }
-  out.append(s.data() + run, s.size() - run);
-  out.push_back('"');
 }
 
 void serialize_meta_json(const MetaMap& m, std::string& out) {

@@ -3,6 +3,7 @@
 // and serde_json::to_string(&HashMap<String,String>) (parquet_writer.rs:107) on output.
 #pragma once
 #include <cstdint>
+#include <cstring>
 #include <string>
 #include <string_view>
 #include <utility>
@@ -32,7 +33,54 @@ struct FlatMeta {
 bool parse_meta_json(std::string_view s, MetaMap& out);
 bool parse_meta_json(std::string_view s, FlatMeta& out);
 
-void json_escape_append(std::string& out, std::string_view s);
+// True if any of the 8 bytes is < 0x20, '"' or '\\' (SWAR: "has a zero byte" tests).
+inline bool json_word_needs_escape(uint64_t x) {
+  constexpr uint64_t kOnes = 0x0101010101010101ull, kHigh = 0x8080808080808080ull;
+  const uint64_t lt20 = (x - 0x2020202020202020ull) & ~x & kHigh;
+  const uint64_t q = x ^ 0x2222222222222222ull, bs = x ^ 0x5C5C5C5C5C5C5C5Cull;
+  const uint64_t zq = (q - kOnes) & ~q & kHigh, zb = (bs - kOnes) & ~bs & kHigh;
+  return (lt20 | zq | zb) != 0;
+}
+
+template <class Out>
+inline void json_escape_append(Out& out, std::string_view s) {
+  static const char* hex = "0123456789abcdef";
+  out.push_back('"');
+  size_t run = 0;  // start of the pending run of bytes that need no escaping
+  size_t i = 0;
+  const size_t n = s.size();
+  while (i < n) {
+    // skip clean 8-byte words in bulk (the common case: generated ASCII values)
+    while (i + 8 <= n) {
+      uint64_t w;
+      std::memcpy(&w, s.data() + i, 8);
+      if (json_word_needs_escape(w)) break;
+      i += 8;
+    }
+    if (i >= n) break;
+    const unsigned char c = (unsigned char)s[i];
+    if (c >= 0x20 && c != '"' && c != '\\') { ++i; continue; }
+    out.append(s.data() + run, i - run);
+    run = i + 1;
+    switch (c) {
+      case '"': out += "\\\""; break;
+      case '\\': out += "\\\\"; break;
+      case '\n': out += "\\n"; break;
+      case '\r': out += "\\r"; break;
+      case '\t': out += "\\t"; break;
+      case '\b': out += "\\b"; break;
+      case '\f': out += "\\f"; break;
+      default:
+        out += "\\u00";
+        out.push_back(hex[c >> 4]);
+        out.push_back(hex[c & 15]);
+    }
+    ++i;
+  }
+  out.append(s.data() + run, n - run);
+  out.push_back('"');
+}
+
 void serialize_meta_json(const MetaMap& m, std::string& out);
 
 // Insert-or-overwrite with HashMap semantics (position of an existing key is kept).

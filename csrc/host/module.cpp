@@ -200,6 +200,7 @@ PYBIND11_MODULE(_tbhost, m) {
                           to_numpy(std::move(l2)));
   });
   m.def("fmt_f64", [](double x) { return fmt_f64(x); });
+  m.def("fmt_fixed", [](double x, int prec) { return fmt_fixed(x, prec); });
 
   // ---- per-step records and decisions ----
   m.def("compute_record", [](const StepCfg& c, const std::string& text, const std::string& be) {

@@ -3,9 +3,11 @@
 #include <unicode/uchar.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <fstream>
+#include <condition_variable>
 #include <mutex>
 #include <random>
 #include <sstream>
@@ -14,24 +16,94 @@
 
 namespace tb {
 
+// Persistent worker pool shared by every parallel_for of the process (resolve, assembly,
+// staging copies, emulation, HTML decoding). Several Python threads submit jobs concurrently;
+// each job is a chunk counter that its caller and up to nthreads-1 pool workers drain. The
+// caller always works on its own job, so a job completes even when every worker is busy
+// elsewhere. Workers live for the whole process (no per-call thread creation).
+namespace {
+struct PoolJob {
+  const std::function<void(int64_t)>* fn;
+  int64_t nchunks;
+  int max_helpers;
+  std::atomic<int64_t> next{0};
+  std::atomic<int64_t> done{0};
+  int helpers = 0;   // workers that took the job (guarded by the pool mutex)
+  int active = 0;    // workers still inside work() (guarded by the pool mutex)
+  void work() {
+    int64_t c;
+    while ((c = next.fetch_add(1, std::memory_order_relaxed)) < nchunks) {
+      (*fn)(c);
+      done.fetch_add(1, std::memory_order_release);
+    }
+  }
+};
+
+class WorkerPool {
+ public:
+  static WorkerPool& get() {
+    static WorkerPool* p = new WorkerPool();  // leaked on purpose: workers outlive statics
+    return *p;
+  }
+  void run(int64_t nchunks, int nthreads, const std::function<void(int64_t)>& fn) {
+    PoolJob job;
+    job.fn = &fn;
+    job.nchunks = nchunks;
+    job.max_helpers = std::max(0, nthreads - 1);
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      while ((int)workers_.size() < job.max_helpers) workers_.emplace_back([this] { loop(); });
+      jobs_.push_back(&job);
+    }
+    cv_.notify_all();
+    job.work();
+    std::unique_lock<std::mutex> g(mu_);
+    for (size_t i = 0; i < jobs_.size(); ++i)
+      if (jobs_[i] == &job) { jobs_.erase(jobs_.begin() + (long)i); break; }
+    // chunks taken by workers may still be running; the job lives on this stack frame
+    done_cv_.wait(g, [&] { return job.active == 0 && job.done.load(std::memory_order_acquire) == nchunks; });
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> g(mu_);
+    while (true) {
+      PoolJob* j = nullptr;
+      cv_.wait(g, [&] {
+        for (PoolJob* c : jobs_)
+          if (c->helpers < c->max_helpers && c->next.load(std::memory_order_relaxed) < c->nchunks) { j = c; return true; }
+        return false;
+      });
+      ++j->helpers;
+      ++j->active;
+      g.unlock();
+      j->work();
+      g.lock();
+      --j->active;
+      done_cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<PoolJob*> jobs_;
+  std::vector<std::thread> workers_;
+};
+}  // namespace
+
+void parallel_tasks(int64_t ntasks, int nthreads, const std::function<void(int64_t)>& fn) {
+  if (ntasks <= 0) return;
+  if (nthreads <= 1 || ntasks == 1) {
+    for (int64_t c = 0; c < ntasks; ++c) fn(c);
+    return;
+  }
+  WorkerPool::get().run(ntasks, (int)std::min<int64_t>(nthreads, ntasks), fn);
+}
+
 void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t, int64_t)>& fn) {
   if (n <= 0) return;
   if (nthreads <= 1 || n < 256) { fn(0, n); return; }
   const int64_t chunks = std::min<int64_t>((int64_t)nthreads * 8, (n + 63) / 64);
-  std::atomic<int64_t> next{0};
-  auto worker = [&]() {
-    while (true) {
-      int64_t c = next.fetch_add(1);
-      if (c >= chunks) break;
-      int64_t a = n * c / chunks, b = n * (c + 1) / chunks;
-      fn(a, b);
-    }
-  };
-  std::vector<std::thread> ts;
-  int nt = (int)std::min<int64_t>(nthreads, chunks);
-  for (int t = 1; t < nt; ++t) ts.emplace_back(worker);
-  worker();
-  for (auto& t : ts) t.join();
+  parallel_tasks(chunks, nthreads, [&](int64_t c) { fn(n * c / chunks, n * (c + 1) / chunks); });
 }
 
 // ------------------------------------------------------------------------------------------
@@ -532,12 +604,71 @@ void BatchState::step_meta(int64_t doc, int s, Decision& d) const {
   decide(*sr.cfg, sr.rec + doc * sr.width, d);
 }
 
+int BatchState::step_kind(int s) const {
+  if (s < (int)bw_.size() && bw_[s]) return (int)StepKind::C4BadWords;
+  if (s < (int)recs_.size() && recs_[s].cfg) return (int)recs_[s].cfg->kind;
+  return -1;
+}
+
+static void json_member(CharBuf& out, bool& first, std::string_view k, std::string_view v) {
+  if (!first) out.push_back(',');
+  first = false;
+  json_escape_append(out, k);
+  out.push_back(':');
+  json_escape_append(out, v);
+}
+
+void BatchState::step_meta_json(int64_t doc, int s, CharBuf& out, bool& first) const {
+  if (s < (int)bw_.size() && bw_[s]) {
+    const BwOut& b = *bw_[s];
+    switch (b.code[doc]) {
+      case BW_PASSED: json_member(out, first, "c4_badwords_filter_status", "passed"); break;
+      case BW_NO_REGEX: json_member(out, first, "c4_badwords_filter_status", "passed_no_regex"); break;
+      case BW_KEPT_BY_FRACTION: json_member(out, first, "c4_badwords_filter_status", "passed_kept_by_fraction"); break;
+      case BW_FILTERED:
+        json_member(out, first, "c4_badwords_filter_status", "filtered");
+        json_member(out, first, "c4_badwords_filter_reason", "document_removed_with_badwords");
+        break;
+      case BW_MISSING_LANG_FAIL: {
+        Decision d;
+        step_meta(doc, s, d);
+        for (auto& kv : d.meta) json_member(out, first, kv.first, kv.second);
+        break;
+      }
+      default: break;
+    }
+    return;
+  }
+  if (s >= (int)recs_.size() || !recs_[s].cfg) return;
+  const StepRec& sr = recs_[s];
+  decide_meta_json(*sr.cfg, sr.rec + doc * sr.width, out, first);
+}
+
 std::string BatchState::reason(int64_t i) const {
   const int s = fail_step_[i];
   if (s < 0 || s >= n_applied_) return std::string();
   Decision d;
   step_meta(i, s, d);
   return d.reason;
+}
+
+namespace {
+std::mutex g_charbuf_mu;
+std::vector<std::unique_ptr<CharBuf>>* g_charbufs = new std::vector<std::unique_ptr<CharBuf>>();
+}  // namespace
+
+static std::unique_ptr<CharBuf> take_charbuf() {
+  std::lock_guard<std::mutex> g(g_charbuf_mu);
+  if (g_charbufs->empty()) return std::make_unique<CharBuf>();
+  auto p = std::move(g_charbufs->back());
+  g_charbufs->pop_back();
+  p->clear();
+  return p;
+}
+
+static void give_charbuf(std::unique_ptr<CharBuf> p) {
+  std::lock_guard<std::mutex> g(g_charbuf_mu);
+  if (g_charbufs->size() < 512) g_charbufs->push_back(std::move(p));
 }
 
 void BatchState::assemble(const std::vector<int64_t>& idx, RawBuf& text_data, std::vector<int64_t>& text_off,
@@ -557,29 +688,53 @@ void BatchState::assemble(const std::vector<int64_t>& idx, RawBuf& text_data, st
   text_data.alloc((size_t)text_off[m]);
   // metadata: formatted per chunk (sizes unknown), then concatenated
   const int nchunks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)nthreads_ * 4, m / 256));
-  std::vector<std::string> mparts(nchunks);
+  // per-chunk metadata buffers come from a process-wide free list: their pages stay mapped and
+  // warm from batch to batch
+  std::vector<std::unique_ptr<CharBuf>> mparts(nchunks);
+  for (auto& p : mparts) p = take_charbuf();
   meta_off.assign(m + 1, 0);
   meta_valid.assign(m, 0);
-  std::atomic<int> next{0};
-  auto worker = [&]() {
-    FlatMeta fm;
-    Decision d;
-    while (true) {
-      const int c = next.fetch_add(1);
-      if (c >= nchunks) break;
+  // Steps of distinct kinds never write the same metadata key (each kind has its own keys), so
+  // per-document metadata is then a plain concatenation in step order.
+  bool fast_meta = std::getenv("TB_META_FAST") == nullptr || std::string(std::getenv("TB_META_FAST")) != "0";
+  for (int a = 0; a < n_applied_ && fast_meta; ++a)
+    for (int b = a + 1; b < n_applied_ && fast_meta; ++b)
+      if (step_kind(a) >= 0 && step_kind(a) == step_kind(b)) fast_meta = false;
+  auto worker = [&](int64_t c) {
+    thread_local FlatMeta fm;
+    thread_local Decision d;
+    {
       const int64_t a = m * c / nchunks, b = m * (c + 1) / nchunks;
-      std::string& md = mparts[c];
+      CharBuf& md = *mparts[c];
       md.reserve((size_t)(b - a) * 192);
       for (int64_t k = a; k < b; ++k) {
         const int64_t i = idx[k];
         std::string_view t = content(i);
         if (!t.empty()) std::memcpy(text_data.p + text_off[k], t.data(), t.size());
-        if (meta_data_ && (!meta_valid_ || meta_valid_[i])) {
+        const bool has_input = meta_data_ && (!meta_valid_ || meta_valid_[i]);
+        const int last = status_[i] == 0 ? n_applied_ - 1 : std::min(fail_step_[i], n_applied_ - 1);
+        if (!has_input && fast_meta) {
+          // no input metadata and no key written by two steps: the steps' members go straight
+          // into the column buffer in step order (what the map below would produce)
+          const size_t before = md.size();
+          md.push_back('{');
+          bool first = true;
+          for (int s = 0; s <= last; ++s) step_meta_json(i, s, md, first);
+          if (first) {
+            md.resize(before);
+            meta_off[k + 1] = 0;
+          } else {
+            md.push_back('}');
+            meta_off[k + 1] = (int64_t)(md.size() - before);
+            meta_valid[k] = 1;
+          }
+          continue;
+        }
+        if (has_input) {
           if (!input_meta(i, fm)) meta_fail_.fetch_add(1, std::memory_order_relaxed);
         } else {
           fm.clear();
         }
-        const int last = status_[i] == 0 ? n_applied_ - 1 : std::min(fail_step_[i], n_applied_ - 1);
         for (int s = 0; s <= last; ++s) {
           step_meta(i, s, d);
           for (auto& kv : d.meta) fm.set(kv.first, kv.second);
@@ -588,25 +743,25 @@ void BatchState::assemble(const std::vector<int64_t>& idx, RawBuf& text_data, st
           meta_off[k + 1] = 0;  // length; prefix-summed below
         } else {
           const size_t before = md.size();
-          fm.append_json(md);
+          thread_local std::string js;
+          js.clear();
+          fm.append_json(js);
+          md.append(js.data(), js.size());
           meta_off[k + 1] = (int64_t)(md.size() - before);
           meta_valid[k] = 1;
         }
       }
     }
   };
-  std::vector<std::thread> ts;
-  for (int t = 1; t < std::min(nthreads_, nchunks); ++t) ts.emplace_back(worker);
-  worker();
-  for (auto& t : ts) t.join();
+  parallel_tasks(nchunks, nthreads_, worker);
   for (int64_t k = 0; k < m; ++k) meta_off[k + 1] += meta_off[k];
   meta_data.alloc((size_t)meta_off[m]);
   std::vector<size_t> base(nchunks + 1, 0);
-  for (int c = 0; c < nchunks; ++c) base[c + 1] = base[c] + mparts[c].size();
-  parallel_for(nchunks, std::min(nthreads_, nchunks), [&](int64_t a, int64_t b) {
-    for (int64_t c = a; c < b; ++c)
-      if (!mparts[c].empty()) std::memcpy(meta_data.p + base[c], mparts[c].data(), mparts[c].size());
+  for (int c = 0; c < nchunks; ++c) base[c + 1] = base[c] + mparts[c]->size();
+  parallel_tasks(nchunks, nthreads_, [&](int64_t c) {
+    if (mparts[c]->size()) std::memcpy(meta_data.p + base[c], mparts[c]->data(), mparts[c]->size());
   });
+  for (auto& p : mparts) give_charbuf(std::move(p));
 }
 
 }  // namespace tb

@@ -20,7 +20,10 @@
 
 namespace tb {
 
+// fn(begin, end) over [0, n) in chunks on the process-wide worker pool (nthreads incl. the caller).
 void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t, int64_t)>& fn);
+// fn(task) for task in [0, ntasks) on the worker pool, at most nthreads at a time.
+void parallel_tasks(int64_t ntasks, int nthreads, const std::function<void(int64_t)>& fn);
 
 struct LangidModel {
   std::vector<uint16_t> emb;   // [kLidBuckets * kLidDim] bf16
@@ -155,6 +158,8 @@ class BatchState {
   void set_status(int64_t doc, int step_index, uint8_t st);
   bool input_meta(int64_t i, FlatMeta& out) const;
   void step_meta(int64_t doc, int s, Decision& d) const;  // metadata of step s for doc
+  void step_meta_json(int64_t doc, int s, CharBuf& out, bool& first) const;  // same, as JSON members
+  int step_kind(int s) const;  // StepKind of applied step s, -1 if none
 
   int64_t n_;
   int nthreads_;

@@ -1,0 +1,60 @@
+"""Host output formatting: the allocation-free Rust `{:.N}` / f64 Display formatters against
+Python's correctly rounded formatting, and the direct-to-JSON metadata path of output assembly
+against the map-based path (TB_META_FAST=0)."""
+import os
+import random
+import struct
+
+import numpy as np
+
+from textblaster_amd.config import load_pipeline_config
+from textblaster_amd.pipeline.engine import Engine
+from textblaster_amd.utils import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_fmt_fixed_matches_correct_rounding(host):
+    rng = random.Random(5)
+    vals = [0.0, -0.0, 0.125, 0.375, 2.675, 1.005, 0.5, 1.5, 2.5, 0.045, 0.00005, 123456.785, 1e13 + 0.5, 5e-324,
+            0.30000000000000004, 99.995, -0.001, -2.5, 1e15, float("inf"), float("nan")]
+    vals += [rng.random() * 10 ** rng.randint(-6, 12) for _ in range(20000)]
+    vals += [k / 200.0 for k in range(2000)] + [k / 20000.0 for k in range(2000)]
+    vals += [struct.unpack("<d", struct.pack("<Q", rng.getrandbits(62)))[0] for _ in range(2000)]
+    for v in vals:
+        for p in range(5):
+            want = format(v, f".{p}f")
+            if want in ("inf", "nan", "-inf"):
+                continue
+            assert host.fmt_fixed(v, p) == want, (v, p)
+
+
+def test_fmt_f64_shortest_roundtrip(host):
+    rng = random.Random(9)
+    for _ in range(5000):
+        v = rng.random() ** rng.randint(1, 40)
+        s = host.fmt_f64(v)
+        assert "e" not in s and float(s) == v
+
+
+def _collect(eng, data, off, meta):
+    res = eng.process(data, off, meta)
+    out = []
+    for part in res.kept + res.excluded:
+        md, mo, mv = part.meta_data, part.meta_off, part.meta_valid
+        for j, r in enumerate(part.rows):
+            out.append((int(r), bytes(md[mo[j]:mo[j + 1]]) if mv[j] else None))
+    return sorted(out)
+
+
+def test_direct_json_metadata_equals_map_path(monkeypatch):
+    cfg = load_pipeline_config(os.path.join(ROOT, "config", "bench_pipeline.yaml"))
+    eng = Engine(cfg, backend="cpu", segmentation="rules", nthreads=2)
+    texts = synth.make_corpus(600, 600, seed=21)
+    data, off = synth.pack(texts)
+    monkeypatch.setenv("TB_META_FAST", "1")
+    fast = _collect(eng, data, off, None)
+    monkeypatch.setenv("TB_META_FAST", "0")
+    slow = _collect(eng, data, off, None)
+    assert fast == slow
+    assert sum(1 for _, m in fast if m) > 500

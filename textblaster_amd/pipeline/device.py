@@ -129,6 +129,8 @@ class DeviceRunner:
     DEFAULT_LDS_BYTES = 10240
     DEFAULT_LDS_BYTES_C4 = 2560
     DEFAULT_LONG_DOC_BYTES = 8192
+    DEFAULT_MID_DOC_BYTES = 0        # 0: no separate mid-size launch
+    DEFAULT_LDS_BYTES_MID = 32768
     DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; sweep: tools/occ_sweep.sh)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None):
@@ -172,6 +174,12 @@ class DeviceRunner:
         self.stage_waves = int(os.environ.get("TB_STAGE_WAVES", str(self.DEFAULT_STAGE_WAVES)))
         # documents longer than this run one workgroup (4 waves) each instead of one wave
         self.long_doc_bytes = int(os.environ.get("TB_LONG_DOC_BYTES", str(self.DEFAULT_LONG_DOC_BYTES)))
+        # mid-size documents (one wave each, like the short ones) get their own launch with a larger
+        # LDS slice so their code point arrays and hash tables stay on chip (fewer of them per CU)
+        self.mid_doc_bytes = int(os.environ.get("TB_MID_DOC_BYTES", str(self.DEFAULT_MID_DOC_BYTES)))
+        self.lds_bytes_mid = int(os.environ.get("TB_LDS_BYTES_MID", str(self.DEFAULT_LDS_BYTES_MID)))
+        if not 0 <= self.lds_bytes_mid <= 131072 or not 0 <= self.lds_bytes <= 131072:
+            raise DeviceError("TB_LDS_BYTES / TB_LDS_BYTES_MID must be in [0, 131072]")
         self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", "65536"))
         if not 0 <= self.lds_bytes_blk <= 131072:
             # the workgroup kernels also hold static LDS (cross-wave exchange buffers): a 160 KB
@@ -374,6 +382,9 @@ class DeviceRunner:
         np.cumsum(per_doc[perm], out=scratch_off[1:])
         maxlen = int(lens.max()) if ndocs else 0
         n_long = int(np.count_nonzero(lens > self.long_doc_bytes)) if self.long_doc_bytes > 0 else 0
+        # perm is longest first: [0, n_long) workgroup docs, [n_long, n_mid) mid-size wave docs
+        n_mid = int(np.count_nonzero(lens > self.mid_doc_bytes)) if self.mid_doc_bytes > 0 else n_long
+        n_mid = max(n_mid, n_long)
         with tracing.trace_range("tb.stage_h2d"):
             (d_bytes, d_off, d_perm, d_soff), staged = self._stage_inputs(
                 slot, [data if len(data) else np.zeros(1, np.uint8), off, perm, scratch_off])
@@ -427,11 +438,21 @@ class DeviceRunner:
                                                  ndocs, scratch, d_soff, pw, pw_n, rec, flags, lid_vec, lid_cnt,
                                                  self.lds_bytes_blk, prof, skip)
                         ev_blk = self._record(slot.s_blk)
-                if n_long < ndocs:
-                    self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,
-                                         scratch, d_soff[n_long:], pw, pw_n, rec, flags,
+                if n_mid > n_long:
+                    # mid-size documents on the long-document stream, after its workgroup kernel
+                    if ev_blk is None:
+                        slot.s_blk.wait_event(ev_pre)
+                    with torch.cuda.stream(slot.s_blk):
+                        self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,
+                                             scratch, d_soff[n_long:], pw, pw_n, rec, flags,
+                                             self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
+                                             self.lds_bytes_mid, prof, self.stage_waves, n_mid - n_long, skip)
+                        ev_blk = self._record(slot.s_blk)
+                if n_mid < ndocs:
+                    self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_mid:], ndocs,
+                                         scratch, d_soff[n_mid:], pw, pw_n, rec, flags,
                                          self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
-                                         self.lds_bytes, prof, self.stage_waves, ndocs - n_long, skip)
+                                         self.lds_bytes, prof, self.stage_waves, ndocs - n_mid, skip)
                 if lid_vec is not None:
                     self._last_lid = (lid_vec, lid_cnt)
                     main.wait_event(ev_lid)

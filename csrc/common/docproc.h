@@ -140,6 +140,7 @@ struct DocCtx {
   uint32_t lused = 0;        // bytes allocated from the bottom of the LDS slice
   uint32_t lhi = 0;          // bytes allocated from the top (temporaries, releasable props)
   uint32_t* flag = nullptr;  // per-document status word
+  bool weak_keys = false;     // test hook: canonicalize() sees keys cut to 2 bits (forced collisions)
   bool overflow = false;
   uint64_t* prof = nullptr;  // optional per-document phase cycle counters (kPhaseSlots)
   uint64_t t_last = 0;
@@ -415,7 +416,7 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
     x.par.for_n(capn, [&](uint32_t i) { tab[i] = 0; });
     x.par.sync();
     x.par.for_n(n, [&](uint32_t i) {
-      const uint64_t k = key(i);
+      const uint64_t k = x.weak_keys ? (key(i) & 3ull) : key(i);
       const uint32_t fp = (uint32_t)(k >> 48);
       const uint32_t mine = (fp << 16) | (i + 1);
       uint32_t slot = (uint32_t)(((k & 0xFFFFFFFFull) * capn) >> 32);
@@ -444,7 +445,7 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
   x.par.for_n(capn, [&](uint32_t i) { tab[i] = 0; });
   x.par.sync();
   x.par.for_n(n, [&](uint32_t i) {
-    const uint64_t k = key(i);
+    const uint64_t k = x.weak_keys ? (key(i) & 3ull) : key(i);
     const uint64_t fp = (k >> 32) | 1ull;
     const uint64_t mine = (fp << 32) | (uint64_t)(i + 1);
     uint32_t slot = (uint32_t)(((k & 0xFFFFFFFFull) * capn) >> 32);

@@ -21,6 +21,9 @@ using namespace tb;
 namespace {
 
 constexpr uint32_t kMaxLdsPerDoc = 160 * 1024;
+// Workgroup kernels also hold static LDS (g_block_xs) on top of the dynamic slice: a 160 KB
+// slice fails at launch (HSA_STATUS_ERROR_INVALID_ALLOCATION, measured), so they take <= 128 KB.
+constexpr uint32_t kMaxLdsPerBlk = 128 * 1024;
 
 struct DevTables {
   const uint16_t* s1;
@@ -493,7 +496,7 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
                          uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes, uint64_t* prof,
                          const uint8_t* dead) {
   if (nblocks <= 0) return 0;
-  if (!perm || lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
+  if (!perm || lds_bytes > kMaxLdsPerBlk) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k_stage_analyze_blk, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -510,7 +513,7 @@ int tb_c4_pass_a_blk(hipStream_t stream, const void* c4, const uint8_t* bytes, c
                      const int32_t* l2, int64_t* rec, int64_t* src, uint32_t* flags, uint32_t lds_bytes,
                      uint64_t* prof, const uint8_t* dead) {
   if (nblocks <= 0) return 0;
-  if (!perm || lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
+  if (!perm || lds_bytes > kMaxLdsPerBlk) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k_c4_pass_a_blk, hipFuncAttributeMaxDynamicSharedMemorySize,

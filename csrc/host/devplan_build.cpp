@@ -245,7 +245,8 @@ static void lid_head_host(const LangidModel& m, const uint16_t* v, int32_t cnt, 
 
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
-                   std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes, const uint8_t* dead) {
+                   std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes, const uint8_t* dead,
+                   bool weak_keys) {
   DevPlan* plan = new DevPlan();
   std::memset(plan, 0, sizeof(DevPlan));
   DevStage st = build_stage(steps, idx, *plan);
@@ -278,6 +279,7 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
       x.lds = lds_bytes ? lds.data() : nullptr;
       x.lcap = lds_bytes;
       x.flag = &flags[i];
+      x.weak_keys = weak_keys;
       StageOut out{rec.data(), (uint32_t)ndocs, (uint32_t)i, lvec.data(), lcnt.data()};
       analyze_stage(x, st, *plan, lid ? lid->emb.data() : nullptr, (const uint8_t*)data + off[i], n, out);
       if (has_lid) {

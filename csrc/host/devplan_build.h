@@ -26,7 +26,7 @@ std::vector<uint64_t> pow_table(uint32_t n);  // B^0..B^n followed by B^-0..B^-n
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
                    std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes = 0,
-                   const uint8_t* dead = nullptr);
+                   const uint8_t* dead = nullptr, bool weak_keys = false);
 void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
                 std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,
                 std::vector<uint32_t>& flags, uint32_t lds_bytes = 0, const uint8_t* dead = nullptr);

@@ -201,6 +201,12 @@ PYBIND11_MODULE(_tbhost, m) {
   });
   m.def("fmt_f64", [](double x) { return fmt_f64(x); });
   m.def("fmt_fixed", [](double x, int prec) { return fmt_fixed(x, prec); });
+  m.def("contains_byte", [](py::array_t<uint8_t, py::array::c_style> a, int v) {
+    const void* p = a.data();
+    const size_t n = (size_t)a.size();
+    py::gil_scoped_release nogil;
+    return n > 0 && std::memchr(p, v, n) != nullptr;
+  });
 
   // ---- per-step records and decisions ----
   m.def("compute_record", [](const StepCfg& c, const std::string& text, const std::string& be) {
@@ -540,7 +546,7 @@ PYBIND11_MODULE(_tbhost, m) {
   m.def("emulate_stage", [](const std::vector<StepCfg>& steps, const std::vector<int>& idx,
                             py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
                             int nthreads, std::shared_ptr<LangidModel> lid, uint32_t lds_bytes,
-                            std::optional<py::array_t<uint8_t, py::array::c_style>> dead) {
+                            std::optional<py::array_t<uint8_t, py::array::c_style>> dead, bool weak_keys) {
     std::vector<int64_t> rec;
     std::vector<uint32_t> flags;
     const int64_t nd = (int64_t)off.size() - 1;
@@ -549,11 +555,12 @@ PYBIND11_MODULE(_tbhost, m) {
     {
       py::gil_scoped_release nogil;
       emulate_stage(steps, idx, nd, (const char*)data.data(), off.data(), nthreads, lid.get(), rec, flags, lds_bytes,
-                    dp);
+                    dp, weak_keys);
     }
     return py::make_tuple(to_numpy(std::move(rec)), to_numpy(std::move(flags)));
   }, py::arg("steps"), py::arg("idx"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8,
-     py::arg("lid") = nullptr, py::arg("lds_bytes") = 0, py::arg("dead") = py::none());
+     py::arg("lid") = nullptr, py::arg("lds_bytes") = 0, py::arg("dead") = py::none(),
+     py::arg("weak_keys") = false);
   m.def("gate_host", [](const py::bytes& gate, const std::vector<py::array_t<int64_t, py::array::c_style>>& recs,
                         int64_t ndocs, py::array_t<uint32_t, py::array::c_style> flags,
                         py::array_t<uint8_t, py::array::c_style> dead, int code) {

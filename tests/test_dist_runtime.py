@@ -172,3 +172,30 @@ def test_rank_failure_then_resume(tmp_path):
     r2, o2, e2 = _cli(tmp_path, inp, "ft", "--gpus", "2", "--work-dir", work, "--resume")
     assert "resumed" in r2.stdout
     assert pq.read_table(o2).equals(pq.read_table(o1)) and pq.read_table(e2).equals(pq.read_table(e1))
+
+
+def test_block_kernels_reject_oversized_lds_slice():
+    """The workgroup launchers refuse a dynamic LDS slice their static LDS would push past the
+    CU's 160 KB (argument check only: no HIP call happens, so this runs without a GPU)."""
+    import ctypes
+
+    from textblaster_amd import native
+    from textblaster_amd.ops import kernels
+
+    lib = native.hip()
+    kernels.declare(lib)
+    dummy = ctypes.c_void_p(16)
+    for lds, want_err in ((160 * 1024, True), (128 * 1024 + 16, True)):
+        rc = lib.tb_stage_analyze_blk(None, dummy, dummy, dummy, dummy, dummy, 1, 1, dummy, dummy, dummy, 0,
+                                      dummy, dummy, dummy, dummy, dummy, dummy, None, None, lds, None, None)
+        assert (rc != 0) == want_err
+        rc = lib.tb_c4_pass_a_blk(None, dummy, dummy, dummy, dummy, 1, 1, dummy, dummy, dummy, 0, dummy, dummy,
+                                  dummy, dummy, dummy, dummy, dummy, lds, None, None)
+        assert (rc != 0) == want_err
+
+
+def test_metrics_expose_device_counters():
+    from textblaster_amd.utils import metrics
+
+    text = metrics.render().decode()
+    assert "tb_h2d_bytes_total" in text and "tb_gpu_kernel_seconds" in text

@@ -1,7 +1,13 @@
 """Device kernels vs. the host emulation of the same algorithms (bit-exact records) and vs. the
 ICU oracle (end-to-end decisions). Needs an MI355X."""
+import os
+import sys
+
 import numpy as np
 import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from adversarial import adversarial_corpus  # noqa: E402
 
 from textblaster_amd.config import load_pipeline_config
 from textblaster_amd.utils import synth
@@ -16,7 +22,8 @@ EDGE = ["", "   ", "\n\n", "a", "a\r\nb\r\n", "Hello.\n\n\nHello.\n\nHello.", "x
 
 @pytest.fixture(scope="module")
 def corpus():
-    texts = synth.make_corpus(3000, 1024, seed=11) + EDGE
+    # adversarial documents (UAX#29 fuzz pool, constructs across the 64-item chunk boundaries)
+    texts = synth.make_corpus(3000, 1024, seed=11) + EDGE + adversarial_corpus()
     rng = np.random.default_rng(7)
     # long documents run one workgroup each (BlockPar kernels): a spread of sizes and languages,
     # plus long C4-heavy text (citations, policy lines, javascript, ellipses)

@@ -77,6 +77,11 @@ class HtmlDecoder:
         ndocs = off.numel() - 1
         if ndocs <= 0:
             return data[:0], off.clone()
+        # the kernels trust the offsets: check the bounds (and, cheaply on the device, monotonicity)
+        # before they index device memory with them
+        first, last = int(off[0].item()), int(off[-1].item())
+        if first < 0 or last > data.numel() or bool((off[1:] < off[:-1]).any().item()):
+            raise ValueError("html decode: offsets must be non-decreasing and within the data")
         data = data.contiguous()
         off = off.contiguous()
         lens = torch.empty(ndocs, dtype=torch.int64, device=self.device)
@@ -99,7 +104,8 @@ class HtmlDecoder:
         """Host arrays in, host arrays out (H2D, the two kernels, D2H); None when no document
         changes, like the host decoder's html_decode_batch."""
         torch = self.torch
-        if data.size == 0 or not np.any(data == ord("&")):
+        # look for '&' without a full-size boolean mask or copy (memchr in the host module)
+        if data.size == 0 or not native.host().contains_byte(np.ascontiguousarray(data, dtype=np.uint8), ord("&")):
             return None
         with self._lock, torch.cuda.device(self.device):
             d = torch.from_numpy(np.ascontiguousarray(data)).to(self.device)

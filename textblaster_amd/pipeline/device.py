@@ -15,7 +15,7 @@ import numpy as np
 
 from .. import native
 from ..errors import DeviceError
-from ..utils import tracing
+from ..utils import metrics, tracing
 from .plan import ExecPlan
 
 SCRATCH_ALIGN = 256
@@ -93,6 +93,13 @@ class PendingBatch:
         dead = self._dead.numpy() if self._dead is not None else None
         if self.runner.phase_prof:
             self.runner.collect_phase_prof(self._keep)
+        kt = {}
+        for item in self._keep or ():
+            if isinstance(item, tuple) and len(item) == 3 and item[0] == "ktime":
+                e0, e1 = item[2]
+                kt[item[1]] = kt.get(item[1], 0.0) + e0.elapsed_time(e1) / 1000.0
+        for name, sec in kt.items():
+            metrics.GPU_KERNEL_SECONDS.labels(name).observe(sec)
         self._keep = None
         timings = dict(self._t_submit)
         timings["gpu_wait"] = t1 - t0
@@ -171,6 +178,8 @@ class DeviceRunner:
 
         self.lds_bytes = int(os.environ.get("TB_LDS_BYTES", str(self.DEFAULT_LDS_BYTES)))
         self.lds_bytes_c4 = int(os.environ.get("TB_LDS_BYTES_C4", str(self.DEFAULT_LDS_BYTES_C4)))
+        if not 0 <= self.lds_bytes_c4 <= 131072:
+            raise DeviceError("TB_LDS_BYTES_C4 must be in [0, 131072]")
         self.stage_waves = int(os.environ.get("TB_STAGE_WAVES", str(self.DEFAULT_STAGE_WAVES)))
         # documents longer than this run one workgroup (4 waves) each instead of one wave
         self.long_doc_bytes = int(os.environ.get("TB_LONG_DOC_BYTES", str(self.DEFAULT_LONG_DOC_BYTES)))
@@ -298,6 +307,7 @@ class DeviceRunner:
             ev = torch.cuda.Event()
             ev.record(self.h2d_stream)
         slot.h2d_done = ev
+        metrics.H2D_BYTES_TOTAL.inc(total)
         compute = torch.cuda.current_stream(self.device)
         compute.wait_event(ev)
         dev.record_stream(compute)
@@ -320,6 +330,25 @@ class DeviceRunner:
         ev = self.torch.cuda.Event()
         ev.record(stream)
         return ev
+
+    def _ktimed(self, keep, name: str):
+        """Context manager: HIP events around the launches inside it on the current stream; the
+        elapsed time lands in tb_gpu_kernel_seconds{kernel=name} when the batch is collected."""
+        import contextlib
+
+        torch = self.torch
+
+        @contextlib.contextmanager
+        def cm():
+            st = torch.cuda.current_stream(self.device)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            yield
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(st)
+            keep.append(("ktime", name, (e0, e1)))
+
+        return cm()
 
     def _prof_buf(self, ndocs, keep, name):
         if not self.phase_prof:
@@ -424,7 +453,7 @@ class DeviceRunner:
                 ev_lid = ev_blk = None
                 if lid_vec is not None:
                     slot.s_lid.wait_event(ev_pre)
-                    with torch.cuda.stream(slot.s_lid):
+                    with torch.cuda.stream(slot.s_lid), self._ktimed(keep, "langid_features"):
                         self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec,
                                                lid_cnt, flags, self.lds_bytes_lid,
                                                self._prof_buf(ndocs, keep, f"langid{s}"))
@@ -433,7 +462,7 @@ class DeviceRunner:
                 skip = dead if pass_idx > 0 else None
                 if n_long:
                     slot.s_blk.wait_event(ev_pre)
-                    with torch.cuda.stream(slot.s_blk):
+                    with torch.cuda.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_blk"):
                         self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[:n_long], n_long,
                                                  ndocs, scratch, d_soff, pw, pw_n, rec, flags, lid_vec, lid_cnt,
                                                  self.lds_bytes_blk, prof, skip)
@@ -442,17 +471,18 @@ class DeviceRunner:
                     # mid-size documents on the long-document stream, after its workgroup kernel
                     if ev_blk is None:
                         slot.s_blk.wait_event(ev_pre)
-                    with torch.cuda.stream(slot.s_blk):
+                    with torch.cuda.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_mid"):
                         self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,
                                              scratch, d_soff[n_long:], pw, pw_n, rec, flags,
                                              self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
                                              self.lds_bytes_mid, prof, self.stage_waves, n_mid - n_long, skip)
                         ev_blk = self._record(slot.s_blk)
                 if n_mid < ndocs:
-                    self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_mid:], ndocs,
-                                         scratch, d_soff[n_mid:], pw, pw_n, rec, flags,
-                                         self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
-                                         self.lds_bytes, prof, self.stage_waves, ndocs - n_mid, skip)
+                    with self._ktimed(keep, f"stage{s}"):
+                        self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_mid:], ndocs,
+                                             scratch, d_soff[n_mid:], pw, pw_n, rec, flags,
+                                             self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
+                                             self.lds_bytes, prof, self.stage_waves, ndocs - n_mid, skip)
                 if lid_vec is not None:
                     self._last_lid = (lid_vec, lid_cnt)
                     main.wait_event(ev_lid)
@@ -488,7 +518,7 @@ class DeviceRunner:
                         self.k.c4_pass_a_blk(self.c4_ts[i], vb, vo, d_perm[:n_long], n_long, ndocs, c4_scratch,
                                              d_soff, pw, pw_n, rec, src, flags, self.lds_bytes_blk, prof, skip)
                         ev_c4blk = self._record(slot.s_c4blk)
-                with torch.cuda.stream(slot.s_c4):
+                with torch.cuda.stream(slot.s_c4), self._ktimed(keep, f"c4_step{i}"):
                     if n_long < ndocs:
                         self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm[n_long:], ndocs, c4_scratch, d_soff[n_long:], pw,
                                          pw_n, rec, src, flags, self.lds_bytes_c4, prof, ndocs - n_long, skip)

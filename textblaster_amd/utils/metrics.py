@@ -62,6 +62,9 @@ DOCS_PER_SECOND = Gauge("tb_docs_per_second", "Throughput of the last batch (doc
 BYTES_PROCESSED_TOTAL = Counter("tb_bytes_processed_total", "Input text bytes processed.", registry=REGISTRY)
 H2D_BYTES_TOTAL = Counter("tb_h2d_bytes_total", "Bytes staged host-to-device.", registry=REGISTRY)
 GPU_PHASE_SECONDS = Histogram("tb_gpu_phase_seconds", "Per-batch time by phase.", ["phase"], registry=REGISTRY)
+GPU_KERNEL_SECONDS = Histogram("tb_gpu_kernel_seconds", "Per-batch device time of each kernel group (HIP events).",
+                               ["kernel"], registry=REGISTRY,
+                               buckets=(0.0005, 0.001, 0.002, 0.005, 0.01, 0.02, 0.05, 0.1, 0.2, 0.5, 1.0, float("inf")))
 DELEGATED_DOCS_TOTAL = Counter("tb_cpu_delegated_docs_total",
                                "Documents recomputed on the CPU oracle path (dictionary scripts, collisions).",
                                registry=REGISTRY)

@@ -1,7 +1,10 @@
 """Train the language-id weights (textblaster_amd/models/data/langid_v1.npz).
 
-Training text: the hand-written sentences in models/data/langid_corpus/<lang>.txt plus random
-word sequences from the synthetic-corpus vocabularies. Features come from the native featurizer
+Training text: the hand-written sentences in models/data/langid_corpus/<lang>.txt (whole
+sentences, runs of sentences and sentence fragments). Random word sequences from the
+synthetic-corpus vocabularies (utils/synth.VOCAB) are off by default (--vocab-share 0), so the
+benchmark corpus is not generated from the training text; the held-out evaluation
+(tools/eval_langid.py, models/data/langid_eval) shares nothing with either. Features come from the native featurizer
 (_tbhost.langid_buckets), so training and inference hash identically. Label smoothing keeps the
 confidence of short texts below ~0.93, like lingua's relative confidences.
 
@@ -26,24 +29,23 @@ def bf16_bits(a: np.ndarray) -> np.ndarray:
     return t.view(torch.int16).numpy().view(np.uint16)
 
 
-def samples(rng: random.Random, n_per_lang: int):
+def samples(rng: random.Random, n_per_lang: int, vocab_share: float = 0.0):
     out = []
     for li, lang in enumerate(LANGS):
         sents = [s.strip() for s in open(os.path.join(DATA_DIR, "langid_corpus", f"{lang}.txt"), encoding="utf-8")
                  if s.strip()]
         vocab = VOCAB[lang]
         for _ in range(n_per_lang):
-            r = rng.random()
-            if r < 0.45:
+            if rng.random() < vocab_share:
+                text = " ".join(rng.choice(vocab) for _ in range(rng.randint(3, 40)))
+            elif rng.random() < 0.6:
                 k = rng.randint(1, 4)
                 i = rng.randint(0, len(sents) - 1)
                 text = " ".join(sents[i:i + k])
-            elif r < 0.7:
+            else:
                 s = rng.choice(sents).split()
                 a = rng.randint(0, max(0, len(s) - 2))
                 text = " ".join(s[a:a + rng.randint(2, 8)])
-            else:
-                text = " ".join(rng.choice(vocab) for _ in range(rng.randint(3, 40)))
             if rng.random() < 0.1:
                 text = text.upper()
             out.append((text, li))
@@ -56,11 +58,13 @@ def main():
     ap.add_argument("--epochs", type=int, default=12)
     ap.add_argument("--n", type=int, default=6000)
     ap.add_argument("--out", default=os.path.join(DATA_DIR, "langid_v1.npz"))
+    ap.add_argument("--vocab-share", type=float, default=0.0,
+                    help="fraction of samples drawn from the synthetic benchmark vocabulary (default 0)")
     args = ap.parse_args()
     h = native.host()
     rng = random.Random(1234)
     torch.manual_seed(1234)
-    train = samples(rng, args.n)
+    train = samples(rng, args.n, args.vocab_share)
     feats = [np.asarray(h.langid_buckets(t), dtype=np.int64) for t, _ in train]
     keep = [i for i, f in enumerate(feats) if len(f)]
     feats = [feats[i] for i in keep]

@@ -18,9 +18,9 @@ CFG = os.path.join(REPO, "config", "bench_pipeline.yaml")
 
 
 def test_device_run_equals_cpu_oracle(tmp_path):
-    import torch
+    from textblaster_amd.ops import hiprt
 
-    assert torch.cuda.is_available()
+    assert hiprt.device_count() > 0
     texts = synth.make_corpus(6000, 1024, seed=21) + ["", "日本語のテキストです。", "&amp; entity &lt;b&gt; text."]
     docs = [TextDocument(f"g{i}", t, "gpu", metadata={"n": str(i)} if i % 5 == 0 else {}) for i, t in enumerate(texts)]
     inp = str(tmp_path / "in.parquet")

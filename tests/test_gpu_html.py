@@ -24,8 +24,7 @@ def _corpus(rng, n):
 
 
 def test_gpu_html_decode_matches_host():
-    import torch
-
+    from textblaster_amd.ops import hiprt
     from textblaster_amd.ops.html import HtmlDecoder
 
     h = native.host()
@@ -33,9 +32,10 @@ def test_gpu_html_decode_matches_host():
     texts = _corpus(rng, 3000)
     data, off = synth.pack(texts)
     dec = HtmlDecoder("cuda:0")
-    od, oo = dec.decode(torch.from_numpy(data).cuda(), torch.from_numpy(off.astype(np.int64)).cuda())
-    od = od.cpu().numpy()
-    oo = oo.cpu().numpy()
+    od, oo = dec.decode(hiprt.to_device(data), hiprt.to_device(off.astype(np.int64)))
+    with hiprt.stream(dec.stream):
+        od = od.to_host()
+        oo = oo.to_host()
     for i, t in enumerate(texts):
         want = h.html_decode(t).encode("utf-8")
         got = bytes(od[oo[i]:oo[i + 1]])

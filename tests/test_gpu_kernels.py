@@ -35,11 +35,21 @@ def corpus():
     return texts
 
 
+def _to_bf16(x: np.ndarray) -> np.ndarray:
+    """f32 -> bf16 bits, round to nearest even."""
+    b = x.astype(np.float32).view(np.uint32).astype(np.uint64)
+    return ((b + 0x7FFF + ((b >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+def _from_bf16(b: np.ndarray) -> np.ndarray:
+    return (b.astype(np.uint32) << 16).view(np.float32)
+
+
 @pytest.fixture(scope="module")
 def runner_parts(host):
-    import torch
+    from textblaster_amd.ops import hiprt
 
-    assert torch.cuda.is_available()
+    assert hiprt.device_count() > 0
     from textblaster_amd.models.langid import load_default
     from textblaster_amd.pipeline.device import DeviceRunner
     from textblaster_amd.pipeline.plan import build_plan
@@ -124,25 +134,24 @@ def test_dictionary_scripts_are_flagged(host, runner_parts):
 
 def test_langid_head_mfma_matches_numpy(host, runner_parts):
     """The bf16 MFMA head on known inputs vs. an fp64 numpy reference (isolates the head)."""
-    import torch
+    from textblaster_amd.ops import hiprt
 
     _, _, _, runner, lid = runner_parts
     rng = np.random.default_rng(0)
     n = 200
-    vec = torch.from_numpy(rng.normal(0, 0.5, size=(n, 32)).astype(np.float32)).to(torch.bfloat16)
+    vec16 = _to_bf16(rng.normal(0, 0.5, size=(n, 32)).astype(np.float32))
     w = lid.w.copy().view(np.uint16).reshape(32, 16)
-    wf = torch.from_numpy(w.view(np.int16)).view(torch.bfloat16).float().numpy()
-    logits_ref = vec.float().numpy() @ wf + lid.b
-    dev = runner.device
-    vec_d = vec.view(torch.int16).reshape(-1).to(dev)
-    cnt_d = torch.ones(n, dtype=torch.int32, device=dev)
-    rec = torch.zeros(2 * n, dtype=torch.int64, device=dev)
-    dbg = torch.zeros(n * 16, dtype=torch.float32, device=dev)
+    wf = _from_bf16(w)
+    logits_ref = _from_bf16(vec16).astype(np.float64) @ wf + lid.b
+    vec_d = hiprt.to_device(vec16.view(np.int16).reshape(-1))
+    cnt_d = hiprt.to_device(np.ones(n, dtype=np.int32))
+    rec = hiprt.zeros(2 * n, np.int64)
+    dbg = hiprt.zeros(n * 16, np.float32)
     runner.k.langid_head(vec_d, cnt_d, runner.lid_wT, runner.lid_b, n, rec, 0, 2, dbg)
-    torch.cuda.synchronize()
-    got_logits = dbg.cpu().numpy().reshape(n, 16)[:, :5]
+    hiprt.synchronize()
+    got_logits = dbg.to_host().reshape(n, 16)[:, :5]
     assert np.allclose(got_logits, logits_ref[:, :5], atol=1e-4), np.abs(got_logits - logits_ref[:, :5]).max()
-    r = rec.cpu().numpy().reshape(n, 2)
+    r = rec.to_host().reshape(n, 2)
     best_ref = logits_ref[:, :5].argmax(1)
     print("head argmax mismatches", np.nonzero(r[:, 0] != best_ref)[0][:20])
     assert np.array_equal(r[:, 0], best_ref)
@@ -151,7 +160,7 @@ def test_langid_head_mfma_matches_numpy(host, runner_parts):
 def test_langid_pipeline_vectors_and_head(host, corpus, runner_parts):
     """Doc vectors from the analysis kernel are bit-exact vs. the host featurizer, and the head
     applied to them gives the host's language."""
-    import torch
+    from textblaster_amd.ops import hiprt
 
     _, _, _, runner, lid = runner_parts
     texts = corpus[:512]
@@ -159,8 +168,8 @@ def test_langid_pipeline_vectors_and_head(host, corpus, runner_parts):
     res = runner.run(data, off)
     vec_d, cnt_d = runner._last_lid
     n = len(texts)
-    vec = vec_d.cpu().numpy().view(np.uint16).reshape(n, 32)
-    cnt = cnt_d.cpu().numpy()
+    vec = vec_d.to_host().view(np.uint16).reshape(n, 32)
+    cnt = cnt_d.to_host()
     m = lid.native()
     bad_vec = []
     for i, t in enumerate(texts):
@@ -168,18 +177,18 @@ def test_langid_pipeline_vectors_and_head(host, corpus, runner_parts):
         if c != cnt[i] or (c and list(v) != list(vec[i])):
             bad_vec.append(i)
     print("vector mismatches", len(bad_vec), bad_vec[:10])
-    rec2 = torch.zeros(2 * n, dtype=torch.int64, device=runner.device)
-    dbg = torch.zeros(16 * n, dtype=torch.float32, device=runner.device)
+    rec2 = hiprt.zeros(2 * n, np.int64)
+    dbg = hiprt.zeros(16 * n, np.float32)
     runner.k.langid_head(vec_d, cnt_d, runner.lid_wT, runner.lid_b, n, rec2, 0, 2, dbg)
-    rec3 = torch.zeros(2 * n, dtype=torch.int64, device=runner.device)
+    rec3 = hiprt.zeros(2 * n, np.int64)
     runner.k.langid_head(vec_d, cnt_d, runner.lid_wT, runner.lid_b, n, rec3, 0, 2, None)
-    torch.cuda.synchronize()
+    hiprt.synchronize()
     width_total, layout = runner.stage_layout[0]
     _, w, prefix = [t for t in layout if t[0] == 4][0]
     r1 = res.stage_recs[0][prefix * n:(prefix + w) * n].reshape(n, w)
-    r2 = rec2.cpu().numpy().reshape(n, 2)
-    r3 = rec3.cpu().numpy().reshape(n, 2)
-    lg = dbg.cpu().numpy().reshape(n, 16)[:, :5]
+    r2 = rec2.to_host().reshape(n, 2)
+    r3 = rec3.to_host().reshape(n, 2)
+    lg = dbg.to_host().reshape(n, 16)[:, :5]
     cpu = np.array([m.detect(t)[0] for t in texts])
     print("pipeline lang", r1[:12, 0], "\nhead+dbg", r2[:12, 0], "\nhead nodbg", r3[:12, 0],
           "\nlogit argmax", lg[:12].argmax(1), "\ncpu", cpu[:12])
@@ -206,8 +215,8 @@ def test_langid_bag_edge_cases_bit_exact(host, runner_parts):
     runner.run(data, off)
     vec_d, cnt_d = runner._last_lid
     n = len(texts)
-    vec = vec_d.cpu().numpy().view(np.uint16).reshape(n, 32)
-    cnt = cnt_d.cpu().numpy()
+    vec = vec_d.to_host().view(np.uint16).reshape(n, 32)
+    cnt = cnt_d.to_host()
     m = lid.native()
     for i, t in enumerate(texts):
         c, v = m.featurize(t)

@@ -366,6 +366,19 @@ class ParquetWriter:
             self._w = None
 
 
+def encode_table(table: pa.Table, compression: str = "none") -> pa.Buffer:
+    """One table -> a complete Parquet file in memory, written exactly as ``ParquetWriter``
+    would write it (same schema, properties and row groups). Encoders on several threads run
+    concurrently (the encode releases the GIL); ``io.pqconcat.StreamConcat`` appends the
+    results to one file without re-encoding."""
+    sink = pa.BufferOutputStream()
+    w = pq.ParquetWriter(sink, OUTPUT_SCHEMA, compression=compression)
+    if table.num_rows:
+        w.write_table(table)
+    w.close()
+    return sink.getvalue()
+
+
 def build_output_table(ids, source, text, added_days_ce, created, metadata) -> pa.Table:
     added = pa.Array.from_buffers(pa.date32(), len(added_days_ce), added_days_ce.buffers(),
                                   offset=added_days_ce.offset)

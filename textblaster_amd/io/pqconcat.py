@@ -222,6 +222,17 @@ def read_footer(path: str) -> Tuple[int, int, list]:
     return size, start, fmd
 
 
+def parse_buffer(buf) -> Tuple[int, list]:
+    """(body end = footer start, decoded FileMetaData) of a whole Parquet file held in memory."""
+    mv = memoryview(buf)
+    size = len(mv)
+    if size < 12 or bytes(mv[:4]) != MAGIC or bytes(mv[size - 4:]) != MAGIC:
+        raise ThriftError("buffer is not a Parquet file (or an encrypted one)")
+    flen = struct.unpack("<I", bytes(mv[size - 8:size - 4]))[0]
+    start = size - 8 - flen
+    return start, decode_struct(bytes(mv[start:size - 8]))
+
+
 def shift_row_group(rg: list, delta: int) -> None:
     """Adds ``delta`` to every absolute file offset of one RowGroup (in place)."""
     # 0 means "unset" for the deprecated file_offset fields, which then stay 0
@@ -336,3 +347,51 @@ def concat(paths: Sequence[str], out_path: str) -> int:
     finally:
         os.close(fd)
     return lay.num_rows
+
+
+class StreamConcat:
+    """Appends whole in-memory Parquet files (e.g. row groups encoded concurrently by several
+    threads into ``pa.BufferOutputStream``s) to one output file in call order, without
+    re-encoding: each body is written once at the running offset and its row groups are
+    shifted there; ``close`` writes the merged footer. Returns False from ``close`` when nothing
+    was appended (the caller writes an empty file with its schema)."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self.fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+        self.pos = 4
+        self.row_groups: List[list] = []
+        self.num_rows = 0
+        self.template: list = []
+        self.schema = b""
+
+    def append(self, buf) -> None:
+        end, fmd = parse_buffer(buf)
+        sch = encode_struct([_get(fmd, FMD_SCHEMA)])
+        if not self.template:
+            self.template, self.schema = fmd, sch
+        elif sch != self.schema:
+            raise ThriftError(f"{self.path}: appended file has a different schema")
+        mv = memoryview(buf)[4:end]
+        done = 0
+        while done < len(mv):
+            k = os.pwrite(self.fd, mv[done:], self.pos + done)
+            if k <= 0:
+                raise OSError(f"short write to {self.path}")
+            done += k
+        for rg in (_get(fmd, FMD_ROW_GROUPS) or [0, 0, (T_STRUCT, [])])[2][1]:
+            shift_row_group(rg, self.pos - 4)
+            self.row_groups.append(rg)
+        self.pos += len(mv)
+        self.num_rows += (_get(fmd, FMD_NUM_ROWS) or [0, 0, 0])[2]
+
+    def close(self) -> bool:
+        if self.fd < 0:
+            return bool(self.template)
+        try:
+            if self.template:
+                finish(self.fd, self.pos, self.template, self.row_groups, self.num_rows)
+        finally:
+            os.close(self.fd)
+            self.fd = -1
+        return bool(self.template)

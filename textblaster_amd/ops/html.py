@@ -43,72 +43,75 @@ def build_slots(names: bytes, noff) -> np.ndarray:
 
 
 class HtmlDecoder:
-    """Holds the entity table on one device; ``decode`` works on device tensors."""
+    """Holds the entity table on one device; ``decode`` works on device arrays (ops/hiprt.py)."""
 
     def __init__(self, device="cuda:0"):
-        import torch
+        from . import hiprt
 
-        self.torch = torch
-        self.device = torch.device(device)
+        self.rt = hiprt
+        self.device = hiprt.parse_device(device)
         self.lib = native.hip()
+        hiprt.set_device(self.device)
+        self.stream = hiprt.Stream()
         names, noff, vals, voff = native.host().html_entity_table()
-        dev = self.device
-        self.names = torch.from_numpy(np.frombuffer(names, dtype=np.uint8).copy()).to(dev)
-        self.name_off = torch.tensor(noff, dtype=torch.int32, device=dev)
-        self.vals = torch.from_numpy(np.frombuffer(vals, dtype=np.uint8).copy()).to(dev)
-        self.val_off = torch.tensor(voff, dtype=torch.int32, device=dev)
-        self.nent = len(noff) - 1
-        slots = build_slots(names, noff)
-        assert (slots < 0).any(), "the device probe loop needs an empty slot"
-        self.slots = torch.from_numpy(slots).to(dev)
+        with hiprt.stream(self.stream):
+            self.names = hiprt.to_device(np.frombuffer(names, dtype=np.uint8))
+            self.name_off = hiprt.to_device(np.asarray(noff, dtype=np.int32))
+            self.vals = hiprt.to_device(np.frombuffer(vals, dtype=np.uint8))
+            self.val_off = hiprt.to_device(np.asarray(voff, dtype=np.int32))
+            self.nent = len(noff) - 1
+            slots = build_slots(names, noff)
+            assert (slots < 0).any(), "the device probe loop needs an empty slot"
+            self.slots = hiprt.to_device(slots)
         self.slot_mask = len(slots) - 1
         self._lock = threading.Lock()  # the reader pool calls decode_host from several threads
 
-    def _stream(self) -> int:
-        return self.torch.cuda.current_stream(self.device).cuda_stream
-
-    def decode(self, data, off) -> Tuple["torch.Tensor", "torch.Tensor"]:  # noqa: F821
-        """data: uint8[N], off: int64[B+1] (CUDA tensors) -> decoded (data', off')."""
-        torch = self.torch
-        if data.dtype != torch.uint8 or off.dtype != torch.int64 or off.dim() != 1:
+    def decode(self, data, off, host_off: np.ndarray = None):
+        """data: uint8[N], off: int64[B+1] (device arrays) -> decoded (data', off') on the device,
+        ordered on this decoder's stream. ``host_off``: the same offsets on the host, when the
+        caller has them (skips the download for the bounds check)."""
+        rt = self.rt
+        if data.dtype != np.uint8 or off.dtype != np.int64:
             raise ValueError("html decode needs uint8 data and int64 offsets")
-        if data.device != self.device or off.device != self.device:
-            raise ValueError("html decode inputs must live on " + str(self.device))
         ndocs = off.numel() - 1
-        if ndocs <= 0:
-            return data[:0], off.clone()
-        # the kernels trust the offsets: check the bounds (and, cheaply on the device, monotonicity)
-        # before they index device memory with them
-        first, last = int(off[0].item()), int(off[-1].item())
-        if first < 0 or last > data.numel() or bool((off[1:] < off[:-1]).any().item()):
-            raise ValueError("html decode: offsets must be non-decreasing and within the data")
-        data = data.contiguous()
-        off = off.contiguous()
-        lens = torch.empty(ndocs, dtype=torch.int64, device=self.device)
-        _check(self.lib.tb_html_sizes(self._stream(), data.data_ptr(), off.data_ptr(), ndocs, self.names.data_ptr(),
-                                      self.name_off.data_ptr(), self.vals.data_ptr(), self.val_off.data_ptr(),
-                                      self.nent, self.slots.data_ptr(), self.slot_mask, lens.data_ptr()),
-               "tb_html_sizes")
-        out_off = torch.zeros(ndocs + 1, dtype=torch.int64, device=self.device)
-        torch.cumsum(lens, 0, out=out_off[1:])
-        total = int(out_off[-1].item())
-        out = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
-        _check(self.lib.tb_html_scatter(self._stream(), data.data_ptr(), off.data_ptr(), ndocs,
-                                        self.names.data_ptr(), self.name_off.data_ptr(), self.vals.data_ptr(),
-                                        self.val_off.data_ptr(), self.nent, self.slots.data_ptr(), self.slot_mask,
-                                        out_off.data_ptr(), out.data_ptr()),
-               "tb_html_scatter")
-        return out[:total], out_off
+        with rt.stream(self.stream):
+            if ndocs <= 0:
+                return data[:0], rt.zeros(off.numel(), np.int64)
+            # the kernels trust the offsets: check the bounds and monotonicity before they index
+            # device memory with them
+            ho = host_off if host_off is not None else off.to_host()
+            if len(ho) != ndocs + 1 or ho[0] < 0 or ho[-1] > data.numel() or bool((ho[1:] < ho[:-1]).any()):
+                raise ValueError("html decode: offsets must be non-decreasing and within the data")
+            lens = rt.empty(ndocs, np.int64)
+            _check(self.lib.tb_html_sizes(self.stream.handle, data.data_ptr(), off.data_ptr(), ndocs,
+                                          self.names.data_ptr(), self.name_off.data_ptr(), self.vals.data_ptr(),
+                                          self.val_off.data_ptr(), self.nent, self.slots.data_ptr(), self.slot_mask,
+                                          lens.data_ptr()), "tb_html_sizes")
+            out_off = rt.zeros(ndocs + 1, np.int64)
+            rt.scan_strided_i64(lens, 1, ndocs, out_off[1:])
+            tot = np.zeros(1, np.int64)
+            out_off[ndocs:].copy_to_host(tot, self.stream)
+            self.stream.synchronize()
+            total = int(tot[0])
+            out = rt.empty(max(total, 1), np.uint8)
+            _check(self.lib.tb_html_scatter(self.stream.handle, data.data_ptr(), off.data_ptr(), ndocs,
+                                            self.names.data_ptr(), self.name_off.data_ptr(), self.vals.data_ptr(),
+                                            self.val_off.data_ptr(), self.nent, self.slots.data_ptr(),
+                                            self.slot_mask, out_off.data_ptr(), out.data_ptr()), "tb_html_scatter")
+            return out[:total], out_off
 
     def decode_host(self, data: np.ndarray, off: np.ndarray):
         """Host arrays in, host arrays out (H2D, the two kernels, D2H); None when no document
         changes, like the host decoder's html_decode_batch."""
-        torch = self.torch
+        rt = self.rt
         # look for '&' without a full-size boolean mask or copy (memchr in the host module)
         if data.size == 0 or not native.host().contains_byte(np.ascontiguousarray(data, dtype=np.uint8), ord("&")):
             return None
-        with self._lock, torch.cuda.device(self.device):
-            d = torch.from_numpy(np.ascontiguousarray(data)).to(self.device)
-            o = torch.from_numpy(np.ascontiguousarray(off, dtype=np.int64)).to(self.device)
-            od, oo = self.decode(d, o)
-            return od.cpu().numpy(), oo.cpu().numpy()
+        o64 = np.ascontiguousarray(off, dtype=np.int64)
+        with self._lock:
+            rt.set_device(self.device)
+            with rt.stream(self.stream):
+                d = rt.to_device(np.ascontiguousarray(data, dtype=np.uint8))
+                o = rt.to_device(o64)
+                od, oo = self.decode(d, o, host_off=o64)
+                return od.to_host(), oo.to_host()

@@ -1,13 +1,16 @@
-"""ctypes bindings for libtbhip.so (csrc/hip/kernels.hip) and thin launch helpers.
+"""ctypes bindings for libtbhip.so (csrc/hip/kernels.hip, html.hip, runtime.hip) and thin launch
+helpers.
 
-Device memory is owned by PyTorch (``torch.empty(..., device="cuda")``); kernels are launched on
-the caller's current PyTorch stream. Every launch checks the returned hipError_t and raises —
-there is no silent fallback on a GPU box.
+Device memory comes from the native runtime layer (ops/hiprt.py: caching HBM allocator,
+``DevArray`` views); kernels are launched on the calling thread's current hiprt stream. Every
+launch checks the returned hipError_t and raises — there is no silent fallback on a GPU box.
 """
 from __future__ import annotations
 
 import ctypes
 from typing import Optional
+
+import numpy as np
 
 from ..errors import DeviceError
 
@@ -15,6 +18,7 @@ _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _U32 = ctypes.c_uint32
 _I64 = ctypes.c_int64
+_SZ = ctypes.c_size_t
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32,
@@ -34,6 +38,16 @@ _SIGS = {
     "tb_html_sizes": [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _P, _U32, _P],
     "tb_html_scatter": [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _P, _U32, _P, _P],
     "tb_abi_version": [],
+    # native runtime layer (csrc/hip/runtime.hip)
+    "tbrt_device_count": [_P], "tbrt_set_device": [_I32], "tbrt_get_device": [_P], "tbrt_device_sync": [],
+    "tbrt_mem_info": [_P, _P], "tbrt_malloc": [_P, _SZ], "tbrt_free": [_P], "tbrt_host_alloc": [_P, _SZ],
+    "tbrt_host_free": [_P], "tbrt_empty_cache": [], "tbrt_cache_stats": [_P], "tbrt_stream_create": [_P, _I32],
+    "tbrt_stream_destroy": [_P], "tbrt_stream_sync": [_P], "tbrt_stream_priority_range": [_P, _P],
+    "tbrt_event_create": [_P, _I32], "tbrt_event_destroy": [_P], "tbrt_event_record": [_P, _P],
+    "tbrt_event_sync": [_P], "tbrt_event_query": [_P], "tbrt_event_elapsed": [_P, _P, _P],
+    "tbrt_stream_wait_event": [_P, _P], "tbrt_memcpy_h2d": [_P, _P, _SZ, _P], "tbrt_memcpy_d2h": [_P, _P, _SZ, _P],
+    "tbrt_memcpy_d2d": [_P, _P, _SZ, _P], "tbrt_memset": [_P, _I32, _SZ, _P],
+    "tb_scan_strided_i64": [_P, _P, _I64, _I64, _P],
     "tb_phase_slots": [],
     "tb_sizeof_plan": [],
     "tb_sizeof_stage": [],
@@ -57,17 +71,13 @@ def _check(rc: int, what: str) -> None:
         raise DeviceError(f"{what} failed with hipError_t {rc}")
 
 
-def stream_handle(torch, device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
-
-
 class Kernels:
     """Launch helpers bound to one device (holds the Unicode tables in HBM)."""
 
-    def __init__(self, torch, device):
+    def __init__(self, device: int):
         from .. import native
+        from . import hiprt
 
-        self.torch = torch
         self.device = device
         self.lib = native.hip()
         h = native.host()
@@ -75,19 +85,24 @@ class Kernels:
                 or self.lib.tb_sizeof_gate() != h.SIZEOF_DEV_GATE):
             raise DeviceError("libtbhip.so and _tbhost disagree on the device plan layout; rebuild")
         s1, s2, l1, l2 = h.ucd_tables()
-        self.tabs = [torch.from_numpy(a).to(device) for a in (s1, s2, l1, l2)]
+        self.tabs = [hiprt.to_device(a) for a in (s1, s2, l1, l2)]
         self._pw = None
         self._pw_n = 0
 
-    def stream(self) -> int:
-        return self.torch.cuda.current_stream(self.device).cuda_stream
+    @staticmethod
+    def stream() -> int:
+        from . import hiprt
+
+        return hiprt.current_stream().handle
 
     def pow_table(self, n: int):
         if n > self._pw_n:
+            from . import hiprt
+
             cap = max(n, 1 << 16)
             cap = 1 << (cap - 1).bit_length()
             # B^0..B^cap followed by B^-0..B^-cap (k_pow_table)
-            self._pw = self.torch.empty(2 * cap + 2, dtype=self.torch.int64, device=self.device)
+            self._pw = hiprt.empty(2 * cap + 2, np.int64)
             _check(self.lib.tb_pow_table(self.stream(), self._pw.data_ptr(), cap), "tb_pow_table")
             self._pw_n = cap
         return self._pw, self._pw_n

@@ -21,16 +21,6 @@ from .plan import ExecPlan
 SCRATCH_ALIGN = 256
 
 
-def _torch_dtypes():
-    import torch
-
-    return {np.dtype(np.uint8).str: torch.uint8, np.dtype(np.int32).str: torch.int32,
-            np.dtype(np.int64).str: torch.int64, np.dtype(np.uint16).str: torch.int16}
-
-
-_TORCH_DTYPES = _torch_dtypes() if __import__('importlib').util.find_spec('torch') else {}
-
-
 @dataclasses.dataclass
 class DeviceResult:
     stage_recs: List[np.ndarray]            # per stage: int64 [width_total * ndocs]
@@ -54,10 +44,12 @@ class _Slot:
         self.scratch = None
         self.scratch_c4 = None
         self.h2d_done = None  # event: the pinned staging buffer may be rewritten after it
-        # per-slot streams (compute, language-id bag, long-document kernels, C4 wave / long):
-        # a batch's kernels only order against the batch that used the slot before it, so batch
-        # k+1 starts while batch k's tail (long documents, C4, FineWeb, D2H) still runs
+        # per-slot streams (compute, language-id bag, long-document kernels, C4 wave / long, and
+        # the copies): a batch's kernels only order against the batch that used the slot before
+        # it, so batch k+1 starts while batch k's tail (long documents, C4, FineWeb, D2H) runs.
+        # With the default layout these alias two streams per slot (see DeviceRunner).
         self.main = self.s_lid = self.s_blk = self.s_c4 = self.s_c4blk = None
+        self.s_h2d = self.s_d2h = None
 
 
 class PendingBatch:
@@ -83,14 +75,13 @@ class PendingBatch:
         with tracing.trace_range("tb.gpu_wait"):
             self.event.synchronize()
         t1 = time.perf_counter()
-        stage_recs = [r.numpy() if r is not None else None for r in self._stage_recs]
-        c4_recs = {i: r.numpy() for i, r in self._c4_recs.items()}
+        stage_recs = list(self._stage_recs)
+        c4_recs = dict(self._c4_recs)
         host_versions = {}
         for ver, (vb, vo) in self._versions.items():
-            o = vo.numpy()
-            host_versions[ver] = (vb.numpy()[: int(o[-1])], o)
-        fl = self._flags.numpy().view(np.uint32)
-        dead = self._dead.numpy() if self._dead is not None else None
+            host_versions[ver] = (vb[: int(vo[-1])], vo)
+        fl = self._flags.view(np.uint32)
+        dead = self._dead
         if self.runner.phase_prof:
             self.runner.collect_phase_prof(self._keep)
         kt = {}
@@ -141,41 +132,80 @@ class DeviceRunner:
     DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; sweep: tools/occ_sweep.sh)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None):
-        import torch
+        import os
 
-        self.torch = torch
-        self.device = torch.device(device)
-        if self.device.index is None:  # "cuda" -> the current device, explicitly (helper threads bind to it)
-            self.device = torch.device("cuda", torch.cuda.current_device())
+        from ..ops import hiprt
+
+        self.rt = hiprt
+        with tracing.trace_range("tb.init.hip_context"):
+            self.device = hiprt.parse_device(device)
+            if self.device >= hiprt.device_count():
+                raise DeviceError(f"no HIP device {self.device}")
+            hiprt.set_device(self.device)
         self.plan = plan
         self.steps = steps_native
         h = native.host()
-        from ..ops.kernels import Kernels
+        # Streams. The box exposes GPU_MAX_HW_QUEUES=4 hardware queues per process and HIP maps
+        # streams onto them round-robin, so the default layout ("4") creates exactly four: per
+        # slot one compute stream (wave kernels, C4, language-id head, gates, D2H) and one side
+        # stream (long-document workgroup kernels first, then the language-id bag, and the H2D
+        # of the next batch), at high priority so the long-document tail is dispatched early.
+        # TB_STREAMS=13 restores the previous layout (5 per slot + copies) for A/B runs;
+        # TB_SERIAL_STREAMS=1 puts everything on one stream (exclusive kernel timings).
+        blk_prio = int(os.environ.get("TB_BLK_PRIORITY", "-1"))
+        serial = os.environ.get("TB_SERIAL_STREAMS", "") not in ("", "0")
+        self.stream_layout = "serial" if serial else os.environ.get("TB_STREAMS", "4")
+        if self.stream_layout not in ("serial", "4", "13"):
+            raise DeviceError("TB_STREAMS must be 4 or 13")
+        self.slots = [_Slot() for _ in range(self.N_SLOTS)]
+        if self.stream_layout == "serial":
+            one = hiprt.Stream()
+            for sl in self.slots:
+                sl.main = sl.s_lid = sl.s_blk = sl.s_c4 = sl.s_c4blk = sl.s_h2d = sl.s_d2h = one
+        elif self.stream_layout == "4":
+            for sl in self.slots:
+                sl.main = sl.s_c4 = sl.s_d2h = hiprt.Stream()
+                sl.s_blk = sl.s_lid = sl.s_c4blk = sl.s_h2d = hiprt.Stream(priority=blk_prio)
+        else:
+            h2d, d2h = hiprt.Stream(), hiprt.Stream()
+            for sl in self.slots:
+                sl.main = hiprt.Stream()
+                sl.s_lid = hiprt.Stream()
+                sl.s_blk = hiprt.Stream(priority=blk_prio)
+                sl.s_c4 = hiprt.Stream()
+                sl.s_c4blk = hiprt.Stream(priority=blk_prio)
+                sl.s_h2d, sl.s_d2h = h2d, d2h
+        init = self.slots[0].main
+        with hiprt.stream(init):
+            from ..ops.kernels import Kernels
 
-        self.k = Kernels(torch, self.device)
-        plan_b, stage_bs = h.build_device_plan(steps_native, plan.stages)
-        self.plan_t = self._to_dev(plan_b)
-        self.stage_ts = [self._to_dev(b) for b in stage_bs]
-        self.stage_layout = [h.stage_layout(b) for b in stage_bs]
-        self.c4_ts = {i: self._to_dev(h.build_c4(steps_native[i])) for i in plan.c4_steps}
-        self.has_lid = any(steps_native[i].kind == h.StepKind.LanguageDetection for st in plan.stages for i in st)
-        if self.has_lid:
-            if langid is None:
-                raise DeviceError("LanguageDetectionFilter needs a language-id model")
-            self.lid_emb = torch.from_numpy(langid.emb).to(self.device)
-            wT = np.ascontiguousarray(langid.w.reshape(h.LID_DIM, h.LID_LANGS_PAD).T)  # [16][32]
-            self.lid_wT = torch.from_numpy(wT).to(self.device)
-            self.lid_b = torch.from_numpy(langid.b.astype(np.float32)).to(self.device)
-        self.c4_growth = int(h.C4_MAX_GROWTH)
-        # TB_GATE=0 disables step gating (every pass runs over every document)
-        import os as _os
-
-        self.gating = _os.environ.get("TB_GATE", "1") not in ("", "0")
-        self.passes, self.pass_of_step, gates = plan_passes(plan, self.stage_layout, steps_native, self.gating)
-        self.gate_ts = {p: self._to_dev(b) for p, b in gates.items()}
+            with tracing.trace_range("tb.init.kernels"):
+                self.k = Kernels(self.device)
+            plan_b, stage_bs = h.build_device_plan(steps_native, plan.stages)
+            self.plan_t = self._to_dev(plan_b)
+            self.stage_ts = [self._to_dev(b) for b in stage_bs]
+            self.stage_layout = [h.stage_layout(b) for b in stage_bs]
+            self.c4_ts = {i: self._to_dev(h.build_c4(steps_native[i])) for i in plan.c4_steps}
+            self.has_lid = any(steps_native[i].kind == h.StepKind.LanguageDetection
+                               for st in plan.stages for i in st)
+            if self.has_lid:
+                if langid is None:
+                    raise DeviceError("LanguageDetectionFilter needs a language-id model")
+                self.lid_emb = hiprt.to_device(langid.emb)
+                wT = np.ascontiguousarray(langid.w.reshape(h.LID_DIM, h.LID_LANGS_PAD).T)  # [16][32]
+                self.lid_wT = hiprt.to_device(wT)
+                self.lid_b = hiprt.to_device(langid.b.astype(np.float32))
+            self.c4_growth = int(h.C4_MAX_GROWTH)
+            # TB_GATE=0 disables step gating (every pass runs over every document)
+            self.gating = os.environ.get("TB_GATE", "1") not in ("", "0")
+            self.passes, self.pass_of_step, gates = plan_passes(plan, self.stage_layout, steps_native, self.gating)
+            self.gate_ts = {p: self._to_dev(b) for p, b in gates.items()}
+            # B^k for the hashes, shared read-only by both slots: allocated once (longer spans
+            # fall back to powmod61 in the kernels)
+            with tracing.trace_range("tb.init.pow_table"):
+                self.k.pow_table(1 << 22)
+            init.synchronize()  # uploads and the table are complete before any slot stream reads them
         # LDS arena per document (one wave per workgroup); TB_LDS_BYTES overrides for tuning
-        import os
-
         self.lds_bytes = int(os.environ.get("TB_LDS_BYTES", str(self.DEFAULT_LDS_BYTES)))
         self.lds_bytes_c4 = int(os.environ.get("TB_LDS_BYTES_C4", str(self.DEFAULT_LDS_BYTES_C4)))
         if not 0 <= self.lds_bytes_c4 <= 131072:
@@ -205,87 +235,65 @@ class DeviceRunner:
         self.phase_prof = os.environ.get("TB_PHASE_PROF", "") not in ("", "0")
         self.phase_totals: Dict[str, np.ndarray] = {}
         self.phase_docs: Dict[str, int] = {}
-        self.slots = [_Slot() for _ in range(self.N_SLOTS)]
-        self.h2d_stream = torch.cuda.Stream(self.device)
-        self.d2h_stream = torch.cuda.Stream(self.device)
-        # The long-document workgroup kernels are the tail of every stage (few, long-lived
-        # workgroups): their stream gets the highest priority so they are dispatched before the
-        # wave kernels that run next to them (TB_BLK_PRIORITY=0 disables).
-        blk_prio = int(os.environ.get("TB_BLK_PRIORITY", "-1"))
-        serial = os.environ.get("TB_SERIAL_STREAMS", "") not in ("", "0")
-        for sl in self.slots:
-            if serial:
-                # profiling aid: every kernel on one stream (exclusive durations, no overlap)
-                sl.main = sl.s_lid = sl.s_blk = sl.s_c4 = sl.s_c4blk = torch.cuda.current_stream(self.device)
-                continue
-            sl.main = torch.cuda.Stream(self.device)
-            sl.s_lid = torch.cuda.Stream(self.device)
-            sl.s_blk = torch.cuda.Stream(self.device, priority=blk_prio)
-            sl.s_c4 = torch.cuda.Stream(self.device)
-            sl.s_c4blk = torch.cuda.Stream(self.device, priority=blk_prio)
-        # B^k for the hashes, shared read-only by both slots: allocated once (longer spans fall
-        # back to powmod61 in the kernels)
-        self.k.pow_table(1 << 22)
-        torch.cuda.synchronize(self.device)  # uploads and the table are complete before any slot stream reads them
         self.copy_threads = int(os.environ.get("TB_COPY_THREADS", "8"))
         self._next_slot = 0
         self._last_lid = None
-        self.s_bw = torch.cuda.Stream(self.device)
-        self._bw_auto = None  # (key, device tensors) of the flattened bad-words automaton
+        self.s_bw = None      # bad-words stream, created on first use (not part of the batch pipeline)
+        self._bw_auto = None  # (key, device arrays) of the flattened bad-words automaton
         self._bw_fold = None
 
     def bind_thread(self) -> None:
         """Make this runner's GPU the current device of the calling thread (HIP's current device
         is per thread; helper threads that launch work for this runner call this first)."""
-        self.torch.cuda.set_device(self.device)
+        self.rt.set_device(self.device)
+
+    def synchronize(self) -> None:
+        """Wait for all queued device work (error recovery drains the queues before it frees)."""
+        self.rt.synchronize()
 
     def badwords_match(self, key, automaton, data: np.ndarray, off: np.ndarray, roots: np.ndarray,
                        cjk: np.ndarray) -> np.ndarray:
         """C4 bad-words matching of post-resolve contents on the device (k_badwords_match): one
         wave per document walks the flattened word-list tries from every code point. ``roots``:
         per document the root node of its language's trie. Returns 1 (match) / 0 per document."""
-        torch = self.torch
+        rt = self.rt
         n = len(off) - 1
         if n == 0:
             return np.zeros(0, dtype=np.int8)
         if roots.shape != (n,) or cjk.shape != (n,) or int(off[-1]) > len(data):
             raise DeviceError("badwords_match: operand shapes")
-        if self._bw_fold is None:
-            f1, f2 = native.host().ucd_fold_tables()
-            self._bw_fold = (torch.from_numpy(f1).to(self.device), torch.from_numpy(f2).to(self.device))
-        if self._bw_auto is None or self._bw_auto[0] != key:
-            fe, ec, et, term = automaton
-            nodes = len(term)
-            if len(fe) != nodes + 1 or len(ec) != len(et) or int(fe[-1]) != len(ec):
-                raise DeviceError("badwords automaton is malformed")
-            if nodes and (int(roots.max()) >= nodes or (len(et) and (int(et.min()) < 0 or int(et.max()) >= nodes))):
-                raise DeviceError("badwords automaton node index out of range")
-            dev = tuple(torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
-                        for a in (fe, ec.view(np.int32), et, np.ascontiguousarray(term, dtype=np.uint8)))
-            self._bw_auto = (key, dev)
-        with torch.cuda.stream(self.s_bw):
-            d_bytes = torch.from_numpy(np.ascontiguousarray(data, dtype=np.uint8)).to(self.device, non_blocking=False)
-            d_off = torch.from_numpy(np.ascontiguousarray(off, dtype=np.int64)).to(self.device)
-            d_root = torch.from_numpy(np.ascontiguousarray(roots, dtype=np.int32)).to(self.device)
-            d_cjk = torch.from_numpy(np.ascontiguousarray(cjk, dtype=np.uint8)).to(self.device)
-            out = torch.zeros(n, dtype=torch.int8, device=self.device)
+        if self.s_bw is None:
+            self.s_bw = rt.Stream()
+        with rt.stream(self.s_bw):
+            if self._bw_fold is None:
+                f1, f2 = native.host().ucd_fold_tables()
+                self._bw_fold = (rt.to_device(f1), rt.to_device(f2))
+            if self._bw_auto is None or self._bw_auto[0] != key:
+                fe, ec, et, term = automaton
+                nodes = len(term)
+                if len(fe) != nodes + 1 or len(ec) != len(et) or int(fe[-1]) != len(ec):
+                    raise DeviceError("badwords automaton is malformed")
+                if nodes and (int(roots.max()) >= nodes or (len(et) and (int(et.min()) < 0 or int(et.max()) >= nodes))):
+                    raise DeviceError("badwords automaton node index out of range")
+                dev = tuple(rt.to_device(np.ascontiguousarray(a))
+                            for a in (fe, ec.view(np.int32), et, np.ascontiguousarray(term, dtype=np.uint8)))
+                self._bw_auto = (key, dev)
+            d_bytes = rt.to_device(np.ascontiguousarray(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8))
+            d_off = rt.to_device(np.ascontiguousarray(off, dtype=np.int64))
+            d_root = rt.to_device(np.ascontiguousarray(roots, dtype=np.int32))
+            d_cjk = rt.to_device(np.ascontiguousarray(cjk, dtype=np.uint8))
+            out = rt.zeros(n, np.int8)
             self.k.badwords_match(d_bytes, d_off, n, d_root, d_cjk, self._bw_auto[1], self._bw_fold, out)
-            res = out.cpu().numpy()
-        return res
+            return out.to_host()
 
     def _to_dev(self, b: bytes):
-        t = self.torch.frombuffer(bytearray(b), dtype=self.torch.uint8)
-        return t.to(self.device)
-
-    def _pinned(self, nbytes: int, dtype):
-        t = self.torch.empty(max(nbytes, 8), dtype=self.torch.uint8, pin_memory=True)
-        return t[:nbytes].view(dtype) if nbytes else t[:0].view(dtype)
+        return self.rt.to_device(np.frombuffer(bytes(b), dtype=np.uint8))
 
     def _stage_inputs(self, slot: _Slot, arrays):
         """One H2D transfer for all per-batch inputs: arrays are packed at 256-byte aligned
         offsets into the slot's pinned buffer, copied with one DMA, and returned as typed views
         of the device buffer."""
-        torch = self.torch
+        rt = self.rt
         offs, total = [], 0
         for a in arrays:
             offs.append(total)
@@ -293,59 +301,52 @@ class DeviceRunner:
         total = max(total, SCRATCH_ALIGN)
         if slot.h2d_done is not None:
             slot.h2d_done.synchronize()  # the previous DMA out of this buffer has finished
-        if slot.pinned is None or slot.pinned.numel() < total:
-            slot.pinned = torch.empty(int(total * 1.25), dtype=torch.uint8, pin_memory=True)
-        hv = slot.pinned.numpy()
+        if slot.pinned is None or slot.pinned.nbytes < total:
+            slot.pinned = None
+            slot.pinned = rt.pinned(int(total * 1.25))
+        hv = slot.pinned
         h = native.host()
         for a, o in zip(arrays, offs):
             if a.nbytes:
                 h.parallel_copy(hv, o, np.ascontiguousarray(a).view(np.uint8).reshape(-1), self.copy_threads)
-        # H2D on its own stream: batch k+1's upload overlaps batch k's kernels
-        with torch.cuda.stream(self.h2d_stream):
-            dev = torch.empty(total, dtype=torch.uint8, device=self.device)
-            dev.copy_(slot.pinned[:total], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(self.h2d_stream)
+        # H2D on the upload stream: batch k+1's upload overlaps batch k's kernels
+        dev = rt.empty(total, np.uint8)
+        dev.copy_from_host(hv[:total], slot.s_h2d)
+        ev = slot.s_h2d.record()
         slot.h2d_done = ev
         metrics.H2D_BYTES_TOTAL.inc(total)
-        compute = torch.cuda.current_stream(self.device)
-        compute.wait_event(ev)
-        dev.record_stream(compute)
+        rt.current_stream().wait_event(ev)
         out = []
         for a, o in zip(arrays, offs):
-            dt = _TORCH_DTYPES[np.dtype(a.dtype).str]
-            out.append(dev[o:o + a.nbytes].view(dt) if a.nbytes else dev[o:o].view(dt))
+            out.append(dev[o:o + a.nbytes].view(a.dtype) if a.nbytes else dev[o:o].view(a.dtype))
         return out, dev
 
     def _scratch_for(self, slot: _Slot, nbytes: int, which: str = "stage"):
         attr = "scratch" if which == "stage" else "scratch_c4"
         cur = getattr(slot, attr)
         if cur is None or cur.numel() < nbytes:
+            # the old arena stays alive in the keep list of the batch that last used it
             setattr(slot, attr, None)
-            cur = self.torch.empty(int(nbytes * 1.25) + (1 << 20), dtype=self.torch.uint8, device=self.device)
+            cur = self.rt.empty(int(nbytes * 1.25) + (1 << 20), np.uint8)
             setattr(slot, attr, cur)
         return cur
 
     def _record(self, stream):
-        ev = self.torch.cuda.Event()
-        ev.record(stream)
-        return ev
+        return stream.record()
 
     def _ktimed(self, keep, name: str):
         """Context manager: HIP events around the launches inside it on the current stream; the
         elapsed time lands in tb_gpu_kernel_seconds{kernel=name} when the batch is collected."""
         import contextlib
 
-        torch = self.torch
+        rt = self.rt
 
         @contextlib.contextmanager
         def cm():
-            st = torch.cuda.current_stream(self.device)
-            e0 = torch.cuda.Event(enable_timing=True)
-            e0.record(st)
+            st = rt.current_stream()
+            e0 = rt.Event(timing=True).record(st)
             yield
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record(st)
+            e1 = rt.Event(timing=True).record(st)
             keep.append(("ktime", name, (e0, e1)))
 
         return cm()
@@ -353,7 +354,7 @@ class DeviceRunner:
     def _prof_buf(self, ndocs, keep, name):
         if not self.phase_prof:
             return None
-        t = self.torch.zeros(ndocs * 32, dtype=self.torch.int64, device=self.device)
+        t = self.rt.zeros(ndocs * 32, np.int64)
         keep.append(("prof", name, t))
         return t
 
@@ -361,7 +362,7 @@ class DeviceRunner:
         for item in keep:
             if isinstance(item, tuple) and len(item) == 3 and item[0] == "prof":
                 _, name, t = item
-                a = t.view(-1, 32).sum(0).cpu().numpy()
+                a = t.to_host().reshape(-1, 32).sum(0)
                 self.phase_totals[name] = self.phase_totals.get(name, 0) + a
                 self.phase_docs[name] = self.phase_docs.get(name, 0) + t.numel() // 32
 
@@ -383,18 +384,16 @@ class DeviceRunner:
         """Stage inputs, enqueue every device stage and the D2H copies; returns immediately."""
         import time
 
-        torch = self.torch
-        h = native.host()
         t0 = time.perf_counter()
         slot = self.slots[self._next_slot]
         self._next_slot = (self._next_slot + 1) % self.N_SLOTS
-        with torch.cuda.stream(slot.main):
+        with self.rt.stream(slot.main):
             return self._submit_on(slot, data, off, t0)
 
     def _submit_on(self, slot: "_Slot", data: np.ndarray, off: np.ndarray, t0: float) -> PendingBatch:
         import time
 
-        torch = self.torch
+        rt = self.rt
         h = native.host()
         ndocs = len(off) - 1
         lens = np.diff(off)
@@ -421,8 +420,8 @@ class DeviceRunner:
         # grows (new tensor, on this slot's stream) only for documents over 2 MB; the batch keeps a
         # reference to the table it used, so the other slot's kernels never see it freed
         pw, pw_n = self.k.pow_table(2 * maxlen + 64)
-        flags = torch.zeros(ndocs, dtype=torch.int32, device=self.device)
-        dead = torch.zeros(ndocs, dtype=torch.uint8, device=self.device) if self.gate_ts else None
+        flags = rt.zeros(ndocs, np.int32)
+        dead = rt.zeros(ndocs, np.uint8) if self.gate_ts else None
         pass_idx = 0
         t1 = time.perf_counter()
         versions = {0: (d_bytes, d_off, len(data))}
@@ -433,7 +432,7 @@ class DeviceRunner:
         #   language-id bag (s_lid) | long-doc workgroup kernels (s_blk) | wave kernels (main)
         #   | C4 pass A/B of the same content version (s_c4, own scratch arena)
         # Block and wave kernels touch disjoint documents, so they share the stage arena.
-        main = torch.cuda.current_stream(self.device)
+        main = rt.current_stream()
         ready = {0: self._record(main)}
         tails = []
         c4_scratch = None
@@ -444,34 +443,36 @@ class DeviceRunner:
                 if sv != ver:
                     continue
                 width_total, layout = self.stage_layout[s]
-                rec = torch.zeros(width_total * ndocs, dtype=torch.int64, device=self.device)
+                rec = rt.zeros(width_total * ndocs, np.int64)
                 lid_vec = lid_cnt = None
                 if any(kind == 4 for kind, _, _ in layout):
-                    lid_vec = torch.zeros(ndocs * h.LID_DIM, dtype=torch.int16, device=self.device)
-                    lid_cnt = torch.zeros(ndocs, dtype=torch.int32, device=self.device)
+                    lid_vec = rt.zeros(ndocs * h.LID_DIM, np.int16)
+                    lid_cnt = rt.zeros(ndocs, np.int32)
                 ev_pre = self._record(main)  # rec / lid buffers zeroed
                 ev_lid = ev_blk = None
-                if lid_vec is not None:
-                    slot.s_lid.wait_event(ev_pre)
-                    with torch.cuda.stream(slot.s_lid), self._ktimed(keep, "langid_features"):
-                        self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec,
-                                               lid_cnt, flags, self.lds_bytes_lid,
-                                               self._prof_buf(ndocs, keep, f"langid{s}"))
-                        ev_lid = self._record(slot.s_lid)
                 prof = self._prof_buf(ndocs, keep, f"stage{s}")
                 skip = dead if pass_idx > 0 else None
+                # long documents first: with the 4-stream layout the workgroup kernels and the
+                # language-id bag share the side stream, and the long-document tail must start early
                 if n_long:
                     slot.s_blk.wait_event(ev_pre)
-                    with torch.cuda.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_blk"):
+                    with rt.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_blk"):
                         self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[:n_long], n_long,
                                                  ndocs, scratch, d_soff, pw, pw_n, rec, flags, lid_vec, lid_cnt,
                                                  self.lds_bytes_blk, prof, skip)
                         ev_blk = self._record(slot.s_blk)
+                if lid_vec is not None:
+                    slot.s_lid.wait_event(ev_pre)
+                    with rt.stream(slot.s_lid), self._ktimed(keep, "langid_features"):
+                        self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec,
+                                               lid_cnt, flags, self.lds_bytes_lid,
+                                               self._prof_buf(ndocs, keep, f"langid{s}"))
+                        ev_lid = self._record(slot.s_lid)
                 if n_mid > n_long:
                     # mid-size documents on the long-document stream, after its workgroup kernel
                     if ev_blk is None:
                         slot.s_blk.wait_event(ev_pre)
-                    with torch.cuda.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_mid"):
+                    with rt.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_mid"):
                         self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,
                                              scratch, d_soff[n_long:], pw, pw_n, rec, flags,
                                              self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
@@ -501,11 +502,11 @@ class DeviceRunner:
                 # content version (it waits for the gate on the compute stream), and the stages of
                 # the next version start after its pass B (ready event).
                 c4_scratch = scratch
-                rec = torch.zeros(7 * ndocs, dtype=torch.int64, device=self.device)
-                src = torch.zeros(2 * ndocs, dtype=torch.int64, device=self.device)
-                new_off = torch.zeros(ndocs + 1, dtype=torch.int64, device=self.device)
+                rec = rt.zeros(7 * ndocs, np.int64)
+                src = rt.zeros(2 * ndocs, np.int64)
+                new_off = rt.zeros(ndocs + 1, np.int64)
                 cap = vlen + self.c4_growth * ndocs + 16  # device rewrites never grow more (kC4MaxGrowth)
-                out = torch.empty(cap, dtype=torch.uint8, device=self.device)
+                out = rt.empty(cap, np.uint8)
                 slot.s_c4.wait_event(self._record(main))
                 slot.s_c4.wait_event(ready[ver])
                 skip = dead if pass_idx > 0 else None
@@ -514,17 +515,17 @@ class DeviceRunner:
                 if n_long:
                     # long documents (workgroup kernel) next to the wave kernel: disjoint docs
                     slot.s_c4blk.wait_event(self._record(slot.s_c4))
-                    with torch.cuda.stream(slot.s_c4blk):
+                    with rt.stream(slot.s_c4blk):
                         self.k.c4_pass_a_blk(self.c4_ts[i], vb, vo, d_perm[:n_long], n_long, ndocs, c4_scratch,
                                              d_soff, pw, pw_n, rec, src, flags, self.lds_bytes_blk, prof, skip)
                         ev_c4blk = self._record(slot.s_c4blk)
-                with torch.cuda.stream(slot.s_c4), self._ktimed(keep, f"c4_step{i}"):
+                with rt.stream(slot.s_c4), self._ktimed(keep, f"c4_step{i}"):
                     if n_long < ndocs:
                         self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm[n_long:], ndocs, c4_scratch, d_soff[n_long:], pw,
                                          pw_n, rec, src, flags, self.lds_bytes_c4, prof, ndocs - n_long, skip)
                     if ev_c4blk is not None:
                         slot.s_c4.wait_event(ev_c4blk)
-                    torch.cumsum(src.view(ndocs, 2)[:, 1], 0, out=new_off[1:])
+                    rt.scan_strided_i64(src[1:], 2, ndocs, new_off[1:])
                     self.k.c4_pass_b(vb, vo, ndocs, c4_scratch, d_soff, src, new_off, out)
                     if pass_idx in self.gate_ts:
                         self.k.gate(self.gate_ts[pass_idx], [rec], ndocs, flags, dead, pass_idx + 1, 0)
@@ -537,33 +538,27 @@ class DeviceRunner:
                 keep.append(src)
         for ev in tails:
             main.wait_event(ev)
-        # D2H into pinned host buffers on the download stream (overlaps the next batch's
-        # kernels), then one completion event
-        done = torch.cuda.Event()
-        done.record(torch.cuda.current_stream(self.device))
-        self.d2h_stream.wait_event(done)
+        # D2H into pinned host buffers on the download stream (the slot's compute stream in the
+        # 4-stream layout: it is last in line there anyway), then one completion event
+        done = self._record(main)
+        d2h_s = slot.s_d2h
+        if d2h_s is not main:
+            d2h_s.wait_event(done)
 
         def d2h(t):
-            ht = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-            ht.copy_(t, non_blocking=True)
-            t.record_stream(self.d2h_stream)
+            ht = rt.pinned(t.numel(), t.dtype)
+            t.copy_to_host(ht, d2h_s)
             return ht
 
-        with torch.cuda.stream(self.d2h_stream):
-            h_stage = [d2h(r) if r is not None else None for r in stage_recs_d]
-            h_c4 = {i: d2h(r) for i, r in c4_recs_d.items()}
-            h_versions = {}
-            for ver in range(1, self.plan.n_versions):
-                vb, vo, _ = versions[ver]
-                h_versions[ver] = (d2h(vb), d2h(vo))
-            h_flags = d2h(flags)
-            h_dead = d2h(dead) if dead is not None else None
-            if self.phase_prof:
-                for item in keep:
-                    if isinstance(item, tuple) and len(item) == 3 and item[0] == "prof":
-                        item[2].record_stream(self.d2h_stream)
-            ev = torch.cuda.Event()
-            ev.record(self.d2h_stream)
+        h_stage = [d2h(r) if r is not None else None for r in stage_recs_d]
+        h_c4 = {i: d2h(r) for i, r in c4_recs_d.items()}
+        h_versions = {}
+        for ver in range(1, self.plan.n_versions):
+            vb, vo, _ = versions[ver]
+            h_versions[ver] = (d2h(vb), d2h(vo))
+        h_flags = d2h(flags)
+        h_dead = d2h(dead) if dead is not None else None
+        ev = self._record(d2h_s)
         keep += [stage_recs_d, c4_recs_d, versions, flags, dead]
         t2 = time.perf_counter()
         return PendingBatch(self, ndocs, ev, h_stage, h_c4, h_versions, h_flags,

@@ -124,7 +124,8 @@ class Engine:
         if "LanguageDetectionFilter" in types:
             from ..models.langid import load_default
 
-            self.langid = langid or load_default()
+            with tracing.trace_range("tb.init.langid"):
+                self.langid = langid or load_default()
         self.lid_native = self.langid.native() if self.langid is not None else None
         self.tokenizers: Dict[int, object] = dict(tokenizers or {})
         for i, s in enumerate(cfg.pipeline):
@@ -137,7 +138,8 @@ class Engine:
             bw_dirs = [s.params.cache_base_path for s in cfg.pipeline
                        if s.type == "C4BadWordsFilter" and s.params.cache_base_path]
             d = badwords_dir or (bw_dirs[0] if bw_dirs else os.path.join("data", "c4_badwords"))
-            self.badwords = self.h.BadWordsModule(d)
+            with tracing.trace_range("tb.init.badwords"):
+                self.badwords = self.h.BadWordsModule(d)
         self.device_runner = None
         if backend == "emulate":
             from .device import EmulatedRunner
@@ -150,7 +152,8 @@ class Engine:
                     raise ConfigError(f"step {st.name} cannot run on the device: {why}")
             from .device import DeviceRunner
 
-            self.device_runner = DeviceRunner(self.steps, self.plan, device or "cuda", self.langid)
+            with tracing.trace_range("tb.init.device_runner"):
+                self.device_runner = DeviceRunner(self.steps, self.plan, device or "cuda", self.langid)
 
     # ------------------------------------------------------------------------------------------
     def process(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None,
@@ -294,6 +297,12 @@ class Engine:
         log = logging.getLogger("textblaster_amd.engine")
         n = len(off) - 1
         log.warning("batch of %d docs failed on %s (%s: %s); recovering", n, self.backend, type(err).__name__, err)
+        drain = getattr(self.device_runner, "synchronize", None)
+        if drain is not None:
+            try:  # work queued by the failed submission finishes before its buffers are reused
+                drain()
+            except Exception:  # noqa: BLE001 - a sticky device error surfaces again on the retry
+                pass
         metrics.BATCH_FAILURES_TOTAL.labels(type(err).__name__).inc()
         if self.backend != "cpu" and n > 1 and not _is_sticky(err):
             try:
@@ -576,9 +585,10 @@ class _Submitted:
 
 
 def _cuda_available() -> bool:
+    """A HIP device is visible (asked through the native runtime layer, no PyTorch import)."""
     try:
-        import torch
+        from ..ops import hiprt
 
-        return torch.cuda.is_available()
+        return hiprt.device_count() > 0
     except Exception:
         return False

@@ -48,7 +48,7 @@ import pyarrow.parquet as pq
 from .config.pipeline import PipelineConfig, load_pipeline_config
 from .errors import PipelineError, Unexpected
 from .io.parquet import (DocBatch, ParquetInputConfig, ParquetReader, ParquetWriter, build_output_table,
-                         packed_to_string_array)
+                         encode_table, packed_to_string_array)
 from .parallel.dist import DistContext, shard_ranges
 from .parallel.heartbeat import Heartbeat
 from .utils import metrics, tracing
@@ -79,7 +79,8 @@ class RunConfig:
     metrics_port: Optional[int] = None
     progress_interval: float = 1.0
     tokenizer_file: Optional[str] = None
-    read_threads: int = int(os.environ.get("TB_READ_THREADS", "3"))  # row groups decoded concurrently
+    read_threads: int = int(os.environ.get("TB_READ_THREADS", "8"))   # row groups decoded concurrently
+    write_threads: int = int(os.environ.get("TB_WRITE_THREADS", "4"))  # units encoded concurrently
     fault_inject: Optional[str] = None   # debug: "kernel@N" / "oom@N" (N = 1-based batch)
 
 
@@ -152,7 +153,10 @@ class _UnitReader:
         self._tbl = None
         self.seconds = 0.0
         # worker threads open their own ParquetFile (a reader object is not shared across threads)
-        self._pf = pq.ParquetFile(reader.config.path) if own_file else None
+        self._pf = pq.ParquetFile(reader.config.path, memory_map=True) if own_file else None
+        # several reader threads decode row groups side by side: Arrow's own column threads on
+        # top of that only add contention (measured slower)
+        self._use_threads = not own_file
 
     def read(self, u: Unit) -> DocBatch:
         t0 = time.perf_counter()
@@ -165,12 +169,14 @@ class _UnitReader:
     def _read(self, u: Unit) -> DocBatch:
         if u.row_group != self._rg:
             pf = self._pf if self._pf is not None else self.reader._pf
-            self._tbl = pf.read_row_group(u.row_group, columns=self.reader.columns, use_threads=True)
+            with tracing.trace_range("tb.read_row_group"):
+                self._tbl = pf.read_row_group(u.row_group, columns=self.reader.columns, use_threads=self._use_threads)
             self._rg = u.row_group
         t = self._tbl.slice(u.start, u.stop - u.start).combine_chunks()
         batches = t.to_batches()
         rb = batches[0] if batches else pa.RecordBatch.from_pylist([], schema=t.schema)
-        return self.reader._to_docbatch(rb)
+        with tracing.trace_range("tb.to_docbatch"):
+            return self.reader._to_docbatch(rb)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -185,7 +191,9 @@ def part_table(batch: DocBatch, part) -> pa.Table:
 
 
 class _Sink:
-    def write(self, unit: Unit, kept: pa.Table, excluded: pa.Table, counts: Dict) -> None:
+    """Receives every unit's two encoded Parquet files (kept, excluded) in unit order."""
+
+    def commit(self, unit: Unit, kept: Tuple[pa.Buffer, int], excluded: Tuple[pa.Buffer, int], counts: Dict) -> None:
         raise NotImplementedError
 
     def close(self) -> None:
@@ -193,17 +201,27 @@ class _Sink:
 
 
 class _DirectSink(_Sink):
-    def __init__(self, rc: RunConfig):
-        self.out = ParquetWriter(rc.output_file, rc.compression)
-        self.exc = ParquetWriter(rc.excluded_file, rc.compression)
+    """Single rank without checkpoints: row groups are appended straight to the two outputs."""
 
-    def write(self, unit, kept, excluded, counts):
-        self.out.write_table(kept)
-        self.exc.write_table(excluded)
+    def __init__(self, rc: RunConfig):
+        from .io.pqconcat import StreamConcat
+
+        self.rc = rc
+        self.outs = []
+        for path in (rc.output_file, rc.excluded_file):
+            parent = os.path.dirname(os.path.abspath(path))
+            os.makedirs(parent, exist_ok=True)
+            self.outs.append(StreamConcat(path))
+
+    def commit(self, unit, kept, excluded, counts):
+        for out, (buf, rows) in zip(self.outs, (kept, excluded)):
+            if rows:
+                out.append(buf)
 
     def close(self):
-        self.out.close()
-        self.exc.close()
+        for out in self.outs:
+            if not out.close():        # nothing appended: a valid empty file with the schema
+                ParquetWriter(out.path, self.rc.compression).close()
 
 
 class _PartSink(_Sink):
@@ -213,13 +231,12 @@ class _PartSink(_Sink):
         os.makedirs(self.parts, exist_ok=True)
         self.manifest = open(os.path.join(work_dir, f"manifest.rank{rank}.jsonl"), "a", encoding="utf-8")
 
-    def write(self, unit, kept, excluded, counts):
-        for kind, tbl in (("kept", kept), ("excluded", excluded)):
+    def commit(self, unit, kept, excluded, counts):
+        for kind, (buf, _) in (("kept", kept), ("excluded", excluded)):
             final = os.path.join(self.parts, f"u{unit.index:07d}.{kind}.parquet")
             tmp = final + ".tmp"
-            w = ParquetWriter(tmp, self.rc.compression)
-            w.write_table(tbl)
-            w.close()
+            with open(tmp, "wb") as f:
+                f.write(memoryview(buf))
             os.replace(tmp, final)
         self.manifest.write(json.dumps(dict(unit=unit.index, **counts)) + "\n")
         self.manifest.flush()
@@ -320,41 +337,54 @@ def merge_parts(work_dir: str, my_units: List[int], rc: RunConfig, ctx: Optional
 
 # ---------------------------------------------------------------------------------------------
 
-def _prefetch(gen: Iterator, depth: int) -> Iterator:
-    """Runs ``gen`` in a thread, keeping up to ``depth`` items ready."""
-    q: queue.Queue = queue.Queue(maxsize=depth)
-    sentinel = object()
-    err: List[BaseException] = []
-    stop = threading.Event()
+class _Prefetcher:
+    """Drives ``gen`` on its own thread, keeping up to ``depth`` items ready. Started before the
+    engine is built, so Parquet decoding overlaps HIP context creation and kernel loading
+    instead of following them. ``close`` stops the thread (also when nothing was consumed)."""
 
-    def worker():
+    def __init__(self, gen: Iterator, depth: int):
+        self.q: queue.Queue = queue.Queue(maxsize=max(1, depth))
+        self.err: List[BaseException] = []
+        self.stop = threading.Event()
+        self._end = object()
+        self._gen = gen
+        self.t = threading.Thread(target=self._work, name="tb-prefetch", daemon=True)
+        self.t.start()
+
+    def _put(self, item) -> bool:
+        while not self.stop.is_set():
+            try:
+                self.q.put(item, timeout=0.1)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def _work(self):
         try:
-            for item in gen:
-                while not stop.is_set():
-                    try:
-                        q.put(item, timeout=0.1)
-                        break
-                    except queue.Full:
-                        continue
-                if stop.is_set():
-                    return
+            for item in self._gen:
+                if not self._put(item):
+                    break
         except BaseException as e:  # noqa: BLE001 - re-raised in the consumer
-            err.append(e)
+            self.err.append(e)
         finally:
-            q.put(sentinel)
+            self._put(self._end)
+            close = getattr(self._gen, "close", None)
+            if close is not None and self.stop.is_set():
+                close()
 
-    t = threading.Thread(target=worker, name="tb-reader", daemon=True)
-    t.start()
-    try:
+    def __iter__(self):
         while True:
-            item = q.get()
-            if item is sentinel:
+            item = self.q.get()
+            if item is self._end:
                 break
             yield item
-        if err:
-            raise err[0]
-    finally:
-        stop.set()
+        if self.err:
+            raise self.err[0]
+
+    def close(self):
+        self.stop.set()
+        self.t.join(timeout=60)
 
 
 def _read_units(reader: ParquetReader, units: List[Unit], nthreads: int, timer: _UnitReader):
@@ -396,49 +426,83 @@ def _read_units(reader: ParquetReader, units: List[Unit], nthreads: int, timer: 
 
 
 class _Writer:
-    """Single background writer thread; ``submit`` blocks when ``depth`` writes are pending."""
+    """Output side of the run. A pool of encoder threads turns each unit's kept / excluded rows
+    into two in-memory Parquet files concurrently (Arrow assembly and Parquet encoding release
+    the GIL); one committer thread hands them to the sink in unit order (appending row groups
+    to the final files, or writing checkpoint parts). ``submit`` blocks when ``depth`` units
+    are pending. reference parquet_writer.rs:69-164 writes one row group per batch on the
+    producer thread."""
 
-    def __init__(self, sink: _Sink, depth: int = 2):
+    def __init__(self, sink: _Sink, compression: str = "none", threads: int = 4, depth: Optional[int] = None):
+        import concurrent.futures as cf
+
         self.sink = sink
-        self.q: queue.Queue = queue.Queue(maxsize=depth)
+        self.compression = compression
+        self.pool = cf.ThreadPoolExecutor(max_workers=max(1, threads), thread_name_prefix="tb-encode")
+        self.q: queue.Queue = queue.Queue(maxsize=depth or max(1, threads) + 2)
         self.err: List[BaseException] = []
         self.seconds = 0.0
+        self._lock = threading.Lock()
         self.t = threading.Thread(target=self._run, name="tb-writer", daemon=True)
         self.t.start()
 
+    def _encode(self, job):
+        t0 = time.perf_counter()
+        batch, res, unit, counts = job
+        with tracing.trace_range("tb.part_table"):
+            kept, exc = self._tables(batch, res)
+        with tracing.trace_range("tb.encode"):
+            out = (unit, (encode_table(kept, self.compression), kept.num_rows),
+                   (encode_table(exc, self.compression), exc.num_rows), counts)
+        with self._lock:
+            self.seconds += time.perf_counter() - t0
+        return out
+
     def _run(self):
         while True:
-            job = self.q.get()
-            if job is None:
+            fut = self.q.get()
+            if fut is None:
                 return
-            if self.err:
-                continue
-            t0 = time.perf_counter()
             try:
-                batch, res, unit, counts = job
-                kept = part_table(batch, res.kept[0]) if len(res.kept) == 1 else pa.concat_tables(
-                    [part_table(batch, p) for p in res.kept])
-                exc = part_table(batch, res.excluded[0]) if len(res.excluded) == 1 else pa.concat_tables(
-                    [part_table(batch, p) for p in res.excluded])
-                if len(res.kept) > 1:
-                    kept = _sort_by_row(kept, np.concatenate([p.rows for p in res.kept]))
-                if len(res.excluded) > 1:
-                    exc = _sort_by_row(exc, np.concatenate([p.rows for p in res.excluded]))
+                unit, kept, exc, counts = fut.result()
+                if self.err:
+                    continue
+                t0 = time.perf_counter()
                 with tracing.trace_range("tb.write"):
-                    self.sink.write(unit, kept, exc, counts)
-            except BaseException as e:  # noqa: BLE001
+                    self.sink.commit(unit, kept, exc, counts)
+                with self._lock:
+                    self.seconds += time.perf_counter() - t0
+            except BaseException as e:  # noqa: BLE001 - re-raised on the main thread
                 self.err.append(e)
-            self.seconds += time.perf_counter() - t0
+
+    @staticmethod
+    def _tables(batch, res):
+        kept = part_table(batch, res.kept[0]) if len(res.kept) == 1 else pa.concat_tables(
+            [part_table(batch, p) for p in res.kept])
+        exc = part_table(batch, res.excluded[0]) if len(res.excluded) == 1 else pa.concat_tables(
+            [part_table(batch, p) for p in res.excluded])
+        if len(res.kept) > 1:
+            kept = _sort_by_row(kept, np.concatenate([p.rows for p in res.kept]))
+        if len(res.excluded) > 1:
+            exc = _sort_by_row(exc, np.concatenate([p.rows for p in res.excluded]))
+        return kept, exc
 
     def submit(self, job):
         if self.err:
             raise self.err[0]
-        self.q.put(job)
+        self.q.put(self.pool.submit(self._encode, job))
 
     def close(self):
         self.q.put(None)
         self.t.join()
-        self.sink.close()
+        self.pool.shutdown(wait=True)
+        if not self.err:
+            self.sink.close()
+        else:
+            try:
+                self.sink.close()
+            except BaseException:  # noqa: BLE001 - the first error wins
+                pass
         if self.err:
             raise self.err[0]
 
@@ -461,22 +525,16 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     rank_fault = _parse_rank_fault(rc.fault_inject, world)
     html_dec = None
     if rc.html_decode == "gpu":
-        if ctx.device is None:
+        dev = ctx.device if ctx.device is not None else ("cuda" if rc.backend == "cuda" else None)
+        if dev is None:
             raise PipelineError("--html-decode gpu needs a GPU rank")
         from .ops.html import HtmlDecoder
 
-        html_dec = HtmlDecoder(ctx.device)
+        html_dec = HtmlDecoder(dev)
     elif rc.html_decode != "cpu":
         raise PipelineError(f"unknown html decode backend {rc.html_decode!r} (cpu | gpu)")
     reader = ParquetReader(ParquetInputConfig(rc.input_file, rc.text_column, rc.id_column), html_decoder=html_dec)
     units = plan_units(reader, rc.unit_rows)
-    if engine is None:
-        backend = rc.backend
-        device = ctx.device if backend in ("cuda", "auto") else None
-        engine = Engine(cfg, backend=backend, device=device, nthreads=rc.threads, segmentation=rc.segmentation,
-                        tokenizer_dir=rc.tokenizer_dir, badwords_dir=rc.badwords_dir,
-                        tokenizer_file=rc.tokenizer_file,
-                        fault_inject=None if rank_fault is not None else rc.fault_inject)
     use_parts = world > 1 or rc.checkpoint or rc.resume
     work_dir = rc.work_dir or (rc.output_file + ".work")
     done: Dict[int, Dict] = {}
@@ -521,6 +579,21 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     metrics.WORLD_SIZE.set(world)
     if rank == 0 and rc.metrics_port is not None:
         metrics.setup_prometheus_metrics(rc.metrics_port)
+    # input decoding starts now and overlaps the engine (HIP context, kernels, model) set-up
+    ureader = _UnitReader(reader)
+    source = _Prefetcher(_read_units(reader, todo, rc.read_threads, ureader), depth=rc.read_threads + 2)
+    try:
+        if engine is None:
+            backend = rc.backend
+            device = ctx.device if backend in ("cuda", "auto") else None
+            with tracing.trace_range("tb.engine_init"):
+                engine = Engine(cfg, backend=backend, device=device, nthreads=rc.threads,
+                                segmentation=rc.segmentation, tokenizer_dir=rc.tokenizer_dir,
+                                badwords_dir=rc.badwords_dir, tokenizer_file=rc.tokenizer_file,
+                                fault_inject=None if rank_fault is not None else rc.fault_inject)
+    except BaseException:
+        source.close()
+        raise
     log.info("rank %d/%d: %d units (%d already done), backend=%s", rank, world, len(mine), len(mine) - len(todo),
              engine.backend)
 
@@ -528,18 +601,18 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
                    on_global=_publish_global if rank == 0 else None)
     hb.update(local.vector(nsteps))
     sink = _PartSink(rc, work_dir, rank) if use_parts else _DirectSink(rc)
-    writer = _Writer(sink)
-    ureader = _UnitReader(reader)
+    writer = _Writer(sink, rc.compression, rc.write_threads)
     last_report = time.perf_counter()
     last_docs = local.docs
     inflight: collections.deque = collections.deque()
 
     def feed():
-        for unit, batch in _read_units(reader, todo, rc.read_threads, ureader):
+        for unit, batch in source:
             inflight.append((unit, batch))
             yield batch.text[0], batch.text[1], batch.meta
 
     t_loop = time.perf_counter()
+    setup_s = t_loop - t_start
     try:
         t_prev = time.perf_counter()
         for res in engine.process_many(feed(), on_error="recover"):
@@ -552,7 +625,8 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
             counts = dict(docs=batch.n + batch.error_rows, kept=res.n_kept, excluded=res.n_excluded,
                           errors=int(len(res.error_rows)) + batch.error_rows,
                           step_filtered=[int(x) for x in step_counts])
-            writer.submit((batch, res, unit, counts))
+            with tracing.trace_range("tb.writer_submit"):
+                writer.submit((batch, res, unit, counts))
             local.docs += counts["docs"]
             local.kept += counts["kept"]
             local.excluded += counts["excluded"]
@@ -577,9 +651,11 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
                          local.excluded, local.errors, speed)
                 last_report, last_docs = now, local.docs
     finally:
+        source.close()
         writer.close()
     hb.finish(local.vector(nsteps))
-    phase = {"read": ureader.seconds, "write": writer.seconds, "main_loop": time.perf_counter() - t_loop}
+    phase = {"setup": setup_s, "read": ureader.seconds, "write": writer.seconds,
+             "main_loop": time.perf_counter() - t_loop}
     log.info("rank %d phases: %s", rank, {k: round(v, 3) for k, v in phase.items()})
     elapsed = time.perf_counter() - t_start
     total_vec = ctx.all_reduce_sum(local.vector(nsteps))
@@ -597,6 +673,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
             shutil.rmtree(work_dir, ignore_errors=True)
         ctx.barrier()
     stats.seconds = ctx.all_reduce_max(time.perf_counter() - t_start)
+    tracing.dump_timeline(f".rank{rank}" if world > 1 else "")
     if rank == 0:
         metrics.set_global_counts(stats.docs, stats.kept, stats.excluded, stats.errors)
     return stats

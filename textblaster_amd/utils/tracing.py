@@ -5,16 +5,54 @@ Enabled with ``TB_ROCTX=1``: ranges are pushed through librocprofiler-sdk-roctx,
 ``rocprofv3 --marker-trace --kernel-trace`` run shows, per thread, the host phases of every
 batch (stage_h2d, launch, gpu_wait, resolve, assemble, parquet read/write) next to the kernels
 they enqueue. Disabled (the default) the helpers cost one attribute check.
+
+``TB_TIMELINE=<path>`` (or ``record_timeline(path)``) additionally records every range in
+process as ``(thread, name, start, end)`` and ``dump_timeline()`` writes them as JSON: a
+profiler-free host timeline of the reader / submit / wait / assemble / writer overlap
+(tools/timeline_summary.py turns it into per-thread busy time and the critical path).
 """
 from __future__ import annotations
 
 import contextlib
 import ctypes
+import json
 import os
-from typing import Iterator, Optional
+import threading
+import time
+from typing import Iterator, List, Optional, Tuple
 
 _lib: Optional[ctypes.CDLL] = None
 _enabled = os.environ.get("TB_ROCTX", "") not in ("", "0")
+_tl_path: Optional[str] = os.environ.get("TB_TIMELINE") or None
+_tl_events: List[Tuple[str, str, float, float]] = []
+_tl_lock = threading.Lock()
+_tl_t0 = time.perf_counter()
+
+
+def record_timeline(path: Optional[str]) -> None:
+    """Start (path) or stop (None) recording host ranges; clears earlier events."""
+    global _tl_path, _tl_t0
+    with _tl_lock:
+        _tl_path = path
+        _tl_events.clear()
+        _tl_t0 = time.perf_counter()
+
+
+def timeline_events() -> List[Tuple[str, str, float, float]]:
+    with _tl_lock:
+        return list(_tl_events)
+
+
+def dump_timeline(suffix: str = "") -> Optional[str]:
+    """Writes the recorded ranges to the timeline path (+suffix); returns the file name."""
+    if not _tl_path:
+        return None
+    path = _tl_path + suffix
+    ev = timeline_events()
+    with open(path, "w", encoding="utf-8") as f:
+        json.dump({"t0": 0.0, "events": [{"thread": t, "name": n, "start": round(a - _tl_t0, 6),
+                                          "end": round(b - _tl_t0, 6)} for t, n, a, b in ev]}, f)
+    return path
 
 
 def _load() -> Optional[ctypes.CDLL]:
@@ -52,14 +90,18 @@ def enable(on: bool = True) -> None:
 def trace_range(name: str) -> Iterator[None]:
     """``with trace_range("resolve"): ...`` -> one roctx range (no-op unless TB_ROCTX=1)."""
     lib = _load() if _enabled else None
-    if lib is None:
-        yield
-        return
-    lib.roctxRangePushA(name.encode())
+    t0 = time.perf_counter() if _tl_path else 0.0
+    if lib is not None:
+        lib.roctxRangePushA(name.encode())
     try:
         yield
     finally:
-        lib.roctxRangePop()
+        if lib is not None:
+            lib.roctxRangePop()
+        if _tl_path and t0:
+            t1 = time.perf_counter()
+            with _tl_lock:
+                _tl_events.append((threading.current_thread().name, name, t0, t1))
 
 
 def mark(name: str) -> None:

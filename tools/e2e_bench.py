@@ -25,6 +25,8 @@ def make_input(path: str, ndocs: int, mean_bytes: int, pool: int, row_group: int
     from textblaster_amd.utils import synth
 
     texts = synth.make_corpus(pool, mean_bytes, seed=5)
+    text_arr = pa.array(texts, pa.string())
+    lens = np.array([len(t.encode()) for t in texts], dtype=np.int64)
     rng = np.random.default_rng(5)
     w = None
     total = 0
@@ -33,11 +35,11 @@ def make_input(path: str, ndocs: int, mean_bytes: int, pool: int, row_group: int
         idx = rng.integers(0, len(texts), size=n)
         tbl = pa.table({
             "id": pa.array([f"doc-{start + i}" for i in range(n)]),
-            "text": pa.array([texts[i] for i in idx]),
+            "text": text_arr.take(pa.array(idx)),
             "source": pa.array(["s3://commoncrawl/synthetic"] * n),
             "metadata": pa.array(['{"url":"https://example.com/%d"}' % (start + i) for i in range(n)]),
         })
-        total += sum(len(texts[i].encode()) for i in idx[:1000]) * n // min(n, 1000)
+        total += int(lens[idx].sum())
         if w is None:
             w = pq.ParquetWriter(path, tbl.schema, compression="snappy")
         w.write_table(tbl)
@@ -55,27 +57,45 @@ def main():
     ap.add_argument("--backend", action="append", default=None)
     ap.add_argument("--config", default=os.path.join(ROOT, "config", "bench_pipeline.yaml"))
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "e2e"))
+    ap.add_argument("--timeline", action="store_true", help="record the host timeline (TB_TIMELINE) per backend")
+    ap.add_argument("--html-decode", default="cpu")
+    ap.add_argument("--keep-input", action="store_true")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     inp = os.path.join(args.out, "input.parquet")
     t = time.perf_counter()
-    make_input(inp, args.docs, args.mean_bytes, args.pool, args.row_group)
+    if not (args.keep_input and os.path.exists(inp)):
+        make_input(inp, args.docs, args.mean_bytes, args.pool, args.row_group)
     print(f"input: {args.docs} docs, {os.path.getsize(inp) / 1e6:.1f} MB in {time.perf_counter() - t:.1f}s",
           flush=True)
     from textblaster_amd.runner import RunConfig, run
+    from textblaster_amd.utils import tracing
 
     for backend in args.backend or ["cuda"]:
         o = os.path.join(args.out, f"{backend}.out.parquet")
         e = os.path.join(args.out, f"{backend}.excluded.parquet")
-        st = run(RunConfig(inp, o, e, args.config, backend=backend, unit_rows=args.unit_rows))
+        tl = os.path.join(args.out, f"timeline_{backend}.json") if args.timeline else None
+        tracing.record_timeline(tl)
+        st = run(RunConfig(inp, o, e, args.config, backend=backend, unit_rows=args.unit_rows,
+                           html_decode=args.html_decode))
         line = {"backend": backend, "docs": st.docs, "kept": st.kept, "excluded": st.excluded, "errors": st.errors,
                 "seconds": round(st.seconds, 3), "docs_per_sec": round(st.docs_per_sec, 1),
                 "step_filtered": st.step_filtered, "delegated": st.delegated,
                 "phase_seconds": {k: round(v, 3) for k, v in st.phase_seconds.items()}}
         print(json.dumps(line), flush=True)
+        if tl:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            from timeline_summary import summarise
+
+            with open(tl, encoding="utf-8") as f:
+                summary = summarise(json.load(f))
+            with open(tl.replace(".json", ".txt"), "w", encoding="utf-8") as f:
+                f.write(json.dumps(line) + "\n\n" + summary + "\n")
+            print(summary, flush=True)
         for p in (o, e):
             os.remove(p)
-    os.remove(inp)
+    if not args.keep_input:
+        os.remove(inp)
 
 
 if __name__ == "__main__":

@@ -78,9 +78,10 @@ def parse_device(device) -> int:
         return current_device()
     if isinstance(device, int):
         return device
-    idx = getattr(device, "index", None)
-    if idx is not None:
-        return int(idx)
+    if not isinstance(device, str):
+        idx = getattr(device, "index", None)   # e.g. torch.device
+        if isinstance(idx, int):
+            return idx
     s = str(device)
     if s in ("cuda", "hip", "gpu"):
         return current_device()

@@ -145,18 +145,21 @@ class DeviceRunner:
         self.plan = plan
         self.steps = steps_native
         h = native.host()
-        # Streams. The box exposes GPU_MAX_HW_QUEUES=4 hardware queues per process and HIP maps
-        # streams onto them round-robin, so the default layout ("4") creates exactly four: per
-        # slot one compute stream (wave kernels, C4, language-id head, gates, D2H) and one side
-        # stream (long-document workgroup kernels first, then the language-id bag, and the H2D
-        # of the next batch), at high priority so the long-document tail is dispatched early.
-        # TB_STREAMS=13 restores the previous layout (5 per slot + copies) for A/B runs;
+        # Streams. The box exposes GPU_MAX_HW_QUEUES=4 hardware queues per process. The default
+        # layout ("6") has exactly four streams that carry kernels — per slot one compute stream
+        # (wave kernels, C4, language-id head, gates) and one side stream (long-document
+        # workgroup kernels first, then the language-id bag; high priority so the long-document
+        # tail is dispatched early) — plus one upload and one download stream shared by the
+        # slots, which carry only DMA copies. Measured on the 1-GPU bench (profiles/r2_streams/):
+        # 6 -> 44.5 ms/step, 13 (5 per slot + copies, the round-1 layout) -> 45-47.5,
+        # 4 (copies folded into the slot streams) -> 50, 5 (one shared copy stream) -> 55: an
+        # upload must never queue behind a download. TB_STREAMS selects a layout for A/B runs;
         # TB_SERIAL_STREAMS=1 puts everything on one stream (exclusive kernel timings).
         blk_prio = int(os.environ.get("TB_BLK_PRIORITY", "-1"))
         serial = os.environ.get("TB_SERIAL_STREAMS", "") not in ("", "0")
-        self.stream_layout = "serial" if serial else os.environ.get("TB_STREAMS", "4")
-        if self.stream_layout not in ("serial", "4", "13"):
-            raise DeviceError("TB_STREAMS must be 4 or 13")
+        self.stream_layout = "serial" if serial else os.environ.get("TB_STREAMS", "6")
+        if self.stream_layout not in ("serial", "4", "4c", "4f", "5", "6", "13"):
+            raise DeviceError("TB_STREAMS must be one of 4, 4c, 4f, 5, 6, 13")
         self.slots = [_Slot() for _ in range(self.N_SLOTS)]
         if self.stream_layout == "serial":
             one = hiprt.Stream()
@@ -166,6 +169,30 @@ class DeviceRunner:
             for sl in self.slots:
                 sl.main = sl.s_c4 = sl.s_d2h = hiprt.Stream()
                 sl.s_blk = sl.s_lid = sl.s_c4blk = sl.s_h2d = hiprt.Stream(priority=blk_prio)
+        elif self.stream_layout == "4c":
+            side, copy = hiprt.Stream(priority=blk_prio), hiprt.Stream()
+            for sl in self.slots:
+                sl.main = sl.s_c4 = hiprt.Stream()
+                sl.s_blk = sl.s_lid = sl.s_c4blk = side
+                sl.s_h2d = sl.s_d2h = copy
+        elif self.stream_layout == "4f":
+            # per slot: compute + side; the side stream also carries the slot's copies in both
+            # directions (D2H after the batch's completion event)
+            for sl in self.slots:
+                sl.main = sl.s_c4 = hiprt.Stream()
+                sl.s_blk = sl.s_lid = sl.s_c4blk = sl.s_h2d = sl.s_d2h = hiprt.Stream(priority=blk_prio)
+        elif self.stream_layout == "5":
+            copy = hiprt.Stream()
+            for sl in self.slots:
+                sl.main = sl.s_c4 = hiprt.Stream()
+                sl.s_blk = sl.s_lid = sl.s_c4blk = hiprt.Stream(priority=blk_prio)
+                sl.s_h2d = sl.s_d2h = copy
+        elif self.stream_layout == "6":
+            h2d, d2h = hiprt.Stream(), hiprt.Stream()
+            for sl in self.slots:
+                sl.main = sl.s_c4 = hiprt.Stream()
+                sl.s_blk = sl.s_lid = sl.s_c4blk = hiprt.Stream(priority=blk_prio)
+                sl.s_h2d, sl.s_d2h = h2d, d2h
         else:
             h2d, d2h = hiprt.Stream(), hiprt.Stream()
             for sl in self.slots:
@@ -448,7 +475,9 @@ class DeviceRunner:
                 if any(kind == 4 for kind, _, _ in layout):
                     lid_vec = rt.zeros(ndocs * h.LID_DIM, np.int16)
                     lid_cnt = rt.zeros(ndocs, np.int32)
+                    keep += [lid_vec, lid_cnt]   # freed (returned to the cache) only after the batch
                 ev_pre = self._record(main)  # rec / lid buffers zeroed
+                keep.append(ev_pre)
                 ev_lid = ev_blk = None
                 prof = self._prof_buf(ndocs, keep, f"stage{s}")
                 skip = dead if pass_idx > 0 else None
@@ -461,6 +490,7 @@ class DeviceRunner:
                                                  ndocs, scratch, d_soff, pw, pw_n, rec, flags, lid_vec, lid_cnt,
                                                  self.lds_bytes_blk, prof, skip)
                         ev_blk = self._record(slot.s_blk)
+                        keep.append(ev_blk)
                 if lid_vec is not None:
                     slot.s_lid.wait_event(ev_pre)
                     with rt.stream(slot.s_lid), self._ktimed(keep, "langid_features"):
@@ -468,6 +498,7 @@ class DeviceRunner:
                                                lid_cnt, flags, self.lds_bytes_lid,
                                                self._prof_buf(ndocs, keep, f"langid{s}"))
                         ev_lid = self._record(slot.s_lid)
+                        keep.append(ev_lid)
                 if n_mid > n_long:
                     # mid-size documents on the long-document stream, after its workgroup kernel
                     if ev_blk is None:
@@ -478,6 +509,7 @@ class DeviceRunner:
                                              self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
                                              self.lds_bytes_mid, prof, self.stage_waves, n_mid - n_long, skip)
                         ev_blk = self._record(slot.s_blk)
+                        keep.append(ev_blk)
                 if n_mid < ndocs:
                     with self._ktimed(keep, f"stage{s}"):
                         self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_mid:], ndocs,
@@ -507,18 +539,23 @@ class DeviceRunner:
                 new_off = rt.zeros(ndocs + 1, np.int64)
                 cap = vlen + self.c4_growth * ndocs + 16  # device rewrites never grow more (kC4MaxGrowth)
                 out = rt.empty(cap, np.uint8)
-                slot.s_c4.wait_event(self._record(main))
+                ev_main = self._record(main)
+                slot.s_c4.wait_event(ev_main)
                 slot.s_c4.wait_event(ready[ver])
+                keep.append(ev_main)
                 skip = dead if pass_idx > 0 else None
                 prof = self._prof_buf(ndocs, keep, f"c4_step{i}")
                 ev_c4blk = None
                 if n_long:
                     # long documents (workgroup kernel) next to the wave kernel: disjoint docs
-                    slot.s_c4blk.wait_event(self._record(slot.s_c4))
+                    ev_c4 = self._record(slot.s_c4)
+                    slot.s_c4blk.wait_event(ev_c4)
+                    keep.append(ev_c4)
                     with rt.stream(slot.s_c4blk):
                         self.k.c4_pass_a_blk(self.c4_ts[i], vb, vo, d_perm[:n_long], n_long, ndocs, c4_scratch,
                                              d_soff, pw, pw_n, rec, src, flags, self.lds_bytes_blk, prof, skip)
                         ev_c4blk = self._record(slot.s_c4blk)
+                        keep.append(ev_c4blk)
                 with rt.stream(slot.s_c4), self._ktimed(keep, f"c4_step{i}"):
                     if n_long < ndocs:
                         self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm[n_long:], ndocs, c4_scratch, d_soff[n_long:], pw,
@@ -559,7 +596,7 @@ class DeviceRunner:
         h_flags = d2h(flags)
         h_dead = d2h(dead) if dead is not None else None
         ev = self._record(d2h_s)
-        keep += [stage_recs_d, c4_recs_d, versions, flags, dead]
+        keep += [stage_recs_d, c4_recs_d, versions, flags, dead, ready, tails, done]
         t2 = time.perf_counter()
         return PendingBatch(self, ndocs, ev, h_stage, h_c4, h_versions, h_flags,
                             {"stage_h2d": t1 - t0, "launch": t2 - t1}, keep, h_dead)

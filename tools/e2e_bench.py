@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--timeline", action="store_true", help="record the host timeline (TB_TIMELINE) per backend")
     ap.add_argument("--html-decode", default="cpu")
     ap.add_argument("--keep-input", action="store_true")
+    ap.add_argument("--repeat", type=int, default=1, help="runs per backend (all reported; the median last)")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     inp = os.path.join(args.out, "input.parquet")
@@ -71,7 +72,9 @@ def main():
     from textblaster_amd.runner import RunConfig, run
     from textblaster_amd.utils import tracing
 
-    for backend in args.backend or ["cuda"]:
+    runs = [b for b in (args.backend or ["cuda"]) for _ in range(args.repeat)]
+    rates = {}
+    for backend in runs:
         o = os.path.join(args.out, f"{backend}.out.parquet")
         e = os.path.join(args.out, f"{backend}.excluded.parquet")
         tl = os.path.join(args.out, f"timeline_{backend}.json") if args.timeline else None
@@ -83,6 +86,7 @@ def main():
                 "step_filtered": st.step_filtered, "delegated": st.delegated,
                 "phase_seconds": {k: round(v, 3) for k, v in st.phase_seconds.items()}}
         print(json.dumps(line), flush=True)
+        rates.setdefault(backend, []).append(line["docs_per_sec"])
         if tl:
             sys.path.insert(0, os.path.join(ROOT, "tools"))
             from timeline_summary import summarise
@@ -94,6 +98,10 @@ def main():
             print(summary, flush=True)
         for p in (o, e):
             os.remove(p)
+    for backend, r in rates.items():
+        if len(r) > 1:
+            print(json.dumps({"backend": backend, "runs": len(r), "docs_per_sec_median": float(np.median(r)),
+                              "docs_per_sec_all": r}), flush=True)
     if not args.keep_input:
         os.remove(inp)
 

@@ -4,12 +4,13 @@
 set -e
 mkdir -p gpurun_out/e2e /tmp/tb_e2e
 DOCS=${TB_E2E_DOCS:-4000000}
-timeout -k 10 400 python -u tools/e2e_bench.py --docs $DOCS --backend cuda --out /tmp/tb_e2e --timeline \
-  --keep-input --html-decode cpu > gpurun_out/e2e/run_cpuhtml.log 2>&1
+timeout -k 10 500 python -u tools/e2e_bench.py --docs $DOCS --backend cuda --out /tmp/tb_e2e --timeline \
+  --keep-input --html-decode cpu --repeat ${TB_E2E_REPEAT:-3} > gpurun_out/e2e/run_cpuhtml.log 2>&1
 cp /tmp/tb_e2e/timeline_cuda.txt gpurun_out/e2e/timeline_cuda_cpuhtml.txt
 cp /tmp/tb_e2e/timeline_cuda.json gpurun_out/e2e/timeline_cuda_cpuhtml.json
+if [ -n "$TB_E2E_GPUHTML" ]; then
 timeout -k 10 300 python -u tools/e2e_bench.py --docs $DOCS --backend cuda --out /tmp/tb_e2e --timeline \
   --keep-input --html-decode gpu > gpurun_out/e2e/run_gpuhtml.log 2>&1
 cp /tmp/tb_e2e/timeline_cuda.txt gpurun_out/e2e/timeline_cuda_gpuhtml.txt
-cp /tmp/tb_e2e/timeline_cuda.json gpurun_out/e2e/timeline_cuda_gpuhtml.json
-head -3 gpurun_out/e2e/run_cpuhtml.log gpurun_out/e2e/run_gpuhtml.log
+fi
+grep -h '"backend"' gpurun_out/e2e/run_*.log | cut -c1-400

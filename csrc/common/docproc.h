@@ -794,28 +794,38 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     }
     x.stamp(PH_GR_TOP);
     if (ds.n_dup > 0) {
-      // One n at a time (its canonical-gram array, visited and repeated-position bitmaps and
-      // hash table are scratch for this n only, so they fit the LDS slice):
-      //   canonicalize the n-gram concatenations, mark repeated positions in R (p with
-      //   gc[p] != p, and their first occurrence gc[p]), then one lane runs the greedy walk.
-      // The walk only has to stop at repeated grams: at a gram that occurs once it would mark an
-      // id no other position has and advance by one, so it jumps from one set bit of R to the
-      // next instead (reference find_all_duplicate, utils/text.rs:241-259).
+      // Two phases over all requested orders n (reference find_all_duplicate,
+      // utils/text.rs:241-259):
+      //   1. per n: canonicalise the n-gram concatenations into gc_n (exact: hash groups, then
+      //      word-id / byte equality) and mark repeated positions in R_n (p with gc[p] != p, and
+      //      their first occurrence gc[p]);
+      //   2. the greedy walks of all orders run at once, one lane each (they are independent
+      //      and sequential, so n walks cost about the longest one instead of their sum).
+      // A walk only has to stop at repeated grams: at a gram that occurs once it would mark an id
+      // no other position has and advance by one, so it jumps from one set bit of R_n to the next.
+      // Arrays of all orders are packed back to back: gc_n at gbase(t), bitmaps at t * 2 * SW.
       const uint32_t SW = (W + 31) / 32 + 1;
-      for (int t = 0; t < ds.n_dup; ++t) {
+      const int nd = ds.n_dup;
+      auto gsize = [&](int t) -> uint32_t {
         const uint32_t n = (uint32_t)ds.dup_n[t];
-        int64_t* rt = &r[rec_gr_fixed() + ds.n_top + t];
-        if (n == 0 || W < n) {
-          x.par.single([&]() { *rt = 0; });
-          continue;
-        }
-        const uint32_t G = W - n + 1;
-        const auto m3 = x.mark();
-        uint32_t* sn = x.template alloc_hot<uint32_t>(2 * (uint64_t)SW);
-        uint32_t* R = sn + SW;
-        uint32_t* gc = x.template alloc_hot<uint32_t>(G);
-        if (x.overflow) return;
-        x.par.for_n(2 * SW, [&](uint32_t i) { sn[i] = 0; });
+        return (n == 0 || W < n) ? 0u : W - n + 1;
+      };
+      uint32_t gtot = 0;
+      for (int t = 0; t < nd; ++t) gtot += gsize(t);
+      const auto m3 = x.mark();
+      uint32_t* bits = x.template alloc_hot<uint32_t>(2 * (uint64_t)SW * (uint64_t)nd);  // [sn | R] per order
+      uint32_t* gcall = x.template alloc_hot<uint32_t>((uint64_t)gtot + 1);
+      if (x.overflow) return;
+      x.par.for_n(2 * SW * (uint32_t)nd, [&](uint32_t i) { bits[i] = 0; });
+      x.par.sync();
+      uint32_t gb = 0;
+      for (int t = 0; t < nd; ++t) {
+        const uint32_t n = (uint32_t)ds.dup_n[t];
+        const uint32_t G = gsize(t);
+        if (G == 0) continue;
+        uint32_t* gc = gcall + gb;
+        uint32_t* R = bits + (uint32_t)t * 2 * SW + SW;
+        gb += G;
         canonicalize(
             x, G, [&](uint32_t p) { return dev_key(run_hash(p, n), WL[p + n] - WL[p]); },
             [&](uint32_t p, uint32_t q) {
@@ -846,20 +856,29 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
           }
         });
         x.par.sync();
-        x.par.single([&]() {
+      }
+      x.par.for_n((uint32_t)nd, [&](uint32_t t) {
+        const uint32_t n = (uint32_t)ds.dup_n[t];
+        const uint32_t G = gsize((int)t);
+        int64_t rep = 0;
+        if (G > 0) {
+          uint32_t base = 0;
+          for (uint32_t u = 0; u < t; ++u) base += gsize((int)u);
+          const uint32_t* gc = gcall + base;
+          uint32_t* sn = bits + t * 2 * SW;
+          const uint32_t* R = sn + SW;
           const uint32_t nw = (G + 31) >> 5;
           auto next_rep = [&](uint32_t from) -> uint32_t {  // first repeated position >= from, or G
             if (from >= G) return G;
             uint32_t wi = from >> 5;
-            uint32_t bits = R[wi] & (~0u << (from & 31));
-            while (!bits) {
+            uint32_t bw = R[wi] & (~0u << (from & 31));
+            while (!bw) {
               if (++wi >= nw) return G;
-              bits = R[wi];
+              bw = R[wi];
             }
-            const uint32_t q = (wi << 5) + (uint32_t)__builtin_ctz(bits);
+            const uint32_t q = (wi << 5) + (uint32_t)__builtin_ctz(bw);
             return q < G ? q : G;
           };
-          int64_t rep = 0;
           uint32_t idx = next_rep(0);
           while (idx < G) {
             const uint32_t g = gc[idx];
@@ -871,12 +890,12 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
               idx = next_rep(idx + 1);
             }
           }
-          *rt = rep;
-        });
-        x.par.sync();
-        x.stamp(PH_GR_DUP_WALK);
-        x.reset(m3);
-      }
+        }
+        r[rec_gr_fixed() + ds.n_top + t] = rep;
+      });
+      x.par.sync();
+      x.stamp(PH_GR_DUP_WALK);
+      x.reset(m3);
       x.stamp(PH_GR_DUP);
     }
   }

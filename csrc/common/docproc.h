@@ -191,6 +191,20 @@ struct DocCtx {
     return alloc_global<T>(count);
   }
   TB_HD void release_hi() { lhi = 0; }
+  // bytes of the LDS slice still free between the bottom and top allocations
+  TB_HD uint32_t lds_free() const {
+    if (!lds) return 0;
+    const uint32_t lo = (lused + 15u) & ~15u;
+    return lo + lhi >= lcap ? 0u : lcap - lo - lhi;
+  }
+  // alloc_hot, but only while `keep` bytes of the slice stay free afterwards (for the hash
+  // tables of a later phase, whose random accesses gain far more from the LDS than the
+  // sequential scans of this array do); otherwise HBM
+  template <class T>
+  TB_HD T* alloc_hot_keep(uint64_t count, uint64_t keep) {
+    if (lds && (uint64_t)lds_free() >= count * sizeof(T) + 16 + keep) return alloc_hot<T>(count);
+    return alloc_global<T>(count);
+  }
   template <class T>
   TB_HD T* alloc_global(uint64_t count) {
     uint64_t a = (used + 15) & ~15ull;
@@ -411,6 +425,66 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
   const uint32_t capn = n + (n >> 1) + 2;
   const auto mark = x.mark();
   if (n < 65535u) {
+    // The table's random probes want the LDS. When the whole table does not fit the free part
+    // of the slice (long documents), the slot range is cut into parts that do: part q holds
+    // the elements whose home slot falls in [q*capp, (q+1)*capp), and the parts are built one
+    // after another in the same LDS table, from keys computed once into HBM. Equal elements
+    // share a home slot, hence a part, so the grouping stays exact.
+    const uint32_t fit = x.lds_free() >= 64u ? (x.lds_free() - 32u) / 4u : 0u;
+    uint32_t parts = 1;
+    if (P::kPartTables && x.lds && capn > fit && fit >= 2048u) parts = (capn + fit - 1) / fit;
+    if (P::kPartTables && parts > 1) {
+      const uint32_t capp = (capn + parts - 1) / parts;
+      uint32_t* tab = x.template alloc_hot_hi<uint32_t>(capp);
+      uint64_t* keys = x.template alloc<uint64_t>(n);
+      if (x.overflow) return;
+      x.par.for_n(n, [&](uint32_t i) { keys[i] = x.weak_keys ? (key(i) & 3ull) : key(i); });
+      x.par.sync();
+      bool full = false;
+      for (uint32_t q = 0; q < parts; ++q) {
+        x.par.for_n(capp, [&](uint32_t i) { tab[i] = 0; });
+        x.par.sync();
+        x.par.for_n(n, [&](uint32_t i) {
+          const uint64_t k = keys[i];
+          const uint32_t home = (uint32_t)(((k & 0xFFFFFFFFull) * capn) >> 32);
+          if (home / capp != q) return;
+          const uint32_t fp = (uint32_t)(k >> 48);
+          const uint32_t mine = (fp << 16) | (i + 1);
+          uint32_t slot = home - q * capp;
+          for (uint32_t probes = 0;; ++probes) {
+            if (probes >= capp) {  // a part ran full (never for hashed keys): exact CPU path
+              full = true;
+              slot = 0;
+              break;
+            }
+            uint32_t cur = tab[slot];
+            if (cur == 0) {
+              cur = P::cas32(&tab[slot], 0u, mine);
+              if (cur == 0) break;
+            }
+            if ((cur >> 16) == fp && eq(i, (cur & 0xFFFFu) - 1u)) {
+              P::min32(&tab[slot], mine);
+              break;
+            }
+            if (++slot == capp) slot = 0;
+          }
+          canon[i] = slot;
+        });
+        x.par.sync();
+        x.par.for_n(n, [&](uint32_t i) {
+          const uint32_t home = (uint32_t)(((keys[i] & 0xFFFFFFFFull) * capn) >> 32);
+          if (home / capp == q) canon[i] = (tab[canon[i]] & 0xFFFFu) - 1u;
+        });
+        x.par.sync();
+      }
+      if (x.par.reduce_or(full ? 1u : 0u)) {  // uniform: every lane takes the branch together
+        x.set_flag(DOC_NEEDS_CPU);
+        x.par.for_n(n, [&](uint32_t i) { canon[i] = i; });
+        x.par.sync();
+      }
+      x.reset(mark);
+      return;
+    }
     uint32_t* tab = x.template alloc_hot_hi<uint32_t>(capn);
     if (x.overflow) return;
     x.par.for_n(capn, [&](uint32_t i) { tab[i] = 0; });
@@ -708,10 +782,12 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
   uint64_t* K = nullptr;
   uint64_t* PB = nullptr;
   if (ngrams) {
-    wid = x.template alloc_hot<uint32_t>(W + 1);
-    WL = x.template alloc_hot<uint32_t>(W + 1);
-    K = x.template alloc_hot<uint64_t>(W + 1);
-    PB = x.template alloc_hot<uint64_t>(W + 1);
+    // LDS only while a canonicalisation table for W elements (~6 W bytes) still fits next to them
+    const uint64_t tab_bytes = 6ull * W + 64;
+    wid = x.template alloc_hot_keep<uint32_t>(W + 1, tab_bytes);
+    WL = x.template alloc_hot_keep<uint32_t>(W + 1, tab_bytes);
+    K = x.template alloc_hot_keep<uint64_t>(W + 1, tab_bytes);
+    PB = x.template alloc_hot_keep<uint64_t>(W + 1, tab_bytes);
     const auto mw = x.mark();
     uint64_t* wh = x.template alloc_hot_hi<uint64_t>(W + 1);
     if (x.overflow) return;
@@ -752,8 +828,8 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       for (int t = 0; t < ds.n_top; ++t) max_top = ds.top_n[t] > max_top ? ds.top_n[t] : max_top;
       const auto m2 = x.mark();
       // two id arrays in turn; the counts of order n go to the one the (n-1)-gram ids used
-      uint32_t* ga = x.template alloc_hot<uint32_t>(W + 1);
-      uint32_t* gb = x.template alloc_hot<uint32_t>(W + 1);
+      uint32_t* ga = x.template alloc_hot_keep<uint32_t>(W + 1, 6ull * W + 64);
+      uint32_t* gb = x.template alloc_hot_keep<uint32_t>(W + 1, 6ull * W + 64);
       if (x.overflow) return;
       x.par.single([&]() { for (int t = 0; t < ds.n_top; ++t) r[rec_gr_fixed() + t] = 0; });
       const uint32_t* gprev = wid;
@@ -814,7 +890,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       for (int t = 0; t < nd; ++t) gtot += gsize(t);
       const auto m3 = x.mark();
       uint32_t* bits = x.template alloc_hot<uint32_t>(2 * (uint64_t)SW * (uint64_t)nd);  // [sn | R] per order
-      uint32_t* gcall = x.template alloc_hot<uint32_t>((uint64_t)gtot + 1);
+      uint32_t* gcall = x.template alloc_hot_keep<uint32_t>((uint64_t)gtot + 1, 6ull * W + 64);
       if (x.overflow) return;
       x.par.for_n(2 * SW * (uint32_t)nd, [&](uint32_t i) { bits[i] = 0; });
       x.par.sync();

@@ -36,6 +36,7 @@ namespace tb {
 TB_HD constexpr uint32_t mask_words(uint32_t n) { return ((n + 63) / 64) * 2; }
 
 struct SeqPar {
+  static constexpr bool kPartTables = false;  // canonicalize(): LDS-partitioned tables (no LDS here)
   template <class F>
   void for_n(uint32_t n, F&& f) const {
     for (uint32_t i = 0; i < n; ++i) f(i);
@@ -218,6 +219,7 @@ __device__ __forceinline__ T wave_incl_scan(T x, uint32_t lane, Op&& op) {
 }  // namespace pardetail
 
 struct WavePar {
+  static constexpr bool kPartTables = false;  // short documents: tables fit the slice (registers matter more)
   uint32_t lane;
   __device__ WavePar() : lane(threadIdx.x & 63) {}
 
@@ -474,6 +476,11 @@ template <int NT>
 struct BlockPar {
   static_assert(NT % 64 == 0 && NT >= 128 && NT <= 1024, "block of whole waves");
   static constexpr int NW = NT / 64;
+#ifdef TB_NO_PART_TABLES
+  static constexpr bool kPartTables = false;
+#else
+  static constexpr bool kPartTables = true;   // long documents: LDS-partitioned hash tables
+#endif
   uint32_t tid, lane, wid;
   char* xs = nullptr;
   __device__ BlockPar() : tid(threadIdx.x), lane(threadIdx.x & 63), wid(threadIdx.x >> 6) {}

@@ -123,9 +123,15 @@ TB_STAGE_KERNEL(k_stage_analyze_w6, __attribute__((amdgpu_waves_per_eu(6, 8))))
 #define TB_BLOCK_THREADS 512
 #endif
 constexpr int kBlockThreads = TB_BLOCK_THREADS;
+// TB_BLK_WPE=k: force a k-waves-per-SIMD register budget on the long-document kernels (A/B builds)
+#ifdef TB_BLK_WPE
+#define TB_BLK_ATTR __attribute__((amdgpu_waves_per_eu(TB_BLK_WPE, 8)))
+#else
+#define TB_BLK_ATTR
+#endif
 __shared__ __attribute__((aligned(16))) char g_block_xs[16 * (kBlockThreads / 64) + 64];
 
-__global__ __launch_bounds__(kBlockThreads) void k_stage_analyze_blk(
+__global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_stage_analyze_blk(
     const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes,
     const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,
     const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,

@@ -139,4 +139,47 @@ TB_HD bool gate_fails(const DevGateStep& g, const int64_t* r) {
   }
 }
 
+// ---- K16 resolve: the executor's first-failure chain over the whole pipeline ----------------
+// (reference executor.rs:32-46 + producer_logic.rs:148-167). Valid only when every pipeline step
+// runs on the device and has a gate kind (build_resolve refuses otherwise): then the per-document
+// outcome — first failing step, kept / filtered, final content version — is a pure function of
+// the device records and needs no host decision. The host still re-derives every decision from
+// the same records (decide_t) and compares; a disagreement falls back to host assembly.
+
+// status codes (as BatchState::status_): 0 kept, 1 filtered, 3 delegated to the CPU path
+constexpr uint8_t kResolveKept = 0, kResolveFiltered = 1, kResolveDelegated = 3;
+constexpr int32_t kResolveDelegatedStep = 1 << 30;
+constexpr int kMaxVersions = 8;  // content versions the resolve kernel can read (C4 rewrites + 1)
+
+struct DevResolve {
+  DevGate gate;                          // every pipeline step in pipeline order
+  int32_t step_index[kMaxGateSteps];     // pipeline index of gate.steps[k]
+  int32_t c4_version[kMaxGateSteps];     // C4 rewrite step: content version it produces, else -1
+};
+
+// One document: fail = first failing pipeline step (-1 none, kResolveDelegatedStep when flagged),
+// status, ver = content version the outputs carry (C4 rewrites apply to every document that reaches
+// the step unless its lorem-ipsum / curly-bracket branch fired: BatchState::apply_records).
+TB_HD void resolve_doc(const DevResolve& rp, const int64_t* const* recs, int64_t ndocs, int64_t doc, uint32_t flags,
+                       int32_t& fail, uint8_t& status, int32_t& ver) {
+  fail = -1;
+  status = kResolveKept;
+  ver = 0;
+  if (flags) {
+    fail = kResolveDelegatedStep;
+    status = kResolveDelegated;
+    return;
+  }
+  for (int s = 0; s < rp.gate.n_steps; ++s) {
+    const DevGateStep& g = rp.gate.steps[s];
+    const int64_t* r = recs[g.slot] + (int64_t)g.prefix * ndocs + doc * g.width;
+    if (rp.c4_version[s] >= 0 && !r[0] && !r[1]) ver = rp.c4_version[s];
+    if (gate_fails(g, r)) {
+      fail = rp.step_index[s];
+      status = kResolveFiltered;
+      return;
+    }
+  }
+}
+
 }  // namespace tb

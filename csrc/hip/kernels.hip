@@ -459,6 +459,74 @@ __global__ __launch_bounds__(256) void k_gate(const DevGate* __restrict__ gate, 
   if (fail) dead[doc] = code;
 }
 
+// K16 resolve (csrc/common/gate.h resolve_doc): one thread per document. Writes the first failing
+// step, the status, and the compaction inputs of the outputs: per document 4 int64 lanes
+// {kept bytes, excluded bytes, kept count, excluded count} of its final content version, which four
+// strided scans turn into output positions and byte offsets for k_compact.
+struct VersionTab {
+  const uint8_t* b[kMaxVersions];
+  const int64_t* off[kMaxVersions];
+};
+
+__global__ __launch_bounds__(256) void k_resolve(const DevResolve* __restrict__ rp, GateRecs recs, int32_t ndocs,
+                                                 const uint32_t* __restrict__ flags, VersionTab vt,
+                                                 int32_t* __restrict__ fail, uint8_t* __restrict__ status,
+                                                 uint8_t* __restrict__ fver, int64_t* __restrict__ lanes) {
+  const int doc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (doc >= ndocs) return;
+  int32_t f, v;
+  uint8_t st;
+  resolve_doc(*rp, recs.p, ndocs, doc, flags[doc], f, st, v);
+  fail[doc] = f;
+  status[doc] = st;
+  fver[doc] = (uint8_t)v;
+  const int64_t len = vt.off[v][doc + 1] - vt.off[v][doc];
+  int64_t* l = lanes + 4 * (int64_t)doc;
+  l[0] = st == kResolveKept ? len : 0;
+  l[1] = st == kResolveFiltered ? len : 0;
+  l[2] = st == kResolveKept ? 1 : 0;
+  l[3] = st == kResolveFiltered ? 1 : 0;
+}
+
+// K16 compaction: one wave per document copies its final content into the output buffer — kept
+// documents first, then excluded ones, each group in document order (the order the host path
+// produces) — and writes its output row and start offset. sc = the four inclusive scans
+// [kept bytes | excluded bytes | kept count | excluded count], n entries each.
+__global__ __launch_bounds__(64) void k_compact(const uint8_t* __restrict__ status, const uint8_t* __restrict__ fver,
+                                                VersionTab vt, int32_t ndocs, const int64_t* __restrict__ sc,
+                                                uint8_t* __restrict__ out, int64_t cap, int64_t* __restrict__ out_off,
+                                                int32_t* __restrict__ rows, int32_t* __restrict__ err) {
+  const int doc = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (doc >= ndocs) return;
+  const int64_t n = ndocs;
+  const int64_t nk = sc[3 * n - 1], nx = sc[4 * n - 1], kb = sc[n - 1], xb = sc[2 * n - 1];
+  if (doc == 0 && lane == 0) out_off[nk + nx] = kb + xb;
+  const uint8_t st = status[doc];
+  if (st != kResolveKept && st != kResolveFiltered) return;
+  const int v = fver[doc];
+  const int64_t s0 = vt.off[v][doc], len = vt.off[v][doc + 1] - s0;
+  int64_t pos, boff;
+  if (st == kResolveKept) {
+    pos = sc[2 * n + doc] - 1;
+    boff = sc[doc] - len;
+  } else {
+    pos = nk + sc[3 * n + doc] - 1;
+    boff = kb + sc[n + doc] - len;
+  }
+  if (boff < 0 || len < 0 || boff + len > cap) {  // never with the C4 growth bound; checked anyway
+    if (lane == 0) *err = 1;
+    return;
+  }
+  if (lane == 0) {
+    out_off[pos] = boff;
+    rows[pos] = doc;
+  }
+  const uint8_t* from = vt.b[v] + s0;
+  uint8_t* to = out + boff;
+  for (int64_t i = lane; i < len; i += 64) to[i] = from[i];
+}
+
 __global__ void k_pow_table(uint64_t* pw, uint32_t n) {
   // pw[i] = B^i and pw[n + 1 + i] = B^-i, computed independently per element (exact modular
   // arithmetic); the buffer holds 2n + 2 entries
@@ -472,6 +540,8 @@ __global__ void k_pow_table(uint64_t* pw, uint32_t n) {
 }  // namespace
 
 extern "C" {
+
+int tb_scan_strided_i64(hipStream_t stream, const int64_t* src, int64_t stride, int64_t n, int64_t* out);  // runtime.hip
 
 int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, const uint8_t* bytes,
                      const int64_t* off, const int32_t* perm, int32_t ndocs, char* scratch,
@@ -603,6 +673,37 @@ int tb_gate(hipStream_t stream, const void* gate, const int64_t* const* recs, in
 }
 
 size_t tb_sizeof_gate() { return sizeof(DevGate); }
+
+// K16: resolve + four scans + compaction, all on `stream`. vb/vo: content versions 0..nver-1;
+// lanes: 4*ndocs int64 scratch, sc: 4*ndocs int64 scan output; out must hold the final contents
+// (cap bytes: the caller bounds it by version 0 plus the C4 growth; a document that would pass
+// the end sets *err and is not written), out_off ndocs+1, rows ndocs.
+int tb_resolve(hipStream_t stream, const void* rp, const int64_t* const* recs, int32_t nrecs, int32_t ndocs,
+               const uint32_t* flags, const uint8_t* const* vb, const int64_t* const* vo, int32_t nver,
+               int32_t* fail, uint8_t* status, uint8_t* fver, int64_t* lanes, int64_t* sc, uint8_t* out,
+               int64_t cap, int64_t* out_off, int32_t* rows, int32_t* err) {
+  if (ndocs <= 0) return 0;
+  if (nrecs < 0 || nrecs > kMaxGateSteps || nver < 1 || nver > kMaxVersions) return (int)hipErrorInvalidValue;
+  GateRecs r{};
+  for (int i = 0; i < nrecs; ++i) r.p[i] = recs[i];
+  VersionTab vt{};
+  for (int i = 0; i < nver; ++i) {
+    vt.b[i] = vb[i];
+    vt.off[i] = vo[i];
+  }
+  hipLaunchKernelGGL(k_resolve, dim3((ndocs + 255) / 256), dim3(256), 0, stream, (const DevResolve*)rp, r, ndocs,
+                     flags, vt, fail, status, fver, lanes);
+  for (int j = 0; j < 4; ++j) {
+    const int rc = tb_scan_strided_i64(stream, lanes + j, 4, ndocs, sc + (int64_t)j * ndocs);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(k_compact, dim3(ndocs), dim3(64), 0, stream, status, fver, vt, ndocs, sc, out, cap, out_off, rows,
+                     err);
+  return (int)hipGetLastError();
+}
+
+size_t tb_sizeof_resolve() { return sizeof(DevResolve); }
+
 
 int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
   hipLaunchKernelGGL(k_pow_table, dim3((n + 256) / 256), dim3(256), 0, stream, pw, n);

@@ -13,7 +13,7 @@
 // retried once.
 //
 // Also here: k_scan_strided_i64, the inclusive prefix sum used for content-version offsets
-// (C4 pass B, HTML decode) — one workgroup, each thread scanning a contiguous chunk.
+// (C4 pass B, HTML decode, K16 output compaction) — tile partials, then per-tile scans.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -100,32 +100,104 @@ Cache* dev_cache() {
   return &g_dev[d];
 }
 
-// inclusive prefix sum of src[i * stride], i < n -> out[i]; one workgroup of 1024 threads,
-// thread t owns the contiguous chunk [t*chunk, (t+1)*chunk)
-constexpr int kScanThreads = 1024;
+// Inclusive prefix sum of src[i * stride], i < n -> out[i], over the whole chip: k_scan_partials
+// reduces each 2048-element tile (256 threads x 8 consecutive elements) to one partial, then
+// k_scan_tiles gives every tile the sum of the partials before it (at most a few hundred, read by
+// the whole workgroup) and scans the tile: thread-serial over its 8 elements, DPP-free wave scan of
+// the thread totals with shuffles, and a 4-entry cross-wave pass in LDS. A 262,144-element scan is
+// 128 workgroups per kernel instead of one 1024-thread workgroup walking everything.
+constexpr int kScanThreads = 256;
 
-__global__ __launch_bounds__(kScanThreads) void k_scan_strided_i64(const int64_t* __restrict__ src, int64_t stride,
-                                                                    int64_t n, int64_t* __restrict__ out) {
-  __shared__ int64_t sums[kScanThreads];
-  const int t = threadIdx.x;
-  const int64_t chunk = (n + kScanThreads - 1) / kScanThreads;
-  const int64_t b = t * chunk;
-  const int64_t e = b + chunk < n ? b + chunk : n;
-  int64_t s = 0;
-  for (int64_t i = b; i < e; ++i) s += src[i * stride];
-  sums[t] = s;
-  __syncthreads();
-  // Hillis-Steele over the 1024 chunk sums
-  for (int d = 1; d < kScanThreads; d <<= 1) {
-    const int64_t v = t >= d ? sums[t - d] : 0;
-    __syncthreads();
-    sums[t] += v;
-    __syncthreads();
+std::mutex g_scan_mu;
+std::map<std::pair<int, hipStream_t>, std::pair<int64_t*, int64_t>> g_scan_bufs;
+
+int64_t* scan_partials_for(hipStream_t stream, int64_t n) {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(g_scan_mu);
+  auto& e = g_scan_bufs[{d, stream}];
+  if (e.second < n) {
+    if (e.first) (void)hipFree(e.first);
+    e.first = nullptr;
+    e.second = 0;
+    const int64_t cap = n < 1024 ? 1024 : 2 * n;
+    if (hipMalloc((void**)&e.first, (size_t)cap * sizeof(int64_t)) != hipSuccess) return nullptr;
+    e.second = cap;
   }
-  int64_t run = t ? sums[t - 1] : 0;
-  for (int64_t i = b; i < e; ++i) {
-    run += src[i * stride];
-    out[i] = run;
+  return e.first;
+}
+constexpr int kScanPer = 8;
+constexpr int64_t kScanTile = (int64_t)kScanThreads * kScanPer;
+
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t u = __shfl_up(v, d, 64);
+    if (lane >= d) v += u;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_partials(const int64_t* __restrict__ src, int64_t stride,
+                                                                int64_t n, int64_t* __restrict__ partials) {
+  __shared__ int64_t ws[kScanThreads / 64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kScanTile;
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    const int64_t i = base + (int64_t)k * kScanThreads + t;  // coalesced for the reduction
+    if (i < n) s += src[i * stride];
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+  if (lane == 0) ws[w] = s;
+  __syncthreads();
+  if (t == 0) {
+    int64_t tot = 0;
+    for (int k = 0; k < kScanThreads / 64; ++k) tot += ws[k];
+    partials[blockIdx.x] = tot;
+  }
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_tiles(const int64_t* __restrict__ src, int64_t stride,
+                                                             int64_t n, const int64_t* __restrict__ partials,
+                                                             int64_t* __restrict__ out) {
+  __shared__ int64_t ws[kScanThreads / 64];
+  __shared__ int64_t tile_base;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // sum of the partials of the tiles before this one
+  int64_t pre = 0;
+  for (int64_t k = t; k < (int64_t)blockIdx.x; k += kScanThreads) pre += partials[k];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) pre += __shfl_xor(pre, d, 64);
+  if (lane == 0) ws[w] = pre;
+  __syncthreads();
+  if (t == 0) {
+    int64_t tot = 0;
+    for (int k = 0; k < kScanThreads / 64; ++k) tot += ws[k];
+    tile_base = tot;
+  }
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * kScanTile + (int64_t)t * kScanPer;
+  int64_t v[kScanPer];
+  int64_t run = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    const int64_t i = b0 + k;
+    run += i < n ? src[i * stride] : 0;
+    v[k] = run;
+  }
+  const int64_t incl = wave_incl_scan(run, lane);
+  __syncthreads();  // ws reused
+  if (lane == 63) ws[w] = incl;
+  __syncthreads();
+  int64_t off = tile_base + incl - run;
+  for (int k = 0; k < w; ++k) off += ws[k];
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    const int64_t i = b0 + k;
+    if (i < n) out[i] = off + v[k];
   }
 }
 
@@ -227,7 +299,16 @@ int tbrt_memset(void* p, int v, size_t n, hipStream_t s) { return (int)hipMemset
 
 int tb_scan_strided_i64(hipStream_t stream, const int64_t* src, int64_t stride, int64_t n, int64_t* out) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(k_scan_strided_i64, dim3(1), dim3(kScanThreads), 0, stream, src, stride, n, out);
+  const int64_t tiles = (n + kScanTile - 1) / kScanTile;
+  int64_t* partials = nullptr;
+  if (tiles > 1) {
+    // one partials buffer per (device, stream): scans on a stream run in order, so it is never
+    // shared by two scans in flight; it only grows (hipFree synchronises before the old one goes)
+    partials = scan_partials_for(stream, tiles);
+    if (!partials) return (int)hipErrorOutOfMemory;
+    hipLaunchKernelGGL(k_scan_partials, dim3((uint32_t)tiles), dim3(kScanThreads), 0, stream, src, stride, n, partials);
+  }
+  hipLaunchKernelGGL(k_scan_tiles, dim3((uint32_t)tiles), dim3(kScanThreads), 0, stream, src, stride, n, partials, out);
   return (int)hipGetLastError();
 }
 

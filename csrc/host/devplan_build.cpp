@@ -211,6 +211,54 @@ void gate_host(const DevGate& g, const std::vector<const int64_t*>& recs, int64_
   }
 }
 
+DevResolve build_resolve(const std::vector<StepCfg>& steps, const std::vector<std::array<int, 3>>& entries,
+                         const std::vector<int>& c4_version) {
+  if (entries.size() != c4_version.size()) throw std::invalid_argument("resolve: entries / versions length");
+  if (entries.size() != steps.size()) throw std::invalid_argument("resolve: every pipeline step needs an entry");
+  DevResolve rp;
+  std::memset(&rp, 0, sizeof(rp));
+  rp.gate = build_gate(steps, entries);  // range checks, <= kMaxGateSteps
+  for (size_t k = 0; k < entries.size(); ++k) {
+    if (rp.gate.steps[k].kind == GK_NONE)
+      throw std::invalid_argument("resolve: step " + std::to_string(entries[k][0]) + " has no device decision");
+    if (k > 0 && entries[k][0] <= entries[k - 1][0]) throw std::invalid_argument("resolve: steps out of order");
+    if (c4_version[k] >= kMaxVersions || (c4_version[k] >= 0 && rp.gate.steps[k].kind != GK_C4))
+      throw std::invalid_argument("resolve: content version out of range");
+    rp.step_index[k] = entries[k][0];
+    rp.c4_version[k] = c4_version[k];
+  }
+  return rp;
+}
+
+void resolve_host(const DevResolve& rp, const std::vector<const int64_t*>& recs, int64_t ndocs,
+                  const uint32_t* flags, const std::vector<const char*>& vdata,
+                  const std::vector<const int64_t*>& voff, std::vector<int32_t>& fail, std::vector<uint8_t>& status,
+                  std::string& out, std::vector<int64_t>& out_off, std::vector<int32_t>& rows) {
+  for (int s = 0; s < rp.gate.n_steps; ++s) {
+    if (rp.gate.steps[s].slot < 0 || rp.gate.steps[s].slot >= (int)recs.size())
+      throw std::runtime_error("resolve record slot out of range");
+    if (rp.c4_version[s] >= (int)voff.size()) throw std::runtime_error("resolve version out of range");
+  }
+  fail.assign(ndocs, -1);
+  status.assign(ndocs, 0);
+  std::vector<int32_t> ver(ndocs, 0);
+  for (int64_t doc = 0; doc < ndocs; ++doc)  // k_resolve
+    resolve_doc(rp, recs.data(), ndocs, doc, flags ? flags[doc] : 0u, fail[doc], status[doc], ver[doc]);
+  out.clear();
+  out_off.assign(ndocs + 1, 0);
+  rows.assign(ndocs, 0);
+  int64_t pos = 0;
+  for (uint8_t want : {kResolveKept, kResolveFiltered})  // k_compact: kept, then excluded, doc order
+    for (int64_t doc = 0; doc < ndocs; ++doc) {
+      if (status[doc] != want) continue;
+      const int v = ver[doc];
+      out_off[pos] = (int64_t)out.size();
+      rows[pos++] = (int32_t)doc;
+      out.append(vdata[v] + voff[v][doc], (size_t)(voff[v][doc + 1] - voff[v][doc]));
+    }
+  out_off[pos] = (int64_t)out.size();
+}
+
 std::vector<uint64_t> pow_table(uint32_t n) {
   // [0, n]: B^i, then [n + 1, 2n + 1]: B^-i (the layout tb_pow_table writes on the device)
   std::vector<uint64_t> pw(2 * (size_t)n + 2);

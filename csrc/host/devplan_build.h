@@ -21,6 +21,17 @@ DevC4 build_c4(const StepCfg& c);
 // Gate (csrc/common/gate.h) over steps: entries = (step index, record slot, record prefix).
 DevGateStep build_gate_step(const StepCfg& c, int slot, int prefix);
 DevGate build_gate(const std::vector<StepCfg>& steps, const std::vector<std::array<int, 3>>& entries);
+// K16 resolve plan over the whole pipeline: entries = (step index, record slot, record prefix) of
+// every step in pipeline order, c4_version[k] = content version step k produces (-1: none).
+// Throws std::invalid_argument when the pipeline cannot be resolved on the device (a host-only
+// step, a step without a gate kind, too many steps or versions).
+DevResolve build_resolve(const std::vector<StepCfg>& steps, const std::vector<std::array<int, 3>>& entries,
+                         const std::vector<int>& c4_version);
+// Host run of k_resolve + k_compact (same per-document function, same output layout).
+void resolve_host(const DevResolve& rp, const std::vector<const int64_t*>& recs, int64_t ndocs,
+                  const uint32_t* flags, const std::vector<const char*>& vdata,
+                  const std::vector<const int64_t*>& voff, std::vector<int32_t>& fail, std::vector<uint8_t>& status,
+                  std::string& out, std::vector<int64_t>& out_off, std::vector<int32_t>& rows);
 std::vector<uint64_t> pow_table(uint32_t n);  // B^0..B^n followed by B^-0..B^-n
 
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,

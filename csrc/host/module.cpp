@@ -477,18 +477,20 @@ PYBIND11_MODULE(_tbhost, m) {
         }
         return out;
       })
-      .def("assemble", [](PyBatch& b, py::array_t<int64_t, py::array::c_style> idx) {
+      .def("assemble", [](PyBatch& b, py::array_t<int64_t, py::array::c_style> idx, bool with_text) -> py::tuple {
         std::vector<int64_t> iv(idx.data(), idx.data() + idx.size());
         RawBuf td, md;
         std::vector<int64_t> to, mo;
         std::vector<uint8_t> mv;
         {
           py::gil_scoped_release nogil;
-          b.st->assemble(iv, td, to, md, mo, mv);
+          b.st->assemble(iv, td, to, md, mo, mv, with_text);
         }
+        if (!with_text) return py::make_tuple(py::none(), py::none(), raw_to_numpy(md), to_numpy(std::move(mo)),
+                                              to_numpy(std::move(mv)));
         return py::make_tuple(raw_to_numpy(td), to_numpy(std::move(to)), raw_to_numpy(md),
                               to_numpy(std::move(mo)), to_numpy(std::move(mv)));
-      });
+      }, py::arg("idx"), py::arg("with_text") = true);
 
   // ---- device plan building + host emulation of the device algorithms ----
   m.def("device_supported", [](const StepCfg& c) {
@@ -526,6 +528,48 @@ PYBIND11_MODULE(_tbhost, m) {
     return (int)decide_status(c, r.data());
   });
   m.attr("SIZEOF_DEV_GATE") = sizeof(DevGate);
+  m.attr("SIZEOF_DEV_RESOLVE") = sizeof(DevResolve);
+  m.attr("MAX_VERSIONS") = kMaxVersions;
+  m.def("build_resolve", [](const std::vector<StepCfg>& steps, const std::vector<std::array<int, 3>>& entries,
+                            const std::vector<int>& c4_version) {
+    DevResolve rp = build_resolve(steps, entries, c4_version);
+    return py::bytes((const char*)&rp, sizeof(rp));
+  });
+  m.def("resolve_host", [](const py::bytes& blob, const std::vector<py::array_t<int64_t, py::array::c_style>>& recs,
+                           int64_t ndocs, py::array_t<uint32_t, py::array::c_style> flags,
+                           const std::vector<py::array_t<uint8_t, py::array::c_style>>& vdata,
+                           const std::vector<py::array_t<int64_t, py::array::c_style>>& voff) {
+    std::string bs = blob;
+    if (bs.size() != sizeof(DevResolve)) throw std::runtime_error("bad resolve blob");
+    DevResolve rp;
+    std::memcpy(&rp, bs.data(), sizeof(rp));
+    if ((int64_t)flags.size() < ndocs || vdata.size() != voff.size()) throw std::runtime_error("resolve: operand shapes");
+    for (int s = 0; s < rp.gate.n_steps; ++s) {
+      const DevGateStep& st = rp.gate.steps[s];
+      if (st.slot < 0 || st.slot >= (int)recs.size() ||
+          (int64_t)recs[st.slot].size() < ((int64_t)st.prefix + st.width) * ndocs)
+        throw std::runtime_error("resolve record buffer too short");
+    }
+    std::vector<const int64_t*> rp_ptrs;
+    for (auto& r : recs) rp_ptrs.push_back(r.data());
+    std::vector<const char*> vd;
+    std::vector<const int64_t*> vo;
+    for (size_t v = 0; v < vdata.size(); ++v) {
+      if ((int64_t)voff[v].size() != ndocs + 1) throw std::runtime_error("resolve: version offsets length");
+      vd.push_back((const char*)vdata[v].data());
+      vo.push_back(voff[v].data());
+    }
+    std::vector<int32_t> fail, rows;
+    std::vector<uint8_t> status;
+    std::string out;
+    std::vector<int64_t> out_off;
+    {
+      py::gil_scoped_release nogil;
+      resolve_host(rp, rp_ptrs, ndocs, flags.data(), vd, vo, fail, status, out, out_off, rows);
+    }
+    return py::make_tuple(to_numpy(std::move(fail)), to_numpy(std::move(status)), str_to_numpy(std::move(out)),
+                          to_numpy(std::move(out_off)), to_numpy(std::move(rows)));
+  });
   m.def("stage_layout", [](const py::bytes& b) {
     std::string s = b;
     DevStage d;

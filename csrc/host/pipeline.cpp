@@ -673,11 +673,12 @@ static void give_charbuf(std::unique_ptr<CharBuf> p) {
 
 void BatchState::assemble(const std::vector<int64_t>& idx, RawBuf& text_data, std::vector<int64_t>& text_off,
                           RawBuf& meta_data, std::vector<int64_t>& meta_off,
-                          std::vector<uint8_t>& meta_valid) const {
+                          std::vector<uint8_t>& meta_valid, bool with_text) const {
   const int64_t m = (int64_t)idx.size();
   // text: sizes are known up front -> offsets, then one parallel gather into the final buffer
-  text_off.assign(m + 1, 0);
-  for (int64_t k = 0; k < m; ++k) {
+  // (with_text=false: the device compacted the texts already, only the metadata is built here)
+  text_off.assign(with_text ? m + 1 : 0, 0);
+  for (int64_t k = 0; k < m && with_text; ++k) {
     const int64_t i = idx[k];
     int64_t len;
     const int v = cur_version_[i];
@@ -685,7 +686,7 @@ void BatchState::assemble(const std::vector<int64_t>& idx, RawBuf& text_data, st
     else len = versions_[v].off[i + 1] - versions_[v].off[i];
     text_off[k + 1] = text_off[k] + len;
   }
-  text_data.alloc((size_t)text_off[m]);
+  if (with_text) text_data.alloc((size_t)text_off[m]);
   // metadata: formatted per chunk (sizes unknown), then concatenated
   const int nchunks = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)nthreads_ * 4, m / 256));
   // per-chunk metadata buffers come from a process-wide free list: their pages stay mapped and
@@ -709,8 +710,10 @@ void BatchState::assemble(const std::vector<int64_t>& idx, RawBuf& text_data, st
       md.reserve((size_t)(b - a) * 192);
       for (int64_t k = a; k < b; ++k) {
         const int64_t i = idx[k];
-        std::string_view t = content(i);
-        if (!t.empty()) std::memcpy(text_data.p + text_off[k], t.data(), t.size());
+        if (with_text) {
+          std::string_view t = content(i);
+          if (!t.empty()) std::memcpy(text_data.p + text_off[k], t.data(), t.size());
+        }
         const bool has_input = meta_data_ && (!meta_valid_ || meta_valid_[i]);
         const int last = status_[i] == 0 ? n_applied_ - 1 : std::min(fail_step_[i], n_applied_ - 1);
         if (!has_input && fast_meta) {

@@ -139,7 +139,8 @@ class BatchState {
 
   // Output assembly for a subset of documents (indices): contents and metadata JSON.
   void assemble(const std::vector<int64_t>& idx, RawBuf& text_data, std::vector<int64_t>& text_off,
-                RawBuf& meta_data, std::vector<int64_t>& meta_off, std::vector<uint8_t>& meta_valid) const;
+                RawBuf& meta_data, std::vector<int64_t>& meta_off, std::vector<uint8_t>& meta_valid,
+                bool with_text = true) const;
   int64_t meta_parse_failures() const { return meta_fail_.load(); }
 
  private:

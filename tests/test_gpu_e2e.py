@@ -66,3 +66,28 @@ def test_device_fault_recovery(tmp_path):
         res[tag] = (st.kept, st.excluded, pq.read_table(o).column("id"), pq.read_table(e).column("id"))
     assert res["ok"][:2] == res["fault"][:2]
     assert res["ok"][2].equals(res["fault"][2]) and res["ok"][3].equals(res["fault"][3])
+
+
+def test_device_resolve_fast_path_equals_host_assembly(monkeypatch):
+    """K16 on the GPU: k_resolve + scans + k_compact outputs are used (no fallback) and equal the
+    host-assembled outputs of the same records."""
+    import numpy as np
+
+    from textblaster_amd.config import load_pipeline_config
+    from textblaster_amd.pipeline.engine import Engine
+    from textblaster_amd.utils import metrics
+
+    from test_emulated_device_path import EDGE, outputs
+
+    cfg = load_pipeline_config(CFG)
+    data, off = synth.pack(synth.make_corpus(20000, 1024, seed=33) + EDGE)
+    before = metrics.DEVICE_RESOLVE_FALLBACK_TOTAL._value.get()
+    eng = Engine(cfg, backend="cuda")
+    assert eng.device_runner.resolve_t is not None
+    a = eng.process(data, off)
+    assert metrics.DEVICE_RESOLVE_FALLBACK_TOTAL._value.get() == before
+    monkeypatch.setenv("TB_DEVICE_RESOLVE", "0")
+    b = Engine(cfg, backend="cuda").process(data, off)
+    np.testing.assert_array_equal(a.status, b.status)
+    np.testing.assert_array_equal(a.fail_step, b.fail_step)
+    assert outputs(a) == outputs(b)

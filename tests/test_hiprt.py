@@ -48,7 +48,7 @@ def test_pinned_async_copies_and_events(rt):
 
 def test_scan_strided_matches_numpy(rt):
     rng = np.random.default_rng(1)
-    for n in (1, 2, 63, 1024, 1025, 100_003):
+    for n in (1, 2, 63, 1024, 1025, 2047, 2048, 2049, 12295, 100_003, 600_001):
         src = rng.integers(0, 1000, 2 * n, dtype=np.int64)
         d = rt.to_device(src)
         out = rt.zeros(n, np.int64)

@@ -29,6 +29,8 @@ _SIGS = {
     "tb_c4_pass_a_blk": [_P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _P],
     "tb_gate": [_P, _P, _P, _I32, _I32, _P, _P, _I32],
     "tb_sizeof_gate": [],
+    "tb_resolve": [_P, _P, _P, _I32, _I32, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P],
+    "tb_sizeof_resolve": [],
     "tb_block_threads": [],
     "tb_badwords_match": [_P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
@@ -82,7 +84,8 @@ class Kernels:
         self.lib = native.hip()
         h = native.host()
         if (self.lib.tb_sizeof_plan() != h.SIZEOF_DEV_PLAN or self.lib.tb_sizeof_stage() != h.SIZEOF_DEV_STAGE
-                or self.lib.tb_sizeof_gate() != h.SIZEOF_DEV_GATE):
+                or self.lib.tb_sizeof_gate() != h.SIZEOF_DEV_GATE
+                or self.lib.tb_sizeof_resolve() != h.SIZEOF_DEV_RESOLVE):
             raise DeviceError("libtbhip.so and _tbhost disagree on the device plan layout; rebuild")
         s1, s2, l1, l2 = h.ucd_tables()
         self.tabs = [hiprt.to_device(a) for a in (s1, s2, l1, l2)]
@@ -186,3 +189,22 @@ class Kernels:
         rc = self.lib.tb_langid_head(self.stream(), vec.data_ptr(), cnt.data_ptr(), wT.data_ptr(), bias.data_ptr(),
                                      ndocs, rec.data_ptr(), rec_off, width, _ptr(dbg_logits))
         _check(rc, "tb_langid_head")
+
+    def resolve(self, rp, recs, ndocs, flags, versions, fail, status, fver, lanes, sc, out, out_off, rows, err):
+        """K16: k_resolve + four scans + k_compact (see tb_resolve). ``recs``: record buffers by
+        slot; ``versions``: [(bytes, offsets)] by content version; the rest are outputs/scratch."""
+        if len(recs) > 8 or not 1 <= len(versions) <= 8:
+            raise DeviceError("resolve: too many record buffers or versions")
+        if (flags.numel() < ndocs or fail.numel() < ndocs or status.numel() < ndocs or fver.numel() < ndocs
+                or lanes.numel() < 4 * ndocs or sc.numel() < 4 * ndocs or out_off.numel() < ndocs + 1
+                or rows.numel() < ndocs or err.numel() < 1 or any(vo.numel() != ndocs + 1 for _, vo in versions)):
+            raise DeviceError("resolve: operand shapes")
+        ra = (ctypes.c_void_p * 8)(*([r.data_ptr() for r in recs] + [None] * (8 - len(recs))))
+        vb = (ctypes.c_void_p * 8)(*([b.data_ptr() for b, _ in versions] + [None] * (8 - len(versions))))
+        vo = (ctypes.c_void_p * 8)(*([o.data_ptr() for _, o in versions] + [None] * (8 - len(versions))))
+        rc = self.lib.tb_resolve(self.stream(), rp.data_ptr(), ctypes.cast(ra, ctypes.c_void_p), len(recs), ndocs,
+                                 flags.data_ptr(), ctypes.cast(vb, ctypes.c_void_p), ctypes.cast(vo, ctypes.c_void_p),
+                                 len(versions), fail.data_ptr(), status.data_ptr(), fver.data_ptr(), lanes.data_ptr(),
+                                 sc.data_ptr(), out.data_ptr(), out.numel(), out_off.data_ptr(), rows.data_ptr(),
+                                 err.data_ptr())
+        _check(rc, "tb_resolve")

@@ -32,6 +32,97 @@ class DeviceResult:
     # (a step of pass k-1 or earlier filtered it on the device); pass_of_step: step -> pass index
     dead: Optional[np.ndarray] = None
     pass_of_step: Optional[Dict[int, int]] = None
+    # K16 (device resolve + compaction, csrc/common/gate.h resolve_doc): per document the first
+    # failing step and status, and the final contents of kept then excluded documents compacted
+    # into one buffer. None when the pipeline has host steps (TB_DEVICE_RESOLVE=0: off).
+    resolved: Optional["Resolved"] = None
+
+
+@dataclasses.dataclass
+class Resolved:
+    fail: np.ndarray        # int32 [ndocs]: first failing step, -1 kept, 1<<30 delegated
+    status: np.ndarray      # uint8 [ndocs]: 0 kept, 1 filtered, 3 delegated (CPU path)
+    out: np.ndarray         # uint8: kept texts, then excluded texts
+    out_off: np.ndarray     # int64 [ndocs + 1]: start of output k (first nk + nx + 1 valid)
+    rows: np.ndarray        # int32 [ndocs]: document of output k
+    err: int = 0            # nonzero: the compaction ran out of room (never with the C4 bound)
+
+    def parts(self):
+        """(kept rows, kept offsets, kept text), (excluded ...) as views of the buffers."""
+        nk = int(np.count_nonzero(self.status == 0))
+        nx = int(np.count_nonzero(self.status == 1))
+        o = self.out_off
+        kb, tot = int(o[nk]), int(o[nk + nx])
+        kept = (self.rows[:nk].astype(np.int64), o[:nk + 1], self.out[:kb])
+        excl = (self.rows[nk:nk + nx].astype(np.int64), o[nk:nk + nx + 1] - kb, self.out[kb:tot])
+        return kept, excl
+
+
+class LazyVersions(dict):
+    """Content versions >= 1 left in HBM (K16 mode: the outputs come compacted from the device, so
+    the host needs the versions only when it falls back to host assembly). Indexing or iterating
+    items downloads them once."""
+
+    def __init__(self, dev):
+        super().__init__()
+        self._dev = dict(dev)
+
+    def _fetch(self):
+        for v, (vb, vo) in sorted(self._dev.items()):
+            ho = vo.to_host()
+            dict.__setitem__(self, v, (vb[: int(ho[-1])].to_host() if int(ho[-1]) else np.zeros(0, np.uint8), ho))
+        self._dev = {}
+
+    def __getitem__(self, v):
+        if self._dev:
+            self._fetch()
+        return dict.__getitem__(self, v)
+
+    def items(self):
+        if self._dev:
+            self._fetch()
+        return dict.items(self)
+
+    def keys(self):
+        return set(self._dev) | set(dict.keys(self))
+
+    def __iter__(self):
+        return iter(sorted(self.keys()))
+
+    def __len__(self):
+        return len(self.keys())
+
+
+def resolve_entries(plan: ExecPlan, stage_layout):
+    """K16 plan: (entries, c4_versions) over every pipeline step in order — entries are (step,
+    record slot, prefix) with slots = [stage 0 .. stage S-1, C4 step 0 ..] — or None when a step
+    runs on the host (TokenCounter, C4BadWords)."""
+    entries, vers = [], []
+    ns = len(plan.stages)
+    for sp in plan.steps:
+        if sp.stage >= 0:
+            pos = plan.stages[sp.stage].index(sp.index)
+            _, _, prefix = stage_layout[sp.stage][1][pos]
+            entries.append((sp.index, sp.stage, prefix))
+            vers.append(-1)
+        elif sp.c4_pass >= 0:
+            entries.append((sp.index, ns + plan.c4_steps.index(sp.index), 0))
+            vers.append(sp.version_out)
+        else:
+            return None
+    if ns + len(plan.c4_steps) > 8 or plan.n_versions > native.host().MAX_VERSIONS or not entries:
+        return None
+    return entries, vers
+
+
+def build_resolve(plan: ExecPlan, stage_layout, steps_native) -> Optional[bytes]:
+    r = resolve_entries(plan, stage_layout)
+    if r is None:
+        return None
+    try:
+        return native.host().build_resolve(steps_native, r[0], r[1])
+    except ValueError:  # a step without a device decision (e.g. > 16 n-gram orders)
+        return None
 
 
 class _Slot:
@@ -56,7 +147,8 @@ class PendingBatch:
     """A submitted batch: kernels and D2H copies are queued on the stream; ``wait()`` blocks on
     the completion event and returns host views of the results."""
 
-    def __init__(self, runner, ndocs, event, stage_recs, c4_recs, versions, flags, t_submit, keep, dead=None):
+    def __init__(self, runner, ndocs, event, stage_recs, c4_recs, versions, flags, t_submit, keep, dead=None,
+                 resolved=None):
         self.runner = runner
         self.ndocs = ndocs
         self.event = event
@@ -67,6 +159,7 @@ class PendingBatch:
         self._dead = dead
         self._t_submit = t_submit
         self._keep = keep  # device tensors that must stay alive until the event completes
+        self._resolved = resolved
 
     def wait(self) -> DeviceResult:
         import time
@@ -77,9 +170,12 @@ class PendingBatch:
         t1 = time.perf_counter()
         stage_recs = list(self._stage_recs)
         c4_recs = dict(self._c4_recs)
-        host_versions = {}
-        for ver, (vb, vo) in self._versions.items():
-            host_versions[ver] = (vb[: int(vo[-1])], vo)
+        if isinstance(self._versions, LazyVersions):
+            host_versions = self._versions
+        else:
+            host_versions = {}
+            for ver, (vb, vo) in self._versions.items():
+                host_versions[ver] = (vb[: int(vo[-1])], vo)
         fl = self._flags.view(np.uint32)
         dead = self._dead
         if self.runner.phase_prof:
@@ -94,7 +190,11 @@ class PendingBatch:
         self._keep = None
         timings = dict(self._t_submit)
         timings["gpu_wait"] = t1 - t0
-        return DeviceResult(stage_recs, c4_recs, host_versions, fl, timings, dead, self.runner.pass_of_step)
+        res = None
+        if self._resolved is not None:
+            fail, st, out, out_off, rows, err = self._resolved
+            res = Resolved(fail, st, out, out_off, rows, int(err[0]))
+        return DeviceResult(stage_recs, c4_recs, host_versions, fl, timings, dead, self.runner.pass_of_step, res)
 
 
 def plan_passes(plan: ExecPlan, stage_layout, steps_native, gating: bool):
@@ -227,6 +327,12 @@ class DeviceRunner:
             self.gating = os.environ.get("TB_GATE", "1") not in ("", "0")
             self.passes, self.pass_of_step, gates = plan_passes(plan, self.stage_layout, steps_native, self.gating)
             self.gate_ts = {p: self._to_dev(b) for p, b in gates.items()}
+            # K16: device resolve + output compaction when every step runs on the device
+            self.resolve_t = None
+            if os.environ.get("TB_DEVICE_RESOLVE", "1") not in ("", "0"):
+                blob = build_resolve(plan, self.stage_layout, steps_native)
+                if blob is not None:
+                    self.resolve_t = self._to_dev(blob)
             # B^k for the hashes, shared read-only by both slots: allocated once (longer spans
             # fall back to powmod61 in the kernels)
             with tracing.trace_range("tb.init.pow_table"):
@@ -575,6 +681,28 @@ class DeviceRunner:
                 keep.append(src)
         for ev in tails:
             main.wait_event(ev)
+        res_d = None
+        if self.resolve_t is not None:
+            # K16 on the compute stream after every pass: first failure, status, and the final
+            # contents of kept / excluded documents compacted into one buffer (the host then only
+            # formats metadata). Output bound: a C4 rewrite grows a document by <= C4_MAX_GROWTH.
+            recs = [r for r in stage_recs_d] + [c4_recs_d[i] for i in self.plan.c4_steps]
+            vlist = [(versions[v][0], versions[v][1]) for v in range(self.plan.n_versions)]
+            cap = len(data) + self.c4_growth * (self.plan.n_versions - 1) * ndocs + 16
+            r_fail = rt.empty(ndocs, np.int32)
+            r_status = rt.empty(ndocs, np.uint8)
+            r_ver = rt.empty(ndocs, np.uint8)
+            r_lanes = rt.empty(4 * ndocs, np.int64)
+            r_sc = rt.empty(4 * ndocs, np.int64)
+            r_out = rt.empty(max(cap, 1), np.uint8)
+            r_off = rt.zeros(ndocs + 1, np.int64)
+            r_rows = rt.empty(ndocs, np.int32)
+            r_err = rt.zeros(1, np.int32)
+            with self._ktimed(keep, "resolve"):
+                self.k.resolve(self.resolve_t, recs, ndocs, flags.view(np.uint32), vlist, r_fail, r_status, r_ver,
+                               r_lanes, r_sc, r_out, r_off, r_rows, r_err)
+            keep += [r_fail, r_status, r_ver, r_lanes, r_sc, r_out, r_off, r_rows, r_err]
+            res_d = (r_fail, r_status, r_out, r_off, r_rows, r_err)
         # D2H into pinned host buffers on the download stream (the slot's compute stream in the
         # 4-stream layout: it is last in line there anyway), then one completion event
         done = self._record(main)
@@ -590,16 +718,24 @@ class DeviceRunner:
         h_stage = [d2h(r) if r is not None else None for r in stage_recs_d]
         h_c4 = {i: d2h(r) for i, r in c4_recs_d.items()}
         h_versions = {}
-        for ver in range(1, self.plan.n_versions):
-            vb, vo, _ = versions[ver]
-            h_versions[ver] = (d2h(vb), d2h(vo))
+        h_res = None
+        if res_d is not None:
+            h_res = tuple(d2h(t) for t in res_d)
+        if h_res is not None:
+            # K16: the compacted outputs replace the versions on the host path; they stay in HBM
+            # (downloaded only if the host has to assemble this batch itself)
+            h_versions = LazyVersions({v: versions[v][:2] for v in range(1, self.plan.n_versions)})
+        else:
+            for ver in range(1, self.plan.n_versions):
+                vb, vo, _ = versions[ver]
+                h_versions[ver] = (d2h(vb), d2h(vo))
         h_flags = d2h(flags)
         h_dead = d2h(dead) if dead is not None else None
         ev = self._record(d2h_s)
         keep += [stage_recs_d, c4_recs_d, versions, flags, dead, ready, tails, done]
         t2 = time.perf_counter()
         return PendingBatch(self, ndocs, ev, h_stage, h_c4, h_versions, h_flags,
-                            {"stage_h2d": t1 - t0, "launch": t2 - t1}, keep, h_dead)
+                            {"stage_h2d": t1 - t0, "launch": t2 - t1}, keep, h_dead, h_res)
 
     def run(self, data: np.ndarray, off: np.ndarray) -> DeviceResult:
         return self.submit(data, off).wait()
@@ -628,6 +764,9 @@ class EmulatedRunner:
         # test hook: additionally mark every k-th document dead after the first pass (a wrong
         # device gate), to exercise the resolver's recovery path
         self.gate_corrupt = gate_corrupt
+        self.resolve_blob = None
+        if os.environ.get("TB_DEVICE_RESOLVE", "1") not in ("", "0"):
+            self.resolve_blob = build_resolve(plan, self.stage_layout, steps_native)
 
     def run(self, data: np.ndarray, off: np.ndarray) -> DeviceResult:
         import time
@@ -658,5 +797,13 @@ class EmulatedRunner:
                     extra = np.arange(0, ndocs, self.gate_corrupt)
                     dead[extra[dead[extra] == 0]] = 1
         host_versions = {v: versions[v] for v in range(1, self.plan.n_versions)}
+        resolved = None
+        if self.resolve_blob is not None:
+            recs = list(stage_recs) + [c4_recs[i] for i in self.plan.c4_steps]
+            vl = [versions[v] for v in range(self.plan.n_versions)]
+            fail, st, out, out_off, rows = h.resolve_host(self.resolve_blob, recs, ndocs, flags,
+                                                          [np.ascontiguousarray(d) for d, _ in vl],
+                                                          [np.ascontiguousarray(o) for _, o in vl])
+            resolved = Resolved(fail, st, out, out_off, rows)
         return DeviceResult(stage_recs, c4_recs, host_versions, flags, {"emulate": time.perf_counter() - t0}, dead,
-                            self.pass_of_step)
+                            self.pass_of_step, resolved)

@@ -357,6 +357,7 @@ class Engine:
         bs = self.h.BatchState(data, off, md, mo, mv, self.nthreads)
         timings: Dict[str, float] = {"batch_state": time.perf_counter() - tf}
         delegated = np.zeros(0, dtype=np.int64)
+        resolved = None
         if sub.dev is not None:
             tw = time.perf_counter()
             res = sub.dev.wait() if hasattr(sub.dev, "wait") else sub.dev
@@ -366,10 +367,15 @@ class Engine:
             delegated = np.nonzero(res.flags)[0].astype(np.int64)
             if len(delegated):
                 bs.delegate(delegated)
+            resolved = getattr(res, "resolved", None)
             vid = {0: 0}
-            for v in sorted(res.versions):
-                vd, vo = res.versions[v]
-                vid[v] = bs.add_version(np.ascontiguousarray(vd), np.ascontiguousarray(vo))
+            if resolved is not None:
+                # versions are registered (index v) only if the host assembles this batch
+                vid.update({v: v for v in res.versions})
+            else:
+                for v in sorted(res.versions):
+                    vd, vo = res.versions[v]
+                    vid[v] = bs.add_version(np.ascontiguousarray(vd), np.ascontiguousarray(vo))
             dead = getattr(res, "dead", None)
             gate_checked = set()
             for sp in self.plan.steps:
@@ -394,6 +400,12 @@ class Engine:
                     bs.apply_records(st, sp.index, res.c4_recs[sp.index], vid[sp.version_out])
                 else:
                     self._host_step(bs, sp.index, ndocs)
+            if resolved is not None and not self._device_resolve_agrees(bs, resolved):
+                resolved = None
+                for v in sorted(res.versions):
+                    vd, vo = res.versions[v]
+                    if bs.add_version(np.ascontiguousarray(vd), np.ascontiguousarray(vo)) != v:
+                        raise Unexpected("content version registration order")
             timings["resolve"] = time.perf_counter() - t1
         else:
             t1 = time.perf_counter()
@@ -401,7 +413,7 @@ class Engine:
             timings["cpu_pipeline"] = time.perf_counter() - t1
         t2 = time.perf_counter()
         with tracing.trace_range("tb.assemble"):
-            result = self._collect(bs, ndocs, timings)
+            result = self._collect(bs, ndocs, timings, resolved)
         if len(delegated):
             sub2 = self._process_subset_cpu(data, off, meta, delegated)
             result.kept += sub2.kept
@@ -506,14 +518,37 @@ class Engine:
         res.reasons = {int(rows[k]): v for k, v in res.reasons.items()}
         return res
 
-    def _collect(self, bs, ndocs: int, timings) -> BatchResult:
+    def _device_resolve_agrees(self, bs, resolved) -> bool:
+        """The host re-derived every decision from the device records (apply_records); the
+        device-compacted outputs are used only when both agree on every document's first failing
+        step and status, and the compaction did not run out of room. Otherwise the batch is
+        assembled on the host (counted in tb_device_resolve_fallback_total)."""
+        ok = (resolved.err == 0 and np.array_equal(bs.fail_step(), resolved.fail)
+              and np.array_equal(bs.status(), resolved.status))
+        if not ok:
+            import logging
+
+            from ..utils import metrics
+
+            logging.getLogger("textblaster_amd.engine").warning(
+                "device resolve disagrees with the host decisions (or overflowed); assembling this batch on the host")
+            metrics.DEVICE_RESOLVE_FALLBACK_TOTAL.inc()
+        return ok
+
+    def _collect(self, bs, ndocs: int, timings, resolved=None) -> BatchResult:
         status = bs.status()
         fail = bs.fail_step()
         kept_rows = np.nonzero(status == 0)[0].astype(np.int64)
         excl_rows = np.nonzero(status == 1)[0].astype(np.int64)
         err_rows = np.nonzero(status == 2)[0].astype(np.int64)
         parts = []
-        for rows in (kept_rows, excl_rows):
+        if resolved is not None:
+            # K16: texts were compacted on the device (kept, then excluded, document order — the
+            # rows above); only the metadata columns are built here
+            for rows, off, text in resolved.parts():
+                _, _, md, mo, mv = bs.assemble(rows, False)
+                parts.append(OutputPart(rows, text, off, md, mo, mv))
+        for rows in ((kept_rows, excl_rows) if resolved is None else ()):
             td, to, md, mo, mv = bs.assemble(rows)
             parts.append(OutputPart(rows, td, to, md, mo, mv))
         reasons = {}

@@ -75,6 +75,9 @@ CPU_FALLBACK_DOCS_TOTAL = Counter("tb_cpu_fallback_docs_total",
 GATE_MISMATCH_DOCS_TOTAL = Counter("tb_gate_mismatch_docs_total",
                                    "Documents a device step gate skipped that the host resolver found alive "
                                    "(recomputed on the CPU path; expected 0).", registry=REGISTRY)
+DEVICE_RESOLVE_FALLBACK_TOTAL = Counter("tb_device_resolve_fallback_total",
+                                        "Batches whose device resolve/compaction (K16) disagreed with the host "
+                                        "decisions and were assembled on the host (expected 0).", registry=REGISTRY)
 RANK = Gauge("tb_rank", "Data-parallel rank of this process.", registry=REGISTRY)
 WORLD_SIZE = Gauge("tb_world_size", "Number of data-parallel ranks.", registry=REGISTRY)
 GLOBAL_DOCS = Gauge("tb_global_docs_total", "All-reduced document counters (rank 0).", ["kind"],

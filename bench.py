@@ -172,6 +172,9 @@ def main():
             "mean_step_timings": {k: round(v / n_done, 5) for k, v in tsum.items()},
         }
         print(json.dumps(line), flush=True)
+        from textblaster_amd.utils import tracing
+
+        tracing.dump_timeline()  # TB_TIMELINE=<path>: host per-thread ranges of this run
         dr = getattr(eng, "device_runner", None)
         if dr is not None and getattr(dr, "phase_prof", False):
             print(dr.phase_report(), file=sys.stderr, flush=True)

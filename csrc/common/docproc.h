@@ -552,8 +552,19 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
 template <class P>
 TB_HD bool bytes_eq(const uint8_t* b, uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1) {
   if (a1 - a0 != b1 - b0) return false;
-  for (uint32_t i = 0; i < a1 - a0; ++i) if (b[a0 + i] != b[b0 + i]) return false;
-  return true;
+  const uint32_t n = a1 - a0;
+  // 16 independent byte loads per side before any compare: one memory round trip per 16 bytes
+  // instead of one per byte (the equal case — a verified duplicate — reads everything anyway)
+  uint32_t i = 0;
+  for (; i + 16 <= n; i += 16) {
+    uint32_t diff = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) diff |= (uint32_t)(b[a0 + i + k] ^ b[b0 + i + k]);
+    if (diff) return false;
+  }
+  uint32_t diff = 0;
+  for (; i < n; ++i) diff |= (uint32_t)(b[a0 + i] ^ b[b0 + i]);
+  return diff == 0;
 }
 
 // find_duplicates over byte spans [s[i], e[i]): (#repeats, sum of repeat byte lengths).
@@ -908,9 +919,12 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
               if (WL[p + n] - WL[p] != WL[q + n] - WL[q]) return false;
               // same canonical word sequence => same concatenation (the common case); only
               // different word splits of equal-hash text need the byte comparison
-              bool same = true;
-              for (uint32_t k = 0; k < n && same; ++k) same = wid[p + k] == wid[q + k];
-              if (same) return true;
+              // all n id pairs loaded before the compare (no early exit: n <= a few dozen and
+              // the loads then overlap instead of forming a chain of dependent round trips)
+              uint32_t dw = 0;
+#pragma unroll 5
+              for (uint32_t k = 0; k < n; ++k) dw |= wid[p + k] ^ wid[q + k];
+              if (dw == 0) return true;
               uint32_t wp = p, wq = q, bp = w.bs[p], bq = w.bs[q];
               const uint32_t L = WL[p + n] - WL[p];
               for (uint32_t i = 0; i < L; ++i) {

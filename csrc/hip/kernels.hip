@@ -259,6 +259,18 @@ __global__ __launch_bounds__(64) void k_langid_features(
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   x.stamp(PH_START);
   langid_features_coop(x, b, n, emb, lid_vec + (size_t)doc * kLidDim, lid_cnt + doc);
+  // Documents with dictionary-segmented scripts go to the CPU path (the stage kernel's decode
+  // flags them too). With the language-id gate in front of the stage (device.py plan_passes) the
+  // stage kernel never sees a document this pass filters, so the flag is raised here as well:
+  // dictionary scripts are >= U+0E00, i.e. lead bytes >= 0xE0 (host: has_dict_script).
+  bool dict = false;
+  for (uint32_t i = x.par.lane; i < n; i += 64) {
+    if (b[i] >= 0xE0) {
+      int len;
+      dict |= (x.ucd.props(utf8_decode(b, i, n, &len)) & P_DICT) != 0;
+    }
+  }
+  if (__ballot(dict) && x.par.leader()) x.set_flag(DOC_NEEDS_CPU);
   x.stamp(PH_LID);
   if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
 }

@@ -174,12 +174,16 @@ class Kernels:
                                    scratch_off.data_ptr(), src.data_ptr(), new_off.data_ptr(), out.data_ptr())
         _check(rc, "tb_c4_pass_b")
 
-    def gate(self, gate, recs, ndocs, flags, dead, code, max_slot):
-        """k_gate: mark documents that a step of the finished pass filtered (dead[doc] = code)."""
+    def gate(self, gate, recs, ndocs, flags, dead, code, max_slot, need):
+        """k_gate: mark documents that a step of the finished pass filtered (dead[doc] = code).
+        ``need``: int64 fields per document the gate's steps read from each record buffer (the
+        kernel trusts the blob's prefix/width, so the buffers are checked here)."""
         if not 0 < code <= 255:
             raise DeviceError("gate code out of range")
         if max_slot >= len(recs) or len(recs) > 8 or dead.numel() < ndocs or flags.numel() < ndocs:
             raise DeviceError("gate: operand shapes")
+        if any(r.numel() < need * ndocs for r in recs):
+            raise DeviceError("gate: a record buffer is smaller than the gate's steps read")
         arr = (ctypes.c_void_p * 8)(*([r.data_ptr() for r in recs] + [None] * (8 - len(recs))))
         rc = self.lib.tb_gate(self.stream(), gate.data_ptr(), ctypes.cast(arr, ctypes.c_void_p), len(recs), ndocs,
                               flags.data_ptr(), dead.data_ptr(), code)

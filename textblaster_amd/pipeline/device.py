@@ -197,26 +197,45 @@ class PendingBatch:
         return DeviceResult(stage_recs, c4_recs, host_versions, fl, timings, dead, self.runner.pass_of_step, res)
 
 
-def plan_passes(plan: ExecPlan, stage_layout, steps_native, gating: bool):
+KIND_LANGID = 4  # DevStep kind of LanguageDetectionFilter in a stage layout (csrc/common/devplan.h)
+
+
+def plan_passes(plan: ExecPlan, stage_layout, steps_native, gating: bool, lid_gate: bool = True):
     """Device passes in execution order (stages and C4 rewrites, by content version), the pass of
     every device step, and per pass (except the last) the gate blob over the steps it produced
-    records for."""
+    records for.
+
+    With gating, a stage that holds the language-id step next to other steps is preceded by a
+    ("lid", s) pass: the language-id bag and MFMA head run first, their gate marks the documents
+    the language filter drops, and the stage kernels skip them (the reference never runs the
+    later filters on those documents: executor.rs:30-57). TB_LID_GATE=0 keeps one pass."""
     h = native.host()
     passes = []
     for ver in range(plan.n_versions):
-        passes += [("stage", s) for s, sv in enumerate(plan.stage_version) if sv == ver]
+        for s, sv in enumerate(plan.stage_version):
+            if sv != ver:
+                continue
+            kinds = [k for k, _, _ in stage_layout[s][1]]
+            if gating and lid_gate and KIND_LANGID in kinds and len(kinds) > 1:
+                passes.append(("lid", s))
+            passes.append(("stage", s))
         passes += [("c4", i) for i in plan.c4_steps if plan.steps[i].version_in == ver]
     pass_of_step: Dict[int, int] = {}
     gates: Dict[int, bytes] = {}
     for p, (kind, x) in enumerate(passes):
-        if kind == "stage":
-            entries = [(j, 0, prefix) for j, (_, _, prefix) in zip(plan.stages[x], stage_layout[x][1])]
+        if kind in ("stage", "lid"):
+            sel = [(j, prefix, width) for j, (k, width, prefix) in zip(plan.stages[x], stage_layout[x][1])
+                   if (kind == "lid") == (k == KIND_LANGID) or (kind == "stage" and ("lid", x) not in passes)]
+            entries = [(j, 0, prefix) for j, prefix, _ in sel]
+            need = max(prefix + width for _, prefix, width in sel)
         else:
             entries = [(x, 0, 0)]
+            need = 7  # C4 record width
         for j, _, _ in entries:
             pass_of_step[j] = p
         if gating and p + 1 < len(passes) and p + 1 <= 255:
-            gates[p] = h.build_gate(steps_native, entries)
+            # need: int64 record fields per document the gate reads (checked at launch)
+            gates[p] = (h.build_gate(steps_native, entries), need)
     return passes, pass_of_step, gates
 
 
@@ -325,14 +344,19 @@ class DeviceRunner:
             self.c4_growth = int(h.C4_MAX_GROWTH)
             # TB_GATE=0 disables step gating (every pass runs over every document)
             self.gating = os.environ.get("TB_GATE", "1") not in ("", "0")
-            self.passes, self.pass_of_step, gates = plan_passes(plan, self.stage_layout, steps_native, self.gating)
-            self.gate_ts = {p: self._to_dev(b) for p, b in gates.items()}
+            self.passes, self.pass_of_step, gates = plan_passes(
+                plan, self.stage_layout, steps_native, self.gating,
+                os.environ.get("TB_LID_GATE", "1") not in ("", "0") and self.has_lid)
+            self.gate_ts = {p: self._to_dev(b) for p, (b, _) in gates.items()}
+            self.gate_need = {p: need for p, (_, need) in gates.items()}
             # K16: device resolve + output compaction when every step runs on the device
             self.resolve_t = None
             if os.environ.get("TB_DEVICE_RESOLVE", "1") not in ("", "0"):
                 blob = build_resolve(plan, self.stage_layout, steps_native)
                 if blob is not None:
                     self.resolve_t = self._to_dev(blob)
+                    # int64 fields per document read from each record buffer (launch-time check)
+                    self.resolve_need = [w for w, _ in self.stage_layout] + [7] * len(plan.c4_steps)
             # B^k for the hashes, shared read-only by both slots: allocated once (longer spans
             # fall back to powmod61 in the kernels)
             with tracing.trace_range("tb.init.pow_table"):
@@ -586,6 +610,27 @@ class DeviceRunner:
                 keep.append(ev_pre)
                 ev_lid = ev_blk = None
                 prof = self._prof_buf(ndocs, keep, f"stage{s}")
+                lid_pass = ("lid", s) in self.passes
+                if lid_pass:
+                    # language-id pass first (bag -> MFMA head -> gate on the side stream); the
+                    # stage kernels below skip the documents it filters
+                    slot.s_lid.wait_event(ev_pre)
+                    with rt.stream(slot.s_lid):
+                        with self._ktimed(keep, "langid_features"):
+                            self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec,
+                                                   lid_cnt, flags, self.lds_bytes_lid,
+                                                   self._prof_buf(ndocs, keep, f"langid{s}"))
+                        for kind, width, prefix in layout:
+                            if kind == KIND_LANGID:
+                                self.k.langid_head(lid_vec, lid_cnt, self.lid_wT, self.lid_b, ndocs, rec, prefix * ndocs,
+                                                   width)
+                        if pass_idx in self.gate_ts:
+                            self.k.gate(self.gate_ts[pass_idx], [rec], ndocs, flags, dead, pass_idx + 1, 0,
+                                        self.gate_need[pass_idx])
+                        ev_pre = self._record(slot.s_lid)
+                        keep.append(ev_pre)
+                    main.wait_event(ev_pre)
+                    pass_idx += 1
                 skip = dead if pass_idx > 0 else None
                 # long documents first: with the 4-stream layout the workgroup kernels and the
                 # language-id bag share the side stream, and the long-document tail must start early
@@ -597,7 +642,7 @@ class DeviceRunner:
                                                  self.lds_bytes_blk, prof, skip)
                         ev_blk = self._record(slot.s_blk)
                         keep.append(ev_blk)
-                if lid_vec is not None:
+                if lid_vec is not None and not lid_pass:
                     slot.s_lid.wait_event(ev_pre)
                     with rt.stream(slot.s_lid), self._ktimed(keep, "langid_features"):
                         self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec,
@@ -624,14 +669,16 @@ class DeviceRunner:
                                              self.lds_bytes, prof, self.stage_waves, ndocs - n_mid, skip)
                 if lid_vec is not None:
                     self._last_lid = (lid_vec, lid_cnt)
-                    main.wait_event(ev_lid)
+                    if ev_lid is not None:
+                        main.wait_event(ev_lid)
                 if ev_blk is not None:
                     main.wait_event(ev_blk)
                 for kind, width, prefix in layout:
-                    if kind == 4:
+                    if kind == KIND_LANGID and not lid_pass:
                         self.k.langid_head(lid_vec, lid_cnt, self.lid_wT, self.lid_b, ndocs, rec, prefix * ndocs, width)
                 if pass_idx in self.gate_ts:
-                    self.k.gate(self.gate_ts[pass_idx], [rec], ndocs, flags, dead, pass_idx + 1, 0)
+                    self.k.gate(self.gate_ts[pass_idx], [rec], ndocs, flags, dead, pass_idx + 1, 0,
+                                        self.gate_need[pass_idx])
                 pass_idx += 1
                 stage_recs_d[s] = rec
             c4_here = [i for i in self.plan.c4_steps if self.plan.steps[i].version_in == ver]
@@ -671,7 +718,8 @@ class DeviceRunner:
                     rt.scan_strided_i64(src[1:], 2, ndocs, new_off[1:])
                     self.k.c4_pass_b(vb, vo, ndocs, c4_scratch, d_soff, src, new_off, out)
                     if pass_idx in self.gate_ts:
-                        self.k.gate(self.gate_ts[pass_idx], [rec], ndocs, flags, dead, pass_idx + 1, 0)
+                        self.k.gate(self.gate_ts[pass_idx], [rec], ndocs, flags, dead, pass_idx + 1, 0,
+                                        self.gate_need[pass_idx])
                     ev = self._record(slot.s_c4)
                 pass_idx += 1
                 versions[ver + 1] = (out, new_off, cap)
@@ -698,6 +746,8 @@ class DeviceRunner:
             r_off = rt.zeros(ndocs + 1, np.int64)
             r_rows = rt.empty(ndocs, np.int32)
             r_err = rt.zeros(1, np.int32)
+            if any(r.numel() < need * ndocs for r, need in zip(recs, self.resolve_need)):
+                raise DeviceError("resolve: a record buffer is smaller than the resolve plan reads")
             with self._ktimed(keep, "resolve"):
                 self.k.resolve(self.resolve_t, recs, ndocs, flags.view(np.uint32), vlist, r_fail, r_status, r_ver,
                                r_lanes, r_sc, r_out, r_off, r_rows, r_err)
@@ -741,6 +791,20 @@ class DeviceRunner:
         return self.submit(data, off).wait()
 
 
+def _dict_script_flags(data: np.ndarray, off: np.ndarray) -> np.ndarray:
+    """DOC_NEEDS_CPU (1) for documents with a dictionary-script code point (host twin of the check
+    in k_langid_features); only documents with a byte >= 0xE0 are decoded."""
+    h = native.host()
+    n = len(off) - 1
+    out = np.zeros(n, dtype=np.uint32)
+    hi = np.nonzero(data >= 0xE0)[0]
+    if len(hi):
+        for d in np.unique(np.searchsorted(off, hi, side="right") - 1).tolist():
+            if 0 <= d < n and h.has_dict_script(bytes(data[off[d]:off[d + 1]]).decode("utf-8", "replace")):
+                out[d] = 1
+    return out
+
+
 class EmulatedRunner:
     """Host emulation of :class:`DeviceRunner` (same records, versions and flags, computed by the
     C++ port of the device algorithms). Drives the exact resolve path of the GPU backend on a
@@ -760,7 +824,8 @@ class EmulatedRunner:
         self.stage_layout = [h.stage_layout(b) for b in stage_bs]
         if gating is None:
             gating = os.environ.get("TB_GATE", "1") not in ("", "0")
-        self.passes, self.pass_of_step, self.gates = plan_passes(plan, self.stage_layout, steps_native, gating)
+        self.passes, self.pass_of_step, self.gates = plan_passes(
+            plan, self.stage_layout, steps_native, gating, os.environ.get("TB_LID_GATE", "1") not in ("", "0"))
         # test hook: additionally mark every k-th document dead after the first pass (a wrong
         # device gate), to exercise the resolver's recovery path
         self.gate_corrupt = gate_corrupt
@@ -779,11 +844,23 @@ class EmulatedRunner:
         stage_recs: List[Optional[np.ndarray]] = [None] * len(self.plan.stages)
         c4_recs = {}
         dead = np.zeros(ndocs, dtype=np.uint8) if self.gates else None
+        lid_rec = {}
         for p, (kind, x) in enumerate(self.passes):
             skip = dead if p > 0 else None
-            if kind == "stage":
+            if kind == "lid":
+                # the whole stage once (the language-id columns are what this pass produces; the
+                # other columns are recomputed below for the documents the gate leaves alive)
                 vd, vo = versions[self.plan.stage_version[x]]
                 rec, fl = h.emulate_stage(self.steps, self.plan.stages[x], vd, vo, self.nthreads, self.lid, 0, skip)
+                lid_rec[x] = rec
+                fl = _dict_script_flags(vd, vo)  # k_langid_features raises DOC_NEEDS_CPU for these
+            elif kind == "stage":
+                vd, vo = versions[self.plan.stage_version[x]]
+                rec, fl = h.emulate_stage(self.steps, self.plan.stages[x], vd, vo, self.nthreads, self.lid, 0, skip)
+                if x in lid_rec:
+                    for k, width, prefix in self.stage_layout[x][1]:
+                        if k == KIND_LANGID:
+                            rec[prefix * ndocs:(prefix + width) * ndocs] = lid_rec[x][prefix * ndocs:(prefix + width) * ndocs]
                 stage_recs[x] = rec
             else:
                 vd, vo = versions[self.plan.steps[x].version_in]
@@ -792,7 +869,7 @@ class EmulatedRunner:
                 versions[self.plan.steps[x].version_out] = (nd, no)
             flags |= fl
             if p in self.gates:
-                h.gate_host(self.gates[p], [rec], ndocs, flags, dead, p + 1)
+                h.gate_host(self.gates[p][0], [rec], ndocs, flags, dead, p + 1)
                 if p == 0 and self.gate_corrupt > 0:
                     extra = np.arange(0, ndocs, self.gate_corrupt)
                     dead[extra[dead[extra] == 0]] = 1

@@ -158,8 +158,11 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_stage_analyze_blk
 // position; then, for each gram slot, 4 lanes share one row: lane (4*src + q) loads 16 bytes
 // (dims 8q..8q+7) of the row of lane j*16+src's gram, so an instruction covers 16 whole rows
 // (16 lines instead of 64) and each lane keeps 8 accumulators instead of 33.
+// embx (optional): the embedding table pre-converted to the fixed-point sums' int32 values
+// (lid_fixed of every entry, 128-byte rows): a gather is two 16-byte loads and no conversions.
 __device__ __forceinline__ void langid_features_coop(DocCtx<WavePar>& x, const uint8_t* b, uint32_t n,
-                                                     const uint16_t* __restrict__ emb, uint16_t* vec,
+                                                     const uint16_t* __restrict__ emb,
+                                                     const int32_t* __restrict__ embx, uint16_t* vec,
                                                      int32_t* cnt_out) {
   const UcdView ucd = x.ucd;
   const auto mark = x.mark();
@@ -213,7 +216,12 @@ __device__ __forceinline__ void langid_features_coop(DocCtx<WavePar>& x, const u
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int32_t bk = __shfl(g[slot], j * 16 + (int)src);
-        if (bk >= 0) {
+        if (bk >= 0 && embx) {
+          const int4* r = (const int4*)(embx + (size_t)bk * kLidDim + q * 8u);
+          const int4 a = r[0], c = r[1];
+          part[0] += a.x; part[1] += a.y; part[2] += a.z; part[3] += a.w;
+          part[4] += c.x; part[5] += c.y; part[6] += c.z; part[7] += c.w;
+        } else if (bk >= 0) {
           const uint4 w = *(const uint4*)(emb + (size_t)bk * kLidDim + q * 8u);
           const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
@@ -250,15 +258,15 @@ __device__ __forceinline__ void langid_features_coop(DocCtx<WavePar>& x, const u
 __global__ __launch_bounds__(64) void k_langid_features(
     const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off, const int32_t* __restrict__ perm,
     int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off, DevTables tabs,
-    const uint16_t* __restrict__ emb, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t* flags, uint32_t lds_bytes,
-    uint64_t* prof) {
+    const uint16_t* __restrict__ emb, const int32_t* __restrict__ embx, uint16_t* lid_vec, int32_t* lid_cnt,
+    uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
   const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
   if (doc >= ndocs) return;
   DocCtx<WavePar> x = make_ctx(tabs, nullptr, 0, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   x.stamp(PH_START);
-  langid_features_coop(x, b, n, emb, lid_vec + (size_t)doc * kLidDim, lid_cnt + doc);
+  langid_features_coop(x, b, n, emb, embx, lid_vec + (size_t)doc * kLidDim, lid_cnt + doc);
   // Documents with dictionary-segmented scripts go to the CPU path (the stage kernel's decode
   // flags them too). With the language-id gate in front of the stage (device.py plan_passes) the
   // stage kernel never sees a document this pass filters, so the flag is raised here as well:
@@ -628,7 +636,8 @@ int tb_badwords_match(hipStream_t stream, const uint8_t* bytes, const int64_t* o
 int tb_langid_features(hipStream_t stream, const uint8_t* bytes, const int64_t* off, const int32_t* perm,
                        int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint16_t* s1,
                        const uint32_t* s2, const uint16_t* l1, const int32_t* l2, const uint16_t* emb,
-                       uint16_t* lid_vec, int32_t* lid_cnt, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
+                       const int32_t* embx, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t* flags, uint32_t lds_bytes,
+                       uint64_t* prof) {
   if (ndocs <= 0) return 0;
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
@@ -636,7 +645,7 @@ int tb_langid_features(hipStream_t stream, const uint8_t* bytes, const int64_t* 
     (void)hipFuncSetAttribute((const void*)k_langid_features, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds_bytes);
   hipLaunchKernelGGL(k_langid_features, dim3(ndocs), dim3(64), lds_bytes, stream, bytes, off, perm, ndocs, scratch,
-                     scratch_off, t, emb, lid_vec, lid_cnt, flags, lds_bytes, prof);
+                     scratch_off, t, emb, embx, lid_vec, lid_cnt, flags, lds_bytes, prof);
   return (int)hipGetLastError();
 }
 
@@ -724,7 +733,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 
 int tb_phase_slots() { return kPhaseSlots; }
 
-int tb_abi_version() { return 3; }
+int tb_abi_version() { return 4; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

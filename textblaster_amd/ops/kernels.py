@@ -20,6 +20,10 @@ _U32 = ctypes.c_uint32
 _I64 = ctypes.c_int64
 _SZ = ctypes.c_size_t
 
+# Bumped with every change of an entry point's signature in the table below: a stale
+# libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
+ABI_VERSION = 4
+
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32,
                          _P],
@@ -33,7 +37,7 @@ _SIGS = {
     "tb_sizeof_resolve": [],
     "tb_block_threads": [],
     "tb_badwords_match": [_P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
-    "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
+    "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
     "tb_c4_pass_b": [_P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "tb_langid_head": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I32, _P],
     "tb_pow_table": [_P, _P, _U32],
@@ -83,6 +87,8 @@ class Kernels:
         self.device = device
         self.lib = native.hip()
         h = native.host()
+        if self.lib.tb_abi_version() != ABI_VERSION:
+            raise DeviceError(f"libtbhip.so ABI {self.lib.tb_abi_version()} != {ABI_VERSION}; rebuild")
         if (self.lib.tb_sizeof_plan() != h.SIZEOF_DEV_PLAN or self.lib.tb_sizeof_stage() != h.SIZEOF_DEV_STAGE
                 or self.lib.tb_sizeof_gate() != h.SIZEOF_DEV_GATE
                 or self.lib.tb_sizeof_resolve() != h.SIZEOF_DEV_RESOLVE):
@@ -151,12 +157,15 @@ class Kernels:
         _check(rc, "tb_badwords_match")
 
     def langid_features(self, bytes_, off, perm, ndocs, scratch, scratch_off, emb, vec, cnt, flags, lds_bytes=0,
-                        prof=None):
+                        prof=None, embx=None):
+        """k_langid_features; ``embx``: optional int32 fixed-point copy of ``emb`` (same shape)."""
         t = self.tabs
+        if embx is not None and embx.numel() != emb.numel():
+            raise DeviceError("langid_features: fixed-point table shape")
         rc = self.lib.tb_langid_features(
             self.stream(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs, scratch.data_ptr(),
             scratch_off.data_ptr(), t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), emb.data_ptr(),
-            vec.data_ptr(), cnt.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof))
+            _ptr(embx), vec.data_ptr(), cnt.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof))
         _check(rc, "tb_langid_features")
 
     def c4_pass_a(self, c4, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags, lds_bytes=0,

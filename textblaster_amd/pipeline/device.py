@@ -334,10 +334,17 @@ class DeviceRunner:
             self.c4_ts = {i: self._to_dev(h.build_c4(steps_native[i])) for i in plan.c4_steps}
             self.has_lid = any(steps_native[i].kind == h.StepKind.LanguageDetection
                                for st in plan.stages for i in st)
+            self.lid_embx = None
             if self.has_lid:
                 if langid is None:
                     raise DeviceError("LanguageDetectionFilter needs a language-id model")
                 self.lid_emb = hiprt.to_device(langid.emb)
+                # the same table as the bag's int32 fixed-point terms (lid_fixed: rint(e * 2^16),
+                # exact in float32), so the gathers need no conversion; TB_LID_FIXED=0: bf16 path
+                self.lid_embx = None
+                if os.environ.get("TB_LID_FIXED", "1") not in ("", "0"):
+                    e = (np.ascontiguousarray(langid.emb, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
+                    self.lid_embx = hiprt.to_device(np.rint(e * np.float32(65536.0)).astype(np.int32))
                 wT = np.ascontiguousarray(langid.w.reshape(h.LID_DIM, h.LID_LANGS_PAD).T)  # [16][32]
                 self.lid_wT = hiprt.to_device(wT)
                 self.lid_b = hiprt.to_device(langid.b.astype(np.float32))
@@ -619,7 +626,7 @@ class DeviceRunner:
                         with self._ktimed(keep, "langid_features"):
                             self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec,
                                                    lid_cnt, flags, self.lds_bytes_lid,
-                                                   self._prof_buf(ndocs, keep, f"langid{s}"))
+                                                   self._prof_buf(ndocs, keep, f"langid{s}"), self.lid_embx)
                         for kind, width, prefix in layout:
                             if kind == KIND_LANGID:
                                 self.k.langid_head(lid_vec, lid_cnt, self.lid_wT, self.lid_b, ndocs, rec, prefix * ndocs,
@@ -647,7 +654,7 @@ class DeviceRunner:
                     with rt.stream(slot.s_lid), self._ktimed(keep, "langid_features"):
                         self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec,
                                                lid_cnt, flags, self.lds_bytes_lid,
-                                               self._prof_buf(ndocs, keep, f"langid{s}"))
+                                               self._prof_buf(ndocs, keep, f"langid{s}"), self.lid_embx)
                         ev_lid = self._record(slot.s_lid)
                         keep.append(ev_lid)
                 if n_mid > n_long:

@@ -1000,6 +1000,11 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
 // device (k_langid_features) and inside the stage emulation on the host.
 TB_HD uint32_t lid_letter(const UcdView& ucd, const uint8_t* b, uint32_t n, int64_t s) {
   if (s < 0) return 0;
+  const uint32_t c0 = b[s];
+  if (c0 < 0x80u) {  // ASCII: alphabetic = A-Z / a-z, lowercase = c | 0x20 (no table lookups)
+    const uint32_t l = c0 | 0x20u;
+    return (l >= 'a' && l <= 'z') ? l : 0u;
+  }
   int len;
   const uint32_t c = utf8_decode(b, (uint32_t)s, n, &len);
   if (!(ucd.props(c) & P_ALPHA)) return 0;

@@ -38,6 +38,15 @@ template <class A>
 TB_HD bool wb_break(const A& a, int n, int i) {
   const uint32_t pp = a.p(i - 1), pc = a.p(i);
   const int cp = wb_of(pp), cc = wb_of(pc);
+  // The common pairs of running text, decided without look-around: neither side is a newline,
+  // ZWJ or ignorable, so the effective left context is cp itself; ALetter x ALetter is WB5,
+  // ALetter / WSegSpace in either order matches no rule before WB999 (break).
+  if (cp == WB_ALetter) {
+    if (cc == WB_ALetter) return false;
+    if (cc == WB_WSegSpace) return true;
+  } else if (cp == WB_WSegSpace && cc == WB_ALetter) {
+    return true;
+  }
   if (cp == WB_CR && cc == WB_LF) return false;            // WB3
   if (wb_nl(cp)) return true;                              // WB3a
   if (wb_nl(cc)) return true;                              // WB3b

@@ -187,7 +187,9 @@ def test_two_ranks_gloo(corpus, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     assert "Documents Read: 3000" in r.stdout
     assert pq.read_table(out).equals(o0) and pq.read_table(exc).equals(e0)
-    assert os.path.exists(tmp_path / "log" / "producer.rank1.log")
+    import glob
+
+    assert glob.glob(str(tmp_path / "log" / "producer.rank1.log.*-*-*"))
 
 
 # ---- CLI --------------------------------------------------------------------------------------
@@ -235,7 +237,10 @@ def test_cli_run_and_worker(tmp_path, capsys):
                    str(tmp_path / "log")])
     assert rc == 0
     assert "Kept (output): 2" in capsys.readouterr().out
-    lines = [json.loads(l) for l in open(tmp_path / "log" / "producer.log")]
+    import glob
+
+    (logf,) = glob.glob(str(tmp_path / "log" / "producer.log.*-*-*"))  # daily file (reference layout)
+    lines = [json.loads(l) for l in open(logf)]
     assert lines and {"timestamp", "level", "fields", "target"} <= set(lines[0])
     # worker: task JSON lines in, outcome JSON lines out (reference message formats)
     tasks = "".join(d.to_json().decode() + "\n" for d in e2e_docs()) + "not json\n"
@@ -276,3 +281,20 @@ def test_html_decode_backend_is_validated(tmp_path):
     with _pytest.raises(PipelineError):
         _run(_RC(inp, str(tmp_path / "o.parquet"), str(tmp_path / "e.parquet"), cfg, backend="cpu",
                  html_decode="bogus"))
+
+
+def test_daily_log_handler_rolls_over(tmp_path):
+    """Reference tracing_appender::rolling::daily: one file per date, <name>.log.<YYYY-MM-DD>."""
+    import logging
+
+    day = ["2026-10-16"]
+    h = cli.DailyFileHandler(str(tmp_path), "producer", today=lambda: day[0])
+    h.setFormatter(logging.Formatter("%(message)s"))
+    rec = lambda m: logging.LogRecord("t", logging.INFO, __file__, 1, m, None, None)  # noqa: E731
+    h.emit(rec("a"))
+    day[0] = "2026-10-17"
+    h.emit(rec("b"))
+    h.emit(rec("c"))
+    h.close()
+    assert open(tmp_path / "producer.log.2026-10-16").read() == "a\n"
+    assert open(tmp_path / "producer.log.2026-10-17").read() == "b\nc\n"

@@ -39,9 +39,47 @@ class _JsonFormatter(logging.Formatter):
         })
 
 
+class DailyFileHandler(logging.Handler):
+    """JSON log lines into ``<dir>/<name>.log.<YYYY-MM-DD>`` (local date), switching files when
+    the date changes — the file layout of the reference's tracing_appender::rolling::daily
+    (bin/producer.rs:57-83)."""
+
+    def __init__(self, log_dir: str, name: str, today=None):
+        super().__init__()
+        import datetime
+
+        self.dir, self.name = log_dir, name
+        self._today = today or (lambda: datetime.date.today().isoformat())
+        self._date = None
+        self._fh = None
+
+    def path_for(self, date: str) -> str:
+        return os.path.join(self.dir, f"{self.name}.log.{date}")
+
+    def emit(self, record: logging.LogRecord) -> None:
+        try:
+            d = self._today()
+            if d != self._date or self._fh is None:
+                if self._fh is not None:
+                    self._fh.close()
+                self._fh = open(self.path_for(d), "a", encoding="utf-8")
+                self._date = d
+            self._fh.write(self.format(record) + "\n")
+            self._fh.flush()
+        except Exception:  # noqa: BLE001 - logging must never raise
+            self.handleError(record)
+
+    def close(self) -> None:
+        if self._fh is not None:
+            self._fh.close()
+            self._fh = None
+        super().close()
+
+
 def setup_logging(log_dir: Optional[str], name: str, console_level: str = "WARNING") -> None:
-    """Console at WARNING, JSON lines at INFO (or $TB_LOG) into ``<log_dir>/<name>.log``
-    (reference: tracing console=warn, daily JSON file ./log/<name>.log)."""
+    """Console at WARNING, JSON lines at INFO (or $TB_LOG) into daily files
+    ``<log_dir>/<name>.log.<YYYY-MM-DD>`` (reference: tracing console=warn, daily rolling JSON
+    file ./log/<name>.log)."""
     root = logging.getLogger()
     root.handlers.clear()
     level = (os.environ.get("TB_LOG") or os.environ.get("RUST_LOG") or "INFO").upper()
@@ -53,7 +91,7 @@ def setup_logging(log_dir: Optional[str], name: str, console_level: str = "WARNI
     if log_dir:
         try:
             os.makedirs(log_dir, exist_ok=True)
-            fh = logging.FileHandler(os.path.join(log_dir, f"{name}.log"), encoding="utf-8")
+            fh = DailyFileHandler(log_dir, name)
             fh.setFormatter(_JsonFormatter())
             root.addHandler(fh)
         except OSError as e:

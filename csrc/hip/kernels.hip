@@ -123,8 +123,15 @@ TB_STAGE_KERNEL(k_stage_analyze_w6, __attribute__((amdgpu_waves_per_eu(6, 8))))
 #define TB_BLOCK_THREADS 512
 #endif
 constexpr int kBlockThreads = TB_BLOCK_THREADS;
-// TB_BLK_WPE=k: force a k-waves-per-SIMD register budget on the long-document kernels (A/B builds)
-#ifdef TB_BLK_WPE
+// Register budget of the long-document stage kernel: 6 waves per SIMD (<= 80 VGPRs), so with the
+// default 48 KB LDS slice three 512-thread workgroups (three documents) share a CU instead of one
+// (174 VGPRs unconstrained). The kernel is latency-bound; config 5 (4096 x 50 KB documents,
+// profiles/r2_c5/blk_variants.txt): 70.9K docs/s unconstrained/64 KB, 110.0K at 4 waves/64 KB,
+// 113.7K at 6 waves/48 KB. TB_BLK_WPE=k builds another budget (0: none) for A/B runs.
+#ifndef TB_BLK_WPE
+#define TB_BLK_WPE 6
+#endif
+#if TB_BLK_WPE > 0
 #define TB_BLK_ATTR __attribute__((amdgpu_waves_per_eu(TB_BLK_WPE, 8)))
 #else
 #define TB_BLK_ATTR

@@ -248,6 +248,7 @@ class DeviceRunner:
     DEFAULT_LONG_DOC_BYTES = 8192
     DEFAULT_MID_DOC_BYTES = 0        # 0: no separate mid-size launch
     DEFAULT_LDS_BYTES_MID = 32768
+    DEFAULT_LDS_BYTES_BLK = 49152
     DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; sweep: tools/occ_sweep.sh)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None):
@@ -383,7 +384,9 @@ class DeviceRunner:
         self.lds_bytes_mid = int(os.environ.get("TB_LDS_BYTES_MID", str(self.DEFAULT_LDS_BYTES_MID)))
         if not 0 <= self.lds_bytes_mid <= 131072 or not 0 <= self.lds_bytes <= 131072:
             raise DeviceError("TB_LDS_BYTES / TB_LDS_BYTES_MID must be in [0, 131072]")
-        self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", "65536"))
+        # 48 KB: three long-document workgroups per CU (with the 6-wave register budget of
+        # k_stage_analyze_blk, csrc/hip/kernels.hip TB_BLK_WPE)
+        self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", str(self.DEFAULT_LDS_BYTES_BLK)))
         if not 0 <= self.lds_bytes_blk <= 131072:
             # the workgroup kernels also hold static LDS (cross-wave exchange buffers): a 160 KB
             # dynamic slice does not fit the CU's 160 KB and the launch fails with

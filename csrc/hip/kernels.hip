@@ -515,20 +515,28 @@ __global__ __launch_bounds__(256) void k_resolve(const DevResolve* __restrict__ 
   l[3] = st == kResolveFiltered ? 1 : 0;
 }
 
-// K16 compaction: one wave per document copies its final content into the output buffer — kept
-// documents first, then excluded ones, each group in document order (the order the host path
-// produces) — and writes its output row and start offset. sc = the four inclusive scans
-// [kept bytes | excluded bytes | kept count | excluded count], n entries each.
-__global__ __launch_bounds__(64) void k_compact(const uint8_t* __restrict__ status, const uint8_t* __restrict__ fver,
-                                                VersionTab vt, int32_t ndocs, const int64_t* __restrict__ sc,
-                                                uint8_t* __restrict__ out, int64_t cap, int64_t* __restrict__ out_off,
-                                                int32_t* __restrict__ rows, int32_t* __restrict__ err) {
+// K16 compaction: one 256-thread workgroup per document copies its final content into the output
+// buffer — kept documents first, then excluded ones, each group in document order (the order the
+// host path produces) — and writes its output row and start offset. sc = the four inclusive scans
+// [kept bytes | excluded bytes | kept count | excluded count], n entries each. The copy works in
+// destination-aligned dwords: each thread loads the two source dwords that cover its destination
+// dword and funnel-shifts them together (v_alignbyte), so interior bytes move 4 at a time whatever
+// the relative alignment; only the partial first and last destination dwords go byte by byte.
+// Source reads may run up to 3 bytes past a document (the batch and version buffers are padded).
+constexpr int kCompactThreads = 256;
+
+__global__ __launch_bounds__(kCompactThreads) void k_compact(const uint8_t* __restrict__ status,
+                                                             const uint8_t* __restrict__ fver, VersionTab vt,
+                                                             int32_t ndocs, const int64_t* __restrict__ sc,
+                                                             uint8_t* __restrict__ out, int64_t cap,
+                                                             int64_t* __restrict__ out_off, int32_t* __restrict__ rows,
+                                                             int32_t* __restrict__ err) {
   const int doc = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int t = threadIdx.x;
   if (doc >= ndocs) return;
   const int64_t n = ndocs;
   const int64_t nk = sc[3 * n - 1], nx = sc[4 * n - 1], kb = sc[n - 1], xb = sc[2 * n - 1];
-  if (doc == 0 && lane == 0) out_off[nk + nx] = kb + xb;
+  if (doc == 0 && t == 0) out_off[nk + nx] = kb + xb;
   const uint8_t st = status[doc];
   if (st != kResolveKept && st != kResolveFiltered) return;
   const int v = fver[doc];
@@ -542,16 +550,37 @@ __global__ __launch_bounds__(64) void k_compact(const uint8_t* __restrict__ stat
     boff = kb + sc[n + doc] - len;
   }
   if (boff < 0 || len < 0 || boff + len > cap) {  // never with the C4 growth bound; checked anyway
-    if (lane == 0) *err = 1;
+    if (t == 0) *err = 1;
     return;
   }
-  if (lane == 0) {
+  if (t == 0) {
     out_off[pos] = boff;
     rows[pos] = doc;
   }
-  const uint8_t* from = vt.b[v] + s0;
-  uint8_t* to = out + boff;
-  for (int64_t i = lane; i < len; i += 64) to[i] = from[i];
+  if (len == 0) return;
+  const uint8_t* src = vt.b[v] + s0;
+  uint8_t* dst = out + boff;
+  // destination dwords fully inside [boff, boff + len): [a0, a1) in dword units of `out`
+  const int64_t a0 = (boff + 3) >> 2, a1 = (boff + len) >> 2;
+  if (a1 <= a0) {  // short: no whole destination dword
+    for (int64_t i = t; i < len; i += kCompactThreads) dst[i] = src[i];
+    return;
+  }
+  const int64_t head = a0 * 4 - boff, tail = boff + len - a1 * 4;  // bytes before / after
+  if (t < head) dst[t] = src[t];
+  if (t < tail) dst[len - tail + t] = src[len - tail + t];
+  // destination dword w (absolute) takes source bytes from sp = src + (4w - boff)
+  const uintptr_t sbase = (uintptr_t)src + (uintptr_t)head;  // source of the first whole dword
+  const uint32_t sh = (uint32_t)(sbase & 3u);
+  const uint32_t* s32 = (const uint32_t*)(sbase - sh);
+  uint32_t* d32 = (uint32_t*)out + a0;
+  const int64_t nw = a1 - a0;
+  for (int64_t k = t; k < nw; k += kCompactThreads) {
+    const uint32_t lo = s32[k];
+    const uint32_t hi = sh ? s32[k + 1] : 0u;
+    // little endian: bytes sh.. of lo, then the low bytes of hi
+    d32[k] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+  }
 }
 
 __global__ void k_pow_table(uint64_t* pw, uint32_t n) {
@@ -725,7 +754,7 @@ int tb_resolve(hipStream_t stream, const void* rp, const int64_t* const* recs, i
     const int rc = tb_scan_strided_i64(stream, lanes + j, 4, ndocs, sc + (int64_t)j * ndocs);
     if (rc) return rc;
   }
-  hipLaunchKernelGGL(k_compact, dim3(ndocs), dim3(64), 0, stream, status, fver, vt, ndocs, sc, out, cap, out_off, rows,
+  hipLaunchKernelGGL(k_compact, dim3(ndocs), dim3(kCompactThreads), 0, stream, status, fver, vt, ndocs, sc, out, cap, out_off, rows,
                      err);
   return (int)hipGetLastError();
 }

@@ -280,6 +280,8 @@ class DeviceRunner:
         self.stream_layout = "serial" if serial else os.environ.get("TB_STREAMS", "6")
         if self.stream_layout not in ("serial", "4", "4c", "4f", "5", "6", "13"):
             raise DeviceError("TB_STREAMS must be one of 4, 4c, 4f, 5, 6, 13")
+        # TB_SLOTS: batches in flight on the device (A/B; each slot holds its own scratch arena)
+        self.N_SLOTS = max(1, int(os.environ.get("TB_SLOTS", str(self.N_SLOTS))))
         self.slots = [_Slot() for _ in range(self.N_SLOTS)]
         if self.stream_layout == "serial":
             one = hiprt.Stream()

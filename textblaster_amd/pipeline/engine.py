@@ -212,7 +212,9 @@ class Engine:
         import queue
         import threading
 
-        q: "queue.Queue" = queue.Queue(maxsize=1)
+        # submitted batches waiting for the consumer: one fewer than the device's batch slots
+        depth = max(1, getattr(self.device_runner, "N_SLOTS", 2) - 1)
+        q: "queue.Queue" = queue.Queue(maxsize=depth)
         stop = threading.Event()
         _END = object()
 

@@ -245,7 +245,7 @@ class DeviceRunner:
     # 10 KB each costs no occupancy; the C4 kernel (7 waves/SIMD) only keeps per-line arrays there
     DEFAULT_LDS_BYTES = 10240
     DEFAULT_LDS_BYTES_C4 = 2560
-    DEFAULT_LONG_DOC_BYTES = 8192
+    DEFAULT_LONG_DOC_BYTES = 4096  # with the 3-per-CU workgroup kernel (profiles/r2_c5/long_doc_threshold.txt)
     DEFAULT_MID_DOC_BYTES = 0        # 0: no separate mid-size launch
     DEFAULT_LDS_BYTES_MID = 32768
     DEFAULT_LDS_BYTES_BLK = 49152

@@ -676,13 +676,103 @@ TB_HD bool ci_contains(const uint8_t* b, uint32_t n, const char* pat, int plen) 
   return false;
 }
 
+// SURVEY 5.7 intra-document split (documents over TB_SPLIT_DOC_BYTES): the stage workgroup
+// computes everything except the duplicated n-gram orders and exports the per-word arrays those
+// need (all in the document's HBM scratch slice); then one workgroup per (document, order) —
+// k_gr_dup_split — canonicalises its order, marks repeats and runs its greedy walk, in parallel.
+struct GrExport {
+  const uint32_t* wid;   // canonical word ids
+  const uint32_t* WL;    // byte prefix of word lengths
+  const uint64_t* K;     // concatenation hash prefixes (see gopher_rep_record)
+  const uint64_t* PB;    // B^WL
+  const uint32_t* bs;    // word byte starts / ends
+  const uint32_t* be;
+  const uint8_t* b;      // document bytes
+  char* free_base;       // unused rest of the document's scratch slice
+  uint64_t free_cap;
+  uint32_t W;
+  uint32_t valid;        // 1: exported (0: the document returned early / was skipped)
+};
+
 struct StageOut {
   int64_t* rec;     // record buffer (all steps of the stage)
   uint32_t ndocs;
   uint32_t doc;
   uint16_t* lid_vec;  // [ndocs][kLidDim] doc vectors (bf16) for the MFMA head
   int32_t* lid_cnt;   // [ndocs] n-gram counts (0 = nothing to detect)
+  GrExport* gr_export = nullptr;  // non-null: split mode for this document (see GrExport)
 };
+
+// The duplicated n-gram key / equality of order n over the exported word arrays (one definition
+// for the in-stage path and the split kernel): grams are equal iff their concatenations are.
+struct DupGrams {
+  const uint32_t* wid;
+  const uint32_t* WL;
+  const uint64_t* K;
+  const uint64_t* PB;
+  const uint32_t* bs;
+  const uint32_t* be;
+  const uint8_t* b;
+  TB_HD uint64_t run_hash(uint32_t p, uint32_t n) const {
+    const uint64_t d = K[p + n] >= K[p] ? K[p + n] - K[p] : K[p + n] + kM61 - K[p];
+    return mulmod61(PB[p + n], d);
+  }
+  TB_HD uint64_t key(uint32_t p, uint32_t n) const { return dev_key(run_hash(p, n), WL[p + n] - WL[p]); }
+  TB_HD bool eq(uint32_t p, uint32_t q, uint32_t n) const {
+    if (WL[p + n] - WL[p] != WL[q + n] - WL[q]) return false;
+    // same canonical word sequence => same concatenation (the common case); only different word
+    // splits of equal-hash text need the byte comparison. All n id pairs are loaded before the
+    // compare (no early exit), so the loads overlap instead of forming a dependent chain.
+    uint32_t dw = 0;
+#pragma unroll 5
+    for (uint32_t k = 0; k < n; ++k) dw |= wid[p + k] ^ wid[q + k];
+    if (dw == 0) return true;
+    uint32_t wp = p, wq = q, bp = bs[p], bq = bs[q];
+    const uint32_t L = WL[p + n] - WL[p];
+    for (uint32_t i = 0; i < L; ++i) {
+      while (bp == be[wp]) { ++wp; bp = bs[wp]; }
+      while (bq == be[wq]) { ++wq; bq = bs[wq]; }
+      if (b[bp] != b[bq]) return false;
+      ++bp;
+      ++bq;
+    }
+    return true;
+  }
+};
+
+// Greedy duplicated-n-gram walk of one order (reference find_all_duplicate, utils/text.rs:
+// 241-259) over canonical gram ids gc[0, G), repeat bitmap R (bit p: gram p occurs more than
+// once) and the seen-bitmap sn (zeroed): bytes of the repeated grams the walk counts. A walk only
+// stops at repeated grams; at a gram that occurs once it would mark an id nobody else has and
+// advance by one, so it jumps from one set bit of R to the next.
+TB_HD int64_t dup_walk(uint32_t G, uint32_t n, const uint32_t* gc, const uint32_t* R, uint32_t* sn,
+                       const uint32_t* WL) {
+  const uint32_t nw = (G + 31) >> 5;
+  auto next_rep = [&](uint32_t from) -> uint32_t {  // first repeated position >= from, or G
+    if (from >= G) return G;
+    uint32_t wi = from >> 5;
+    uint32_t bw = R[wi] & (~0u << (from & 31));
+    while (!bw) {
+      if (++wi >= nw) return G;
+      bw = R[wi];
+    }
+    const uint32_t q = (wi << 5) + (uint32_t)__builtin_ctz(bw);
+    return q < G ? q : G;
+  };
+  int64_t rep = 0;
+  uint32_t idx = next_rep(0);
+  while (idx < G) {
+    const uint32_t g = gc[idx];
+    if ((sn[g >> 5] >> (g & 31)) & 1u) {
+      rep += (int64_t)(WL[idx + n] - WL[idx]);
+      idx = next_rep(idx + n);
+    } else {
+      sn[g >> 5] |= 1u << (g & 31);
+      idx = next_rep(idx + 1);
+    }
+  }
+  return rep;
+}
 
 TB_HD uint64_t span_hash(uint64_t pa, uint64_t pb, uint64_t blen_pow) {
   uint64_t x = mulmod61(pa, blen_pow);
@@ -714,7 +804,8 @@ TB_HD uint32_t count_sentences(DocCtx<P>& x, const Cps& c, uint32_t s, uint32_t 
 
 template <class P>
 TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, const Cps& c,
-                             const PHView& ph, const Words& w, int64_t* r, bool release_props = false) {
+                             const PHView& ph, const Words& w, int64_t* r, bool release_props = false,
+                             GrExport* ex = nullptr) {
   const uint32_t C = c.n;
   const PropArr prop = c.props();
   const OffArr off = c.offs();
@@ -794,11 +885,12 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
   uint64_t* PB = nullptr;
   if (ngrams) {
     // LDS only while a canonicalisation table for W elements (~6 W bytes) still fits next to them
+    // (split mode: HBM, they outlive this kernel)
     const uint64_t tab_bytes = 6ull * W + 64;
-    wid = x.template alloc_hot_keep<uint32_t>(W + 1, tab_bytes);
-    WL = x.template alloc_hot_keep<uint32_t>(W + 1, tab_bytes);
-    K = x.template alloc_hot_keep<uint64_t>(W + 1, tab_bytes);
-    PB = x.template alloc_hot_keep<uint64_t>(W + 1, tab_bytes);
+    wid = ex ? x.template alloc<uint32_t>(W + 1) : x.template alloc_hot_keep<uint32_t>(W + 1, tab_bytes);
+    WL = ex ? x.template alloc<uint32_t>(W + 1) : x.template alloc_hot_keep<uint32_t>(W + 1, tab_bytes);
+    K = ex ? x.template alloc<uint64_t>(W + 1) : x.template alloc_hot_keep<uint64_t>(W + 1, tab_bytes);
+    PB = ex ? x.template alloc<uint64_t>(W + 1) : x.template alloc_hot_keep<uint64_t>(W + 1, tab_bytes);
     const auto mw = x.mark();
     uint64_t* wh = x.template alloc_hot_hi<uint64_t>(W + 1);
     if (x.overflow) return;
@@ -826,10 +918,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
   // (code point arrays, prefix hashes) goes to their hash tables
   if (release_props) x.release_hi();
   if (ngrams) {
-    auto run_hash = [&](uint32_t p, uint32_t n) {
-      const uint64_t d = K[p + n] >= K[p] ? K[p + n] - K[p] : K[p + n] + kM61 - K[p];
-      return mulmod61(PB[p + n], d);
-    };
+    const DupGrams dg{wid, WL, K, PB, w.bs, w.be, b};
     // Top n-grams (space-joined grams: equal iff their word sequences are equal). Canonical ids
     // of the n-grams are built incrementally: the n-gram at p is the pair (id of the (n-1)-gram
     // at p, id of word p+n-1), so each order is one exact pair canonicalisation (O(1) equality,
@@ -880,7 +969,20 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       x.reset(m2);
     }
     x.stamp(PH_GR_TOP);
-    if (ds.n_dup > 0) {
+    if (ds.n_dup > 0 && ex) {
+      // split mode: export the word arrays; k_gr_dup_split finishes every order in its own
+      // workgroup and writes the duplicated n-gram fields
+      const uint64_t base = (x.used + 255) & ~255ull;
+      x.par.single([&]() {
+        for (int t = 0; t < ds.n_dup; ++t) r[rec_gr_fixed() + ds.n_top + t] = 0;
+        ex->wid = wid; ex->WL = WL; ex->K = K; ex->PB = PB; ex->bs = w.bs; ex->be = w.be; ex->b = b;
+        ex->free_base = x.scr + base;
+        ex->free_cap = x.cap > base ? x.cap - base : 0;
+        ex->W = W;
+        ex->valid = x.overflow ? 0u : 1u;
+      });
+      x.par.sync();
+    } else if (ds.n_dup > 0) {
       // Two phases over all requested orders n (reference find_all_duplicate,
       // utils/text.rs:241-259):
       //   1. per n: canonicalise the n-gram concatenations into gc_n (exact: hash groups, then
@@ -888,8 +990,6 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       //      their first occurrence gc[p]);
       //   2. the greedy walks of all orders run at once, one lane each (they are independent
       //      and sequential, so n walks cost about the longest one instead of their sum).
-      // A walk only has to stop at repeated grams: at a gram that occurs once it would mark an id
-      // no other position has and advance by one, so it jumps from one set bit of R_n to the next.
       // Arrays of all orders are packed back to back: gc_n at gbase(t), bitmaps at t * 2 * SW.
       const uint32_t SW = (W + 31) / 32 + 1;
       const int nd = ds.n_dup;
@@ -914,28 +1014,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
         uint32_t* R = bits + (uint32_t)t * 2 * SW + SW;
         gb += G;
         canonicalize(
-            x, G, [&](uint32_t p) { return dev_key(run_hash(p, n), WL[p + n] - WL[p]); },
-            [&](uint32_t p, uint32_t q) {
-              if (WL[p + n] - WL[p] != WL[q + n] - WL[q]) return false;
-              // same canonical word sequence => same concatenation (the common case); only
-              // different word splits of equal-hash text need the byte comparison
-              // all n id pairs loaded before the compare (no early exit: n <= a few dozen and
-              // the loads then overlap instead of forming a chain of dependent round trips)
-              uint32_t dw = 0;
-#pragma unroll 5
-              for (uint32_t k = 0; k < n; ++k) dw |= wid[p + k] ^ wid[q + k];
-              if (dw == 0) return true;
-              uint32_t wp = p, wq = q, bp = w.bs[p], bq = w.bs[q];
-              const uint32_t L = WL[p + n] - WL[p];
-              for (uint32_t i = 0; i < L; ++i) {
-                while (bp == w.be[wp]) { ++wp; bp = w.bs[wp]; }
-                while (bq == w.be[wq]) { ++wq; bq = w.bs[wq]; }
-                if (b[bp] != b[bq]) return false;
-                ++bp;
-                ++bq;
-              }
-              return true;
-            },
+            x, G, [&](uint32_t p) { return dg.key(p, n); }, [&](uint32_t p, uint32_t q) { return dg.eq(p, q, n); },
             gc);
         x.stamp(PH_GR_DUP_CANON);
         x.par.for_n(G, [&](uint32_t p) {
@@ -948,38 +1027,13 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
         x.par.sync();
       }
       x.par.for_n((uint32_t)nd, [&](uint32_t t) {
-        const uint32_t n = (uint32_t)ds.dup_n[t];
         const uint32_t G = gsize((int)t);
         int64_t rep = 0;
         if (G > 0) {
           uint32_t base = 0;
           for (uint32_t u = 0; u < t; ++u) base += gsize((int)u);
-          const uint32_t* gc = gcall + base;
           uint32_t* sn = bits + t * 2 * SW;
-          const uint32_t* R = sn + SW;
-          const uint32_t nw = (G + 31) >> 5;
-          auto next_rep = [&](uint32_t from) -> uint32_t {  // first repeated position >= from, or G
-            if (from >= G) return G;
-            uint32_t wi = from >> 5;
-            uint32_t bw = R[wi] & (~0u << (from & 31));
-            while (!bw) {
-              if (++wi >= nw) return G;
-              bw = R[wi];
-            }
-            const uint32_t q = (wi << 5) + (uint32_t)__builtin_ctz(bw);
-            return q < G ? q : G;
-          };
-          uint32_t idx = next_rep(0);
-          while (idx < G) {
-            const uint32_t g = gc[idx];
-            if ((sn[g >> 5] >> (g & 31)) & 1u) {
-              rep += (int64_t)(WL[idx + n] - WL[idx]);
-              idx = next_rep(idx + n);
-            } else {
-              sn[g >> 5] |= 1u << (g & 31);
-              idx = next_rep(idx + 1);
-            }
-          }
+          rep = dup_walk(G, (uint32_t)ds.dup_n[t], gcall + base, sn + SW, sn, WL);
         }
         r[rec_gr_fixed() + ds.n_top + t] = rep;
       });
@@ -989,6 +1043,41 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       x.stamp(PH_GR_DUP);
     }
   }
+  x.reset(mark);
+}
+
+// One duplicated n-gram order of a split document (k_gr_dup_split): the in-stage dup phase for
+// order t alone, over the arrays the stage workgroup exported. Writes r[7 + n_top + t].
+template <class P>
+TB_HD void gr_dup_one_order(DocCtx<P>& x, const DevStep& ds, int t, const GrExport& e, int64_t* r) {
+  const uint32_t W = e.W, n = (uint32_t)ds.dup_n[t];
+  const uint32_t G = (n == 0 || W < n) ? 0u : W - n + 1;
+  int64_t* out = r + rec_gr_fixed() + ds.n_top + t;
+  if (G == 0) {
+    x.par.single([&]() { *out = 0; });
+    return;
+  }
+  const DupGrams dg{e.wid, e.WL, e.K, e.PB, e.bs, e.be, e.b};
+  const uint32_t SW = (G + 31) / 32 + 1;
+  const auto mark = x.mark();
+  uint32_t* bits = x.template alloc_hot<uint32_t>(2 * (uint64_t)SW);  // [sn | R]
+  uint32_t* gc = x.template alloc_hot_keep<uint32_t>((uint64_t)G + 1, 6ull * G + 64);
+  if (x.overflow) return;
+  x.par.for_n(2 * SW, [&](uint32_t i) { bits[i] = 0; });
+  x.par.sync();
+  canonicalize(x, G, [&](uint32_t p) { return dg.key(p, n); }, [&](uint32_t p, uint32_t q) { return dg.eq(p, q, n); }, gc);
+  if (x.overflow) return;
+  uint32_t* R = bits + SW;
+  x.par.for_n(G, [&](uint32_t p) {
+    const uint32_t g = gc[p];
+    if (g != p) {
+      P::or32(&R[p >> 5], 1u << (p & 31));
+      P::or32(&R[g >> 5], 1u << (g & 31));
+    }
+  });
+  x.par.sync();
+  x.par.single([&]() { *out = dup_walk(G, n, gc, R, bits, e.WL); });
+  x.par.sync();
   x.reset(mark);
 }
 
@@ -1486,7 +1575,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
       x.stamp(PH_GQ);
     } else if (ds.kind == DK_GOPHER_REP) {
       ++gr_seen;
-      gopher_rep_record(x, ds, b, c, ph, w, r, kHotProps && gr_seen == n_gr);
+      gopher_rep_record(x, ds, b, c, ph, w, r, kHotProps && gr_seen == n_gr, n_gr == 1 ? out.gr_export : nullptr);
     } else if (ds.kind == DK_FINEWEB) {
       const auto mark = x.mark();
       uint32_t* nb = x.template alloc<uint32_t>(L.n + 1);

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_stage_analyze_blk
     const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,
     const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
     int64_t* rec, uint32_t* flags, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes, uint64_t* prof,
-    const uint8_t* __restrict__ dead) {
+    const uint8_t* __restrict__ dead, GrExport* gr_export, int32_t n_split, uint32_t split_bytes) {
   const int doc = perm[blockIdx.x];
   if (doc >= ndocs || (dead && dead[doc])) return;
   DocCtx<BlockPar<kBlockThreads>> x =
@@ -153,7 +153,43 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_stage_analyze_blk
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, lid_vec, lid_cnt};
+  // split documents (the first n_split launch positions, longer than split_bytes) export their
+  // word arrays; k_gr_dup_split finishes their duplicated n-gram orders
+  if (gr_export && (int)blockIdx.x < n_split && n > split_bytes) out.gr_export = gr_export + blockIdx.x;
   analyze_stage<BlockPar<kBlockThreads>, false>(x, *stage, *plan, nullptr, b, n, out);
+}
+
+// SURVEY 5.7 intra-document split: one workgroup per (split document, duplicated n-gram order).
+// Block k handles launch position k / n_dup (perm order, the stage kernel's export slot) and order
+// k % n_dup; each order works in its own 1/n_dup share of the document's unused scratch slice.
+__global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_gr_dup_split(
+    const DevStage* __restrict__ stage, int32_t gr_step, const int32_t* __restrict__ perm, int32_t n_dup,
+    int32_t ndocs, const GrExport* __restrict__ ex, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
+    int64_t* rec, uint32_t* flags, uint32_t lds_bytes) {
+  const int k = (int)blockIdx.x / n_dup, t = (int)blockIdx.x % n_dup;
+  const int doc = perm[k];
+  if (doc >= ndocs) return;
+  const GrExport e = ex[k];
+  if (!e.valid) return;  // not exported: skipped, returned early (flagged for the CPU path) or short
+  DocCtx<BlockPar<kBlockThreads>> x;
+  x.prof = nullptr;
+  x.lds = lds_bytes ? (char*)g_lds_arena : nullptr;
+  x.lcap = lds_bytes;
+  x.lused = 0;
+  x.ucd = UcdView{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
+  x.pw = pw;
+  x.pw_n = pw_n;
+  x.ipw = pw ? pw + pw_n + 1 : nullptr;
+  const uint64_t region = (e.free_cap / (uint64_t)n_dup) & ~255ull;
+  x.scr = e.free_base + (uint64_t)t * region;
+  x.cap = region;
+  x.used = 0;
+  x.flag = flags + doc;
+  x.par.xs = g_block_xs;
+  const DevStep& ds = stage->steps[gr_step];
+  int64_t* r = rec + (int64_t)ds.rec_prefix * ndocs + (int64_t)doc * ds.width;
+  gr_dup_one_order(x, ds, t, e, r);
+  if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
 }
 
 // Language-id n-gram bag, one wave per document, with cooperative row gathers.
@@ -626,18 +662,40 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
                          const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                          const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
                          uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes, uint64_t* prof,
-                         const uint8_t* dead) {
+                         const uint8_t* dead, void* gr_export, int32_t n_split, uint32_t split_bytes) {
   if (nblocks <= 0) return 0;
-  if (!perm || lds_bytes > kMaxLdsPerBlk) return (int)hipErrorInvalidValue;
+  if (!perm || lds_bytes > kMaxLdsPerBlk || n_split < 0 || n_split > nblocks) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k_stage_analyze_blk, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds_bytes);
   hipLaunchKernelGGL(k_stage_analyze_blk, dim3(nblocks), dim3(kBlockThreads), lds_bytes, stream,
                      (const DevPlan*)plan, (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw,
-                     pw_n, t, rec, flags, lid_vec, lid_cnt, lds_bytes, prof, dead);
+                     pw_n, t, rec, flags, lid_vec, lid_cnt, lds_bytes, prof, dead, (GrExport*)gr_export, n_split,
+                     split_bytes);
   return (int)hipGetLastError();
 }
+
+// gr_export: n_split descriptors written by tb_stage_analyze_blk (zeroed by the caller first);
+// gr_step: index of the GopherRepetition step in the stage, n_dup its duplicated n-gram orders.
+int tb_gr_dup_split(hipStream_t stream, const void* stage, int32_t gr_step, const int32_t* perm, int32_t n_split,
+                    int32_t n_dup, int32_t ndocs, const void* gr_export, const uint64_t* pw, uint32_t pw_n,
+                    const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
+                    uint32_t* flags, uint32_t lds_bytes) {
+  if (n_split <= 0 || n_dup <= 0) return 0;
+  if (!perm || !gr_export || gr_step < 0 || gr_step >= kMaxStageSteps || n_dup > kMaxNgramEntries ||
+      lds_bytes > kMaxLdsPerBlk)
+    return (int)hipErrorInvalidValue;
+  DevTables t{s1, s2, l1, l2};
+  if (lds_bytes > 65536)
+    (void)hipFuncSetAttribute((const void*)k_gr_dup_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  hipLaunchKernelGGL(k_gr_dup_split, dim3((uint32_t)n_split * (uint32_t)n_dup), dim3(kBlockThreads), lds_bytes, stream,
+                     (const DevStage*)stage, gr_step, perm, n_dup, ndocs, (const GrExport*)gr_export, pw, pw_n, t, rec,
+                     flags, lds_bytes);
+  return (int)hipGetLastError();
+}
+
+size_t tb_sizeof_gr_export() { return sizeof(GrExport); }
 
 int tb_c4_pass_a_blk(hipStream_t stream, const void* c4, const uint8_t* bytes, const int64_t* off,
                      const int32_t* perm, int32_t nblocks, int32_t ndocs, char* scratch, const int64_t* scratch_off,
@@ -769,7 +827,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 
 int tb_phase_slots() { return kPhaseSlots; }
 
-int tb_abi_version() { return 4; }
+int tb_abi_version() { return 5; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

@@ -241,3 +241,37 @@ def test_device_run_is_deterministic(host, corpus, runner_parts):
     for v in a.versions:
         np.testing.assert_array_equal(a.versions[v][0], b.versions[v][0])
         np.testing.assert_array_equal(a.versions[v][1], b.versions[v][1])
+
+
+def test_split_documents_match_host_emulation(host, corpus, runner_parts, monkeypatch):
+    """SURVEY 5.7 intra-document split (k_gr_dup_split: one workgroup per duplicated n-gram order)
+    with the split threshold at the long-document threshold, so every workgroup-path document of
+    the corpus (4.5-90 KB) is split: GopherRepetition records stay bit-exact against the host."""
+    from textblaster_amd.pipeline.device import KIND_GOPHER_REP, DeviceRunner
+
+    cfg, steps, plan, _, lid = runner_parts
+    monkeypatch.setenv("TB_SPLIT_DOC_BYTES", "1")  # clamped to the long-document threshold
+    runner = DeviceRunner(steps, plan, "cuda:0", lid)
+    assert runner.gr_split and runner.split_doc_bytes == runner.long_doc_bytes
+    data, off = synth.pack(corpus)
+    n = len(corpus)
+    lens = np.diff(off)
+    assert np.count_nonzero(lens > runner.split_doc_bytes) >= 20
+    res = runner.run(data, off)
+    for s, idx in enumerate(plan.stages):
+        if s not in runner.gr_split:
+            continue
+        ref, rflags = host.emulate_stage(steps, idx, np.ascontiguousarray(data), np.ascontiguousarray(off), 8,
+                                         lid.native())
+        width_total, layout = runner.stage_layout[s]
+        for (kind, width, prefix), step_i in zip(layout, idx):
+            if kind != KIND_GOPHER_REP:
+                continue
+            p = runner.pass_of_step[step_i]
+            live = ~((res.dead != 0) & (res.dead <= p)) if res.dead is not None else np.ones(n, bool)
+            ok = (res.flags == 0) & (rflags == 0) & live
+            assert np.count_nonzero(ok & (lens > runner.split_doc_bytes)) >= 10  # split docs compared
+            a = res.stage_recs[s][prefix * n:(prefix + width) * n].reshape(n, width)
+            b = ref[prefix * n:(prefix + width) * n].reshape(n, width)
+            bad = np.nonzero(~np.all(a[ok] == b[ok], axis=1))[0]
+            assert len(bad) == 0, (bad[:5], a[ok][bad[:3]], b[ok][bad[:3]])

@@ -22,14 +22,16 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32,
                          _P],
     "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _P],
     "tb_stage_analyze_blk": [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P,
-                             _U32, _P, _P],
+                             _U32, _P, _P, _P, _I32, _U32],
+    "tb_gr_dup_split": [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32],
+    "tb_sizeof_gr_export": [],
     "tb_c4_pass_a_blk": [_P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _P],
     "tb_gate": [_P, _P, _P, _I32, _I32, _P, _P, _I32],
     "tb_sizeof_gate": [],
@@ -93,6 +95,7 @@ class Kernels:
                 or self.lib.tb_sizeof_gate() != h.SIZEOF_DEV_GATE
                 or self.lib.tb_sizeof_resolve() != h.SIZEOF_DEV_RESOLVE):
             raise DeviceError("libtbhip.so and _tbhost disagree on the device plan layout; rebuild")
+        self.sizeof_gr_export = int(self.lib.tb_sizeof_gr_export())
         s1, s2, l1, l2 = h.ucd_tables()
         self.tabs = [hiprt.to_device(a) for a in (s1, s2, l1, l2)]
         self._pw = None
@@ -127,14 +130,32 @@ class Kernels:
         _check(rc, "tb_stage_analyze")
 
     def stage_analyze_blk(self, plan, stage, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n,
-                          rec, flags, lid_vec=None, lid_cnt=None, lds_bytes=0, prof=None, dead=None):
+                          rec, flags, lid_vec=None, lid_cnt=None, lds_bytes=0, prof=None, dead=None,
+                          gr_export=None, n_split=0, split_bytes=0):
+        """k_stage_analyze_blk; ``gr_export`` (zeroed, >= n_split descriptors): the first n_split
+        launch positions longer than ``split_bytes`` export their word arrays (split mode)."""
         t = self.tabs
+        if gr_export is not None and gr_export.nbytes < n_split * self.sizeof_gr_export:
+            raise DeviceError("stage_analyze_blk: export buffer too small")
+        if not 0 <= n_split <= nlong:
+            raise DeviceError("stage_analyze_blk: n_split out of range")
         rc = self.lib.tb_stage_analyze_blk(
             self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), perm_long.data_ptr(),
             nlong, ndocs, scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(),
             t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), _ptr(lid_vec),
-            _ptr(lid_cnt), lds_bytes, _ptr(prof), _ptr(dead))
+            _ptr(lid_cnt), lds_bytes, _ptr(prof), _ptr(dead), _ptr(gr_export), n_split if gr_export is not None else 0,
+            split_bytes)
         _check(rc, "tb_stage_analyze_blk")
+
+    def gr_dup_split(self, stage, gr_step, perm, n_split, n_dup, ndocs, gr_export, pw, pw_n, rec, flags, lds_bytes):
+        """k_gr_dup_split: one workgroup per (split document, duplicated n-gram order)."""
+        if gr_export.nbytes < n_split * self.sizeof_gr_export or perm.numel() < n_split:
+            raise DeviceError("gr_dup_split: operand shapes")
+        t = self.tabs
+        rc = self.lib.tb_gr_dup_split(self.stream(), stage.data_ptr(), gr_step, perm.data_ptr(), n_split, n_dup, ndocs,
+                                      gr_export.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
+                                      t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), lds_bytes)
+        _check(rc, "tb_gr_dup_split")
 
     def c4_pass_a_blk(self, c4, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags,
                       lds_bytes=0, prof=None, dead=None):

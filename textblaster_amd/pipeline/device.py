@@ -198,6 +198,7 @@ class PendingBatch:
 
 
 KIND_LANGID = 4  # DevStep kind of LanguageDetectionFilter in a stage layout (csrc/common/devplan.h)
+KIND_GOPHER_REP = 2
 
 
 def plan_passes(plan: ExecPlan, stage_layout, steps_native, gating: bool, lid_gate: bool = True):
@@ -249,6 +250,7 @@ class DeviceRunner:
     DEFAULT_MID_DOC_BYTES = 0        # 0: no separate mid-size launch
     DEFAULT_LDS_BYTES_MID = 32768
     DEFAULT_LDS_BYTES_BLK = 49152
+    DEFAULT_SPLIT_DOC_BYTES = 65536
     DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; sweep: tools/occ_sweep.sh)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None):
@@ -389,6 +391,19 @@ class DeviceRunner:
         # 48 KB: three long-document workgroups per CU (with the 6-wave register budget of
         # k_stage_analyze_blk, csrc/hip/kernels.hip TB_BLK_WPE)
         self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", str(self.DEFAULT_LDS_BYTES_BLK)))
+        # SURVEY 5.7 split: documents longer than this finish their duplicated n-gram orders in one
+        # workgroup per order (k_gr_dup_split) instead of one after another in their stage
+        # workgroup; 0 disables. Never below the long-document threshold (wave documents cannot
+        # export: their arrays may live in LDS).
+        self.split_doc_bytes = int(os.environ.get("TB_SPLIT_DOC_BYTES", str(self.DEFAULT_SPLIT_DOC_BYTES)))
+        if self.split_doc_bytes > 0:
+            self.split_doc_bytes = max(self.split_doc_bytes, self.long_doc_bytes)
+        # per stage: (position of its GopherRepetition step, number of duplicated n-gram orders)
+        self.gr_split = {}
+        for si, idx in enumerate(plan.stages):
+            grs = [k for k, (kind, _, _) in enumerate(self.stage_layout[si][1]) if kind == KIND_GOPHER_REP]
+            if len(grs) == 1 and steps_native[idx[grs[0]]].n_dup > 0:
+                self.gr_split[si] = (grs[0], steps_native[idx[grs[0]]].n_dup)
         if not 0 <= self.lds_bytes_blk <= 131072:
             # the workgroup kernels also hold static LDS (cross-wave exchange buffers): a 160 KB
             # dynamic slice does not fit the CU's 160 KB and the launch fails with
@@ -648,10 +663,22 @@ class DeviceRunner:
                 # language-id bag share the side stream, and the long-document tail must start early
                 if n_long:
                     slot.s_blk.wait_event(ev_pre)
+                    n_split, gx = 0, None
+                    if s in self.gr_split and self.split_doc_bytes > 0:
+                        # launch positions [0, n_split) hold every document over the split size
+                        huge = np.nonzero(lens[perm[:n_long]] > self.split_doc_bytes)[0]
+                        if len(huge):
+                            n_split = int(huge[-1]) + 1
+                            gx = rt.zeros(n_split * self.k.sizeof_gr_export, np.uint8)
+                            keep.append(gx)
                     with rt.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_blk"):
                         self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[:n_long], n_long,
                                                  ndocs, scratch, d_soff, pw, pw_n, rec, flags, lid_vec, lid_cnt,
-                                                 self.lds_bytes_blk, prof, skip)
+                                                 self.lds_bytes_blk, prof, skip, gx, n_split, self.split_doc_bytes)
+                        if n_split:
+                            gr_pos, n_dup = self.gr_split[s]
+                            self.k.gr_dup_split(self.stage_ts[s], gr_pos, d_perm[:n_split], n_split, n_dup, ndocs,
+                                                gx, pw, pw_n, rec, flags, self.lds_bytes_blk)
                         ev_blk = self._record(slot.s_blk)
                         keep.append(ev_blk)
                 if lid_vec is not None and not lid_pass:

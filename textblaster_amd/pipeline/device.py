@@ -669,7 +669,8 @@ class DeviceRunner:
                         huge = np.nonzero(lens[perm[:n_long]] > self.split_doc_bytes)[0]
                         if len(huge):
                             n_split = int(huge[-1]) + 1
-                            gx = rt.zeros(n_split * self.k.sizeof_gr_export, np.uint8)
+                            # zeroed on the stream of the kernels that write and read it
+                            gx = rt.zeros(n_split * self.k.sizeof_gr_export, np.uint8, slot.s_blk)
                             keep.append(gx)
                     with rt.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_blk"):
                         self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[:n_long], n_long,

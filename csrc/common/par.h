@@ -26,8 +26,10 @@
 #include "tb_common.h"
 
 // Chunks of 64 items whose loads a wave issues together in the latency-bound passes (WavePar).
+// 1 since the round-2 kernel rework: serialized stage-kernel time per 262,144-doc step (two
+// stages, tools/kernel_ab.sh) 89.1 ms at 1, 90.9 ms at 2, 93.5 ms at 4 (register pressure).
 #ifndef TB_UNROLL
-#define TB_UNROLL 2
+#define TB_UNROLL 1
 #endif
 
 namespace tb {

@@ -253,7 +253,7 @@ class DeviceRunner:
     DEFAULT_SPLIT_DOC_BYTES = 65536
     DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; sweep: tools/occ_sweep.sh)
 
-    def __init__(self, steps_native, plan: ExecPlan, device, langid=None):
+    def __init__(self, steps_native, plan: ExecPlan, device, langid=None, max_batch_bytes: int = 384 << 20):
         import os
 
         from ..ops import hiprt
@@ -282,8 +282,20 @@ class DeviceRunner:
         self.stream_layout = "serial" if serial else os.environ.get("TB_STREAMS", "6")
         if self.stream_layout not in ("serial", "4", "4c", "4f", "5", "6", "13"):
             raise DeviceError("TB_STREAMS must be one of 4, 4c, 4f, 5, 6, 13")
-        # TB_SLOTS: batches in flight on the device (A/B; each slot holds its own scratch arena)
-        self.N_SLOTS = max(1, int(os.environ.get("TB_SLOTS", str(self.N_SLOTS))))
+        # Batches in flight on the device. Each slot holds its own scratch arena (~160 B per text
+        # byte, x1.25 headroom): three slots keep the GPU fed (interleaved A/B, 20-step headline
+        # bench: 35.3 vs 38.6 ms/step, profiles/r2_slots/ab.txt) and fit 288 GB of HBM with
+        # 384 MB device batches; a smaller device gets two. TB_SLOTS overrides.
+        env_slots = os.environ.get("TB_SLOTS")
+        if env_slots:
+            self.N_SLOTS = max(1, int(env_slots))
+        else:
+            try:
+                _, total = hiprt.mem_info()
+            except Exception:  # noqa: BLE001 - no info: the conservative choice
+                total = 0
+            per_slot = int(1.25 * 160 * max_batch_bytes) + (2 << 30)  # arena + staged/output buffers
+            self.N_SLOTS = 3 if total >= 3 * per_slot + (8 << 30) else 2
         self.slots = [_Slot() for _ in range(self.N_SLOTS)]
         if self.stream_layout == "serial":
             one = hiprt.Stream()

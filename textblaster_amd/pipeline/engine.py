@@ -107,9 +107,9 @@ class Engine:
         self._submit_lock = threading.RLock()
         # process_many on the GPU backend submits from a helper thread (TB_PREFETCH_THREAD=0: off)
         self.prefetch_threads = os.environ.get("TB_PREFETCH_THREAD", "1") not in ("", "0")
-        # text bytes per device batch (scratch ~160 B per text byte per in-flight slot: 512 MB of
-        # text -> ~80 GB of HBM per slot, two slots in flight on a 288 GB MI355X)
-        self.max_batch_bytes = int(os.environ.get("TB_MAX_BATCH_BYTES", str(512 << 20)))
+        # text bytes per device batch (scratch ~160 B per text byte per in-flight slot: 384 MB of
+        # text -> ~77 GB of HBM per slot, three slots in flight on a 288 GB MI355X)
+        self.max_batch_bytes = int(os.environ.get("TB_MAX_BATCH_BYTES", str(384 << 20)))
         self.h = native.host()
         self.plan: ExecPlan = build_plan(cfg)
         self.steps = [self.h.make_step(s.native_dict()) for s in cfg.pipeline]
@@ -153,7 +153,8 @@ class Engine:
             from .device import DeviceRunner
 
             with tracing.trace_range("tb.init.device_runner"):
-                self.device_runner = DeviceRunner(self.steps, self.plan, device or "cuda", self.langid)
+                self.device_runner = DeviceRunner(self.steps, self.plan, device or "cuda", self.langid,
+                                                  max_batch_bytes=self.max_batch_bytes)
 
     # ------------------------------------------------------------------------------------------
     def process(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None,

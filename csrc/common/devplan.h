@@ -41,6 +41,17 @@ struct DevStep {
   int64_t short_line_length;
 };
 
+// Compact form of a small stop-word set for the LDS-resident kernel (copied into each wave's
+// slice): open addressing on the FNV-1a hash of the word, lite_nslots (power of two) u32 entries
+// (hash bits 16..31 << 16 | word index + 1, 0 = empty); the words are blob[off[w] .. off[w + 1]).
+constexpr int kStopLiteMaxSlots = 256;
+constexpr int kStopLiteMaxWords = 64;
+constexpr int kStopLiteMaxBlob = 1024;
+
+TB_HD uint32_t stop_lite_hash_push(uint32_t h, uint8_t v) { return (h ^ v) * 16777619u; }
+constexpr uint32_t kStopLiteHash0 = 2166136261u;
+TB_HD uint32_t stop_lite_slot(uint32_t h, uint32_t nslots) { return (h * 0x9E3779B1u) & (nslots - 1); }
+
 struct DevStopSet {
   // open-addressing table of lowercase stop words: key (0 = empty) -> word index
   uint64_t keys[kStopTableSize];
@@ -49,6 +60,8 @@ struct DevStopSet {
   int32_t n;
   int32_t max_len;  // longest entry in bytes: a word of more code points cannot match
   uint8_t blob[kStopBlobBytes];
+  int32_t lite_nslots;  // 0: the set is too large for the compact form
+  uint32_t lite_slots[kStopLiteMaxSlots];
 };
 
 struct DevC4 {
@@ -69,6 +82,11 @@ struct DevPlan {
   int32_t n_stop_sets;
   DevStopSet stops[kMaxStopSets];
 };
+
+// Per-document HBM scratch of the generic (analyze_stage / c4_pass_a) kernels:
+// kScratchPerByte * (len + 64) + 4096 bytes.
+constexpr uint64_t kScratchPerByte = 160;
+TB_HD uint64_t scratch_bytes_for_dev(uint32_t doc_len) { return kScratchPerByte * ((uint64_t)doc_len + 64) + 4096; }
 
 TB_HD uint64_t dev_key(uint64_t h, uint32_t len) {
   uint64_t x = h ^ ((uint64_t)len * 0xD6E8FEB86659FD93ull);

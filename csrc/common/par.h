@@ -92,6 +92,19 @@ struct SeqPar {
     for (uint32_t w = 0; w < nw; ++w) bits[w] = 0;
     for (uint32_t i = 0; i < n; ++i) if (pred(i)) bits[i >> 5] |= 1u << (i & 31);
   }
+  // mask_bits with the words handed to store(w, bits) (any destination address space).
+  template <class Pred, class Store>
+  void mask_store(uint32_t n, Pred&& pred, Store&& store) const {
+    const uint32_t nw = ((n + 63) / 64) * 2;
+    for (uint32_t w = 0; w < nw; ++w) {
+      uint32_t v = 0;
+      for (uint32_t j = 0; j < 32; ++j) {
+        const uint32_t i = w * 32 + j;
+        if (i < n && pred(i)) v |= 1u << j;
+      }
+      store(w, v);
+    }
+  }
   // Inclusive scan fused with a compaction: sel(i, incl) picks items given their inclusive
   // prefix, emit(i, k, incl) gets the rank k among picked items. Returns the number picked.
   template <class T, class Op, class In, class Sel, class Emit>
@@ -105,6 +118,8 @@ struct SeqPar {
     return k;
   }
   uint32_t reduce_or(uint32_t v) const { return v; }
+  template <class T>
+  T reduce_add(T v) const { return v; }
   void sync() const {}
   static uint64_t clock() { return 0; }
   template <class F>
@@ -373,6 +388,8 @@ struct WavePar {
     for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o);
     return v;
   }
+  template <class T>
+  __device__ __forceinline__ T reduce_add(T v) const { return wave_sum(v); }
   template <class Pred>
   __device__ __forceinline__ void mask_bits(uint32_t n, Pred&& pred, uint32_t* bits) const {
     for (uint32_t base = 0; base < n; base += 64 * kU) {
@@ -388,6 +405,14 @@ struct WavePar {
         const uint64_t m = __ballot(p[u]);
         if (b0 < n && lane < 2) bits[(b0 >> 5) + lane] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
       }
+    }
+  }
+  template <class Pred, class Store>
+  __device__ __forceinline__ void mask_store(uint32_t n, Pred&& pred, Store&& store) const {
+    for (uint32_t b0 = 0; b0 < n; b0 += 64) {
+      const uint32_t i = b0 + lane;
+      const uint64_t m = __ballot(i < n && pred(i));
+      if (lane < 2) store((b0 >> 5) + lane, lane ? (uint32_t)(m >> 32) : (uint32_t)m);
     }
   }
   template <class T, class Op, class In, class Sel, class Emit>
@@ -605,6 +630,10 @@ struct BlockPar {
   }
   __device__ __forceinline__ uint32_t reduce_or(uint32_t v) const {
     return block_reduce(v, [](uint32_t a, uint32_t b) { return a | b; });
+  }
+  template <class T>
+  __device__ __forceinline__ T reduce_add(T v) const {
+    return block_reduce(v, [](T a, T b) { return a + b; });
   }
   template <class Pred>
   __device__ __forceinline__ void mask_bits(uint32_t n, Pred&& pred, uint32_t* bits) const {

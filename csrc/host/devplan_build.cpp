@@ -1,6 +1,7 @@
 // Builds the POD device plan (csrc/common/devplan.h) from step configs, and runs the device
 // document algorithms (csrc/common/docproc.h) on the host with the sequential policy.
 #include "devplan_build.h"
+#include "../common/lds_stage.h"
 
 #include <algorithm>
 #include <array>
@@ -68,6 +69,18 @@ static int add_stop_set(DevPlan& plan, const std::vector<std::string>& words) {
   ss.off[uniq.size()] = pos;
   ss.n = (int32_t)uniq.size();
   for (auto& w : uniq) ss.max_len = std::max<int32_t>(ss.max_len, (int32_t)w.size());
+  if (ss.n <= kStopLiteMaxWords && pos <= kStopLiteMaxBlob) {
+    uint32_t ns = 16;
+    while (ns < 4u * (uint32_t)ss.n) ns <<= 1;
+    ss.lite_nslots = (int32_t)ns;
+    for (size_t i = 0; i < uniq.size(); ++i) {
+      uint32_t h = kStopLiteHash0;
+      for (unsigned char c : uniq[i]) h = stop_lite_hash_push(h, c);
+      uint32_t slot = stop_lite_slot(h, ns);
+      while (ss.lite_slots[slot] != 0) slot = (slot + 1) & (ns - 1);
+      ss.lite_slots[slot] = (h & 0xFFFF0000u) | (uint32_t)(i + 1);
+    }
+  }
   return plan.n_stop_sets++;
 }
 
@@ -271,7 +284,7 @@ std::vector<uint64_t> pow_table(uint32_t n) {
   return pw;
 }
 
-uint64_t scratch_bytes_for(uint32_t doc_len) { return (uint64_t)kScratchPerByte * (doc_len + 64) + 4096; }
+uint64_t scratch_bytes_for(uint32_t doc_len) { return scratch_bytes_for_dev(doc_len); }
 
 // Head of the language model on one doc vector (host arithmetic; the device uses MFMA).
 static void lid_head_host(const LangidModel& m, const uint16_t* v, int32_t cnt, int64_t* r) {
@@ -330,6 +343,96 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
       x.weak_keys = weak_keys;
       StageOut out{rec.data(), (uint32_t)ndocs, (uint32_t)i, lvec.data(), lcnt.data()};
       analyze_stage(x, st, *plan, lid ? lid->emb.data() : nullptr, (const uint8_t*)data + off[i], n, out);
+      if (has_lid) {
+        for (int s = 0; s < st.n_steps; ++s)
+          if (st.steps[s].kind == DK_LANGID)
+            lid_head_host(*lid, &lvec[(size_t)i * kLidDim], lcnt[i],
+                          rec.data() + (int64_t)st.steps[s].rec_prefix * ndocs + i * st.steps[s].width);
+      }
+    }
+  });
+  delete plan;
+}
+
+// Host run of the LDS-resident short-document kernel (k_stage_lds, csrc/common/lds_stage.h):
+// per document the same slice (slice[i] bytes; 0 = not an LDS-path document), the same
+// allocation order and so the same overflow decisions; a document that does not fit is
+// recomputed by analyze_stage exactly as the device retry kernel does (retried[i] = 1).
+void emulate_stage_lds(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
+                       const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
+                       std::vector<int64_t>& rec, std::vector<uint32_t>& flags, const uint32_t* slice,
+                       const uint8_t* dead, std::vector<uint8_t>& retried) {
+  DevPlan* plan = new DevPlan();
+  std::memset(plan, 0, sizeof(DevPlan));
+  DevStage st = build_stage(steps, idx, *plan);
+  DevStage st_lid{};
+  bool has_lid = false;
+  for (int s = 0; s < st.n_steps; ++s)
+    if (st.steps[s].kind == DK_LANGID) {
+      has_lid = true;
+      st_lid.steps[st_lid.n_steps++] = st.steps[s];
+    }
+  st_lid.width_total = st.width_total;
+  if (has_lid && !lid) { delete plan; throw std::runtime_error("language model required"); }
+  rec.assign((size_t)st.width_total * ndocs, 0);
+  flags.assign(ndocs, 0);
+  retried.assign(ndocs, 0);
+  std::vector<uint16_t> lvec(has_lid ? (size_t)ndocs * kLidDim : 1);
+  std::vector<int32_t> lcnt(has_lid ? ndocs : 1);
+  uint32_t maxlen = 0;
+  for (int64_t i = 0; i < ndocs; ++i) maxlen = std::max<uint32_t>(maxlen, (uint32_t)(off[i + 1] - off[i]));
+  std::vector<uint64_t> pw = pow_table(maxlen + 16);
+  const UcdView ucd = host_ucd();
+  constexpr uint32_t kGenericLds = 10240;  // the retry kernel's slice (DeviceRunner.DEFAULT_LDS_BYTES)
+  parallel_for(ndocs, nthreads, [&](int64_t a, int64_t b) {
+    std::vector<char> scratch;
+    std::vector<char> lds(kGenericLds + 16);
+    std::vector<uint64_t> arena;  // 8-byte aligned LDS slice stand-in
+    for (int64_t i = a; i < b; ++i) {
+      if (dead && dead[i]) continue;
+      const uint32_t n = (uint32_t)(off[i + 1] - off[i]);
+      const uint8_t* src = (const uint8_t*)data + off[i];
+      auto generic = [&](const DevStage& stage) {
+        const uint64_t need = scratch_bytes_for(n);
+        if (scratch.size() < need) scratch.resize(need);
+        DocCtx<SeqPar> x;
+        x.ucd = ucd;
+        x.pw = pw.data();
+        x.pw_n = (uint32_t)(pw.size() / 2 - 1);
+        x.ipw = pw.data() + x.pw_n + 1;
+        x.scr = scratch.data();
+        x.cap = need;
+        x.lds = lds.data();
+        x.lcap = kGenericLds;
+        x.flag = &flags[i];
+        StageOut out{rec.data(), (uint32_t)ndocs, (uint32_t)i, lvec.data(), lcnt.data()};
+        analyze_stage(x, stage, *plan, lid ? lid->emb.data() : nullptr, src, n, out);
+      };
+      bool done = false;
+      if (slice && slice[i]) {
+        const uint32_t cap = slice[i] & ~7u;
+        if (arena.size() * 8 < cap) arena.resize(cap / 8 + 1);
+        LCtx<SeqPar> x;
+        x.a.base = (char*)arena.data();
+        x.a.cap = cap;
+        x.ucd = ucd;
+        x.flag = &flags[i];
+        uint16_t* asc = x.a.get<uint16_t>(128);
+        uint8_t* tx = x.a.get<uint8_t>(n + 16);
+        if (!x.a.ovf && n <= kLdsMaxDoc) {
+          for (uint32_t c = 0; c < 128; ++c) asc[c] = compact_prop(ucd.props(c));
+          std::memcpy(tx, src, n);
+          std::memset(tx + n, 0, 16);
+          x.asc = asc;
+          done = lds_analyze_stage(x, st, *plan, tx, n, rec.data(), (uint32_t)ndocs, (uint32_t)i) == LDS_OK;
+        }
+        if (!done) retried[i] = 1;
+      }
+      if (!done) {
+        generic(st);
+      } else if (has_lid) {
+        generic(st_lid);
+      }
       if (has_lid) {
         for (int s = 0; s < st.n_steps; ++s)
           if (st.steps[s].kind == DK_LANGID)

@@ -10,8 +10,7 @@
 
 namespace tb {
 
-// Per-document device scratch: kScratchPerByte * (len + 64) + 4096 bytes.
-constexpr uint64_t kScratchPerByte = 160;
+// Per-document device scratch (devplan.h scratch_bytes_for_dev).
 uint64_t scratch_bytes_for(uint32_t doc_len);
 
 int dev_kind_of(const StepCfg& c);
@@ -38,6 +37,10 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
                    std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes = 0,
                    const uint8_t* dead = nullptr, bool weak_keys = false);
+void emulate_stage_lds(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
+                       const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
+                       std::vector<int64_t>& rec, std::vector<uint32_t>& flags, const uint32_t* slice,
+                       const uint8_t* dead, std::vector<uint8_t>& retried);
 void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
                 std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,
                 std::vector<uint32_t>& flags, uint32_t lds_bytes = 0, const uint8_t* dead = nullptr);

@@ -286,6 +286,7 @@ def test_lds_stage_kernel_matches_host(host, corpus, runner_parts, monkeypatch, 
 
     cfg, steps, plan, _, lid = runner_parts
     monkeypatch.setenv("TB_LDS_PER_BYTE", per_byte)
+    monkeypatch.setenv("TB_LDS_STAGE", "1")
     runner = DeviceRunner(steps, plan, "cuda:0", lid)
     assert runner.lds_stage
     data, off = synth.pack(corpus)

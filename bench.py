@@ -15,8 +15,10 @@ the per-step document counters (the only cross-GPU traffic).
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
+import resource
 import sys
 import time
 
@@ -78,6 +80,8 @@ def main():
         if have < args.gpus:
             print(f"bench.py: --gpus {args.gpus} requested but only {have} GPU(s) are visible", file=sys.stderr)
             sys.exit(2)
+    # one process group per multi-GPU job (RCCL over xGMI); TB_FORCE_PG=1 also creates a one-rank
+    # group on one GPU, so the per-step AR1 below runs over RCCL and is timed there too
     ctx = dist.init_from_env(backend="nccl" if args.backend == "cuda" else "gloo")
     rank, world = ctx.rank, ctx.world_size
     device = f"cuda:{ctx.local_rank}" if args.backend == "cuda" else None
@@ -112,28 +116,39 @@ def main():
     ctx.barrier()
     if args.backend == "cuda":
         torch.cuda.synchronize()
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     n_done = 0
     tsum: dict = {}
-    ar1 = None
+    # AR1 every TB_AR1_EVERY steps (default every step; 0: only the final totals reduction)
+    ar1_every = int(os.environ.get("TB_AR1_EVERY", "1"))
+    ar1_window = int(os.environ.get("TB_AR1_WINDOW", "4"))
+    ar1s = collections.deque()
     for res in eng.process_many(feed(args.steps, args.warmup)):
         step = np.asarray([res.n_docs, res.n_kept, res.n_excluded, len(res.error_rows)], dtype=np.int64)
         counters += step
         # AR1 once per step: the global counter vector (what rank 0's /metrics serves), reduced
-        # over RCCL while the next step runs; waited one step later
-        if ar1 is not None:
-            ar1.wait()
-        ar1 = ctx.all_reduce_sum_async(step)
+        # over RCCL while the next steps run; the main thread (which also assembles outputs)
+        # only waits once more than TB_AR1_WINDOW reductions are outstanding
+        if ar1_every and n_done % ar1_every == 0:
+            ar1s.append(ctx.all_reduce_sum_async(step))
+        while ar1s and (len(ar1s) > ar1_window or ar1s[0].done()):
+            ar1s.popleft().wait()
         for k, v in res.timings.items():
             tsum[k] = tsum.get(k, 0.0) + v
         n_done += 1
-    if ar1 is not None:
-        ar1.wait()
+    while ar1s:
+        ar1s.popleft().wait()
     assert n_done == args.steps
     if args.backend == "cuda":
         torch.cuda.synchronize()
     ctx.barrier()
     elapsed = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    # host CPU time of this rank's process over the timed steps (all threads: submitter, copy
+    # and assembly pools), the per-rank budget an 8-GPU node has to provide
+    cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+    cpu_ms_step_max = ctx.all_reduce_max(1000.0 * cpu_s / args.steps)
     elapsed_max = ctx.all_reduce_max(elapsed)
     totals = ctx.all_reduce_sum(counters)
     docs_total = int(totals[0])
@@ -162,6 +177,9 @@ def main():
                 "backend": args.backend,
                 "pipeline_config": os.path.relpath(args.config, ROOT),
             },
+            "process_group": ctx.backend,
+            "host_cpu_ms_per_step": round(cpu_ms_step_max, 3),
+            "host_cpu_us_per_doc": round(1000.0 * cpu_ms_step_max / args.docs_per_step, 4),
             "kept": int(totals[1]),
             "excluded": int(totals[2]),
             "errors": int(totals[3]),

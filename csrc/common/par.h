@@ -643,6 +643,14 @@ struct BlockPar {
       if (lane < 2) bits[(base >> 5) + lane] = lane ? (uint32_t)(m >> 32) : (uint32_t)m;
     }
   }
+  template <class Pred, class Store>
+  __device__ __forceinline__ void mask_store(uint32_t n, Pred&& pred, Store&& store) const {
+    for (uint32_t base = wid * 64; base < n; base += NT) {
+      const uint32_t i = base + lane;
+      const uint64_t m = __ballot(i < n && pred(i));
+      if (lane < 2) store((base >> 5) + lane, lane ? (uint32_t)(m >> 32) : (uint32_t)m);
+    }
+  }
   template <class T, class Op, class In, class Sel, class Emit>
   __device__ __forceinline__ uint32_t scan_compact(uint32_t n, T id, Op&& op, In&& in, Sel&& sel,
                                                    Emit&& emit) const {
@@ -691,6 +699,212 @@ struct BlockPar {
   }
   __device__ __forceinline__ static void max32(uint32_t* p, uint32_t v) { atomicMax(p, v); }
   __device__ __forceinline__ static uint32_t add32(uint32_t* p, uint32_t v) { return atomicAdd(p, v); }
+  __device__ __forceinline__ static void or32(uint32_t* p, uint32_t v) { atomicOr(p, v); }
+};
+
+// NT/64 waves on one document with few barriers: items [0, n) are cut into one contiguous
+// segment per wave (whole 64-item chunks), every wave runs the WavePar loop over its own
+// segment, and only the per-wave totals cross waves (through `xs`, double-buffered so one barrier
+// per primitive suffices). Compactions and scans run in two passes over the segment (count /
+// total first, then emit with the wave's offset): their predicates and inputs are evaluated
+// twice, in exchange for one barrier per call instead of two per 64 x NW items (BlockPar).
+// `xs` must hold >= 2 * 16 * NW bytes; the owner resets `gen` never (it only alternates halves).
+template <int NT>
+struct SegPar {
+  static_assert(NT % 64 == 0 && NT >= 128 && NT <= 1024, "block of whole waves");
+  static constexpr int NW = NT / 64;
+  static constexpr bool kPartTables = false;
+  uint32_t tid, lane, wid;
+  char* xs = nullptr;
+  mutable uint32_t gen = 0;
+  __device__ SegPar() : tid(threadIdx.x), lane(threadIdx.x & 63), wid(threadIdx.x >> 6) {}
+
+  // this wave's item range [b, e)
+  __device__ __forceinline__ void seg(uint32_t n, uint32_t& b, uint32_t& e) const {
+    const uint32_t chunks = (n + 63) >> 6;
+    const uint32_t per = (chunks + NW - 1) / NW;
+    b = wid * per * 64;
+    e = b + per * 64;
+    if (b > n) b = n;
+    if (e > n) e = n;
+  }
+  template <class T>
+  __device__ __forceinline__ T* slot() const {
+    return (T*)(xs + (gen & 1u) * 16 * NW);
+  }
+  // exclusive prefix (over waves before this one) and total of a per-wave value; one barrier
+  template <class T, class Op>
+  __device__ __forceinline__ void across(T mine, T id, Op&& op, T& before, T& total) const {
+    T* t = slot<T>();
+    if (lane == 0) t[wid] = mine;
+    __syncthreads();
+    before = id;
+    total = id;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const T v = t[w];
+      if (w < (int)wid) before = op(before, v);
+      total = op(total, v);
+    }
+    ++gen;
+  }
+  template <class T, class Op>
+  __device__ __forceinline__ T all(T mine, T id, Op&& op) const {
+    T before, total;
+    across(mine, id, op, before, total);
+    return total;
+  }
+
+  template <class F>
+  __device__ __forceinline__ void for_n(uint32_t n, F&& f) const {
+    uint32_t b, e;
+    seg(n, b, e);
+    for (uint32_t i = b + lane; i < e; i += 64) f(i);
+  }
+  template <class S, class Pred, class Emit>
+  __device__ __forceinline__ uint32_t compact(uint32_t n, Pred&& pred, Emit&& emit) const {
+    uint32_t b, e;
+    seg(n, b, e);
+    uint32_t cnt = 0;
+    for (uint32_t base = b; base < e; base += 64) {
+      const uint32_t i = base + lane;
+      S st{};
+      cnt += (uint32_t)__popcll(__ballot(i < e && pred(i, st)));
+    }
+    uint32_t before, total;
+    across(cnt, 0u, [](uint32_t a, uint32_t c) { return a + c; }, before, total);
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t k = before;
+    for (uint32_t base = b; base < e; base += 64) {
+      const uint32_t i = base + lane;
+      S st{};
+      const bool p = i < e && pred(i, st);
+      const uint64_t m = __ballot(p);
+      if (p) emit(i, k + (uint32_t)__popcll(m & lt), st);
+      k += (uint32_t)__popcll(m);
+    }
+    return total;
+  }
+  template <class T>
+  __device__ __forceinline__ T wave_sum(T v) const {
+    return pardetail::bcast63(pardetail::wave_incl_scan(v, lane, [](T a, T c) { return a + c; }));
+  }
+  template <class T, class F>
+  __device__ __forceinline__ T sum(uint32_t n, F&& f) const {
+    uint32_t b, e;
+    seg(n, b, e);
+    T s = 0;
+    for (uint32_t i = b + lane; i < e; i += 64) s += f(i);
+    return all(wave_sum(s), (T)0, [](T a, T c) { return a + c; });
+  }
+  template <class T, class F>
+  __device__ __forceinline__ T max(uint32_t n, T init, F&& f) const {
+    uint32_t b, e;
+    seg(n, b, e);
+    T s = init;
+    for (uint32_t i = b + lane; i < e; i += 64) { T v = f(i); if (v > s) s = v; }
+    s = pardetail::bcast63(pardetail::wave_incl_scan(s, lane, [](T a, T c) { return a > c ? a : c; }));
+    return all(s, init, [](T a, T c) { return a > c ? a : c; });
+  }
+  template <class T, class F>
+  __device__ __forceinline__ T min(uint32_t n, T init, F&& f) const {
+    uint32_t b, e;
+    seg(n, b, e);
+    T s = init;
+    for (uint32_t i = b + lane; i < e; i += 64) { T v = f(i); if (v < s) s = v; }
+    s = pardetail::bcast63(pardetail::wave_incl_scan(s, lane, [](T a, T c) { return a < c ? a : c; }));
+    return all(s, init, [](T a, T c) { return a < c ? a : c; });
+  }
+  template <class T, class Op, class In, class Out>
+  __device__ __forceinline__ T scan(uint32_t n, T id, Op&& op, In&& in, Out&& out) const {
+    uint32_t b, e;
+    seg(n, b, e);
+    T tot = id;
+    for (uint32_t base = b; base < e; base += 64) {
+      const uint32_t i = base + lane;
+      const T x = pardetail::wave_incl_scan(i < e ? in(i) : id, lane, op);
+      tot = op(tot, pardetail::bcast63(x));
+    }
+    T before, total;
+    across(tot, id, op, before, total);
+    T carry = before;
+    for (uint32_t base = b; base < e; base += 64) {
+      const uint32_t i = base + lane;
+      const T v = i < e ? in(i) : id;
+      const T x = pardetail::wave_incl_scan(v, lane, op);
+      T excl = pardetail::shfl_up_t(x, 1);
+      if (lane == 0) excl = id;
+      if (i < e) out(i, op(carry, excl));
+      carry = op(carry, pardetail::bcast63(x));
+    }
+    return total;
+  }
+  template <class T, class Op, class In, class Sel, class Emit>
+  __device__ __forceinline__ uint32_t scan_compact(uint32_t n, T id, Op&& op, In&& in, Sel&& sel,
+                                                   Emit&& emit) const {
+    // pass 1: the segment's scan total (what carries into the next segment); its selected count
+    // needs the incoming carry, so the two are exchanged in two steps
+    uint32_t b, e;
+    seg(n, b, e);
+    T tot = id;
+    for (uint32_t base = b; base < e; base += 64) {
+      const uint32_t i = base + lane;
+      const T x = pardetail::wave_incl_scan(i < e ? in(i) : id, lane, op);
+      tot = op(tot, pardetail::bcast63(x));
+    }
+    T before, total;
+    across(tot, id, op, before, total);
+    uint32_t cnt = 0;
+    {
+      T carry = before;
+      for (uint32_t base = b; base < e; base += 64) {
+        const uint32_t i = base + lane;
+        const T x = pardetail::wave_incl_scan(i < e ? in(i) : id, lane, op);
+        const T incl = op(carry, x);
+        cnt += (uint32_t)__popcll(__ballot(i < e && sel(i, incl)));
+        carry = op(carry, pardetail::bcast63(x));
+      }
+    }
+    uint32_t kbefore, ktotal;
+    across(cnt, 0u, [](uint32_t a, uint32_t c) { return a + c; }, kbefore, ktotal);
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    T carry = before;
+    uint32_t k = kbefore;
+    for (uint32_t base = b; base < e; base += 64) {
+      const uint32_t i = base + lane;
+      const T x = pardetail::wave_incl_scan(i < e ? in(i) : id, lane, op);
+      const T incl = op(carry, x);
+      const bool p = i < e && sel(i, incl);
+      const uint64_t m = __ballot(p);
+      if (p) emit(i, k + (uint32_t)__popcll(m & lt), incl);
+      k += (uint32_t)__popcll(m);
+      carry = op(carry, pardetail::bcast63(x));
+    }
+    return ktotal;
+  }
+  __device__ __forceinline__ uint32_t reduce_or(uint32_t v) const {
+    for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o);
+    return all(v, 0u, [](uint32_t a, uint32_t c) { return a | c; });
+  }
+  template <class T>
+  __device__ __forceinline__ T reduce_add(T v) const {
+    return all(wave_sum(v), (T)0, [](T a, T c) { return a + c; });
+  }
+  template <class Pred, class Store>
+  __device__ __forceinline__ void mask_store(uint32_t n, Pred&& pred, Store&& store) const {
+    uint32_t b, e;
+    seg(n, b, e);
+    for (uint32_t b0 = b; b0 < e; b0 += 64) {
+      const uint32_t i = b0 + lane;
+      const uint64_t m = __ballot(i < e && pred(i));
+      if (lane < 2) store((b0 >> 5) + lane, lane ? (uint32_t)(m >> 32) : (uint32_t)m);
+    }
+  }
+  __device__ __forceinline__ void sync() const { __syncthreads(); }
+  __device__ __forceinline__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
+  template <class F>
+  __device__ __forceinline__ void single(F&& f) const { if (tid == 0) f(); }
+  __device__ __forceinline__ bool leader() const { return tid == 0; }
   __device__ __forceinline__ static void or32(uint32_t* p, uint32_t v) { atomicOr(p, v); }
 };
 #endif

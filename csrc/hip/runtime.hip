@@ -270,8 +270,12 @@ int tbrt_stream_destroy(hipStream_t s) { return (int)hipStreamDestroy(s); }
 int tbrt_stream_sync(hipStream_t s) { return (int)hipStreamSynchronize(s); }
 int tbrt_stream_priority_range(int* lo, int* hi) { return (int)hipDeviceGetStreamPriorityRange(lo, hi); }
 
-int tbrt_event_create(hipEvent_t* e, int timing) {
-  return (int)hipEventCreateWithFlags(e, timing ? hipEventDefault : hipEventDisableTiming);
+// flags: bit 0 = timing, bit 1 = blocking sync (the waiting host thread sleeps until the event
+// signals instead of spinning a core: the batch pipeline waits ~20 ms per step on the device)
+int tbrt_event_create(hipEvent_t* e, int flags) {
+  unsigned f = (flags & 1) ? hipEventDefault : hipEventDisableTiming;
+  if (flags & 2) f |= hipEventBlockingSync;
+  return (int)hipEventCreateWithFlags(e, f);
 }
 int tbrt_event_destroy(hipEvent_t e) { return (int)hipEventDestroy(e); }
 int tbrt_event_record(hipEvent_t e, hipStream_t s) { return (int)hipEventRecord(e, s); }

@@ -22,8 +22,10 @@ struct LdsTables {
 
 extern __shared__ __attribute__((aligned(16))) char g_lds_stage[];
 
-// Stage of one content version for launch positions [pos0, pos0 + gridDim.x) of `perm`.
-__device__ __forceinline__ void stage_lds_body(const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage,
+// Stage of one content version for launch positions [pos0, pos0 + gridDim.x) of `perm`: one
+// document per workgroup, P = WavePar (one wave) or BlockPar<NT> (NT/64 waves sharing the slice).
+template <class P>
+__device__ __forceinline__ void stage_lds_body(P par, const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage,
                                                   const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
                                                   const int32_t* __restrict__ perm, int32_t pos0, int32_t ndocs,
                                                   LdsTables tabs, int64_t* rec, uint32_t* flags, uint32_t lds_bytes,
@@ -34,14 +36,15 @@ __device__ __forceinline__ void stage_lds_body(const DevPlan* __restrict__ plan,
   if (doc >= ndocs || (dead && dead[doc])) return;
   const int64_t o0 = off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - o0);
-  LCtx<WavePar> x;
+  LCtx<P> x;
+  x.par = par;
   x.a.base = (TB_LDS char*)g_lds_stage;
   x.a.cap = lds_bytes & ~7u;
   x.ucd = UcdView{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
   x.flag = flags + doc;
   x.prof = prof ? prof + (size_t)doc * kPhaseSlots : nullptr;
-  TB_LDS uint16_t* asc = x.a.get<uint16_t>(128);
-  TB_LDS uint8_t* tx = x.a.get<uint8_t>(n + 16);
+  TB_LDS uint16_t* asc = x.a.template get<uint16_t>(128);
+  TB_LDS uint8_t* tx = x.a.template get<uint8_t>(n + 16);
   bool fail = x.a.ovf || n > kLdsMaxDoc;
   if (!fail) {
     x.par.for_n(128, [&](uint32_t c) { asc[c] = compact_prop(x.ucd.props(c)); });
@@ -82,12 +85,34 @@ __device__ __forceinline__ void stage_lds_body(const DevPlan* __restrict__ plan,
       const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t pos0, int32_t ndocs,           \
       LdsTables tabs, int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof,                       \
       const uint8_t* __restrict__ dead, uint32_t* __restrict__ retry_cnt, int32_t* __restrict__ retry_pos) {   \
-    stage_lds_body(plan, stage, bytes, off, perm, pos0, ndocs, tabs, rec, flags, lds_bytes, prof, dead,         \
-                   retry_cnt, retry_pos);                                                                      \
+    stage_lds_body(WavePar(), plan, stage, bytes, off, perm, pos0, ndocs, tabs, rec, flags, lds_bytes, prof,     \
+                   dead, retry_cnt, retry_pos);                                                                \
   }
 TB_STAGE_LDS_KERNEL(k_stage_lds, )
 TB_STAGE_LDS_KERNEL(k_stage_lds_w4, __attribute__((amdgpu_waves_per_eu(4, 8))))
 TB_STAGE_LDS_KERNEL(k_stage_lds_w8, __attribute__((amdgpu_waves_per_eu(8, 8))))
+
+// Multi-wave workgroups for the longer short documents: NT/64 waves cooperate on one document in
+// one slice (SegPar: each wave scans a contiguous segment of every pass, one barrier per
+// primitive), so a 2-4 KB document's ~40 KB slice keeps several waves busy instead of one.
+template <int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_stage_lds_seg(
+    const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes,
+    const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t pos0, int32_t ndocs, LdsTables tabs,
+    int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead,
+    uint32_t* __restrict__ retry_cnt, int32_t* __restrict__ retry_pos) {
+  __shared__ __attribute__((aligned(16))) char xs[2 * 16 * (NT / 64) + 64];
+  SegPar<NT> par;
+  par.xs = xs;
+  stage_lds_body(par, plan, stage, bytes, off, perm, pos0, ndocs, tabs, rec, flags, lds_bytes, prof, dead, retry_cnt,
+                 retry_pos);
+}
+template __global__ void k_stage_lds_seg<128>(const DevPlan*, const DevStage*, const uint8_t*, const int64_t*,
+                                              const int32_t*, int32_t, int32_t, LdsTables, int64_t*, uint32_t*,
+                                              uint32_t, uint64_t*, const uint8_t*, uint32_t*, int32_t*);
+template __global__ void k_stage_lds_seg<256>(const DevPlan*, const DevStage*, const uint8_t*, const int64_t*,
+                                              const int32_t*, int32_t, int32_t, LdsTables, int64_t*, uint32_t*,
+                                              uint32_t, uint64_t*, const uint8_t*, uint32_t*, int32_t*);
 
 // Generic recomputation of the documents k_stage_lds could not fit: workgroup b handles list
 // entries b, b + gridDim.x, ... in its own HBM scratch slice (slice_bytes each) and the usual
@@ -141,15 +166,18 @@ int tb_stage_lds(hipStream_t stream, const void* plan, const void* stage, const 
                  const int32_t* perm, int32_t pos0, int32_t nblocks, int32_t ndocs, const uint16_t* s1,
                  const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
                  uint32_t lds_bytes, uint64_t* prof, const uint8_t* dead, uint32_t* retry_cnt, int32_t* retry_pos,
-                 int32_t waves) {
+                 int32_t waves, int32_t threads) {
   if (nblocks <= 0) return 0;
-  if (!perm || !retry_cnt || !retry_pos || pos0 < 0 || lds_bytes < 512 || lds_bytes > 160 * 1024)
+  if (!perm || !retry_cnt || !retry_pos || pos0 < 0 || lds_bytes < 512 || lds_bytes > 159 * 1024)
     return (int)hipErrorInvalidValue;
   LdsTables t{s1, s2, l1, l2};
-  auto kern = waves == 8 ? k_stage_lds_w8 : waves == 4 ? k_stage_lds_w4 : k_stage_lds;
+  // threads > 64: one multi-wave workgroup per document (k_stage_lds_seg)
+  auto kern = threads == 256 ? k_stage_lds_seg<256> : threads == 128 ? k_stage_lds_seg<128>
+              : waves == 8   ? k_stage_lds_w8       : waves == 4      ? k_stage_lds_w4 : k_stage_lds;
+  if (threads != 64 && threads != 128 && threads != 256) return (int)hipErrorInvalidValue;
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-  hipLaunchKernelGGL(kern, dim3((uint32_t)nblocks), dim3(64), lds_bytes, stream, (const DevPlan*)plan,
+  hipLaunchKernelGGL(kern, dim3((uint32_t)nblocks), dim3((uint32_t)threads), lds_bytes, stream, (const DevPlan*)plan,
                      (const DevStage*)stage, bytes, off, perm, pos0, ndocs, t, rec, flags, lds_bytes, prof, dead,
                      retry_cnt, retry_pos);
   return (int)hipGetLastError();

@@ -204,3 +204,23 @@ def test_metrics_expose_device_counters():
 
     text = metrics.render().decode()
     assert "tb_h2d_bytes_total" in text and "tb_gpu_kernel_seconds" in text
+
+
+def test_forced_world1_group_on_gloo(monkeypatch):
+    """TB_FORCE_PG: a one-rank process group (in-process store, no rendezvous) carries the same
+    AR1 / AG1 / BAR calls as a multi-rank job; without it no group is created."""
+    from textblaster_amd.parallel import dist
+
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    assert dist.init_from_env("gloo").backend is None
+    monkeypatch.setenv("TB_FORCE_PG", "1")
+    ctx = dist.init_from_env("gloo")
+    try:
+        assert ctx.backend == "gloo"
+        assert list(ctx.all_reduce_sum([1, 2, 3])) == [1, 2, 3]
+        assert list(ctx.all_reduce_sum_async([4, 5]).wait()) == [4, 5]
+        assert ctx.all_gather_counts([7, 8]).tolist() == [[7, 8]]
+        ctx.barrier()
+    finally:
+        ctx.destroy()

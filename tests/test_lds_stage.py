@@ -78,7 +78,7 @@ def test_bucket_planner_covers_positions_and_bounds_slices():
     b = lds_buckets(lp[n_long:], 10, 1024)
     assert b[0][0] == 0 and b[-1][1] == len(lp) - n_long
     for (p0, p1, sl), nxt in zip(b, b[1:] + [None]):
-        assert p1 > p0 and sl % 256 == 0 and sl <= 160 * 1024
+        assert p1 > p0 and sl % 256 == 0 and sl <= 159 * 1024
         assert sl >= 10 * int(lp[n_long + p0:n_long + p1].max()) + 1024  # the longest document fits
         if nxt is not None:
             assert nxt[0] == p1

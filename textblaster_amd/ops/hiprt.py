@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 import threading
 from typing import Iterator, Optional
 
@@ -141,10 +142,16 @@ class Stream:
         return ev
 
 
+# host waits on events sleep instead of spinning (TB_EVENT_BLOCKING=0: spin, HIP's default)
+_BLOCKING_EVENTS = os.environ.get("TB_EVENT_BLOCKING", "1") not in ("", "0")
+
+
 class Event:
-    def __init__(self, timing: bool = False):
+    def __init__(self, timing: bool = False, blocking: Optional[bool] = None):
         h = ctypes.c_void_p()
-        check(lib().tbrt_event_create(ctypes.byref(h), 1 if timing else 0), "hipEventCreate")
+        blocking = _BLOCKING_EVENTS if blocking is None else blocking
+        flags = (1 if timing else 0) | (2 if blocking else 0)
+        check(lib().tbrt_event_create(ctypes.byref(h), flags), "hipEventCreate")
         self.handle = h.value
 
     def record(self, s: Optional[Stream] = None) -> "Event":

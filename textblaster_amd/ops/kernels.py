@@ -45,7 +45,8 @@ _SIGS = {
     "tb_pow_table": [_P, _P, _U32],
     "tb_html_sizes": [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _P, _U32, _P],
     "tb_html_scatter": [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _P, _U32, _P, _P],
-    "tb_stage_lds": [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _U32, _P, _P, _P, _P, _I32],
+    "tb_stage_lds": [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _U32, _P, _P, _P, _P, _I32,
+                     _I32],
     "tb_stage_retry": [_P, _P, _P, _P, _P, _P, _I32, _P, ctypes.c_uint64, _I32, _P, _U32, _P, _P, _P, _P, _P, _P, _U32,
                        _P, _P, _P],
     "tb_abi_version": [],
@@ -133,7 +134,7 @@ class Kernels:
         _check(rc, "tb_stage_analyze")
 
     def stage_lds(self, plan, stage, bytes_, off, perm, pos0, nblocks, ndocs, rec, flags, lds_bytes, retry_cnt,
-                  retry_pos, prof=None, dead=None, waves=0):
+                  retry_pos, prof=None, dead=None, waves=0, threads=64):
         """k_stage_lds (csrc/hip/stage_lds.hip): launch positions [pos0, pos0 + nblocks) of ``perm``,
         one wave each with ``lds_bytes`` of LDS; documents that do not fit are appended to
         ``retry_pos`` (count in ``retry_cnt``) for :meth:`stage_retry`."""
@@ -143,7 +144,8 @@ class Kernels:
         rc = self.lib.tb_stage_lds(
             self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), perm.data_ptr(), pos0,
             nblocks, ndocs, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(),
-            flags.data_ptr(), lds_bytes, _ptr(prof), _ptr(dead), retry_cnt.data_ptr(), retry_pos.data_ptr(), waves)
+            flags.data_ptr(), lds_bytes, _ptr(prof), _ptr(dead), retry_cnt.data_ptr(), retry_pos.data_ptr(), waves,
+            threads)
         _check(rc, "tb_stage_lds")
 
     def stage_retry(self, plan, stage, bytes_, off, perm, ndocs, scratch, slice_bytes, grid, pw, pw_n, rec, flags,

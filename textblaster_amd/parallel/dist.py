@@ -64,13 +64,25 @@ class DistContext:
         return t.cpu().numpy()
 
     def all_reduce_sum_async(self, arr) -> "PendingReduce":
-        """Non-blocking all_reduce(SUM) of a small int64 vector (AR1); ``.wait()`` returns it."""
+        """Non-blocking all_reduce(SUM) of a small int64 vector (AR1); ``.wait()`` returns it.
+
+        With RCCL the vector goes up and comes back through pinned host memory on a dedicated
+        torch stream (non-blocking copies): nothing touches the null stream, so the reduction
+        never waits for (or holds up) the document kernels of the native runtime's streams."""
         a = np.asarray(arr, dtype=np.int64)
         if not self.initialized:
             return PendingReduce(None, a.copy())
-        _, td = self._torch()
-        t = self._tensor(a)
-        return PendingReduce(td.all_reduce(t, op=td.ReduceOp.SUM, async_op=True), t)
+        torch, td = self._torch()
+        if self.backend != "nccl":
+            t = self._tensor(a)
+            return PendingReduce(td.all_reduce(t, op=td.ReduceOp.SUM, async_op=True), t)
+        if getattr(self, "_ar_stream", None) is None:
+            self._ar_stream = torch.cuda.Stream(device=self.device, priority=-1)
+        host = torch.from_numpy(np.ascontiguousarray(a)).pin_memory()
+        with torch.cuda.stream(self._ar_stream):
+            t = host.to(self.device, non_blocking=True)
+            work = td.all_reduce(t, op=td.ReduceOp.SUM, async_op=True)
+        return PendingReduce(work, t, host, self._ar_stream)
 
     def all_reduce_max(self, x: float) -> float:
         if not self.initialized:
@@ -98,41 +110,76 @@ class DistContext:
 
 
 class PendingReduce:
-    def __init__(self, work, tensor):
+    def done(self) -> bool:
+        """True once wait() would not block."""
+        return self.work is None or self.work.is_completed()
+
+    def __init__(self, work, tensor, host=None, stream=None):
         self.work = work
         self.tensor = tensor
+        self.host = host
+        self.stream = stream
 
     def wait(self) -> np.ndarray:
         if self.work is not None:
-            self.work.wait()
+            if self.stream is not None:
+                import torch
+
+                with torch.cuda.stream(self.stream):
+                    self.work.wait()  # orders the stream after the collective
+                    self.host.copy_(self.tensor, non_blocking=True)
+                self.stream.synchronize()
+                self.tensor = self.host.numpy()
+            else:
+                self.work.wait()
+                self.tensor = self.tensor.cpu().numpy()
             self.work = None
-            self.tensor = self.tensor.cpu().numpy()
         return self.tensor
 
 
-def init_from_env(backend: str = "nccl") -> DistContext:
-    """Initialise from torchrun's env (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT)."""
+def init_from_env(backend: str = "nccl", force_pg: Optional[bool] = None) -> DistContext:
+    """Initialise from torchrun's env (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT).
+
+    A process group exists when WORLD_SIZE > 1, or at world size 1 when ``force_pg`` (default:
+    env ``TB_FORCE_PG=1``) asks for one: then the per-step AR1 / AG1 / BAR collectives of the
+    multi-GPU path run (and are timed) on a single GPU too, over a one-rank RCCL communicator
+    (an in-process HashStore, no rendezvous). Without a group nothing imports torch: a one-GPU
+    run only needs the native HIP runtime."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if force_pg is None:
+        force_pg = os.environ.get("TB_FORCE_PG", "") not in ("", "0")
     ctx = DistContext(rank, world, local)
     if backend == "nccl":
-        import torch
-
-        torch.cuda.set_device(local)
         ctx.device = f"cuda:{local}"
-    if world > 1:
-        import torch.distributed as td
-
+    if world > 1 or force_pg:
         import datetime
 
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        import torch
+        import torch.distributed as td
+
+        if backend == "nccl":
+            # RCCL and torch add their own streams next to the engine's eight; with the box's
+            # default of 4 hardware queues per process they land behind document kernels on a
+            # shared queue (measured: a one-rank group with no collective at all took the
+            # 1-GPU bench from 35.6 to 47.9 ms/step; 8 queues: 37.0). Set before the first HIP
+            # call of this process (TB_PG_HW_QUEUES overrides, 0 keeps the inherited value).
+            q = os.environ.get("TB_PG_HW_QUEUES", "8")
+            if q not in ("", "0"):
+                os.environ["GPU_MAX_HW_QUEUES"] = q
+            # the collective streams at high priority: a counter reduction is never queued
+            # behind a batch's kernels
+            os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
+            torch.cuda.set_device(local)
         # a dead or hung peer turns into an error after this long instead of a silent hang
         kwargs = {"timeout": datetime.timedelta(seconds=float(os.environ.get("TB_COLLECTIVE_TIMEOUT", "600")))}
         if backend == "nccl":
-            import torch
-
             kwargs["device_id"] = torch.device(f"cuda:{local}")
+        if world == 1:
+            kwargs["store"] = td.HashStore()
+        else:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         td.init_process_group(backend=backend, rank=rank, world_size=world, **kwargs)
         ctx.backend = backend
     return ctx

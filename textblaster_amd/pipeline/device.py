@@ -125,7 +125,7 @@ def build_resolve(plan: ExecPlan, stage_layout, steps_native) -> Optional[bytes]
         return None
 
 
-LDS_MAX_SLICE = 160 * 1024
+LDS_MAX_SLICE = 159 * 1024  # the multi-wave kernels also hold a small static exchange buffer
 # LDS-resident short-document stage kernel on by default (TB_LDS_STAGE overrides)
 LDS_STAGE_DEFAULT = "0"
 
@@ -169,6 +169,15 @@ def lds_doc_slices(lens: np.ndarray, long_doc_bytes: int, per_byte: float, fixed
     for p0, p1, sl in lds_buckets(lp[n_long:], per_byte, fixed, ratio):
         out[perm[n_long + p0:n_long + p1]] = sl
     return out
+
+
+def lds_threads_for(slice_bytes: int, wave_bytes: int) -> int:
+    """Workgroup size of k_stage_lds for a slice: one wave per ~wave_bytes of slice (1, 2 or 4
+    waves), so long short-documents keep several waves per CU busy on one slice."""
+    if wave_bytes <= 0:
+        return 64
+    nw = -(-slice_bytes // wave_bytes)
+    return 64 if nw <= 1 else 128 if nw <= 2 else 256
 
 
 def lds_waves_for(slice_bytes: int, mode: str) -> int:
@@ -487,6 +496,7 @@ class DeviceRunner:
         self.lds_waves = os.environ.get("TB_LDS_WAVES", "auto")
         if self.lds_waves not in ("auto", "0", "4", "8"):
             raise DeviceError("TB_LDS_WAVES must be auto, 0, 4 or 8")
+        self.lds_wave_bytes = int(os.environ.get("TB_LDS_WAVE_BYTES", "10240"))
         self.retry_grid = int(os.environ.get("TB_RETRY_GRID", "1024"))
         self.retry_slice = int(h.scratch_bytes_for(max(self.long_doc_bytes, 1) + 16)) // SCRATCH_ALIGN * SCRATCH_ALIGN + SCRATCH_ALIGN
         # the cooperative-gather bag keeps its sums in registers; LDS holds only the cut offset
@@ -794,7 +804,8 @@ class DeviceRunner:
                                                       self.lds_ratio):
                             self.k.stage_lds(self.plan_t, self.stage_ts[s], vb, vo, d_perm, n_mid + p0, p1 - p0, ndocs,
                                              rec, flags, sl, retry_cnt, retry_pos, prof, skip,
-                                             lds_waves_for(sl, self.lds_waves))
+                                             lds_waves_for(sl, self.lds_waves),
+                                             lds_threads_for(sl, self.lds_wave_bytes))
                         self.k.stage_retry(self.plan_t, self.stage_ts[s], vb, vo, d_perm, ndocs, slot.retry_scratch,
                                            self.retry_slice, min(self.retry_grid, nshort), pw, pw_n, rec, flags,
                                            self.lds_bytes, retry_cnt, retry_pos, prof)

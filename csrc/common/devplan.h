@@ -62,7 +62,16 @@ struct DevStopSet {
   uint8_t blob[kStopBlobBytes];
   int32_t lite_nslots;  // 0: the set is too large for the compact form
   uint32_t lite_slots[kStopLiteMaxSlots];
+  // ASCII words of <= 7 bytes: key = bytes (little endian) | length << 56, open addressing on
+  // stop_fast_slot (lite_nslots entries, 0 = empty). An ASCII word of <= 7 bytes is a stop word
+  // iff its lowercase key is here (no other entry can equal it), so those need no byte compare.
+  uint64_t fast_keys[kStopLiteMaxSlots];
 };
+
+TB_HD uint32_t stop_fast_slot(uint64_t key, uint32_t nslots) {
+  uint64_t h = key * 0x9E3779B97F4A7C15ull;
+  return (uint32_t)(h >> 40) & (nslots - 1);
+}
 
 struct DevC4 {
   int32_t split_paragraph, remove_citations, filter_no_terminal_punct;

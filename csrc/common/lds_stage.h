@@ -34,6 +34,11 @@
 namespace tb {
 
 constexpr uint32_t kLdsMaxDoc = 65535;  // 16-bit byte offsets
+#ifndef TB_LDS_SCAN_WORDS
+#define TB_LDS_SCAN_WORDS 0
+#endif
+// 1: the segmented-scan word pass for every policy (A/B against the chunked-ballot pass)
+constexpr bool kLdsScanWords = TB_LDS_SCAN_WORDS != 0;
 
 // ---- LDS atomics (relaxed, workgroup scope; lanes of one instruction serialise per address) ----
 TB_HD uint32_t l_cas(TB_LDS uint32_t* p, uint32_t cmp, uint32_t v) {
@@ -104,11 +109,20 @@ TB_HD uint32_t l_utf8_decode(TB_LDS const uint8_t* s, uint32_t i, uint32_t n, in
 TB_HD uint64_t l_span_key(TB_LDS const uint8_t* b, uint32_t s, uint32_t e) {
   uint64_t h = 0x243F6A8885A308D3ull ^ ((uint64_t)(e - s) * 0x9E3779B97F4A7C15ull);
   uint32_t i = s;
-  for (; i + 4 <= e; i += 4) {
-    h ^= l_ld32(b, i);
+  auto step = [&](uint32_t u) {
+    h ^= u;
     h *= 0xff51afd7ed558ccdull;
     h ^= h >> 31;
+  };
+  // 16 bytes per iteration: four independent LDS reads in flight before the (serial) mixing
+  for (; i + 16 <= e; i += 16) {
+    const uint32_t u0 = l_ld32(b, i), u1 = l_ld32(b, i + 4), u2 = l_ld32(b, i + 8), u3 = l_ld32(b, i + 12);
+    step(u0);
+    step(u1);
+    step(u2);
+    step(u3);
   }
+  for (; i + 4 <= e; i += 4) step(l_ld32(b, i));
   if (i < e) {
     const uint32_t r = e - i;
     h ^= (uint64_t)(l_ld32(b, i) & (0xFFFFFFFFu >> (32 - 8 * r))) | ((uint64_t)r << 40);
@@ -121,6 +135,12 @@ TB_HD bool l_bytes_eq(TB_LDS const uint8_t* b, uint32_t a0, uint32_t a1, uint32_
   if (a1 - a0 != b1 - b0) return false;
   const uint32_t n = a1 - a0;
   uint32_t i = 0;
+  for (; i + 16 <= n; i += 16) {
+    const uint32_t d = (l_ld32(b, a0 + i) ^ l_ld32(b, b0 + i)) | (l_ld32(b, a0 + i + 4) ^ l_ld32(b, b0 + i + 4)) |
+                       (l_ld32(b, a0 + i + 8) ^ l_ld32(b, b0 + i + 8)) |
+                       (l_ld32(b, a0 + i + 12) ^ l_ld32(b, b0 + i + 12));
+    if (d) return false;
+  }
   for (; i + 4 <= n; i += 4)
     if (l_ld32(b, a0 + i) != l_ld32(b, b0 + i)) return false;
   if (i < n) {
@@ -325,6 +345,7 @@ TB_HD bool l_is_stop(const UcdView& ucd, const DevStopSet& ss, TB_LDS const uint
 struct LStop {
   uint32_t nslots = 0;
   int32_t max_len = 0;
+  TB_LDS const uint64_t* fast = nullptr;
   TB_LDS const uint32_t* slots = nullptr;
   TB_LDS const uint16_t* off = nullptr;
   TB_LDS const uint8_t* blob = nullptr;
@@ -333,17 +354,22 @@ struct LStop {
 template <class P>
 TB_HD bool l_stop_load(LCtx<P>& x, const DevStopSet& ss, LStop& out) {
   const uint32_t ns = (uint32_t)ss.lite_nslots, nw = (uint32_t)ss.n, nb = (uint32_t)ss.off[nw];
+  TB_LDS uint64_t* fk = x.a.template get<uint64_t>(ns);
   TB_LDS uint32_t* sl = x.a.template get<uint32_t>(ns);
   TB_LDS uint16_t* of = x.a.template get<uint16_t>(nw + 1);
   TB_LDS uint8_t* bl = x.a.template get<uint8_t>(nb + 1);
   if (x.a.ovf) return false;
-  x.par.for_n(ns, [&](uint32_t i) { sl[i] = ss.lite_slots[i]; });
+  x.par.for_n(ns, [&](uint32_t i) {
+    sl[i] = ss.lite_slots[i];
+    fk[i] = ss.fast_keys[i];
+  });
   x.par.for_n(nw + 1, [&](uint32_t i) { of[i] = (uint16_t)ss.off[i]; });
   x.par.for_n(nb, [&](uint32_t i) { bl[i] = ss.blob[i]; });
   x.par.sync();
   out.nslots = ns;
   out.max_len = ss.max_len;
   out.slots = sl;
+  out.fast = fk;
   out.off = of;
   out.blob = bl;
   return true;
@@ -353,6 +379,26 @@ TB_HD bool l_stop_load(LCtx<P>& x, const DevStopSet& ss, LStop& out) {
 TB_HD bool l_is_stop_lite(const UcdView& ucd, const LStop& st, TB_LDS const uint8_t* b, uint32_t nb, uint32_t s,
                           uint32_t e, uint32_t ncp) {
   if (st.nslots == 0 || (int32_t)ncp > st.max_len) return false;
+  if (e - s <= 7) {
+    // ASCII words of <= 7 bytes: lowercase 8 bytes at once (SWAR) and look the key up
+    const uint32_t len = e - s;
+    uint64_t v = (uint64_t)l_ld32(b, s) | ((uint64_t)l_ld32(b, s + 4) << 32);
+    v &= len ? (~0ull >> (64 - 8 * len)) : 0ull;
+    if ((v & 0x8080808080808080ull) == 0) {
+      const uint64_t hb = 0x8080808080808080ull;
+      const uint64_t ge_a = (v | hb) - 0x4141414141414141ull;  // high bit: byte >= 'A'
+      const uint64_t ge_z = (v | hb) - 0x5B5B5B5B5B5B5B5Bull;  // high bit: byte > 'Z'
+      const uint64_t up = ge_a & ~ge_z & hb;
+      const uint64_t key = (v | (up >> 2)) | ((uint64_t)len << 56);
+      uint32_t slot = stop_fast_slot(key, st.nslots);
+      while (true) {
+        const uint64_t k = st.fast[slot];
+        if (k == key) return true;
+        if (k == 0) return false;
+        slot = (slot + 1) & (st.nslots - 1);
+      }
+    }
+  }
   uint32_t h = kStopLiteHash0, len = 0;
   l_lower_bytes(ucd, b, nb, s, e, [&](uint8_t v) { h = stop_lite_hash_push(h, v); ++len; });
   uint32_t slot = stop_lite_slot(h, st.nslots);
@@ -419,6 +465,38 @@ TB_HD bool l_canon(LCtx<P>& x, uint32_t N, KeyF&& key, EqF&& eq, TB_LDS uint16_t
   x.par.sync();
   x.a.reset(m);
   return true;
+}
+
+// Classes of N items without the resolve pass: cls[i] = the table slot of i's class (a
+// canonical identifier: equal items <-> equal slot, < capn), and cnt[slot] = the class size.
+// tab / cnt hold >= capn = N + N/2 + 2 entries (the caller's arrays).
+template <class P, class KeyF, class EqF>
+TB_HD void l_classes(LCtx<P>& x, uint32_t N, KeyF&& key, EqF&& eq, TB_LDS uint32_t* tab, TB_LDS uint32_t* cnt,
+                     TB_LDS uint16_t* cls) {
+  const uint32_t capn = N + (N >> 1) + 2;
+  x.par.for_n(capn, [&](uint32_t i) {
+    tab[i] = 0;
+    cnt[i] = 0;
+  });
+  x.par.sync();
+  x.par.for_n(N, [&](uint32_t i) {
+    const uint64_t k = key(i);
+    const uint32_t fp = (uint32_t)(k >> 48);
+    const uint32_t mine = (fp << 16) | (i + 1);
+    uint32_t slot = (uint32_t)(((k & 0xFFFFFFFFull) * capn) >> 32);
+    while (true) {
+      uint32_t cur = tab[slot];
+      if (cur == 0) {
+        cur = l_cas(&tab[slot], 0u, mine);
+        if (cur == 0) break;
+      }
+      if ((cur >> 16) == fp && eq(i, (cur & 0xFFFFu) - 1u)) break;
+      if (++slot == capn) slot = 0;
+    }
+    l_add(&cnt[slot], 1u);
+    cls[i] = (uint16_t)slot;
+  });
+  x.par.sync();
 }
 
 // find_duplicates over N byte spans: (#repeats, sum of repeat byte lengths).
@@ -492,15 +570,31 @@ struct LWords {
 };
 
 template <class P>
+TB_HD bool l_words_chunks(LCtx<P>& x, const LCps& c, bool store, const DevStopSet* ss, LWords& out, bool use_lite,
+                          LStop lite);
+
+template <class P>
 TB_HD bool l_words(LCtx<P>& x, const LCps& c, bool store, const DevStopSet* ss, LWords& out,
                    bool use_lite = false, LStop lite = LStop{}) {
+  if constexpr (P::kChunks) {
+    if (!kLdsScanWords) return l_words_chunks(x, c, store, ss, out, use_lite, lite);
+  }
   const uint32_t C = c.n;
   const auto m = x.a.mark();
   TB_LDS uint32_t* wbm = x.a.template get_hi<uint32_t>(mask_words(C + 1));
   if (x.a.ovf) return false;
   const LAcc acc{c.ent};
+  // the window i-2 .. i+1 comes from four independent LDS reads; the look-around of wb_break
+  // runs only where the window holds Extend/Format/ZWJ/RI
   x.par.mask_store(
-      C + 1, [&](uint32_t i) { return i == 0 || i == C || wb_break(acc, (int)C, (int)i); },
+      C + 1,
+      [&](uint32_t i) {
+        if (i == 0 || i >= C) return true;
+        const uint32_t pm2 = i >= 2 ? c.p(i - 2) : 0xFFFFFFFFu;
+        const uint32_t pp1 = i + 1 < C ? c.p(i + 1) : 0xFFFFFFFFu;
+        const int r = wb_break_ctx(pm2, c.p(i - 1), c.p(i), pp1);
+        return r == 2 ? wb_break(acc, (int)C, (int)i) : r != 0;
+      },
       [&](uint32_t w, uint32_t v) { wbm[w] = v; });
   x.par.sync();
   x.stamp(PH_W_MASK);
@@ -550,6 +644,162 @@ TB_HD bool l_words(LCtx<P>& x, const LCps& c, bool store, const DevStopSet* ss, 
   x.par.sync();
   // release the mask (the words, if stored, stay: they were allocated after the mark's lo)
   x.a.hi = m.hi;
+  out.w = words;
+  return true;
+}
+
+// l_words by chunked ballots (policies with P::kChunks): per chunk of 64 code points four
+// 64-bit masks (break before, non-whitespace, word char, alphabetic) and per-lane bit arithmetic
+// replace the segmented scan over a 12-byte state: a word is a segment (between consecutive
+// breaks) with a word char, trimmed to its first and last non-whitespace code point. The segment
+// still open at a chunk's end is carried in uniform state. Pass 1 finds the breaks (stored as a
+// bitmask) and counts the words (one per segment: its first word char); pass 2 emits them.
+TB_HD uint64_t lmask(uint32_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1); }  // bits [0, k)
+TB_HD uint32_t hibit(uint64_t v) { return 63u - (uint32_t)__builtin_clzll(v); }
+TB_HD uint32_t lobit(uint64_t v) { return (uint32_t)__builtin_ctzll(v); }
+
+template <class P>
+TB_HD bool l_words_chunks(LCtx<P>& x, const LCps& c, bool store, const DevStopSet* ss, LWords& out, bool use_lite,
+                          LStop lite) {
+  const uint32_t C = c.n;
+  const auto m = x.a.mark();
+  const uint32_t nwm = mask_words(C + 1);
+  TB_LDS uint32_t* wbm = x.a.template get_hi<uint32_t>(nwm);
+  if (x.a.ovf) return false;
+  const LAcc acc{c.ent};
+  // ---- pass 1: break mask + word count ----
+  bool open_wc = false;
+  const uint32_t W = x.par.chunks(
+      C,
+      [&](uint32_t i) -> uint32_t {
+        const uint32_t p0 = c.p(i);
+        bool brk = true;
+        if (i > 0) {
+          const uint32_t pm2 = i >= 2 ? c.p(i - 2) : 0xFFFFFFFFu;
+          const uint32_t pp1 = i + 1 < C ? c.p(i + 1) : 0xFFFFFFFFu;
+          const int r = wb_break_ctx(pm2, c.p(i - 1), p0, pp1);
+          brk = r == 2 ? wb_break(acc, (int)C, (int)i) : r != 0;
+        }
+        const bool ws = is_ws(p0);
+        const bool wc = !(p0 & P_PUNCT) && !ws;
+        return (brk ? 1u : 0u) | (wc ? 2u : 0u);
+      },
+      [&](uint32_t, uint32_t l, const uint64_t* mm) {  // the first word char of its segment
+        if (!((mm[1] >> l) & 1u)) return false;
+        const uint64_t below = mm[0] & lmask(l + 1);
+        if (below) return (mm[1] & lmask(l) & ~lmask(hibit(below))) == 0;
+        return !open_wc && (mm[1] & lmask(l)) == 0;
+      },
+      [&](uint32_t, uint32_t, const uint64_t*, uint32_t) {},
+      [&](uint32_t base, const uint64_t* mm) {
+        x.par.single([&]() {
+          wbm[base >> 5] = (uint32_t)mm[0];
+          wbm[(base >> 5) + 1] = (uint32_t)(mm[0] >> 32);
+        });
+        if (mm[0]) open_wc = (mm[1] & ~lmask(hibit(mm[0]))) != 0;
+        else open_wc = open_wc || mm[1] != 0;
+      });
+  x.par.single([&]() {  // the end-of-text break (bit C), in a word pass 1 may not have written
+    if ((C & 63u) == 0) {
+      wbm[C >> 5] = 0;
+      wbm[(C >> 5) + 1] = 0;
+    }
+    wbm[C >> 5] |= 1u << (C & 31);
+  });
+  x.par.sync();
+  x.stamp(PH_W_MASK);
+  TB_LDS uint32_t* words = nullptr;
+  if (store) {
+    words = x.a.template get<uint32_t>(W + 1);
+    if (x.a.ovf) return false;
+  }
+  // ---- pass 2: emit (spans, GopherQuality sums) ----
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  uint32_t o_first = kNone, o_last = 0;
+  bool o_wc = false, o_al = false;
+  const uint32_t nb = c.nb;
+  TB_LDS const uint8_t* b = c.b;
+  uint32_t chars = 0, alpha = 0, stop = 0;
+  const UcdView ucd = x.ucd;
+  auto bmask = [&](uint32_t base) {
+    return (uint64_t)wbm[base >> 5] | ((uint64_t)wbm[(base >> 5) + 1] << 32);
+  };
+  auto next_brk = [&](uint32_t base) { return base + 64 <= C ? (wbm[(base + 64) >> 5] & 1u) : 1u; };
+  // the segment ending at lane l: first / last non-whitespace code point, word char, alphabetic
+  auto segment = [&](uint32_t base, uint32_t l, const uint64_t* mm, uint32_t& first, uint32_t& last, bool& wc,
+                     bool& al) {
+    const uint64_t B = bmask(base);
+    const uint64_t below = B & lmask(l + 1);
+    const bool carried = below == 0;
+    const uint64_t seg = lmask(l + 1) & (carried ? ~0ull : ~lmask(hibit(below)));
+    const uint64_t nws = mm[0] & seg;
+    wc = (mm[1] & seg) != 0 || (carried && o_wc);
+    al = (mm[2] & seg) != 0 || (carried && o_al);
+    first = (carried && o_first != kNone) ? o_first : (nws ? base + lobit(nws) : kNone);
+    last = nws ? base + hibit(nws) + 1 : (carried ? o_last : 0u);
+  };
+  const uint32_t got = x.par.chunks(
+      C,
+      [&](uint32_t i) -> uint32_t {
+        const uint32_t p0 = c.p(i);
+        const bool ws = is_ws(p0);
+        return (ws ? 0u : 1u) | ((!(p0 & P_PUNCT) && !ws) ? 2u : 0u) | ((p0 & P_ALPHA) ? 4u : 0u);
+      },
+      [&](uint32_t i, uint32_t l, const uint64_t* mm) {
+        const uint32_t base = i - l;
+        const uint64_t E = (bmask(base) >> 1) | ((uint64_t)next_brk(base) << 63);
+        if (!((E >> l) & 1u)) return false;
+        uint32_t first, last;
+        bool wc, al;
+        segment(base, l, mm, first, last, wc, al);
+        return wc;
+      },
+      [&](uint32_t i, uint32_t l, const uint64_t* mm, uint32_t k) {
+        uint32_t first, last;
+        bool wc, al;
+        segment(i - l, l, mm, first, last, wc, al);
+        const uint32_t bs = c.o(first), be = c.o(last);
+        if (store && k < W) words[k] = bs | (be << 16);
+        if (ss) {
+          chars += last - first;
+          alpha += al ? 1u : 0u;
+          const bool st = use_lite ? l_is_stop_lite(ucd, lite, b, nb, bs, be, last - first)
+                                   : l_is_stop(ucd, *ss, b, nb, bs, be, last - first);
+          stop += st ? 1u : 0u;
+        }
+      },
+      [&](uint32_t base, const uint64_t* mm) {
+        if (next_brk(base)) {  // the next chunk starts a new segment
+          o_first = kNone;
+          o_last = 0;
+          o_wc = o_al = false;
+          return;
+        }
+        const uint64_t B = bmask(base);
+        uint64_t seg = ~0ull;
+        if (B) {
+          seg = ~lmask(hibit(B));
+          o_first = kNone;
+          o_last = 0;
+          o_wc = o_al = false;
+        }
+        const uint64_t nws = mm[0] & seg;
+        o_wc = o_wc || (mm[1] & seg) != 0;
+        o_al = o_al || (mm[2] & seg) != 0;
+        if (nws) {
+          if (o_first == kNone) o_first = base + lobit(nws);
+          o_last = base + hibit(nws) + 1;
+        }
+      });
+  if (got != W) return false;  // the passes disagree: never expected; the generic path decides
+  if (ss) {
+    out.chars = x.par.reduce_add((int64_t)chars);
+    out.alpha = x.par.reduce_add((int64_t)alpha);
+    out.stop = x.par.reduce_add((int64_t)stop);
+  }
+  x.par.sync();
+  x.a.hi = m.hi;
+  out.n = W;
   out.w = words;
   return true;
 }
@@ -706,46 +956,54 @@ TB_HD bool l_gopher_rep(LCtx<P>& x, const DevStep& ds, const LCps& c, const LWor
   x.par.single([&]() { SK[W] = sktot; });
   x.par.sync();
   x.stamp(PH_GR_WORDS);
-  // Top n-grams: the n-gram at p is the pair (id of the (n-1)-gram at p, id of word p+n-1): one
-  // exact pair canonicalisation per order.
+  // Top n-grams: the n-gram at p is the pair (class of the (n-1)-gram at p, id of word p+n-1):
+  // per order one exact pair classification that also counts the classes (l_classes: the table
+  // slot is the class id, no resolve pass), then two reductions.
   if (ds.n_top > 0) {
     int max_top = 0;
     for (int t = 0; t < ds.n_top; ++t) max_top = ds.top_n[t] > max_top ? ds.top_n[t] : max_top;
     const auto m2 = x.a.mark();
+    const uint32_t capw = W + (W >> 1) + 2;
     TB_LDS uint16_t* ga = x.a.template get<uint16_t>(W + 1);
     TB_LDS uint16_t* gb = x.a.template get<uint16_t>(W + 1);
-    TB_LDS uint32_t* cnt = x.a.template get<uint32_t>(W + 1);
-    if (x.a.ovf) return false;
+    TB_LDS uint32_t* cnt = x.a.template get<uint32_t>(capw);
+    TB_LDS uint32_t* tab = x.a.template get_hi<uint32_t>(capw);
+    if (x.a.ovf || W >= 43000u) return false;
     TB_LDS const uint16_t* gprev = wid;
     for (uint32_t n = 1; n <= (uint32_t)max_top && W >= n; ++n) {
       const uint32_t G = W - n + 1;
       TB_LDS const uint16_t* gc = wid;
-      if (n > 1) {
+      uint32_t ncls;  // class ids are < ncls
+      if (n == 1) {
+        // words: classes = canonical word ids; counted directly
+        x.par.for_n(W, [&](uint32_t p) { cnt[p] = 0; });
+        x.par.sync();
+        x.par.for_n(W, [&](uint32_t p) { l_add(&cnt[wid[p]], 1u); });
+        x.par.sync();
+        ncls = W;
+      } else {
         TB_LDS uint16_t* gcur = (n & 1) ? ga : gb;
-        if (!l_canon(
-                x, G,
-                [&](uint32_t p) {
-                  return mix64(((uint64_t)gprev[p] << 32) ^ (uint64_t)wid[p + n - 1] ^ ((uint64_t)n << 60));
-                },
-                [&](uint32_t p, uint32_t q) { return gprev[p] == gprev[q] && wid[p + n - 1] == wid[q + n - 1]; },
-                gcur))
-          return false;
+        l_classes(
+            x, G,
+            [&](uint32_t p) {
+              return mix64(((uint64_t)gprev[p] << 32) ^ (uint64_t)wid[p + n - 1] ^ ((uint64_t)n << 60));
+            },
+            [&](uint32_t p, uint32_t q) { return gprev[p] == gprev[q] && wid[p + n - 1] == wid[q + n - 1]; },
+            tab, cnt, gcur);
         gc = gcur;
         gprev = gcur;
+        ncls = G + (G >> 1) + 2;
         x.stamp(PH_GR_TOP_CANON);
       }
       bool wanted = false;
       for (int t = 0; t < ds.n_top; ++t) wanted |= ds.top_n[t] == (int32_t)n;
       if (!wanted) continue;
-      x.par.for_n(G, [&](uint32_t p) { cnt[p] = 0; });
-      x.par.sync();
-      x.par.for_n(G, [&](uint32_t p) { l_add(&cnt[gc[p]], 1u); });
-      x.par.sync();
-      const uint32_t maxc = x.par.template max<uint32_t>(G, 0u, [&](uint32_t p) { return cnt[p]; });
+      const uint32_t maxc = x.par.template max<uint32_t>(ncls, 0u, [&](uint32_t k) { return cnt[k]; });
       int64_t v = 0;
       if (maxc > 1) {
+        // the longest gram among the most frequent (equal grams have equal lengths)
         const uint32_t maxlen = x.par.template max<uint32_t>(G, 0u, [&](uint32_t p) {
-          return cnt[p] == maxc ? ((uint32_t)WL[p + n] - (uint32_t)WL[p] + n - 1) : 0u;
+          return cnt[gc[p]] == maxc ? ((uint32_t)WL[p + n] - (uint32_t)WL[p] + n - 1) : 0u;
         });
         v = (int64_t)maxlen * (int64_t)maxc;
       }
@@ -812,8 +1070,11 @@ TB_HD bool l_gopher_rep(LCtx<P>& x, const DevStep& ds, const LCps& c, const LWor
                 if (tq != t) return false;
                 const uint32_t L = (uint32_t)WL[p + n] - (uint32_t)WL[p];
                 if ((uint32_t)WL[q + n] - (uint32_t)WL[q] != L) return false;
-                uint32_t dw = 0;
-                for (uint32_t k = 0; k < n; ++k) dw |= (uint32_t)(wid[p + k] ^ wid[q + k]);
+                uint32_t dw = 0, k = 0;
+                for (; k + 4 <= n; k += 4)  // four id pairs per iteration, loads issued together
+                  dw |= (uint32_t)((wid[p + k] ^ wid[q + k]) | (wid[p + k + 1] ^ wid[q + k + 1]) |
+                                   (wid[p + k + 2] ^ wid[q + k + 2]) | (wid[p + k + 3] ^ wid[q + k + 3]));
+                for (; k < n; ++k) dw |= (uint32_t)(wid[p + k] ^ wid[q + k]);
                 if (dw == 0) return true;
                 // different word splits: compare the concatenations byte by byte
                 uint32_t wp = p, wq = q, bp = ws(p), bq = ws(q);

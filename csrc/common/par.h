@@ -120,6 +120,30 @@ struct SeqPar {
   uint32_t reduce_or(uint32_t v) const { return v; }
   template <class T>
   T reduce_add(T v) const { return v; }
+  // Chunked ballots (the WavePar loop, run sequentially): per chunk of 64 items, bits(i) gives up
+  // to 4 predicate bits per item, m[k] = the chunk's 64-bit mask of bit k; sel(i, l, m) picks items,
+  // emit(i, l, m, rank) runs for the picked ones in item order, then uni(base, m) once per chunk
+  // (state carried between chunks). Returns the number picked.
+  static constexpr bool kChunks = true;
+  template <class Bits, class Sel, class Emit, class Uni>
+  uint32_t chunks(uint32_t n, Bits&& bits, Sel&& sel, Emit&& emit, Uni&& uni) const {
+    uint32_t k = 0;
+    for (uint32_t base = 0; base < n; base += 64) {
+      uint64_t m[4] = {0, 0, 0, 0};
+      for (uint32_t l = 0; l < 64; ++l) {
+        const uint32_t i = base + l;
+        const uint32_t b = i < n ? bits(i) : 0u;
+        for (int q = 0; q < 4; ++q)
+          if ((b >> q) & 1u) m[q] |= 1ull << l;
+      }
+      for (uint32_t l = 0; l < 64; ++l) {
+        const uint32_t i = base + l;
+        if (i < n && sel(i, l, m)) emit(i, l, m, k++);
+      }
+      uni(base, m);
+    }
+    return k;
+  }
   void sync() const {}
   static uint64_t clock() { return 0; }
   template <class F>
@@ -390,6 +414,27 @@ struct WavePar {
   }
   template <class T>
   __device__ __forceinline__ T reduce_add(T v) const { return wave_sum(v); }
+  static constexpr bool kChunks = true;
+  template <class Bits, class Sel, class Emit, class Uni>
+  __device__ __forceinline__ uint32_t chunks(uint32_t n, Bits&& bits, Sel&& sel, Emit&& emit, Uni&& uni) const {
+    uint32_t k = 0;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t i = base + lane;
+      const uint32_t b = i < n ? bits(i) : 0u;
+      uint64_t m[4];
+      m[0] = __ballot(b & 1u);
+      m[1] = __ballot(b & 2u);
+      m[2] = __ballot(b & 4u);
+      m[3] = __ballot(b & 8u);
+      const bool s = i < n && sel(i, lane, m);
+      const uint64_t sm = __ballot(s);
+      if (s) emit(i, lane, m, k + (uint32_t)__popcll(sm & lt));
+      k += (uint32_t)__popcll(sm);
+      uni(base, m);
+    }
+    return k;
+  }
   template <class Pred>
   __device__ __forceinline__ void mask_bits(uint32_t n, Pred&& pred, uint32_t* bits) const {
     for (uint32_t base = 0; base < n; base += 64 * kU) {
@@ -503,6 +548,7 @@ template <int NT>
 struct BlockPar {
   static_assert(NT % 64 == 0 && NT >= 128 && NT <= 1024, "block of whole waves");
   static constexpr int NW = NT / 64;
+  static constexpr bool kChunks = false;
 #ifdef TB_NO_PART_TABLES
   static constexpr bool kPartTables = false;
 #else
@@ -714,6 +760,7 @@ struct SegPar {
   static_assert(NT % 64 == 0 && NT >= 128 && NT <= 1024, "block of whole waves");
   static constexpr int NW = NT / 64;
   static constexpr bool kPartTables = false;
+  static constexpr bool kChunks = false;
   uint32_t tid, lane, wid;
   char* xs = nullptr;
   mutable uint32_t gen = 0;

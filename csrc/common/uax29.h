@@ -97,6 +97,47 @@ TB_HD bool wb_break(const A& a, int n, int i) {
   return true;                                                             // WB999
 }
 
+// wb_break from the properties of code points i-2, i-1, i, i+1 alone (pm2 / pp1 = 0xFFFFFFFF when
+// out of range), for positions whose window holds no Extend/Format/ZWJ/RI: then the effective
+// left contexts are i-1 and i-2 and the effective right context is i+1, so every rule is decided
+// from registers. Returns 0 / 1, or 2 when the window needs the general look-around.
+TB_HD int wb_break_ctx(uint32_t pm2, uint32_t pm1, uint32_t p0, uint32_t pp1) {
+  const int L0 = wb_of(pm1), R = wb_of(p0);
+  if (L0 == WB_ALetter) {  // the common pairs first (as wb_break)
+    if (R == WB_ALetter) return 0;
+    if (R == WB_WSegSpace) return 1;
+  } else if (L0 == WB_WSegSpace && R == WB_ALetter) {
+    return 1;
+  }
+  const int LL0 = pm2 == 0xFFFFFFFFu ? -1 : wb_of(pm2);
+  const int RR = pp1 == 0xFFFFFFFFu ? -1 : wb_of(pp1);
+  auto special = [](int c) { return c == WB_Extend || c == WB_Format || c == WB_ZWJ || c == WB_RI; };
+  if (special(L0) || special(R) || (LL0 >= 0 && special(LL0)) || (RR >= 0 && special(RR))) return 2;
+  if (L0 == WB_CR && R == WB_LF) return 0;      // WB3
+  if (wb_nl(L0)) return 1;                      // WB3a
+  if (wb_nl(R)) return 1;                       // WB3b
+  if (L0 == WB_WSegSpace && R == WB_WSegSpace) return 0;  // WB3d
+  const int L = L0;                             // not a newline here
+  // left2(): Other when there is no i-2 or L is Other (wb_break's definition)
+  const int LL = (LL0 < 0 || L == WB_Other) ? (int)WB_Other : LL0;
+  if (wb_ah(L) && wb_ah(R)) return 0;                                   // WB5
+  if (wb_ah(L) && wb_midletq(R) && wb_ah(RR)) return 0;                 // WB6
+  if (wb_midletq(L) && wb_ah(R) && wb_ah(LL)) return 0;                 // WB7
+  if (L == WB_Hebrew && R == WB_SQ) return 0;                           // WB7a
+  if (L == WB_Hebrew && R == WB_DQ && RR == WB_Hebrew) return 0;        // WB7b
+  if (L == WB_DQ && R == WB_Hebrew && LL == WB_Hebrew) return 0;        // WB7c
+  if (L == WB_Numeric && R == WB_Numeric) return 0;                     // WB8
+  if (wb_ah(L) && R == WB_Numeric) return 0;                            // WB9
+  if (L == WB_Numeric && wb_ah(R)) return 0;                            // WB10
+  if (wb_midnumq(L) && R == WB_Numeric && LL == WB_Numeric) return 0;   // WB11
+  if (L == WB_Numeric && wb_midnumq(R) && RR == WB_Numeric) return 0;   // WB12
+  if (L == WB_Katakana && R == WB_Katakana) return 0;                   // WB13
+  if ((wb_ah(L) || L == WB_Numeric || L == WB_Katakana || L == WB_ExtendNumLet) && R == WB_ExtendNumLet)
+    return 0;                                                           // WB13a
+  if (L == WB_ExtendNumLet && (wb_ah(R) || R == WB_Numeric || R == WB_Katakana)) return 0;  // WB13b
+  return 1;                                                             // WB999
+}
+
 // ---------------------------------------------------------------------------------------------
 // Sentence boundaries.
 TB_HD bool sb_ign(int c) { return c == SB_Extend || c == SB_Format; }

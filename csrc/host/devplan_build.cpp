@@ -79,6 +79,16 @@ static int add_stop_set(DevPlan& plan, const std::vector<std::string>& words) {
       uint32_t slot = stop_lite_slot(h, ns);
       while (ss.lite_slots[slot] != 0) slot = (slot + 1) & (ns - 1);
       ss.lite_slots[slot] = (h & 0xFFFF0000u) | (uint32_t)(i + 1);
+      const std::string& w = uniq[i];
+      bool ascii = !w.empty() && w.size() <= 7;
+      for (unsigned char c : w) ascii = ascii && c < 0x80;
+      if (ascii) {
+        uint64_t key = (uint64_t)w.size() << 56;
+        for (size_t k = 0; k < w.size(); ++k) key |= (uint64_t)(unsigned char)w[k] << (8 * k);
+        uint32_t fs = stop_fast_slot(key, ns);
+        while (ss.fast_keys[fs] != 0) fs = (fs + 1) & (ns - 1);
+        ss.fast_keys[fs] = key;
+      }
     }
   }
   return plan.n_stop_sets++;

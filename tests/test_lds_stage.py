@@ -22,16 +22,28 @@ def _corpus():
     rng = np.random.default_rng(3)
     words = "the cat sat on the mat and the dog ran".split()
     rep = [" ".join(rng.choice(words[:int(rng.integers(2, 10))], size=int(rng.integers(20, 400)))) for _ in range(150)]
-    return (synth.make_corpus(1200, 1100, seed=5) + EDGE + adversarial_corpus() + rep
+    danish = ["Jeg er ikke sikker på, at det er det rigtige. Det var også godt, når vi KAN være der.",
+              "OG SÅ VAR DER IKKE MERE. Hun havde været der før, men ikke siden.",
+              "Være eller ikke være, det er spørgsmålet. Også HER."]
+    # segments longer than a 64-code-point chunk: long words, URLs, whitespace and punctuation
+    # runs, word chars after long non-word runs (state carried across chunks)
+    long_tokens = ["a" * 70 + " b", "x " + "y" * 130 + ".", "http://example.com/" + "q" * 150 + " end.",
+                   " " * 150 + "word " + "\t" * 70 + "more", "." * 200 + "x", "-" * 90 + "ab" + "," * 70,
+                   "\u0301" * 80 + "a", " " + "\u0301" * 70 + " x", "word" + "\u00e6" * 100 + " z",
+                   ("ab" * 40 + " ") * 5, "1" * 100 + ".5 " + "2,000" * 30]
+    return (synth.make_corpus(1200, 1100, seed=5) + EDGE + adversarial_corpus() + rep + danish * 3 + long_tokens
             + ["ab c a bc ab c a bc " * 20, "a b a b a b a b a b a b a b a b", "x y z\n\nx y z\nx y z",
                "abab ab ab abab " * 30, "aa aaa a aaaa aa a aaa " * 25])
 
 
-@pytest.fixture(scope="module")
-def setup(host):
+@pytest.fixture(scope="module", params=["config/bench_pipeline.yaml", "config/pipeline_config.yaml"])
+def setup(host, request):
+    """The bench pipeline (English stop words) and the reference default pipeline (Danish stop
+    words, some with non-ASCII letters)."""
     from textblaster_amd.models.langid import load_default
 
-    cfg = load_pipeline_config("config/bench_pipeline.yaml")
+    cfg = load_pipeline_config(request.param)
+    cfg.pipeline = [s for s in cfg.pipeline if s.type != "TokenCounter"]
     steps = [host.make_step(s.native_dict()) for s in cfg.pipeline]
     plan = build_plan(cfg)
     texts = _corpus()

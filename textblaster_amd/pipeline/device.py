@@ -790,7 +790,7 @@ class DeviceRunner:
                                              self.lds_bytes_mid, prof, self.stage_waves, n_mid - n_long, skip)
                         ev_blk = self._record(slot.s_blk)
                         keep.append(ev_blk)
-                if n_mid < ndocs and self.lds_stage and n_mid == n_long:
+                if n_mid < ndocs and self.lds_stage:
                     # LDS-resident kernel per length bucket, then the generic retry of the
                     # documents that did not fit their slice
                     nshort = ndocs - n_mid

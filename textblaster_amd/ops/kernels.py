@@ -120,6 +120,9 @@ class Kernels:
             # B^0..B^cap followed by B^-0..B^-cap (k_pow_table)
             self._pw = hiprt.empty(2 * cap + 2, np.int64)
             _check(self.lib.tb_pow_table(self.stream(), self._pw.data_ptr(), cap), "tb_pow_table")
+            # other slots' streams read the table right away with no event ordering them after
+            # the kernel that fills it: growth is rare (documents over ~2 MB), so wait for it here
+            hiprt.current_stream().synchronize()
             self._pw_n = cap
         return self._pw, self._pw_n
 

@@ -46,6 +46,7 @@ class Resolved:
     out_off: np.ndarray     # int64 [ndocs + 1]: start of output k (first nk + nx + 1 valid)
     rows: np.ndarray        # int32 [ndocs]: document of output k
     err: int = 0            # nonzero: the compaction ran out of room (never with the C4 bound)
+    ver: Optional[np.ndarray] = None  # uint8 [ndocs]: content version each document's output came from
 
     def parts(self):
         """(kept rows, kept offsets, kept text), (excluded ...) as views of the buffers."""
@@ -257,8 +258,8 @@ class PendingBatch:
         timings["gpu_wait"] = t1 - t0
         res = None
         if self._resolved is not None:
-            fail, st, out, out_off, rows, err = self._resolved
-            res = Resolved(fail, st, out, out_off, rows, int(err[0]))
+            fail, st, out, out_off, rows, err, ver = self._resolved
+            res = Resolved(fail, st, out, out_off, rows, int(err[0]), ver)
         return DeviceResult(stage_recs, c4_recs, host_versions, fl, timings, dead, self.runner.pass_of_step, res)
 
 
@@ -497,6 +498,8 @@ class DeviceRunner:
         if self.lds_waves not in ("auto", "0", "4", "8"):
             raise DeviceError("TB_LDS_WAVES must be auto, 0, 4 or 8")
         self.lds_wave_bytes = int(os.environ.get("TB_LDS_WAVE_BYTES", "10240"))
+        # buckets whose LDS slice would exceed this many bytes run the generic kernel instead (0: none)
+        self.lds_generic_above = int(os.environ.get("TB_LDS_GENERIC_ABOVE", "0"))
         self.retry_grid = int(os.environ.get("TB_RETRY_GRID", "1024"))
         self.retry_slice = int(h.scratch_bytes_for(max(self.long_doc_bytes, 1) + 16)) // SCRATCH_ALIGN * SCRATCH_ALIGN + SCRATCH_ALIGN
         # the cooperative-gather bag keeps its sums in registers; LDS holds only the cut offset
@@ -802,6 +805,14 @@ class DeviceRunner:
                     with self._ktimed(keep, f"stage{s}"):
                         for p0, p1, sl in lds_buckets(lens_perm[n_mid:], self.lds_per_byte, self.lds_fixed,
                                                       self.lds_ratio):
+                            if self.lds_generic_above and sl > self.lds_generic_above:
+                                # hybrid: this bucket's documents take the generic wave kernel
+                                # (HBM scratch arrays, small LDS slice, higher occupancy)
+                                a0 = n_mid + p0
+                                self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[a0:], ndocs,
+                                                     scratch, d_soff[a0:], pw, pw_n, rec, flags, None, lid_vec,
+                                                     lid_cnt, self.lds_bytes, prof, self.stage_waves, p1 - p0, skip)
+                                continue
                             self.k.stage_lds(self.plan_t, self.stage_ts[s], vb, vo, d_perm, n_mid + p0, p1 - p0, ndocs,
                                              rec, flags, sl, retry_cnt, retry_pos, prof, skip,
                                              lds_waves_for(sl, self.lds_waves),
@@ -900,7 +911,7 @@ class DeviceRunner:
                 self.k.resolve(self.resolve_t, recs, ndocs, flags.view(np.uint32), vlist, r_fail, r_status, r_ver,
                                r_lanes, r_sc, r_out, r_off, r_rows, r_err)
             keep += [r_fail, r_status, r_ver, r_lanes, r_sc, r_out, r_off, r_rows, r_err]
-            res_d = (r_fail, r_status, r_out, r_off, r_rows, r_err)
+            res_d = (r_fail, r_status, r_out, r_off, r_rows, r_err, r_ver)
         # D2H into pinned host buffers on the download stream (the slot's compute stream in the
         # 4-stream layout: it is last in line there anyway), then one completion event
         done = self._record(main)

@@ -209,7 +209,15 @@ class Engine:
         """process_many with a submitter thread: input staging (pinned copy + H2D) and kernel
         launches of the next batches run on their own thread while this thread resolves and
         assembles the current one, so the host critical path is max(staging, resolve+assemble)
-        instead of their sum. At most two batches wait in the hand-off queue."""
+        instead of their sum.
+
+        In flight: up to N_SLOTS - 1 submitted batches wait in the hand-off queue, plus the one the
+        submitter holds (blocked on put) and the one being collected, so N_SLOTS + 1 batches may be
+        outstanding while only N_SLOTS device slots exist. Reusing a slot is still safe: its pinned
+        staging buffer is rewritten only after the previous upload's h2d_done event, and its scratch
+        arena is written only by kernels ordered on the slot's stream behind the previous batch's
+        kernels. Batches dropped by an early exit are synchronised before their buffers go back to
+        the caching allocator (which does not track streams)."""
         import queue
         import threading
 
@@ -247,24 +255,50 @@ class Engine:
                     yield out
         finally:
             stop.set()
+            drained = []
             while th.is_alive():
                 try:
-                    q.get(timeout=0.05)
+                    drained.append(q.get(timeout=0.05))
                 except queue.Empty:
                     pass
             th.join()
+            while True:
+                try:
+                    drained.append(q.get_nowait())
+                except queue.Empty:
+                    break
+            if any(x is not _END for x in drained):
+                # submitted but never collected: their kernels and copies may still be running on
+                # buffers the caching allocator would hand out again once these objects die
+                sync = getattr(self.device_runner, "synchronize", None)
+                if sync is not None:
+                    sync()
+
+    # HBM scratch of the generic document kernels per device batch: 160 B per text byte plus a
+    # fixed ~14 KB per document (csrc/common/devplan.h scratch_bytes_for_dev); DeviceRunner sizes
+    # its slots for 1.25 x 160 x max_batch_bytes, so batches of many short documents are also cut
+    # at that scratch budget (a 384 MB batch of 200-byte documents would need ~110 GB otherwise)
+    SCRATCH_PER_BYTE = 160
+    SCRATCH_PER_DOC = 160 * 64 + 4096
 
     def _split_by_bytes(self, item):
         data, off = item[0], item[1]
         meta = item[2] if len(item) > 2 else None
         n = len(off) - 1
-        if self.backend == "cpu" or n <= 1 or int(off[-1]) - int(off[0]) <= self.max_batch_bytes:
+        if self.backend == "cpu" or n <= 1:
             return [(0, item)]
+        nbytes = int(off[-1]) - int(off[0])
+        budget = self.SCRATCH_PER_BYTE * self.max_batch_bytes
+        if nbytes <= self.max_batch_bytes and self.SCRATCH_PER_BYTE * nbytes + self.SCRATCH_PER_DOC * n <= budget:
+            return [(0, item)]
+        # cumulative scratch need of documents [0, k): 160 B x bytes + the per-document constant
+        need = self.SCRATCH_PER_BYTE * (off - off[0]) + self.SCRATCH_PER_DOC * np.arange(n + 1, dtype=np.int64)
         out, a = [], 0
         while a < n:
-            # largest b with off[b] - off[a] <= budget (at least one document)
-            b = int(np.searchsorted(off, off[a] + self.max_batch_bytes, side="right")) - 1
-            b = min(n, max(b, a + 1))
+            # largest b with off[b] - off[a] <= byte budget and scratch(a, b) <= scratch budget
+            b1 = int(np.searchsorted(off, off[a] + self.max_batch_bytes, side="right")) - 1
+            b2 = int(np.searchsorted(need, need[a] + budget, side="right")) - 1
+            b = min(n, max(min(b1, b2), a + 1))
             out.append((a, _slice_batch(data, off, meta, a, b)))
             a = b
         return out
@@ -528,6 +562,10 @@ class Engine:
         assembled on the host (counted in tb_device_resolve_fallback_total)."""
         ok = (resolved.err == 0 and np.array_equal(bs.fail_step(), resolved.fail)
               and np.array_equal(bs.status(), resolved.status))
+        if ok and resolved.ver is not None:
+            # the content version the device compacted each output from must be the host's too
+            out = resolved.status <= 1
+            ok = bool(np.array_equal(resolved.ver[out].astype(np.int32), bs.cur_version()[out]))
         if not ok:
             import logging
 

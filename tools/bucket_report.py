@@ -12,7 +12,8 @@ def main():
         k = r["Kernel_Name"]
         if "stage_lds" not in k and "stage_retry" not in k and "stage_analyze" not in k:
             continue
-        name = k.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+        name = k.replace("(anonymous namespace)::", "").replace("void ", "")
+        name = name.split("(")[0]
         wg = int(r["Workgroup_Size_X"])
         grid = int(r["Grid_Size_X"]) // wg
         d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])

@@ -9,6 +9,7 @@
 #include <fstream>
 #include <condition_variable>
 #include <mutex>
+#include <pthread.h>
 #include <random>
 #include <sstream>
 
@@ -52,7 +53,11 @@ class WorkerPool {
     job.max_helpers = std::max(0, nthreads - 1);
     {
       std::unique_lock<std::mutex> g(mu_);
-      while ((int)workers_.size() < job.max_helpers) workers_.emplace_back([this] { loop(); });
+      while ((int)workers_.size() < job.max_helpers)
+        workers_.emplace_back([this] {
+          pthread_setname_np(pthread_self(), "tb-pool");  // attributable in per-thread CPU profiles
+          loop();
+        });
       jobs_.push_back(&job);
     }
     cv_.notify_all();

@@ -91,3 +91,77 @@ def test_device_resolve_fast_path_equals_host_assembly(monkeypatch):
     np.testing.assert_array_equal(a.status, b.status)
     np.testing.assert_array_equal(a.fail_step, b.fail_step)
     assert outputs(a) == outputs(b)
+
+
+def _hard_corpus():
+    """The adversarial pool (UAX#29 fuzz, chunk-boundary constructs), 4.5-90 KB documents in five
+    languages and C4-heavy long documents (citations, policy / javascript lines, ellipses)."""
+    import sys
+
+    import numpy as np
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from adversarial import adversarial_corpus
+    from test_emulated_device_path import EDGE
+
+    rng = np.random.default_rng(19)
+    langs = ["eng", "dan", "swe", "nob", "nno"]
+    texts = synth.make_corpus(1500, 1024, seed=23) + EDGE + adversarial_corpus()
+    texts += [synth.make_doc(rng, langs[k % 5], int(s)) for k, s in enumerate(np.geomspace(4500, 90000, 20))]
+    texts += [synth.make_doc(rng, langs[k % 5], int(s), vocab_kind="zipf") for k, s in enumerate(np.geomspace(3000, 70000, 10))]
+    c4ish = ("A line with a citation [1] and another [2, 3] here. Read our privacy policy today.\n"
+             "JavaScript must be enabled. Short one...\nThe quick brown fox jumps over the lazy dog.\n"
+             "Terms of use {apply} here and lorem ipsum is not.\n\n")
+    texts += [c4ish * 150, (c4ish * 150).replace("\n", " "), c4ish * 600]
+    return texts
+
+
+@pytest.mark.parametrize("mode", ["default", "split", "lds"])
+def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
+    """Independent net for the device kernels: the GPU engine against the CPU ICU oracle (not the
+    host emulation of the same source) on adversarial, long, split and C4-heavy documents; with
+    the GopherRepetition dup orders of every >4.5 KB document split across workgroups ("split")
+    and with the LDS-resident short-document kernel ("lds")."""
+    import json
+
+    import numpy as np
+
+    from textblaster_amd.config import load_pipeline_config
+    from textblaster_amd.pipeline.engine import Engine
+
+    from test_emulated_device_path import outputs
+
+    if mode == "split":
+        monkeypatch.setenv("TB_SPLIT_DOC_BYTES", "4096")
+    if mode == "lds":
+        monkeypatch.setenv("TB_LDS_STAGE", "1")
+    cfg = load_pipeline_config(CFG)
+    texts = _hard_corpus()
+    data, off = synth.pack(texts)
+    eng = Engine(cfg, backend="cuda", keep_reasons=True)
+    if mode == "split":
+        assert eng.device_runner.gr_split and eng.device_runner.split_doc_bytes <= 4608
+    if mode == "lds":
+        assert eng.device_runner.lds_stage
+    a = eng.process(data, off)
+    b = Engine(cfg, backend="cpu", segmentation="icu", keep_reasons=True).process(data, off)
+    np.testing.assert_array_equal(a.status, b.status)
+    np.testing.assert_array_equal(a.fail_step, b.fail_step)
+    assert a.reasons == b.reasons
+    oa, ob = outputs(a), outputs(b)
+    assert oa.keys() == ob.keys()
+    bad = []
+    for k in oa:
+        (ka, ta, ma), (kb, tb, mb) = oa[k], ob[k]
+        if ka != kb or ta != tb or (ma is None) != (mb is None):
+            bad.append(k)
+            continue
+        if ma is not None:
+            ja, jb = json.loads(ma), json.loads(mb)
+            if ja.keys() != jb.keys() or any(
+                    abs(float(ja[f]) - float(jb[f])) >= 1e-5 if f == "Detected language confidence" else ja[f] != jb[f]
+                    for f in ja):
+                bad.append(k)
+    assert not bad, [(k, texts[k][:80]) for k in bad[:5]]
+    lens = np.diff(off)
+    assert np.count_nonzero(lens > 4500) >= 30

@@ -350,6 +350,19 @@ def pinned(n: int, dtype=np.uint8) -> np.ndarray:
     return np.frombuffer(raw, dtype=np.uint8)[: int(n) * dt.itemsize].view(dt)
 
 
+def is_pinned(a: np.ndarray) -> bool:
+    """True when ``a`` is a view of memory from :func:`pinned` (page-locked: an async H2D copy
+    can DMA straight from it, no staging copy)."""
+    obj = a
+    for _ in range(8):
+        if obj is None:
+            return False
+        if getattr(obj, "_tb_block", None) is not None:
+            return True
+        obj = getattr(obj, "base", None) if not isinstance(obj, memoryview) else obj.obj
+    return False
+
+
 def scan_strided_i64(src: DevArray, stride: int, n: int, out: DevArray, s: Optional[Stream] = None) -> None:
     """out[i] = sum(src[j * stride] for j <= i), i < n (k_scan_strided_i64)."""
     if src.dtype != np.int64 or out.dtype != np.int64:

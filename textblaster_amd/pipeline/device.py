@@ -501,6 +501,8 @@ class DeviceRunner:
         # buckets whose LDS slice would exceed this many bytes run the generic kernel instead (0: none)
         self.lds_generic_above = int(os.environ.get("TB_LDS_GENERIC_ABOVE", "0"))
         self.retry_grid = int(os.environ.get("TB_RETRY_GRID", "1024"))
+        # pinned inputs DMA'd in place (no host staging copy); TB_ZERO_COPY=0 forces the copy
+        self.zero_copy = os.environ.get("TB_ZERO_COPY", "1") != "0"
         self.retry_slice = int(h.scratch_bytes_for(max(self.long_doc_bytes, 1) + 16)) // SCRATCH_ALIGN * SCRATCH_ALIGN + SCRATCH_ALIGN
         # the cooperative-gather bag keeps its sums in registers; LDS holds only the cut offset
         self.lds_bytes_lid = int(os.environ.get("TB_LDS_BYTES_LID", "256"))
@@ -566,29 +568,49 @@ class DeviceRunner:
     def _to_dev(self, b: bytes):
         return self.rt.to_device(np.frombuffer(bytes(b), dtype=np.uint8))
 
-    def _stage_inputs(self, slot: _Slot, arrays):
-        """One H2D transfer for all per-batch inputs: arrays are packed at 256-byte aligned
+    def _stage_inputs(self, slot: _Slot, arrays, keep=None):
+        """One H2D transfer for the per-batch inputs: arrays are packed at 256-byte aligned
         offsets into the slot's pinned buffer, copied with one DMA, and returned as typed views
-        of the device buffer."""
+        of the device buffer. An input that already lives in page-locked memory (hiprt.pinned,
+        e.g. a reader that decodes into pinned batch buffers) is not copied on the host at all: its
+        own DMA reads it in place (it is appended to ``keep`` so it outlives the copy)."""
         rt = self.rt
         offs, total = [], 0
+        direct = [bool(self.zero_copy and a.nbytes >= (1 << 20) and a.flags.c_contiguous and rt.is_pinned(a))
+                  for a in arrays]
         for a in arrays:
             offs.append(total)
             total += (a.nbytes + SCRATCH_ALIGN - 1) // SCRATCH_ALIGN * SCRATCH_ALIGN
         total = max(total, SCRATCH_ALIGN)
+        packed = max([o + (a.nbytes + SCRATCH_ALIGN - 1) // SCRATCH_ALIGN * SCRATCH_ALIGN
+                      for a, o, d in zip(arrays, offs, direct) if not d] + [SCRATCH_ALIGN])
         if slot.h2d_done is not None:
             slot.h2d_done.synchronize()  # the previous DMA out of this buffer has finished
-        if slot.pinned is None or slot.pinned.nbytes < total:
+        if slot.pinned is None or slot.pinned.nbytes < packed:
             slot.pinned = None
-            slot.pinned = rt.pinned(int(total * 1.25))
+            slot.pinned = rt.pinned(int(packed * 1.25))
         hv = slot.pinned
         h = native.host()
-        for a, o in zip(arrays, offs):
-            if a.nbytes:
+        for a, o, d in zip(arrays, offs, direct):
+            if a.nbytes and not d:
                 h.parallel_copy(hv, o, np.ascontiguousarray(a).view(np.uint8).reshape(-1), self.copy_threads)
         # H2D on the upload stream: batch k+1's upload overlaps batch k's kernels
         dev = rt.empty(total, np.uint8)
-        dev.copy_from_host(hv[:total], slot.s_h2d)
+        if any(direct):
+            # the packed (small) arrays and each pinned input as separate DMAs
+            o0 = 0
+            for a, o, d in zip(arrays, offs, direct):
+                if d:
+                    if o > o0:
+                        dev[o0:o].copy_from_host(hv[o0:o], slot.s_h2d)
+                    dev[o:o + a.nbytes].copy_from_host(a.view(np.uint8).reshape(-1), slot.s_h2d)
+                    if keep is not None:
+                        keep.append(a)
+                    o0 = o + (a.nbytes + SCRATCH_ALIGN - 1) // SCRATCH_ALIGN * SCRATCH_ALIGN
+            if packed > o0:
+                dev[o0:packed].copy_from_host(hv[o0:packed], slot.s_h2d)
+        else:
+            dev.copy_from_host(hv[:total], slot.s_h2d)
         ev = slot.s_h2d.record()
         slot.h2d_done = ev
         metrics.H2D_BYTES_TOTAL.inc(total)
@@ -689,9 +711,10 @@ class DeviceRunner:
         # perm is longest first: [0, n_long) workgroup docs, [n_long, n_mid) mid-size wave docs
         n_mid = int(np.count_nonzero(lens > self.mid_doc_bytes)) if self.mid_doc_bytes > 0 else n_long
         n_mid = max(n_mid, n_long)
+        direct_keep: List = []
         with tracing.trace_range("tb.stage_h2d"):
             (d_bytes, d_off, d_perm, d_soff), staged = self._stage_inputs(
-                slot, [data if len(data) else np.zeros(1, np.uint8), off, perm, scratch_off])
+                slot, [data if len(data) else np.zeros(1, np.uint8), off, perm, scratch_off], direct_keep)
         scratch = self._scratch_for(slot, int(scratch_off[-1]))
         # grows (new tensor, on this slot's stream) only for documents over 2 MB; the batch keeps a
         # reference to the table it used, so the other slot's kernels never see it freed
@@ -703,7 +726,7 @@ class DeviceRunner:
         versions = {0: (d_bytes, d_off, len(data))}
         stage_recs_d: List = [None] * len(self.plan.stages)
         c4_recs_d = {}
-        keep = [staged, scratch, pw]
+        keep = [staged, scratch, pw] + direct_keep
         # Independent work runs concurrently on side streams (events order the dependencies):
         #   language-id bag (s_lid) | long-doc workgroup kernels (s_blk) | wave kernels (main)
         #   | C4 pass A/B of the same content version (s_c4, own scratch arena)

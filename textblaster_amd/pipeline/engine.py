@@ -229,6 +229,7 @@ class Engine:
 
         def producer():
             try:
+                tracing.name_os_thread("tb-submit")
                 bind = getattr(self.device_runner, "bind_thread", None)
                 if bind is not None:
                     bind()
@@ -280,6 +281,16 @@ class Engine:
     # at that scratch budget (a 384 MB batch of 200-byte documents would need ~110 GB otherwise)
     SCRATCH_PER_BYTE = 160
     SCRATCH_PER_DOC = 160 * 64 + 4096
+
+    def host_buffer(self, nbytes: int) -> np.ndarray:
+        """A uint8 host buffer for batch text: page-locked (hiprt.pinned) on the GPU backend, so a
+        producer that decodes into it lets the batch upload DMA straight from it (DeviceRunner
+        skips the staging copy); plain memory otherwise."""
+        if self.backend == "cuda":
+            from ..ops import hiprt
+
+            return hiprt.pinned(max(int(nbytes), 1))[: int(nbytes)]
+        return np.empty(int(nbytes), dtype=np.uint8)
 
     def _split_by_bytes(self, item):
         data, off = item[0], item[1]

@@ -50,9 +50,77 @@ BOILER = ["We use cookies to improve your experience.", "Read our privacy policy
           "function() { return 0; }"]
 
 
-def _sentence(rng: np.random.Generator, vocab: List[str]) -> str:
+# ---- large-vocabulary (Zipf) lexicons -------------------------------------------------------
+# Per language: the function words above at the head of a Zipf-Mandelbrot rank-frequency law
+# (p(r) ~ 1 / (r + 2.7)^1.07, as measured on web text), followed by ~60,000 synthetic content
+# words built from that language's syllable inventory (1-4 syllables: 3-14 letters, mean ~7), so
+# word, n-gram and hash-table statistics resemble real text instead of a ~130-word vocabulary.
+_SYLL = {
+    "eng": (["b", "c", "d", "f", "g", "h", "j", "k", "l", "m", "n", "p", "r", "s", "t", "v", "w", "st", "tr",
+             "pl", "ch", "sh", "th", "br", "cr", "gr", "fl", ""],
+            ["a", "e", "i", "o", "u", "ea", "ou", "ai", "ee", "y"],
+            ["", "", "n", "r", "s", "t", "nd", "st", "ck", "ng", "l", "m", "rt", "ss"]),
+    "dan": (["b", "d", "f", "g", "h", "j", "k", "l", "m", "n", "p", "r", "s", "t", "v", "sk", "sp", "st", "kr",
+             "tr", "bl", "fl", "gr", "hv", ""],
+            ["a", "e", "i", "o", "u", "y", "æ", "ø", "å", "ej", "ø"],
+            ["", "", "n", "r", "s", "t", "d", "g", "k", "l", "nd", "st", "rt", "ns", "ld"]),
+    "swe": (["b", "d", "f", "g", "h", "j", "k", "l", "m", "n", "p", "r", "s", "t", "v", "sk", "sp", "st", "kr",
+             "tr", "bl", "fr", "gr", "sj", ""],
+            ["a", "e", "i", "o", "u", "y", "å", "ä", "ö", "ä"],
+            ["", "", "n", "r", "s", "t", "d", "g", "k", "l", "nd", "st", "rt", "ng", "ck"]),
+    "nob": (["b", "d", "f", "g", "h", "j", "k", "l", "m", "n", "p", "r", "s", "t", "v", "sk", "sp", "st", "kr",
+             "tr", "bl", "fl", "gr", "hv", ""],
+            ["a", "e", "i", "o", "u", "y", "æ", "ø", "å", "ei", "ø"],
+            ["", "", "n", "r", "s", "t", "d", "g", "k", "l", "nd", "st", "rt", "ns", "kk"]),
+    "nno": (["b", "d", "f", "g", "h", "j", "k", "l", "m", "n", "p", "r", "s", "t", "v", "sk", "sp", "st", "kj",
+             "gj", "tr", "bl", "fl", "gr", "kv", ""],
+            ["a", "e", "i", "o", "u", "y", "æ", "ø", "å", "ei", "au"],
+            ["", "", "n", "r", "s", "t", "d", "g", "k", "l", "nd", "st", "rt", "ng", "kk"]),
+}
+ZIPF_TYPES = 60000
+_LEX = {}
+
+
+def lexicon(lang: str, n_types: int = ZIPF_TYPES):
+    """(words, cumulative probabilities) of a language's Zipf lexicon (deterministic, cached)."""
+    key = (lang, n_types)
+    if key not in _LEX:
+        rng = np.random.default_rng(90210 + sorted(_SYLL).index(lang))
+        on, nu, co = _SYLL[lang]
+        words = list(dict.fromkeys(VOCAB[lang]))
+        seen = set(words)
+        while len(words) < n_types:
+            k = 1 + min(3, int(rng.poisson(1.1)))
+            w = "".join(on[int(rng.integers(0, len(on)))] + nu[int(rng.integers(0, len(nu)))] + co[int(rng.integers(0, len(co)))]
+                        for _ in range(k))
+            if len(w) >= 2 and w not in seen:
+                seen.add(w)
+                words.append(w)
+        r = np.arange(len(words), dtype=np.float64)
+        p = 1.0 / np.power(r + 2.7, 1.07)
+        _LEX[key] = (words, np.cumsum(p / p.sum()))
+    return _LEX[key]
+
+
+class _ZipfVocab:
+    """Word sampler with the list interface make_doc uses (len / index), drawing by Zipf rank."""
+
+    def __init__(self, lang: str):
+        self.words, self.cdf = lexicon(lang)
+        self._pending = None
+
+    def draw(self, rng: np.random.Generator, k: int) -> List[str]:
+        idx = np.searchsorted(self.cdf, rng.random(k), side="right")
+        idx = np.minimum(idx, len(self.words) - 1)
+        return [self.words[int(i)] for i in idx]
+
+
+def _sentence(rng: np.random.Generator, vocab) -> str:
     n = int(rng.integers(4, 18))
-    words = [vocab[int(rng.integers(0, len(vocab)))] for _ in range(n)]
+    if isinstance(vocab, _ZipfVocab):
+        words = vocab.draw(rng, n)
+    else:
+        words = [vocab[int(rng.integers(0, len(vocab)))] for _ in range(n)]
     words[0] = words[0].capitalize()
     r = rng.random()
     if r < 0.05:
@@ -68,8 +136,14 @@ def _sentence(rng: np.random.Generator, vocab: List[str]) -> str:
     return s
 
 
-def make_doc(rng: np.random.Generator, lang: str, target_bytes: int) -> str:
-    vocab = VOCAB[lang]
+def _pick(rng: np.random.Generator, vocab) -> str:
+    if isinstance(vocab, _ZipfVocab):
+        return vocab.draw(rng, 1)[0]
+    return vocab[int(rng.integers(0, len(vocab)))]
+
+
+def make_doc(rng: np.random.Generator, lang: str, target_bytes: int, vocab_kind: str = "small") -> str:
+    vocab = VOCAB[lang] if vocab_kind == "small" else _ZipfVocab(lang)
     lines: List[str] = []
     size = 0
     prev_par: Optional[str] = None
@@ -80,11 +154,11 @@ def make_doc(rng: np.random.Generator, lang: str, target_bytes: int) -> str:
         elif r < 0.10:
             line = "- " + _sentence(rng, vocab)
         elif r < 0.12:
-            line = "• " + " ".join(vocab[int(rng.integers(0, len(vocab)))] for _ in range(3))
+            line = "• " + " ".join(_pick(rng, vocab) for _ in range(3))
         elif r < 0.13:
             line = BOILER[int(rng.integers(0, len(BOILER)))]
         elif r < 0.16:
-            line = vocab[int(rng.integers(0, len(vocab)))].capitalize()  # short heading
+            line = _pick(rng, vocab).capitalize()  # short heading
         else:
             line = " ".join(_sentence(rng, vocab) for _ in range(int(rng.integers(1, 5))))
         lines.append(line)
@@ -102,14 +176,18 @@ def make_doc(rng: np.random.Generator, lang: str, target_bytes: int) -> str:
 
 
 def make_corpus(n_docs: int, mean_bytes: int = 1024, seed: int = 0,
-                langs=("eng", "dan", "swe", "nob", "nno"), lang_p=None) -> List[str]:
+                langs=("eng", "dan", "swe", "nob", "nno"), lang_p=None, vocab: str = "small") -> List[str]:
+    """``vocab``: "small" (the ~130 function words per language, the original benchmark corpus)
+    or "zipf" (60,000-type Zipf lexicons per language, see ``lexicon``)."""
+    if vocab not in ("small", "zipf"):
+        raise ValueError("vocab must be 'small' or 'zipf'")
     rng = np.random.default_rng(seed)
     sigma = 0.8
     mu = math.log(mean_bytes) - sigma * sigma / 2
     sizes = np.clip(rng.lognormal(mu, sigma, n_docs), 16, 64 * mean_bytes).astype(np.int64)
     langs = list(langs)
     choice = rng.choice(len(langs), size=n_docs, p=lang_p)
-    return [make_doc(rng, langs[int(c)], int(s)) for c, s in zip(choice, sizes)]
+    return [make_doc(rng, langs[int(c)], int(s), vocab) for c, s in zip(choice, sizes)]
 
 
 def pack(texts: List[str]):

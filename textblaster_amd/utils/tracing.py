@@ -108,3 +108,15 @@ def mark(name: str) -> None:
     lib = _load() if _enabled else None
     if lib is not None:
         lib.roctxMarkA(name.encode())
+
+
+def name_os_thread(name: str) -> None:
+    """Give the calling thread an OS-level name (15 chars, Linux prctl PR_SET_NAME) so per-thread
+    CPU profiles (tools/thread_cpu.py) can attribute it; a no-op elsewhere."""
+    try:
+        import ctypes
+
+        libc = ctypes.CDLL(None)
+        libc.prctl(15, name.encode()[:15], 0, 0, 0)  # PR_SET_NAME
+    except Exception:  # noqa: BLE001 - best effort
+        pass

@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--vocab", default="small", choices=["small", "zipf"],
                     help="synthetic vocabulary: ~130 words per language (default) or 60k-type Zipf lexicons")
     ap.add_argument("--config", default=os.path.join(ROOT, "config", "bench_pipeline.yaml"))
+    ap.add_argument("--tokenizer", default=None,
+                    help="tokenizer.json for a TokenCounter step in --config ('synthetic': a GPT-2-format "
+                         "byte-level BPE with 50257 entries trained on the Zipf corpus, cached under /tmp)")
     ap.add_argument("--backend", default="cuda", choices=["cuda", "cpu", "emulate"])
     ap.add_argument("--segmentation", default="icu", help="CPU backend segmentation (icu|rules)")
     ap.add_argument("--threads", type=int, default=None)
@@ -88,7 +91,13 @@ def main():
     rank, world = ctx.rank, ctx.world_size
     device = f"cuda:{ctx.local_rank}" if args.backend == "cuda" else None
     cfg = load_pipeline_config(args.config)
-    eng = Engine(cfg, backend=args.backend, device=device, nthreads=args.threads, segmentation=args.segmentation)
+    tok_file = args.tokenizer
+    if tok_file == "synthetic":
+        from textblaster_amd.models.tokenizer import train_synthetic_bpe
+
+        tok_file = train_synthetic_bpe(os.path.join(os.environ.get("TMPDIR", "/tmp"), "tb_synth_bpe50257.json"))
+    eng = Engine(cfg, backend=args.backend, device=device, nthreads=args.threads, segmentation=args.segmentation,
+                 tokenizer_file=tok_file)
 
     # synthetic corpus: a pool of distinct docs per rank, batches are fresh permutations of it
     texts = synth.make_corpus(args.pool, args.mean_bytes, seed=1000 + rank, vocab=args.vocab)
@@ -183,6 +192,7 @@ def main():
                 "parallelism": f"dp{world}",
                 "backend": args.backend,
                 "pipeline_config": os.path.relpath(args.config, ROOT),
+                "tokenizer": args.tokenizer,
             },
             "process_group": ctx.backend,
             "host_cpu_ms_per_step": round(cpu_ms_step_max, 3),

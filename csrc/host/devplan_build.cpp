@@ -237,7 +237,15 @@ void gate_host(const DevGate& g, const std::vector<const int64_t*>& recs, int64_
 DevResolve build_resolve(const std::vector<StepCfg>& steps, const std::vector<std::array<int, 3>>& entries,
                          const std::vector<int>& c4_version) {
   if (entries.size() != c4_version.size()) throw std::invalid_argument("resolve: entries / versions length");
-  if (entries.size() != steps.size()) throw std::invalid_argument("resolve: every pipeline step needs an entry");
+  // every step needs an entry, except trailing TokenCounter steps (they never filter; their
+  // counts are added after the resolve)
+  size_t n_need = steps.size();
+  while (n_need > 0 && steps[n_need - 1].kind == StepKind::TokenCounter) --n_need;
+  if (entries.size() < n_need || entries.size() > steps.size())
+    throw std::invalid_argument("resolve: every pipeline step needs an entry");
+  for (size_t k = 0; k < entries.size(); ++k)
+    if (entries[k][0] < 0 || entries[k][0] >= (int)n_need)
+      throw std::invalid_argument("resolve: every pipeline step needs an entry");
   DevResolve rp;
   std::memset(&rp, 0, sizeof(rp));
   rp.gate = build_gate(steps, entries);  // range checks, <= kMaxGateSteps

@@ -6,7 +6,10 @@
 
 #include <cstring>
 #include <optional>
+#include <thread>
 
+#include "../common/bpe.h"
+#include "../common/bpe_classes.inc"
 #include "../common/langid.h"
 #include "../common/ucd_tables.inc"
 #include "filters.h"
@@ -200,6 +203,87 @@ PYBIND11_MODULE(_tbhost, m) {
     return py::make_tuple(to_numpy(std::move(s1)), to_numpy(std::move(s2)), to_numpy(std::move(l1)),
                           to_numpy(std::move(l2)));
   });
+  // ---- byte-level BPE token counting (csrc/common/bpe.h; device kernel csrc/hip/bpe.hip) ----
+  m.def("bpe_classes", []() {
+    std::vector<uint16_t> c1(TB_BPE_CLS_STAGE1, TB_BPE_CLS_STAGE1 + sizeof(TB_BPE_CLS_STAGE1) / 2);
+    std::vector<uint32_t> c2(TB_BPE_CLS_STAGE2, TB_BPE_CLS_STAGE2 + sizeof(TB_BPE_CLS_STAGE2) / 4);
+    return py::make_tuple(to_numpy(std::move(c1)), to_numpy(std::move(c2)));
+  });
+  m.def("bpe_build_table", [](py::array_t<uint32_t, py::array::c_style> a, py::array_t<uint32_t, py::array::c_style> b,
+                              py::array_t<uint32_t, py::array::c_style> rank, py::array_t<uint32_t, py::array::c_style> nid) {
+    // open addressing, load <= 1/2; a pair listed twice keeps its last rank (HashMap collect)
+    const size_t n = (size_t)a.size();
+    if ((size_t)b.size() != n || (size_t)rank.size() != n || (size_t)nid.size() != n)
+      throw std::invalid_argument("bpe_build_table: operand shapes");
+    size_t cap = 16;
+    while (cap < 2 * n) cap <<= 1;
+    std::vector<uint64_t> keys(cap, kBpeEmpty), vals(cap, ~0ull);
+    const uint64_t mask = cap - 1;
+    for (size_t i = 0; i < n; ++i) {
+      const uint64_t key = ((uint64_t)a.data()[i] << 32) | b.data()[i];
+      if (key == kBpeEmpty) throw std::invalid_argument("bpe_build_table: reserved pair");
+      uint64_t h = bpe_hash(key) & mask;
+      while (keys[h] != kBpeEmpty && keys[h] != key) h = (h + 1) & mask;
+      keys[h] = key;
+      vals[h] = ((uint64_t)rank.data()[i] << 32) | nid.data()[i];
+    }
+    return py::make_tuple(to_numpy(std::move(keys)), to_numpy(std::move(vals)), (uint32_t)mask);
+  });
+  m.def("bpe_count", [](py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
+                        py::array_t<uint32_t, py::array::c_style> byte_id, py::array_t<uint64_t, py::array::c_style> keys,
+                        py::array_t<uint64_t, py::array::c_style> vals, uint32_t mask,
+                        py::array_t<uint8_t, py::array::c_style> added, std::vector<int32_t> added_off, int32_t post_add,
+                        int nthreads, int64_t chunk) {
+    // host emulation of k_bpe_count: per document the token count, or kBpeHost. chunk > 0: the
+    // wave split — the pre-tokens starting in each chunk-byte range counted independently
+    // (bpe_count_range), as the kernel's lanes do
+    if (byte_id.size() != 256 || (size_t)keys.size() != (size_t)mask + 1 || vals.size() != keys.size() ||
+        added_off.size() > kBpeMaxAdded + 1 || (added_off.size() && added_off.back() > added.size()))
+      throw std::invalid_argument("bpe_count: operand shapes");
+    const int64_t nd = off.size() - 1;
+    std::vector<int32_t> out(nd > 0 ? nd : 0);
+    DevBpe T{};
+    T.byte_id = byte_id.data();
+    T.keys = keys.data();
+    T.vals = vals.data();
+    T.cls1 = TB_BPE_CLS_STAGE1;
+    T.cls2 = TB_BPE_CLS_STAGE2;
+    T.added = added.data();
+    T.mask = mask;
+    T.n_added = added_off.empty() ? 0 : (int32_t)added_off.size() - 1;
+    for (size_t i = 0; i < added_off.size(); ++i) T.added_off[i] = added_off[i];
+    T.post_add = post_add;
+    const uint8_t* d = data.data();
+    const int64_t* o = off.data();
+    {
+      py::gil_scoped_release nogil;
+      const int nt = std::max(1, std::min<int>(nthreads, (int)(nd / 256) + 1));
+      std::vector<std::thread> th;
+      for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t]() {
+          uint32_t cbuf[kBpeMaxWord], rbuf[kBpeMaxWord];
+          for (int64_t k = t; k < nd; k += nt) {
+            const uint8_t* b = d + o[k];
+            const int64_t n = o[k + 1] - o[k];
+            if (chunk <= 0) {
+              out[k] = bpe_count_doc(T, b, n, BpeArr{cbuf, 1}, BpeArr{rbuf, 1});
+              continue;
+            }
+            int64_t tot = T.post_add;
+            bool bad = T.n_added && bpe_has_added(T, b, n);
+            for (int64_t s0 = 0; s0 < n && !bad; s0 += chunk) {
+              const int64_t x = bpe_count_range(T, b, n, s0, std::min(n, s0 + chunk), BpeArr{cbuf, 1}, BpeArr{rbuf, 1});
+              if (x < 0) bad = true;
+              tot += x;
+            }
+            out[k] = (bad || tot > 0x7FFFFFFF) ? kBpeHost : (int32_t)tot;
+          }
+        });
+      for (auto& x : th) x.join();
+    }
+    return to_numpy(std::move(out));
+  }, py::arg("data"), py::arg("off"), py::arg("byte_id"), py::arg("keys"), py::arg("vals"), py::arg("mask"),
+        py::arg("added"), py::arg("added_off"), py::arg("post_add"), py::arg("nthreads") = 8, py::arg("chunk") = 0);
   m.def("fmt_f64", [](double x) { return fmt_f64(x); });
   m.def("fmt_fixed", [](double x, int prec) { return fmt_fixed(x, prec); });
   m.def("contains_byte", [](py::array_t<uint8_t, py::array::c_style> a, int v) {

@@ -147,7 +147,13 @@ def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
     b = Engine(cfg, backend="cpu", segmentation="icu", keep_reasons=True).process(data, off)
     np.testing.assert_array_equal(a.status, b.status)
     np.testing.assert_array_equal(a.fail_step, b.fail_step)
-    assert a.reasons == b.reasons
+    assert a.reasons.keys() == b.reasons.keys()
+    for k, ra in a.reasons.items():
+        rb = b.reasons[k]
+        if ra != rb:  # the language confidence in the message: bf16 MFMA head vs fp32 host head
+            pa, pb = ra.split(": ", 1), rb.split(": ", 1)
+            assert pa[0] == pb[0] == "Language detection confidence is not satified", (ra, rb)
+            assert abs(float(pa[1].split()[0]) - float(pb[1].split()[0])) < 1e-5, (ra, rb)
     oa, ob = outputs(a), outputs(b)
     assert oa.keys() == ob.keys()
     bad = []

@@ -22,7 +22,7 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32,
@@ -49,6 +49,8 @@ _SIGS = {
                      _I32],
     "tb_stage_retry": [_P, _P, _P, _P, _P, _P, _I32, _P, ctypes.c_uint64, _I32, _P, _U32, _P, _P, _P, _P, _P, _P, _U32,
                        _P, _P, _P],
+    "tb_bpe_count": [_P, _P, _P, _P, _P, _I32, _P],
+    "tb_sizeof_bpe": [],
     "tb_abi_version": [],
     # native runtime layer (csrc/hip/runtime.hip)
     "tbrt_device_count": [_P], "tbrt_set_device": [_I32], "tbrt_get_device": [_P], "tbrt_device_sync": [],
@@ -65,6 +67,33 @@ _SIGS = {
     "tb_sizeof_stage": [],
     "tb_sizeof_c4": [],
 }
+
+
+class DevBpe(ctypes.Structure):
+    """csrc/common/bpe.h DevBpe (checked against tb_sizeof_bpe)."""
+    _fields_ = [("byte_id", _P), ("keys", _P), ("vals", _P), ("cls1", _P), ("cls2", _P), ("added", _P),
+                ("mask", _U32), ("n_added", _I32), ("added_off", _I32 * 9), ("post_add", _I32)]
+
+
+class BpeTables:
+    """A byte-level BPE tokenizer's tables in HBM (models/tokenizer.py BpeSpec) and the kernel's
+    parameter block pointing at them."""
+
+    def __init__(self, spec, cls_tables):
+        from . import hiprt
+
+        self.arrays = [hiprt.to_device(a) for a in (spec.byte_id, spec.keys, spec.vals, cls_tables[0], cls_tables[1],
+                                                    spec.added)]
+        if len(spec.added_off) > 9:
+            raise DeviceError("bpe: too many added tokens")
+        st = DevBpe()
+        st.byte_id, st.keys, st.vals, st.cls1, st.cls2, st.added = [a.data_ptr() for a in self.arrays]
+        st.mask = spec.mask
+        st.n_added = max(len(spec.added_off) - 1, 0)
+        for i, v in enumerate(spec.added_off):
+            st.added_off[i] = v
+        st.post_add = spec.post_add
+        self.struct = st
 
 
 def declare(lib: ctypes.CDLL) -> None:
@@ -259,6 +288,22 @@ class Kernels:
         rc = self.lib.tb_langid_head(self.stream(), vec.data_ptr(), cnt.data_ptr(), wT.data_ptr(), bias.data_ptr(),
                                      ndocs, rec.data_ptr(), rec_off, width, _ptr(dbg_logits))
         _check(rc, "tb_langid_head")
+
+    def bpe_tables(self, spec) -> BpeTables:
+        from .. import native
+
+        if self.lib.tb_sizeof_bpe() != ctypes.sizeof(DevBpe):
+            raise DeviceError("libtbhip.so DevBpe layout differs from the binding; rebuild")
+        return BpeTables(spec, native.host().bpe_classes())
+
+    def bpe_count(self, tabs: BpeTables, text, off, n_dev, n_max: int, counts):
+        """k_bpe_count: token counts of documents k < min(n_dev[0], n_max) (csrc/hip/bpe.hip);
+        ``n_dev``: optional one-element int64 device array (the kept count of K16)."""
+        if off.numel() < n_max + 1 or counts.numel() < n_max or off.dtype != np.int64 or counts.dtype != np.int32:
+            raise DeviceError("bpe_count: operand shapes")
+        rc = self.lib.tb_bpe_count(self.stream(), ctypes.byref(tabs.struct), text.data_ptr(), off.data_ptr(),
+                                   _ptr(n_dev), n_max, counts.data_ptr())
+        _check(rc, "tb_bpe_count")
 
     def resolve(self, rp, recs, ndocs, flags, versions, fail, status, fver, lanes, sc, out, out_off, rows, err):
         """K16: k_resolve + four scans + k_compact (see tb_resolve). ``recs``: record buffers by

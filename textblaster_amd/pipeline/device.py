@@ -47,6 +47,9 @@ class Resolved:
     rows: np.ndarray        # int32 [ndocs]: document of output k
     err: int = 0            # nonzero: the compaction ran out of room (never with the C4 bound)
     ver: Optional[np.ndarray] = None  # uint8 [ndocs]: content version each document's output came from
+    # trailing TokenCounter steps counted on the device (k_bpe_count): step -> int32 count of kept
+    # output k (k < number kept; -2: count it on the host)
+    tokens: Optional[Dict[int, np.ndarray]] = None
 
     def parts(self):
         """(kept rows, kept offsets, kept text), (excluded ...) as views of the buffers."""
@@ -94,13 +97,29 @@ class LazyVersions(dict):
         return len(self.keys())
 
 
+def trailing_token_counters(plan: ExecPlan) -> List[int]:
+    """TokenCounter steps after the last filtering step (the reference's default config ends with
+    one): they never filter, and they count the kept documents' final contents."""
+    out = []
+    for sp in reversed(plan.steps):
+        if sp.type != "TokenCounter":
+            break
+        out.append(sp.index)
+    return out[::-1]
+
+
 def resolve_entries(plan: ExecPlan, stage_layout):
     """K16 plan: (entries, c4_versions) over every pipeline step in order — entries are (step,
     record slot, prefix) with slots = [stage 0 .. stage S-1, C4 step 0 ..] — or None when a step
-    runs on the host (TokenCounter, C4BadWords)."""
+    runs on the host (C4BadWords, a TokenCounter in front of a filter). Trailing TokenCounter
+    steps never filter, so K16 resolves the steps before them; the counts are added afterwards
+    (k_bpe_count on the kept outputs, or the host tokenizer)."""
     entries, vers = [], []
     ns = len(plan.stages)
+    trailing = set(trailing_token_counters(plan))
     for sp in plan.steps:
+        if sp.index in trailing:
+            continue
         if sp.stage >= 0:
             pos = plan.stages[sp.stage].index(sp.index)
             _, _, prefix = stage_layout[sp.stage][1][pos]
@@ -258,8 +277,9 @@ class PendingBatch:
         timings["gpu_wait"] = t1 - t0
         res = None
         if self._resolved is not None:
-            fail, st, out, out_off, rows, err, ver = self._resolved
-            res = Resolved(fail, st, out, out_off, rows, int(err[0]), ver)
+            fail, st, out, out_off, rows, err, ver = self._resolved[:7]
+            tokens = {si: t for si, t in self._resolved[7:]} or None
+            res = Resolved(fail, st, out, out_off, rows, int(err[0]), ver, tokens)
         return DeviceResult(stage_recs, c4_recs, host_versions, fl, timings, dead, self.runner.pass_of_step, res)
 
 
@@ -319,7 +339,8 @@ class DeviceRunner:
     DEFAULT_SPLIT_DOC_BYTES = 65536
     DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; sweep: tools/occ_sweep.sh)
 
-    def __init__(self, steps_native, plan: ExecPlan, device, langid=None, max_batch_bytes: int = 384 << 20):
+    def __init__(self, steps_native, plan: ExecPlan, device, langid=None, max_batch_bytes: int = 384 << 20,
+                 token_counters=None):
         import os
 
         from ..ops import hiprt
@@ -447,6 +468,11 @@ class DeviceRunner:
                     self.resolve_t = self._to_dev(blob)
                     # int64 fields per document read from each record buffer (launch-time check)
                     self.resolve_need = [w for w, _ in self.stage_layout] + [7] * len(plan.c4_steps)
+            # trailing TokenCounter steps with a byte-level BPE tokenizer: counted on the device
+            # after K16 (token_counters: [(step, BpeSpec)]; TB_DEVICE_TOKENS=0 leaves them to the host)
+            self.bpe = []
+            if self.resolve_t is not None and os.environ.get("TB_DEVICE_TOKENS", "1") not in ("", "0"):
+                self.bpe = [(i, self.k.bpe_tables(sp)) for i, sp in (token_counters or [])]
             # B^k for the hashes, shared read-only by both slots: allocated once (longer spans
             # fall back to powmod61 in the kernels)
             with tracing.trace_range("tb.init.pow_table"):
@@ -935,6 +961,14 @@ class DeviceRunner:
                                r_lanes, r_sc, r_out, r_off, r_rows, r_err)
             keep += [r_fail, r_status, r_ver, r_lanes, r_sc, r_out, r_off, r_rows, r_err]
             res_d = (r_fail, r_status, r_out, r_off, r_rows, r_err, r_ver)
+            for si, tabs in self.bpe:
+                # the kept outputs are r_out[r_off[k]:r_off[k + 1]], k < the kept count (the last
+                # entry of the kept-count scan, read by the kernel)
+                r_tok = rt.empty(ndocs, np.int32)
+                with self._ktimed(keep, "bpe_count"):
+                    self.k.bpe_count(tabs, r_out, r_off, r_sc[3 * ndocs - 1:3 * ndocs], ndocs, r_tok)
+                keep.append(r_tok)
+                res_d = res_d + ((si, r_tok),)
         # D2H into pinned host buffers on the download stream (the slot's compute stream in the
         # 4-stream layout: it is last in line there anyway), then one completion event
         done = self._record(main)
@@ -952,7 +986,7 @@ class DeviceRunner:
         h_versions = {}
         h_res = None
         if res_d is not None:
-            h_res = tuple(d2h(t) for t in res_d)
+            h_res = tuple(d2h(t) for t in res_d[:7]) + tuple((si, d2h(t)) for si, t in res_d[7:])
         if h_res is not None:
             # K16: the compacted outputs replace the versions on the host path; they stay in HBM
             # (downloaded only if the host has to assemble this batch itself)
@@ -994,7 +1028,7 @@ class EmulatedRunner:
     the host side of the device pipeline."""
 
     def __init__(self, steps_native, plan: ExecPlan, langid=None, nthreads: int = 8, gating: Optional[bool] = None,
-                 gate_corrupt: int = 0):
+                 gate_corrupt: int = 0, token_counters=None):
         import os
 
         h = native.host()
@@ -1016,6 +1050,9 @@ class EmulatedRunner:
             self.resolve_blob = build_resolve(plan, self.stage_layout, steps_native)
         self.lds_stage = os.environ.get("TB_LDS_STAGE", LDS_STAGE_DEFAULT) not in ("", "0")
         self.lds_per_byte = float(os.environ.get("TB_LDS_PER_BYTE", "10"))
+        self.bpe = []
+        if self.resolve_blob is not None and os.environ.get("TB_DEVICE_TOKENS", "1") not in ("", "0"):
+            self.bpe = list(token_counters or [])
 
     def run(self, data: np.ndarray, off: np.ndarray) -> DeviceResult:
         import time
@@ -1073,5 +1110,12 @@ class EmulatedRunner:
                                                           [np.ascontiguousarray(d) for d, _ in vl],
                                                           [np.ascontiguousarray(o) for _, o in vl])
             resolved = Resolved(fail, st, out, out_off, rows)
+            if self.bpe:
+                # k_bpe_count's algorithm (csrc/common/bpe.h) over the kept outputs
+                nk = int(np.count_nonzero(st == 0))
+                ko = np.ascontiguousarray(out_off[:nk + 1])
+                resolved.tokens = {
+                    si: h.bpe_count(out, ko, sp.byte_id, sp.keys, sp.vals, sp.mask, sp.added, sp.added_off,
+                                    sp.post_add, self.nthreads) for si, sp in self.bpe}
         return DeviceResult(stage_recs, c4_recs, host_versions, flags, {"emulate": time.perf_counter() - t0}, dead,
                             self.pass_of_step, resolved)

@@ -141,10 +141,23 @@ class Engine:
             with tracing.trace_range("tb.init.badwords"):
                 self.badwords = self.h.BadWordsModule(d)
         self.device_runner = None
+        # trailing TokenCounter steps (after every filter) whose tokenizer is a byte-level BPE are
+        # counted by the device path on the kept outputs (k_bpe_count); the others on the host
+        from .device import trailing_token_counters
+
+        self._trailing_tc = set(trailing_token_counters(self.plan))
+        token_counters = []
+        if backend in ("cuda", "emulate"):
+            for i in sorted(self._trailing_tc):
+                spec_fn = getattr(self.tokenizers.get(i), "bpe_spec", None)
+                spec = spec_fn() if spec_fn is not None else None
+                if spec is not None:
+                    token_counters.append((i, spec))
         if backend == "emulate":
             from .device import EmulatedRunner
 
-            self.device_runner = EmulatedRunner(self.steps, self.plan, self.langid, self.nthreads)
+            self.device_runner = EmulatedRunner(self.steps, self.plan, self.langid, self.nthreads,
+                                                token_counters=token_counters)
         if backend == "cuda":
             for st in self.steps:
                 ok, why = self.h.device_supported(st)
@@ -154,7 +167,7 @@ class Engine:
 
             with tracing.trace_range("tb.init.device_runner"):
                 self.device_runner = DeviceRunner(self.steps, self.plan, device or "cuda", self.langid,
-                                                  max_batch_bytes=self.max_batch_bytes)
+                                                  max_batch_bytes=self.max_batch_bytes, token_counters=token_counters)
 
     # ------------------------------------------------------------------------------------------
     def process(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None,
@@ -426,6 +439,7 @@ class Engine:
                     vid[v] = bs.add_version(np.ascontiguousarray(vd), np.ascontiguousarray(vo))
             dead = getattr(res, "dead", None)
             gate_checked = set()
+            agreed = False
             for sp in self.plan.steps:
                 st = self.steps[sp.index]
                 p = res.pass_of_step.get(sp.index, 0) if dead is not None else 0
@@ -447,13 +461,17 @@ class Engine:
                 elif sp.c4_pass >= 0:
                     bs.apply_records(st, sp.index, res.c4_recs[sp.index], vid[sp.version_out])
                 else:
-                    self._host_step(bs, sp.index, ndocs)
-            if resolved is not None and not self._device_resolve_agrees(bs, resolved):
+                    if resolved is not None and sp.index in self._trailing_tc and not agreed:
+                        # every filter's records are applied: the device's kept outputs must be the
+                        # host's alive documents before the counter reads them
+                        agreed = True
+                        if not self._device_resolve_agrees(bs, resolved):
+                            resolved = None
+                            self._register_versions(bs, res)
+                    self._host_step(bs, sp.index, ndocs, resolved)
+            if resolved is not None and not agreed and not self._device_resolve_agrees(bs, resolved):
                 resolved = None
-                for v in sorted(res.versions):
-                    vd, vo = res.versions[v]
-                    if bs.add_version(np.ascontiguousarray(vd), np.ascontiguousarray(vo)) != v:
-                        raise Unexpected("content version registration order")
+                self._register_versions(bs, res)
             timings["resolve"] = time.perf_counter() - t1
         else:
             t1 = time.perf_counter()
@@ -480,6 +498,14 @@ class Engine:
                 p.rows = p.rows + row_base
         return result
 
+    @staticmethod
+    def _register_versions(bs, res) -> None:
+        """Content versions >= 1 into the batch state (host assembly after a K16 disagreement)."""
+        for v in sorted(res.versions):
+            vd, vo = res.versions[v]
+            if bs.add_version(np.ascontiguousarray(vd), np.ascontiguousarray(vo)) != v:
+                raise Unexpected("content version registration order")
+
     def _run_cpu_steps(self, bs, begin: int, end: int, ndocs: int, seg: str) -> None:
         a = begin
         for i in range(begin, end):
@@ -491,13 +517,25 @@ class Engine:
         if end > a:
             bs.run_cpu(self.steps, a, end, seg, self.lid_native, self.badwords)
 
-    def _host_step(self, bs, i: int, ndocs: int) -> None:
+    def _host_step(self, bs, i: int, ndocs: int, resolved=None) -> None:
         st = self.steps[i]
         t = self.cfg.pipeline[i].type
         if t == "TokenCounter":
             alive = bs.alive_indices()
             rec = np.full(ndocs, -1, dtype=np.int64)
-            if len(alive):
+            if len(alive) and resolved is not None and np.count_nonzero(resolved.status == 0) == len(alive):
+                # K16 agreed: kept output k is alive[k]; its count came from k_bpe_count (or -2:
+                # added-token text / a pre-token over 64 bytes -> the tokenizer, like unsupported
+                # tokenizers)
+                dev = (resolved.tokens or {}).get(i)
+                cnt = dev[:len(alive)].astype(np.int64) if dev is not None else np.full(len(alive), -2, np.int64)
+                bad = np.nonzero(cnt < 0)[0]
+                if len(bad):
+                    o = resolved.out_off
+                    cnt[bad] = self.tokenizers[i].count(
+                        [bytes(resolved.out[o[k]:o[k + 1]]).decode("utf-8", "replace") for k in bad.tolist()])
+                rec[alive] = cnt
+            elif len(alive):
                 texts = bs.contents(alive)
                 rec[alive] = self.tokenizers[i].count(texts)
             bs.apply_records(st, i, rec, -1)

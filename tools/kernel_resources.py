@@ -11,11 +11,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     flags = sys.argv[1:]
+    text = ""
     with tempfile.TemporaryDirectory() as d:
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--offload-device-only",
-                        "-S", *flags, os.path.join(ROOT, "csrc/hip/kernels.hip"), "-o", os.path.join(d, "k.s")],
-                       check=True)
-        text = open(os.path.join(d, "k.s")).read()
+        for src in ("kernels.hip", "stage_lds.hip", "bpe.hip", "html.hip"):
+            subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--offload-device-only",
+                            "-S", *flags, os.path.join(ROOT, "csrc/hip", src), "-o", os.path.join(d, "k.s")],
+                           check=True)
+            text += open(os.path.join(d, "k.s")).read()
     cur = None
     info = {}
     for line in text.splitlines():

@@ -50,6 +50,10 @@ def main():
     ap.add_argument("--tokenizer", default=None,
                     help="tokenizer.json for a TokenCounter step in --config ('synthetic': a GPT-2-format "
                          "byte-level BPE with 50257 entries trained on the Zipf corpus, cached under /tmp)")
+    ap.add_argument("--badwords-dir", default=os.path.join(ROOT, "config", "badwords"),
+                    help="word lists of a C4BadWordsFilter step in --config (default: the synthetic list)")
+    ap.add_argument("--badwords-rate", type=float, default=0.05,
+                    help="with a C4BadWordsFilter step: fraction of pool documents given one list entry")
     ap.add_argument("--backend", default="cuda", choices=["cuda", "cpu", "emulate"])
     ap.add_argument("--segmentation", default="icu", help="CPU backend segmentation (icu|rules)")
     ap.add_argument("--threads", type=int, default=None)
@@ -96,11 +100,14 @@ def main():
         from textblaster_amd.models.tokenizer import train_synthetic_bpe
 
         tok_file = train_synthetic_bpe(os.path.join(os.environ.get("TMPDIR", "/tmp"), "tb_synth_bpe50257.json"))
+    has_bw = any(s.type == "C4BadWordsFilter" for s in cfg.pipeline)
     eng = Engine(cfg, backend=args.backend, device=device, nthreads=args.threads, segmentation=args.segmentation,
-                 tokenizer_file=tok_file)
+                 tokenizer_file=tok_file, badwords_dir=args.badwords_dir if has_bw else None)
 
     # synthetic corpus: a pool of distinct docs per rank, batches are fresh permutations of it
     texts = synth.make_corpus(args.pool, args.mean_bytes, seed=1000 + rank, vocab=args.vocab)
+    if has_bw and args.badwords_rate > 0:
+        texts = synth.inject_words(texts, os.path.join(args.badwords_dir, "en"), args.badwords_rate, seed=rank)
     enc = [t.encode("utf-8") for t in texts]
     rng = np.random.default_rng(rank)
 

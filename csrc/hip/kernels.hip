@@ -15,6 +15,7 @@
 
 #include "../common/docproc.h"
 #include "../common/gate.h"
+#include "../common/badwords.h"
 
 using namespace tb;
 
@@ -358,74 +359,36 @@ __global__ __launch_bounds__(kBlockThreads) void k_c4_pass_a_blk(
   c4_src_absolute(x, src + (int64_t)doc * 2, scratch_off[blockIdx.x]);
 }
 
-// C4 bad words (reference c4_filters.rs:431-441,516): does any list entry occur, case-folded,
+// C4 bad words (reference c4_filters.rs:431-441,463-551): does any list entry occur, case-folded,
 // with \W (or text edge) on both sides (no boundary requirement for CJK lists)? One wave per
-// document; every code point position (UTF-8 lead byte) starts an automaton walk in parallel;
-// the wave stops at the first 64-position chunk that contains a match.
-struct BwAutomaton {
-  const int32_t* first_edge;
-  const uint32_t* edge_cp;
-  const int32_t* edge_to;
-  const uint8_t* term;
-};
-
-__device__ __forceinline__ int32_t bw_next(const BwAutomaton& a, int32_t node, uint32_t c) {
-  int32_t lo = a.first_edge[node], hi = a.first_edge[node + 1];
-  while (lo < hi) {
-    const int32_t mid = (lo + hi) >> 1;
-    const uint32_t v = a.edge_cp[mid];
-    if (v == c) return a.edge_to[mid];
-    if (v < c) lo = mid + 1; else hi = mid;
-  }
-  return -1;
-}
-
-__global__ __launch_bounds__(64) void k_badwords_match(const uint8_t* __restrict__ bytes,
-                                                       const int64_t* __restrict__ off, int32_t ndocs,
-                                                       const int32_t* __restrict__ root,
-                                                       const uint8_t* __restrict__ cjk, BwAutomaton a,
-                                                       DevTables tabs, const uint16_t* __restrict__ f1,
-                                                       const int32_t* __restrict__ f2, int8_t* matched) {
-  const int doc = blockIdx.x;
+// document, four documents per workgroup; every code point position (UTF-8 lead byte) of a
+// 64-byte chunk starts a walk of the hashed trie table (csrc/common/badwords.h) in parallel; the
+// wave stops at the first chunk that contains a match. In the batch pipeline it reads the content
+// version its step sees and skips the documents a pass before the step filtered
+// (0 < dead <= dead_max); matched: -1 skipped / no list, 0 no match, 1 match.
+constexpr int kBwWaves = 4;
+__global__ __launch_bounds__(64 * kBwWaves) void k_badwords_match(
+    const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off, int32_t ndocs,
+    const int32_t* __restrict__ root, const uint8_t* __restrict__ cjk, int32_t root0, int32_t cjk0,
+    const uint8_t* __restrict__ dead, uint32_t dead_max, BwTable tab, DevTables tabs, BwFold fold,
+    int8_t* __restrict__ matched) {
+  const int doc = (int)blockIdx.x * kBwWaves + (int)(threadIdx.x >> 6);
   if (doc >= ndocs) return;
-  const int32_t r0 = root[doc];
-  if (r0 < 0) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const int32_t r0 = root ? root[doc] : root0;
+  const uint32_t dd = dead ? dead[doc] : 0u;
+  if (r0 < 0 || (dd != 0 && dd <= dead_max)) {
+    if (lane == 0) matched[doc] = -1;
+    return;
+  }
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   const UcdView ucd{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
-  const bool any_edge = cjk[doc] != 0;
-  const uint32_t lane = threadIdx.x;
-  auto fold = [&](uint32_t c) -> uint32_t {
-    if (c > 0x10FFFF) return c;
-    return (uint32_t)((int32_t)c + f2[((uint32_t)f1[c >> 7] << 7) | (c & 127)]);
-  };
-  auto wordchar_at = [&](uint32_t s) {  // code point starting at byte s
-    int len;
-    return (ucd.props(utf8_decode(b, s, n, &len)) & P_WORDCHAR) != 0;
-  };
+  const bool any_edge = (cjk ? cjk[doc] : (uint8_t)cjk0) != 0;
   bool found = false;
   for (uint32_t base = 0; base < n; base += 64) {
     const uint32_t s = base + lane;
-    if (s < n && utf8_is_lead(b[s])) {
-      bool ok = any_edge || s == 0;
-      if (!ok) {
-        int64_t p = (int64_t)s - 1;
-        while (p >= 0 && !utf8_is_lead(b[p])) --p;
-        ok = p < 0 || !wordchar_at((uint32_t)p);
-      }
-      if (ok) {
-        int32_t node = r0;
-        uint32_t j = s;
-        while (j < n) {
-          int len;
-          const uint32_t c = utf8_decode(b, j, n, &len);
-          node = bw_next(a, node, fold(c));
-          if (node < 0) break;
-          j += (uint32_t)len;
-          if (a.term[node] && (any_edge || j >= n || !wordchar_at(j))) { found = true; break; }
-        }
-      }
-    }
+    if (s < n && utf8_is_lead(b[s])) found = bw_match_from(b, n, s, r0, any_edge, tab, ucd, fold);
     if (__ballot(found)) break;
   }
   const bool anyf = __ballot(found) != 0;
@@ -716,14 +679,16 @@ int tb_c4_pass_a_blk(hipStream_t stream, const void* c4, const uint8_t* bytes, c
 int tb_block_threads() { return kBlockThreads; }
 
 int tb_badwords_match(hipStream_t stream, const uint8_t* bytes, const int64_t* off, int32_t ndocs, const int32_t* root,
-                      const uint8_t* cjk, const int32_t* first_edge, const uint32_t* edge_cp, const int32_t* edge_to,
-                      const uint8_t* term, const uint16_t* s1, const uint32_t* s2, const uint16_t* l1,
-                      const int32_t* l2, const uint16_t* f1, const int32_t* f2, int8_t* matched) {
+                      const uint8_t* cjk, int32_t root0, int32_t cjk0, const uint8_t* dead, uint32_t dead_max,
+                      const uint32_t* table, uint32_t table_mask, const uint16_t* s1, const uint32_t* s2,
+                      const uint16_t* l1, const int32_t* l2, const uint16_t* f1, const int32_t* f2, int8_t* matched) {
   if (ndocs <= 0) return 0;
+  if (!table || ((table_mask + 1) & table_mask) != 0) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
-  BwAutomaton a{first_edge, edge_cp, edge_to, term};
-  hipLaunchKernelGGL(k_badwords_match, dim3(ndocs), dim3(64), 0, stream, bytes, off, ndocs, root, cjk, a, t, f1, f2,
-                     matched);
+  const BwTable bt{table, table_mask};
+  const BwFold fold{f1, f2};
+  hipLaunchKernelGGL(k_badwords_match, dim3((ndocs + kBwWaves - 1) / kBwWaves), dim3(64 * kBwWaves), 0, stream, bytes,
+                     off, ndocs, root, cjk, root0, cjk0, dead, dead_max, bt, t, fold, matched);
   return (int)hipGetLastError();
 }
 
@@ -827,7 +792,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 
 int tb_phase_slots() { return kPhaseSlots; }
 
-int tb_abi_version() { return 7; }
+int tb_abi_version() { return 8; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

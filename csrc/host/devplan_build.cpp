@@ -238,11 +238,17 @@ DevResolve build_resolve(const std::vector<StepCfg>& steps, const std::vector<st
                          const std::vector<int>& c4_version) {
   if (entries.size() != c4_version.size()) throw std::invalid_argument("resolve: entries / versions length");
   // every step needs an entry, except trailing TokenCounter steps (they never filter; their
-  // counts are added after the resolve)
+  // counts are added after the resolve) and C4BadWords steps (resolved as passing: the host
+  // draws their keep fractions and moves the documents they filter, Engine._device_resolve_agrees)
   size_t n_need = steps.size();
   while (n_need > 0 && steps[n_need - 1].kind == StepKind::TokenCounter) --n_need;
-  if (entries.size() < n_need || entries.size() > steps.size())
+  size_t n_bw = 0;
+  for (size_t s = 0; s < n_need; ++s) n_bw += steps[s].kind == StepKind::C4BadWords;
+  if (entries.size() + n_bw < n_need || entries.size() > steps.size())
     throw std::invalid_argument("resolve: every pipeline step needs an entry");
+  for (size_t k = 0; k < entries.size(); ++k)
+    if (entries[k][0] >= 0 && entries[k][0] < (int)steps.size() && steps[entries[k][0]].kind == StepKind::C4BadWords)
+      throw std::invalid_argument("resolve: C4BadWords has no device decision");
   for (size_t k = 0; k < entries.size(); ++k)
     if (entries[k][0] < 0 || entries[k][0] >= (int)n_need)
       throw std::invalid_argument("resolve: every pipeline step needs an entry");

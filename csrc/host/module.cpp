@@ -7,7 +7,9 @@
 #include <cstring>
 #include <optional>
 #include <thread>
+#include <unordered_map>
 
+#include "../common/badwords.h"
 #include "../common/bpe.h"
 #include "../common/bpe_classes.inc"
 #include "../common/langid.h"
@@ -203,6 +205,99 @@ PYBIND11_MODULE(_tbhost, m) {
     return py::make_tuple(to_numpy(std::move(s1)), to_numpy(std::move(s2)), to_numpy(std::move(l1)),
                           to_numpy(std::move(l2)));
   });
+  // ---- C4 bad words: hashed trie table + host twin of k_badwords_match (csrc/common/badwords.h) ----
+  m.def("bw_build_table", [](py::array_t<int32_t, py::array::c_style> fe, py::array_t<uint32_t, py::array::c_style> ec,
+                             py::array_t<int32_t, py::array::c_style> et, py::array_t<uint8_t, py::array::c_style> term) {
+    const int64_t nodes = (int64_t)term.size();
+    if ((int64_t)fe.size() != nodes + 1 || ec.size() != et.size() || (nodes && fe.data()[nodes] != (int32_t)ec.size()))
+      throw std::invalid_argument("bad-words automaton is malformed");
+    return to_numpy(bw_build_table(fe.data(), nodes, ec.data(), et.data(), (int64_t)ec.size(), term.data()));
+  });
+  // Per document the input metadata's "language" value (the only source of that key: reference
+  // c4_filters.rs:464-468) as an index into the returned name list, -1 when absent.
+  m.def("meta_languages", [](py::array_t<uint8_t, py::array::c_style> md, py::array_t<int64_t, py::array::c_style> mo,
+                             py::object mv, int nthreads) {
+    const int64_t n = (int64_t)mo.size() - 1;
+    const uint8_t* valid = nullptr;
+    py::array_t<uint8_t, py::array::c_style> va;
+    if (!mv.is_none()) {
+      va = mv.cast<py::array_t<uint8_t, py::array::c_style>>();
+      if (va.size() < n) throw std::invalid_argument("meta_languages: validity shorter than the batch");
+      valid = va.data();
+    }
+    if (n < 0 || (n > 0 && mo.data()[n] > (int64_t)md.size())) throw std::invalid_argument("meta_languages: offsets");
+    std::vector<std::string> val((size_t)std::max<int64_t>(n, 0));
+    std::vector<uint8_t> has((size_t)std::max<int64_t>(n, 0), 0);
+    const char* d = (const char*)md.data();
+    const int64_t* o = mo.data();
+    {
+      py::gil_scoped_release nogil;
+      parallel_for(n, nthreads, [&](int64_t a, int64_t b) {
+        FlatMeta fm;
+        for (int64_t i = a; i < b; ++i) {
+          if (valid && !valid[i]) continue;
+          fm.clear();
+          if (parse_meta_json(std::string_view(d + o[i], (size_t)(o[i + 1] - o[i])), fm) && fm.has("language")) {
+            val[(size_t)i] = std::string(fm.get("language"));
+            has[(size_t)i] = 1;
+          }
+        }
+      });
+    }
+    std::vector<int32_t> code((size_t)std::max<int64_t>(n, 0), -1);
+    std::vector<std::string> names;
+    std::unordered_map<std::string, int32_t> idx;
+    for (int64_t i = 0; i < n; ++i) {
+      if (!has[(size_t)i]) continue;
+      auto it = idx.find(val[(size_t)i]);
+      if (it == idx.end()) {
+        it = idx.emplace(val[(size_t)i], (int32_t)names.size()).first;
+        names.push_back(val[(size_t)i]);
+      }
+      code[(size_t)i] = it->second;
+    }
+    return py::make_tuple(to_numpy(std::move(code)), names);
+  }, py::arg("meta_data"), py::arg("meta_off"), py::arg("meta_valid") = py::none(), py::arg("nthreads") = 8);
+  m.def("bw_match_batch", [](py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
+                             py::array_t<uint32_t, py::array::c_style> table, py::object roots, py::object cjk,
+                             int32_t root0, int32_t cjk0, py::object dead, uint32_t dead_max, int nthreads) {
+    const int64_t n = (int64_t)off.size() - 1;
+    const uint64_t slots = (uint64_t)table.size() / 4;
+    if (n < 0 || slots == 0 || (slots & (slots - 1))) throw std::invalid_argument("bw_match_batch: shapes");
+    const int32_t* rp = nullptr;
+    const uint8_t* cp = nullptr;
+    const uint8_t* dp = nullptr;
+    py::array_t<int32_t, py::array::c_style> ra;
+    py::array_t<uint8_t, py::array::c_style> ca, da;
+    if (!roots.is_none()) { ra = roots.cast<py::array_t<int32_t, py::array::c_style>>(); rp = ra.data(); }
+    if (!cjk.is_none()) { ca = cjk.cast<py::array_t<uint8_t, py::array::c_style>>(); cp = ca.data(); }
+    if (!dead.is_none()) { da = dead.cast<py::array_t<uint8_t, py::array::c_style>>(); dp = da.data(); }
+    if ((rp && ra.size() < n) || (cp && ca.size() < n) || (dp && da.size() < n))
+      throw std::invalid_argument("bw_match_batch: per-document array shorter than the batch");
+    std::vector<int8_t> out((size_t)n, -1);
+    const BwTable bt{table.data(), (uint32_t)(slots - 1)};
+    static const std::vector<uint16_t> f1(TB_UCD_FOLD_STAGE1, TB_UCD_FOLD_STAGE1 + sizeof(TB_UCD_FOLD_STAGE1) / 2);
+    static const std::vector<int32_t> f2(TB_UCD_FOLD_STAGE2, TB_UCD_FOLD_STAGE2 + sizeof(TB_UCD_FOLD_STAGE2) / 4);
+    const BwFold fold{f1.data(), f2.data()};
+    const UcdView& ucd = host_ucd();
+    const uint8_t* b = data.data();
+    const int64_t* o = off.data();
+    {
+      py::gil_scoped_release nogil;
+      parallel_for(n, nthreads, [&](int64_t a, int64_t e) {
+        for (int64_t i = a; i < e; ++i) {
+          const int32_t r = rp ? rp[i] : root0;
+          const uint32_t d = dp ? dp[i] : 0u;
+          if (r < 0 || (d != 0 && d <= dead_max)) continue;
+          out[(size_t)i] = bw_match_doc(b + o[i], (uint32_t)(o[i + 1] - o[i]), r, (cp ? cp[i] : cjk0) != 0, bt, ucd,
+                                        fold) ? 1 : 0;
+        }
+      });
+    }
+    return to_numpy(std::move(out));
+  }, py::arg("data"), py::arg("off"), py::arg("table"), py::arg("roots") = py::none(), py::arg("cjk") = py::none(),
+     py::arg("root0") = -1, py::arg("cjk0") = 0, py::arg("dead") = py::none(), py::arg("dead_max") = 0,
+     py::arg("nthreads") = 8);
   // ---- byte-level BPE token counting (csrc/common/bpe.h; device kernel csrc/hip/bpe.hip) ----
   m.def("bpe_classes", []() {
     std::vector<uint16_t> c1(TB_BPE_CLS_STAGE1, TB_BPE_CLS_STAGE1 + sizeof(TB_BPE_CLS_STAGE1) / 2);
@@ -451,6 +546,34 @@ PYBIND11_MODULE(_tbhost, m) {
         return py::make_tuple(sup, (bool)l);
       });
 
+  // Spans idx[k] of a packed (text, off) column gathered into a new packed column (multithreaded).
+  m.def("gather_spans", [](py::array_t<uint8_t, py::array::c_style> text, py::array_t<int64_t, py::array::c_style> off,
+                           py::array_t<int64_t, py::array::c_style> idx, int nthreads) {
+    const int64_t n = (int64_t)off.size() - 1, m = (int64_t)idx.size();
+    const int64_t* o = off.data();
+    const int64_t* ix = idx.data();
+    std::vector<int64_t> no((size_t)m + 1, 0);
+    for (int64_t k = 0; k < m; ++k) {
+      if (ix[k] < 0 || ix[k] >= n) throw std::invalid_argument("gather_spans: index out of range");
+      if (o[ix[k]] < 0 || o[ix[k] + 1] < o[ix[k]] || o[ix[k] + 1] > (int64_t)text.size())
+        throw std::invalid_argument("gather_spans: offsets out of range");
+      no[(size_t)k + 1] = no[(size_t)k] + (o[ix[k] + 1] - o[ix[k]]);
+    }
+    py::array_t<uint8_t> out((py::ssize_t)std::max<int64_t>(no[(size_t)m], 1));
+    uint8_t* d = out.mutable_data();
+    const uint8_t* t = text.data();
+    {
+      py::gil_scoped_release nogil;
+      parallel_for(m, no[(size_t)m] >= (4 << 20) ? nthreads : 1, [&](int64_t a, int64_t b) {
+        for (int64_t k = a; k < b; ++k)
+          std::memcpy(d + no[(size_t)k], t + o[ix[k]], (size_t)(no[(size_t)k + 1] - no[(size_t)k]));
+      });
+    }
+    const py::ssize_t total = (py::ssize_t)no[(size_t)m];
+    py::object view = out[py::slice(0, total, 1)];
+    return py::make_tuple(view, to_numpy(std::move(no)));
+  }, py::arg("text"), py::arg("off"), py::arg("idx"), py::arg("nthreads") = 8);
+
   // Multi-threaded memcpy into a (pinned) staging buffer: dst[dst_off : dst_off + src.nbytes] = src.
   m.def("parallel_copy", [](py::array dst, int64_t dst_off, py::array src, int nthreads) {
     if (!(dst.flags() & py::array::c_style) || !(src.flags() & py::array::c_style))
@@ -531,6 +654,15 @@ PYBIND11_MODULE(_tbhost, m) {
           throw std::invalid_argument("matched/langs length");
         py::gil_scoped_release nogil;
         b.st->apply_badwords_matched(c, step_index, *bw, matched.data(), langs);
+      })
+      .def("apply_badwords_device", [](PyBatch& b, const StepCfg& c, int step_index, std::shared_ptr<BadWordsModule> bw,
+                                       py::array_t<int8_t, py::array::c_style> matched) {
+        // the device matched the documents (k_badwords_match); languages and the keep-fraction
+        // draws (document order) are decided here, as apply_badwords does
+        if ((int64_t)matched.size() != b.st->size()) throw std::invalid_argument("matched length");
+        py::gil_scoped_release nogil;
+        const std::vector<std::string> lang = b.st->badwords_languages(c, *bw);
+        b.st->apply_badwords_matched(c, step_index, *bw, matched.data(), lang);
       })
       .def("gather", [](PyBatch& b, py::array_t<int64_t, py::array::c_style> idx) {
         std::vector<int64_t> iv(idx.data(), idx.data() + idx.size());

@@ -161,3 +161,146 @@ def rows_out(res):
                 m = bytes(p.meta_data[p.meta_off[k]:p.meta_off[k + 1]]) if p.meta_valid[k] else None
                 out[int(r)] = (kind, t, m)
     return out
+
+
+# ---- in-pipeline matching (device pass + host draws), emulated on the CPU -------------------
+def _bw_corpus(n, seed):
+    """Synthetic web documents with list words sprinkled in (some on word boundaries, some
+    inside words), plus per-document language metadata."""
+    rng = random.Random(seed)
+    texts = synth.make_corpus(n, 700, seed=seed)
+    out = []
+    for t in texts:
+        r = rng.random()
+        if r < 0.25:
+            w = rng.choice(["dummybadword", "Exact Phrase", "GRIMT", "xdummybadwordx", "co-op"])
+            cut = rng.randrange(len(t) + 1)
+            t = t[:cut] + " " + w + " " + t[cut:]
+        out.append(t)
+    meta = [(b'{"language":"%s"}' % rng.choice([b"en", b"da", b"ja", b"zz"])) if i % 3 else b""
+            for i in range(len(out))]
+    return out, meta
+
+
+def _pack_meta(meta):
+    md = np.frombuffer(b"".join(meta), np.uint8).copy()
+    mo = np.zeros(len(meta) + 1, np.int64)
+    np.cumsum([len(m) for m in meta], out=mo[1:])
+    mv = np.array([1 if m else 0 for m in meta], np.uint8)
+    return md, mo, mv
+
+
+BW_PIPE = """pipeline:
+  - {type: GopherQualityFilter, min_doc_words: 20, max_doc_words: 100000, min_stop_words: 1}
+%(pre)s  - {type: C4BadWordsFilter, keep_fraction: %(kf)s, fail_on_missing_language: false, default_language: en, seed: 11}
+%(post)s  - {type: FineWebQualityFilter, line_punct_thr: 0.12, line_punct_exclude_zero: false, short_line_thr: 0.67, short_line_length: 30, char_duplicates_ratio: 0.01, new_line_ratio: 0.3}
+%(tc)s"""
+C4 = ("  - {type: C4QualityFilter, split_paragraph: true, remove_citations: true, filter_no_terminal_punct: false, "
+      "min_num_sentences: 1, min_words_per_line: 1, max_word_length: 1000, filter_lorem_ipsum: true, "
+      "filter_javascript: true, filter_curly_bracket: true, filter_policy: true}\n")
+TC = "  - {type: TokenCounter, tokenizer_name: gpt2}\n"
+
+
+CASES = [("pre", 0.4, True), ("pre", 0.0, False), ("post", 0.4, False), ("none", 1.0, True)]
+
+
+@pytest.mark.parametrize("c4_where,kf,tc", CASES)
+def test_emulated_inpipeline_badwords_equals_cpu(tmp_path, c4_where, kf, tc):
+    """The GPU backend's flow (matches from the device pass, draws + decisions on the host, K16
+    outputs with badwords-filtered documents moved to the excluded side) == the CPU oracle.
+    A C4 rewrite after the step disables K16 (host assembly)."""
+    _inpipeline_case(tmp_path, c4_where, kf, tc, "emulate")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c4_where,kf,tc", CASES)
+def test_device_inpipeline_badwords_equals_cpu(tmp_path, c4_where, kf, tc):
+    """Same on the MI355X: k_badwords_match in the batch's pass sequence."""
+    _inpipeline_case(tmp_path, c4_where, kf, tc, "cuda")
+
+
+def _inpipeline_case(tmp_path, c4_where, kf, tc, backend):
+    import os
+
+    write_lists(tmp_path)
+    texts, meta = _bw_corpus(1200, seed=21)
+    data, off = synth.pack(texts)
+    y = BW_PIPE % dict(pre=C4 if c4_where == "pre" else "", post=C4 if c4_where == "post" else "", kf=kf,
+                       tc=TC if tc else "")
+    cfg = parse_pipeline_config(y)
+    tok_dir = os.path.join(os.path.dirname(__file__), "fixtures", "tokenizers")
+    kw = dict(keep_reasons=True, badwords_dir=str(tmp_path), nthreads=4, tokenizer_dir=tok_dir)
+    ea = Engine(cfg, backend=backend, **kw)
+    a = ea.process(data, off, _pack_meta(meta))
+    b = Engine(cfg, backend="cpu", segmentation="icu", **kw).process(data, off, _pack_meta(meta))
+    np.testing.assert_array_equal(a.status, b.status)
+    np.testing.assert_array_equal(a.fail_step, b.fail_step)
+    assert a.reasons == b.reasons
+    oa, ob = rows_out(a), rows_out(b)
+    assert oa == ob
+    bw_i = [i for i, s in enumerate(cfg.pipeline) if s.type == "C4BadWordsFilter"][0]
+    n_bw = int(np.count_nonzero(b.fail_step == bw_i))
+    assert n_bw > 20 if kf < 1.0 else n_bw == 0  # the step filtered documents (none at keep_fraction 1)
+    if 0 < kf < 1 and c4_where != "post":
+        # K16 stayed on: some kept-on-device documents were moved by the host's draws
+        assert len(a.excluded) == 2
+
+
+def test_emulated_badwords_pipelined_keeps_draw_order(tmp_path):
+    """process_many over several batches draws the keep-fraction numbers in document order
+    across batches, like the sequential CPU path."""
+    write_lists(tmp_path)
+    cfg = parse_pipeline_config(BW_PIPE % dict(pre="", post="", kf=0.5, tc=""))
+    kw = dict(keep_reasons=True, badwords_dir=str(tmp_path), nthreads=4)
+    batches = []
+    for s in range(4):
+        t, m = _bw_corpus(300, seed=40 + s)
+        d, o = synth.pack(t)
+        batches.append((d, o, _pack_meta(m)))
+    a = [rows_out(r) for r in Engine(cfg, backend="emulate", **kw).process_many(batches)]
+    eb = Engine(cfg, backend="cpu", segmentation="icu", **kw)
+    b = [rows_out(eb.process(*x)) for x in batches]
+    assert a == b
+
+
+def test_meta_languages_and_gather_spans():
+    h = native.host()
+    meta = [b'{"language":"da","x":"1"}', b"", b'{"y":"z"}', b'{"language":"en"}', b"not json", b'{"language":"da"}']
+    md, mo, mv = _pack_meta(meta)
+    codes, names = h.meta_languages(md, mo, mv, 2)
+    langs = [names[c] if c >= 0 else None for c in codes]
+    assert langs == ["da", None, None, "en", None, "da"]
+    t = np.frombuffer(b"aaabbcdddd", np.uint8).copy()
+    o = np.array([0, 3, 5, 6, 10], np.int64)
+    d, no = h.gather_spans(t, o, np.array([3, 1], np.int64), 2)
+    assert bytes(d) == b"ddddbb" and list(no) == [0, 4, 6]
+    with pytest.raises(ValueError):
+        h.gather_spans(t, o, np.array([4], np.int64), 2)
+
+
+@pytest.mark.parametrize("lang", ["en", "da", "ja"])
+def test_hashed_table_walk_equals_host_matcher(tmp_path, lang):
+    """bw_match_batch (the kernel's hashed-table walk, csrc/common/badwords.h) == the ICU
+    oracle (BadWordsModule.matches) for every document, including dead/no-list skips."""
+    write_lists(tmp_path)
+    h = native.host()
+    bw = h.BadWordsModule(str(tmp_path))
+    for l in LISTS:
+        bw.lookup(l)
+    fe, ec, et, term, roots, cjk = bw.flatten()
+    term = np.ascontiguousarray(term, dtype=np.uint8)
+    tab = h.bw_build_table(fe, np.ascontiguousarray(ec).view(np.uint32), et, term)
+    texts = corpus(1500, seed=hash(lang) & 0xFFF) + ["", "dummybadword", "日本語悪い", "ΣΑΣ."]
+    data, off = synth.pack(texts)
+    m = h.bw_match_batch(data, off, tab, root0=roots[lang], cjk0=int(cjk[lang]), nthreads=2)
+    ref = np.array([bw.matches(lang, t) for t in texts])
+    np.testing.assert_array_equal(m == 1, ref)
+    dead = np.zeros(len(texts), np.uint8)
+    dead[::5] = 2
+    dead[1::5] = 3
+    m2 = h.bw_match_batch(data, off, tab, root0=roots[lang], cjk0=int(cjk[lang]), dead=dead, dead_max=2)
+    assert np.all(m2[::5] == -1) and np.array_equal(m2[1::5], m[1::5])
+    roots_arr = np.full(len(texts), roots[lang], np.int32)
+    roots_arr[::7] = -1
+    m3 = h.bw_match_batch(data, off, tab, roots=roots_arr, cjk=np.full(len(texts), int(cjk[lang]), np.uint8))
+    assert np.all(m3[::7] == -1)

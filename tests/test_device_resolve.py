@@ -69,7 +69,7 @@ def test_resolve_host_matches_decisions_per_document():
     assert r.fail.shape == (n,) and r.status.shape == (n,)
     assert set(np.unique(r.status)).issubset({0, 1, 3})
     assert np.all((r.fail >= 0) == (r.status != 0))
-    (kr, ko, kt), (xr, xo, xt) = r.parts()
+    ((kr, ko, kt),), ((xr, xo, xt),) = r.parts()
     assert len(kr) == np.count_nonzero(r.status == 0) and len(xr) == np.count_nonzero(r.status == 1)
     assert ko[0] == 0 and ko[-1] == len(kt) and xo[0] == 0 and xo[-1] == len(xt)
     # a document filtered before the C4 step carries its input text
@@ -87,8 +87,8 @@ def test_resolve_disagreement_falls_back_to_host(monkeypatch):
     good = outputs(eng.process(data, off))
     orig = devmod.EmulatedRunner.run
 
-    def corrupt(self, d, o):
-        res = orig(self, d, o)
+    def corrupt(self, d, o, bw=None):
+        res = orig(self, d, o, bw)
         res.resolved.status = res.resolved.status.copy()
         res.resolved.status[0] ^= 1  # flip one document's outcome
         return res

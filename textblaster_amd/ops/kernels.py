@@ -22,7 +22,7 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32,
@@ -38,7 +38,7 @@ _SIGS = {
     "tb_resolve": [_P, _P, _P, _I32, _I32, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P],
     "tb_sizeof_resolve": [],
     "tb_block_threads": [],
-    "tb_badwords_match": [_P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "tb_badwords_match": [_P, _P, _P, _I32, _P, _P, _I32, _I32, _P, _U32, _P, _U32, _P, _P, _P, _P, _P, _P, _P],
     "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
     "tb_c4_pass_b": [_P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "tb_langid_head": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I32, _P],
@@ -232,14 +232,23 @@ class Kernels:
             _ptr(dead))
         _check(rc, "tb_c4_pass_a_blk")
 
-    def badwords_match(self, bytes_, off, ndocs, root, cjk, automaton, fold, matched):
+    def badwords_match(self, bytes_, off, ndocs, table, fold, matched, root=None, cjk=None, root0=-1, cjk0=0,
+                       dead=None, dead_max=0):
+        """k_badwords_match over documents [0, ndocs) of (bytes_, off): ``table`` is the hashed trie
+        table (uint32 [4 * slots], csrc/common/badwords.h); per document root/cjk arrays, or one
+        root0/cjk0 for all; documents with 0 < dead <= dead_max are skipped (matched -1)."""
         t = self.tabs
-        fe, ec, et, term = automaton
         f1, f2 = fold
+        slots = table.numel() // 4
+        if slots < 1 or slots & (slots - 1) or matched.numel() < ndocs or off.numel() < ndocs + 1:
+            raise DeviceError("badwords_match: operand shapes")
+        for a in (root, cjk, dead):
+            if a is not None and a.numel() < ndocs:
+                raise DeviceError("badwords_match: per-document array shorter than the batch")
         rc = self.lib.tb_badwords_match(
-            self.stream(), bytes_.data_ptr(), off.data_ptr(), ndocs, root.data_ptr(), cjk.data_ptr(), fe.data_ptr(),
-            ec.data_ptr(), et.data_ptr(), term.data_ptr(), t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
-            t[3].data_ptr(), f1.data_ptr(), f2.data_ptr(), matched.data_ptr())
+            self.stream(), bytes_.data_ptr(), off.data_ptr(), ndocs, _ptr(root), _ptr(cjk), int(root0), int(cjk0),
+            _ptr(dead), int(dead_max), table.data_ptr(), slots - 1, t[0].data_ptr(), t[1].data_ptr(),
+            t[2].data_ptr(), t[3].data_ptr(), f1.data_ptr(), f2.data_ptr(), matched.data_ptr())
         _check(rc, "tb_badwords_match")
 
     def langid_features(self, bytes_, off, perm, ndocs, scratch, scratch_off, emb, vec, cnt, flags, lds_bytes=0,

@@ -36,6 +36,22 @@ class DeviceResult:
     # failing step and status, and the final contents of kept then excluded documents compacted
     # into one buffer. None when the pipeline has host steps (TB_DEVICE_RESOLVE=0: off).
     resolved: Optional["Resolved"] = None
+    # C4BadWords steps matched on the device (k_badwords_match over the content version the step
+    # reads): step -> int8 [ndocs] (-1 skipped / no list, 0 no match, 1 match)
+    bw_matched: Optional[Dict[int, np.ndarray]] = None
+
+
+@dataclasses.dataclass
+class BwInput:
+    """Per batch and C4BadWords step: the hashed trie table of every loaded list (``gen`` names
+    it, so the device copy is uploaded once) and per document the root of its language's trie —
+    one ``root0`` / ``cjk0`` for all documents, or per-document ``roots`` / ``cjk`` arrays."""
+    gen: int
+    table: np.ndarray                 # uint32 [4 * slots] (csrc/common/badwords.h)
+    roots: Optional[np.ndarray] = None  # int32 [ndocs], -1: no list
+    cjk: Optional[np.ndarray] = None    # uint8 [ndocs]
+    root0: int = -1
+    cjk0: int = 0
 
 
 @dataclasses.dataclass
@@ -51,15 +67,43 @@ class Resolved:
     # output k (k < number kept; -2: count it on the host)
     tokens: Optional[Dict[int, np.ndarray]] = None
 
-    def parts(self):
-        """(kept rows, kept offsets, kept text), (excluded ...) as views of the buffers."""
-        nk = int(np.count_nonzero(self.status == 0))
-        nx = int(np.count_nonzero(self.status == 1))
+    # kept outputs a host step filtered afterwards (C4BadWords keep-fraction draws): bool over
+    # the device's kept outputs; they move to the excluded side (Engine._device_resolve_agrees)
+    moved: Optional[np.ndarray] = None
+
+    def counts(self):
+        return int(np.count_nonzero(self.status == 0)), int(np.count_nonzero(self.status == 1))
+
+    def n_kept_final(self) -> int:
+        nk, _ = self.counts()
+        return nk - (int(np.count_nonzero(self.moved)) if self.moved is not None else 0)
+
+    def kept_tokens(self, step: int) -> Optional[np.ndarray]:
+        """k_bpe_count results of the final kept outputs (moved ones dropped)."""
+        dev = (self.tokens or {}).get(step)
+        if dev is None:
+            return None
+        nk, _ = self.counts()
+        dev = dev[:nk]
+        return dev[~self.moved] if self.moved is not None else dev
+
+    def parts(self, nthreads: int = 8):
+        """([(kept rows, offsets, text)], [(excluded ...), ...]): views of the compacted buffer; with
+        ``moved``, the kept side is gathered without them and they form a second excluded part."""
+        nk, nx = self.counts()
         o = self.out_off
         kb, tot = int(o[nk]), int(o[nk + nx])
         kept = (self.rows[:nk].astype(np.int64), o[:nk + 1], self.out[:kb])
         excl = (self.rows[nk:nk + nx].astype(np.int64), o[nk:nk + nx + 1] - kb, self.out[kb:tot])
-        return kept, excl
+        if self.moved is None or not self.moved.any():
+            return [kept], [excl]
+        h = native.host()
+        ko = np.ascontiguousarray(o[:nk + 1])
+        stay = np.nonzero(~self.moved)[0].astype(np.int64)
+        gone = np.nonzero(self.moved)[0].astype(np.int64)
+        kd, ko2 = h.gather_spans(self.out, ko, stay, nthreads)
+        md, mo2 = h.gather_spans(self.out, ko, gone, nthreads)
+        return [(kept[0][stay], ko2, kd)], [excl, (kept[0][gone], mo2, md)]
 
 
 class LazyVersions(dict):
@@ -111,14 +155,22 @@ def trailing_token_counters(plan: ExecPlan) -> List[int]:
 def resolve_entries(plan: ExecPlan, stage_layout):
     """K16 plan: (entries, c4_versions) over every pipeline step in order — entries are (step,
     record slot, prefix) with slots = [stage 0 .. stage S-1, C4 step 0 ..] — or None when a step
-    runs on the host (C4BadWords, a TokenCounter in front of a filter). Trailing TokenCounter
+    runs on the host (a TokenCounter in front of a filter, a C4 rewrite after C4BadWords).
+    C4BadWords steps are skipped (see below). Trailing TokenCounter
     steps never filter, so K16 resolves the steps before them; the counts are added afterwards
     (k_bpe_count on the kept outputs, or the host tokenizer)."""
     entries, vers = [], []
     ns = len(plan.stages)
     trailing = set(trailing_token_counters(plan))
+    # C4BadWords decides with keep-fraction draws on the host (document order): K16 resolves the
+    # device steps as if it passed every document, and the host moves the documents it filters
+    # afterwards; exact only while no content rewrite follows it (then their outputs are the
+    # contents the step saw)
+    bw = [sp.index for sp in plan.steps if sp.type == "C4BadWordsFilter"]
+    if bw and any(sp.type == "C4QualityFilter" and sp.index > bw[0] for sp in plan.steps):
+        return None
     for sp in plan.steps:
-        if sp.index in trailing:
+        if sp.index in trailing or sp.type == "C4BadWordsFilter":
             continue
         if sp.stage >= 0:
             pos = plan.stages[sp.stage].index(sp.index)
@@ -233,7 +285,7 @@ class PendingBatch:
     the completion event and returns host views of the results."""
 
     def __init__(self, runner, ndocs, event, stage_recs, c4_recs, versions, flags, t_submit, keep, dead=None,
-                 resolved=None):
+                 resolved=None, bw=None):
         self.runner = runner
         self.ndocs = ndocs
         self.event = event
@@ -245,6 +297,7 @@ class PendingBatch:
         self._t_submit = t_submit
         self._keep = keep  # device tensors that must stay alive until the event completes
         self._resolved = resolved
+        self._bw = bw or {}
 
     def wait(self) -> DeviceResult:
         import time
@@ -280,7 +333,8 @@ class PendingBatch:
             fail, st, out, out_off, rows, err, ver = self._resolved[:7]
             tokens = {si: t for si, t in self._resolved[7:]} or None
             res = Resolved(fail, st, out, out_off, rows, int(err[0]), ver, tokens)
-        return DeviceResult(stage_recs, c4_recs, host_versions, fl, timings, dead, self.runner.pass_of_step, res)
+        bwm = {i: m[:self.ndocs] for i, m in self._bw.items()} or None
+        return DeviceResult(stage_recs, c4_recs, host_versions, fl, timings, dead, self.runner.pass_of_step, res, bwm)
 
 
 KIND_LANGID = 4  # DevStep kind of LanguageDetectionFilter in a stage layout (csrc/common/devplan.h)
@@ -324,6 +378,19 @@ def plan_passes(plan: ExecPlan, stage_layout, steps_native, gating: bool, lid_ga
             # need: int64 record fields per document the gate reads (checked at launch)
             gates[p] = (h.build_gate(steps_native, entries), need)
     return passes, pass_of_step, gates
+
+
+def bw_dead_max(plan: ExecPlan, passes, pass_of_step: Dict[int, int]) -> Dict[int, int]:
+    """Per C4BadWords step q: the device passes [0, q) hold only steps before it, so a document a
+    gate marked dead <= q never reached the step (dead = k: the gate of pass k-1 filtered it);
+    documents dead after a later pass did reach it and still need their match."""
+    out = {}
+    for sp in plan.steps:
+        if sp.type != "C4BadWordsFilter":
+            continue
+        later = [p for j, p in pass_of_step.items() if j > sp.index]
+        out[sp.index] = min(later) if later else len(passes)
+    return out
 
 
 class DeviceRunner:
@@ -459,6 +526,7 @@ class DeviceRunner:
                 plan, self.stage_layout, steps_native, self.gating,
                 os.environ.get("TB_LID_GATE", "1") not in ("", "0") and self.has_lid)
             self.gate_ts = {p: self._to_dev(b) for p, (b, _) in gates.items()}
+            self.bw_dead_max = bw_dead_max(plan, self.passes, self.pass_of_step)
             self.gate_need = {p: need for p, (_, need) in gates.items()}
             # K16: device resolve + output compaction when every step runs on the device
             self.resolve_t = None
@@ -543,8 +611,7 @@ class DeviceRunner:
         self.copy_threads = int(os.environ.get("TB_COPY_THREADS", "8"))
         self._next_slot = 0
         self._last_lid = None
-        self.s_bw = None      # bad-words stream, created on first use (not part of the batch pipeline)
-        self._bw_auto = None  # (key, device arrays) of the flattened bad-words automaton
+        self._bw_table = None  # (gen, device copy) of the hashed bad-words trie table
         self._bw_fold = None
 
     def bind_thread(self) -> None:
@@ -556,40 +623,16 @@ class DeviceRunner:
         """Wait for all queued device work (error recovery drains the queues before it frees)."""
         self.rt.synchronize()
 
-    def badwords_match(self, key, automaton, data: np.ndarray, off: np.ndarray, roots: np.ndarray,
-                       cjk: np.ndarray) -> np.ndarray:
-        """C4 bad-words matching of post-resolve contents on the device (k_badwords_match): one
-        wave per document walks the flattened word-list tries from every code point. ``roots``:
-        per document the root node of its language's trie. Returns 1 (match) / 0 per document."""
+    def _bw_tables(self, bw: BwInput):
+        """Device copies of the case-fold tables and of the batch's trie table (uploaded once per
+        table generation, on the calling stream before any kernel that reads them)."""
         rt = self.rt
-        n = len(off) - 1
-        if n == 0:
-            return np.zeros(0, dtype=np.int8)
-        if roots.shape != (n,) or cjk.shape != (n,) or int(off[-1]) > len(data):
-            raise DeviceError("badwords_match: operand shapes")
-        if self.s_bw is None:
-            self.s_bw = rt.Stream()
-        with rt.stream(self.s_bw):
-            if self._bw_fold is None:
-                f1, f2 = native.host().ucd_fold_tables()
-                self._bw_fold = (rt.to_device(f1), rt.to_device(f2))
-            if self._bw_auto is None or self._bw_auto[0] != key:
-                fe, ec, et, term = automaton
-                nodes = len(term)
-                if len(fe) != nodes + 1 or len(ec) != len(et) or int(fe[-1]) != len(ec):
-                    raise DeviceError("badwords automaton is malformed")
-                if nodes and (int(roots.max()) >= nodes or (len(et) and (int(et.min()) < 0 or int(et.max()) >= nodes))):
-                    raise DeviceError("badwords automaton node index out of range")
-                dev = tuple(rt.to_device(np.ascontiguousarray(a))
-                            for a in (fe, ec.view(np.int32), et, np.ascontiguousarray(term, dtype=np.uint8)))
-                self._bw_auto = (key, dev)
-            d_bytes = rt.to_device(np.ascontiguousarray(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8))
-            d_off = rt.to_device(np.ascontiguousarray(off, dtype=np.int64))
-            d_root = rt.to_device(np.ascontiguousarray(roots, dtype=np.int32))
-            d_cjk = rt.to_device(np.ascontiguousarray(cjk, dtype=np.uint8))
-            out = rt.zeros(n, np.int8)
-            self.k.badwords_match(d_bytes, d_off, n, d_root, d_cjk, self._bw_auto[1], self._bw_fold, out)
-            return out.to_host()
+        if self._bw_fold is None:
+            f1, f2 = native.host().ucd_fold_tables()
+            self._bw_fold = (rt.to_device(f1), rt.to_device(f2))
+        if self._bw_table is None or self._bw_table[0] != bw.gen:
+            self._bw_table = (bw.gen, rt.to_device(np.ascontiguousarray(bw.table, dtype=np.uint32)))
+        return self._bw_table[1], self._bw_fold
 
     def _to_dev(self, b: bytes):
         return self.rt.to_device(np.frombuffer(bytes(b), dtype=np.uint8))
@@ -706,17 +749,19 @@ class DeviceRunner:
                 lines.append(f"   {names.get(int(i), i):>16}: {tot[i] / nd:>12,.0f}  ({100 * tot[i] / allc:5.1f}%)")
         return "\n".join(lines)
 
-    def submit(self, data: np.ndarray, off: np.ndarray) -> PendingBatch:
-        """Stage inputs, enqueue every device stage and the D2H copies; returns immediately."""
+    def submit(self, data: np.ndarray, off: np.ndarray, bw: Optional[Dict[int, BwInput]] = None) -> PendingBatch:
+        """Stage inputs, enqueue every device stage and the D2H copies; returns immediately.
+        ``bw``: inputs of the pipeline's C4BadWords steps (Engine._bw_inputs)."""
         import time
 
         t0 = time.perf_counter()
         slot = self.slots[self._next_slot]
         self._next_slot = (self._next_slot + 1) % self.N_SLOTS
         with self.rt.stream(slot.main):
-            return self._submit_on(slot, data, off, t0)
+            return self._submit_on(slot, data, off, t0, bw or {})
 
-    def _submit_on(self, slot: "_Slot", data: np.ndarray, off: np.ndarray, t0: float) -> PendingBatch:
+    def _submit_on(self, slot: "_Slot", data: np.ndarray, off: np.ndarray, t0: float,
+                   bw: Dict[int, BwInput]) -> PendingBatch:
         import time
 
         rt = self.rt
@@ -738,9 +783,19 @@ class DeviceRunner:
         n_mid = int(np.count_nonzero(lens > self.mid_doc_bytes)) if self.mid_doc_bytes > 0 else n_long
         n_mid = max(n_mid, n_long)
         direct_keep: List = []
+        # per-document bad-words roots / CJK flags travel in the same upload
+        bw_arrays = [(i, a) for i in sorted(bw) for a in (bw[i].roots, bw[i].cjk) if a is not None]
+        for _, a in bw_arrays:
+            if len(a) != ndocs:
+                raise DeviceError("badwords: per-document inputs do not match the batch")
         with tracing.trace_range("tb.stage_h2d"):
-            (d_bytes, d_off, d_perm, d_soff), staged = self._stage_inputs(
-                slot, [data if len(data) else np.zeros(1, np.uint8), off, perm, scratch_off], direct_keep)
+            staged_views, staged = self._stage_inputs(
+                slot, [data if len(data) else np.zeros(1, np.uint8), off, perm, scratch_off]
+                + [np.ascontiguousarray(a) for _, a in bw_arrays], direct_keep)
+        d_bytes, d_off, d_perm, d_soff = staged_views[:4]
+        bw_dev = {}
+        for (i, a), d in zip(bw_arrays, staged_views[4:]):
+            bw_dev[(i, a.dtype == np.int32)] = d
         scratch = self._scratch_for(slot, int(scratch_off[-1]))
         # grows (new tensor, on this slot's stream) only for documents over 2 MB; the batch keeps a
         # reference to the table it used, so the other slot's kernels never see it freed
@@ -937,6 +992,20 @@ class DeviceRunner:
                 keep.append(src)
         for ev in tails:
             main.wait_event(ev)
+        bw_d = {}
+        for i in sorted(bw):
+            # C4BadWords: match every document that reached the step on the content version it
+            # reads; the keep-fraction draws and the decision stay on the host (document order)
+            x = bw[i]
+            sp = self.plan.steps[i]
+            vb, vo, _ = versions[sp.version_in]
+            table, fold = self._bw_tables(x)
+            m = rt.empty(max(ndocs, 1), np.int8)
+            with self._ktimed(keep, "badwords"):
+                self.k.badwords_match(vb, vo, ndocs, table, fold, m, bw_dev.get((i, True)), bw_dev.get((i, False)),
+                                      x.root0, x.cjk0, dead, self.bw_dead_max[i])
+            keep += [table, m]
+            bw_d[i] = m
         res_d = None
         if self.resolve_t is not None:
             # K16 on the compute stream after every pass: first failure, status, and the final
@@ -997,14 +1066,15 @@ class DeviceRunner:
                 h_versions[ver] = (d2h(vb), d2h(vo))
         h_flags = d2h(flags)
         h_dead = d2h(dead) if dead is not None else None
+        h_bw = {i: d2h(m) for i, m in bw_d.items()}
         ev = self._record(d2h_s)
         keep += [stage_recs_d, c4_recs_d, versions, flags, dead, ready, tails, done]
         t2 = time.perf_counter()
         return PendingBatch(self, ndocs, ev, h_stage, h_c4, h_versions, h_flags,
-                            {"stage_h2d": t1 - t0, "launch": t2 - t1}, keep, h_dead, h_res)
+                            {"stage_h2d": t1 - t0, "launch": t2 - t1}, keep, h_dead, h_res, h_bw)
 
-    def run(self, data: np.ndarray, off: np.ndarray) -> DeviceResult:
-        return self.submit(data, off).wait()
+    def run(self, data: np.ndarray, off: np.ndarray, bw: Optional[Dict[int, BwInput]] = None) -> DeviceResult:
+        return self.submit(data, off, bw).wait()
 
 
 def _dict_script_flags(data: np.ndarray, off: np.ndarray) -> np.ndarray:
@@ -1042,6 +1112,7 @@ class EmulatedRunner:
             gating = os.environ.get("TB_GATE", "1") not in ("", "0")
         self.passes, self.pass_of_step, self.gates = plan_passes(
             plan, self.stage_layout, steps_native, gating, os.environ.get("TB_LID_GATE", "1") not in ("", "0"))
+        self.bw_dead_max = bw_dead_max(plan, self.passes, self.pass_of_step)
         # test hook: additionally mark every k-th document dead after the first pass (a wrong
         # device gate), to exercise the resolver's recovery path
         self.gate_corrupt = gate_corrupt
@@ -1054,7 +1125,7 @@ class EmulatedRunner:
         if self.resolve_blob is not None and os.environ.get("TB_DEVICE_TOKENS", "1") not in ("", "0"):
             self.bpe = list(token_counters or [])
 
-    def run(self, data: np.ndarray, off: np.ndarray) -> DeviceResult:
+    def run(self, data: np.ndarray, off: np.ndarray, bw: Optional[Dict[int, BwInput]] = None) -> DeviceResult:
         import time
 
         h = native.host()
@@ -1102,6 +1173,12 @@ class EmulatedRunner:
                     extra = np.arange(0, ndocs, self.gate_corrupt)
                     dead[extra[dead[extra] == 0]] = 1
         host_versions = {v: versions[v] for v in range(1, self.plan.n_versions)}
+        bwm = {}
+        for i, x in sorted((bw or {}).items()):
+            # k_badwords_match's walk (csrc/common/badwords.h bw_match_doc), same skip rule
+            vd, vo = versions[self.plan.steps[i].version_in]
+            bwm[i] = h.bw_match_batch(vd, vo, np.ascontiguousarray(x.table, dtype=np.uint32), x.roots, x.cjk, x.root0,
+                                      x.cjk0, dead, self.bw_dead_max[i], self.nthreads)
         resolved = None
         if self.resolve_blob is not None:
             recs = list(stage_recs) + [c4_recs[i] for i in self.plan.c4_steps]
@@ -1118,4 +1195,4 @@ class EmulatedRunner:
                     si: h.bpe_count(out, ko, sp.byte_id, sp.keys, sp.vals, sp.mask, sp.added, sp.added_off,
                                     sp.post_add, self.nthreads) for si, sp in self.bpe}
         return DeviceResult(stage_recs, c4_recs, host_versions, flags, {"emulate": time.perf_counter() - t0}, dead,
-                            self.pass_of_step, resolved)
+                            self.pass_of_step, resolved, bwm or None)

@@ -140,6 +140,12 @@ class Engine:
             d = badwords_dir or (bw_dirs[0] if bw_dirs else os.path.join("data", "c4_badwords"))
             with tracing.trace_range("tb.init.badwords"):
                 self.badwords = self.h.BadWordsModule(d)
+        # C4BadWords steps: on the GPU backends the matching runs in the batch's device pass
+        # sequence (k_badwords_match); languages and keep-fraction draws stay on the host. The lock
+        # serialises the word-list loading of the submitter and consumer threads.
+        self._bw_steps = [i for i, s in enumerate(cfg.pipeline) if s.type == "C4BadWordsFilter"]
+        self._bw_lock = threading.Lock()
+        self._bw_nolist = set()
         self.device_runner = None
         # trailing TokenCounter steps (after every filter) whose tokenizer is a byte-level BPE are
         # counted by the device path on the kept outputs (k_bpe_count); the others on the host
@@ -402,9 +408,39 @@ class Engine:
         off = np.ascontiguousarray(off, dtype=np.int64)
         dev = None
         if self.backend in ("cuda", "emulate"):
+            bw = self._bw_inputs(len(off) - 1, meta) if self._bw_steps else None
             submit = getattr(self.device_runner, "submit", None)
-            dev = submit(data, off) if submit is not None else self.device_runner.run(data, off)
+            dev = submit(data, off, bw) if submit is not None else self.device_runner.run(data, off, bw)
         return _Submitted(data, off, meta, row_base, dev, t0)
+
+    def _bw_inputs(self, ndocs: int, meta) -> Dict[int, object]:
+        """Per C4BadWords step: the hashed trie table and each document's list root (language =
+        input metadata "language", else the step's default_language; reference
+        c4_filters.rs:464-468). Lists load here, once per language."""
+        from .device import BwInput
+
+        codes, names = None, []
+        if meta is not None and meta[0] is not None:
+            md, mo, mv = meta
+            codes, names = self.h.meta_languages(np.ascontiguousarray(md, dtype=np.uint8),
+                                                 np.ascontiguousarray(mo, dtype=np.int64),
+                                                 None if mv is None else np.ascontiguousarray(mv, dtype=np.uint8),
+                                                 self.nthreads)
+            if not (codes >= 0).any():
+                codes = None
+        out = {}
+        with self._bw_lock:
+            for i in self._bw_steps:
+                langs = list(names) + [self.cfg.pipeline[i].params.default_language]
+                fe, ec, et, term, roots, cjk, gen, table = self._badwords_automaton(set(langs))
+                rl = np.array([roots.get(l, -1) for l in langs], dtype=np.int32)
+                cl = np.array([1 if cjk.get(l, False) else 0 for l in langs], dtype=np.uint8)
+                if codes is None:
+                    out[i] = BwInput(gen, table, root0=int(rl[-1]), cjk0=int(cl[-1]))
+                else:
+                    ix = np.where(codes >= 0, codes, len(names))
+                    out[i] = BwInput(gen, table, roots=rl[ix], cjk=cl[ix])
+        return out
 
     def finish(self, sub: "_Submitted") -> BatchResult:
         with tracing.trace_range("tb.finish"):
@@ -461,6 +497,15 @@ class Engine:
                 elif sp.c4_pass >= 0:
                     bs.apply_records(st, sp.index, res.c4_recs[sp.index], vid[sp.version_out])
                 else:
+                    matched = (res.bw_matched or {}).get(sp.index) if sp.type == "C4BadWordsFilter" else None
+                    if matched is not None and dead is not None:
+                        # the device matched only documents no pass before the step filtered
+                        q = self.device_runner.bw_dead_max[sp.index]
+                        bad = np.nonzero((dead != 0) & (dead <= q) & (bs.fail_step() < 0))[0].astype(np.int64)
+                        if len(bad):
+                            _gate_mismatch(len(bad), q)
+                            bs.delegate(bad)
+                            delegated = np.union1d(delegated, bad).astype(np.int64)
                     if resolved is not None and sp.index in self._trailing_tc and not agreed:
                         # every filter's records are applied: the device's kept outputs must be the
                         # host's alive documents before the counter reads them
@@ -468,7 +513,7 @@ class Engine:
                         if not self._device_resolve_agrees(bs, resolved):
                             resolved = None
                             self._register_versions(bs, res)
-                    self._host_step(bs, sp.index, ndocs, resolved)
+                    self._host_step(bs, sp.index, ndocs, resolved, matched)
             if resolved is not None and not agreed and not self._device_resolve_agrees(bs, resolved):
                 resolved = None
                 self._register_versions(bs, res)
@@ -517,68 +562,56 @@ class Engine:
         if end > a:
             bs.run_cpu(self.steps, a, end, seg, self.lid_native, self.badwords)
 
-    def _host_step(self, bs, i: int, ndocs: int, resolved=None) -> None:
+    def _host_step(self, bs, i: int, ndocs: int, resolved=None, matched=None) -> None:
         st = self.steps[i]
         t = self.cfg.pipeline[i].type
         if t == "TokenCounter":
             alive = bs.alive_indices()
             rec = np.full(ndocs, -1, dtype=np.int64)
-            if len(alive) and resolved is not None and np.count_nonzero(resolved.status == 0) == len(alive):
-                # K16 agreed: kept output k is alive[k]; its count came from k_bpe_count (or -2:
-                # added-token text / a pre-token over 64 bytes -> the tokenizer, like unsupported
-                # tokenizers)
-                dev = (resolved.tokens or {}).get(i)
-                cnt = dev[:len(alive)].astype(np.int64) if dev is not None else np.full(len(alive), -2, np.int64)
+            if len(alive) and resolved is not None and resolved.n_kept_final() == len(alive):
+                # K16 agreed: final kept output k is alive[k]; its count came from k_bpe_count (or
+                # -2: added-token text / a pre-token over 64 bytes -> the tokenizer, like
+                # unsupported tokenizers)
+                dev = resolved.kept_tokens(i)
+                cnt = dev.astype(np.int64) if dev is not None else np.full(len(alive), -2, np.int64)
                 bad = np.nonzero(cnt < 0)[0]
                 if len(bad):
                     o = resolved.out_off
+                    ko = np.nonzero(~resolved.moved)[0] if resolved.moved is not None else np.arange(len(alive))
                     cnt[bad] = self.tokenizers[i].count(
-                        [bytes(resolved.out[o[k]:o[k + 1]]).decode("utf-8", "replace") for k in bad.tolist()])
+                        [bytes(resolved.out[o[k]:o[k + 1]]).decode("utf-8", "replace") for k in ko[bad].tolist()])
                 rec[alive] = cnt
             elif len(alive):
                 texts = bs.contents(alive)
                 rec[alive] = self.tokenizers[i].count(texts)
             bs.apply_records(st, i, rec, -1)
         elif t == "C4BadWordsFilter":
-            if self.backend == "cuda":
-                self._badwords_device(bs, st, i, ndocs)
-            else:
-                bs.apply_badwords(st, i, self.badwords)
+            with self._bw_lock:
+                if matched is not None:
+                    bs.apply_badwords_device(st, i, self.badwords, np.ascontiguousarray(matched, dtype=np.int8))
+                else:
+                    bs.apply_badwords(st, i, self.badwords)
         else:
             raise Unexpected(f"{t} is not a host step")
 
     def _badwords_automaton(self, needed) -> Tuple:
-        """Flattened tries of every loaded bad-words list (re-flattened when a batch needs a
-        language whose list was loaded since)."""
+        """Flattened tries of every loaded bad-words list and their hashed transition table
+        (rebuilt when a batch needs a language whose list was loaded since). A list that cannot
+        be loaded gets no root: the host step raises the same error the CPU path does."""
         a = getattr(self, "_bw_flat", None)
         if a is None or any(l not in a[4] and l not in self._bw_nolist for l in needed):
             for l in needed:
-                if not self.badwords.lookup(l)[1]:
+                try:
+                    if not self.badwords.lookup(l)[1]:
+                        self._bw_nolist.add(l)
+                except RuntimeError:
                     self._bw_nolist.add(l)
             fe, ec, et, term, roots, cjk = self.badwords.flatten()
+            term = np.ascontiguousarray(term, dtype=np.uint8)
+            table = self.h.bw_build_table(fe, np.ascontiguousarray(ec).view(np.uint32), et, term)
             self._bw_gen = getattr(self, "_bw_gen", 0) + 1
-            a = self._bw_flat = (fe, ec, et, term, roots, cjk, self._bw_gen)
+            a = self._bw_flat = (fe, ec, et, term, roots, cjk, self._bw_gen, table)
         return a
-
-    def _badwords_device(self, bs, st, i: int, ndocs: int) -> None:
-        """C4BadWordsFilter with the matching on the GPU: languages and keep-fraction draws
-        stay on the host (document order), the regex-equivalent search runs in k_badwords_match."""
-        if not hasattr(self, "_bw_nolist"):
-            self._bw_nolist = set()
-        langs = bs.badwords_languages(st, self.badwords)  # loads lists as needed
-        alive = bs.alive_indices()
-        matched = np.full(ndocs, -1, dtype=np.int8)
-        if len(alive):
-            alangs = [langs[j] for j in alive.tolist()]
-            fe, ec, et, term, roots, cjk, gen = self._badwords_automaton(set(alangs))
-            r = np.fromiter((roots.get(l, -1) for l in alangs), dtype=np.int32, count=len(alangs))
-            c = np.fromiter((cjk.get(l, False) for l in alangs), dtype=np.uint8, count=len(alangs))
-            sel = r >= 0
-            if sel.any():
-                idx = alive[sel]
-                d, o = bs.gather(idx)
-                matched[idx] = self.device_runner.badwords_match(gen, (fe, ec, et, term), d, o, r[sel], c[sel])
-        bs.apply_badwords_matched(st, i, self.badwords, matched, langs)
 
     def _process_subset_cpu(self, data, off, meta, rows: np.ndarray) -> BatchResult:
         lens = off[rows + 1] - off[rows]
@@ -608,9 +641,24 @@ class Engine:
         """The host re-derived every decision from the device records (apply_records); the
         device-compacted outputs are used only when both agree on every document's first failing
         step and status, and the compaction did not run out of room. Otherwise the batch is
-        assembled on the host (counted in tb_device_resolve_fallback_total)."""
-        ok = (resolved.err == 0 and np.array_equal(bs.fail_step(), resolved.fail)
-              and np.array_equal(bs.status(), resolved.status))
+        assembled on the host (counted in tb_device_resolve_fallback_total).
+
+        The one allowed difference: a C4BadWords step (resolved on the device as passing every
+        document) filtered a document the device kept or filtered at a later step; its output is
+        the same text (no rewrite follows the step, resolve_entries), so kept ones move to the
+        excluded side (``resolved.moved``) and the others keep their place."""
+        hf, hs = bs.fail_step(), bs.status()
+        ok = resolved.err == 0
+        if ok:
+            diff = np.nonzero((hf != resolved.fail) | (hs != resolved.status))[0]
+            if len(diff):
+                df, ds = resolved.fail[diff], resolved.status[diff]
+                ok = bool(len(self._bw_steps)) and bool(np.all(
+                    np.isin(hf[diff], self._bw_steps) & (hs[diff] == 1) & (ds <= 1) & ((df < 0) | (df > hf[diff]))))
+                if ok:
+                    nk, _ = resolved.counts()
+                    moved_docs = diff[ds == 0]
+                    resolved.moved = np.isin(resolved.rows[:nk], moved_docs) if len(moved_docs) else None
         if ok and resolved.ver is not None:
             # the content version the device compacted each output from must be the host's too
             out = resolved.status <= 1
@@ -620,6 +668,7 @@ class Engine:
 
             from ..utils import metrics
 
+            resolved.moved = None
             logging.getLogger("textblaster_amd.engine").warning(
                 "device resolve disagrees with the host decisions (or overflowed); assembling this batch on the host")
             metrics.DEVICE_RESOLVE_FALLBACK_TOTAL.inc()
@@ -631,20 +680,27 @@ class Engine:
         kept_rows = np.nonzero(status == 0)[0].astype(np.int64)
         excl_rows = np.nonzero(status == 1)[0].astype(np.int64)
         err_rows = np.nonzero(status == 2)[0].astype(np.int64)
-        parts = []
         if resolved is not None:
             # K16: texts were compacted on the device (kept, then excluded, document order — the
-            # rows above); only the metadata columns are built here
-            for rows, off, text in resolved.parts():
-                _, _, md, mo, mv = bs.assemble(rows, False)
-                parts.append(OutputPart(rows, text, off, md, mo, mv))
-        for rows in ((kept_rows, excl_rows) if resolved is None else ()):
-            td, to, md, mo, mv = bs.assemble(rows)
-            parts.append(OutputPart(rows, td, to, md, mo, mv))
+            # rows above; documents a host step filtered afterwards in a second excluded part);
+            # only the metadata columns are built here
+            sides = []
+            for side in resolved.parts(self.nthreads):
+                out = []
+                for rows, off, text in side:
+                    _, _, md, mo, mv = bs.assemble(rows, False)
+                    out.append(OutputPart(rows, text, off, md, mo, mv))
+                sides.append(out)
+            kept_parts, excl_parts = sides
+        else:
+            kept_parts, excl_parts = [], []
+            for rows, dst in ((kept_rows, kept_parts), (excl_rows, excl_parts)):
+                td, to, md, mo, mv = bs.assemble(rows)
+                dst.append(OutputPart(rows, td, to, md, mo, mv))
         reasons = {}
         if self.keep_reasons and len(excl_rows):
             reasons = dict(zip(excl_rows.tolist(), bs.reasons(excl_rows)))
-        return BatchResult(ndocs, [parts[0]], [parts[1]], err_rows, fail, status, reasons, timings)
+        return BatchResult(ndocs, kept_parts, excl_parts, err_rows, fail, status, reasons, timings)
 
     def step_names(self) -> List[str]:
         return [s.type for s in self.cfg.pipeline]

@@ -190,6 +190,21 @@ def make_corpus(n_docs: int, mean_bytes: int = 1024, seed: int = 0,
     return [make_doc(rng, langs[int(c)], int(s), vocab) for c, s in zip(choice, sizes)]
 
 
+def inject_words(texts: List[str], list_path: str, rate: float, seed: int = 0) -> List[str]:
+    """A fraction ``rate`` of the documents gets one entry of a word list (e.g. a C4 bad-words
+    list) inserted after a random space, so a word-list filter has matches to act on."""
+    with open(list_path, encoding="utf-8") as f:
+        entries = [ln.strip() for ln in f if ln.strip()]
+    rng = np.random.default_rng(7331 + seed)
+    out = list(texts)
+    for i in np.nonzero(rng.random(len(out)) < rate)[0].tolist():
+        t = out[i]
+        sp = [k for k in range(len(t)) if t[k] == " "]
+        at = sp[int(rng.integers(len(sp)))] + 1 if sp else 0
+        out[i] = t[:at] + entries[int(rng.integers(len(entries)))] + " " + t[at:]
+    return out
+
+
 def pack(texts: List[str]):
     """Pack strings into (uint8 data, int64 offsets) like an Arrow LargeUtf8 column."""
     enc = [t.encode("utf-8") for t in texts]

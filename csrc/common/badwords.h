@@ -1,6 +1,6 @@
 // C4 bad-words matching over the flattened word-list tries (reference c4_filters.rs:431-441,516:
 // `(?i)(?:\W|^)(w1|w2|...)(?:\W|$)`, no boundary requirement for the CJK lists). Shared by the
-// device kernel (k_badwords_match: one wave per document, one start position per lane) and the
+// device kernel (k_badwords_match: one wave per document, four start positions per lane) and the
 // host emulation (bw_match_doc), so the CPU tests pin the exact walk the GPU runs.
 //
 // Transitions are one open-addressing hash table over (node, folded code point) instead of a
@@ -54,42 +54,64 @@ TB_HD int32_t bw_step(const BwTable& t, int32_t node, uint32_t cp, bool* term) {
   }
 }
 
-TB_HD bool bw_wordchar(const UcdView& ucd, uint32_t cp) { return (ucd.props(cp) & P_WORDCHAR) != 0; }
+// ASCII code points resolved from a 128-entry table (word-character bit 7 | simple fold, from
+// the same property / fold tables): the kernel keeps it in LDS, so the common case needs no
+// dependent global lookups.
+template <class A>
+TB_HD bool bw_wordchar(const UcdView& ucd, const A& asc, uint32_t cp) {
+  if (cp < 128) return (asc[cp] & 0x80u) != 0;
+  return (ucd.props(cp) & P_WORDCHAR) != 0;
+}
+template <class A>
+TB_HD uint32_t bw_fold(const BwFold& fold, const A& asc, uint32_t cp) {
+  return cp < 128 ? (uint32_t)(asc[cp] & 0x7Fu) : fold(cp);
+}
+TB_HD uint8_t bw_ascii_entry(const UcdView& ucd, const BwFold& fold, uint32_t c) {
+  return (uint8_t)(((ucd.props(c) & P_WORDCHAR) ? 0x80u : 0u) | (fold(c) & 0x7Fu));
+}
 
-// Does a list entry start at byte s (a code point boundary) of b[0, n)?
-TB_HD bool bw_match_from(const uint8_t* b, uint32_t n, uint32_t s, int32_t root, bool cjk, const BwTable& t,
-                         const UcdView& ucd, const BwFold& fold) {
-  if (!cjk && s > 0) {  // (?:\W|^): the previous code point is not a word character
-    uint32_t p = s - 1;
-    while (p > 0 && !utf8_is_lead(b[p])) --p;
-    int len;
-    const uint32_t c = b[p] < 0x80 ? b[p] : utf8_decode(b, p, n, &len);
-    if (bw_wordchar(ucd, c)) return false;
-  }
+// (?:\W|^) before byte s (a code point boundary): the previous code point is not a word character.
+template <class A>
+TB_HD bool bw_left_ok(const uint8_t* b, uint32_t n, uint32_t s, const UcdView& ucd, const A& asc) {
+  if (s == 0) return true;
+  const uint8_t pb = b[s - 1];
+  if (pb < 0x80) return (asc[pb] & 0x80u) == 0;
+  uint32_t p = s - 1;
+  while (p > 0 && !utf8_is_lead(b[p])) --p;
+  int len;
+  return !bw_wordchar(ucd, asc, utf8_decode(b, p, n, &len));
+}
+
+// Does a list entry start at byte s (a code point boundary whose left side is already checked)?
+template <class A>
+TB_HD bool bw_walk_from(const uint8_t* b, uint32_t n, uint32_t s, int32_t root, bool cjk, const BwTable& t,
+                        const UcdView& ucd, const BwFold& fold, const A& asc) {
   int32_t node = root;
   uint32_t j = s;
   while (j < n) {
     int len = 1;
     const uint32_t c = b[j] < 0x80 ? b[j] : utf8_decode(b, j, n, &len);
     bool term = false;
-    node = bw_step(t, node, fold(c), &term);
+    node = bw_step(t, node, bw_fold(fold, asc, c), &term);
     if (node < 0) return false;
     j += (uint32_t)len;
     if (term) {
       if (cjk || j >= n) return true;
       int l2;
       const uint32_t d = b[j] < 0x80 ? b[j] : utf8_decode(b, j, n, &l2);
-      if (!bw_wordchar(ucd, d)) return true;  // (?:\W|$)
+      if (!bw_wordchar(ucd, asc, d)) return true;  // (?:\W|$)
     }
   }
   return false;
 }
 
 // Host twin of k_badwords_match for one document.
+template <class A>
 TB_HD bool bw_match_doc(const uint8_t* b, uint32_t n, int32_t root, bool cjk, const BwTable& t, const UcdView& ucd,
-                        const BwFold& fold) {
+                        const BwFold& fold, const A& asc) {
   for (uint32_t s = 0; s < n; ++s)
-    if (utf8_is_lead(b[s]) && bw_match_from(b, n, s, root, cjk, t, ucd, fold)) return true;
+    if (utf8_is_lead(b[s]) && (cjk || bw_left_ok(b, n, s, ucd, asc)) && bw_walk_from(b, n, s, root, cjk, t, ucd, fold, asc))
+      return true;
   return false;
 }
 

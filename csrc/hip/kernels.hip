@@ -367,32 +367,59 @@ __global__ __launch_bounds__(kBlockThreads) void k_c4_pass_a_blk(
 // version its step sees and skips the documents a pass before the step filtered
 // (0 < dead <= dead_max); matched: -1 skipped / no list, 0 no match, 1 match.
 constexpr int kBwWaves = 4;
+// Work items: without a segment list, wave w takes document w and the start positions
+// [0, seg_bytes) and writes its verdict; with one (seg_doc / seg_idx, launched afterwards on the
+// same stream), wave w takes positions [seg_idx * seg_bytes, +seg_bytes) of document seg_doc[w] —
+// the long documents' remaining segments, so no single wave walks a whole long document — skips
+// documents already decided, and only ever writes a match.
 __global__ __launch_bounds__(64 * kBwWaves) void k_badwords_match(
-    const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off, int32_t ndocs,
+    const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off, int32_t nitems,
     const int32_t* __restrict__ root, const uint8_t* __restrict__ cjk, int32_t root0, int32_t cjk0,
     const uint8_t* __restrict__ dead, uint32_t dead_max, BwTable tab, DevTables tabs, BwFold fold,
-    int8_t* __restrict__ matched) {
-  const int doc = (int)blockIdx.x * kBwWaves + (int)(threadIdx.x >> 6);
-  if (doc >= ndocs) return;
+    int8_t* __restrict__ matched, const int32_t* __restrict__ seg_doc, const int32_t* __restrict__ seg_idx,
+    uint32_t seg_bytes) {
+  __shared__ uint8_t asc[128];
+  const UcdView ucd{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
+  if (threadIdx.x < 128) asc[threadIdx.x] = bw_ascii_entry(ucd, fold, threadIdx.x);
+  __syncthreads();
+  const int item = (int)blockIdx.x * kBwWaves + (int)(threadIdx.x >> 6);
+  if (item >= nitems) return;
+  const int doc = seg_doc ? seg_doc[item] : item;
   const uint32_t lane = threadIdx.x & 63;
   const int32_t r0 = root ? root[doc] : root0;
   const uint32_t dd = dead ? dead[doc] : 0u;
-  if (r0 < 0 || (dd != 0 && dd <= dead_max)) {
+  if (seg_doc) {
+    if (matched[doc] != 0) return;  // decided (match, or skipped) by the first pass
+  } else if (r0 < 0 || (dd != 0 && dd <= dead_max)) {
     if (lane == 0) matched[doc] = -1;
     return;
   }
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
-  const UcdView ucd{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
   const bool any_edge = (cjk ? cjk[doc] : (uint8_t)cjk0) != 0;
+  const uint32_t p0 = seg_doc ? (uint32_t)seg_idx[item] * seg_bytes : 0u;
+  const uint32_t p1 = p0 + seg_bytes < n ? p0 + seg_bytes : n;
   bool found = false;
-  for (uint32_t base = 0; base < n; base += 64) {
-    const uint32_t s = base + lane;
-    if (s < n && utf8_is_lead(b[s])) found = bw_match_from(b, n, s, r0, any_edge, tab, ucd, fold);
-    if (__ballot(found)) break;
+  // 256 positions per iteration, 4 consecutive bytes per lane: the left-boundary test of a
+  // position reads the previous byte from the lane's own bytes or its neighbour; only positions
+  // that start a word walk the trie (the walk itself may run past the segment end)
+  for (uint32_t base = p0; base < p1 && !found; base += 256) {
+    const uint32_t s0 = base + 4 * lane;
+    uint8_t c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = s0 + k < p1 ? b[s0 + k] : (uint8_t)0;
+    const uint8_t before = s0 > 0 && s0 < p1 ? b[s0 - 1] : (uint8_t)' ';
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t s = s0 + k;
+      if (s >= p1 || !utf8_is_lead(c[k])) continue;
+      const uint8_t pb = k ? c[k - 1] : before;
+      bool left = any_edge || s == 0 || (pb < 0x80 ? (asc[pb] & 0x80u) == 0 : bw_left_ok(b, n, s, ucd, asc));
+      if (left && bw_walk_from(b, n, s, r0, any_edge, tab, ucd, fold, asc)) { found = true; break; }
+    }
+    found = __ballot(found) != 0;
   }
-  const bool anyf = __ballot(found) != 0;
-  if (lane == 0) matched[doc] = anyf ? 1 : 0;
+  if (lane == 0 && (found || !seg_doc)) matched[doc] = found ? 1 : 0;
 }
 
 __global__ __launch_bounds__(256) void k_c4_pass_b(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
@@ -678,17 +705,20 @@ int tb_c4_pass_a_blk(hipStream_t stream, const void* c4, const uint8_t* bytes, c
 
 int tb_block_threads() { return kBlockThreads; }
 
-int tb_badwords_match(hipStream_t stream, const uint8_t* bytes, const int64_t* off, int32_t ndocs, const int32_t* root,
+int tb_badwords_match(hipStream_t stream, const uint8_t* bytes, const int64_t* off, int32_t nitems, const int32_t* root,
                       const uint8_t* cjk, int32_t root0, int32_t cjk0, const uint8_t* dead, uint32_t dead_max,
                       const uint32_t* table, uint32_t table_mask, const uint16_t* s1, const uint32_t* s2,
-                      const uint16_t* l1, const int32_t* l2, const uint16_t* f1, const int32_t* f2, int8_t* matched) {
-  if (ndocs <= 0) return 0;
-  if (!table || ((table_mask + 1) & table_mask) != 0) return (int)hipErrorInvalidValue;
+                      const uint16_t* l1, const int32_t* l2, const uint16_t* f1, const int32_t* f2, int8_t* matched,
+                      const int32_t* seg_doc, const int32_t* seg_idx, uint32_t seg_bytes) {
+  if (nitems <= 0) return 0;
+  if (!table || ((table_mask + 1) & table_mask) != 0 || seg_bytes < 256 || (seg_bytes & 255) || (!seg_doc != !seg_idx))
+    return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
   const BwTable bt{table, table_mask};
   const BwFold fold{f1, f2};
-  hipLaunchKernelGGL(k_badwords_match, dim3((ndocs + kBwWaves - 1) / kBwWaves), dim3(64 * kBwWaves), 0, stream, bytes,
-                     off, ndocs, root, cjk, root0, cjk0, dead, dead_max, bt, t, fold, matched);
+  hipLaunchKernelGGL(k_badwords_match, dim3((nitems + kBwWaves - 1) / kBwWaves), dim3(64 * kBwWaves), 0, stream, bytes,
+                     off, nitems, root, cjk, root0, cjk0, dead, dead_max, bt, t, fold, matched, seg_doc, seg_idx,
+                     seg_bytes);
   return (int)hipGetLastError();
 }
 

@@ -280,6 +280,8 @@ PYBIND11_MODULE(_tbhost, m) {
     static const std::vector<int32_t> f2(TB_UCD_FOLD_STAGE2, TB_UCD_FOLD_STAGE2 + sizeof(TB_UCD_FOLD_STAGE2) / 4);
     const BwFold fold{f1.data(), f2.data()};
     const UcdView& ucd = host_ucd();
+    uint8_t asc[128];
+    for (uint32_t c = 0; c < 128; ++c) asc[c] = bw_ascii_entry(ucd, fold, c);
     const uint8_t* b = data.data();
     const int64_t* o = off.data();
     {
@@ -290,7 +292,7 @@ PYBIND11_MODULE(_tbhost, m) {
           const uint32_t d = dp ? dp[i] : 0u;
           if (r < 0 || (d != 0 && d <= dead_max)) continue;
           out[(size_t)i] = bw_match_doc(b + o[i], (uint32_t)(o[i + 1] - o[i]), r, (cp ? cp[i] : cjk0) != 0, bt, ucd,
-                                        fold) ? 1 : 0;
+                                        fold, asc) ? 1 : 0;
         }
       });
     }
@@ -661,8 +663,10 @@ PYBIND11_MODULE(_tbhost, m) {
         // draws (document order) are decided here, as apply_badwords does
         if ((int64_t)matched.size() != b.st->size()) throw std::invalid_argument("matched length");
         py::gil_scoped_release nogil;
-        const std::vector<std::string> lang = b.st->badwords_languages(c, *bw);
-        b.st->apply_badwords_matched(c, step_index, *bw, matched.data(), lang);
+        std::vector<int32_t> code;
+        std::vector<std::string> names;
+        b.st->badwords_lang_codes(c, *bw, code, names);
+        b.st->apply_badwords_codes(c, step_index, *bw, matched.data(), code, names);
       })
       .def("gather", [](PyBatch& b, py::array_t<int64_t, py::array::c_style> idx) {
         std::vector<int64_t> iv(idx.data(), idx.data() + idx.size());

@@ -1,3 +1,4 @@
+#include <unordered_map>
 #include "pipeline.h"
 
 #include <unicode/uchar.h>
@@ -451,42 +452,101 @@ void BatchState::apply_records(const StepCfg& cfg, int step_index, const int64_t
   });
 }
 
-std::vector<std::string> BatchState::badwords_languages(const StepCfg& cfg, BadWordsModule& mod) const {
+void BatchState::badwords_lang_codes(const StepCfg& cfg, BadWordsModule& mod, std::vector<int32_t>& code,
+                                     std::vector<std::string>& names) const {
   // The document language: metadata "language" (no step writes that key, so only the input
-  // metadata can hold it), else the configured default (reference c4_filters.rs:478-486).
-  std::vector<std::string> lang(n_);
-  parallel_for(n_, nthreads_, [&](int64_t a, int64_t b) {
-    FlatMeta fm;
-    for (int64_t i = a; i < b; ++i) {
-      if (fail_step_[i] >= 0) continue;
-      lang[i] = cfg.default_language;
-      if (input_meta(i, fm) && fm.has("language")) lang[i] = std::string(fm.get("language"));
-    }
-  });
-  // word lists load lazily, on this thread
+  // metadata can hold it), else the configured default (reference c4_filters.rs:464-468); as an
+  // index into `names` (names[0] = the default), -1 for documents already filtered.
+  code.assign((size_t)n_, -1);
+  names.assign(1, cfg.default_language);
+  std::vector<std::string> val;
+  std::vector<uint8_t> has;
+  if (meta_data_) {
+    val.resize((size_t)n_);
+    has.assign((size_t)n_, 0);
+    parallel_for(n_, nthreads_, [&](int64_t a, int64_t b) {
+      FlatMeta fm;
+      for (int64_t i = a; i < b; ++i)
+        if (fail_step_[i] < 0 && input_meta(i, fm) && fm.has("language")) {
+          val[(size_t)i] = std::string(fm.get("language"));
+          has[(size_t)i] = 1;
+        }
+    });
+  }
+  std::unordered_map<std::string, int32_t> idx;
+  idx.emplace(cfg.default_language, 0);
+  std::vector<uint8_t> used(1, 0);
   for (int64_t i = 0; i < n_; ++i) {
     if (fail_step_[i] >= 0) continue;
-    bool sup;
-    mod.get(lang[i], &sup);
+    int32_t c = 0;
+    if (!has.empty() && has[(size_t)i]) {
+      auto it = idx.find(val[(size_t)i]);
+      if (it == idx.end()) {
+        it = idx.emplace(val[(size_t)i], (int32_t)names.size()).first;
+        names.push_back(val[(size_t)i]);
+        used.push_back(0);
+      }
+      c = it->second;
+    }
+    code[(size_t)i] = c;
+    used[(size_t)c] = 1;
   }
+  // word lists load lazily, on this thread, once per language some document uses
+  for (size_t k = 0; k < names.size(); ++k) {
+    if (!used[k]) continue;
+    bool sup;
+    mod.get(names[k], &sup);
+  }
+}
+
+std::vector<std::string> BatchState::badwords_languages(const StepCfg& cfg, BadWordsModule& mod) const {
+  std::vector<int32_t> code;
+  std::vector<std::string> names;
+  badwords_lang_codes(cfg, mod, code, names);
+  std::vector<std::string> lang((size_t)n_);
+  for (int64_t i = 0; i < n_; ++i) if (code[(size_t)i] >= 0) lang[(size_t)i] = names[(size_t)code[(size_t)i]];
   return lang;
 }
 
 void BatchState::apply_badwords(const StepCfg& cfg, int step_index, BadWordsModule& mod) {
-  const std::vector<std::string> lang = badwords_languages(cfg, mod);
+  std::vector<int32_t> code;
+  std::vector<std::string> names;
+  badwords_lang_codes(cfg, mod, code, names);
+  std::vector<std::shared_ptr<BadWordsLang>> lists(names.size());
+  for (size_t k = 0; k < names.size(); ++k) {
+    auto it = mod.langs.find(names[k]);
+    if (it != mod.langs.end()) lists[k] = it->second;
+  }
   std::vector<int8_t> matched(n_, -1);  // -1 n/a, 0 no match, 1 match
   parallel_for(n_, nthreads_, [&](int64_t a, int64_t b) {
     for (int64_t i = a; i < b; ++i) {
-      if (fail_step_[i] >= 0) continue;
-      auto it = mod.langs.find(lang[i]);
-      if (it != mod.langs.end() && it->second) matched[i] = it->second->match(content(i)) ? 1 : 0;
+      if (code[(size_t)i] < 0) continue;
+      const auto& l = lists[(size_t)code[(size_t)i]];
+      if (l) matched[i] = l->match(content(i)) ? 1 : 0;
     }
   });
-  apply_badwords_matched(cfg, step_index, mod, matched.data(), lang);
+  apply_badwords_codes(cfg, step_index, mod, matched.data(), code, names);
 }
 
 void BatchState::apply_badwords_matched(const StepCfg& cfg, int step_index, BadWordsModule& mod,
                                         const int8_t* matched, const std::vector<std::string>& lang) {
+  std::vector<int32_t> code((size_t)n_, -1);
+  std::vector<std::string> names;
+  std::unordered_map<std::string, int32_t> idx;
+  for (int64_t i = 0; i < n_; ++i) {
+    if (fail_step_[i] >= 0) continue;
+    auto it = idx.find(lang[(size_t)i]);
+    if (it == idx.end()) {
+      it = idx.emplace(lang[(size_t)i], (int32_t)names.size()).first;
+      names.push_back(lang[(size_t)i]);
+    }
+    code[(size_t)i] = it->second;
+  }
+  apply_badwords_codes(cfg, step_index, mod, matched, code, names);
+}
+
+void BatchState::apply_badwords_codes(const StepCfg& cfg, int step_index, BadWordsModule& mod, const int8_t* matched,
+                                      const std::vector<int32_t>& code, const std::vector<std::string>& names) {
   step_slot(step_index);
   auto out = std::make_unique<BwOut>();
   out->code.assign(n_, -1);
@@ -495,25 +555,27 @@ void BatchState::apply_badwords_matched(const StepCfg& cfg, int step_index, BadW
     uint64_t seed = cfg.seed ? *cfg.seed : (((uint64_t)std::random_device{}() << 32) ^ std::random_device{}());
     mod.rng = std::make_unique<StdRng>(seed);
   }
+  std::vector<uint8_t> sup(names.size(), 0);
+  for (size_t k = 0; k < names.size(); ++k)
+    for (auto l : kBadwordsLangs) if (names[k] == l) sup[k] = 1;
   // keep-fraction draws from the shared stream, in document order
   for (int64_t i = 0; i < n_; ++i) {
-    if (fail_step_[i] >= 0) continue;
-    bool sup = false;
-    for (auto l : kBadwordsLangs) if (lang[i] == l) sup = true;
-    int8_t code;
-    if (!sup) {
-      code = cfg.fail_on_missing_language ? BW_MISSING_LANG_FAIL : BW_NO_REGEX;
-      if (code == BW_MISSING_LANG_FAIL) out->lang[i] = lang[i];
+    if (fail_step_[i] >= 0 || code[(size_t)i] < 0) continue;
+    const size_t c = (size_t)code[(size_t)i];
+    int8_t st;
+    if (!sup[c]) {
+      st = cfg.fail_on_missing_language ? BW_MISSING_LANG_FAIL : BW_NO_REGEX;
+      if (st == BW_MISSING_LANG_FAIL) out->lang[i] = names[c];
     } else if (matched[i] < 0) {
-      code = BW_NO_REGEX;
+      st = BW_NO_REGEX;
     } else if (matched[i] == 1) {
-      code = (cfg.keep_fraction > 0.0 && mod.rng->gen_f32() < (float)cfg.keep_fraction) ? BW_KEPT_BY_FRACTION
-                                                                                          : BW_FILTERED;
+      st = (cfg.keep_fraction > 0.0 && mod.rng->gen_f32() < (float)cfg.keep_fraction) ? BW_KEPT_BY_FRACTION
+                                                                                      : BW_FILTERED;
     } else {
-      code = BW_PASSED;
+      st = BW_PASSED;
     }
-    out->code[i] = code;
-    set_status(i, step_index, (code == BW_FILTERED || code == BW_MISSING_LANG_FAIL) ? 1 : 0);
+    out->code[i] = st;
+    set_status(i, step_index, (st == BW_FILTERED || st == BW_MISSING_LANG_FAIL) ? 1 : 0);
   }
   bw_[step_index] = std::move(out);
 }

@@ -124,6 +124,11 @@ class BatchState {
   // decisions from externally computed matches (-1 n/a, 0, 1), drawing the keep-fraction RNG
   // in document order exactly like apply_badwords.
   std::vector<std::string> badwords_languages(const StepCfg& cfg, BadWordsModule& mod) const;
+  // per alive document an index into names (names[0] = the step's default language), lists loaded
+  void badwords_lang_codes(const StepCfg& cfg, BadWordsModule& mod, std::vector<int32_t>& code,
+                           std::vector<std::string>& names) const;
+  void apply_badwords_codes(const StepCfg& cfg, int step_index, BadWordsModule& mod, const int8_t* matched,
+                            const std::vector<int32_t>& code, const std::vector<std::string>& names);
   void apply_badwords_matched(const StepCfg& cfg, int step_index, BadWordsModule& mod, const int8_t* matched,
                               const std::vector<std::string>& lang);
   // Current contents of documents idx, packed (for device steps that run after the resolve).

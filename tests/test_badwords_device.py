@@ -170,11 +170,13 @@ def _bw_corpus(n, seed):
     rng = random.Random(seed)
     texts = synth.make_corpus(n, 700, seed=seed)
     out = []
-    for t in texts:
+    for k, t in enumerate(texts):
+        if k % 40 == 7:
+            t = (t + "\n") * 12  # long documents: matches deep in later k_badwords_match segments
         r = rng.random()
         if r < 0.25:
             w = rng.choice(["dummybadword", "Exact Phrase", "GRIMT", "xdummybadwordx", "co-op"])
-            cut = rng.randrange(len(t) + 1)
+            cut = rng.randrange(len(t) + 1) if k % 40 != 7 else len(t) - rng.randrange(1, 40)
             t = t[:cut] + " " + w + " " + t[cut:]
         out.append(t)
     meta = [(b'{"language":"%s"}' % rng.choice([b"en", b"da", b"ja", b"zz"])) if i % 3 else b""

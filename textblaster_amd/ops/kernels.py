@@ -38,7 +38,8 @@ _SIGS = {
     "tb_resolve": [_P, _P, _P, _I32, _I32, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P],
     "tb_sizeof_resolve": [],
     "tb_block_threads": [],
-    "tb_badwords_match": [_P, _P, _P, _I32, _P, _P, _I32, _I32, _P, _U32, _P, _U32, _P, _P, _P, _P, _P, _P, _P],
+    "tb_badwords_match": [_P, _P, _P, _I32, _P, _P, _I32, _I32, _P, _U32, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                          _U32],
     "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
     "tb_c4_pass_b": [_P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "tb_langid_head": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I32, _P],
@@ -233,10 +234,12 @@ class Kernels:
         _check(rc, "tb_c4_pass_a_blk")
 
     def badwords_match(self, bytes_, off, ndocs, table, fold, matched, root=None, cjk=None, root0=-1, cjk0=0,
-                       dead=None, dead_max=0):
+                       dead=None, dead_max=0, seg_bytes=2048, seg_doc=None, seg_idx=None):
         """k_badwords_match over documents [0, ndocs) of (bytes_, off): ``table`` is the hashed trie
         table (uint32 [4 * slots], csrc/common/badwords.h); per document root/cjk arrays, or one
-        root0/cjk0 for all; documents with 0 < dead <= dead_max are skipped (matched -1)."""
+        root0/cjk0 for all; documents with 0 < dead <= dead_max are skipped (matched -1). The first
+        launch covers the first ``seg_bytes`` of every document; ``seg_doc`` / ``seg_idx`` (int32,
+        the documents' further segments) add a second launch over those segments."""
         t = self.tabs
         f1, f2 = fold
         slots = table.numel() // 4
@@ -245,11 +248,18 @@ class Kernels:
         for a in (root, cjk, dead):
             if a is not None and a.numel() < ndocs:
                 raise DeviceError("badwords_match: per-document array shorter than the batch")
-        rc = self.lib.tb_badwords_match(
-            self.stream(), bytes_.data_ptr(), off.data_ptr(), ndocs, _ptr(root), _ptr(cjk), int(root0), int(cjk0),
-            _ptr(dead), int(dead_max), table.data_ptr(), slots - 1, t[0].data_ptr(), t[1].data_ptr(),
-            t[2].data_ptr(), t[3].data_ptr(), f1.data_ptr(), f2.data_ptr(), matched.data_ptr())
-        _check(rc, "tb_badwords_match")
+        if (seg_doc is None) != (seg_idx is None) or (seg_doc is not None and seg_doc.numel() != seg_idx.numel()):
+            raise DeviceError("badwords_match: segment lists")
+        for sd, si in ((None, None), (seg_doc, seg_idx)):
+            nitems = ndocs if sd is None else sd.numel()
+            if sd is not None and nitems == 0:
+                continue
+            rc = self.lib.tb_badwords_match(
+                self.stream(), bytes_.data_ptr(), off.data_ptr(), nitems, _ptr(root), _ptr(cjk), int(root0), int(cjk0),
+                _ptr(dead), int(dead_max), table.data_ptr(), slots - 1, t[0].data_ptr(), t[1].data_ptr(),
+                t[2].data_ptr(), t[3].data_ptr(), f1.data_ptr(), f2.data_ptr(), matched.data_ptr(), _ptr(sd), _ptr(si),
+                int(seg_bytes))
+            _check(rc, "tb_badwords_match")
 
     def langid_features(self, bytes_, off, perm, ndocs, scratch, scratch_off, emb, vec, cnt, flags, lds_bytes=0,
                         prof=None, embx=None):

@@ -380,6 +380,26 @@ def plan_passes(plan: ExecPlan, stage_layout, steps_native, gating: bool, lid_ga
     return passes, pass_of_step, gates
 
 
+BW_SEG_BYTES = 2048  # start positions per k_badwords_match wave
+
+
+def bw_segments(lens: np.ndarray, growth: int, seg: int):
+    """(doc, segment) lists of k_badwords_match's second launch: segments 1.. of every document
+    whose length bound (input length + the content growth its C4 rewrites allow) exceeds one
+    segment, so long documents are spread over waves instead of one wave walking them whole."""
+    bound = lens.astype(np.int64) + int(growth)
+    extra = np.maximum((bound + seg - 1) // seg - 1, 0)
+    idx = np.nonzero(extra)[0]
+    if not len(idx):
+        z = np.zeros(0, dtype=np.int32)
+        return z, z
+    cnt = extra[idx]
+    seg_doc = np.repeat(idx, cnt).astype(np.int32)
+    starts = np.cumsum(cnt) - cnt
+    seg_idx = (np.arange(int(cnt.sum()), dtype=np.int64) - np.repeat(starts, cnt) + 1).astype(np.int32)
+    return seg_doc, seg_idx
+
+
 def bw_dead_max(plan: ExecPlan, passes, pass_of_step: Dict[int, int]) -> Dict[int, int]:
     """Per C4BadWords step q: the device passes [0, q) hold only steps before it, so a document a
     gate marked dead <= q never reached the step (dead = k: the gate of pass k-1 filtered it);
@@ -783,19 +803,23 @@ class DeviceRunner:
         n_mid = int(np.count_nonzero(lens > self.mid_doc_bytes)) if self.mid_doc_bytes > 0 else n_long
         n_mid = max(n_mid, n_long)
         direct_keep: List = []
-        # per-document bad-words roots / CJK flags travel in the same upload
-        bw_arrays = [(i, a) for i in sorted(bw) for a in (bw[i].roots, bw[i].cjk) if a is not None]
+        # per-document bad-words roots / CJK flags and the long documents' segment lists travel in
+        # the same upload
+        bw_arrays = [((i, "root" if a.dtype == np.int32 else "cjk"), a) for i in sorted(bw)
+                     for a in (bw[i].roots, bw[i].cjk) if a is not None]
         for _, a in bw_arrays:
             if len(a) != ndocs:
                 raise DeviceError("badwords: per-document inputs do not match the batch")
+        for v in sorted({self.plan.steps[i].version_in for i in bw}):
+            sd, si = bw_segments(lens, self.c4_growth * v, BW_SEG_BYTES)
+            if len(sd):
+                bw_arrays += [((v, "seg_doc"), sd), ((v, "seg_idx"), si)]
         with tracing.trace_range("tb.stage_h2d"):
             staged_views, staged = self._stage_inputs(
                 slot, [data if len(data) else np.zeros(1, np.uint8), off, perm, scratch_off]
                 + [np.ascontiguousarray(a) for _, a in bw_arrays], direct_keep)
         d_bytes, d_off, d_perm, d_soff = staged_views[:4]
-        bw_dev = {}
-        for (i, a), d in zip(bw_arrays, staged_views[4:]):
-            bw_dev[(i, a.dtype == np.int32)] = d
+        bw_dev = {key: d for (key, _), d in zip(bw_arrays, staged_views[4:])}
         scratch = self._scratch_for(slot, int(scratch_off[-1]))
         # grows (new tensor, on this slot's stream) only for documents over 2 MB; the batch keeps a
         # reference to the table it used, so the other slot's kernels never see it freed
@@ -1001,9 +1025,11 @@ class DeviceRunner:
             vb, vo, _ = versions[sp.version_in]
             table, fold = self._bw_tables(x)
             m = rt.empty(max(ndocs, 1), np.int8)
+            v = sp.version_in
             with self._ktimed(keep, "badwords"):
-                self.k.badwords_match(vb, vo, ndocs, table, fold, m, bw_dev.get((i, True)), bw_dev.get((i, False)),
-                                      x.root0, x.cjk0, dead, self.bw_dead_max[i])
+                self.k.badwords_match(vb, vo, ndocs, table, fold, m, bw_dev.get((i, "root")), bw_dev.get((i, "cjk")),
+                                      x.root0, x.cjk0, dead, self.bw_dead_max[i], BW_SEG_BYTES,
+                                      bw_dev.get((v, "seg_doc")), bw_dev.get((v, "seg_idx")))
             keep += [table, m]
             bw_d[i] = m
         res_d = None

@@ -18,8 +18,11 @@ def test_heldout_accuracy():
     sent, doc = res["sentence"], res["document"]
     acc_s = np.diag(sent[:, :len(LANGS)]) / sent.sum(1)
     acc_d = np.diag(doc[:, :len(LANGS)]) / doc.sum(1)
+    assert sent.sum(1).min() >= 100  # >= 100 held-out sentences per language
     for i, lang in enumerate(LANGS):
-        if lang in ("eng", "dan", "swe"):
-            assert acc_s[i] >= 0.95 and acc_d[i] >= 0.95, (lang, acc_s[i], acc_d[i])
+        if lang in ("eng", "swe"):
+            assert acc_s[i] >= 0.97 and acc_d[i] >= 0.97, (lang, acc_s[i], acc_d[i])
+        elif lang == "dan":  # Danish / Bokmal share most trigrams on single sentences
+            assert acc_s[i] >= 0.95 and acc_d[i] >= 0.97, (lang, acc_s[i], acc_d[i])
         else:  # Bokmal / Nynorsk: the close pair
-            assert acc_s[i] >= 0.75 and acc_d[i] >= 0.9, (lang, acc_s[i], acc_d[i])
+            assert acc_s[i] >= 0.90 and acc_d[i] >= 0.97, (lang, acc_s[i], acc_d[i])

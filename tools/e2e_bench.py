@@ -61,6 +61,9 @@ def main():
     ap.add_argument("--html-decode", default="cpu")
     ap.add_argument("--keep-input", action="store_true")
     ap.add_argument("--repeat", type=int, default=1, help="runs per backend (all reported; the median last)")
+    ap.add_argument("--cli", action="store_true",
+                    help="also run the CLI (`python -m textblaster_amd.cli run --backend cuda`) as a child process: "
+                         "wall time from process start to exit, CPU time of the child")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     inp = os.path.join(args.out, "input.parquet")
@@ -98,6 +101,34 @@ def main():
             print(summary, flush=True)
         for p in (o, e):
             os.remove(p)
+    if args.cli:
+        import resource
+        import subprocess
+
+        o = os.path.join(args.out, "cli.out.parquet")
+        e = os.path.join(args.out, "cli.excluded.parquet")
+        cmd = [sys.executable, "-m", "textblaster_amd", "run", "-i", inp, "-o", o, "-e", e, "-c", args.config,
+               "--backend", "cuda", "--unit-rows", str(args.unit_rows), "--html-decode", args.html_decode,
+               "--log-dir", os.path.join(args.out, "log")]
+        ru0 = resource.getrusage(resource.RUSAGE_CHILDREN)
+        t0 = time.perf_counter()
+        cp = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True)
+        wall = time.perf_counter() - t0
+        ru1 = resource.getrusage(resource.RUSAGE_CHILDREN)
+        cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+        if cp.returncode != 0:
+            print(cp.stdout[-2000:], cp.stderr[-4000:], file=sys.stderr)
+            raise SystemExit(f"CLI run failed with exit code {cp.returncode}")
+        summary = [ln.strip() for ln in cp.stdout.splitlines() if ":" in ln]
+        read = [int(ln.split(":")[1]) for ln in summary if ln.startswith("Documents Read")]
+        ndocs = read[0] if read else args.docs
+        print(json.dumps({"backend": "cli-cuda", "docs": ndocs, "seconds_wall_incl_startup": round(wall, 3),
+                          "docs_per_sec": round(ndocs / wall, 1), "cpu_seconds": round(cpu, 3),
+                          "cpu_us_per_doc": round(1e6 * cpu / max(ndocs, 1), 3), "summary": summary[:12]}),
+              flush=True)
+        for p in (o, e):
+            if os.path.exists(p):
+                os.remove(p)
     for backend, r in rates.items():
         if len(r) > 1:
             print(json.dumps({"backend": backend, "runs": len(r), "docs_per_sec_median": float(np.median(r)),

@@ -6,7 +6,7 @@ pipeline (BASELINE.json metric) on N MI355X GPUs of one node, one process per GP
 
 One step = every rank pushes one batch of synthetic CommonCrawl-shaped documents (log-normal
 lengths around 1 KB, 5 languages) through the whole pipeline: H2D staging, all device stages
-(analysis kernels, C4 rewrite passes, bf16 MFMA language-id head), D2H, per-document
+(analysis kernels, C4 rewrite passes, hashed n-gram language-id kernel), D2H, per-document
 first-failure resolution with reason/metadata formatting, and assembly of the kept/excluded
 text + metadata JSON columns. Parquet decode/encode is not in the timed step (the reference's
 worker docs/sec excludes it too). Weak scaling: per-GPU batch fixed as N grows; RCCL all-reduces
@@ -192,7 +192,7 @@ def main():
                     f"{'~130-word' if args.vocab == 'small' else '60k-type Zipf'} vocabularies), "
                     f"{args.docs_per_step} docs/GPU/step",
             "config": {
-                "model": "+".join(s.type.replace("LanguageDetectionFilter", "LanguageDetection(fastText bf16 MFMA head)")
+                "model": "+".join(s.type.replace("LanguageDetectionFilter", "LanguageDetection(hashed 1-4-gram int16 logit table)")
                                   .replace("Filter", "") for s in cfg.pipeline),
                 "global_batch": args.docs_per_step * world,
                 "seq_len": int(bytes_per_step / args.docs_per_step),

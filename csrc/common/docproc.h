@@ -700,8 +700,6 @@ struct StageOut {
   int64_t* rec;     // record buffer (all steps of the stage)
   uint32_t ndocs;
   uint32_t doc;
-  uint16_t* lid_vec;  // [ndocs][kLidDim] doc vectors (bf16) for the MFMA head
-  int32_t* lid_cnt;   // [ndocs] n-gram counts (0 = nothing to detect)
   GrExport* gr_export = nullptr;  // non-null: split mode for this document (see GrExport)
 };
 
@@ -1083,37 +1081,17 @@ TB_HD void gr_dup_one_order(DocCtx<P>& x, const DevStep& ds, int t, const GrExpo
   x.reset(mark);
 }
 
-// Language-id features straight from the UTF-8 bytes: every code point position (a UTF-8 lead
+// Language-id record straight from the UTF-8 bytes: every code point position (a UTF-8 lead
 // byte, as decode() defines them) of the first kLidMaxCps code points, plus the virtual end
-// position, emits the 1..3-grams ending there (lid_grams_at); their embedding rows are summed
-// in exact fixed point. Neighbouring letters are found by stepping back to the previous lead
-// bytes, so no per-code-point arrays are needed: this runs as its own small kernel on the
-// device (k_langid_features) and inside the stage emulation on the host.
-TB_HD uint32_t lid_letter(const UcdView& ucd, const uint8_t* b, uint32_t n, int64_t s) {
-  if (s < 0) return 0;
-  const uint32_t c0 = b[s];
-  if (c0 < 0x80u) {  // ASCII: alphabetic = A-Z / a-z, lowercase = c | 0x20 (no table lookups)
-    const uint32_t l = c0 | 0x20u;
-    return (l >= 'a' && l <= 'z') ? l : 0u;
-  }
-  int len;
-  const uint32_t c = utf8_decode(b, (uint32_t)s, n, &len);
-  if (!(ucd.props(c) & P_ALPHA)) return 0;
-  const uint32_t l = ucd.lower(c);
-  return l ? l : c;
-}
-TB_HD int64_t prev_lead(const uint8_t* b, int64_t s) {
-  int64_t k = s - 1;
-  while (k >= 0 && !utf8_is_lead(b[k])) --k;
-  return k;
-}
-
+// position, emits the 1..4-grams ending there (lid_grams_at); their int16 logit rows are summed
+// exactly. Neighbouring letters are found by stepping back to the previous lead bytes, so no
+// per-code-point arrays are needed. The device runs its own kernel for this (k_langid_features,
+// same sums); this version runs inside the stage emulation on the host.
 template <class P>
-TB_HD void langid_features_bytes(DocCtx<P>& x, const uint8_t* b, uint32_t n, const uint16_t* emb,
-                                 uint16_t* vec, int32_t* cnt_out) {
+TB_HD void langid_record(DocCtx<P>& x, const uint8_t* b, uint32_t n, const LidTables& lt, int64_t* r) {
   const UcdView ucd = x.ucd;
   const auto mark = x.mark();
-  constexpr int D = kLidDim + 1;  // 32 embedding dims + the n-gram count
+  constexpr int D = kLidLangs + 1;  // 5 language sums + the n-gram count
   int32_t* tmp = x.template alloc_hot<int32_t>(64 * D);
   int64_t* sums = x.template alloc_hot<int64_t>(D);
   uint32_t* limb = x.template alloc_hot<uint32_t>(1);
@@ -1129,30 +1107,21 @@ TB_HD void langid_features_bytes(DocCtx<P>& x, const uint8_t* b, uint32_t n, con
   }
   const uint32_t lim = *limb;
   // A lane visits ceil((lim + 1) / 64) <= 257 byte positions (lim <= 4 * kLidMaxCps) with at most
-  // 3 grams each, and |fixed(e)| < 2^21 (|e| < 32, checked at model load): int32 partials
-  // cannot overflow.
+  // 4 grams each and |P| <= 2^15: int32 partials cannot overflow.
   x.par.template accum_rows<D>(
       lim + 1,
       [&](uint32_t s, int32_t* part) {
         if (s < lim && !utf8_is_lead(b[s])) return;
         const uint32_t l0 = s < lim ? lid_letter(ucd, b, n, s) : 0u;
         const int64_t p1 = prev_lead(b, s);
-        const uint32_t lm1 = lid_letter(ucd, b, n, p1);
-        const uint32_t lm2 = p1 >= 0 ? lid_letter(ucd, b, n, prev_lead(b, p1)) : 0u;
-        lid_grams_at(lm2, lm1, l0, true, true, [&](uint32_t bk) {
-          const uint16_t* row = emb + (size_t)bk * kLidDim;
-#pragma unroll
-          for (int d = 0; d < kLidDim; ++d) part[d] += lid_fixed(row[d]);
-          part[kLidDim] += 1;
-        });
+        const int64_t p2 = p1 >= 0 ? prev_lead(b, p1) : -1;
+        const int64_t p3 = p2 >= 0 ? prev_lead(b, p2) : -1;
+        part[kLidLangs] += lid_grams_at(lid_letter(ucd, b, n, p3), lid_letter(ucd, b, n, p2),
+                                        lid_letter(ucd, b, n, p1), l0,
+                                        [&](uint32_t g) { lid_add_row(lt.P, g, part); });
       },
       tmp, sums);
-  const int64_t K = sums[kLidDim];
-  x.par.for_n((uint32_t)kLidDim, [&](uint32_t d) {
-    float v = K ? (float)((double)sums[d] / (double)K / (double)kLidFixedScale) : 0.0f;
-    vec[d] = f32_to_bf16(v);
-  });
-  x.par.single([&]() { *cnt_out = (int32_t)K; });
+  x.par.single([&]() { lid_decide(sums, sums[kLidLangs], lt.bias, r); });
   x.par.sync();
   x.reset(mark);
 }
@@ -1469,7 +1438,7 @@ constexpr bool kHotProps = TB_HOT_PROPS != 0;
 
 template <class P, bool kWithLid = true>
 TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
-                         const uint16_t* lid_emb, const uint8_t* b, uint32_t n, StageOut& out) {
+                         const LidTables& lid, const uint8_t* b, uint32_t n, StageOut& out) {
   bool need_words = false, need_lines = false, need_ph = false, need_lid = false;
   for (int s = 0; s < st.n_steps; ++s) {
     const int k = st.steps[s].kind;
@@ -1613,9 +1582,9 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
       x.reset(mark);
       x.stamp(PH_FW);
     } else if (ds.kind == DK_LANGID) {
-      // on the device this runs as a separate kernel (k_langid_features): lid_emb == nullptr
+      // on the device this runs as a separate kernel (k_langid_features): lid.P == nullptr
       if constexpr (kWithLid)
-        if (lid_emb) langid_features_bytes(x, b, n, lid_emb, out.lid_vec + (size_t)out.doc * kLidDim, out.lid_cnt + out.doc);
+        if (lid.P) langid_record(x, b, n, lid, r);
       x.stamp(PH_LID);
     }
     if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }

@@ -179,17 +179,6 @@ struct SeqPar {
     }
     for (int d = 0; d < D; ++d) sums[d] = acc[d];
   }
-  // Sum of fixed-point embedding rows: out(d, sum_k fixed(E[rows[k]][d])) for d < D.
-  template <int D, class Row, class Out>
-  void gather_rows_fixed(uint32_t K, Row&& row_ptr, Out&& out) const {
-    int64_t acc[D];
-    for (int d = 0; d < D; ++d) acc[d] = 0;
-    for (uint32_t k = 0; k < K; ++k) {
-      const uint16_t* r = row_ptr(k);
-      for (int d = 0; d < D; ++d) acc[d] += lid_fixed(r[d]);
-    }
-    for (int d = 0; d < D; ++d) out(d, acc[d]);
-  }
 };
 
 #if defined(__HIPCC__)
@@ -527,15 +516,6 @@ struct WavePar {
       sums[d] = s;
     }
     __syncthreads();
-  }
-  template <int D, class Row, class Out>
-  __device__ __forceinline__ void gather_rows_fixed(uint32_t K, Row&& row_ptr, Out&& out) const {
-    static_assert(D == 32, "lane layout assumes 32 dims");
-    const int d = lane & 31, h = lane >> 5;
-    int64_t s = 0;
-    for (uint32_t k = h; k < K; k += 2) s += lid_fixed(row_ptr(k)[d]);
-    s += __shfl_xor(s, 32);
-    if (lane < 32) out(d, s);
   }
 
 };

@@ -6,11 +6,10 @@
 // works on it). Grid = number of documents, visited through a length-sorted permutation so the
 // longest documents start first (tail-latency balance under the power-law length distribution).
 //
-//  tb_stage_analyze : decode + UAX#29 words + lines + hashes -> Gopher/FineWeb records,
-//                     language-id n-gram doc vectors
-//  tb_c4_pass_a     : C4 line filtering, citation removal, rewritten text into scratch
-//  tb_c4_pass_b     : compaction of the rewritten texts into the next content version
-//  tb_langid_head   : bf16 MFMA (v_mfma_f32_16x16x32_bf16) linear head + softmax -> records
+//  tb_stage_analyze   : decode + UAX#29 words + lines + hashes -> Gopher/FineWeb records
+//  tb_langid_features : hashed 1..4-gram int16 logit rows summed per document -> language records
+//  tb_c4_pass_a       : C4 line filtering, citation removal, rewritten text into scratch
+//  tb_c4_pass_b       : compaction of the rewritten texts into the next content version
 #include <hip/hip_runtime.h>
 
 #include "../common/docproc.h"
@@ -101,16 +100,16 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
       const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes, \
       const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,        \
       const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, \
-      int64_t* rec, uint32_t* flags, const uint16_t* __restrict__ lid_emb, uint16_t* lid_vec, int32_t* lid_cnt, \
-      uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead) {                         \
+      int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof,                               \
+      const uint8_t* __restrict__ dead) {                                                             \
     const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;                                        \
     if (doc >= ndocs || (dead && dead[doc])) return;                                                  \
     DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);   \
     const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);                                           \
     lds_ascii_props(x);                                                                               \
     const uint8_t* b = lds_text(x, bytes + off[doc], n);                                              \
-    StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, lid_vec, lid_cnt};                              \
-    analyze_stage<WavePar, false>(x, *stage, *plan, lid_emb, b, n, out); /* LD: k_langid_features */  \
+    StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc};                                                \
+    analyze_stage<WavePar, false>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out); /* LD: own kernel */ \
   }
 
 TB_STAGE_KERNEL(k_stage_analyze, )
@@ -143,8 +142,8 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_stage_analyze_blk
     const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes,
     const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,
     const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
-    int64_t* rec, uint32_t* flags, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes, uint64_t* prof,
-    const uint8_t* __restrict__ dead, GrExport* gr_export, int32_t n_split, uint32_t split_bytes) {
+    int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead,
+    GrExport* gr_export, int32_t n_split, uint32_t split_bytes) {
   const int doc = perm[blockIdx.x];
   if (doc >= ndocs || (dead && dead[doc])) return;
   DocCtx<BlockPar<kBlockThreads>> x =
@@ -153,11 +152,11 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_stage_analyze_blk
   lds_ascii_props(x);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
-  StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, lid_vec, lid_cnt};
+  StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc};
   // split documents (the first n_split launch positions, longer than split_bytes) export their
   // word arrays; k_gr_dup_split finishes their duplicated n-gram orders
   if (gr_export && (int)blockIdx.x < n_split && n > split_bytes) out.gr_export = gr_export + blockIdx.x;
-  analyze_stage<BlockPar<kBlockThreads>, false>(x, *stage, *plan, nullptr, b, n, out);
+  analyze_stage<BlockPar<kBlockThreads>, false>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out);
 }
 
 // SURVEY 5.7 intra-document split: one workgroup per (split document, duplicated n-gram order).
@@ -193,21 +192,24 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_gr_dup_split(
   if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
 }
 
-// Language-id n-gram bag, one wave per document, with cooperative row gathers.
-// Same result as langid_features_bytes (docproc.h; the fixed-point sum is exact, so the order
-// of the terms does not matter), different memory schedule: there every lane gathered the
-// whole 64-byte embedding row of each of its grams with 4 dwordx4 loads, so one load
-// instruction touched 64 distinct cache lines and the kernel was bound by the per-line rate of
-// the vector memory pipeline. Here each lane first derives the (up to 3) bucket ids of its byte
-// position; then, for each gram slot, 4 lanes share one row: lane (4*src + q) loads 16 bytes
-// (dims 8q..8q+7) of the row of lane j*16+src's gram, so an instruction covers 16 whole rows
-// (16 lines instead of 64) and each lane keeps 8 accumulators instead of 33.
-// embx (optional): the embedding table pre-converted to the fixed-point sums' int32 values
-// (lid_fixed of every entry, 128-byte rows): a gather is two 16-byte loads and no conversions.
-__device__ __forceinline__ void langid_features_coop(DocCtx<WavePar>& x, const uint8_t* b, uint32_t n,
-                                                     const uint16_t* __restrict__ emb,
-                                                     const int32_t* __restrict__ embx, uint16_t* vec,
-                                                     int32_t* cnt_out) {
+// Language ID, one wave per document (csrc/common/langid.h): every lane takes one byte position
+// of a 64-byte chunk; a code point position emits the 1..4-grams ending there, and each gram
+// costs one 16-byte gather of its int16 logit row (the model's table is 1 MB: L2-resident). The
+// letters of the three previous code points come from the lanes holding their lead bytes
+// (pointer jumping with shuffles: lane -> its previous lead -> that lane's previous lead ...),
+// so a position decodes only its own code point; only the first lanes of a chunk look further
+// back in memory. Same exact integer sums as the host (langid_record / LangidModel::sums).
+__device__ __forceinline__ void lid_add_row16(const int16_t* __restrict__ P, uint32_t g, int32_t* acc) {
+  const uint4 w = *(const uint4*)(P + (size_t)g * kLidRow);
+  acc[0] += (int32_t)(int16_t)(w.x & 0xffffu);
+  acc[1] += (int32_t)w.x >> 16;
+  acc[2] += (int32_t)(int16_t)(w.y & 0xffffu);
+  acc[3] += (int32_t)w.y >> 16;
+  acc[4] += (int32_t)(int16_t)(w.z & 0xffffu);
+}
+
+__device__ __forceinline__ void langid_coop(DocCtx<WavePar>& x, const uint8_t* b, uint32_t n, const LidTables lt,
+                                            int64_t* r) {
   const UcdView ucd = x.ucd;
   const auto mark = x.mark();
   uint32_t* limb = x.template alloc_hot<uint32_t>(1);
@@ -221,96 +223,60 @@ __device__ __forceinline__ void langid_features_coop(DocCtx<WavePar>& x, const u
     x.par.sync();
   }
   const uint32_t lim = *limb;
-  const uint32_t lane = x.par.lane, q = lane & 3u, src = lane >> 2;
-  int64_t acc[8];
-#pragma unroll
-  for (int d = 0; d < 8; ++d) acc[d] = 0;
+  const int lane = (int)x.par.lane;
+  // a lane adds at most 4 rows (|P| <= 2^15) per chunk of <= 257 chunks: int32 cannot overflow
+  int32_t acc[kLidLangs] = {0, 0, 0, 0, 0};
   uint32_t cnt = 0;
   for (uint32_t base = 0; base <= lim; base += 64) {  // wave-uniform trip count
-    const uint32_t s = base + lane;
-    int32_t g[3] = {-1, -1, -1};
-    // Each lane decodes only its own code point; the letters of the two previous code points
-    // come from the lanes holding their lead bytes when those are in this chunk (all but the
-    // first few lanes), so a position costs one decode + property lookup instead of three.
+    const uint32_t s = base + (uint32_t)lane;
     const bool act = s <= lim && (s == lim || utf8_is_lead(b[s]));
     const uint32_t l0 = act && s < lim ? lid_letter(ucd, b, n, s) : 0u;
     const int64_t p1 = act ? prev_lead(b, s) : -1;
-    const int src1 = p1 >= (int64_t)base ? (int)(p1 - base) : (int)lane;
-    const uint32_t lm1_sh = (uint32_t)__shfl((int)l0, src1);
-    const int64_t p2_sh = pardetail::shfl_t(p1, src1);
-    const int src2 = p1 >= (int64_t)base && p2_sh >= (int64_t)base ? (int)(p2_sh - base) : (int)lane;
-    const uint32_t lm2_sh = (uint32_t)__shfl((int)l0, src2);
+    // previous positions inside this chunk come from their lanes (valid: a lead byte < lim is an
+    // active lane), earlier ones from memory
+    const bool in1 = p1 >= (int64_t)base;
+    const int64_t p2s = pardetail::shfl_t(p1, in1 ? (int)(p1 - (int64_t)base) : lane);
+    const uint32_t lm1s = (uint32_t)__shfl((int)l0, in1 ? (int)(p1 - (int64_t)base) : lane);
+    const bool in2 = in1 && p2s >= (int64_t)base;
+    const int64_t p3s = pardetail::shfl_t(p1, in2 ? (int)(p2s - (int64_t)base) : lane);
+    const uint32_t lm2s = (uint32_t)__shfl((int)l0, in2 ? (int)(p2s - (int64_t)base) : lane);
+    const bool in3 = in2 && p3s >= (int64_t)base;
+    const uint32_t lm3s = (uint32_t)__shfl((int)l0, in3 ? (int)(p3s - (int64_t)base) : lane);
     if (act) {
-      const uint32_t lm1 = p1 >= (int64_t)base ? lm1_sh : lid_letter(ucd, b, n, p1);
-      uint32_t lm2;
-      if (p1 < 0) lm2 = 0u;
-      else if (p1 >= (int64_t)base && p2_sh >= (int64_t)base) lm2 = lm2_sh;
-      else lm2 = lid_letter(ucd, b, n, p1 >= (int64_t)base ? p2_sh : prev_lead(b, p1));
-      int k = 0;
-      lid_grams_at(lm2, lm1, l0, true, true, [&](uint32_t bk) { g[k++] = (int32_t)bk; });
-      cnt += (uint32_t)k;
+      const uint32_t lm1 = in1 ? lm1s : lid_letter(ucd, b, n, p1);
+      const int64_t p2 = p1 < 0 ? -1 : (in1 ? p2s : prev_lead(b, p1));
+      const uint32_t lm2 = in2 ? lm2s : lid_letter(ucd, b, n, p2);
+      const int64_t p3 = p2 < 0 ? -1 : (in2 ? p3s : prev_lead(b, p2));
+      const uint32_t lm3 = in3 ? lm3s : lid_letter(ucd, b, n, p3);
+      cnt += (uint32_t)lid_grams_at(lm3, lm2, lm1, l0, [&](uint32_t g) { lid_add_row16(lt.P, g, acc); });
     }
-    // |fixed(e)| < 2^21 and a lane adds at most 12 rows per chunk: int32 partials cannot overflow
-    int32_t part[8];
-#pragma unroll
-    for (int d = 0; d < 8; ++d) part[d] = 0;
-#pragma unroll
-    for (int slot = 0; slot < 3; ++slot) {
-      if (__ballot(g[slot] >= 0) == 0) break;  // slots fill in order: later ones are empty too
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int32_t bk = __shfl(g[slot], j * 16 + (int)src);
-        if (bk >= 0 && embx) {
-          const int4* r = (const int4*)(embx + (size_t)bk * kLidDim + q * 8u);
-          const int4 a = r[0], c = r[1];
-          part[0] += a.x; part[1] += a.y; part[2] += a.z; part[3] += a.w;
-          part[4] += c.x; part[5] += c.y; part[6] += c.z; part[7] += c.w;
-        } else if (bk >= 0) {
-          const uint4 w = *(const uint4*)(emb + (size_t)bk * kLidDim + q * 8u);
-          const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            part[2 * h] += lid_fixed((uint16_t)(ws[h] & 0xffffu));
-            part[2 * h + 1] += lid_fixed((uint16_t)(ws[h] >> 16));
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int d = 0; d < 8; ++d) acc[d] += part[d];
   }
-  // lanes with the same q hold partial sums of the same 8 dims
+  int64_t sums[kLidLangs];
 #pragma unroll
-  for (int d = 0; d < 8; ++d)
-    for (int o = 4; o < 64; o <<= 1) acc[d] += pardetail::shfl_t(acc[d], (int)(lane ^ (uint32_t)o));
+  for (int l = 0; l < kLidLangs; ++l) {
+    int64_t v = acc[l];
+    for (int o = 1; o < 64; o <<= 1) v += pardetail::shfl_t(v, lane ^ o);
+    sums[l] = v;
+  }
   for (int o = 1; o < 64; o <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, o);
-  const int64_t K = cnt;
-  if (lane < 4) {
-#pragma unroll
-    for (int d = 0; d < 8; ++d) {
-      const float v = K ? (float)((double)acc[d] / (double)K / (double)kLidFixedScale) : 0.0f;
-      vec[q * 8u + d] = f32_to_bf16(v);
-    }
-  }
-  x.par.single([&]() { *cnt_out = (int32_t)K; });
+  if (x.par.leader()) lid_decide(sums, (int64_t)cnt, lt.bias, r);
   x.par.sync();
   x.reset(mark);
 }
 
-// Language-id n-gram bag of one document per wave (own kernel: it would otherwise set the
-// register budget, and so the occupancy, of the whole stage kernel).
+// Language ID of one document per wave (own kernel: it would otherwise set the register budget,
+// and so the occupancy, of the whole stage kernel). Writes the step's record (language, conf).
 __global__ __launch_bounds__(64) void k_langid_features(
     const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off, const int32_t* __restrict__ perm,
-    int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off, DevTables tabs,
-    const uint16_t* __restrict__ emb, const int32_t* __restrict__ embx, uint16_t* lid_vec, int32_t* lid_cnt,
-    uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
+    int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off, DevTables tabs, LidTables lt,
+    int64_t* rec, int32_t width, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
   const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
   if (doc >= ndocs) return;
   DocCtx<WavePar> x = make_ctx(tabs, nullptr, 0, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   x.stamp(PH_START);
-  langid_features_coop(x, b, n, emb, embx, lid_vec + (size_t)doc * kLidDim, lid_cnt + doc);
+  langid_coop(x, b, n, lt, rec + (int64_t)doc * width);
   // Documents with dictionary-segmented scripts go to the CPU path (the stage kernel's decode
   // flags them too). With the language-id gate in front of the stage (device.py plan_passes) the
   // stage kernel never sees a document this pass filters, so the flag is raised here as well:
@@ -437,62 +403,6 @@ __global__ __launch_bounds__(256) void k_c4_pass_b(const uint8_t* __restrict__ b
   for (int64_t i = threadIdx.x; i < len; i += blockDim.x) to[i] = from[i];
 }
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// One wave = 16 documents: logits[16 x 16] = X[16 x 32] . W[32 x 16] in one MFMA.
-// A lane layout: lane l holds X[row l&15][k 8(l>>4) .. +8]; B: W[k 8(l>>4)+j][col l&15] read from
-// the transposed weights wT[col][k]; D: col = l&15, row = 4(l>>4) + i.
-__global__ __launch_bounds__(64) void k_langid_head(const uint16_t* __restrict__ vec, const int32_t* __restrict__ cnt,
-                                                    const uint16_t* __restrict__ wT, const float* __restrict__ bias,
-                                                    int32_t ndocs, int64_t* rec, int64_t rec_off, int32_t width,
-                                                    float* dbg_logits) {
-  const int lane = threadIdx.x;
-  const int row0 = blockIdx.x * 16;
-  const int r = row0 + (lane & 15);
-  bf16x8 a;
-  if (r < ndocs) {
-    a = *reinterpret_cast<const bf16x8*>(vec + (size_t)r * kLidDim + 8 * (lane >> 4));
-  } else {
-    for (int j = 0; j < 8; ++j) a[j] = (__bf16)0.0f;
-  }
-  const bf16x8 bw = *reinterpret_cast<const bf16x8*>(wT + (size_t)(lane & 15) * kLidDim + 8 * (lane >> 4));
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw, acc, 0, 0, 0);
-  // Epilogue: the 16x16 logits tile goes through LDS; one lane per document then does the
-  // arg-max (ties -> lowest index, as the host) and the softmax in f64.
-  __shared__ float tile[16][17];
-  const int col = lane & 15;
-  const float bcol = bias[col];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) tile[4 * (lane >> 4) + i][col] = acc[i] + bcol;
-  __syncthreads();
-  if (lane < 16) {
-    const int row = row0 + lane;
-    if (row < ndocs) {
-      float v[kLidLangs];
-      int best = 0;
-#pragma unroll
-      for (int l = 0; l < kLidLangs; ++l) {
-        v[l] = tile[lane][l];
-        if (l > 0 && v[l] > v[best]) best = l;
-      }
-      if (dbg_logits)
-        for (int l = 0; l < 16; ++l) dbg_logits[(size_t)row * 16 + l] = tile[lane][l];
-      double den = 0.0;
-#pragma unroll
-      for (int l = 0; l < kLidLangs; ++l) den += exp((double)v[l] - (double)v[best]);
-      int64_t* rr = rec + rec_off + (int64_t)row * width;
-      if (cnt[row] == 0) {
-        rr[0] = -1;
-        rr[1] = 0;
-      } else {
-        rr[0] = best;
-        rr[1] = __double_as_longlong(1.0 / den);
-      }
-    }
-  }
-}
 
 // Step gate (csrc/common/gate.h): one thread per document. A live document that a step of the
 // just-finished pass filters (or that a kernel flagged for the CPU path) gets `code`: later
@@ -629,8 +539,7 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
                      const int64_t* off, const int32_t* perm, int32_t ndocs, char* scratch,
                      const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                      const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
-                     const uint16_t* lid_emb, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes,
-                     uint64_t* prof, int32_t waves, int32_t nblocks, const uint8_t* dead) {
+                     uint32_t lds_bytes, uint64_t* prof, int32_t waves, int32_t nblocks, const uint8_t* dead) {
   if (ndocs <= 0) return 0;
   if (nblocks <= 0) nblocks = ndocs;  // grid: docs perm[0 .. nblocks)
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
@@ -641,7 +550,7 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64), lds_bytes, stream, (const DevPlan*)plan,
                      (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, flags,
-                     lid_emb, lid_vec, lid_cnt, lds_bytes, prof, dead);
+                     lds_bytes, prof, dead);
   return (int)hipGetLastError();
 }
 
@@ -651,8 +560,8 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
                          const int64_t* off, const int32_t* perm, int32_t nblocks, int32_t ndocs, char* scratch,
                          const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                          const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
-                         uint16_t* lid_vec, int32_t* lid_cnt, uint32_t lds_bytes, uint64_t* prof,
-                         const uint8_t* dead, void* gr_export, int32_t n_split, uint32_t split_bytes) {
+                         uint32_t lds_bytes, uint64_t* prof, const uint8_t* dead, void* gr_export, int32_t n_split,
+                         uint32_t split_bytes) {
   if (nblocks <= 0) return 0;
   if (!perm || lds_bytes > kMaxLdsPerBlk || n_split < 0 || n_split > nblocks) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
@@ -661,7 +570,7 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
                               (int)lds_bytes);
   hipLaunchKernelGGL(k_stage_analyze_blk, dim3(nblocks), dim3(kBlockThreads), lds_bytes, stream,
                      (const DevPlan*)plan, (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw,
-                     pw_n, t, rec, flags, lid_vec, lid_cnt, lds_bytes, prof, dead, (GrExport*)gr_export, n_split,
+                     pw_n, t, rec, flags, lds_bytes, prof, dead, (GrExport*)gr_export, n_split,
                      split_bytes);
   return (int)hipGetLastError();
 }
@@ -724,17 +633,16 @@ int tb_badwords_match(hipStream_t stream, const uint8_t* bytes, const int64_t* o
 
 int tb_langid_features(hipStream_t stream, const uint8_t* bytes, const int64_t* off, const int32_t* perm,
                        int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint16_t* s1,
-                       const uint32_t* s2, const uint16_t* l1, const int32_t* l2, const uint16_t* emb,
-                       const int32_t* embx, uint16_t* lid_vec, int32_t* lid_cnt, uint32_t* flags, uint32_t lds_bytes,
-                       uint64_t* prof) {
+                       const uint32_t* s2, const uint16_t* l1, const int32_t* l2, const int16_t* P, const float* bias,
+                       int64_t* rec, int32_t width, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
   if (ndocs <= 0) return 0;
-  if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
+  if (lds_bytes > kMaxLdsPerDoc || !P || !bias || !rec || width < 2) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k_langid_features, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds_bytes);
   hipLaunchKernelGGL(k_langid_features, dim3(ndocs), dim3(64), lds_bytes, stream, bytes, off, perm, ndocs, scratch,
-                     scratch_off, t, emb, embx, lid_vec, lid_cnt, flags, lds_bytes, prof);
+                     scratch_off, t, LidTables{P, bias}, rec, width, flags, lds_bytes, prof);
   return (int)hipGetLastError();
 }
 
@@ -762,14 +670,6 @@ int tb_c4_pass_b(hipStream_t stream, const uint8_t* bytes, const int64_t* off, i
   return (int)hipGetLastError();
 }
 
-int tb_langid_head(hipStream_t stream, const uint16_t* vec, const int32_t* cnt, const uint16_t* wT,
-                   const float* bias, int32_t ndocs, int64_t* rec, int64_t rec_off, int32_t width,
-                   float* dbg_logits) {
-  if (ndocs <= 0) return 0;
-  hipLaunchKernelGGL(k_langid_head, dim3((ndocs + 15) / 16), dim3(64), 0, stream, vec, cnt, wT, bias, ndocs, rec,
-                     rec_off, width, dbg_logits);
-  return (int)hipGetLastError();
-}
 
 int tb_gate(hipStream_t stream, const void* gate, const int64_t* const* recs, int32_t nrecs, int32_t ndocs,
             const uint32_t* flags, uint8_t* dead, int32_t code) {
@@ -822,7 +722,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 
 int tb_phase_slots() { return kPhaseSlots; }
 
-int tb_abi_version() { return 8; }
+int tb_abi_version() { return 9; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

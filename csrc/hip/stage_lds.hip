@@ -151,8 +151,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       x.par.sync();
       x.asc = asc;
     }
-    StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc, nullptr, nullptr};
-    analyze_stage<WavePar, false>(x, *stage, *plan, nullptr, b, n, out);
+    StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc};
+    analyze_stage<WavePar, false>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out);
     x.par.sync();
   }
 }

@@ -310,24 +310,6 @@ std::vector<uint64_t> pow_table(uint32_t n) {
 
 uint64_t scratch_bytes_for(uint32_t doc_len) { return scratch_bytes_for_dev(doc_len); }
 
-// Head of the language model on one doc vector (host arithmetic; the device uses MFMA).
-static void lid_head_host(const LangidModel& m, const uint16_t* v, int32_t cnt, int64_t* r) {
-  if (cnt == 0) { r[0] = -1; r[1] = 0; return; }
-  float logits[kLidLangs];
-  for (int l = 0; l < kLidLangs; ++l) {
-    float s = 0.f;
-    for (int d = 0; d < kLidDim; ++d) s += bf16_to_f32(v[d]) * bf16_to_f32(m.w[d * kLidLangsPad + l]);
-    logits[l] = s + m.b[l];
-  }
-  int best = 0;
-  for (int l = 1; l < kLidLangs; ++l) if (logits[l] > logits[best]) best = l;
-  double den = 0;
-  for (int l = 0; l < kLidLangs; ++l) den += std::exp((double)logits[l] - (double)logits[best]);
-  double conf = 1.0 / den;
-  r[0] = best;
-  std::memcpy(&r[1], &conf, sizeof(double));
-}
-
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
                    std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes, const uint8_t* dead,
@@ -340,8 +322,6 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
   if (has_lid && !lid) { delete plan; throw std::runtime_error("language model required"); }
   rec.assign((size_t)st.width_total * ndocs, 0);
   flags.assign(ndocs, 0);
-  std::vector<uint16_t> lvec(has_lid ? (size_t)ndocs * kLidDim : 1);
-  std::vector<int32_t> lcnt(has_lid ? ndocs : 1);
   uint32_t maxlen = 0;
   for (int64_t i = 0; i < ndocs; ++i) maxlen = std::max<uint32_t>(maxlen, (uint32_t)(off[i + 1] - off[i]));
   std::vector<uint64_t> pw = pow_table(maxlen + 16);
@@ -365,14 +345,8 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
       x.lcap = lds_bytes;
       x.flag = &flags[i];
       x.weak_keys = weak_keys;
-      StageOut out{rec.data(), (uint32_t)ndocs, (uint32_t)i, lvec.data(), lcnt.data()};
-      analyze_stage(x, st, *plan, lid ? lid->emb.data() : nullptr, (const uint8_t*)data + off[i], n, out);
-      if (has_lid) {
-        for (int s = 0; s < st.n_steps; ++s)
-          if (st.steps[s].kind == DK_LANGID)
-            lid_head_host(*lid, &lvec[(size_t)i * kLidDim], lcnt[i],
-                          rec.data() + (int64_t)st.steps[s].rec_prefix * ndocs + i * st.steps[s].width);
-      }
+      StageOut out{rec.data(), (uint32_t)ndocs, (uint32_t)i};
+      analyze_stage(x, st, *plan, lid ? lid->tables() : LidTables{nullptr, nullptr}, (const uint8_t*)data + off[i], n, out);
     }
   });
   delete plan;
@@ -401,8 +375,6 @@ void emulate_stage_lds(const std::vector<StepCfg>& steps, const std::vector<int>
   rec.assign((size_t)st.width_total * ndocs, 0);
   flags.assign(ndocs, 0);
   retried.assign(ndocs, 0);
-  std::vector<uint16_t> lvec(has_lid ? (size_t)ndocs * kLidDim : 1);
-  std::vector<int32_t> lcnt(has_lid ? ndocs : 1);
   uint32_t maxlen = 0;
   for (int64_t i = 0; i < ndocs; ++i) maxlen = std::max<uint32_t>(maxlen, (uint32_t)(off[i + 1] - off[i]));
   std::vector<uint64_t> pw = pow_table(maxlen + 16);
@@ -429,8 +401,8 @@ void emulate_stage_lds(const std::vector<StepCfg>& steps, const std::vector<int>
         x.lds = lds.data();
         x.lcap = kGenericLds;
         x.flag = &flags[i];
-        StageOut out{rec.data(), (uint32_t)ndocs, (uint32_t)i, lvec.data(), lcnt.data()};
-        analyze_stage(x, stage, *plan, lid ? lid->emb.data() : nullptr, src, n, out);
+        StageOut out{rec.data(), (uint32_t)ndocs, (uint32_t)i};
+        analyze_stage(x, stage, *plan, lid ? lid->tables() : LidTables{nullptr, nullptr}, src, n, out);
       };
       bool done = false;
       if (slice && slice[i]) {
@@ -456,12 +428,6 @@ void emulate_stage_lds(const std::vector<StepCfg>& steps, const std::vector<int>
         generic(st);
       } else if (has_lid) {
         generic(st_lid);
-      }
-      if (has_lid) {
-        for (int s = 0; s < st.n_steps; ++s)
-          if (st.steps[s].kind == DK_LANGID)
-            lid_head_host(*lid, &lvec[(size_t)i * kLidDim], lcnt[i],
-                          rec.data() + (int64_t)st.steps[s].rec_prefix * ndocs + i * st.steps[s].width);
       }
     }
   });

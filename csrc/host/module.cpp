@@ -469,14 +469,11 @@ PYBIND11_MODULE(_tbhost, m) {
 
   // ---- language id (CPU) ----
   py::class_<LangidModel, std::shared_ptr<LangidModel>>(m, "LangidModel")
-      .def(py::init([](py::array_t<uint16_t, py::array::c_style> emb, py::array_t<uint16_t, py::array::c_style> w,
-                       py::array_t<float, py::array::c_style> b) {
+      .def(py::init([](py::array_t<int16_t, py::array::c_style> P, py::array_t<float, py::array::c_style> b) {
         auto mdl = std::make_shared<LangidModel>();
-        if ((size_t)emb.size() != (size_t)kLidBuckets * kLidDim) throw std::invalid_argument("emb shape");
-        if ((size_t)w.size() != (size_t)kLidDim * kLidLangsPad) throw std::invalid_argument("w shape");
-        if ((size_t)b.size() != (size_t)kLidLangsPad) throw std::invalid_argument("b shape");
-        mdl->emb.assign(emb.data(), emb.data() + emb.size());
-        mdl->w.assign(w.data(), w.data() + w.size());
+        if ((size_t)P.size() != (size_t)kLidBuckets * kLidRow) throw std::invalid_argument("P shape");
+        if ((size_t)b.size() != (size_t)kLidRow) throw std::invalid_argument("b shape");
+        mdl->P.assign(P.data(), P.data() + P.size());
         mdl->b.assign(b.data(), b.data() + b.size());
         return mdl;
       }))
@@ -485,9 +482,9 @@ PYBIND11_MODULE(_tbhost, m) {
         int l = mdl.detect(s, &conf);
         return py::make_tuple(l, conf);
       })
-      .def("featurize", [](const LangidModel& mdl, const std::string& s) {
-        std::vector<uint16_t> v(kLidDim, 0);
-        int c = mdl.featurize(s, v.data());
+      .def("sums", [](const LangidModel& mdl, const std::string& s) {
+        std::vector<int64_t> v(kLidLangs, 0);
+        const int64_t c = mdl.sums(s, v.data());
         return py::make_tuple(c, v);
       });
   m.def("langid_buckets", [](const std::string& s) {
@@ -496,25 +493,26 @@ PYBIND11_MODULE(_tbhost, m) {
     const uint8_t* b = (const uint8_t*)s.data();
     const uint32_t n = (uint32_t)s.size();
     const UcdView& u = host_ucd();
-    uint32_t lm2 = 0, lm1 = 0;
+    uint32_t lm3 = 0, lm2 = 0, lm1 = 0;
     int ncp = 0;
     auto emit = [&](uint32_t k) { out.push_back(k); };
     for (uint32_t i = 0; i < n && ncp < kLidMaxCps; ++ncp) {
+      const uint32_t l0 = lid_letter(u, b, n, i);
       int len;
-      uint32_t c = utf8_decode(b, i, n, &len);
+      (void)utf8_decode(b, i, n, &len);
       i += len;
-      uint32_t l0 = (u.props(c) & P_ALPHA) ? u.lower(c) : 0;
-      if (l0 == 0 && (u.props(c) & P_ALPHA)) l0 = c;
-      lid_grams_at(lm2, lm1, l0, true, true, emit);
+      lid_grams_at(lm3, lm2, lm1, l0, emit);
+      lm3 = lm2;
       lm2 = lm1;
       lm1 = l0;
     }
-    lid_grams_at(lm2, lm1, 0, true, true, emit);
+    lid_grams_at(lm3, lm2, lm1, 0, emit);
     return out;
   });
-  m.attr("LID_DIM") = kLidDim;
+  m.attr("LID_ROW") = kLidRow;
+  m.attr("LID_LANGS") = kLidLangs;
   m.attr("LID_BUCKETS") = kLidBuckets;
-  m.attr("LID_LANGS_PAD") = kLidLangsPad;
+  m.attr("LID_SCALE") = kLidScale;
 
   py::class_<StdRng>(m, "StdRng")
       .def(py::init<uint64_t>())

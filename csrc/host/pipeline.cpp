@@ -114,54 +114,42 @@ void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t, int
 
 // ------------------------------------------------------------------------------------------
 // Language identification (CPU inference with the same arithmetic as the device path).
-int LangidModel::featurize(std::string_view text, uint16_t* out_vec) const {
-  const uint8_t* b = (const uint8_t*)text.data();
+int64_t LangidModel::sums(std::string_view text, int64_t* out) const {
+  const uint8_t* b8 = (const uint8_t*)text.data();
   const uint32_t n = (uint32_t)text.size();
   const UcdView& u = host_ucd();
-  int64_t acc[kLidDim] = {0};
+  int32_t part[kLidLangs] = {0};
+  for (int l = 0; l < kLidLangs; ++l) out[l] = 0;
   int64_t cnt = 0;
-  uint32_t lm2 = 0, lm1 = 0;
+  uint32_t lm3 = 0, lm2 = 0, lm1 = 0;
   int ncp = 0;
-  auto emit = [&](uint32_t bucket) {
-    const uint16_t* row = &emb[(size_t)bucket * kLidDim];
-    for (int d = 0; d < kLidDim; ++d) acc[d] += lid_fixed(row[d]);
+  auto emit = [&](uint32_t g) {
+    lid_add_row(P.data(), g, part);
+    for (int l = 0; l < kLidLangs; ++l) { out[l] += part[l]; part[l] = 0; }
   };
   uint32_t i = 0;
   for (; i < n && ncp < kLidMaxCps; ++ncp) {
+    const uint32_t l0 = lid_letter(u, b8, n, i);
     int len;
-    uint32_t c = utf8_decode(b, i, n, &len);
+    (void)utf8_decode(b8, i, n, &len);
     i += len;
-    uint32_t l0 = (u.props(c) & P_ALPHA) ? u.lower(c) : 0;
-    if (l0 == 0 && (u.props(c) & P_ALPHA)) l0 = c;  // paranoia: a letter never maps to 0
-    cnt += lid_grams_at(lm2, lm1, l0, true, true, emit);
+    cnt += lid_grams_at(lm3, lm2, lm1, l0, emit);
+    lm3 = lm2;
     lm2 = lm1;
     lm1 = l0;
   }
   // virtual non-letter at the cut / end of text
-  cnt += lid_grams_at(lm2, lm1, 0, true, true, emit);
-  if (cnt == 0) return 0;
-  for (int d = 0; d < kLidDim; ++d) {
-    float v = (float)((double)acc[d] / (double)cnt / (double)kLidFixedScale);
-    out_vec[d] = f32_to_bf16(v);
-  }
-  return (int)std::min<int64_t>(cnt, INT32_MAX);
+  cnt += lid_grams_at(lm3, lm2, lm1, 0, emit);
+  return cnt;
 }
 
 int LangidModel::detect(std::string_view text, double* conf) const {
-  uint16_t v[kLidDim];
-  if (featurize(text, v) == 0) return -1;
-  float logits[kLidLangs];
-  for (int l = 0; l < kLidLangs; ++l) {
-    float s = 0.f;
-    for (int d = 0; d < kLidDim; ++d) s += bf16_to_f32(v[d]) * bf16_to_f32(w[d * kLidLangsPad + l]);
-    logits[l] = s + b[l];
-  }
-  int best = 0;
-  for (int l = 1; l < kLidLangs; ++l) if (logits[l] > logits[best]) best = l;
-  double den = 0;
-  for (int l = 0; l < kLidLangs; ++l) den += std::exp((double)logits[l] - (double)logits[best]);
-  *conf = 1.0 / den;
-  return best;
+  int64_t s[kLidLangs];
+  const int64_t cnt = sums(text, s);
+  int64_t r[2];
+  lid_decide(s, cnt, b.data(), r);
+  std::memcpy(conf, &r[1], sizeof(double));
+  return (int)r[0];
 }
 
 // ------------------------------------------------------------------------------------------

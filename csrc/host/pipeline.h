@@ -15,6 +15,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "../common/langid.h"
 #include "filters.h"
 #include "json.h"
 
@@ -26,13 +27,13 @@ void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t, int
 void parallel_tasks(int64_t ntasks, int nthreads, const std::function<void(int64_t)>& fn);
 
 struct LangidModel {
-  std::vector<uint16_t> emb;   // [kLidBuckets * kLidDim] bf16
-  std::vector<uint16_t> w;     // [kLidDim * kLidLangsPad] bf16
-  std::vector<float> b;        // [kLidLangsPad]
+  std::vector<int16_t> P;  // [kLidBuckets * kLidRow] fixed-point logit rows (csrc/common/langid.h)
+  std::vector<float> b;    // [kLidRow]
   // Detect the language of `text`: returns lang index or -1, confidence in *conf.
   int detect(std::string_view text, double* conf) const;
-  // Doc vector (bf16 bits) + n-gram count (for tests / training).
-  int featurize(std::string_view text, uint16_t* out_vec) const;
+  // Exact per-language sums of the text's n-gram rows (out[kLidLangs]); returns the n-gram count.
+  int64_t sums(std::string_view text, int64_t* out) const;
+  LidTables tables() const { return LidTables{P.data(), b.data()}; }
 };
 
 // C4 bad-words matcher for one language (reference c4_filters.rs:298-551).

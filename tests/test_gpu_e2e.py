@@ -150,7 +150,7 @@ def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
     assert a.reasons.keys() == b.reasons.keys()
     for k, ra in a.reasons.items():
         rb = b.reasons[k]
-        if ra != rb:  # the language confidence in the message: bf16 MFMA head vs fp32 host head
+        if ra != rb:  # the language confidence in the message (f64 exp on the device vs the host)
             pa, pb = ra.split(": ", 1), rb.split(": ", 1)
             assert pa[0] == pb[0] == "Language detection confidence is not satified", (ra, rb)
             assert abs(float(pa[1].split()[0]) - float(pb[1].split()[0])) < 1e-5, (ra, rb)

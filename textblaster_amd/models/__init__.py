@@ -1,2 +1,2 @@
-"""Model families used by the pipeline: the language identifier (fastText-style char n-gram
-embedding bag + bf16 MFMA linear head) and the TokenCounter tokenizer wrapper."""
+"""Model families used by the pipeline: the language identifier (hashed character 1-4-gram
+int16 logit table, csrc/common/langid.h) and the TokenCounter tokenizer wrapper."""

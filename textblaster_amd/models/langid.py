@@ -1,10 +1,12 @@
 """Language identification model (stands in for lingua; reference language_filter.rs:35-93).
 
-Architecture (fastText-style, survey H5): hashed character 1..3-grams of lowercased letter runs
--> mean of bf16 embedding rows E[65536, 32] (exact fixed-point sum) -> bf16 doc vector ->
-logits = doc . W[32, 5(+pad 16)] + b -> softmax over {English, Danish, Swedish, Nynorsk, Bokmal}.
-On the device the featurizer runs in the document kernel and the head is one
-``v_mfma_f32_16x16x32_bf16`` per 16 documents; the CPU path uses the same arithmetic.
+Architecture (csrc/common/langid.h): hashed character 1..4-grams of lowercased letter runs ->
+per bucket an int16 row of fixed-point logit contributions to {English, Danish, Swedish,
+Nynorsk, Bokmal} (P[65536, 8], 5 used, scale 1/1024) -> logits = sum of the document's rows /
+#grams / 1024 + b -> softmax; the confidence is the top probability. The sums are exact integers,
+so the device kernel (k_langid_features: one 16-byte gather per n-gram) and the CPU path agree
+bit for bit. This is a fastText-style mean-of-embeddings model with its linear head folded into
+the table ((mean E) W = mean (E W)); tools/train_langid.py trains the folded table directly.
 
 Weights are produced offline by ``tools/train_langid.py`` from the text in
 ``models/data/langid_corpus`` and stored as a plain ``.npz`` (loaded with allow_pickle=False).
@@ -20,21 +22,20 @@ import numpy as np
 from .. import native
 
 DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
-DEFAULT_WEIGHTS = os.path.join(DATA_DIR, "langid_v1.npz")
+DEFAULT_WEIGHTS = os.path.join(DATA_DIR, "langid_v2.npz")
 LANGS = ("eng", "dan", "swe", "nno", "nob")
 NAMES = ("English", "Danish", "Swedish", "Nynorsk", "Bokmal")
 
 
 @dataclasses.dataclass
 class LangidWeights:
-    emb: np.ndarray  # uint16 bf16 bits [BUCKETS * DIM]
-    w: np.ndarray    # uint16 bf16 bits [DIM * PAD]
-    b: np.ndarray    # float32 [PAD]
+    P: np.ndarray  # int16 [BUCKETS * ROW] fixed-point logit rows
+    b: np.ndarray  # float32 [ROW]
     _native: Optional[object] = None
 
     def native(self):
         if self._native is None:
-            self._native = native.host().LangidModel(self.emb, self.w, self.b)
+            self._native = native.host().LangidModel(self.P, self.b)
         return self._native
 
     def detect(self, text: str):
@@ -45,18 +46,16 @@ class LangidWeights:
 
 def load(path: str) -> LangidWeights:
     with np.load(path, allow_pickle=False) as z:
-        emb = np.ascontiguousarray(z["emb"], dtype=np.uint16).reshape(-1)
-        w = np.ascontiguousarray(z["w"], dtype=np.uint16).reshape(-1)
+        if "P" not in z.files or "b" not in z.files:
+            raise ValueError(f"language model {path} is not a hashed n-gram logit table (keys P, b)")
+        P = np.ascontiguousarray(z["P"], dtype=np.int16).reshape(-1)
         b = np.ascontiguousarray(z["b"], dtype=np.float32).reshape(-1)
     h = native.host()
-    if emb.size != h.LID_BUCKETS * h.LID_DIM or w.size != h.LID_DIM * h.LID_LANGS_PAD or b.size != h.LID_LANGS_PAD:
+    if P.size != h.LID_BUCKETS * h.LID_ROW or b.size != h.LID_ROW:
         raise ValueError(f"language model {path} has the wrong shape")
-    # the device accumulates n-gram rows in int32 fixed point per lane (docproc.h
-    # langid_features_bytes): |e| < 32 keeps every partial sum below 2^31
-    emax = float(np.abs((emb.astype(np.uint32) << 16).view(np.float32)).max()) if emb.size else 0.0
-    if not emax < 32.0:
-        raise ValueError(f"language model {path}: embedding magnitude {emax} out of range (< 32)")
-    return LangidWeights(emb, w, b)
+    if np.any(P.reshape(-1, h.LID_ROW)[:, h.LID_LANGS:] != 0):
+        raise ValueError(f"language model {path}: padding columns must be zero")
+    return LangidWeights(P, b)
 
 
 _default: Optional[LangidWeights] = None

@@ -22,13 +22,12 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _SIGS = {
-    "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32,
-                         _P],
+    "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32, _P],
     "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _P],
-    "tb_stage_analyze_blk": [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P,
+    "tb_stage_analyze_blk": [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P,
                              _U32, _P, _P, _P, _I32, _U32],
     "tb_gr_dup_split": [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32],
     "tb_sizeof_gr_export": [],
@@ -40,9 +39,8 @@ _SIGS = {
     "tb_block_threads": [],
     "tb_badwords_match": [_P, _P, _P, _I32, _P, _P, _I32, _I32, _P, _U32, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                           _U32],
-    "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P],
+    "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _U32, _P],
     "tb_c4_pass_b": [_P, _P, _P, _I32, _P, _P, _P, _P, _P],
-    "tb_langid_head": [_P, _P, _P, _P, _P, _I32, _P, _I64, _I32, _P],
     "tb_pow_table": [_P, _P, _U32],
     "tb_html_sizes": [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _P, _U32, _P],
     "tb_html_scatter": [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _P, _U32, _P, _P],
@@ -157,13 +155,13 @@ class Kernels:
         return self._pw, self._pw_n
 
     def stage_analyze(self, plan, stage, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, flags,
-                      lid_emb=None, lid_vec=None, lid_cnt=None, lds_bytes=0, prof=None, waves=0, nblocks=0, dead=None):
+                      lds_bytes=0, prof=None, waves=0, nblocks=0, dead=None):
         t = self.tabs
         rc = self.lib.tb_stage_analyze(
             self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs,
             scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
-            t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), _ptr(lid_emb), _ptr(lid_vec),
-            _ptr(lid_cnt), lds_bytes, _ptr(prof), waves, nblocks, _ptr(dead))
+            t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof), waves, nblocks,
+            _ptr(dead))
         _check(rc, "tb_stage_analyze")
 
     def stage_lds(self, plan, stage, bytes_, off, perm, pos0, nblocks, ndocs, rec, flags, lds_bytes, retry_cnt,
@@ -196,8 +194,7 @@ class Kernels:
         _check(rc, "tb_stage_retry")
 
     def stage_analyze_blk(self, plan, stage, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n,
-                          rec, flags, lid_vec=None, lid_cnt=None, lds_bytes=0, prof=None, dead=None,
-                          gr_export=None, n_split=0, split_bytes=0):
+                          rec, flags, lds_bytes=0, prof=None, dead=None, gr_export=None, n_split=0, split_bytes=0):
         """k_stage_analyze_blk; ``gr_export`` (zeroed, >= n_split descriptors): the first n_split
         launch positions longer than ``split_bytes`` export their word arrays (split mode)."""
         t = self.tabs
@@ -208,9 +205,8 @@ class Kernels:
         rc = self.lib.tb_stage_analyze_blk(
             self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), perm_long.data_ptr(),
             nlong, ndocs, scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(),
-            t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), _ptr(lid_vec),
-            _ptr(lid_cnt), lds_bytes, _ptr(prof), _ptr(dead), _ptr(gr_export), n_split if gr_export is not None else 0,
-            split_bytes)
+            t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof),
+            _ptr(dead), _ptr(gr_export), n_split if gr_export is not None else 0, split_bytes)
         _check(rc, "tb_stage_analyze_blk")
 
     def gr_dup_split(self, stage, gr_step, perm, n_split, n_dup, ndocs, gr_export, pw, pw_n, rec, flags, lds_bytes):
@@ -261,16 +257,21 @@ class Kernels:
                 int(seg_bytes))
             _check(rc, "tb_badwords_match")
 
-    def langid_features(self, bytes_, off, perm, ndocs, scratch, scratch_off, emb, vec, cnt, flags, lds_bytes=0,
-                        prof=None, embx=None):
-        """k_langid_features; ``embx``: optional int32 fixed-point copy of ``emb`` (same shape)."""
+    def langid_features(self, bytes_, off, perm, ndocs, scratch, scratch_off, P, bias, rec, width, flags, lds_bytes=0,
+                        prof=None):
+        """k_langid_features: the language record (language, confidence bits) of every document into
+        ``rec`` (document d at rec[d * width]); ``P``: int16 [buckets * 8] logit rows, ``bias``:
+        float32 [8] (csrc/common/langid.h)."""
+        from .. import native
+
+        h = native.host()
         t = self.tabs
-        if embx is not None and embx.numel() != emb.numel():
-            raise DeviceError("langid_features: fixed-point table shape")
+        if P.numel() != h.LID_BUCKETS * h.LID_ROW or bias.numel() != h.LID_ROW or width < 2 or rec.numel() < ndocs * width:
+            raise DeviceError("langid_features: operand shapes")
         rc = self.lib.tb_langid_features(
             self.stream(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs, scratch.data_ptr(),
-            scratch_off.data_ptr(), t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), emb.data_ptr(),
-            _ptr(embx), vec.data_ptr(), cnt.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof))
+            scratch_off.data_ptr(), t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), P.data_ptr(),
+            bias.data_ptr(), rec.data_ptr(), width, flags.data_ptr(), lds_bytes, _ptr(prof))
         _check(rc, "tb_langid_features")
 
     def c4_pass_a(self, c4, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags, lds_bytes=0,
@@ -302,11 +303,6 @@ class Kernels:
         rc = self.lib.tb_gate(self.stream(), gate.data_ptr(), ctypes.cast(arr, ctypes.c_void_p), len(recs), ndocs,
                               flags.data_ptr(), dead.data_ptr(), code)
         _check(rc, "tb_gate")
-
-    def langid_head(self, vec, cnt, wT, bias, ndocs, rec, rec_off, width, dbg_logits=None):
-        rc = self.lib.tb_langid_head(self.stream(), vec.data_ptr(), cnt.data_ptr(), wT.data_ptr(), bias.data_ptr(),
-                                     ndocs, rec.data_ptr(), rec_off, width, _ptr(dbg_logits))
-        _check(rc, "tb_langid_head")
 
     def bpe_tables(self, spec) -> BpeTables:
         from .. import native

@@ -347,7 +347,7 @@ def plan_passes(plan: ExecPlan, stage_layout, steps_native, gating: bool, lid_ga
     records for.
 
     With gating, a stage that holds the language-id step next to other steps is preceded by a
-    ("lid", s) pass: the language-id bag and MFMA head run first, their gate marks the documents
+    ("lid", s) pass: the language-id kernel runs first, its gate marks the documents
     the language filter drops, and the stage kernels skip them (the reference never runs the
     later filters on those documents: executor.rs:30-57). TB_LID_GATE=0 keeps one pass."""
     h = native.host()
@@ -525,20 +525,13 @@ class DeviceRunner:
             self.c4_ts = {i: self._to_dev(h.build_c4(steps_native[i])) for i in plan.c4_steps}
             self.has_lid = any(steps_native[i].kind == h.StepKind.LanguageDetection
                                for st in plan.stages for i in st)
-            self.lid_embx = None
+            self.lid_P = self.lid_b = None
             if self.has_lid:
                 if langid is None:
                     raise DeviceError("LanguageDetectionFilter needs a language-id model")
-                self.lid_emb = hiprt.to_device(langid.emb)
-                # the same table as the bag's int32 fixed-point terms (lid_fixed: rint(e * 2^16),
-                # exact in float32), so the gathers need no conversion; TB_LID_FIXED=0: bf16 path
-                self.lid_embx = None
-                if os.environ.get("TB_LID_FIXED", "1") not in ("", "0"):
-                    e = (np.ascontiguousarray(langid.emb, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
-                    self.lid_embx = hiprt.to_device(np.rint(e * np.float32(65536.0)).astype(np.int32))
-                wT = np.ascontiguousarray(langid.w.reshape(h.LID_DIM, h.LID_LANGS_PAD).T)  # [16][32]
-                self.lid_wT = hiprt.to_device(wT)
-                self.lid_b = hiprt.to_device(langid.b.astype(np.float32))
+                # int16 logit rows of the hashed n-grams (1 MB, L2-resident) and the bias
+                self.lid_P = hiprt.to_device(np.ascontiguousarray(langid.P, dtype=np.int16))
+                self.lid_b = hiprt.to_device(np.ascontiguousarray(langid.b, dtype=np.float32))
             self.c4_growth = int(h.C4_MAX_GROWTH)
             # TB_GATE=0 disables step gating (every pass runs over every document)
             self.gating = os.environ.get("TB_GATE", "1") not in ("", "0")
@@ -630,7 +623,6 @@ class DeviceRunner:
         self.phase_docs: Dict[str, int] = {}
         self.copy_threads = int(os.environ.get("TB_COPY_THREADS", "8"))
         self._next_slot = 0
-        self._last_lid = None
         self._bw_table = None  # (gen, device copy) of the hashed bad-words trie table
         self._bw_fold = None
 
@@ -848,29 +840,22 @@ class DeviceRunner:
                     continue
                 width_total, layout = self.stage_layout[s]
                 rec = rt.zeros(width_total * ndocs, np.int64)
-                lid_vec = lid_cnt = None
-                if any(kind == 4 for kind, _, _ in layout):
-                    lid_vec = rt.zeros(ndocs * h.LID_DIM, np.int16)
-                    lid_cnt = rt.zeros(ndocs, np.int32)
-                    keep += [lid_vec, lid_cnt]   # freed (returned to the cache) only after the batch
-                ev_pre = self._record(main)  # rec / lid buffers zeroed
+                lid_at = [(width, prefix) for kind, width, prefix in layout if kind == KIND_LANGID]
+                ev_pre = self._record(main)  # rec zeroed
                 keep.append(ev_pre)
                 ev_lid = ev_blk = None
                 prof = self._prof_buf(ndocs, keep, f"stage{s}")
                 lid_pass = ("lid", s) in self.passes
                 if lid_pass:
-                    # language-id pass first (bag -> MFMA head -> gate on the side stream); the
-                    # stage kernels below skip the documents it filters
+                    # language-id pass first (records + gate on the side stream); the stage kernels
+                    # below skip the documents it filters
                     slot.s_lid.wait_event(ev_pre)
                     with rt.stream(slot.s_lid):
                         with self._ktimed(keep, "langid_features"):
-                            self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec,
-                                                   lid_cnt, flags, self.lds_bytes_lid,
-                                                   self._prof_buf(ndocs, keep, f"langid{s}"), self.lid_embx)
-                        for kind, width, prefix in layout:
-                            if kind == KIND_LANGID:
-                                self.k.langid_head(lid_vec, lid_cnt, self.lid_wT, self.lid_b, ndocs, rec, prefix * ndocs,
-                                                   width)
+                            for width, prefix in lid_at:
+                                self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_P, self.lid_b,
+                                                       rec[prefix * ndocs:], width, flags, self.lds_bytes_lid,
+                                                       self._prof_buf(ndocs, keep, f"langid{s}"))
                         if pass_idx in self.gate_ts:
                             self.k.gate(self.gate_ts[pass_idx], [rec], ndocs, flags, dead, pass_idx + 1, 0,
                                         self.gate_need[pass_idx])
@@ -894,7 +879,7 @@ class DeviceRunner:
                             keep.append(gx)
                     with rt.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_blk"):
                         self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[:n_long], n_long,
-                                                 ndocs, scratch, d_soff, pw, pw_n, rec, flags, lid_vec, lid_cnt,
+                                                 ndocs, scratch, d_soff, pw, pw_n, rec, flags,
                                                  self.lds_bytes_blk, prof, skip, gx, n_split, self.split_doc_bytes)
                         if n_split:
                             gr_pos, n_dup = self.gr_split[s]
@@ -902,12 +887,14 @@ class DeviceRunner:
                                                 gx, pw, pw_n, rec, flags, self.lds_bytes_blk)
                         ev_blk = self._record(slot.s_blk)
                         keep.append(ev_blk)
-                if lid_vec is not None and not lid_pass:
+                if lid_at and not lid_pass:
+                    # language ID next to the stage kernels: it writes only its own record columns
                     slot.s_lid.wait_event(ev_pre)
                     with rt.stream(slot.s_lid), self._ktimed(keep, "langid_features"):
-                        self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_emb, lid_vec,
-                                               lid_cnt, flags, self.lds_bytes_lid,
-                                               self._prof_buf(ndocs, keep, f"langid{s}"), self.lid_embx)
+                        for width, prefix in lid_at:
+                            self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_P, self.lid_b,
+                                                   rec[prefix * ndocs:], width, flags, self.lds_bytes_lid,
+                                                   self._prof_buf(ndocs, keep, f"langid{s}"))
                         ev_lid = self._record(slot.s_lid)
                         keep.append(ev_lid)
                 if n_mid > n_long:
@@ -917,7 +904,6 @@ class DeviceRunner:
                     with rt.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_mid"):
                         self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,
                                              scratch, d_soff[n_long:], pw, pw_n, rec, flags,
-                                             self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
                                              self.lds_bytes_mid, prof, self.stage_waves, n_mid - n_long, skip)
                         ev_blk = self._record(slot.s_blk)
                         keep.append(ev_blk)
@@ -938,8 +924,8 @@ class DeviceRunner:
                                 # (HBM scratch arrays, small LDS slice, higher occupancy)
                                 a0 = n_mid + p0
                                 self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[a0:], ndocs,
-                                                     scratch, d_soff[a0:], pw, pw_n, rec, flags, None, lid_vec,
-                                                     lid_cnt, self.lds_bytes, prof, self.stage_waves, p1 - p0, skip)
+                                                     scratch, d_soff[a0:], pw, pw_n, rec, flags,
+                                                     self.lds_bytes, prof, self.stage_waves, p1 - p0, skip)
                                 continue
                             self.k.stage_lds(self.plan_t, self.stage_ts[s], vb, vo, d_perm, n_mid + p0, p1 - p0, ndocs,
                                              rec, flags, sl, retry_cnt, retry_pos, prof, skip,
@@ -952,17 +938,11 @@ class DeviceRunner:
                     with self._ktimed(keep, f"stage{s}"):
                         self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_mid:], ndocs,
                                              scratch, d_soff[n_mid:], pw, pw_n, rec, flags,
-                                             self.lid_emb if lid_vec is not None else None, lid_vec, lid_cnt,
                                              self.lds_bytes, prof, self.stage_waves, ndocs - n_mid, skip)
-                if lid_vec is not None:
-                    self._last_lid = (lid_vec, lid_cnt)
-                    if ev_lid is not None:
-                        main.wait_event(ev_lid)
+                if ev_lid is not None:
+                    main.wait_event(ev_lid)
                 if ev_blk is not None:
                     main.wait_event(ev_blk)
-                for kind, width, prefix in layout:
-                    if kind == KIND_LANGID and not lid_pass:
-                        self.k.langid_head(lid_vec, lid_cnt, self.lid_wT, self.lid_b, ndocs, rec, prefix * ndocs, width)
                 if pass_idx in self.gate_ts:
                     self.k.gate(self.gate_ts[pass_idx], [rec], ndocs, flags, dead, pass_idx + 1, 0,
                                         self.gate_need[pass_idx])

@@ -64,7 +64,7 @@ def category(name):
     if name.startswith("copy") or "copyBuffer" in name:
         return "copy"
     for key in ("k_langid_features", "k_stage_analyze_blk", "k_c4_pass_a_blk", "k_stage_analyze", "k_c4_pass_a",
-                "k_c4_pass_b", "k_langid_head"):
+                "k_c4_pass_b"):
         if name.startswith(key):
             return key
     return "other"
@@ -108,7 +108,7 @@ def report(ev, steps=3, cols=110):
         evw = [e for e in ev if e["b"] > g0]
         g1 = max(e["b"] for e in evw)
         dt = (g1 - g0) / cols
-        letters = {"k_stage_analyze": "S", "k_stage_analyze_blk": "B", "k_langid_features": "L", "k_langid_head": "h",
+        letters = {"k_stage_analyze": "S", "k_stage_analyze_blk": "B", "k_langid_features": "L",
                    "k_c4_pass_a": "C", "k_c4_pass_a_blk": "c", "k_c4_pass_b": "b", "copy": "=", "other": "o"}
         out.append("")
         out.append(f"last {steps} steps, {(g1 - g0) / 1e6:.1f} ms, {dt / 1e3:.0f} us per column  "

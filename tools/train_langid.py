@@ -1,14 +1,19 @@
-"""Train the language-id weights (textblaster_amd/models/data/langid_v1.npz).
+"""Train the language-id weights (textblaster_amd/models/data/langid_v2.npz).
+
+Model (csrc/common/langid.h): per hashed character 1..4-gram bucket an int16 row of fixed-point
+logit contributions to the 5 languages (scale 1/1024) plus a bias; logits = mean of the
+document's rows + b. Trained as a mean-mode EmbeddingBag(buckets, 5) + bias with softmax cross
+entropy, then exported in fixed point (|P| < 32, clamped while training).
 
 Training text: the hand-written sentences in models/data/langid_corpus/<lang>.txt (whole
 sentences, runs of sentences and sentence fragments). Random word sequences from the
 synthetic-corpus vocabularies (utils/synth.VOCAB) are off by default (--vocab-share 0), so the
 benchmark corpus is not generated from the training text; the held-out evaluation
-(tools/eval_langid.py, models/data/langid_eval) shares nothing with either. Features come from the native featurizer
-(_tbhost.langid_buckets), so training and inference hash identically. Label smoothing keeps the
-confidence of short texts below ~0.93, like lingua's relative confidences.
+(tools/eval_langid.py, models/data/langid_eval) shares nothing with either. Features come from
+the native featurizer (_tbhost.langid_buckets), so training and inference hash identically.
+Label smoothing keeps the confidence of short texts moderate, like lingua's relative confidences.
 
-    python tools/train_langid.py [--epochs 30] [--out path]
+    python tools/train_langid.py [--epochs 12] [--n 10000] [--out path]
 """
 import argparse
 import os
@@ -22,11 +27,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from textblaster_amd import native  # noqa: E402
 from textblaster_amd.models.langid import DATA_DIR, LANGS  # noqa: E402
 from textblaster_amd.utils.synth import VOCAB  # noqa: E402
-
-
-def bf16_bits(a: np.ndarray) -> np.ndarray:
-    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(torch.bfloat16)
-    return t.view(torch.int16).numpy().view(np.uint16)
 
 
 def samples(rng: random.Random, n_per_lang: int, vocab_share: float = 0.0):
@@ -56,8 +56,8 @@ def samples(rng: random.Random, n_per_lang: int, vocab_share: float = 0.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--epochs", type=int, default=12)
-    ap.add_argument("--n", type=int, default=6000)
-    ap.add_argument("--out", default=os.path.join(DATA_DIR, "langid_v1.npz"))
+    ap.add_argument("--n", type=int, default=10000)
+    ap.add_argument("--out", default=os.path.join(DATA_DIR, "langid_v2.npz"))
     ap.add_argument("--vocab-share", type=float, default=0.0,
                     help="fraction of samples drawn from the synthetic benchmark vocabulary (default 0)")
     args = ap.parse_args()
@@ -69,11 +69,12 @@ def main():
     keep = [i for i, f in enumerate(feats) if len(f)]
     feats = [feats[i] for i in keep]
     labels = torch.tensor([train[i][1] for i in keep])
-    emb = torch.nn.EmbeddingBag(h.LID_BUCKETS, h.LID_DIM, mode="mean")
-    torch.nn.init.normal_(emb.weight, std=0.05)
-    head = torch.nn.Linear(h.LID_DIM, len(LANGS))
-    opt = torch.optim.Adam(list(emb.parameters()) + list(head.parameters()), lr=0.01)
+    table = torch.nn.EmbeddingBag(h.LID_BUCKETS, len(LANGS), mode="mean")
+    torch.nn.init.zeros_(table.weight)
+    bias = torch.nn.Parameter(torch.zeros(len(LANGS)))
+    opt = torch.optim.Adam(list(table.parameters()) + [bias], lr=0.02)
     lossf = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
+    lim = 32767.0 / h.LID_SCALE
     bs = 256
     for ep in range(args.epochs):
         order = torch.randperm(len(feats))
@@ -82,21 +83,19 @@ def main():
             idx = order[k:k + bs].tolist()
             flat = torch.from_numpy(np.concatenate([feats[i] for i in idx]))
             offs = torch.tensor([0] + list(np.cumsum([len(feats[i]) for i in idx])[:-1]))
-            logits = head(emb(flat, offs))
-            loss = lossf(logits, labels[idx])
+            loss = lossf(table(flat, offs) + bias, labels[idx])
             opt.zero_grad()
             loss.backward()
             opt.step()
             with torch.no_grad():
-                emb.weight.clamp_(-4.0, 4.0)
+                table.weight.clamp_(-lim, lim)
             tot += loss.item() * len(idx)
         print(f"epoch {ep} loss {tot / len(feats):.4f}", flush=True)
-    E = emb.weight.detach().numpy()
-    W = np.zeros((h.LID_DIM, h.LID_LANGS_PAD), dtype=np.float32)
-    W[:, :len(LANGS)] = head.weight.detach().numpy().T
-    b = np.zeros(h.LID_LANGS_PAD, dtype=np.float32)
-    b[:len(LANGS)] = head.bias.detach().numpy()
-    np.savez(args.out, emb=bf16_bits(E).reshape(-1), w=bf16_bits(W).reshape(-1), b=b)
+    P = np.zeros((h.LID_BUCKETS, h.LID_ROW), dtype=np.int16)
+    P[:, :len(LANGS)] = np.clip(np.rint(table.weight.detach().numpy() * h.LID_SCALE), -32767, 32767).astype(np.int16)
+    b = np.zeros(h.LID_ROW, dtype=np.float32)
+    b[:len(LANGS)] = bias.detach().numpy()
+    np.savez(args.out, P=P.reshape(-1), b=b)
     print("saved", args.out, os.path.getsize(args.out))
 
 

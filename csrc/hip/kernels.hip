@@ -194,11 +194,14 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_gr_dup_split(
 
 // Language ID, one wave per document (csrc/common/langid.h): every lane takes one byte position
 // of a 64-byte chunk; a code point position emits the 1..4-grams ending there, and each gram
-// costs one 16-byte gather of its int16 logit row (the model's table is 1 MB: L2-resident). The
-// letters of the three previous code points come from the lanes holding their lead bytes
-// (pointer jumping with shuffles: lane -> its previous lead -> that lane's previous lead ...),
-// so a position decodes only its own code point; only the first lanes of a chunk look further
-// back in memory. Same exact integer sums as the host (langid_record / LangidModel::sums).
+// costs one 16-byte gather of its int16 logit row (the model's table is 1 MB: L2-resident).
+// The letters of the three previous code points come from registers: a ballot of the chunk's
+// lead bytes gives every lane the lanes of its previous code points (highest set bits below it),
+// whose letters are read with shuffles, and the last three letters of the previous chunk are
+// carried in registers for the first lanes. The next chunk's byte is loaded before the current
+// chunk is processed, so the byte load is off the critical path. Only a non-ASCII letter reads
+// the rest of its code point from memory. Same exact integer sums as the host
+// (langid_record / LangidModel::sums).
 __device__ __forceinline__ void lid_add_row16(const int16_t* __restrict__ P, uint32_t g, int32_t* acc) {
   const uint4 w = *(const uint4*)(P + (size_t)g * kLidRow);
   acc[0] += (int32_t)(int16_t)(w.x & 0xffffu);
@@ -207,6 +210,9 @@ __device__ __forceinline__ void lid_add_row16(const int16_t* __restrict__ P, uin
   acc[3] += (int32_t)w.y >> 16;
   acc[4] += (int32_t)(int16_t)(w.z & 0xffffu);
 }
+
+// index of the highest set bit of m (m != 0)
+__device__ __forceinline__ int lid_top(uint64_t m) { return 63 - __clzll((long long)m); }
 
 __device__ __forceinline__ void langid_coop(DocCtx<WavePar>& x, const uint8_t* b, uint32_t n, const LidTables lt,
                                             int64_t* r) {
@@ -224,32 +230,65 @@ __device__ __forceinline__ void langid_coop(DocCtx<WavePar>& x, const uint8_t* b
   }
   const uint32_t lim = *limb;
   const int lane = (int)x.par.lane;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   // a lane adds at most 4 rows (|P| <= 2^15) per chunk of <= 257 chunks: int32 cannot overflow
   int32_t acc[kLidLangs] = {0, 0, 0, 0, 0};
   uint32_t cnt = 0;
+  uint32_t c1 = 0, c2 = 0, c3 = 0;  // letters of the last three code points before the chunk
+  uint8_t cur = (uint32_t)lane < lim ? b[lane] : (uint8_t)0;
   for (uint32_t base = 0; base <= lim; base += 64) {  // wave-uniform trip count
     const uint32_t s = base + (uint32_t)lane;
-    const bool act = s <= lim && (s == lim || utf8_is_lead(b[s]));
-    const uint32_t l0 = act && s < lim ? lid_letter(ucd, b, n, s) : 0u;
-    const int64_t p1 = act ? prev_lead(b, s) : -1;
-    // previous positions inside this chunk come from their lanes (valid: a lead byte < lim is an
-    // active lane), earlier ones from memory
-    const bool in1 = p1 >= (int64_t)base;
-    const int64_t p2s = pardetail::shfl_t(p1, in1 ? (int)(p1 - (int64_t)base) : lane);
-    const uint32_t lm1s = (uint32_t)__shfl((int)l0, in1 ? (int)(p1 - (int64_t)base) : lane);
-    const bool in2 = in1 && p2s >= (int64_t)base;
-    const int64_t p3s = pardetail::shfl_t(p1, in2 ? (int)(p2s - (int64_t)base) : lane);
-    const uint32_t lm2s = (uint32_t)__shfl((int)l0, in2 ? (int)(p2s - (int64_t)base) : lane);
-    const bool in3 = in2 && p3s >= (int64_t)base;
-    const uint32_t lm3s = (uint32_t)__shfl((int)l0, in3 ? (int)(p3s - (int64_t)base) : lane);
-    if (act) {
-      const uint32_t lm1 = in1 ? lm1s : lid_letter(ucd, b, n, p1);
-      const int64_t p2 = p1 < 0 ? -1 : (in1 ? p2s : prev_lead(b, p1));
-      const uint32_t lm2 = in2 ? lm2s : lid_letter(ucd, b, n, p2);
-      const int64_t p3 = p2 < 0 ? -1 : (in2 ? p3s : prev_lead(b, p2));
-      const uint32_t lm3 = in3 ? lm3s : lid_letter(ucd, b, n, p3);
-      cnt += (uint32_t)lid_grams_at(lm3, lm2, lm1, l0, [&](uint32_t g) { lid_add_row16(lt.P, g, acc); });
+    const uint8_t nxt = s + 64 < lim ? b[s + 64] : (uint8_t)0;  // prefetch of the next chunk
+    const bool lead = s < lim && utf8_is_lead(cur);
+    const uint32_t l0 = lead ? (cur < 0x80u ? ((cur | 0x20u) - 'a' < 26u ? (cur | 0x20u) : 0u)
+                                            : lid_letter(ucd, b, n, s))
+                             : 0u;
+    const uint64_t M = __ballot(lead);
+    // previous code points: lanes of the highest lead bits below this one (every lane shuffles,
+    // from a lead lane or itself), then the carry from the previous chunk
+    uint64_t m = M & below;
+    uint32_t lm[3];
+    bool have[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      have[k] = m != 0;
+      const int j = have[k] ? lid_top(m) : lane;
+      if (have[k]) m &= ~(1ull << j);
+      lm[k] = (uint32_t)__shfl((int)l0, j);
     }
+    if (lead || s == lim) {
+      // the slots without a lane in this chunk are a suffix: fill it from the carry, newest first
+      if (!have[0]) {
+        lm[0] = c1; lm[1] = c2; lm[2] = c3;
+      } else if (!have[1]) {
+        lm[1] = c1; lm[2] = c2;
+      } else if (!have[2]) {
+        lm[2] = c1;
+      }
+      cnt += (uint32_t)lid_grams_at(lm[2], lm[1], lm[0], l0, [&](uint32_t g) { lid_add_row16(lt.P, g, acc); });
+    }
+    // carry: letters of this chunk's last three code points (then the older carry); M is
+    // wave-uniform, so these shuffles run in uniform control flow
+    if (M) {
+      uint64_t mm = M;
+      const int j0 = lid_top(mm);
+      mm &= ~(1ull << j0);
+      const uint32_t x0 = (uint32_t)__shfl((int)l0, j0);
+      if (!mm) {
+        c3 = c2; c2 = c1; c1 = x0;
+      } else {
+        const int j1 = lid_top(mm);
+        mm &= ~(1ull << j1);
+        const uint32_t x1 = (uint32_t)__shfl((int)l0, j1);
+        if (!mm) {
+          c3 = c1; c2 = x1; c1 = x0;
+        } else {
+          const uint32_t x2 = (uint32_t)__shfl((int)l0, lid_top(mm));
+          c3 = x2; c2 = x1; c1 = x0;
+        }
+      }
+    }
+    cur = nxt;
   }
   int64_t sums[kLidLangs];
 #pragma unroll

@@ -1301,6 +1301,17 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   });
   x.par.for_n(NLn, [&](uint32_t k) { Pb[poff[k] + plen[k]] = '\n'; });
   x.par.single([&]() { poff[NLn] = Ptot; });
+  // pline[s]: the processed line holding byte s of Pb (= the last line with poff <= s), by a
+  // max-scan of line-start markers (every line owns >= 1 byte, its '\n': starts are distinct)
+  uint32_t* pline = x.template alloc<uint32_t>(Ptot + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  x.par.for_n(Ptot, [&](uint32_t q) { pline[q] = 0; });
+  x.par.sync();
+  x.par.for_n(NLn, [&](uint32_t k) { if (poff[k] < Ptot) pline[poff[k]] = k + 1; });
+  x.par.sync();
+  x.par.template scan<uint32_t>(
+      Ptot, 0u, [](uint32_t a, uint32_t b2) { return a > b2 ? a : b2; }, [&](uint32_t q) { return pline[q]; },
+      [&](uint32_t q, uint32_t e) { const uint32_t v = e > pline[q] ? e : pline[q]; pline[q] = v ? v - 1 : 0u; });
   x.par.sync();
   x.stamp(PH_C4_CITE);
   // ---- words of the processed lines ----
@@ -1313,14 +1324,7 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   x.par.for_n(NLn, [&](uint32_t k) { nw[k] = 0; mx[k] = 0; pf[k] = 0; });
   x.par.sync();
-  auto line_of_byte = [&](uint32_t bs) {  // last line with poff <= bs
-    uint32_t lo = 0, hi = NLn;
-    while (hi - lo > 1) {
-      uint32_t mid = (lo + hi) >> 1;
-      if (poff[mid] <= bs) lo = mid; else hi = mid;
-    }
-    return lo;
-  };
+  auto line_of_byte = [&](uint32_t bs) { return pline[bs]; };  // last line with poff <= bs
   x.par.for_n(pwd.n, [&](uint32_t q) {
     const uint32_t lo = line_of_byte(pwd.bs[q]);
     P::add32(&nw[lo], 1u);
@@ -1333,19 +1337,18 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
     const char* const kPol[6] = {"terms of use", "privacy policy", "cookie policy",
                                  "uses cookies", "use of cookies", "use cookies"};
     const int kPolLen[6] = {12, 14, 13, 12, 14, 11};
+    // The phrases hold letters and spaces only, so a match never runs over the '\n' that ends
+    // its line: match against the rest of Pb first, look the line up only on a match.
     x.par.for_n(Ptot, [&](uint32_t s) {
       uint8_t c0 = Pb[s];
       if (c0 >= 'A' && c0 <= 'Z') c0 = (uint8_t)(c0 + 32);
       if (c0 != 'j' && c0 != 't' && c0 != 'p' && c0 != 'c' && c0 != 'u') return;
-      const uint32_t k = line_of_byte(s);
-      const uint32_t lend = poff[k] + plen[k];
-      if (s >= lend) return;
       uint32_t bits = 0;
-      if (c4.filter_javascript && c0 == 'j' && ci_starts_with(Pb + s, lend - s, "javascript", 10)) bits |= C4F_JS;
+      if (c4.filter_javascript && c0 == 'j' && ci_starts_with(Pb + s, Ptot - s, "javascript", 10)) bits |= C4F_JS;
       if (c4.filter_policy)
         for (int t = 0; t < 6; ++t)
-          if (kPol[t][0] == (char)c0 && ci_starts_with(Pb + s, lend - s, kPol[t], kPolLen[t])) { bits |= C4F_POLICY; break; }
-      if (bits) P::or32(&pf[k], bits);
+          if (kPol[t][0] == (char)c0 && ci_starts_with(Pb + s, Ptot - s, kPol[t], kPolLen[t])) { bits |= C4F_POLICY; break; }
+      if (bits) P::or32(&pf[line_of_byte(s)], bits);
     });
   }
   x.par.sync();

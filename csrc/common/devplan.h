@@ -77,6 +77,9 @@ struct DevC4 {
   int32_t split_paragraph, remove_citations, filter_no_terminal_punct;
   int32_t filter_lorem_ipsum, filter_javascript, filter_curly_bracket, filter_policy;
   int64_t min_words_per_line, max_word_length;
+  // sentences are counted only up to this (the decision and the reason string use smaller
+  // counts only): the record's sentence field saturates here; 0 = not counted
+  int64_t min_num_sentences;
 };
 
 struct DevStage {

@@ -779,25 +779,49 @@ TB_HD uint64_t span_hash(uint64_t pa, uint64_t pb, uint64_t blen_pow) {
   return pb >= x ? pb - x : pb + kM61 - x;
 }
 
-// Sentence count of split_into_sentences() over code points [s, e) (already trimmed text).
+// Sentence count of split_into_sentences() over code points [s, e) (already trimmed text),
+// saturated: sentences are counted chunk by chunk and counting stops after the chunk
+// that reaches `limit`, so the result is exact below `limit` and >= limit otherwise (C4's
+// min_num_sentences test and its reason string only use counts below the limit). A chunk's
+// breaks are compacted, every segment with a non-whitespace code point counts once; the part
+// before the chunk's first break continues the previous chunk's last segment (`seen`: that
+// segment already counted).
 template <class P>
-TB_HD uint32_t count_sentences(DocCtx<P>& x, const Cps& c, uint32_t s, uint32_t e) {
+TB_HD uint32_t count_sentences_upto(DocCtx<P>& x, const Cps& c, uint32_t s, uint32_t e, uint32_t limit) {
   const uint32_t m = e - s;
-  if (m == 0) return 0;
+  if (m == 0 || limit == 0) return 0;
+  constexpr uint32_t kChunk = 256;
   const auto mark = x.mark();
-  uint32_t* starts = x.template alloc<uint32_t>(m + 1);
+  uint32_t* starts = x.template alloc_hot<uint32_t>(kChunk + 1);
+  uint32_t* segf = x.template alloc_hot<uint32_t>(kChunk + 1);
   if (x.overflow) return 0;
   const PropArr prop = c.props() + s;
   CpsAcc acc{prop};
-  const uint32_t NS = x.par.template compact<int>(
-      m, [&](uint32_t i, int&) { return i == 0 || sb_break(acc, (int)m, (int)i); },
-      [&](uint32_t i, uint32_t k, int&) { starts[k] = i; });
-  x.par.sync();
-  const uint32_t cnt = x.par.template sum<uint32_t>(NS, [&](uint32_t k) {
-    const uint32_t a = starts[k], bnd = k + 1 < NS ? starts[k + 1] : m;
-    for (uint32_t j = a; j < bnd; ++j) if (!is_ws(prop[j])) return 1u;
-    return 0u;
-  });
+  uint32_t cnt = 0;
+  bool seen = false;
+  for (uint32_t base = 0; base < m && cnt < limit; base += kChunk) {
+    const uint32_t len = m - base < kChunk ? m - base : kChunk;
+    const uint32_t NS = x.par.template compact<int>(
+        len, [&](uint32_t i, int&) { const uint32_t g = base + i; return g == 0 || sb_break(acc, (int)m, (int)g); },
+        [&](uint32_t i, uint32_t k, int&) { starts[k] = i; });
+    x.par.sync();
+    const uint32_t first = NS ? starts[0] : len;
+    const bool lead_any = x.par.template sum<uint32_t>(first, [&](uint32_t i) {
+      return is_ws(prop[base + i]) ? 0u : 1u;
+    }) != 0;
+    const uint32_t segs = x.par.template sum<uint32_t>(NS, [&](uint32_t k) {
+      const uint32_t a = starts[k], bnd = k + 1 < NS ? starts[k + 1] : len;
+      uint32_t f = 0;
+      for (uint32_t j = a; j < bnd; ++j) if (!is_ws(prop[base + j])) { f = 1; break; }
+      segf[k] = f;
+      return f;
+    });
+    x.par.sync();
+    if (!seen && lead_any) ++cnt;
+    cnt += segs;
+    seen = NS ? segf[NS - 1] != 0 : (seen || lead_any);
+    x.par.sync();
+  }
   x.reset(mark);
   return cnt;
 }
@@ -1301,18 +1325,6 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   });
   x.par.for_n(NLn, [&](uint32_t k) { Pb[poff[k] + plen[k]] = '\n'; });
   x.par.single([&]() { poff[NLn] = Ptot; });
-  // pline[s]: the processed line holding byte s of Pb (= the last line with poff <= s), by a
-  // max-scan of line-start markers (every line owns >= 1 byte, its '\n': starts are distinct)
-  uint32_t* pline = x.template alloc<uint32_t>(Ptot + 1);
-  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
-  x.par.for_n(Ptot, [&](uint32_t q) { pline[q] = 0; });
-  x.par.sync();
-  x.par.for_n(NLn, [&](uint32_t k) { if (poff[k] < Ptot) pline[poff[k]] = k + 1; });
-  x.par.sync();
-  x.par.template scan<uint32_t>(
-      Ptot, 0u, [](uint32_t a, uint32_t b2) { return a > b2 ? a : b2; }, [&](uint32_t q) { return pline[q]; },
-      [&](uint32_t q, uint32_t e) { const uint32_t v = e > pline[q] ? e : pline[q]; pline[q] = v ? v - 1 : 0u; });
-  x.par.sync();
   x.stamp(PH_C4_CITE);
   // ---- words of the processed lines ----
   Cps pc = decode(x, Pb, Ptot);
@@ -1324,7 +1336,14 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   x.par.for_n(NLn, [&](uint32_t k) { nw[k] = 0; mx[k] = 0; pf[k] = 0; });
   x.par.sync();
-  auto line_of_byte = [&](uint32_t bs) { return pline[bs]; };  // last line with poff <= bs
+  auto line_of_byte = [&](uint32_t bs) {  // last line with poff <= bs
+    uint32_t lo = 0, hi = NLn;
+    while (hi - lo > 1) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (poff[mid] <= bs) lo = mid; else hi = mid;
+    }
+    return lo;
+  };
   x.par.for_n(pwd.n, [&](uint32_t q) {
     const uint32_t lo = line_of_byte(pwd.bs[q]);
     P::add32(&nw[lo], 1u);
@@ -1409,7 +1428,8 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   const uint32_t tce = x.par.template max<uint32_t>(JC, 0u, [&](uint32_t i) { return is_ws(jprop[i]) ? 0u : i + 1; });
   uint32_t nsent = 0, bstart = 0, blen = 0;
   if (tcs < tce) {
-    nsent = count_sentences(x, jc, tcs, tce);
+    const uint32_t lim = c4.min_num_sentences > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)c4.min_num_sentences;
+    nsent = count_sentences_upto(x, jc, tcs, tce, lim);
     bstart = jc.o(tcs);
     blen = jc.o(tce) - jc.o(tcs);
   }

@@ -136,9 +136,14 @@ constexpr int kBlockThreads = TB_BLOCK_THREADS;
 #else
 #define TB_BLK_ATTR
 #endif
-__shared__ __attribute__((aligned(16))) char g_block_xs[16 * (kBlockThreads / 64) + 64];
+// The largest documents take a 1024-thread workgroup (k_stage_analyze_blk1k): every
+// phase of the stage is data-parallel over bytes / code points / words, so twice the waves per
+// document halve its passes when a batch holds too few long documents to fill the CUs.
+constexpr int kBlockThreadsMax = 1024;
+__shared__ __attribute__((aligned(16))) char g_block_xs[16 * (kBlockThreadsMax / 64) + 64];
 
-__global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_stage_analyze_blk(
+template <int NT>
+__device__ __forceinline__ void stage_blk_body(
     const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes,
     const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,
     const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
@@ -146,8 +151,8 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_stage_analyze_blk
     GrExport* gr_export, int32_t n_split, uint32_t split_bytes) {
   const int doc = perm[blockIdx.x];
   if (doc >= ndocs || (dead && dead[doc])) return;
-  DocCtx<BlockPar<kBlockThreads>> x =
-      make_ctx<BlockPar<kBlockThreads>>(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
+  DocCtx<BlockPar<NT>> x =
+      make_ctx<BlockPar<NT>>(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
   x.par.xs = g_block_xs;
   lds_ascii_props(x);
   const uint8_t* b = bytes + off[doc];
@@ -156,8 +161,21 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_stage_analyze_blk
   // split documents (the first n_split launch positions, longer than split_bytes) export their
   // word arrays; k_gr_dup_split finishes their duplicated n-gram orders
   if (gr_export && (int)blockIdx.x < n_split && n > split_bytes) out.gr_export = gr_export + blockIdx.x;
-  analyze_stage<BlockPar<kBlockThreads>, false>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out);
+  analyze_stage<BlockPar<NT>, false>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out);
 }
+
+#define TB_STAGE_BLK_KERNEL(NAME, NT)                                                                  \
+  __global__ __launch_bounds__(NT) TB_BLK_ATTR void NAME(                                            \
+      const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes, \
+      const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,         \
+      const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,  \
+      int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead,   \
+      GrExport* gr_export, int32_t n_split, uint32_t split_bytes) {                                    \
+    stage_blk_body<NT>(plan, stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, tabs, rec, flags, \
+                       lds_bytes, prof, dead, gr_export, n_split, split_bytes);                          \
+  }
+TB_STAGE_BLK_KERNEL(k_stage_analyze_blk, kBlockThreads)
+TB_STAGE_BLK_KERNEL(k_stage_analyze_blk1k, kBlockThreadsMax)
 
 // SURVEY 5.7 intra-document split: one workgroup per (split document, duplicated n-gram order).
 // Block k handles launch position k / n_dup (perm order, the stage kernel's export slot) and order
@@ -600,14 +618,15 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
                          const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                          const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
                          uint32_t lds_bytes, uint64_t* prof, const uint8_t* dead, void* gr_export, int32_t n_split,
-                         uint32_t split_bytes) {
+                         uint32_t split_bytes, int32_t threads) {
   if (nblocks <= 0) return 0;
   if (!perm || lds_bytes > kMaxLdsPerBlk || n_split < 0 || n_split > nblocks) return (int)hipErrorInvalidValue;
+  if (threads != kBlockThreads && threads != kBlockThreadsMax) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
+  auto kern = threads == kBlockThreadsMax ? k_stage_analyze_blk1k : k_stage_analyze_blk;
   if (lds_bytes > 65536)
-    (void)hipFuncSetAttribute((const void*)k_stage_analyze_blk, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds_bytes);
-  hipLaunchKernelGGL(k_stage_analyze_blk, dim3(nblocks), dim3(kBlockThreads), lds_bytes, stream,
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  hipLaunchKernelGGL(kern, dim3(nblocks), dim3(threads), lds_bytes, stream,
                      (const DevPlan*)plan, (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw,
                      pw_n, t, rec, flags, lds_bytes, prof, dead, (GrExport*)gr_export, n_split,
                      split_bytes);
@@ -761,7 +780,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 
 int tb_phase_slots() { return kPhaseSlots; }
 
-int tb_abi_version() { return 9; }
+int tb_abi_version() { return 10; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

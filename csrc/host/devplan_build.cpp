@@ -137,6 +137,7 @@ DevC4 build_c4(const StepCfg& c) {
   d.filter_policy = c.filter_policy;
   d.min_words_per_line = c.min_words_per_line;
   d.max_word_length = c.max_word_length;
+  d.min_num_sentences = c.min_num_sentences > 0 ? c.min_num_sentences : 0;
   return d;
 }
 

@@ -186,3 +186,41 @@ def test_badwords_deterministic_seed(tmp_path):
     with pytest.raises(DocumentFiltered) as ei:
         f.process(doc("a", "A sentence with dummybadword.", language="en"))
     assert ei.value.reason == "document_removed_with_badwords"
+
+
+@pytest.mark.parametrize("min_sent", [5, 100000])
+def test_device_sentence_count_saturates_exactly(min_sent):
+    """C4 pass A (device algorithm, host emulation) counts sentences in 256-code-point chunks and
+    stops after the chunk that reaches min_num_sentences: the count equals the ICU oracle's below
+    the threshold (the only counts a decision or a reason string uses) and is >= it otherwise;
+    with a huge threshold every count is exact, including sentences spanning chunk edges."""
+    import numpy as np
+
+    from textblaster_amd import native
+    from textblaster_amd.config import load_pipeline_config_str
+    from textblaster_amd.utils import synth
+
+    h = native.host()
+    cfg = load_pipeline_config_str(
+        "pipeline:\n  - {type: C4QualityFilter, split_paragraph: true, remove_citations: true, "
+        "filter_no_terminal_punct: false, min_num_sentences: %d, min_words_per_line: 1, max_word_length: 1000, "
+        "filter_lorem_ipsum: false, filter_javascript: false, filter_curly_bracket: false, "
+        "filter_policy: false}\n" % min_sent)
+    step = h.make_step(cfg.pipeline[0].native_dict())
+    long_sent = "word " * 120 + "end. "
+    texts = synth.make_corpus(300, 1500, seed=31) + [
+        "", "One.", "One. Two. Three.", long_sent * 4, ("A b. " * 70).strip(), "x" * 600 + ". y.",
+        "Mr. Smith went to Washington. He arrived at 5 p.m. on the U.S. holiday! Was it fun? Yes.",
+        (" \n".join(["Line %d is here." % k for k in range(80)]))]
+    data, off = synth.pack(texts)
+    rec, _, _, flags = h.emulate_c4(step, data, off, 4)
+    rec = rec.reshape(len(texts), 7)
+    for i, t in enumerate(texts):
+        if flags[i]:
+            continue
+        want = h.compute_record(step, t, "icu")[0][5]
+        got = int(rec[i, 5])
+        if want < min_sent:
+            assert got == want, (i, got, want)
+        else:
+            assert got >= min_sent, (i, got, want)

@@ -116,12 +116,13 @@ def _hard_corpus():
     return texts
 
 
-@pytest.mark.parametrize("mode", ["default", "split", "lds"])
+@pytest.mark.parametrize("mode", ["default", "split", "lds", "wide"])
 def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
     """Independent net for the device kernels: the GPU engine against the CPU ICU oracle (not the
     host emulation of the same source) on adversarial, long, split and C4-heavy documents; with
     the GopherRepetition dup orders of every >4.5 KB document split across workgroups ("split")
-    and with the LDS-resident short-document kernel ("lds")."""
+    with the LDS-resident short-document kernel ("lds"), and with every >8 KB document on the
+    1024-thread stage workgroup, half of them also split ("wide")."""
     import json
 
     import numpy as np
@@ -135,6 +136,9 @@ def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
         monkeypatch.setenv("TB_SPLIT_DOC_BYTES", "4096")
     if mode == "lds":
         monkeypatch.setenv("TB_LDS_STAGE", "1")
+    if mode == "wide":
+        monkeypatch.setenv("TB_HUGE_DOC_BYTES", "8192")
+        monkeypatch.setenv("TB_SPLIT_DOC_BYTES", "20000")
     cfg = load_pipeline_config(CFG)
     texts = _hard_corpus()
     data, off = synth.pack(texts)

@@ -22,13 +22,13 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32, _P],
     "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _P],
     "tb_stage_analyze_blk": [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P,
-                             _U32, _P, _P, _P, _I32, _U32],
+                             _U32, _P, _P, _P, _I32, _U32, _I32],
     "tb_gr_dup_split": [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32],
     "tb_sizeof_gr_export": [],
     "tb_c4_pass_a_blk": [_P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _P],
@@ -194,7 +194,8 @@ class Kernels:
         _check(rc, "tb_stage_retry")
 
     def stage_analyze_blk(self, plan, stage, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n,
-                          rec, flags, lds_bytes=0, prof=None, dead=None, gr_export=None, n_split=0, split_bytes=0):
+                          rec, flags, lds_bytes=0, prof=None, dead=None, gr_export=None, n_split=0, split_bytes=0,
+                          threads=512):
         """k_stage_analyze_blk; ``gr_export`` (zeroed, >= n_split descriptors): the first n_split
         launch positions longer than ``split_bytes`` export their word arrays (split mode)."""
         t = self.tabs
@@ -206,7 +207,7 @@ class Kernels:
             self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), perm_long.data_ptr(),
             nlong, ndocs, scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(),
             t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof),
-            _ptr(dead), _ptr(gr_export), n_split if gr_export is not None else 0, split_bytes)
+            _ptr(dead), _ptr(gr_export), n_split if gr_export is not None else 0, split_bytes, int(threads))
         _check(rc, "tb_stage_analyze_blk")
 
     def gr_dup_split(self, stage, gr_step, perm, n_split, n_dup, ndocs, gr_export, pw, pw_n, rec, flags, lds_bytes):

@@ -424,6 +424,10 @@ class DeviceRunner:
     DEFAULT_LDS_BYTES_MID = 32768
     DEFAULT_LDS_BYTES_BLK = 49152
     DEFAULT_SPLIT_DOC_BYTES = 65536
+    # 1024-thread stage workgroups (k_stage_analyze_blk1k) above this size; off by default: at the
+    # 80-VGPR budget the wider variant spills (872 B/lane) and is slower than 512 threads on ~1 MB
+    # documents (profiles/r3_long: 685 vs 728 docs/s at 128 docs/step, 1081 vs 1444 at 384)
+    DEFAULT_HUGE_DOC_BYTES = 0
     DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; sweep: tools/occ_sweep.sh)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None, max_batch_bytes: int = 384 << 20,
@@ -581,6 +585,8 @@ class DeviceRunner:
         # workgroup; 0 disables. Never below the long-document threshold (wave documents cannot
         # export: their arrays may live in LDS).
         self.split_doc_bytes = int(os.environ.get("TB_SPLIT_DOC_BYTES", str(self.DEFAULT_SPLIT_DOC_BYTES)))
+        # documents longer than this get a 1024-thread stage workgroup (0: never)
+        self.huge_doc_bytes = int(os.environ.get("TB_HUGE_DOC_BYTES", str(self.DEFAULT_HUGE_DOC_BYTES)))
         if self.split_doc_bytes > 0:
             self.split_doc_bytes = max(self.split_doc_bytes, self.long_doc_bytes)
         # per stage: (position of its GopherRepetition step, number of duplicated n-gram orders)
@@ -877,10 +883,21 @@ class DeviceRunner:
                             # zeroed on the stream of the kernels that write and read it
                             gx = rt.zeros(n_split * self.k.sizeof_gr_export, np.uint8, slot.s_blk)
                             keep.append(gx)
+                    # launch positions [0, n_huge): 1024-thread workgroups, the rest 512 threads; the
+                    # split export slots are launch positions, so the second launch starts at n_huge
+                    n_huge = (int(np.count_nonzero(lens[perm[:n_long]] > self.huge_doc_bytes))
+                              if self.huge_doc_bytes > 0 else 0)
+                    esz = self.k.sizeof_gr_export
                     with rt.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_blk"):
-                        self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[:n_long], n_long,
-                                                 ndocs, scratch, d_soff, pw, pw_n, rec, flags,
-                                                 self.lds_bytes_blk, prof, skip, gx, n_split, self.split_doc_bytes)
+                        for a0, a1, thr in ((0, n_huge, 1024), (n_huge, n_long, 512)):
+                            if a1 <= a0:
+                                continue
+                            ns = max(0, min(n_split, a1) - a0)
+                            self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[a0:a1], a1 - a0,
+                                                     ndocs, scratch, d_soff[a0:], pw, pw_n, rec, flags,
+                                                     self.lds_bytes_blk, prof, skip,
+                                                     gx[a0 * esz:] if (gx is not None and ns) else None, ns,
+                                                     self.split_doc_bytes, thr)
                         if n_split:
                             gr_pos, n_dup = self.gr_split[s]
                             self.k.gr_dup_split(self.stage_ts[s], gr_pos, d_perm[:n_split], n_split, n_dup, ndocs,

@@ -465,7 +465,8 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
               if (cur == 0) break;
             }
             if ((cur >> 16) == fp && eq(i, (cur & 0xFFFFu) - 1u)) {
-              P::min32(&tab[slot], mine);
+              // the slot's index only decreases: no atomic when it is already below mine
+              if ((cur & 0xFFFFu) > i + 1u) P::min32(&tab[slot], mine);
               break;
             }
             if (++slot == capp) slot = 0;
@@ -503,7 +504,7 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
           if (cur == 0) break;
         }
         if ((cur >> 16) == fp && eq(i, (cur & 0xFFFFu) - 1u)) {
-          P::min32(&tab[slot], mine);
+          if ((cur & 0xFFFFu) > i + 1u) P::min32(&tab[slot], mine);
           break;
         }
         if (++slot == capn) slot = 0;
@@ -532,7 +533,7 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
         if (cur == 0) break;
       }
       if ((cur >> 32) == fp) {
-        P::min64(&tab[slot], mine);
+        if ((cur & 0xFFFFFFFFull) > (uint64_t)i + 1u) P::min64(&tab[slot], mine);
         break;
       }
       if (++slot == capn) slot = 0;
@@ -772,6 +773,77 @@ TB_HD int64_t dup_walk(uint32_t G, uint32_t n, const uint32_t* gc, const uint32_
     }
   }
   return rep;
+}
+
+// dup_walk by one whole wave (every lane calls it with the same arguments; the result is
+// uniform). The chain of the scalar walk pays a memory round trip per step (gc[idx], seen bit);
+// here the wave takes a window of 64 positions starting at the next repeated one, its lanes load
+// the window's canonical ids, seen bits and gram lengths together (one round trip per window),
+// and the walk steps through the window's repeated positions in scalar registers: a first visit
+// marks every lane holding the same id seen (one ballot), a repeat drops the lanes it jumps over.
+// The window's first visits then set their seen bits and the counted lanes' lengths are summed.
+// Same visits, same result as dup_walk.
+template <class P>
+TB_HD int64_t dup_walk_wave(const P& par, uint32_t G, uint32_t n, const uint32_t* gc, const uint32_t* R,
+                            uint32_t* sn, const uint32_t* WL) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lane = par.lane;
+  const uint32_t nw = (G + 31) >> 5;
+  int64_t rep = 0;
+  uint32_t idx = 0;
+  while (idx < G) {
+    uint32_t p0 = G;  // next repeated position >= idx: 64 bitmap words per ballot
+    for (uint32_t base = idx >> 5; base < nw; base += 64) {
+      const uint32_t w = base + lane;
+      uint32_t bw = w < nw ? R[w] : 0u;
+      if (w == (idx >> 5)) bw &= ~0u << (idx & 31);
+      const uint64_t m = __ballot(bw != 0u);
+      if (m) {
+        const int l = __builtin_ctzll(m);
+        p0 = ((base + (uint32_t)l) << 5) + (uint32_t)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)bw, l));
+        break;
+      }
+    }
+    if (p0 >= G) break;
+    const uint32_t p = p0 + lane;
+    const bool act = p < G && ((R[p >> 5] >> (p & 31)) & 1u);
+    uint32_t g = 0xFFFFFFFFu, len = 0;
+    if (act) {
+      g = gc[p];
+      len = WL[p + n] - WL[p];
+    }
+    const bool seen0 =
+        act && ((__hip_atomic_load(&sn[g >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (g & 31)) & 1u);
+    uint64_t A = __ballot(act), S = __ballot(seen0), cnt = 0, fv = 0;
+    uint32_t next = p0 + 64;
+    while (A) {
+      const uint32_t k = (uint32_t)__builtin_ctzll(A);
+      if ((S >> k) & 1ull) {
+        cnt |= 1ull << k;
+        const uint32_t j = k + n;
+        A = j >= 64 ? 0ull : (A & (~0ull << j));
+        if (p0 + j > next) next = p0 + j;
+      } else {
+        fv |= 1ull << k;
+        S |= __ballot(g == (uint32_t)__builtin_amdgcn_readlane((int)g, (int)k));
+        A &= A - 1;
+      }
+    }
+    if ((fv >> lane) & 1ull) atomicOr(&sn[g >> 5], 1u << (g & 31));
+    uint32_t add = ((cnt >> lane) & 1ull) ? len : 0u;
+    for (int o = 32; o > 0; o >>= 1) add += (uint32_t)__shfl_xor((int)add, o);
+    rep += add;
+    // the next window's seen loads (other lanes) must observe these bits
+    // (same wave, same CU: a workgroup-scope fence waits for the atomics; the seen loads read L2)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    idx = next;
+  }
+  return rep;
+#else
+  (void)par;
+  return dup_walk(G, n, gc, R, sn, WL);
+#endif
 }
 
 TB_HD uint64_t span_hash(uint64_t pa, uint64_t pb, uint64_t blen_pow) {
@@ -1050,17 +1122,27 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
         });
         x.par.sync();
       }
-      x.par.for_n((uint32_t)nd, [&](uint32_t t) {
+      auto walk = [&](uint32_t t, bool wave) -> int64_t {
         const uint32_t G = gsize((int)t);
-        int64_t rep = 0;
-        if (G > 0) {
-          uint32_t base = 0;
-          for (uint32_t u = 0; u < t; ++u) base += gsize((int)u);
-          uint32_t* sn = bits + t * 2 * SW;
-          rep = dup_walk(G, (uint32_t)ds.dup_n[t], gcall + base, sn + SW, sn, WL);
+        if (G == 0) return 0;
+        uint32_t base = 0;
+        for (uint32_t u = 0; u < t; ++u) base += gsize((int)u);
+        uint32_t* sn = bits + t * 2 * SW;
+        const uint32_t n = (uint32_t)ds.dup_n[t];
+        return wave ? dup_walk_wave(x.par, G, n, gcall + base, sn + SW, sn, WL)
+                    : dup_walk(G, n, gcall + base, sn + SW, sn, WL);
+      };
+      if constexpr (P::kWaves > 1) {
+        // one wave per order (whole-wave walks)
+        for (uint32_t t = x.par.wave_index(); t < (uint32_t)nd; t += P::kWaves) {
+          const int64_t rep = walk(t, true);
+          if (x.par.lane == 0) r[rec_gr_fixed() + ds.n_top + t] = rep;
         }
-        r[rec_gr_fixed() + ds.n_top + t] = rep;
-      });
+      } else {
+        // one lane per order: the orders' walks overlap (the whole-wave walk would run them
+        // one after another)
+        x.par.for_n((uint32_t)nd, [&](uint32_t t) { r[rec_gr_fixed() + ds.n_top + t] = walk(t, false); });
+      }
       x.par.sync();
       x.stamp(PH_GR_DUP_WALK);
       x.reset(m3);
@@ -1100,7 +1182,14 @@ TB_HD void gr_dup_one_order(DocCtx<P>& x, const DevStep& ds, int t, const GrExpo
     }
   });
   x.par.sync();
-  x.par.single([&]() { *out = dup_walk(G, n, gc, R, bits, e.WL); });
+  if constexpr (P::kWaves > 0) {
+    if (x.par.wave_index() == 0) {
+      const int64_t rep = dup_walk_wave(x.par, G, n, gc, R, bits, e.WL);
+      if (x.par.lane == 0) *out = rep;
+    }
+  } else {
+    x.par.single([&]() { *out = dup_walk(G, n, gc, R, bits, e.WL); });
+  }
   x.par.sync();
   x.reset(mark);
 }

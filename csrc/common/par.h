@@ -39,6 +39,10 @@ TB_HD constexpr uint32_t mask_words(uint32_t n) { return ((n + 63) / 64) * 2; }
 
 struct SeqPar {
   static constexpr bool kPartTables = false;  // canonicalize(): LDS-partitioned tables (no LDS here)
+  // Wave-cooperative sequential loops (dup_walk_wave): the waves of the document's group, each
+  // running whole-wave code; 0 = none (run the scalar version on one lane).
+  static constexpr uint32_t kWaves = 0;
+  uint32_t wave_index() const { return 0; }
   template <class F>
   void for_n(uint32_t n, F&& f) const {
     for (uint32_t i = 0; i < n; ++i) f(i);
@@ -250,7 +254,9 @@ __device__ __forceinline__ T wave_incl_scan(T x, uint32_t lane, Op&& op) {
 
 struct WavePar {
   static constexpr bool kPartTables = false;  // short documents: tables fit the slice (registers matter more)
+  static constexpr uint32_t kWaves = 1;
   uint32_t lane;
+  __device__ uint32_t wave_index() const { return 0; }
   __device__ WavePar() : lane(threadIdx.x & 63) {}
 
   template <class F>
@@ -534,8 +540,10 @@ struct BlockPar {
 #else
   static constexpr bool kPartTables = true;   // long documents: LDS-partitioned hash tables
 #endif
+  static constexpr uint32_t kWaves = NW;
   uint32_t tid, lane, wid;
   char* xs = nullptr;
+  __device__ uint32_t wave_index() const { return wid; }
   __device__ BlockPar() : tid(threadIdx.x), lane(threadIdx.x & 63), wid(threadIdx.x >> 6) {}
 
   template <class F>
@@ -741,9 +749,11 @@ struct SegPar {
   static constexpr int NW = NT / 64;
   static constexpr bool kPartTables = false;
   static constexpr bool kChunks = false;
+  static constexpr uint32_t kWaves = NW;
   uint32_t tid, lane, wid;
   char* xs = nullptr;
   mutable uint32_t gen = 0;
+  __device__ uint32_t wave_index() const { return wid; }
   __device__ SegPar() : tid(threadIdx.x), lane(threadIdx.x & 63), wid(threadIdx.x >> 6) {}
 
   // this wave's item range [b, e)

@@ -1019,7 +1019,10 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     // of the n-grams are built incrementally: the n-gram at p is the pair (id of the (n-1)-gram
     // at p, id of word p+n-1), so each order is one exact pair canonicalisation (O(1) equality,
     // no hashing of the gram text).
-    if (ds.n_top > 0) {
+    if (ds.n_top > 0 && ex) {
+      // split mode: k_gr_dup_split computes each top order in its own workgroup
+      x.par.single([&]() { for (int t = 0; t < ds.n_top; ++t) r[rec_gr_fixed() + t] = 0; });
+    } else if (ds.n_top > 0) {
       int max_top = 0;
       for (int t = 0; t < ds.n_top; ++t) max_top = ds.top_n[t] > max_top ? ds.top_n[t] : max_top;
       const auto m2 = x.mark();
@@ -1065,9 +1068,9 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       x.reset(m2);
     }
     x.stamp(PH_GR_TOP);
-    if (ds.n_dup > 0 && ex) {
-      // split mode: export the word arrays; k_gr_dup_split finishes every order in its own
-      // workgroup and writes the duplicated n-gram fields
+    if (ex) {
+      // split mode: export the word arrays; k_gr_dup_split finishes every order (top and
+      // duplicated) in its own workgroup and writes the n-gram fields
       const uint64_t base = (x.used + 255) & ~255ull;
       x.par.single([&]() {
         for (int t = 0; t < ds.n_dup; ++t) r[rec_gr_fixed() + ds.n_top + t] = 0;
@@ -1149,6 +1152,56 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       x.stamp(PH_GR_DUP);
     }
   }
+  x.reset(mark);
+}
+
+// One top n-gram order of a split document (k_gr_dup_split): the n-grams of order n are grouped
+// by their word-id tuples directly (equal space-joined grams <=> equal word sequences), so the
+// orders are independent of each other (the in-stage path chains order n on order n - 1 instead).
+// Writes r[7 + t], the same value as the in-stage path.
+template <class P>
+TB_HD void gr_top_one_order(DocCtx<P>& x, const DevStep& ds, int t, const GrExport& e, int64_t* r) {
+  const uint32_t W = e.W, n = (uint32_t)ds.top_n[t];
+  int64_t* out = r + rec_gr_fixed() + t;
+  if (n == 0 || W < n) {
+    x.par.single([&]() { *out = 0; });
+    return;
+  }
+  const uint32_t G = W - n + 1;
+  const uint32_t* wid = e.wid;
+  const uint32_t* WL = e.WL;
+  const auto mark = x.mark();
+  uint32_t* gc = x.template alloc_hot_keep<uint32_t>((uint64_t)G + 1, 6ull * G + 64);
+  uint32_t* cnt = x.template alloc_hot_keep<uint32_t>((uint64_t)G + 1, 6ull * G + 64);
+  if (x.overflow) return;
+  canonicalize(
+      x, G,
+      [&](uint32_t p) {
+        uint64_t h = (uint64_t)n << 56;
+        for (uint32_t k = 0; k < n; ++k) h = (h ^ wid[p + k]) * 0x9E3779B97F4A7C15ull + k;
+        return mix64(h);
+      },
+      [&](uint32_t p, uint32_t q) {
+        uint32_t dw = 0;
+        for (uint32_t k = 0; k < n; ++k) dw |= wid[p + k] ^ wid[q + k];
+        return dw == 0;
+      },
+      gc);
+  if (x.overflow) return;
+  x.par.for_n(G, [&](uint32_t p) { cnt[p] = 0; });
+  x.par.sync();
+  x.par.for_n(G, [&](uint32_t p) { P::add32(&cnt[gc[p]], 1u); });
+  x.par.sync();
+  const uint32_t maxc = x.par.template max<uint32_t>(G, 0u, [&](uint32_t p) { return cnt[p]; });
+  int64_t v = 0;
+  if (maxc > 1) {
+    const uint32_t maxlen = x.par.template max<uint32_t>(G, 0u, [&](uint32_t p) {
+      return cnt[p] == maxc ? (WL[p + n] - WL[p] + n - 1) : 0u;
+    });
+    v = (int64_t)maxlen * (int64_t)maxc;
+  }
+  x.par.single([&]() { *out = v; });
+  x.par.sync();
   x.reset(mark);
 }
 

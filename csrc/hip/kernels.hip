@@ -177,14 +177,15 @@ __device__ __forceinline__ void stage_blk_body(
 TB_STAGE_BLK_KERNEL(k_stage_analyze_blk, kBlockThreads)
 TB_STAGE_BLK_KERNEL(k_stage_analyze_blk1k, kBlockThreadsMax)
 
-// SURVEY 5.7 intra-document split: one workgroup per (split document, duplicated n-gram order).
-// Block k handles launch position k / n_dup (perm order, the stage kernel's export slot) and order
-// k % n_dup; each order works in its own 1/n_dup share of the document's unused scratch slice.
+// SURVEY 5.7 intra-document split: one workgroup per (split document, n-gram order): n_tasks =
+// the GopherRepetition step's duplicated orders followed by its top orders. Block k handles launch
+// position k / n_tasks (perm order, the stage kernel's export slot) and task k % n_tasks; each
+// task works in its own 1/n_tasks share of the document's unused scratch slice.
 __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_gr_dup_split(
-    const DevStage* __restrict__ stage, int32_t gr_step, const int32_t* __restrict__ perm, int32_t n_dup,
+    const DevStage* __restrict__ stage, int32_t gr_step, const int32_t* __restrict__ perm, int32_t n_tasks,
     int32_t ndocs, const GrExport* __restrict__ ex, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
     int64_t* rec, uint32_t* flags, uint32_t lds_bytes) {
-  const int k = (int)blockIdx.x / n_dup, t = (int)blockIdx.x % n_dup;
+  const int k = (int)blockIdx.x / n_tasks, t = (int)blockIdx.x % n_tasks;
   const int doc = perm[k];
   if (doc >= ndocs) return;
   const GrExport e = ex[k];
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_gr_dup_split(
   x.pw = pw;
   x.pw_n = pw_n;
   x.ipw = pw ? pw + pw_n + 1 : nullptr;
-  const uint64_t region = (e.free_cap / (uint64_t)n_dup) & ~255ull;
+  const uint64_t region = (e.free_cap / (uint64_t)n_tasks) & ~255ull;
   x.scr = e.free_base + (uint64_t)t * region;
   x.cap = region;
   x.used = 0;
@@ -206,7 +207,8 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_gr_dup_split(
   x.par.xs = g_block_xs;
   const DevStep& ds = stage->steps[gr_step];
   int64_t* r = rec + (int64_t)ds.rec_prefix * ndocs + (int64_t)doc * ds.width;
-  gr_dup_one_order(x, ds, t, e, r);
+  if (t < ds.n_dup) gr_dup_one_order(x, ds, t, e, r);
+  else if (t < ds.n_dup + ds.n_top) gr_top_one_order(x, ds, t - ds.n_dup, e, r);
   if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
 }
 
@@ -634,20 +636,21 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
 }
 
 // gr_export: n_split descriptors written by tb_stage_analyze_blk (zeroed by the caller first);
-// gr_step: index of the GopherRepetition step in the stage, n_dup its duplicated n-gram orders.
+// gr_step: index of the GopherRepetition step in the stage, n_tasks its duplicated + top n-gram
+// orders.
 int tb_gr_dup_split(hipStream_t stream, const void* stage, int32_t gr_step, const int32_t* perm, int32_t n_split,
-                    int32_t n_dup, int32_t ndocs, const void* gr_export, const uint64_t* pw, uint32_t pw_n,
+                    int32_t n_tasks, int32_t ndocs, const void* gr_export, const uint64_t* pw, uint32_t pw_n,
                     const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
                     uint32_t* flags, uint32_t lds_bytes) {
-  if (n_split <= 0 || n_dup <= 0) return 0;
-  if (!perm || !gr_export || gr_step < 0 || gr_step >= kMaxStageSteps || n_dup > kMaxNgramEntries ||
+  if (n_split <= 0 || n_tasks <= 0) return 0;
+  if (!perm || !gr_export || gr_step < 0 || gr_step >= kMaxStageSteps || n_tasks > 2 * kMaxNgramEntries ||
       lds_bytes > kMaxLdsPerBlk)
     return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k_gr_dup_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-  hipLaunchKernelGGL(k_gr_dup_split, dim3((uint32_t)n_split * (uint32_t)n_dup), dim3(kBlockThreads), lds_bytes, stream,
-                     (const DevStage*)stage, gr_step, perm, n_dup, ndocs, (const GrExport*)gr_export, pw, pw_n, t, rec,
+  hipLaunchKernelGGL(k_gr_dup_split, dim3((uint32_t)n_split * (uint32_t)n_tasks), dim3(kBlockThreads), lds_bytes, stream,
+                     (const DevStage*)stage, gr_step, perm, n_tasks, ndocs, (const GrExport*)gr_export, pw, pw_n, t, rec,
                      flags, lds_bytes);
   return (int)hipGetLastError();
 }
@@ -780,7 +783,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 
 int tb_phase_slots() { return kPhaseSlots; }
 
-int tb_abi_version() { return 10; }
+int tb_abi_version() { return 11; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

@@ -150,6 +150,7 @@ PYBIND11_MODULE(_tbhost, m) {
   py::class_<StepCfg>(m, "StepCfg")
       .def_readonly("kind", &StepCfg::kind)
       .def_property_readonly("n_dup", [](const StepCfg& c) { return (int)c.dup_n_grams.size(); })
+      .def_property_readonly("n_top", [](const StepCfg& c) { return (int)c.top_n_grams.size(); })
       .def_readonly("name", &StepCfg::name)
       .def("record_width", [](const StepCfg& c) { return record_width(c); });
   m.def("make_step", &make_step);

@@ -22,7 +22,7 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32, _P],
@@ -210,12 +210,13 @@ class Kernels:
             _ptr(dead), _ptr(gr_export), n_split if gr_export is not None else 0, split_bytes, int(threads))
         _check(rc, "tb_stage_analyze_blk")
 
-    def gr_dup_split(self, stage, gr_step, perm, n_split, n_dup, ndocs, gr_export, pw, pw_n, rec, flags, lds_bytes):
-        """k_gr_dup_split: one workgroup per (split document, duplicated n-gram order)."""
+    def gr_dup_split(self, stage, gr_step, perm, n_split, n_tasks, ndocs, gr_export, pw, pw_n, rec, flags, lds_bytes):
+        """k_gr_dup_split: one workgroup per (split document, n-gram order); n_tasks = the
+        GopherRepetition step's duplicated + top n-gram orders."""
         if gr_export.nbytes < n_split * self.sizeof_gr_export or perm.numel() < n_split:
             raise DeviceError("gr_dup_split: operand shapes")
         t = self.tabs
-        rc = self.lib.tb_gr_dup_split(self.stream(), stage.data_ptr(), gr_step, perm.data_ptr(), n_split, n_dup, ndocs,
+        rc = self.lib.tb_gr_dup_split(self.stream(), stage.data_ptr(), gr_step, perm.data_ptr(), n_split, n_tasks, ndocs,
                                       gr_export.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
                                       t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), lds_bytes)
         _check(rc, "tb_gr_dup_split")

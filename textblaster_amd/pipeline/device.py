@@ -589,12 +589,15 @@ class DeviceRunner:
         self.huge_doc_bytes = int(os.environ.get("TB_HUGE_DOC_BYTES", str(self.DEFAULT_HUGE_DOC_BYTES)))
         if self.split_doc_bytes > 0:
             self.split_doc_bytes = max(self.split_doc_bytes, self.long_doc_bytes)
-        # per stage: (position of its GopherRepetition step, number of duplicated n-gram orders)
+        # per stage: (position of its GopherRepetition step, number of split tasks = its duplicated
+        # + top n-gram orders)
         self.gr_split = {}
         for si, idx in enumerate(plan.stages):
             grs = [k for k, (kind, _, _) in enumerate(self.stage_layout[si][1]) if kind == KIND_GOPHER_REP]
-            if len(grs) == 1 and steps_native[idx[grs[0]]].n_dup > 0:
-                self.gr_split[si] = (grs[0], steps_native[idx[grs[0]]].n_dup)
+            if len(grs) == 1:
+                st = steps_native[idx[grs[0]]]
+                if st.n_dup + st.n_top > 0:
+                    self.gr_split[si] = (grs[0], st.n_dup + st.n_top)
         if not 0 <= self.lds_bytes_blk <= 131072:
             # the workgroup kernels also hold static LDS (cross-wave exchange buffers): a 160 KB
             # dynamic slice does not fit the CU's 160 KB and the launch fails with
@@ -899,8 +902,8 @@ class DeviceRunner:
                                                      gx[a0 * esz:] if (gx is not None and ns) else None, ns,
                                                      self.split_doc_bytes, thr)
                         if n_split:
-                            gr_pos, n_dup = self.gr_split[s]
-                            self.k.gr_dup_split(self.stage_ts[s], gr_pos, d_perm[:n_split], n_split, n_dup, ndocs,
+                            gr_pos, n_tasks = self.gr_split[s]
+                            self.k.gr_dup_split(self.stage_ts[s], gr_pos, d_perm[:n_split], n_split, n_tasks, ndocs,
                                                 gx, pw, pw_n, rec, flags, self.lds_bytes_blk)
                         ev_blk = self._record(slot.s_blk)
                         keep.append(ev_blk)

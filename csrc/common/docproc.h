@@ -193,6 +193,9 @@ struct DocCtx {
     return alloc_global<T>(count);
   }
   TB_HD void release_hi() { lhi = 0; }
+  TB_HD bool in_lds(const void* p) const {
+    return lds && (const char*)p >= lds && (const char*)p < lds + lcap;
+  }
   // bytes of the LDS slice still free between the bottom and top allocations
   TB_HD uint32_t lds_free() const {
     if (!lds) return 0;
@@ -422,9 +425,37 @@ TB_HD Lines rust_lines(DocCtx<P>& x, const Cps& c) {
 // a 32-bit atomic min keeps the smallest index. Larger inputs (workgroup path) use 64-bit slots
 // with a 32-bit fingerprint and a verification pass, where a collision between unequal elements
 // sends the document to the CPU oracle.
+#ifndef TB_ZERO4
+#define TB_ZERO4 1
+#endif
+// Zeroes the u32 table t[0, count rounded up to 4) (allocated that large): 16-byte stores.
+struct alignas(16) Zero4 { uint32_t v[4]; };
+template <class P>
+TB_HD void zero_table(DocCtx<P>& x, uint32_t* t, uint32_t count) {
+  const uint32_t q = (count + 3u) >> 2;
+  // (not in the one-wave kernel: the 16-byte stores cost it registers, measured slower there)
+  if (TB_ZERO4 && P::kWaves != 1 && (((uintptr_t)t) & 15u) == 0) {
+    Zero4* t4 = (Zero4*)t;
+    x.par.for_n(q, [&](uint32_t i) { t4[i] = Zero4{{0u, 0u, 0u, 0u}}; });
+  } else {
+    x.par.for_n(count, [&](uint32_t i) { t[i] = 0; });
+  }
+}
+
+struct NoResolve {
+  TB_HD void operator()(uint32_t, uint32_t) const {}
+};
+
 template <class P, class KeyF, class EqF>
-TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t* canon) {
+TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t* canon);
+
+// Same, and res(i, canon[i]) for every element once its canonical index is final (fused into
+// the last pass, so callers need no extra pass over canon[]).
+template <class P, class KeyF, class EqF, class ResF>
+TB_HD void canonicalize_res(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t* canon, ResF&& res) {
   const uint32_t capn = n + (n >> 1) + 2;
+  // allocated slots: whole 16-byte groups for zero_table's wide stores (exact in the one-wave kernel)
+  const uint32_t capa = P::kWaves == 1 ? capn : (capn + 3u) & ~3u;
   const auto mark = x.mark();
   if (n < 65535u) {
     // The table's random probes want the LDS. When the whole table does not fit the free part
@@ -437,14 +468,14 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
     if (P::kPartTables && x.lds && capn > fit && fit >= 2048u) parts = (capn + fit - 1) / fit;
     if (P::kPartTables && parts > 1) {
       const uint32_t capp = (capn + parts - 1) / parts;
-      uint32_t* tab = x.template alloc_hot_hi<uint32_t>(capp);
+      uint32_t* tab = x.template alloc_hot_hi<uint32_t>(P::kWaves == 1 ? capp : (capp + 3u) & ~3u);
       uint64_t* keys = x.template alloc<uint64_t>(n);
       if (x.overflow) return;
       x.par.for_n(n, [&](uint32_t i) { keys[i] = x.weak_keys ? (key(i) & 3ull) : key(i); });
       x.par.sync();
       bool full = false;
       for (uint32_t q = 0; q < parts; ++q) {
-        x.par.for_n(capp, [&](uint32_t i) { tab[i] = 0; });
+        zero_table(x, tab, capp);
         x.par.sync();
         x.par.for_n(n, [&](uint32_t i) {
           const uint64_t k = keys[i];
@@ -476,11 +507,16 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
         x.par.sync();
         x.par.for_n(n, [&](uint32_t i) {
           const uint32_t home = (uint32_t)(((keys[i] & 0xFFFFFFFFull) * capn) >> 32);
-          if (home / capp == q) canon[i] = (tab[canon[i]] & 0xFFFFu) - 1u;
+          if (home / capp == q) {
+            const uint32_t c = (tab[canon[i]] & 0xFFFFu) - 1u;
+            canon[i] = c;
+            res(i, c);
+          }
         });
         x.par.sync();
       }
       if (x.par.reduce_or(full ? 1u : 0u)) {  // uniform: every lane takes the branch together
+        // (the document goes to the CPU oracle: res() results are discarded with it)
         x.set_flag(DOC_NEEDS_CPU);
         x.par.for_n(n, [&](uint32_t i) { canon[i] = i; });
         x.par.sync();
@@ -488,9 +524,9 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
       x.reset(mark);
       return;
     }
-    uint32_t* tab = x.template alloc_hot_hi<uint32_t>(capn);
+    uint32_t* tab = x.template alloc_hot_hi<uint32_t>(capa);
     if (x.overflow) return;
-    x.par.for_n(capn, [&](uint32_t i) { tab[i] = 0; });
+    zero_table(x, tab, capn);
     x.par.sync();
     x.par.for_n(n, [&](uint32_t i) {
       const uint64_t k = x.weak_keys ? (key(i) & 3ull) : key(i);
@@ -512,14 +548,18 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
       canon[i] = slot;
     });
     x.par.sync();
-    x.par.for_n(n, [&](uint32_t i) { canon[i] = (tab[canon[i]] & 0xFFFFu) - 1u; });
+    x.par.for_n(n, [&](uint32_t i) {
+      const uint32_t c = (tab[canon[i]] & 0xFFFFu) - 1u;
+      canon[i] = c;
+      res(i, c);
+    });
     x.par.sync();
     x.reset(mark);
     return;
   }
-  uint64_t* tab = x.template alloc_hot_hi<uint64_t>(capn);
+  uint64_t* tab = x.template alloc_hot_hi<uint64_t>(capa);
   if (x.overflow) return;
-  x.par.for_n(capn, [&](uint32_t i) { tab[i] = 0; });
+  zero_table(x, (uint32_t*)tab, 2u * capn);
   x.par.sync();
   x.par.for_n(n, [&](uint32_t i) {
     const uint64_t k = x.weak_keys ? (key(i) & 3ull) : key(i);
@@ -546,10 +586,16 @@ TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t
     uint32_t c = (uint32_t)(tab[canon[i]] & 0xFFFFFFFFull) - 1u;
     if (c != i && !eq(i, c)) { collided = true; c = i; }
     canon[i] = c;
+    res(i, c);
   });
   if (collided) x.set_flag(DOC_NEEDS_CPU);
   x.par.sync();
   x.reset(mark);  // the table is scratch; canon[] lives in the caller's allocation
+}
+
+template <class P, class KeyF, class EqF>
+TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t* canon) {
+  canonicalize_res(x, n, key, eq, canon, NoResolve{});
 }
 
 template <class P>
@@ -695,7 +741,34 @@ struct GrExport {
   uint64_t free_cap;
   uint32_t W;
   uint32_t valid;        // 1: exported (0: the document returned early / was skipped)
+  // duplicated lines / paragraphs (lines_valid: their arrays are in HBM and the stage left the
+  // four fields to the split kernel): line break runs rs/rl [NR], paragraph breaks prs [NPR]
+  // (indices into rs), trimmed code point span [tcs, tce), byte offsets, prefix hashes
+  const uint32_t* rs;
+  const uint32_t* rl;
+  const uint32_t* prs;
+  OffArr off;
+  PHView ph;
+  uint32_t NR, NPR, tcs, tce;
+  uint32_t lines_valid;
 };
+
+// Line / paragraph spans of gopher_rep_record (byte ranges of the trimmed text between runs of
+// '\n'): line k of NR + 1, paragraph q of NPR + 1.
+TB_HD void gr_line_span(const uint32_t* rs, const uint32_t* rl, const OffArr& off, uint32_t tcs, uint32_t tce,
+                        uint32_t NR, uint32_t k, uint32_t& s0, uint32_t& e0) {
+  const uint32_t cs = k == 0 ? tcs : rs[k - 1] + rl[k - 1];
+  const uint32_t ce = k == NR ? tce : rs[k];
+  s0 = off[cs];
+  e0 = off[ce];
+}
+TB_HD void gr_para_span(const uint32_t* rs, const uint32_t* rl, const uint32_t* prs, const OffArr& off,
+                        uint32_t tcs, uint32_t tce, uint32_t NPR, uint32_t q, uint32_t& s0, uint32_t& e0) {
+  const uint32_t cs = q == 0 ? tcs : rs[prs[q - 1]] + rl[prs[q - 1]];
+  const uint32_t ce = q == NPR ? tce : rs[prs[q]];
+  s0 = off[cs];
+  e0 = off[ce];
+}
 
 struct StageOut {
   int64_t* rec;     // record buffer (all steps of the stage)
@@ -902,6 +975,7 @@ template <class P>
 TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, const Cps& c,
                              const PHView& ph, const Words& w, int64_t* r, bool release_props = false,
                              GrExport* ex = nullptr) {
+  if constexpr (P::kWaves == 1) ex = nullptr;  // one-wave documents never split (dead code there)
   const uint32_t C = c.n;
   const PropArr prop = c.props();
   const OffArr off = c.offs();
@@ -935,25 +1009,34 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       });
   x.par.sync();
   int64_t line_dup = 0, line_dup_b = 0, para_dup = 0, para_dup_b = 0;
-  dup_spans(x, b, ph, NR + 1,
-            [&](uint32_t k, uint32_t& s0, uint32_t& e0) {
-              const uint32_t cs = k == 0 ? tcs : rs[k - 1] + rl[k - 1];
-              const uint32_t ce = k == NR ? tce : rs[k];
-              s0 = off[cs];
-              e0 = off[ce];
-            },
-            &line_dup, &line_dup_b);
+  // split mode: the duplicated line / paragraph statistics go to k_gr_dup_split when everything
+  // they read is in HBM (it outlives this kernel)
+#ifdef TB_NO_SPLIT_LINES
+  const bool split_lines = false;
+#else
+  const bool split_lines = ex && !x.in_lds(rs) && !x.in_lds(rl) && !x.in_lds(prs) && !x.in_lds(ph.ph8) &&
+                           !x.in_lds(c.ent) && !x.in_lds(c.off);
+#endif
+  if (!split_lines)
+    dup_spans(x, b, ph, NR + 1,
+              [&](uint32_t k, uint32_t& s0, uint32_t& e0) { gr_line_span(rs, rl, off, tcs, tce, NR, k, s0, e0); },
+              &line_dup, &line_dup_b);
   const uint32_t NPR = x.par.template compact<int>(
       NR, [&](uint32_t k, int&) { return rl[k] >= 2; }, [&](uint32_t k, uint32_t q, int&) { prs[q] = k; });
   x.par.sync();
-  dup_spans(x, b, ph, NPR + 1,
-            [&](uint32_t q, uint32_t& s0, uint32_t& e0) {
-              const uint32_t cs = q == 0 ? tcs : rs[prs[q - 1]] + rl[prs[q - 1]];
-              const uint32_t ce = q == NPR ? tce : rs[prs[q]];
-              s0 = off[cs];
-              e0 = off[ce];
-            },
-            &para_dup, &para_dup_b);
+  if (!split_lines)
+    dup_spans(x, b, ph, NPR + 1,
+              [&](uint32_t q, uint32_t& s0, uint32_t& e0) {
+                gr_para_span(rs, rl, prs, off, tcs, tce, NPR, q, s0, e0);
+              },
+              &para_dup, &para_dup_b);
+  if (ex) {
+    x.par.single([&]() {
+      ex->rs = rs; ex->rl = rl; ex->prs = prs; ex->off = off; ex->ph = ph;
+      ex->NR = NR; ex->NPR = NPR; ex->tcs = tcs; ex->tce = tce;
+      ex->lines_valid = split_lines ? 1u : 0u;
+    });
+  }
   x.stamp(PH_GR_LINES);
   x.par.single([&]() {
     r[0] = span;
@@ -1112,18 +1195,27 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
         uint32_t* gc = gcall + gb;
         uint32_t* R = bits + (uint32_t)t * 2 * SW + SW;
         gb += G;
-        canonicalize(
-            x, G, [&](uint32_t p) { return dg.key(p, n); }, [&](uint32_t p, uint32_t q) { return dg.eq(p, q, n); },
-            gc);
-        x.stamp(PH_GR_DUP_CANON);
-        x.par.for_n(G, [&](uint32_t p) {
-          const uint32_t g = gc[p];
-          if (g != p) {
+        auto mark_rep = [&](uint32_t p, uint32_t g) {
+          if (g != p) {  // repeated: the position and its first occurrence
             P::or32(&R[p >> 5], 1u << (p & 31));
             P::or32(&R[g >> 5], 1u << (g & 31));
           }
-        });
-        x.par.sync();
+        };
+        if constexpr (P::kWaves != 1) {
+          // fused into the canonicalisation's last pass
+          canonicalize_res(
+              x, G, [&](uint32_t p) { return dg.key(p, n); }, [&](uint32_t p, uint32_t q) { return dg.eq(p, q, n); },
+              gc, mark_rep);
+          x.stamp(PH_GR_DUP_CANON);
+        } else {
+          // own pass in the one-wave kernel (the fused form costs it registers)
+          canonicalize(
+              x, G, [&](uint32_t p) { return dg.key(p, n); }, [&](uint32_t p, uint32_t q) { return dg.eq(p, q, n); },
+              gc);
+          x.stamp(PH_GR_DUP_CANON);
+          x.par.for_n(G, [&](uint32_t p) { mark_rep(p, gc[p]); });
+          x.par.sync();
+        }
       }
       auto walk = [&](uint32_t t, bool wave) -> int64_t {
         const uint32_t G = gsize((int)t);
@@ -1153,6 +1245,30 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     }
   }
   x.reset(mark);
+}
+
+// Duplicated lines (which = 0: r[5], r[6]) or paragraphs (which = 1: r[2], r[3]) of a split
+// document (k_gr_dup_split), over the arrays gopher_rep_record exported.
+template <class P>
+TB_HD void gr_lines_split(DocCtx<P>& x, int which, const GrExport& e, int64_t* r) {
+  if (!e.lines_valid) return;  // computed in the stage
+  int64_t elems = 0, bytes = 0;
+  if (which == 0)
+    dup_spans(x, e.b, e.ph, e.NR + 1,
+              [&](uint32_t k, uint32_t& s0, uint32_t& e0) { gr_line_span(e.rs, e.rl, e.off, e.tcs, e.tce, e.NR, k, s0, e0); },
+              &elems, &bytes);
+  else
+    dup_spans(x, e.b, e.ph, e.NPR + 1,
+              [&](uint32_t q, uint32_t& s0, uint32_t& e0) {
+                gr_para_span(e.rs, e.rl, e.prs, e.off, e.tcs, e.tce, e.NPR, q, s0, e0);
+              },
+              &elems, &bytes);
+  if (x.overflow) return;
+  x.par.single([&]() {
+    r[which == 0 ? 5 : 2] = elems;
+    r[which == 0 ? 6 : 3] = bytes;
+  });
+  x.par.sync();
 }
 
 // One top n-gram order of a split document (k_gr_dup_split): the n-grams of order n are grouped
@@ -1224,17 +1340,16 @@ TB_HD void gr_dup_one_order(DocCtx<P>& x, const DevStep& ds, int t, const GrExpo
   if (x.overflow) return;
   x.par.for_n(2 * SW, [&](uint32_t i) { bits[i] = 0; });
   x.par.sync();
-  canonicalize(x, G, [&](uint32_t p) { return dg.key(p, n); }, [&](uint32_t p, uint32_t q) { return dg.eq(p, q, n); }, gc);
-  if (x.overflow) return;
   uint32_t* R = bits + SW;
-  x.par.for_n(G, [&](uint32_t p) {
-    const uint32_t g = gc[p];
-    if (g != p) {
-      P::or32(&R[p >> 5], 1u << (p & 31));
-      P::or32(&R[g >> 5], 1u << (g & 31));
-    }
-  });
-  x.par.sync();
+  canonicalize_res(
+      x, G, [&](uint32_t p) { return dg.key(p, n); }, [&](uint32_t p, uint32_t q) { return dg.eq(p, q, n); }, gc,
+      [&](uint32_t p, uint32_t g) {
+        if (g != p) {
+          P::or32(&R[p >> 5], 1u << (p & 31));
+          P::or32(&R[g >> 5], 1u << (g & 31));
+        }
+      });
+  if (x.overflow) return;
   if constexpr (P::kWaves > 0) {
     if (x.par.wave_index() == 0) {
       const int64_t rep = dup_walk_wave(x.par, G, n, gc, R, bits, e.WL);

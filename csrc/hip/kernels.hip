@@ -177,8 +177,9 @@ __device__ __forceinline__ void stage_blk_body(
 TB_STAGE_BLK_KERNEL(k_stage_analyze_blk, kBlockThreads)
 TB_STAGE_BLK_KERNEL(k_stage_analyze_blk1k, kBlockThreadsMax)
 
-// SURVEY 5.7 intra-document split: one workgroup per (split document, n-gram order): n_tasks =
-// the GopherRepetition step's duplicated orders followed by its top orders. Block k handles launch
+// SURVEY 5.7 intra-document split: one workgroup per (split document, task): n_tasks = the
+// GopherRepetition step's duplicated n-gram orders, its top orders, then duplicated lines and
+// duplicated paragraphs. Block k handles launch
 // position k / n_tasks (perm order, the stage kernel's export slot) and task k % n_tasks; each
 // task works in its own 1/n_tasks share of the document's unused scratch slice.
 __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_gr_dup_split(
@@ -209,6 +210,7 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_gr_dup_split(
   int64_t* r = rec + (int64_t)ds.rec_prefix * ndocs + (int64_t)doc * ds.width;
   if (t < ds.n_dup) gr_dup_one_order(x, ds, t, e, r);
   else if (t < ds.n_dup + ds.n_top) gr_top_one_order(x, ds, t - ds.n_dup, e, r);
+  else if (t < ds.n_dup + ds.n_top + 2) gr_lines_split(x, t - ds.n_dup - ds.n_top, e, r);
   if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
 }
 
@@ -643,7 +645,7 @@ int tb_gr_dup_split(hipStream_t stream, const void* stage, int32_t gr_step, cons
                     const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
                     uint32_t* flags, uint32_t lds_bytes) {
   if (n_split <= 0 || n_tasks <= 0) return 0;
-  if (!perm || !gr_export || gr_step < 0 || gr_step >= kMaxStageSteps || n_tasks > 2 * kMaxNgramEntries ||
+  if (!perm || !gr_export || gr_step < 0 || gr_step >= kMaxStageSteps || n_tasks > 2 * kMaxNgramEntries + 2 ||
       lds_bytes > kMaxLdsPerBlk)
     return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};

@@ -590,14 +590,14 @@ class DeviceRunner:
         if self.split_doc_bytes > 0:
             self.split_doc_bytes = max(self.split_doc_bytes, self.long_doc_bytes)
         # per stage: (position of its GopherRepetition step, number of split tasks = its duplicated
-        # + top n-gram orders)
+        # + top n-gram orders + duplicated lines + duplicated paragraphs)
         self.gr_split = {}
         for si, idx in enumerate(plan.stages):
             grs = [k for k, (kind, _, _) in enumerate(self.stage_layout[si][1]) if kind == KIND_GOPHER_REP]
             if len(grs) == 1:
                 st = steps_native[idx[grs[0]]]
                 if st.n_dup + st.n_top > 0:
-                    self.gr_split[si] = (grs[0], st.n_dup + st.n_top)
+                    self.gr_split[si] = (grs[0], st.n_dup + st.n_top + 2)
         if not 0 <= self.lds_bytes_blk <= 131072:
             # the workgroup kernels also hold static LDS (cross-wave exchange buffers): a 160 KB
             # dynamic slice does not fit the CU's 160 KB and the launch fails with

@@ -1431,6 +1431,27 @@ TB_HD bool ci_starts_with(const uint8_t* b, uint32_t n, const char* pat, int ple
   return true;
 }
 
+// The first three bytes at b (n available), ASCII-lowercased, little endian (0 past the end):
+// three independent loads. Every C4 phrase starts with three ASCII letters other than 'k' (the
+// only pattern letter with a multi-byte match, the Kelvin sign), so a phrase can only match where
+// this equals its packed prefix.
+#ifndef TB_C4_PREFIX3
+#define TB_C4_PREFIX3 1
+#endif
+TB_HD uint32_t lower3(const uint8_t* b, uint32_t n) {
+  uint32_t w = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k) {
+    uint32_t c = k < n ? b[k] : 0u;
+    if (c >= 'A' && c <= 'Z') c += 32;
+    w |= c << (8 * k);
+  }
+  return w;
+}
+TB_HD constexpr uint32_t pack3(const char* p) {
+  return (uint32_t)(uint8_t)p[0] | ((uint32_t)(uint8_t)p[1] << 8) | ((uint32_t)(uint8_t)p[2] << 16);
+}
+
 // Bits of the per-line pattern flags (c4_pass_a)
 enum : uint32_t { C4F_JS = 1, C4F_POLICY = 2 };
 
@@ -1441,6 +1462,7 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   const uint32_t lorem = c4.filter_lorem_ipsum
       ? x.par.template sum<uint32_t>(n, [&](uint32_t s) {
           if (b[s] != 'l' && b[s] != 'L') return 0u;
+          if (TB_C4_PREFIX3 && lower3(b + s, n - s) != pack3("lor")) return 0u;
           return ci_starts_with(b + s, n - s, "lorem ipsum", 11) ? 1u : 0u;
         })
       : 0u;
@@ -1620,10 +1642,16 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
       if (c0 >= 'A' && c0 <= 'Z') c0 = (uint8_t)(c0 + 32);
       if (c0 != 'j' && c0 != 't' && c0 != 'p' && c0 != 'c' && c0 != 'u') return;
       uint32_t bits = 0;
-      if (c4.filter_javascript && c0 == 'j' && ci_starts_with(Pb + s, Ptot - s, "javascript", 10)) bits |= C4F_JS;
+      const uint32_t w3 = TB_C4_PREFIX3 ? lower3(Pb + s, Ptot - s) : 0u;
+      auto pre = [&](const char* pat) { return !TB_C4_PREFIX3 || w3 == pack3(pat); };
+      if (c4.filter_javascript && c0 == 'j' && pre("javascript") && ci_starts_with(Pb + s, Ptot - s, "javascript", 10))
+        bits |= C4F_JS;
       if (c4.filter_policy)
         for (int t = 0; t < 6; ++t)
-          if (kPol[t][0] == (char)c0 && ci_starts_with(Pb + s, Ptot - s, kPol[t], kPolLen[t])) { bits |= C4F_POLICY; break; }
+          if (kPol[t][0] == (char)c0 && pre(kPol[t]) && ci_starts_with(Pb + s, Ptot - s, kPol[t], kPolLen[t])) {
+            bits |= C4F_POLICY;
+            break;
+          }
       if (bits) P::or32(&pf[line_of_byte(s)], bits);
     });
   }
@@ -1714,6 +1742,9 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
 #ifndef TB_HOT_PROPS
 #define TB_HOT_PROPS 1
 #endif
+#ifndef TB_GQ_BYTES
+#define TB_GQ_BYTES 1
+#endif
 constexpr bool kHotProps = TB_HOT_PROPS != 0;
 
 template <class P, bool kWithLid = true>
@@ -1791,6 +1822,19 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
           return (int64_t)is_stop_word(ucd, ss, c, w.cs[k], w.ce[k]);
         });
       }
+#if TB_GQ_BYTES
+      // the same counts over the bytes ('#' and '.' are ASCII, U+2026 is E2 80 A6 and E2 is
+      // always a lead byte): no code point offset loads
+      const uint64_t he = x.par.template sum<uint64_t>(n, [&](uint32_t i) {
+        const uint32_t c0 = b[i];
+        if (c0 == '#') return (uint64_t)1 << 32;
+        if (c0 == 0xE2) return (uint64_t)(i + 2 < n && b[i + 1] == 0x80 && b[i + 2] == 0xA6);
+        if (c0 != '.' || (i > 0 && b[i - 1] == '.')) return (uint64_t)0;
+        uint32_t j = i;
+        while (j < n && b[j] == '.') ++j;
+        return (uint64_t)((j - i) / 3);
+      });
+#else
       const uint64_t he = x.par.template sum<uint64_t>(C, [&](uint32_t i) {
         const uint32_t c0 = c.lead(i);
         if (c0 == '#') return (uint64_t)1 << 32;
@@ -1800,6 +1844,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
         while (j < C && c.lead(j) == '.') ++j;
         return (uint64_t)((j - i) / 3);
       });
+#endif
       const int64_t nhash = hi32(he), nell = lo32(he);
       const uint64_t be = x.par.template sum<uint64_t>(L.n, [&](uint32_t k) {
         const uint32_t ls = L.ls[k], le = L.le[k];

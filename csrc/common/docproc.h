@@ -319,7 +319,13 @@ TB_HD PHView prefix_hash8(DocCtx<P>& x, const uint8_t* b, uint32_t n) {
       [&](uint32_t k) {
         const uint32_t s0 = k << 3, e0 = s0 + 8 < n ? s0 + 8 : n;
         uint64_t h = 0;
-        for (uint32_t j = s0; j < e0; ++j) h = hash_push(h, b[j]);
+        if (pwn >= 8) {
+          // the Horner hash of the block as a sum of independent terms (v_j + 1) * B^(L-1-j)
+          const uint32_t L = e0 - s0;
+          for (uint32_t j = 0; j < L; ++j) h = addmod61(h, mulmod61((uint64_t)b[s0 + j] + 1, pw[L - 1 - j]));
+        } else {
+          for (uint32_t j = s0; j < e0; ++j) h = hash_push(h, b[j]);
+        }
         return HL{h, e0 - s0, 0};
       },
       [&](uint32_t k, const HL& e) { ph8[k] = e.h; });
@@ -682,6 +688,27 @@ TB_HD void lower_bytes(const UcdView& ucd, const Cps& cv, uint32_t s, uint32_t e
 TB_HD bool is_stop_word(const UcdView& ucd, const DevStopSet& ss, const Cps& cv, uint32_t s, uint32_t e) {
   // every code point lowercases to at least one byte
   if (ss.n == 0 || (int32_t)(e - s) > ss.max_len) return false;
+  if (ss.lite_nslots > 0) {
+    // ASCII word of <= 7 bytes (as many bytes as code points): its lowercase bytes are the key
+    // of the set's fast table, which holds every ASCII entry of <= 7 bytes (devplan.h)
+    const uint32_t b0 = cv.o(s), nb = cv.o(e) - b0;
+    if (nb <= 7u && nb == e - s) {
+      uint64_t key = (uint64_t)nb << 56;
+      for (uint32_t k = 0; k < nb; ++k) {
+        uint32_t c = cv.b[b0 + k];
+        if (c >= 'A' && c <= 'Z') c += 32;
+        key |= (uint64_t)c << (8 * k);
+      }
+      const uint32_t ns = (uint32_t)ss.lite_nslots;
+      uint32_t slot = stop_fast_slot(key, ns);
+      while (true) {
+        const uint64_t f = ss.fast_keys[slot];
+        if (f == 0) return false;
+        if (f == key) return true;
+        slot = (slot + 1) & (ns - 1);
+      }
+    }
+  }
   uint64_t h = 0;
   uint32_t len = 0;
   lower_bytes(ucd, cv, s, e, [&](uint8_t v) { h = hash_push(h, v); ++len; });

@@ -2,7 +2,7 @@
 # GPU tests, serialized kernel profile + phase cycles, two headline runs.
 cd "$(dirname "$0")/.."
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-OUT=gpurun_out/check4
+OUT=gpurun_out/${1:-check4}
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -2 $OUT/pytest.log

@@ -319,13 +319,9 @@ TB_HD PHView prefix_hash8(DocCtx<P>& x, const uint8_t* b, uint32_t n) {
       [&](uint32_t k) {
         const uint32_t s0 = k << 3, e0 = s0 + 8 < n ? s0 + 8 : n;
         uint64_t h = 0;
-        if (pwn >= 8) {
-          // the Horner hash of the block as a sum of independent terms (v_j + 1) * B^(L-1-j)
-          const uint32_t L = e0 - s0;
-          for (uint32_t j = 0; j < L; ++j) h = addmod61(h, mulmod61((uint64_t)b[s0 + j] + 1, pw[L - 1 - j]));
-        } else {
-          for (uint32_t j = s0; j < e0; ++j) h = hash_push(h, b[j]);
-        }
+        // (a sum of independent (v_j + 1) * B^(L-1-j) terms measured slower: 23.1 K -> 31.5 K
+        // prefix_hash cycles/doc, the power loads)
+        for (uint32_t j = s0; j < e0; ++j) h = hash_push(h, b[j]);
         return HL{h, e0 - s0, 0};
       },
       [&](uint32_t k, const HL& e) { ph8[k] = e.h; });

@@ -175,6 +175,7 @@ def main():
     totals = ctx.all_reduce_sum(counters)
     docs_total = int(totals[0])
     value = docs_total / elapsed_max
+    lid = getattr(eng, "langid", None)
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -187,12 +188,15 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / CPU_BASELINE_DOCS_PER_SEC, 3) if CPU_BASELINE_DOCS_PER_SEC else None,
-            "dtype": "bf16",
+            # the matrix-core dtype of the language-id head that ran (v3: bf16 MFMA; v2 int16 table:
+            # "int16"); the text filters themselves are integer / byte arithmetic
+            "dtype": lid.dtype if lid is not None else "int",
             "data": f"synthetic CommonCrawl-shaped docs (log-normal ~{args.mean_bytes} B, 5 languages, "
                     f"{'~130-word' if args.vocab == 'small' else '60k-type Zipf'} vocabularies), "
                     f"{args.docs_per_step} docs/GPU/step",
             "config": {
-                "model": "+".join(s.type.replace("LanguageDetectionFilter", "LanguageDetection(hashed 1-4-gram int16 logit table)")
+                "model": "+".join(s.type.replace("LanguageDetectionFilter", f"LanguageDetection({lid.description})"
+                                                 if lid is not None else "LanguageDetection")
                                   .replace("Filter", "") for s in cfg.pipeline),
                 "global_batch": args.docs_per_step * world,
                 "seq_len": int(bytes_per_step / args.docs_per_step),

@@ -1391,13 +1391,11 @@ TB_HD void gr_dup_one_order(DocCtx<P>& x, const DevStep& ds, int t, const GrExpo
 // exactly. Neighbouring letters are found by stepping back to the previous lead bytes, so no
 // per-code-point arrays are needed. The device runs its own kernel for this (k_langid_features,
 // same sums); this version runs inside the stage emulation on the host.
-template <class P>
-TB_HD void langid_record(DocCtx<P>& x, const uint8_t* b, uint32_t n, const LidTables& lt, int64_t* r) {
+template <class P, int D>
+TB_HD void langid_sums(DocCtx<P>& x, const uint8_t* b, uint32_t n, const LidTables& lt, int64_t* sums) {
   const UcdView ucd = x.ucd;
   const auto mark = x.mark();
-  constexpr int D = kLidLangs + 1;  // 5 language sums + the n-gram count
   int32_t* tmp = x.template alloc_hot<int32_t>(64 * D);
-  int64_t* sums = x.template alloc_hot<int64_t>(D);
   uint32_t* limb = x.template alloc_hot<uint32_t>(1);
   if (x.overflow) return;
   // byte offset of code point kLidMaxCps (the cut), or n
@@ -1411,7 +1409,7 @@ TB_HD void langid_record(DocCtx<P>& x, const uint8_t* b, uint32_t n, const LidTa
   }
   const uint32_t lim = *limb;
   // A lane visits ceil((lim + 1) / 64) <= 257 byte positions (lim <= 4 * kLidMaxCps) with at most
-  // 4 grams each and |P| <= 2^15: int32 partials cannot overflow.
+  // 4 grams each and |row value| <= 2^15: int32 partials cannot overflow.
   x.par.template accum_rows<D>(
       lim + 1,
       [&](uint32_t s, int32_t* part) {
@@ -1420,12 +1418,38 @@ TB_HD void langid_record(DocCtx<P>& x, const uint8_t* b, uint32_t n, const LidTa
         const int64_t p1 = prev_lead(b, s);
         const int64_t p2 = p1 >= 0 ? prev_lead(b, p1) : -1;
         const int64_t p3 = p2 >= 0 ? prev_lead(b, p2) : -1;
-        part[kLidLangs] += lid_grams_at(lid_letter(ucd, b, n, p3), lid_letter(ucd, b, n, p2),
-                                        lid_letter(ucd, b, n, p1), l0,
-                                        [&](uint32_t g) { lid_add_row(lt.P, g, part); });
+        part[D - 1] += lid_grams_at(lid_letter(ucd, b, n, p3), lid_letter(ucd, b, n, p2),
+                                    lid_letter(ucd, b, n, p1), l0, [&](uint32_t g) {
+                                      if (lt.E) lid_add_emb(lt.E, g, part);
+                                      else lid_add_row(lt.P, g, part);
+                                    });
       },
       tmp, sums);
-  x.par.single([&]() { lid_decide(sums, sums[kLidLangs], lt.bias, r); });
+  x.reset(mark);
+}
+
+// Language-id record straight from the UTF-8 bytes: every code point position (a UTF-8 lead
+// byte, as decode() defines them) of the first kLidMaxCps code points, plus the virtual end
+// position, emits the 1..4-grams ending there (lid_grams_at); their rows (v2: int16 logit rows,
+// v3: int8 embedding rows) are summed exactly, then decided (v3: lid_record_v3, the same integers
+// as the device's MFMA tile). Neighbouring letters are found by stepping back to the previous lead
+// bytes, so no per-code-point arrays are needed. The device runs its own kernel for this
+// (k_langid_features / k_langid_mfma, same records); this version runs inside the stage
+// emulation on the host.
+template <class P>
+TB_HD void langid_record(DocCtx<P>& x, const uint8_t* b, uint32_t n, const LidTables& lt, int64_t* r) {
+  const auto mark = x.mark();
+  int64_t* sums = x.template alloc_hot<int64_t>(kLidDim + 1);  // shared by the lanes
+  if (x.overflow) return;
+  if (lt.E) {
+    langid_sums<P, kLidDim + 1>(x, b, n, lt, sums);
+    if (x.overflow) return;
+    x.par.single([&]() { lid_record_v3(sums, sums[kLidDim], lt, r); });
+  } else {
+    langid_sums<P, kLidLangs + 1>(x, b, n, lt, sums);
+    if (x.overflow) return;
+    x.par.single([&]() { lid_decide(sums, sums[kLidLangs], lt.bias, r); });
+  }
   x.par.sync();
   x.reset(mark);
 }
@@ -1932,7 +1956,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
     } else if (ds.kind == DK_LANGID) {
       // on the device this runs as a separate kernel (k_langid_features): lid.P == nullptr
       if constexpr (kWithLid)
-        if (lid.P) langid_record(x, b, n, lid, r);
+        if (lid.P || lid.E) langid_record(x, b, n, lid, r);
       x.stamp(PH_LID);
     }
     if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }

@@ -1,14 +1,19 @@
 // Character n-gram language identifier that stands in for lingua (reference
-// src/pipeline/filters/language_filter.rs:35-93; survey H5).
+// src/pipeline/filters/language_filter.rs:35-93; survey H5). Two models share the featurizer:
 //
-// Model: a linear classifier over hashed character n-grams. Every bucket holds the int16
-// fixed-point logit contributions of its n-grams to the 5 candidate languages (P[bucket][8],
-// 5 used, scale kLidScale); logits = (sum over the document's grams of P[g]) / #grams / kLidScale
-// + b, softmax over the 5 languages, the confidence is the top probability. The sums are exact
-// integers, so host and device agree bit for bit; the per-gram work is one 16-byte gather.
-// (Equivalent to a mean-of-embeddings fastText model with its linear head folded into the
-// table offline: (mean E) W = mean (E W). The folded table has more capacity than the rank-32
-// factorisation and needs no doc-vector GEMM; tools/train_langid.py trains it directly.)
+// v3 (default, "fastText + bf16 MFMA head"): every hashed n-gram bucket holds an int8 embedding
+// row of kLidDim = 32 dims; a document's rows are summed exactly (int32), the mean doc vector is
+// quantised to integers |a| <= 255 with one exponent per document (block floating point, every
+// value exact in bf16), and the 32 -> 5 linear head runs as one v_mfma_f32_16x16x32_bf16 tile per
+// 16 documents with integer bf16 weights |W| <= 255. All products and partial sums are integers
+// below 2^24, so the MFMA's fp32 result is exact in any summation order and the host computes the
+// same integers: logits = C * w_scale * 2^-e + b, softmax, confidence = top probability.
+//
+// v2 (opt-in): the head folded into the table offline, P[bucket][8] int16 fixed-point logit
+// contributions (scale kLidScale): logits = (sum of the document's rows) / #grams / kLidScale + b.
+//
+// Both decide with lid_exp (a fixed polynomial with explicit fma), so host and device agree on the
+// confidence bits, not only on the integer sums.
 //
 // N-grams: the text is scanned as code points (first kLidMaxCps only); letters (Alphabetic) are
 // lowercased, every maximal letter run is a word padded as "<w>"; n-grams of length 1..4 of the
@@ -28,6 +33,9 @@ constexpr int kLidMaxCps = 4096;
 constexpr int kLidMaxGrams = 4;  // n-grams emitted per code point position, at most
 constexpr uint32_t kLidBoundary = 0x20;
 constexpr double kLidScale = 1024.0;  // P = int16 / 1024 (|P| < 32)
+constexpr int kLidDim = 32;           // v3 embedding dims = the MFMA K
+constexpr int kLidHeadCols = 16;      // v3 head columns (5 languages, zero padded to the MFMA N)
+constexpr int kLidQMax = 255;         // v3 doc-vector / head integers: |v| <= 255 (exact in bf16)
 
 TB_HD uint32_t lid_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d, int n) {
   uint32_t h = 2166136261u ^ (uint32_t)n * 0x9E3779B1u;
@@ -72,8 +80,37 @@ TB_HD void lid_add_row(const int16_t* P, uint32_t g, int32_t* acc) {
   for (int l = 0; l < kLidLangs; ++l) acc[l] += r[l];
 }
 
-// Decision from the exact sums: r[0] = language index (-1: no n-gram), r[1] = confidence bits
-// (f64). Ties go to the lowest index. Same double arithmetic on host and device.
+// exp(x) for x <= 0 with the same bits on host and device: range reduction by ln 2 and a
+// degree-13 Taylor polynomial on |r| <= 0.35 (truncation error < 4e-18), every multiply-add an
+// explicit fma (correctly rounded on both sides; no contraction choices left to the compiler).
+TB_HD double lid_exp(double x) {
+  if (!(x > -745.0)) return 0.0;
+  const double k = floor(fma(x, 1.4426950408889634, 0.5));
+  double r = fma(-k, 6.93147180369123816490e-01, x);  // ln2 hi
+  r = fma(-k, 1.90821492927058770002e-10, r);         // ln2 lo
+  double p = 1.0 / 6227020800.0;                      // 1/13!
+  const double inv[13] = {1.0 / 479001600.0, 1.0 / 39916800.0, 1.0 / 3628800.0, 1.0 / 362880.0, 1.0 / 40320.0,
+                          1.0 / 5040.0, 1.0 / 720.0, 1.0 / 120.0, 1.0 / 24.0, 1.0 / 6.0, 0.5, 1.0, 1.0};
+#pragma unroll
+  for (int i = 0; i < 13; ++i) p = fma(p, r, inv[i]);
+  return ldexp(p, (int)k);
+}
+
+// Softmax decision over kLidLangs logits: r[0] = language index (ties: lowest), r[1] = the
+// confidence (top probability) as f64 bits.
+TB_HD void lid_softmax_decide(const double* logit, int64_t* r) {
+  int best = 0;
+  for (int l = 1; l < kLidLangs; ++l) if (logit[l] > logit[best]) best = l;
+  double den = 0;
+  for (int l = 0; l < kLidLangs; ++l) den += lid_exp(logit[l] - logit[best]);
+  const double conf = 1.0 / den;
+  r[0] = best;
+  union { double d; int64_t i; } u;
+  u.d = conf;
+  r[1] = u.i;
+}
+
+// v2 decision from the exact sums: r[0] = language index (-1: no n-gram), r[1] = confidence bits.
 TB_HD void lid_decide(const int64_t* sums, int64_t cnt, const float* bias, int64_t* r) {
   if (cnt <= 0) {
     r[0] = -1;
@@ -82,15 +119,47 @@ TB_HD void lid_decide(const int64_t* sums, int64_t cnt, const float* bias, int64
   }
   double logit[kLidLangs];
   for (int l = 0; l < kLidLangs; ++l) logit[l] = (double)sums[l] / (double)cnt / kLidScale + (double)bias[l];
-  int best = 0;
-  for (int l = 1; l < kLidLangs; ++l) if (logit[l] > logit[best]) best = l;
-  double den = 0;
-  for (int l = 0; l < kLidLangs; ++l) den += exp(logit[l] - logit[best]);
-  const double conf = 1.0 / den;
-  r[0] = best;
-  union { double d; int64_t i; } u;
-  u.d = conf;
-  r[1] = u.i;
+  lid_softmax_decide(logit, r);
+}
+
+// ---- v3 -----------------------------------------------------------------------------------
+// Block exponent of a document: the largest e in [0, 30] with max|S| * 2^e <= 255 * cnt, so every
+// a[k] = round(S[k] * 2^e / cnt) satisfies |a[k]| <= 255.
+TB_HD int lid_block_exp(int64_t smax, int64_t cnt) {
+  int e = 0;
+  while (e < 30 && (smax << (e + 1)) <= (int64_t)kLidQMax * cnt) ++e;
+  return e;
+}
+
+// round(s * 2^e / cnt), ties to even, exact integer arithmetic (|s| * 2^e < 2^62).
+TB_HD int32_t lid_quant(int64_t s, int e, int64_t cnt) {
+  const bool neg = s < 0;
+  const int64_t num = (neg ? -s : s) << e;
+  int64_t q = num / cnt;
+  const int64_t rem = num - q * cnt;
+  if (2 * rem > cnt || (2 * rem == cnt && (q & 1))) ++q;
+  return (int32_t)(neg ? -q : q);
+}
+
+// v3 decision from the head's integer outputs C[l] (exact: the MFMA fp32 values) and the block
+// exponent e; cnt <= 0: no n-gram (no language).
+TB_HD void lid_decide_v3(const double* C, int e, int64_t cnt, double w_scale, const float* bias, int64_t* r) {
+  if (cnt <= 0) {
+    r[0] = -1;
+    r[1] = 0;
+    return;
+  }
+  const double sc = ldexp(w_scale, -e);
+  double logit[kLidLangs];
+  for (int l = 0; l < kLidLangs; ++l) logit[l] = fma(C[l], sc, (double)bias[l]);
+  lid_softmax_decide(logit, r);
+}
+
+// Float <-> bf16 bits for values that are exact in bf16 (the v3 operands are integers <= 256).
+TB_HD uint16_t lid_bf16_bits(float v) {
+  union { float f; uint32_t u; } x;
+  x.f = v;
+  return (uint16_t)(x.u >> 16);
 }
 
 // Lowercased letter of the code point starting at byte s (0: not a letter / out of range).
@@ -114,10 +183,42 @@ TB_HD int64_t prev_lead(const uint8_t* b, int64_t s) {
   return k;
 }
 
-// The model's tables as the kernels see them.
+// The model's tables as the kernels see them (v2: P; v3: E, W, w_scale).
 struct LidTables {
-  const int16_t* P;    // [kLidBuckets * kLidRow]
+  const int16_t* P;    // v2: [kLidBuckets * kLidRow]
   const float* bias;   // [kLidRow]
+  const int8_t* E = nullptr;   // v3: [kLidBuckets * kLidDim] int8 embedding rows
+  const int16_t* W = nullptr;  // v3: [kLidDim * kLidLangs] integer head (|W| <= 255)
+  double w_scale = 0;          // v3: logit units per head unit at e = 0
 };
+
+// Adds the int8 embedding row of bucket g to the kLidDim sums (v3).
+TB_HD void lid_add_emb(const int8_t* E, uint32_t g, int32_t* acc) {
+  const int8_t* r = E + (size_t)g * kLidDim;
+#pragma unroll
+  for (int d = 0; d < kLidDim; ++d) acc[d] += r[d];
+}
+
+// v3 record from the exact embedding sums S[kLidDim] and the n-gram count (host reference of the
+// device's MFMA tile: the same integers).
+TB_HD void lid_record_v3(const int64_t* S, int64_t cnt, const LidTables& lt, int64_t* r) {
+  if (cnt <= 0) {
+    r[0] = -1;
+    r[1] = 0;
+    return;
+  }
+  int64_t smax = 0;
+  for (int d = 0; d < kLidDim; ++d) smax = (S[d] < 0 ? -S[d] : S[d]) > smax ? (S[d] < 0 ? -S[d] : S[d]) : smax;
+  const int e = lid_block_exp(smax, cnt);
+  int32_t a[kLidDim];
+  for (int d = 0; d < kLidDim; ++d) a[d] = lid_quant(S[d], e, cnt);
+  double C[kLidLangs];
+  for (int l = 0; l < kLidLangs; ++l) {
+    int64_t c = 0;
+    for (int d = 0; d < kLidDim; ++d) c += (int64_t)a[d] * lt.W[d * kLidLangs + l];
+    C[l] = (double)c;
+  }
+  lid_decide_v3(C, e, cnt, lt.w_scale, lt.bias, r);
+}
 
 }  // namespace tb

@@ -1,4 +1,5 @@
-// HIP kernels for gfx950 (MI355X). C ABI, launched on a caller-provided stream (PyTorch's).
+// HIP kernels for gfx950 (MI355X). C ABI, launched on a caller-provided stream (the native HIP
+// runtime layer's, csrc/hip/runtime.hip).
 //
 // Document kernels run one wavefront per document (block = 64 lanes = one wave64): the lanes
 // cooperate through DPP shuffles and ballots (csrc/common/par.h WavePar), per-document working
@@ -7,7 +8,8 @@
 // longest documents start first (tail-latency balance under the power-law length distribution).
 //
 //  tb_stage_analyze   : decode + UAX#29 words + lines + hashes -> Gopher/FineWeb records
-//  tb_langid_features : hashed 1..4-gram int16 logit rows summed per document -> language records
+//  tb_langid_mfma     : fastText int8 embedding bag + bf16 MFMA head (16 docs per tile) -> language records
+//  tb_langid_features : (v2 model) hashed 1..4-gram int16 logit rows summed per document -> language records
 //  tb_c4_pass_a       : C4 line filtering, citation removal, rewritten text into scratch
 //  tb_c4_pass_b       : compaction of the rewritten texts into the next content version
 #include <hip/hip_runtime.h>
@@ -352,6 +354,196 @@ __global__ __launch_bounds__(64) void k_langid_features(
   if (__ballot(dict) && x.par.leader()) x.set_flag(DOC_NEEDS_CPU);
   x.stamp(PH_LID);
   if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
+}
+
+// Language ID v3 (csrc/common/langid.h): fastText bag + bf16 MFMA head, 16 documents per
+// workgroup (one wave each, launch positions blockIdx.x * 16 + wave). Each wave gathers the int8
+// embedding rows of its document's n-grams (two 16-byte loads per gram, the same chunked walk and
+// register letter carry as langid_coop) into 32 per-lane int32 sums, reduces them across the
+// lanes with a halving butterfly (32 shuffles: after it lane l holds dim d(l) summed over the
+// wave), quantises the mean vector with the document's block exponent (lid_block_exp /
+// lid_quant: integers |a| <= 255, exact in bf16) into the workgroup's 16 x 32 A tile in LDS.
+// Wave 0 then runs the head as one v_mfma_f32_16x16x32_bf16 (A: 16 docs x 32 dims, B: the
+// head transposed, 16 columns x 32 dims, integer bf16) and 16 lanes turn their row of the
+// exact fp32 result into the record (lid_decide_v3). Same records as LangidModel on the host.
+constexpr int kLidTile = 16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void lid_add_emb32(const int8_t* __restrict__ E, uint32_t g, int32_t* acc) {
+  const uint4* r = (const uint4*)(E + (size_t)g * kLidDim);
+  const uint4 w0 = r[0], w1 = r[1];
+  const uint32_t v[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[4 * j + k] += (int32_t)(int8_t)(uint8_t)(v[j] >> (8 * k));
+  }
+}
+
+// Butterfly step: the lanes whose bit `m` is set keep the upper half of the n values, the others
+// the lower half; each adds its partner's copy of the half it keeps.
+template <int N>
+__device__ __forceinline__ void lid_halve(const int32_t* in, int32_t* out, bool upper, int m) {
+#pragma unroll
+  for (int j = 0; j < N / 2; ++j) {
+    const int32_t keep = upper ? in[N / 2 + j] : in[j];
+    const int32_t give = upper ? in[j] : in[N / 2 + j];
+    out[j] = keep + __shfl_xor(give, m);
+  }
+}
+
+__global__ __launch_bounds__(64 * kLidTile) void k_langid_mfma(
+    const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off, const int32_t* __restrict__ perm,
+    int32_t ndocs, DevTables tabs, const int8_t* __restrict__ E, const uint16_t* __restrict__ WT, double w_scale,
+    const float* __restrict__ bias, int64_t* rec, int32_t width, uint32_t* flags, uint64_t* prof) {
+  __shared__ __attribute__((aligned(16))) uint16_t A[kLidTile][kLidDim];
+  __shared__ float Cm[kLidTile][kLidHeadCols];
+  __shared__ int32_t ex[kLidTile];
+  __shared__ int64_t cn[kLidTile];
+  const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  const int pos = (int)blockIdx.x * kLidTile + w;
+  const int doc = pos < ndocs ? (perm ? perm[pos] : pos) : -1;
+  const uint64_t t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  if (doc >= 0) {
+    const UcdView ucd{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
+    const uint8_t* b = bytes + off[doc];
+    const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
+    // the cut: byte offset of code point kLidMaxCps (or n), by counting lead bytes per chunk
+    uint32_t lim = n;
+    if (n > (uint32_t)kLidMaxCps) {
+      uint32_t seen = 0;
+      for (uint32_t base = 0; base < n; base += 64) {
+        const uint32_t i = base + (uint32_t)lane;
+        const uint64_t m = __ballot(i < n && utf8_is_lead(b[i]));
+        const uint32_t c = (uint32_t)__popcll(m);
+        if (seen + c > (uint32_t)kLidMaxCps) {
+          uint64_t mm = m;
+          for (uint32_t k = seen; k < (uint32_t)kLidMaxCps; ++k) mm &= mm - 1;
+          lim = base + (uint32_t)__builtin_ctzll(mm);
+          break;
+        }
+        seen += c;
+      }
+    }
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    int32_t acc[kLidDim];
+#pragma unroll
+    for (int d = 0; d < kLidDim; ++d) acc[d] = 0;
+    uint32_t cnt = 0;
+    uint32_t c1 = 0, c2 = 0, c3 = 0;
+    uint8_t cur = (uint32_t)lane < lim ? b[lane] : (uint8_t)0;
+    for (uint32_t base = 0; base <= lim; base += 64) {
+      const uint32_t s = base + (uint32_t)lane;
+      const uint8_t nxt = s + 64 < lim ? b[s + 64] : (uint8_t)0;
+      const bool lead = s < lim && utf8_is_lead(cur);
+      const uint32_t l0 = lead ? (cur < 0x80u ? ((cur | 0x20u) - 'a' < 26u ? (cur | 0x20u) : 0u)
+                                              : lid_letter(ucd, b, n, s))
+                               : 0u;
+      const uint64_t M = __ballot(lead);
+      uint64_t m = M & below;
+      uint32_t lm[3];
+      bool have[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        have[k] = m != 0;
+        const int j = have[k] ? lid_top(m) : lane;
+        if (have[k]) m &= ~(1ull << j);
+        lm[k] = (uint32_t)__shfl((int)l0, j);
+      }
+      if (lead || s == lim) {
+        if (!have[0]) {
+          lm[0] = c1; lm[1] = c2; lm[2] = c3;
+        } else if (!have[1]) {
+          lm[1] = c1; lm[2] = c2;
+        } else if (!have[2]) {
+          lm[2] = c1;
+        }
+        cnt += (uint32_t)lid_grams_at(lm[2], lm[1], lm[0], l0, [&](uint32_t g) { lid_add_emb32(E, g, acc); });
+      }
+      if (M) {
+        uint64_t mm = M;
+        const int j0 = lid_top(mm);
+        mm &= ~(1ull << j0);
+        const uint32_t x0 = (uint32_t)__shfl((int)l0, j0);
+        if (!mm) {
+          c3 = c2; c2 = c1; c1 = x0;
+        } else {
+          const int j1 = lid_top(mm);
+          mm &= ~(1ull << j1);
+          const uint32_t x1 = (uint32_t)__shfl((int)l0, j1);
+          if (!mm) {
+            c3 = c1; c2 = x1; c1 = x0;
+          } else {
+            const uint32_t x2 = (uint32_t)__shfl((int)l0, lid_top(mm));
+            c3 = x2; c2 = x1; c1 = x0;
+          }
+        }
+      }
+      cur = nxt;
+    }
+    // 32 sums over 64 lanes: halve by lane bits 5..1, then pair lanes l, l ^ 1
+    int32_t v16[16], v8[8], v4[4], v2[2];
+    lid_halve<32>(acc, v16, (lane >> 5) & 1, 32);
+    lid_halve<16>(v16, v8, (lane >> 4) & 1, 16);
+    lid_halve<8>(v8, v4, (lane >> 3) & 1, 8);
+    lid_halve<4>(v4, v2, (lane >> 2) & 1, 4);
+    int32_t v1;
+    lid_halve<2>(v2, &v1, (lane >> 1) & 1, 2);
+    const int32_t S = v1 + __shfl_xor(v1, 1);
+    const int dim = (((lane >> 5) & 1) << 4) | (((lane >> 4) & 1) << 3) | (((lane >> 3) & 1) << 2) |
+                    (((lane >> 2) & 1) << 1) | ((lane >> 1) & 1);
+    for (int o = 1; o < 64; o <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, o);
+    int32_t smax = S < 0 ? -S : S;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t t = __shfl_xor(smax, o);
+      smax = t > smax ? t : smax;
+    }
+    const int e = cnt ? lid_block_exp((int64_t)smax, (int64_t)cnt) : 0;
+    if ((lane & 1) == 0) A[w][dim] = cnt ? lid_bf16_bits((float)lid_quant((int64_t)S, e, (int64_t)cnt)) : (uint16_t)0;
+    if (lane == 0) {
+      ex[w] = e;
+      cn[w] = (int64_t)cnt;
+    }
+    // dictionary-segmented scripts go to the CPU path (as k_langid_features)
+    bool dict = false;
+    for (uint32_t i = (uint32_t)lane; i < n; i += 64) {
+      if (b[i] >= 0xE0) {
+        int len;
+        dict |= (ucd.props(utf8_decode(b, i, n, &len)) & P_DICT) != 0;
+      }
+    }
+    if (__ballot(dict) && lane == 0) atomicOr(flags + doc, DOC_NEEDS_CPU);
+  } else {
+    if (lane < kLidDim) A[w][lane] = 0;
+    if (lane == 0) {
+      ex[w] = 0;
+      cn[w] = 0;
+    }
+  }
+  __syncthreads();
+  if (w == 0) {
+    // lane l: A[row l & 15][k 8 (l >> 4) .. +8), B[k 8 (l >> 4) .. +8][col l & 15] (= WT row)
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(&A[lane & 15][8 * (lane >> 4)]);
+    const bf16x8 bw = *reinterpret_cast<const bf16x8*>(WT + (lane & 15) * kLidDim + 8 * (lane >> 4));
+    f32x4 c = {0.f, 0.f, 0.f, 0.f};
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw, c, 0, 0, 0);
+    // D[row (l >> 4) * 4 + r][col l & 15]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Cm[(lane >> 4) * 4 + r][lane & 15] = c[r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const int p2 = (int)blockIdx.x * kLidTile + lane;
+    if (lane < kLidTile && p2 < ndocs) {
+      const int d2 = perm ? perm[p2] : p2;
+      double C[kLidLangs];
+#pragma unroll
+      for (int l = 0; l < kLidLangs; ++l) C[l] = (double)Cm[lane][l];
+      lid_decide_v3(C, ex[lane], cn[lane], w_scale, bias, rec + (int64_t)d2 * width);
+    }
+  }
+  if (prof && doc >= 0 && lane == 0) prof[(size_t)doc * kPhaseSlots + PH_LID] += __builtin_amdgcn_s_memtime() - t0;
 }
 
 __global__ __launch_bounds__(64) void k_c4_pass_a(
@@ -709,6 +901,20 @@ int tb_langid_features(hipStream_t stream, const uint8_t* bytes, const int64_t* 
   return (int)hipGetLastError();
 }
 
+// k_langid_mfma: records of every document (perm order, 16 per workgroup); E int8 [buckets * 32],
+// WT bf16 bits [16 * 32] (the head transposed, columns >= 5 zero), bias float [8].
+int tb_langid_mfma(hipStream_t stream, const uint8_t* bytes, const int64_t* off, const int32_t* perm, int32_t ndocs,
+                   const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, const int8_t* E,
+                   const uint16_t* WT, double w_scale, const float* bias, int64_t* rec, int32_t width,
+                   uint32_t* flags, uint64_t* prof) {
+  if (ndocs <= 0) return 0;
+  if (!E || !WT || !bias || !rec || width < 2 || !(w_scale > 0)) return (int)hipErrorInvalidValue;
+  DevTables t{s1, s2, l1, l2};
+  hipLaunchKernelGGL(k_langid_mfma, dim3((ndocs + kLidTile - 1) / kLidTile), dim3(64 * kLidTile), 0, stream, bytes,
+                     off, perm, ndocs, t, E, WT, w_scale, bias, rec, width, flags, prof);
+  return (int)hipGetLastError();
+}
+
 int tb_c4_pass_a(hipStream_t stream, const void* c4, const uint8_t* bytes, const int64_t* off, const int32_t* perm,
                  int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n,
                  const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
@@ -785,7 +991,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 
 int tb_phase_slots() { return kPhaseSlots; }
 
-int tb_abi_version() { return 11; }
+int tb_abi_version() { return 12; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

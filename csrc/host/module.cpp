@@ -471,6 +471,7 @@ PYBIND11_MODULE(_tbhost, m) {
   // ---- language id (CPU) ----
   py::class_<LangidModel, std::shared_ptr<LangidModel>>(m, "LangidModel")
       .def(py::init([](py::array_t<int16_t, py::array::c_style> P, py::array_t<float, py::array::c_style> b) {
+        // v2: folded int16 logit table
         auto mdl = std::make_shared<LangidModel>();
         if ((size_t)P.size() != (size_t)kLidBuckets * kLidRow) throw std::invalid_argument("P shape");
         if ((size_t)b.size() != (size_t)kLidRow) throw std::invalid_argument("b shape");
@@ -478,16 +479,43 @@ PYBIND11_MODULE(_tbhost, m) {
         mdl->b.assign(b.data(), b.data() + b.size());
         return mdl;
       }))
+      .def(py::init([](py::array_t<int8_t, py::array::c_style> E, py::array_t<int16_t, py::array::c_style> W,
+                       double w_scale, py::array_t<float, py::array::c_style> b) {
+        // v3: int8 embedding rows + integer head (the MFMA tile's operands)
+        auto mdl = std::make_shared<LangidModel>();
+        if ((size_t)E.size() != (size_t)kLidBuckets * kLidDim) throw std::invalid_argument("E shape");
+        if ((size_t)W.size() != (size_t)kLidDim * kLidLangs) throw std::invalid_argument("W shape");
+        if ((size_t)b.size() != (size_t)kLidRow) throw std::invalid_argument("b shape");
+        for (py::ssize_t i = 0; i < W.size(); ++i)
+          if (W.data()[i] > kLidQMax || W.data()[i] < -kLidQMax) throw std::invalid_argument("W out of range");
+        if (!(w_scale > 0)) throw std::invalid_argument("w_scale must be > 0");
+        mdl->version = 3;
+        mdl->E.assign(E.data(), E.data() + E.size());
+        mdl->W.assign(W.data(), W.data() + W.size());
+        mdl->w_scale = w_scale;
+        mdl->b.assign(b.data(), b.data() + b.size());
+        return mdl;
+      }))
+      .def_readonly("version", &LangidModel::version)
       .def("detect", [](const LangidModel& mdl, const std::string& s) {
         double conf = 0;
         int l = mdl.detect(s, &conf);
         return py::make_tuple(l, conf);
       })
       .def("sums", [](const LangidModel& mdl, const std::string& s) {
-        std::vector<int64_t> v(kLidLangs, 0);
+        std::vector<int64_t> v(mdl.sum_width(), 0);
         const int64_t c = mdl.sums(s, v.data());
         return py::make_tuple(c, v);
+      })
+      .def("record", [](const LangidModel& mdl, const std::vector<int64_t>& sums, int64_t cnt) {
+        if ((int)sums.size() != mdl.sum_width()) throw std::invalid_argument("sums width");
+        int64_t r[2];
+        mdl.record(sums.data(), cnt, r);
+        double conf;
+        std::memcpy(&conf, &r[1], sizeof(double));
+        return py::make_tuple(r[0], conf);
       });
+  m.def("lid_exp", [](double x) { return lid_exp(x); });
   m.def("langid_buckets", [](const std::string& s) {
     // The hashed n-gram bucket ids of `s` (training-time featurizer, identical to the model's).
     std::vector<uint32_t> out;
@@ -514,6 +542,8 @@ PYBIND11_MODULE(_tbhost, m) {
   m.attr("LID_LANGS") = kLidLangs;
   m.attr("LID_BUCKETS") = kLidBuckets;
   m.attr("LID_SCALE") = kLidScale;
+  m.attr("LID_DIM") = kLidDim;
+  m.attr("LID_QMAX") = kLidQMax;
 
   py::class_<StdRng>(m, "StdRng")
       .def(py::init<uint64_t>())

@@ -118,14 +118,16 @@ int64_t LangidModel::sums(std::string_view text, int64_t* out) const {
   const uint8_t* b8 = (const uint8_t*)text.data();
   const uint32_t n = (uint32_t)text.size();
   const UcdView& u = host_ucd();
-  int32_t part[kLidLangs] = {0};
-  for (int l = 0; l < kLidLangs; ++l) out[l] = 0;
+  const int D = sum_width();
+  int32_t part[kLidDim] = {0};
+  for (int l = 0; l < D; ++l) out[l] = 0;
   int64_t cnt = 0;
   uint32_t lm3 = 0, lm2 = 0, lm1 = 0;
   int ncp = 0;
   auto emit = [&](uint32_t g) {
-    lid_add_row(P.data(), g, part);
-    for (int l = 0; l < kLidLangs; ++l) { out[l] += part[l]; part[l] = 0; }
+    if (version == 3) lid_add_emb(E.data(), g, part);
+    else lid_add_row(P.data(), g, part);
+    for (int l = 0; l < D; ++l) { out[l] += part[l]; part[l] = 0; }
   };
   uint32_t i = 0;
   for (; i < n && ncp < kLidMaxCps; ++ncp) {
@@ -143,11 +145,16 @@ int64_t LangidModel::sums(std::string_view text, int64_t* out) const {
   return cnt;
 }
 
+void LangidModel::record(const int64_t* s, int64_t cnt, int64_t* r) const {
+  if (version == 3) lid_record_v3(s, cnt, tables(), r);
+  else lid_decide(s, cnt, b.data(), r);
+}
+
 int LangidModel::detect(std::string_view text, double* conf) const {
-  int64_t s[kLidLangs];
+  int64_t s[kLidDim];
   const int64_t cnt = sums(text, s);
   int64_t r[2];
-  lid_decide(s, cnt, b.data(), r);
+  record(s, cnt, r);
   std::memcpy(conf, &r[1], sizeof(double));
   return (int)r[0];
 }

@@ -27,13 +27,29 @@ void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t, int
 void parallel_tasks(int64_t ntasks, int nthreads, const std::function<void(int64_t)>& fn);
 
 struct LangidModel {
-  std::vector<int16_t> P;  // [kLidBuckets * kLidRow] fixed-point logit rows (csrc/common/langid.h)
+  int version = 2;         // 2: folded int16 logit table (P); 3: int8 embeddings + MFMA head (E, W)
+  std::vector<int16_t> P;  // v2: [kLidBuckets * kLidRow] fixed-point logit rows (csrc/common/langid.h)
   std::vector<float> b;    // [kLidRow]
+  std::vector<int8_t> E;   // v3: [kLidBuckets * kLidDim] embedding rows
+  std::vector<int16_t> W;  // v3: [kLidDim * kLidLangs] integer head
+  double w_scale = 0;      // v3
   // Detect the language of `text`: returns lang index or -1, confidence in *conf.
   int detect(std::string_view text, double* conf) const;
-  // Exact per-language sums of the text's n-gram rows (out[kLidLangs]); returns the n-gram count.
+  // Exact sums of the text's n-gram rows (out[sum_width()]: v2 per-language sums, v3 embedding
+  // dims); returns the n-gram count.
   int64_t sums(std::string_view text, int64_t* out) const;
-  LidTables tables() const { return LidTables{P.data(), b.data()}; }
+  int sum_width() const { return version == 3 ? kLidDim : kLidLangs; }
+  // The language record (r[0] language or -1, r[1] confidence bits) from sums() output.
+  void record(const int64_t* s, int64_t cnt, int64_t* r) const;
+  LidTables tables() const {
+    LidTables t{version == 2 ? P.data() : nullptr, b.data()};
+    if (version == 3) {
+      t.E = E.data();
+      t.W = W.data();
+      t.w_scale = w_scale;
+    }
+    return t;
+  }
 };
 
 // C4 bad-words matcher for one language (reference c4_filters.rs:298-551).

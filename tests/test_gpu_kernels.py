@@ -9,6 +9,7 @@ import pytest
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from adversarial import adversarial_corpus  # noqa: E402
 
+from textblaster_amd import native
 from textblaster_amd.config import load_pipeline_config
 from textblaster_amd.utils import synth
 
@@ -125,25 +126,74 @@ def _langid_records(runner, res, n):
 
 
 def _assert_langid_equal(texts, r, m):
-    """Device language records == the host model (csrc/common/langid.h): same language, and the
-    confidence from the same exact sums (the f64 softmax may differ in the last ulp of exp)."""
+    """Device language records == the host model (csrc/common/langid.h): same language and the
+    same confidence bits (exact sums / exact MFMA integers, explicit-fma exp on both sides)."""
     bad = []
     for i, t in enumerate(texts):
         lang, conf = m.detect(t)
         got = float(np.frombuffer(np.int64(r[i, 1]).tobytes(), np.float64)[0]) if r[i, 0] >= 0 else 0.0
-        if int(r[i, 0]) != lang or abs(got - conf) > 1e-12:
+        if int(r[i, 0]) != lang or got != conf:
             bad.append((i, int(r[i, 0]), lang, got, conf))
     assert not bad, bad[:5]
 
 
 def test_langid_records_match_host(host, corpus, runner_parts):
-    """k_langid_features (one 16-byte int16 row gather per n-gram, shuffle-chained letters) vs.
-    the host model on the corpus: same n-gram sums, so the same language and confidence."""
+    """k_langid_mfma (v3: int8 embedding bag, bf16 MFMA head over 16-document tiles) vs. the host
+    model on the corpus: same exact sums and head integers, so the same language and confidence."""
     _, _, _, runner, lid = runner_parts
-    texts = corpus[:512]
+    assert lid.version == 3 and runner.lid_version == 3
+    texts = corpus[:517]  # not a multiple of the 16-document tile
     data, off = synth.pack(texts)
     res = runner.run(data, off)
     _assert_langid_equal(texts, _langid_records(runner, res, len(texts)), lid.native())
+
+
+def test_langid_mfma_head_vs_fp32_reference(host, corpus, runner_parts):
+    """The device's MFMA head vs. plain fp32 inference of the same fastText model in PyTorch
+    (mean of the gathered int8 rows in fp32, fp32 head, softmax): logits agree within the
+    doc vector's 8-bit quantisation, the argmax is the same away from near-ties."""
+    import torch
+
+    _, _, _, runner, lid = runner_parts
+    h = native.host()
+    texts = corpus[:300]
+    data, off = synth.pack(texts)
+    res = runner.run(data, off)
+    r = _langid_records(runner, res, len(texts))
+    E = torch.from_numpy(lid.E.reshape(h.LID_BUCKETS, h.LID_DIM).astype(np.float32))
+    W = torch.from_numpy(lid.W.reshape(h.LID_DIM, h.LID_LANGS).astype(np.float32)) * float(lid.w_scale)
+    b = torch.from_numpy(lid.b[:h.LID_LANGS].astype(np.float32))
+    near = 0
+    for i, t in enumerate(texts):
+        g = torch.tensor(h.langid_buckets(t), dtype=torch.int64)
+        if len(g) == 0:
+            assert r[i, 0] == -1
+            continue
+        logits = E[g].mean(0) @ W + b
+        p = torch.softmax(logits, 0)
+        top2 = torch.topk(logits, 2).values
+        got = float(np.frombuffer(np.int64(r[i, 1]).tobytes(), np.float64)[0])
+        if int(r[i, 0]) != int(torch.argmax(logits)):
+            assert float(top2[0] - top2[1]) < 0.05
+            near += 1
+            continue
+        assert abs(got - float(p.max())) < 0.01 * float(p.max()), (i, got, float(p.max()))
+    assert near <= 2
+
+
+def test_langid_v2_table_records_match_host(host, corpus, runner_parts):
+    """The opt-in v2 model (folded int16 table, k_langid_features) still runs and matches."""
+    from textblaster_amd.models.langid import TABLE_WEIGHTS, load
+    from textblaster_amd.pipeline.device import DeviceRunner
+
+    cfg, steps, plan, _, _ = runner_parts
+    lid2 = load(TABLE_WEIGHTS)
+    runner = DeviceRunner(steps, plan, "cuda:0", lid2)
+    assert runner.lid_version == 2
+    texts = corpus[:256]
+    data, off = synth.pack(texts)
+    res = runner.run(data, off)
+    _assert_langid_equal(texts, _langid_records(runner, res, len(texts)), lid2.native())
 
 
 def test_langid_edge_cases_bit_exact(host, runner_parts):

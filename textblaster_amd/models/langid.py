@@ -1,15 +1,22 @@
 """Language identification model (stands in for lingua; reference language_filter.rs:35-93).
 
-Architecture (csrc/common/langid.h): hashed character 1..4-grams of lowercased letter runs ->
-per bucket an int16 row of fixed-point logit contributions to {English, Danish, Swedish,
-Nynorsk, Bokmal} (P[65536, 8], 5 used, scale 1/1024) -> logits = sum of the document's rows /
-#grams / 1024 + b -> softmax; the confidence is the top probability. The sums are exact integers,
-so the device kernel (k_langid_features: one 16-byte gather per n-gram) and the CPU path agree
-bit for bit. This is a fastText-style mean-of-embeddings model with its linear head folded into
-the table ((mean E) W = mean (E W)); tools/train_langid.py trains the folded table directly.
+Two models share one featurizer: hashed character 1..4-grams of lowercased letter runs
+(csrc/common/langid.h), 65536 buckets.
 
-Weights are produced offline by ``tools/train_langid.py`` from the text in
-``models/data/langid_corpus`` and stored as a plain ``.npz`` (loaded with allow_pickle=False).
+* **v3 (default, ``langid_v3.npz``)**: fastText. Each bucket holds an int8 embedding row of
+  D = 32 dims; a document's rows are summed exactly, the mean doc vector is quantised to
+  integers |a| <= 255 with one exponent per document (block floating point: exact in bf16), and
+  the 32 -> 5 linear head runs on the matrix cores as ``v_mfma_f32_16x16x32_bf16`` tiles of 16
+  documents (k_langid_mfma) with integer bf16 weights. Every product and partial sum is an
+  integer below 2^24, so the MFMA's fp32 output is exact and the CPU path computes the same
+  records bit for bit.
+* **v2 (opt-in, ``langid_v2.npz``)**: the head folded into the table, P[bucket] = int16 logit
+  contributions (scale 1/1024): logits = mean of the document's rows + b
+  (k_langid_features: one 16-byte gather per n-gram, no matrix-core work).
+
+Softmax over {English, Danish, Swedish, Nynorsk, Bokmal}; the confidence is the top probability.
+Weights are produced offline by ``tools/train_langid.py`` from ``models/data/langid_corpus`` and
+stored as plain ``.npz`` files (loaded with allow_pickle=False).
 """
 from __future__ import annotations
 
@@ -22,20 +29,44 @@ import numpy as np
 from .. import native
 
 DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
-DEFAULT_WEIGHTS = os.path.join(DATA_DIR, "langid_v2.npz")
+DEFAULT_WEIGHTS = os.path.join(DATA_DIR, "langid_v3.npz")
+TABLE_WEIGHTS = os.path.join(DATA_DIR, "langid_v2.npz")
 LANGS = ("eng", "dan", "swe", "nno", "nob")
 NAMES = ("English", "Danish", "Swedish", "Nynorsk", "Bokmal")
+QMAX = 255  # |integer| of the v3 doc vectors and head weights: exact in bf16
 
 
 @dataclasses.dataclass
 class LangidWeights:
-    P: np.ndarray  # int16 [BUCKETS * ROW] fixed-point logit rows
-    b: np.ndarray  # float32 [ROW]
+    b: np.ndarray                      # float32 [8] bias
+    P: Optional[np.ndarray] = None     # v2: int16 [BUCKETS * ROW] fixed-point logit rows
+    E: Optional[np.ndarray] = None     # v3: int8 [BUCKETS * DIM] embedding rows
+    W: Optional[np.ndarray] = None     # v3: int16 [DIM * LANGS] integer head, |W| <= 255
+    w_scale: float = 0.0               # v3: logit units per head unit
     _native: Optional[object] = None
+
+    @property
+    def version(self) -> int:
+        return 3 if self.E is not None else 2
+
+    @property
+    def description(self) -> str:
+        if self.version == 3:
+            return "fastText int8 EmbeddingBag(65536x32) -> bf16 MFMA head (v_mfma_f32_16x16x32_bf16)"
+        return "hashed 1-4-gram int16 logit table"
+
+    @property
+    def dtype(self) -> str:
+        """Compute dtype of the model's math on the device (bench.py reports it)."""
+        return "bf16" if self.version == 3 else "int16"
 
     def native(self):
         if self._native is None:
-            self._native = native.host().LangidModel(self.P, self.b)
+            h = native.host()
+            if self.version == 3:
+                self._native = h.LangidModel(self.E, self.W, float(self.w_scale), self.b)
+            else:
+                self._native = h.LangidModel(self.P, self.b)
         return self._native
 
     def detect(self, text: str):
@@ -43,19 +74,51 @@ class LangidWeights:
         lang, conf = self.native().detect(text)
         return (NAMES[lang], conf) if lang >= 0 else (None, 0.0)
 
+    def head_bf16_t(self) -> np.ndarray:
+        """v3 head as the MFMA B operand: uint16 bf16 bits [16 columns][32 dims] (W transposed,
+        languages zero-padded to 16 columns; the integers are exact in bf16)."""
+        h = native.host()
+        wt = np.zeros((16, h.LID_DIM), dtype=np.float32)
+        wt[:len(LANGS), :] = self.W.reshape(h.LID_DIM, len(LANGS)).T
+        return (wt.view(np.uint32) >> 16).astype(np.uint16)
+
+
+def quantize_v3(E: np.ndarray, W: np.ndarray, b: np.ndarray) -> dict:
+    """Float fastText weights (E [buckets, dim], W [dim, langs], b [langs]) -> the v3 arrays:
+    int8 E (per-tensor scale sE), integer W (|W| <= 255, scale sW), w_scale = sE * sW, b."""
+    h = native.host()
+    sE = float(np.abs(E).max()) / 127.0 or 1.0
+    Eq = np.clip(np.rint(E / sE), -127, 127).astype(np.int8)
+    sW = float(np.abs(W).max()) / QMAX or 1.0
+    Wq = np.clip(np.rint(W / sW), -QMAX, QMAX).astype(np.int16)
+    bb = np.zeros(h.LID_ROW, dtype=np.float32)
+    bb[:len(b)] = b
+    return {"E": Eq.reshape(-1), "W": Wq.reshape(-1), "w_scale": np.float64(sE * sW), "b": bb}
+
 
 def load(path: str) -> LangidWeights:
+    h = native.host()
     with np.load(path, allow_pickle=False) as z:
-        if "P" not in z.files or "b" not in z.files:
-            raise ValueError(f"language model {path} is not a hashed n-gram logit table (keys P, b)")
+        files = set(z.files)
+        if {"E", "W", "w_scale", "b"} <= files:
+            E = np.ascontiguousarray(z["E"], dtype=np.int8).reshape(-1)
+            W = np.ascontiguousarray(z["W"], dtype=np.int16).reshape(-1)
+            w_scale = float(np.asarray(z["w_scale"]).reshape(()))
+            b = np.ascontiguousarray(z["b"], dtype=np.float32).reshape(-1)
+            if E.size != h.LID_BUCKETS * h.LID_DIM or W.size != h.LID_DIM * h.LID_LANGS or b.size != h.LID_ROW:
+                raise ValueError(f"language model {path} has the wrong shape")
+            if np.any(np.abs(W.astype(np.int32)) > QMAX) or not w_scale > 0:
+                raise ValueError(f"language model {path}: head out of range")
+            return LangidWeights(b=b, E=E, W=W, w_scale=w_scale)
+        if not {"P", "b"} <= files:
+            raise ValueError(f"language model {path} is neither a v3 (E, W, w_scale, b) nor a v2 (P, b) model")
         P = np.ascontiguousarray(z["P"], dtype=np.int16).reshape(-1)
         b = np.ascontiguousarray(z["b"], dtype=np.float32).reshape(-1)
-    h = native.host()
     if P.size != h.LID_BUCKETS * h.LID_ROW or b.size != h.LID_ROW:
         raise ValueError(f"language model {path} has the wrong shape")
     if np.any(P.reshape(-1, h.LID_ROW)[:, h.LID_LANGS:] != 0):
         raise ValueError(f"language model {path}: padding columns must be zero")
-    return LangidWeights(P, b)
+    return LangidWeights(b=b, P=P)
 
 
 _default: Optional[LangidWeights] = None
@@ -65,6 +128,8 @@ def load_default() -> LangidWeights:
     global _default
     if _default is None:
         path = os.environ.get("TB_LANGID_MODEL", DEFAULT_WEIGHTS)
+        if path == "table":
+            path = TABLE_WEIGHTS
         if not os.path.exists(path):
             raise FileNotFoundError(
                 f"language-id weights not found at {path}; run `python tools/train_langid.py`")

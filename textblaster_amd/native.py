@@ -3,8 +3,9 @@
 * ``_tbhost`` — pybind11 extension (g++): text primitives, the CPU pipeline, batch resolver,
   output assembly, HTML decoding, device-plan building and the host emulation of the device
   algorithms. Links ICU4C (the segmentation oracle).
-* ``libtbhip.so`` — HIP kernels for gfx950 (hipcc), C ABI, loaded with ctypes. Device memory
-  and streams come from PyTorch-ROCm; the library only launches kernels on the given stream.
+* ``libtbhip.so`` — HIP kernels for gfx950 (hipcc), C ABI, loaded with ctypes, plus the native
+  HIP runtime layer (csrc/hip/runtime.hip: caching device / pinned allocators, streams, events,
+  scans) that owns device memory and streams; PyTorch is only used for torch.distributed.
 
 Both are built in-tree (``textblaster_amd/``) so they travel with the repository snapshot.
 """
@@ -106,7 +107,8 @@ def build_hip(verbose: bool = False, force: bool = False) -> str:
             and os.path.getmtime(HIP_LIB) >= _newest(srcs + hdrs)):
         return HIP_LIB
     os.makedirs(os.path.join(BUILD_DIR, "hip"), exist_ok=True)
-    # no -ffast-math: the fixed-point -> f32 -> bf16 conversions must match the host bit for bit
+    # no -ffast-math: the language-id decision (langid.h: explicit-fma exp, IEEE f64 division) and
+    # the exact integer / bf16 MFMA paths must match the host bit for bit
     flags = [f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-fPIC", "-fno-gpu-rdc"]
     objs = []
 

@@ -529,13 +529,22 @@ class DeviceRunner:
             self.c4_ts = {i: self._to_dev(h.build_c4(steps_native[i])) for i in plan.c4_steps}
             self.has_lid = any(steps_native[i].kind == h.StepKind.LanguageDetection
                                for st in plan.stages for i in st)
-            self.lid_P = self.lid_b = None
+            self.lid_P = self.lid_b = self.lid_E = self.lid_WT = None
+            self.lid_version = 0
+            self.lid_w_scale = 0.0
             if self.has_lid:
                 if langid is None:
                     raise DeviceError("LanguageDetectionFilter needs a language-id model")
-                # int16 logit rows of the hashed n-grams (1 MB, L2-resident) and the bias
-                self.lid_P = hiprt.to_device(np.ascontiguousarray(langid.P, dtype=np.int16))
+                self.lid_version = langid.version
                 self.lid_b = hiprt.to_device(np.ascontiguousarray(langid.b, dtype=np.float32))
+                if langid.version == 3:
+                    # v3: int8 embedding rows (2 MB, L2-resident) + the bf16 MFMA head operand
+                    self.lid_E = hiprt.to_device(np.ascontiguousarray(langid.E, dtype=np.int8))
+                    self.lid_WT = hiprt.to_device(np.ascontiguousarray(langid.head_bf16_t()).reshape(-1))
+                    self.lid_w_scale = float(langid.w_scale)
+                else:
+                    # v2: int16 logit rows of the hashed n-grams (1 MB, L2-resident)
+                    self.lid_P = hiprt.to_device(np.ascontiguousarray(langid.P, dtype=np.int16))
             self.c4_growth = int(h.C4_MAX_GROWTH)
             # TB_GATE=0 disables step gating (every pass runs over every document)
             self.gating = os.environ.get("TB_GATE", "1") not in ("", "0")
@@ -710,6 +719,16 @@ class DeviceRunner:
             out.append(dev[o:o + a.nbytes].view(a.dtype) if a.nbytes else dev[o:o].view(a.dtype))
         return out, dev
 
+    def _langid(self, vb, vo, d_perm, ndocs, scratch, d_soff, rec, width, flags, prof):
+        """Language-id records of a content version: k_langid_mfma (v3: embedding bag + bf16 MFMA
+        head) or k_langid_features (v2: folded logit table)."""
+        if self.lid_version == 3:
+            self.k.langid_mfma(vb, vo, d_perm, ndocs, self.lid_E, self.lid_WT, self.lid_w_scale, self.lid_b, rec,
+                               width, flags, prof)
+        else:
+            self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_P, self.lid_b, rec, width, flags,
+                                   self.lds_bytes_lid, prof)
+
     def _scratch_for(self, slot: _Slot, nbytes: int, which: str = "stage"):
         attr = "scratch" if which == "stage" else "scratch_c4"
         cur = getattr(slot, attr)
@@ -862,9 +881,8 @@ class DeviceRunner:
                     with rt.stream(slot.s_lid):
                         with self._ktimed(keep, "langid_features"):
                             for width, prefix in lid_at:
-                                self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_P, self.lid_b,
-                                                       rec[prefix * ndocs:], width, flags, self.lds_bytes_lid,
-                                                       self._prof_buf(ndocs, keep, f"langid{s}"))
+                                self._langid(vb, vo, d_perm, ndocs, scratch, d_soff, rec[prefix * ndocs:], width,
+                                             flags, self._prof_buf(ndocs, keep, f"langid{s}"))
                         if pass_idx in self.gate_ts:
                             self.k.gate(self.gate_ts[pass_idx], [rec], ndocs, flags, dead, pass_idx + 1, 0,
                                         self.gate_need[pass_idx])
@@ -912,9 +930,8 @@ class DeviceRunner:
                     slot.s_lid.wait_event(ev_pre)
                     with rt.stream(slot.s_lid), self._ktimed(keep, "langid_features"):
                         for width, prefix in lid_at:
-                            self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_P, self.lid_b,
-                                                   rec[prefix * ndocs:], width, flags, self.lds_bytes_lid,
-                                                   self._prof_buf(ndocs, keep, f"langid{s}"))
+                            self._langid(vb, vo, d_perm, ndocs, scratch, d_soff, rec[prefix * ndocs:], width,
+                                         flags, self._prof_buf(ndocs, keep, f"langid{s}"))
                         ev_lid = self._record(slot.s_lid)
                         keep.append(ev_lid)
                 if n_mid > n_long:

@@ -52,11 +52,11 @@ def main():
     span = iv[-1][1] - iv[0][0] if iv else 0
     print(f"\nGPU busy (union of kernel intervals): {busy / 1e6:.2f} ms over a {span / 1e6:.2f} ms trace "
           f"({100 * busy / max(1, span):.0f} %)")
-    nstage = sum(1 for _, _, k in iv if k.startswith("k_langid_features"))
+    nstage = sum(1 for _, _, k in iv if k.startswith("k_langid"))
     if nstage:
         print(f"steps in trace (langid launches): {nstage}; GPU busy per step: {busy / nstage / 1e6:.2f} ms")
         # per-step timeline: a step starts at its langid launch; busy = union of kernel time until the next
-        starts = [a for a, _, k in iv if k.startswith("k_langid_features")]
+        starts = [a for a, _, k in iv if k.startswith("k_langid")]
         print(f"\n{'step':>4} {'start ms':>10} {'gap ms':>8} {'busy ms':>8} {'kernels':>8}")
         for j, s0 in enumerate(starts):
             s1 = starts[j + 1] if j + 1 < len(starts) else iv[-1][1] + 1

@@ -1,6 +1,7 @@
 """End-to-end on the MI355X: Parquet -> device pipeline -> Parquet must equal the CPU ICU-oracle
-run byte for byte (kept/excluded rows, rewritten text, metadata JSON), except for documents whose
-language-id decision is an exact bf16 near-tie (none in this corpus). Needs an MI355X."""
+run byte for byte (kept/excluded rows, rewritten text, metadata JSON including the language
+confidence: the MFMA head's integers are exact and both sides share one explicit-fma exp).
+Needs an MI355X."""
 import os
 
 import pyarrow.parquet as pq
@@ -37,18 +38,12 @@ def test_device_run_equals_cpu_oracle(tmp_path):
     assert sg.step_filtered == sc.step_filtered
     assert og.column("id").equals(oc.column("id")) and og.column("text").equals(oc.column("text"))
     assert eg.column("id").equals(ec.column("id")) and eg.column("text").equals(ec.column("text"))
-    # metadata carries the language confidence; fp32 head rounding may differ in the last digits
+    # metadata (with the language confidence) identical, key order aside
     import json
 
     for a, b in zip(og.column("metadata").to_pylist() + eg.column("metadata").to_pylist(),
                     oc.column("metadata").to_pylist() + ec.column("metadata").to_pylist()):
-        ja, jb = json.loads(a), json.loads(b)
-        assert ja.keys() == jb.keys()
-        for k in ja:
-            if k == "Detected language confidence":
-                assert abs(float(ja[k]) - float(jb[k])) < 1e-5
-            else:
-                assert ja[k] == jb[k]
+        assert json.loads(a) == json.loads(b)
 
 
 def test_device_fault_recovery(tmp_path):
@@ -152,12 +147,7 @@ def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
     np.testing.assert_array_equal(a.status, b.status)
     np.testing.assert_array_equal(a.fail_step, b.fail_step)
     assert a.reasons.keys() == b.reasons.keys()
-    for k, ra in a.reasons.items():
-        rb = b.reasons[k]
-        if ra != rb:  # the language confidence in the message (f64 exp on the device vs the host)
-            pa, pb = ra.split(": ", 1), rb.split(": ", 1)
-            assert pa[0] == pb[0] == "Language detection confidence is not satified", (ra, rb)
-            assert abs(float(pa[1].split()[0]) - float(pb[1].split()[0])) < 1e-5, (ra, rb)
+    assert a.reasons == b.reasons  # confidences included (same exp bits on both sides)
     oa, ob = outputs(a), outputs(b)
     assert oa.keys() == ob.keys()
     bad = []
@@ -166,12 +156,8 @@ def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
         if ka != kb or ta != tb or (ma is None) != (mb is None):
             bad.append(k)
             continue
-        if ma is not None:
-            ja, jb = json.loads(ma), json.loads(mb)
-            if ja.keys() != jb.keys() or any(
-                    abs(float(ja[f]) - float(jb[f])) >= 1e-5 if f == "Detected language confidence" else ja[f] != jb[f]
-                    for f in ja):
-                bad.append(k)
+        if ma is not None and json.loads(ma) != json.loads(mb):
+            bad.append(k)
     assert not bad, [(k, texts[k][:80]) for k in bad[:5]]
     lens = np.diff(off)
     assert np.count_nonzero(lens > 4500) >= 30

@@ -204,7 +204,8 @@ def run_cmd(args, argv: List[str]) -> int:
     if not under_launcher and ngpu > 1:
         from .parallel.launch import strip_flag
 
-        if args.backend != "cpu" and args.gpus is not None and _visible_gpus() < ngpu:
+        shared = os.environ.get("TB_SHARED_GPU", "") not in ("", "0")  # all ranks on GPU 0 (dist.py)
+        if args.backend != "cpu" and args.gpus is not None and _visible_gpus() < ngpu and not shared:
             print(f"Error: --gpus {ngpu} requested but only {_visible_gpus()} GPU(s) are visible", file=sys.stderr)
             return 2
         # strip --gpus so the children do not relaunch

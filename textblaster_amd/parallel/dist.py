@@ -137,6 +137,24 @@ class PendingReduce:
         return self.tensor
 
 
+def _hip_initialised() -> bool:
+    """Has this process already loaded (and so initialised) the native HIP runtime layer?"""
+    import sys
+
+    from .. import native
+
+    return getattr(native, "_hip", None) is not None or "torch" in sys.modules and _torch_hip_initialised()
+
+
+def _torch_hip_initialised() -> bool:
+    try:
+        import torch
+
+        return bool(torch.cuda.is_initialized())
+    except Exception:  # noqa: BLE001
+        return False
+
+
 def init_from_env(backend: str = "nccl", force_pg: Optional[bool] = None) -> DistContext:
     """Initialise from torchrun's env (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT).
 
@@ -151,37 +169,53 @@ def init_from_env(backend: str = "nccl", force_pg: Optional[bool] = None) -> Dis
     if force_pg is None:
         force_pg = os.environ.get("TB_FORCE_PG", "") not in ("", "0")
     ctx = DistContext(rank, world, local)
+    # TB_SHARED_GPU=1: every rank runs its engine on GPU 0 (functional multi-rank runs of the
+    # device path on a one-GPU box); the group then uses gloo, since RCCL needs one GPU per rank.
+    # TB_DIST_BACKEND overrides the process-group backend either way.
+    shared = os.environ.get("TB_SHARED_GPU", "") not in ("", "0")
+    pg_backend = os.environ.get("TB_DIST_BACKEND") or ("gloo" if shared else backend)
+    if pg_backend not in ("nccl", "gloo"):
+        raise ValueError(f"TB_DIST_BACKEND must be nccl or gloo, not {pg_backend!r}")
     if backend == "nccl":
-        ctx.device = f"cuda:{local}"
+        ctx.device = f"cuda:{0 if shared else local}"
     if world > 1 or force_pg:
         import datetime
 
         import torch
         import torch.distributed as td
 
-        if backend == "nccl":
+        if pg_backend == "nccl":
             # RCCL and torch add their own streams next to the engine's eight; with the box's
             # default of 4 hardware queues per process they land behind document kernels on a
             # shared queue (measured: a one-rank group with no collective at all took the
-            # 1-GPU bench from 35.6 to 47.9 ms/step; 8 queues: 37.0). Set before the first HIP
-            # call of this process (TB_PG_HW_QUEUES overrides, 0 keeps the inherited value).
-            q = os.environ.get("TB_PG_HW_QUEUES", "8")
-            if q not in ("", "0"):
-                os.environ["GPU_MAX_HW_QUEUES"] = q
+            # 1-GPU bench from 35.6 to 47.9 ms/step; 8 queues: 37.0). It only takes effect
+            # before the first HIP call of this process. An explicit TB_PG_HW_QUEUES wins (0
+            # keeps the inherited value); otherwise an operator's GPU_MAX_HW_QUEUES is kept.
+            q = os.environ.get("TB_PG_HW_QUEUES")
+            if q is not None:
+                if q not in ("", "0"):
+                    os.environ["GPU_MAX_HW_QUEUES"] = q
+            else:
+                os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+            if _hip_initialised():
+                import warnings
+
+                warnings.warn("init_from_env: the HIP runtime is already initialised in this process, so "
+                              "GPU_MAX_HW_QUEUES cannot change the hardware queue count any more")
             # the collective streams at high priority: a counter reduction is never queued
             # behind a batch's kernels
             os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
             torch.cuda.set_device(local)
         # a dead or hung peer turns into an error after this long instead of a silent hang
         kwargs = {"timeout": datetime.timedelta(seconds=float(os.environ.get("TB_COLLECTIVE_TIMEOUT", "600")))}
-        if backend == "nccl":
+        if pg_backend == "nccl":
             kwargs["device_id"] = torch.device(f"cuda:{local}")
         if world == 1:
             kwargs["store"] = td.HashStore()
         else:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        td.init_process_group(backend=backend, rank=rank, world_size=world, **kwargs)
-        ctx.backend = backend
+        td.init_process_group(backend=pg_backend, rank=rank, world_size=world, **kwargs)
+        ctx.backend = pg_backend
     return ctx
 
 

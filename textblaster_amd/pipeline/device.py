@@ -428,7 +428,7 @@ class DeviceRunner:
     # 80-VGPR budget the wider variant spills (872 B/lane) and is slower than 512 threads on ~1 MB
     # documents (profiles/r3_long: 685 vs 728 docs/s at 128 docs/step, 1081 vs 1444 at 384)
     DEFAULT_HUGE_DOC_BYTES = 0
-    DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; sweep: tools/occ_sweep.sh)
+    DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; A/B: tools/gpu.sh ab)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None, max_batch_bytes: int = 384 << 20,
                  token_counters=None):

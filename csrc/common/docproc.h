@@ -1502,6 +1502,167 @@ TB_HD constexpr uint32_t pack3(const char* p) {
 // Bits of the per-line pattern flags (c4_pass_a)
 enum : uint32_t { C4F_JS = 1, C4F_POLICY = 2 };
 
+// C4 pass A, common end: the joined kept lines Jb[0, Jtot) are trimmed and their sentences counted
+// (saturated at min_num_sentences), then the record and the rewritten text's source are written.
+template <class P>
+TB_HD void c4_finish(DocCtx<P>& x, const DevC4& c4, uint32_t n, uint8_t* Jb, uint32_t Jtot, int64_t s_long,
+                     int64_t s_punct, int64_t s_few, int64_t* r, int64_t* src) {
+  Cps jc = decode(x, Jb, Jtot);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  const uint32_t JC = jc.n;
+  const PropArr jprop = jc.props();
+  const uint32_t tcs = x.par.template min<uint32_t>(JC, JC, [&](uint32_t i) { return is_ws(jprop[i]) ? JC : i; });
+  const uint32_t tce = x.par.template max<uint32_t>(JC, 0u, [&](uint32_t i) { return is_ws(jprop[i]) ? 0u : i + 1; });
+  uint32_t nsent = 0, bstart = 0, blen = 0;
+  if (tcs < tce) {
+    const uint32_t lim = c4.min_num_sentences > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)c4.min_num_sentences;
+    nsent = count_sentences_upto(x, jc, tcs, tce, lim);
+    bstart = jc.o(tcs);
+    blen = jc.o(tce) - jc.o(tcs);
+  }
+  x.stamp(PH_C4_SENT);
+  const int64_t jrel = (int64_t)((const char*)Jb - x.scr) + bstart;
+  // The rewrite can only grow a document by one '\n' per sentence not followed by whitespace
+  // (split_paragraph=false). Bounding the growth to kC4MaxGrowth bytes lets the host size the
+  // next version's buffer (and its D2H copy) up front without a sync; the rare document that
+  // would exceed it is recomputed on the CPU path.
+  if (blen > n + kC4MaxGrowth) {
+    x.set_flag(DOC_NEEDS_CPU);
+    x.par.single([&]() { src[0] = 0; src[1] = 0; });
+    return;
+  }
+  x.par.single([&]() {
+    r[0] = 0; r[1] = 0; r[2] = s_long; r[3] = s_punct; r[4] = s_few; r[5] = nsent; r[6] = blen;
+    src[0] = jrel;
+    src[1] = blen;
+  });
+}
+
+// C4 pass A for a document with no citation to remove (every processed line is its trimmed
+// original line): the processed text Pb, the per-code-point line ids and the kept-byte prefix of
+// the general path are not built. Words come from one segmentation of the whole text — the words
+// of a trimmed line are exactly the document's words inside its span (UAX#29 always breaks
+// around a line feed, WB3a/b, and trimming only drops whitespace, which no word contains) — and
+// are assigned to lines by their first code point; the phrase search, terminal punctuation and
+// the join read the original bytes of each line's span. Same records and rewritten text as the
+// general path.
+template <class P>
+TB_HD void c4_pass_a_plain(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, const Cps& c,
+                           const uint32_t* la, const uint32_t* lb, uint32_t NLn, int64_t* r, int64_t* src) {
+  const OffArr off = c.offs();
+  uint32_t* lbs = x.template alloc_hot<uint32_t>(NLn + 1);   // line byte start (trimmed)
+  uint32_t* nw = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* mx = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* pf = x.template alloc_hot<uint32_t>(NLn + 1);   // pattern flags per line
+  uint8_t* code = x.template alloc_hot<uint8_t>(NLn + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  x.par.for_n(NLn, [&](uint32_t k) { lbs[k] = off[la[k]]; nw[k] = 0; mx[k] = 0; pf[k] = 0; });
+  x.par.single([&]() { lbs[NLn] = 0xFFFFFFFFu; });
+  x.par.sync();
+  x.stamp(PH_C4_CITE);
+  auto line_of_cp = [&](uint32_t cs) {  // last line with la <= cs
+    uint32_t lo = 0, hi = NLn;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (la[mid] <= cs) lo = mid; else hi = mid;
+    }
+    return lo;
+  };
+  auto line_of_byte = [&](uint32_t bs) {  // last line with byte start <= bs
+    uint32_t lo = 0, hi = NLn;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (lbs[mid] <= bs) lo = mid; else hi = mid;
+    }
+    return lo;
+  };
+  if (NLn > 0) {
+    const auto mw = x.mark();
+    Words wd = words(x, c);
+    if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+    x.par.for_n(wd.n, [&](uint32_t q) {
+      const uint32_t k = line_of_cp(wd.cs[q]);
+      P::add32(&nw[k], 1u);
+      P::max32(&mx[k], wd.ce[q] - wd.cs[q]);
+    });
+    x.par.sync();
+    x.reset(mw);
+  }
+  x.stamp(PH_C4_WORDS);
+  if (NLn > 0 && (c4.filter_javascript || c4.filter_policy)) {
+    const char* const kPol[6] = {"terms of use", "privacy policy", "cookie policy",
+                                 "uses cookies", "use of cookies", "use cookies"};
+    const int kPolLen[6] = {12, 14, 13, 12, 14, 11};
+    // a phrase (letters and spaces, starting with a letter) that matches at a byte lies inside
+    // one line's trimmed span: it cannot cross the line feed or run into trailing whitespace
+    x.par.for_n(n, [&](uint32_t s) {
+      uint8_t c0 = b[s];
+      if (c0 >= 'A' && c0 <= 'Z') c0 = (uint8_t)(c0 + 32);
+      if (c0 != 'j' && c0 != 't' && c0 != 'p' && c0 != 'c' && c0 != 'u') return;
+      uint32_t bits = 0;
+      const uint32_t w3 = TB_C4_PREFIX3 ? lower3(b + s, n - s) : 0u;
+      auto pre = [&](const char* pat) { return !TB_C4_PREFIX3 || w3 == pack3(pat); };
+      if (c4.filter_javascript && c0 == 'j' && pre("javascript") && ci_starts_with(b + s, n - s, "javascript", 10))
+        bits |= C4F_JS;
+      if (c4.filter_policy)
+        for (int t = 0; t < 6; ++t)
+          if (kPol[t][0] == (char)c0 && pre(kPol[t]) && ci_starts_with(b + s, n - s, kPol[t], kPolLen[t])) {
+            bits |= C4F_POLICY;
+            break;
+          }
+      if (bits) P::or32(&pf[line_of_byte(s)], bits);
+    });
+  }
+  x.par.sync();
+  x.par.for_n(NLn, [&](uint32_t k) {
+    const uint32_t s0 = off[la[k]], e0 = off[lb[k]], ln = e0 - s0;
+    uint8_t cd = 0;
+    if (c4.max_word_length > 0 && (int64_t)mx[k] > c4.max_word_length) {
+      cd = 1;
+    } else if (c4.filter_no_terminal_punct) {
+      const bool term = ln > 0 && end_punct(c.cp(lb[k] - 1));
+      const bool ell = ln >= 3 && b[e0 - 1] == '.' && b[e0 - 2] == '.' && b[e0 - 3] == '.';
+      if (!term || ell) cd = 2;
+    }
+    if (cd == 0 && c4.min_words_per_line > 0 && (int64_t)nw[k] < c4.min_words_per_line) cd = 3;
+    if (cd == 0 && c4.filter_javascript && (pf[k] & C4F_JS)) cd = 4;
+    if (cd == 0 && c4.filter_policy && (pf[k] & C4F_POLICY)) cd = 5;
+    code[k] = cd;
+  });
+  x.par.sync();
+  const uint64_t s12 = x.par.template sum<uint64_t>(NLn, [&](uint32_t k) {
+    return (uint64_t)(code[k] == 1) | ((uint64_t)(code[k] == 2) << 32);
+  });
+  const int64_t s_long = (int64_t)(s12 & 0xFFFFFFFFull), s_punct = (int64_t)(s12 >> 32);
+  const int64_t s_few = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 3); });
+  x.stamp(PH_C4_CODES);
+  // ---- joined kept lines (HBM: read back by pass B), copied byte by byte ----
+  uint32_t* joff = x.template alloc_hot<uint32_t>(NLn + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  uint32_t Jtot = x.par.template scan<uint32_t>(
+      NLn, 0u, [](uint32_t a, uint32_t b2) { return a + b2; },
+      [&](uint32_t k) { return code[k] == 0 ? off[lb[k]] - off[la[k]] + 1 : 0u; },
+      [&](uint32_t k, uint32_t e) { joff[k] = e; });
+  if (Jtot > 0) Jtot -= 1;
+  uint8_t* Jb = x.template alloc_global<uint8_t>(Jtot + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  x.par.sync();
+  if (NLn > 0) {
+    x.par.for_n(n, [&](uint32_t i) {
+      const uint32_t k = line_of_byte(i);
+      if (code[k] != 0 || i < lbs[k] || i >= off[lb[k]]) return;
+      Jb[joff[k] + (i - lbs[k])] = b[i];
+    });
+    x.par.for_n(NLn, [&](uint32_t k) {
+      const uint32_t ln = off[lb[k]] - off[la[k]];
+      if (code[k] == 0 && joff[k] + ln < Jtot) Jb[joff[k] + ln] = '\n';
+    });
+  }
+  x.par.sync();
+  x.stamp(PH_C4_JOIN);
+  c4_finish(x, c4, n, Jb, Jtot, s_long, s_punct, s_few, r, src);
+}
+
 template <class P>
 TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, int64_t* r, int64_t* src) {
   x.stamp(PH_START);
@@ -1579,6 +1740,19 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   }
   x.par.sync();
   x.stamp(PH_C4_LINES);
+  // A citation needs a '[' followed by a digit: without one (the common case) every processed
+  // line is its trimmed original line and the plain path runs on the original bytes.
+#ifndef TB_C4_PLAIN
+#define TB_C4_PLAIN 1
+#endif
+  const bool maybe_cite = c4.remove_citations != 0 &&
+      x.par.reduce_or(x.par.template sum<uint32_t>(C > 0 ? C - 1 : 0, [&](uint32_t j) {
+        return (c.lead(j) == '[' && (prop[j + 1] & P_DIGIT)) ? 1u : 0u;
+      }));
+  if (TB_C4_PLAIN && !maybe_cite) {
+    c4_pass_a_plain(x, c4, b, n, c, la, lb, NLn, r, src);
+    return;
+  }
   // ---- citation removal -> processed lines Pb (every step parallel over code points) ----
   // lid[j]: the line whose trimmed span holds code point j (kNoLine otherwise), by a max-scan
   // of line-start markers (lines are ordered and disjoint).
@@ -1752,35 +1926,7 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   });
   x.par.sync();
   x.stamp(PH_C4_JOIN);
-  Cps jc = decode(x, Jb, Jtot);
-  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
-  const uint32_t JC = jc.n;
-  const PropArr jprop = jc.props();
-  const uint32_t tcs = x.par.template min<uint32_t>(JC, JC, [&](uint32_t i) { return is_ws(jprop[i]) ? JC : i; });
-  const uint32_t tce = x.par.template max<uint32_t>(JC, 0u, [&](uint32_t i) { return is_ws(jprop[i]) ? 0u : i + 1; });
-  uint32_t nsent = 0, bstart = 0, blen = 0;
-  if (tcs < tce) {
-    const uint32_t lim = c4.min_num_sentences > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)c4.min_num_sentences;
-    nsent = count_sentences_upto(x, jc, tcs, tce, lim);
-    bstart = jc.o(tcs);
-    blen = jc.o(tce) - jc.o(tcs);
-  }
-  x.stamp(PH_C4_SENT);
-  const int64_t jrel = (int64_t)((const char*)Jb - x.scr) + bstart;
-  // The rewrite can only grow a document by one '\n' per sentence not followed by whitespace
-  // (split_paragraph=false). Bounding the growth to kC4MaxGrowth bytes lets the host size the
-  // next version's buffer (and its D2H copy) up front without a sync; the rare document that
-  // would exceed it is recomputed on the CPU path.
-  if (blen > n + kC4MaxGrowth) {
-    x.set_flag(DOC_NEEDS_CPU);
-    x.par.single([&]() { src[0] = 0; src[1] = 0; });
-    return;
-  }
-  x.par.single([&]() {
-    r[0] = 0; r[1] = 0; r[2] = s_long; r[3] = s_punct; r[4] = s_few; r[5] = nsent; r[6] = blen;
-    src[0] = jrel;
-    src[1] = blen;
-  });
+  c4_finish(x, c4, n, Jb, Jtot, s_long, s_punct, s_few, r, src);
 }
 
 // ---------------------------------------------------------------------------------------------

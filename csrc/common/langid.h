@@ -1,8 +1,11 @@
 // Character n-gram language identifier that stands in for lingua (reference
 // src/pipeline/filters/language_filter.rs:35-93; survey H5). Two models share the featurizer:
 //
-// v3 (default, "fastText + bf16 MFMA head"): every hashed n-gram bucket holds an int8 embedding
-// row of kLidDim = 32 dims; a document's rows are summed exactly (int32), the mean doc vector is
+// v3 (default, "fastText + bf16 MFMA head"): a document vector of kLidDim = 32 dims from a
+// block-sparse embedding table: the bucket's int8 row of kLidRowDim = 16 values lands in the
+// lower or upper half of the vector by the bucket's top bit (a 65536 x 32 table whose rows have
+// 16 structural zeros, stored as 65536 x 16: 16 bytes per n-gram gather). A document's rows
+// are summed exactly (int32), the mean doc vector is
 // quantised to integers |a| <= 255 with one exponent per document (block floating point, every
 // value exact in bf16), and the 32 -> 5 linear head runs as one v_mfma_f32_16x16x32_bf16 tile per
 // 16 documents with integer bf16 weights |W| <= 255. All products and partial sums are integers
@@ -33,7 +36,8 @@ constexpr int kLidMaxCps = 4096;
 constexpr int kLidMaxGrams = 4;  // n-grams emitted per code point position, at most
 constexpr uint32_t kLidBoundary = 0x20;
 constexpr double kLidScale = 1024.0;  // P = int16 / 1024 (|P| < 32)
-constexpr int kLidDim = 32;           // v3 embedding dims = the MFMA K
+constexpr int kLidDim = 32;           // v3 doc-vector dims = the MFMA K
+constexpr int kLidRowDim = 16;        // v3 stored dims per bucket (half of the doc vector)
 constexpr int kLidHeadCols = 16;      // v3 head columns (5 languages, zero padded to the MFMA N)
 constexpr int kLidQMax = 255;         // v3 doc-vector / head integers: |v| <= 255 (exact in bf16)
 
@@ -70,6 +74,27 @@ TB_HD int lid_grams_at(uint32_t lm3, uint32_t lm2, uint32_t lm1, uint32_t l0, F&
   emit(lid_hash(lm2 ? lm2 : B, lm1, B, 0, 3));
   if (!lm2) return 2;
   emit(lid_hash(lm3 ? lm3 : B, lm2, lm1, B, 4));
+  return 3;
+}
+
+// lid_grams_at with the buckets in fixed slots g[0..count) (straight-line code: no indexed
+// stores into a register array).
+TB_HD int lid_grams4(uint32_t lm3, uint32_t lm2, uint32_t lm1, uint32_t l0, uint32_t* g) {
+  const uint32_t B = kLidBoundary;
+  if (l0) {
+    g[0] = lid_hash(l0, 0, 0, 0, 1);
+    g[1] = lid_hash(lm1 ? lm1 : B, l0, 0, 0, 2);
+    if (!lm1) return 2;
+    g[2] = lid_hash(lm2 ? lm2 : B, lm1, l0, 0, 3);
+    if (!lm2) return 3;
+    g[3] = lid_hash(lm3 ? lm3 : B, lm2, lm1, l0, 4);
+    return 4;
+  }
+  if (!lm1) return 0;
+  g[0] = lid_hash(lm1, B, 0, 0, 2);
+  g[1] = lid_hash(lm2 ? lm2 : B, lm1, B, 0, 3);
+  if (!lm2) return 2;
+  g[2] = lid_hash(lm3 ? lm3 : B, lm2, lm1, B, 4);
   return 3;
 }
 
@@ -187,16 +212,20 @@ TB_HD int64_t prev_lead(const uint8_t* b, int64_t s) {
 struct LidTables {
   const int16_t* P;    // v2: [kLidBuckets * kLidRow]
   const float* bias;   // [kLidRow]
-  const int8_t* E = nullptr;   // v3: [kLidBuckets * kLidDim] int8 embedding rows
+  const int8_t* E = nullptr;   // v3: [kLidBuckets * kLidRowDim] int8 embedding rows
   const int16_t* W = nullptr;  // v3: [kLidDim * kLidLangs] integer head (|W| <= 255)
   double w_scale = 0;          // v3: logit units per head unit at e = 0
 };
 
-// Adds the int8 embedding row of bucket g to the kLidDim sums (v3).
+// Dims of the doc vector that bucket g's row feeds: [lid_half(g), lid_half(g) + 16).
+TB_HD int lid_half(uint32_t g) { return (int)(g >> (kLidBucketsLog2 - 1)) * kLidRowDim; }
+
+// Adds the int8 embedding row of bucket g to its half of the kLidDim sums (v3).
 TB_HD void lid_add_emb(const int8_t* E, uint32_t g, int32_t* acc) {
-  const int8_t* r = E + (size_t)g * kLidDim;
+  const int8_t* r = E + (size_t)g * kLidRowDim;
+  int32_t* a = acc + lid_half(g);
 #pragma unroll
-  for (int d = 0; d < kLidDim; ++d) acc[d] += r[d];
+  for (int d = 0; d < kLidRowDim; ++d) a[d] += r[d];
 }
 
 // v3 record from the exact embedding sums S[kLidDim] and the n-gram count (host reference of the

@@ -357,28 +357,58 @@ __global__ __launch_bounds__(64) void k_langid_features(
 }
 
 // Language ID v3 (csrc/common/langid.h): fastText bag + bf16 MFMA head, 16 documents per
-// workgroup (one wave each, launch positions blockIdx.x * 16 + wave). Each wave gathers the int8
-// embedding rows of its document's n-grams (two 16-byte loads per gram, the same chunked walk and
-// register letter carry as langid_coop) into 32 per-lane int32 sums, reduces them across the
-// lanes with a halving butterfly (32 shuffles: after it lane l holds dim d(l) summed over the
-// wave), quantises the mean vector with the document's block exponent (lid_block_exp /
-// lid_quant: integers |a| <= 255, exact in bf16) into the workgroup's 16 x 32 A tile in LDS.
-// Wave 0 then runs the head as one v_mfma_f32_16x16x32_bf16 (A: 16 docs x 32 dims, B: the
-// head transposed, 16 columns x 32 dims, integer bf16) and 16 lanes turn their row of the
-// exact fp32 result into the record (lid_decide_v3). Same records as LangidModel on the host.
+// 256-thread workgroup: wave w gathers documents w, w + 4, w + 8, w + 12 of the tile one after
+// another (launch positions blockIdx.x * 16 + ...; the length-sorted order keeps a tile's
+// documents alike in size). Per 64-byte chunk every lane finds the <= 4 n-grams ending at its
+// code point (the chunked walk and register letter carry of langid_coop); then the four lanes of
+// a quad share their 16 grams: lane q of the quad loads dword q of each of the 16 embedding rows
+// (16-byte rows, one dword load per row and lane: the same bytes per gram as the v2 table) and
+// adds it SWAR-style into the half of the document vector the bucket feeds (its top bit) — the
+// table holds E + 128 as unsigned bytes, even and odd bytes go to the two 16-bit halves of a
+// register (no overflow within 16 chunks: 16 x 16 x 255 < 2^16), folded into eight int32 sums
+// every 16 chunks. A short butterfly (4 shuffles) sums the lanes' slices into the document's 32
+// exact dims (minus 128 x #grams per half), which the wave quantises with the document's block
+// exponent (lid_block_exp / lid_quant: integers |a| <= 255, exact in bf16) into row r of the
+// workgroup's 16 x 32 A tile in LDS. Wave 0 then runs the head as one v_mfma_f32_16x16x32_bf16
+// (A: 16 docs x 32 dims, B: the head transposed, 16 columns x 32 dims, integer bf16) and 16 lanes
+// turn their row of the exact fp32 result into the record (lid_decide_v3). Same records as
+// LangidModel on the host.
 constexpr int kLidTile = 16;
+constexpr int kLidWaves = 4;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ void lid_add_emb32(const int8_t* __restrict__ E, uint32_t g, int32_t* acc) {
-  const uint4* r = (const uint4*)(E + (size_t)g * kLidDim);
-  const uint4 w0 = r[0], w1 = r[1];
-  const uint32_t v[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+// value of lane (quad base + src) for every lane of a quad (DPP quad_perm broadcast)
+template <int SRC>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, SRC * 0x55, 0xF, 0xF, false);
+}
+
+// adds the lane's dword of the rows g[0..k) of one quad lane into the packed sums of the half
+// each row feeds (p16[0..1]: lower half, p16[2..3]: upper half; even / odd bytes)
+__device__ __forceinline__ void lid_quad_rows(const uint8_t* __restrict__ Eb, uint32_t sub, uint32_t k,
+                                              const uint32_t* g, uint32_t* p16) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) acc[4 * j + k] += (int32_t)(int8_t)(uint8_t)(v[j] >> (8 * k));
+  for (uint32_t j = 0; j < 4; ++j) {
+    if (j < k) {
+      const uint32_t w = *(const uint32_t*)(Eb + (size_t)g[j] * kLidRowDim + 4 * sub);
+      const uint32_t ev = w & 0x00FF00FFu, od = (w >> 8) & 0x00FF00FFu;
+      const bool up = (g[j] >> (kLidBucketsLog2 - 1)) != 0;
+      p16[0] += up ? 0u : ev;
+      p16[1] += up ? 0u : od;
+      p16[2] += up ? ev : 0u;
+      p16[3] += up ? od : 0u;
+    }
   }
+}
+
+__device__ __forceinline__ void lid_fold16(uint32_t* p16, int32_t* s) {
+  // s[0..3]: dims 4 sub + 0..3 (lower half), s[4..7]: dims 16 + 4 sub + 0..3 (upper half)
+  s[0] += (int32_t)(p16[0] & 0xFFFFu); s[2] += (int32_t)(p16[0] >> 16);
+  s[1] += (int32_t)(p16[1] & 0xFFFFu); s[3] += (int32_t)(p16[1] >> 16);
+  s[4] += (int32_t)(p16[2] & 0xFFFFu); s[6] += (int32_t)(p16[2] >> 16);
+  s[5] += (int32_t)(p16[3] & 0xFFFFu); s[7] += (int32_t)(p16[3] >> 16);
+  p16[0] = p16[1] = p16[2] = p16[3] = 0;
 }
 
 // Butterfly step: the lanes whose bit `m` is set keep the upper half of the n values, the others
@@ -393,133 +423,166 @@ __device__ __forceinline__ void lid_halve(const int32_t* in, int32_t* out, bool 
   }
 }
 
-__global__ __launch_bounds__(64 * kLidTile) void k_langid_mfma(
+// One document's quantised doc vector into A row `row` (and its exponent / count).
+__device__ __forceinline__ void lid_doc_vector(const uint8_t* __restrict__ b, uint32_t n, const UcdView& ucd,
+                                               const uint8_t* __restrict__ Eb, uint32_t* flag, int lane,
+                                               uint16_t* arow, int32_t* e_out, int64_t* cnt_out) {
+  // the cut: byte offset of code point kLidMaxCps (or n), by counting lead bytes per chunk
+  uint32_t lim = n;
+  if (n > (uint32_t)kLidMaxCps) {
+    uint32_t seen = 0;
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t i = base + (uint32_t)lane;
+      const uint64_t m = __ballot(i < n && utf8_is_lead(b[i]));
+      const uint32_t c = (uint32_t)__popcll(m);
+      if (seen + c > (uint32_t)kLidMaxCps) {
+        uint64_t mm = m;
+        for (uint32_t k = seen; k < (uint32_t)kLidMaxCps; ++k) mm &= mm - 1;
+        lim = base + (uint32_t)__builtin_ctzll(mm);
+        break;
+      }
+      seen += c;
+    }
+  }
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint32_t sub = (uint32_t)lane & 3u;
+  uint32_t p16[4] = {0u, 0u, 0u, 0u};
+  int32_t s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t cnt = 0, chi = 0, chunks = 0;  // grams, grams feeding the upper half
+  uint32_t c1 = 0, c2 = 0, c3 = 0;
+  uint8_t cur = (uint32_t)lane < lim ? b[lane] : (uint8_t)0;
+  for (uint32_t base = 0; base <= lim; base += 64) {
+    const uint32_t s = base + (uint32_t)lane;
+    const uint8_t nxt = s + 64 < lim ? b[s + 64] : (uint8_t)0;
+    const bool lead = s < lim && utf8_is_lead(cur);
+    const uint32_t l0 = lead ? (cur < 0x80u ? ((cur | 0x20u) - 'a' < 26u ? (cur | 0x20u) : 0u)
+                                            : lid_letter(ucd, b, n, s))
+                             : 0u;
+    const uint64_t M = __ballot(lead);
+    uint64_t m = M & below;
+    uint32_t lm[3];
+    bool have[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      have[k] = m != 0;
+      const int j = have[k] ? lid_top(m) : lane;
+      if (have[k]) m &= ~(1ull << j);
+      lm[k] = (uint32_t)__shfl((int)l0, j);
+    }
+    uint32_t g[4] = {0u, 0u, 0u, 0u}, k = 0;
+    if (lead || s == lim) {
+      if (!have[0]) {
+        lm[0] = c1; lm[1] = c2; lm[2] = c3;
+      } else if (!have[1]) {
+        lm[1] = c1; lm[2] = c2;
+      } else if (!have[2]) {
+        lm[2] = c1;
+      }
+      k = (uint32_t)lid_grams4(lm[2], lm[1], lm[0], l0, g);
+    }
+    cnt += k;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) chi += (j < k && (g[j] >> (kLidBucketsLog2 - 1)) != 0) ? 1u : 0u;
+    if (__ballot(k != 0)) {
+      // the quad's 16 grams, each lane its 8-byte slice of every row
+      uint32_t gq[4], kq;
+#define TB_LID_SRC(SRC)                                                  \
+      kq = quad_bcast<SRC>(k);                                           \
+      gq[0] = quad_bcast<SRC>(g[0]); gq[1] = quad_bcast<SRC>(g[1]);      \
+      gq[2] = quad_bcast<SRC>(g[2]); gq[3] = quad_bcast<SRC>(g[3]);      \
+      lid_quad_rows(Eb, sub, kq, gq, p16);
+      TB_LID_SRC(0)
+      TB_LID_SRC(1)
+      TB_LID_SRC(2)
+      TB_LID_SRC(3)
+#undef TB_LID_SRC
+      if ((++chunks & 15u) == 0) lid_fold16(p16, s8);
+    }
+    if (M) {
+      uint64_t mm = M;
+      const int j0 = lid_top(mm);
+      mm &= ~(1ull << j0);
+      const uint32_t x0 = (uint32_t)__shfl((int)l0, j0);
+      if (!mm) {
+        c3 = c2; c2 = c1; c1 = x0;
+      } else {
+        const int j1 = lid_top(mm);
+        mm &= ~(1ull << j1);
+        const uint32_t x1 = (uint32_t)__shfl((int)l0, j1);
+        if (!mm) {
+          c3 = c1; c2 = x1; c1 = x0;
+        } else {
+          const uint32_t x2 = (uint32_t)__shfl((int)l0, lid_top(mm));
+          c3 = x2; c2 = x1; c1 = x0;
+        }
+      }
+    }
+    cur = nxt;
+  }
+  lid_fold16(p16, s8);
+  // sum over the 16 quads of each lane's 8 dims: halve by lane bits 5, 4, 3, then lanes l, l ^ 4
+  // -> lane l holds dim 16 b5 + 4 (l & 3) + 2 b4 + b3, biased by 128 per gram of its half
+  int32_t v4[4], v2[2], v1;
+  lid_halve<8>(s8, v4, (lane >> 5) & 1, 32);
+  lid_halve<4>(v4, v2, (lane >> 4) & 1, 16);
+  lid_halve<2>(v2, &v1, (lane >> 3) & 1, 8);
+  v1 += __shfl_xor(v1, 4);
+  // grams per half (the bias correction), then the total
+  const bool up = ((lane >> 5) & 1) != 0;
+  uint32_t cnt_hi = chi;
+  for (int o = 1; o < 64; o <<= 1) {
+    cnt += (uint32_t)__shfl_xor((int)cnt, o);
+    cnt_hi += (uint32_t)__shfl_xor((int)cnt_hi, o);
+  }
+  const int32_t S = v1 - 128 * (int32_t)(up ? cnt_hi : cnt - cnt_hi);
+  const int dim = ((lane >> 5) & 1) * 16 + (int)(4 * sub) + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
+  int32_t smax = S < 0 ? -S : S;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t t = __shfl_xor(smax, o);
+    smax = t > smax ? t : smax;
+  }
+  const int e = cnt ? lid_block_exp((int64_t)smax, (int64_t)cnt) : 0;
+  if ((lane & 4) == 0) arow[dim] = cnt ? lid_bf16_bits((float)lid_quant((int64_t)S, e, (int64_t)cnt)) : (uint16_t)0;
+  if (lane == 0) {
+    *e_out = e;
+    *cnt_out = (int64_t)cnt;
+  }
+  // dictionary-segmented scripts go to the CPU path (as k_langid_features)
+  bool dict = false;
+  for (uint32_t i = (uint32_t)lane; i < n; i += 64) {
+    if (b[i] >= 0xE0) {
+      int len;
+      dict |= (ucd.props(utf8_decode(b, i, n, &len)) & P_DICT) != 0;
+    }
+  }
+  if (__ballot(dict) && lane == 0) atomicOr(flag, DOC_NEEDS_CPU);
+}
+
+__global__ __launch_bounds__(64 * kLidWaves) void k_langid_mfma(
     const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off, const int32_t* __restrict__ perm,
-    int32_t ndocs, DevTables tabs, const int8_t* __restrict__ E, const uint16_t* __restrict__ WT, double w_scale,
+    int32_t ndocs, DevTables tabs, const uint8_t* __restrict__ Eb, const uint16_t* __restrict__ WT, double w_scale,
     const float* __restrict__ bias, int64_t* rec, int32_t width, uint32_t* flags, uint64_t* prof) {
   __shared__ __attribute__((aligned(16))) uint16_t A[kLidTile][kLidDim];
   __shared__ float Cm[kLidTile][kLidHeadCols];
   __shared__ int32_t ex[kLidTile];
   __shared__ int64_t cn[kLidTile];
   const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
-  const int pos = (int)blockIdx.x * kLidTile + w;
-  const int doc = pos < ndocs ? (perm ? perm[pos] : pos) : -1;
-  const uint64_t t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-  if (doc >= 0) {
-    const UcdView ucd{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
-    const uint8_t* b = bytes + off[doc];
-    const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
-    // the cut: byte offset of code point kLidMaxCps (or n), by counting lead bytes per chunk
-    uint32_t lim = n;
-    if (n > (uint32_t)kLidMaxCps) {
-      uint32_t seen = 0;
-      for (uint32_t base = 0; base < n; base += 64) {
-        const uint32_t i = base + (uint32_t)lane;
-        const uint64_t m = __ballot(i < n && utf8_is_lead(b[i]));
-        const uint32_t c = (uint32_t)__popcll(m);
-        if (seen + c > (uint32_t)kLidMaxCps) {
-          uint64_t mm = m;
-          for (uint32_t k = seen; k < (uint32_t)kLidMaxCps; ++k) mm &= mm - 1;
-          lim = base + (uint32_t)__builtin_ctzll(mm);
-          break;
-        }
-        seen += c;
+  const UcdView ucd{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
+  for (int r = w; r < kLidTile; r += kLidWaves) {
+    const int pos = (int)blockIdx.x * kLidTile + r;
+    const int doc = pos < ndocs ? (perm ? perm[pos] : pos) : -1;
+    if (doc < 0) {
+      if (lane < kLidDim) A[r][lane] = 0;
+      if (lane == 0) {
+        ex[r] = 0;
+        cn[r] = 0;
       }
+      continue;
     }
-    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    int32_t acc[kLidDim];
-#pragma unroll
-    for (int d = 0; d < kLidDim; ++d) acc[d] = 0;
-    uint32_t cnt = 0;
-    uint32_t c1 = 0, c2 = 0, c3 = 0;
-    uint8_t cur = (uint32_t)lane < lim ? b[lane] : (uint8_t)0;
-    for (uint32_t base = 0; base <= lim; base += 64) {
-      const uint32_t s = base + (uint32_t)lane;
-      const uint8_t nxt = s + 64 < lim ? b[s + 64] : (uint8_t)0;
-      const bool lead = s < lim && utf8_is_lead(cur);
-      const uint32_t l0 = lead ? (cur < 0x80u ? ((cur | 0x20u) - 'a' < 26u ? (cur | 0x20u) : 0u)
-                                              : lid_letter(ucd, b, n, s))
-                               : 0u;
-      const uint64_t M = __ballot(lead);
-      uint64_t m = M & below;
-      uint32_t lm[3];
-      bool have[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        have[k] = m != 0;
-        const int j = have[k] ? lid_top(m) : lane;
-        if (have[k]) m &= ~(1ull << j);
-        lm[k] = (uint32_t)__shfl((int)l0, j);
-      }
-      if (lead || s == lim) {
-        if (!have[0]) {
-          lm[0] = c1; lm[1] = c2; lm[2] = c3;
-        } else if (!have[1]) {
-          lm[1] = c1; lm[2] = c2;
-        } else if (!have[2]) {
-          lm[2] = c1;
-        }
-        cnt += (uint32_t)lid_grams_at(lm[2], lm[1], lm[0], l0, [&](uint32_t g) { lid_add_emb32(E, g, acc); });
-      }
-      if (M) {
-        uint64_t mm = M;
-        const int j0 = lid_top(mm);
-        mm &= ~(1ull << j0);
-        const uint32_t x0 = (uint32_t)__shfl((int)l0, j0);
-        if (!mm) {
-          c3 = c2; c2 = c1; c1 = x0;
-        } else {
-          const int j1 = lid_top(mm);
-          mm &= ~(1ull << j1);
-          const uint32_t x1 = (uint32_t)__shfl((int)l0, j1);
-          if (!mm) {
-            c3 = c1; c2 = x1; c1 = x0;
-          } else {
-            const uint32_t x2 = (uint32_t)__shfl((int)l0, lid_top(mm));
-            c3 = x2; c2 = x1; c1 = x0;
-          }
-        }
-      }
-      cur = nxt;
-    }
-    // 32 sums over 64 lanes: halve by lane bits 5..1, then pair lanes l, l ^ 1
-    int32_t v16[16], v8[8], v4[4], v2[2];
-    lid_halve<32>(acc, v16, (lane >> 5) & 1, 32);
-    lid_halve<16>(v16, v8, (lane >> 4) & 1, 16);
-    lid_halve<8>(v8, v4, (lane >> 3) & 1, 8);
-    lid_halve<4>(v4, v2, (lane >> 2) & 1, 4);
-    int32_t v1;
-    lid_halve<2>(v2, &v1, (lane >> 1) & 1, 2);
-    const int32_t S = v1 + __shfl_xor(v1, 1);
-    const int dim = (((lane >> 5) & 1) << 4) | (((lane >> 4) & 1) << 3) | (((lane >> 3) & 1) << 2) |
-                    (((lane >> 2) & 1) << 1) | ((lane >> 1) & 1);
-    for (int o = 1; o < 64; o <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, o);
-    int32_t smax = S < 0 ? -S : S;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int32_t t = __shfl_xor(smax, o);
-      smax = t > smax ? t : smax;
-    }
-    const int e = cnt ? lid_block_exp((int64_t)smax, (int64_t)cnt) : 0;
-    if ((lane & 1) == 0) A[w][dim] = cnt ? lid_bf16_bits((float)lid_quant((int64_t)S, e, (int64_t)cnt)) : (uint16_t)0;
-    if (lane == 0) {
-      ex[w] = e;
-      cn[w] = (int64_t)cnt;
-    }
-    // dictionary-segmented scripts go to the CPU path (as k_langid_features)
-    bool dict = false;
-    for (uint32_t i = (uint32_t)lane; i < n; i += 64) {
-      if (b[i] >= 0xE0) {
-        int len;
-        dict |= (ucd.props(utf8_decode(b, i, n, &len)) & P_DICT) != 0;
-      }
-    }
-    if (__ballot(dict) && lane == 0) atomicOr(flags + doc, DOC_NEEDS_CPU);
-  } else {
-    if (lane < kLidDim) A[w][lane] = 0;
-    if (lane == 0) {
-      ex[w] = 0;
-      cn[w] = 0;
-    }
+    const uint64_t t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+    lid_doc_vector(bytes + off[doc], (uint32_t)(off[doc + 1] - off[doc]), ucd, Eb, flags + doc, lane, A[r], &ex[r],
+                   &cn[r]);
+    if (prof && lane == 0) prof[(size_t)doc * kPhaseSlots + PH_LID] += __builtin_amdgcn_s_memtime() - t0;
   }
   __syncthreads();
   if (w == 0) {
@@ -543,7 +606,6 @@ __global__ __launch_bounds__(64 * kLidTile) void k_langid_mfma(
       lid_decide_v3(C, ex[lane], cn[lane], w_scale, bias, rec + (int64_t)d2 * width);
     }
   }
-  if (prof && doc >= 0 && lane == 0) prof[(size_t)doc * kPhaseSlots + PH_LID] += __builtin_amdgcn_s_memtime() - t0;
 }
 
 __global__ __launch_bounds__(64) void k_c4_pass_a(
@@ -901,16 +963,17 @@ int tb_langid_features(hipStream_t stream, const uint8_t* bytes, const int64_t* 
   return (int)hipGetLastError();
 }
 
-// k_langid_mfma: records of every document (perm order, 16 per workgroup); E int8 [buckets * 32],
+// k_langid_mfma: records of every document (perm order, 16 per workgroup); Eb = E + 128 as uint8
+// [buckets * 16] (the biased block-sparse embedding table),
 // WT bf16 bits [16 * 32] (the head transposed, columns >= 5 zero), bias float [8].
 int tb_langid_mfma(hipStream_t stream, const uint8_t* bytes, const int64_t* off, const int32_t* perm, int32_t ndocs,
-                   const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, const int8_t* E,
+                   const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, const uint8_t* E,
                    const uint16_t* WT, double w_scale, const float* bias, int64_t* rec, int32_t width,
                    uint32_t* flags, uint64_t* prof) {
   if (ndocs <= 0) return 0;
   if (!E || !WT || !bias || !rec || width < 2 || !(w_scale > 0)) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
-  hipLaunchKernelGGL(k_langid_mfma, dim3((ndocs + kLidTile - 1) / kLidTile), dim3(64 * kLidTile), 0, stream, bytes,
+  hipLaunchKernelGGL(k_langid_mfma, dim3((ndocs + kLidTile - 1) / kLidTile), dim3(64 * kLidWaves), 0, stream, bytes,
                      off, perm, ndocs, t, E, WT, w_scale, bias, rec, width, flags, prof);
   return (int)hipGetLastError();
 }

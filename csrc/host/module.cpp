@@ -483,7 +483,7 @@ PYBIND11_MODULE(_tbhost, m) {
                        double w_scale, py::array_t<float, py::array::c_style> b) {
         // v3: int8 embedding rows + integer head (the MFMA tile's operands)
         auto mdl = std::make_shared<LangidModel>();
-        if ((size_t)E.size() != (size_t)kLidBuckets * kLidDim) throw std::invalid_argument("E shape");
+        if ((size_t)E.size() != (size_t)kLidBuckets * kLidRowDim) throw std::invalid_argument("E shape");
         if ((size_t)W.size() != (size_t)kLidDim * kLidLangs) throw std::invalid_argument("W shape");
         if ((size_t)b.size() != (size_t)kLidRow) throw std::invalid_argument("b shape");
         for (py::ssize_t i = 0; i < W.size(); ++i)
@@ -543,6 +543,7 @@ PYBIND11_MODULE(_tbhost, m) {
   m.attr("LID_BUCKETS") = kLidBuckets;
   m.attr("LID_SCALE") = kLidScale;
   m.attr("LID_DIM") = kLidDim;
+  m.attr("LID_ROW_DIM") = kLidRowDim;
   m.attr("LID_QMAX") = kLidQMax;
 
   py::class_<StdRng>(m, "StdRng")

@@ -30,7 +30,7 @@ struct LangidModel {
   int version = 2;         // 2: folded int16 logit table (P); 3: int8 embeddings + MFMA head (E, W)
   std::vector<int16_t> P;  // v2: [kLidBuckets * kLidRow] fixed-point logit rows (csrc/common/langid.h)
   std::vector<float> b;    // [kLidRow]
-  std::vector<int8_t> E;   // v3: [kLidBuckets * kLidDim] embedding rows
+  std::vector<int8_t> E;   // v3: [kLidBuckets * kLidRowDim] embedding rows (block-sparse halves)
   std::vector<int16_t> W;  // v3: [kLidDim * kLidLangs] integer head
   double w_scale = 0;      // v3
   // Detect the language of `text`: returns lang index or -1, confidence in *conf.

@@ -160,7 +160,7 @@ def test_langid_mfma_head_vs_fp32_reference(host, corpus, runner_parts):
     data, off = synth.pack(texts)
     res = runner.run(data, off)
     r = _langid_records(runner, res, len(texts))
-    E = torch.from_numpy(lid.E.reshape(h.LID_BUCKETS, h.LID_DIM).astype(np.float32))
+    E = torch.from_numpy(lid.dense_E().astype(np.float32))
     W = torch.from_numpy(lid.W.reshape(h.LID_DIM, h.LID_LANGS).astype(np.float32)) * float(lid.w_scale)
     b = torch.from_numpy(lid.b[:h.LID_LANGS].astype(np.float32))
     near = 0

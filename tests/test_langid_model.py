@@ -56,7 +56,7 @@ def _float_reference(lid, text):
     g = np.asarray(h.langid_buckets(text), dtype=np.int64)
     if len(g) == 0:
         return -1, 0.0, None
-    E = lid.E.reshape(h.LID_BUCKETS, h.LID_DIM).astype(np.float64)
+    E = lid.dense_E().astype(np.float64)
     W = lid.W.reshape(h.LID_DIM, h.LID_LANGS).astype(np.float64)
     mean = E[g].sum(0) / len(g)
     logits = mean @ W * lid.w_scale + lid.b[:h.LID_LANGS].astype(np.float64)
@@ -95,7 +95,7 @@ def test_v3_integer_head_reproduced_in_numpy():
     h = native.host()
     lid = load_default()
     m = lid.native()
-    E = lid.E.reshape(h.LID_BUCKETS, h.LID_DIM).astype(np.int64)
+    E = lid.dense_E().astype(np.int64)
     W = lid.W.reshape(h.LID_DIM, h.LID_LANGS).astype(np.int64)
     for t in synth.make_corpus(120, 600, seed=5) + EDGE:
         g = np.asarray(h.langid_buckets(t), dtype=np.int64)

@@ -280,13 +280,14 @@ class Kernels:
     def langid_mfma(self, bytes_, off, perm, ndocs, E, WT, w_scale, bias, rec, width, flags, prof=None):
         """k_langid_mfma (v3 model): fastText int8 embedding bag + bf16 MFMA head, 16 documents per
         workgroup; the language record of every document into ``rec`` (document d at
-        rec[d * width]). ``E``: int8 [buckets * 32], ``WT``: bf16 bits [16 * 32] (head transposed),
+        rec[d * width]). ``E``: the embedding table as E + 128, uint8 [buckets * 16], ``WT``: bf16
+        bits [16 * 32] (head transposed),
         ``bias``: float32 [8] (csrc/common/langid.h)."""
         from .. import native
 
         h = native.host()
         t = self.tabs
-        if (E.numel() != h.LID_BUCKETS * h.LID_DIM or WT.numel() != 16 * h.LID_DIM or bias.numel() != h.LID_ROW
+        if (E.numel() != h.LID_BUCKETS * h.LID_ROW_DIM or WT.numel() != 16 * h.LID_DIM or bias.numel() != h.LID_ROW
                 or width < 2 or rec.numel() < ndocs * width or not w_scale > 0):
             raise DeviceError("langid_mfma: operand shapes")
         rc = self.lib.tb_langid_mfma(

@@ -538,8 +538,9 @@ class DeviceRunner:
                 self.lid_version = langid.version
                 self.lid_b = hiprt.to_device(np.ascontiguousarray(langid.b, dtype=np.float32))
                 if langid.version == 3:
-                    # v3: int8 embedding rows (2 MB, L2-resident) + the bf16 MFMA head operand
-                    self.lid_E = hiprt.to_device(np.ascontiguousarray(langid.E, dtype=np.int8))
+                    # v3: int8 embedding rows, biased to E + 128 as bytes for the kernel's SWAR sums
+                    # (2 MB, L2-resident), + the bf16 MFMA head operand
+                    self.lid_E = hiprt.to_device((langid.E.astype(np.int16) + 128).astype(np.uint8))
                     self.lid_WT = hiprt.to_device(np.ascontiguousarray(langid.head_bf16_t()).reshape(-1))
                     self.lid_w_scale = float(langid.w_scale)
                 else:

@@ -1,11 +1,13 @@
 """Train the language-id weights.
 
 Default model (v3, ``textblaster_amd/models/data/langid_v3.npz``, csrc/common/langid.h): a
-fastText classifier. Hashed character 1..4-grams (65536 buckets) -> int8 embedding rows of
-D = 32 dims, summed per document (mean-mode EmbeddingBag) -> linear head 32 -> 5 languages ->
-softmax. Training: (1) the convex problem first — the mean-mode table of per-bucket logits (the
-head folded in, = the v2 model in float); (2) lifted to D = 32: a seeded Gaussian head W0
-(32 x 5, full column rank) and E = T W0^+, so E W0 = T exactly and every embedding dim is used;
+fastText classifier. Hashed character 1..4-grams (65536 buckets) -> a D = 32 mean document
+vector from a block-sparse embedding table (bucket g's int8 row of 16 values feeds dims
+[16 h, 16 h + 16), h = the bucket's top bit: 16 bytes per gather) -> linear head 32 -> 5
+languages -> softmax. Training: (1) the convex problem first — the mean-mode table of per-bucket
+logits (the head folded in, = the v2 model in float); (2) lifted to D = 32: a seeded Gaussian
+head W0 (32 x 5; each 16 x 5 half has full column rank) and E[g] = T[g] W0_h^+ for the half h
+the bucket feeds, so every bucket's row maps back to its logits exactly and all 32 dims are used;
 (3) optionally jointly fine-tuned (--finetune-epochs, default 0: on the held-out set joint
 fine-tuning from the lifted point measured 97.8 % of sentences against 98.4 % without, and
 joint training from a random start 97.3-97.5 %, profiles/langid_eval.md); (4) quantised.
@@ -103,15 +105,28 @@ def train_table(feats, labels, h, epochs):
 
 
 def train_fasttext(feats, labels, h, epochs, dim, finetune_epochs=0, seed=7):
-    """v3: folded table -> lifted to EmbeddingBag(buckets, dim) + Linear(dim, 5) -> quantize_v3."""
+    """v3: folded table -> lifted to the block-sparse EmbeddingBag (65536 x 32, 16 non-zero dims per
+    bucket) + Linear(32, 5) -> quantize_v3."""
     T, b0 = train_folded(feats, labels, h, epochs)
-    W0 = np.random.default_rng(seed).normal(size=(dim, len(LANGS))) / np.sqrt(dim)
-    E0 = T @ np.linalg.pinv(W0)  # E0 @ W0 == T (W0 has full column rank)
+    rd = h.LID_ROW_DIM
+    W0 = np.random.default_rng(seed).normal(size=(dim, len(LANGS))) / np.sqrt(rd)
+    half = (np.arange(h.LID_BUCKETS) >> 15)  # the half of the doc vector each bucket feeds
+    E0 = np.zeros((h.LID_BUCKETS, rd))
+    for hh in (0, 1):
+        Wh = W0[hh * rd:(hh + 1) * rd]
+        E0[half == hh] = T[half == hh] @ np.linalg.pinv(Wh)  # E0[g] @ W0_h == T[g]
     if finetune_epochs > 0:
+        # the block-sparse bag as a 32-dim EmbeddingBag with the other half pinned at zero
+        full = np.zeros((h.LID_BUCKETS, dim))
+        for hh in (0, 1):
+            full[half == hh, hh * rd:(hh + 1) * rd] = E0[half == hh]
+        mask = torch.zeros(h.LID_BUCKETS, dim)
+        for hh in (0, 1):
+            mask[torch.from_numpy(half == hh), hh * rd:(hh + 1) * rd] = 1.0
         emb = torch.nn.EmbeddingBag(h.LID_BUCKETS, dim, mode="mean")
         head = torch.nn.Linear(dim, len(LANGS))
         with torch.no_grad():
-            emb.weight.copy_(torch.from_numpy(E0))
+            emb.weight.copy_(torch.from_numpy(full))
             head.weight.copy_(torch.from_numpy(W0.T))
             head.bias.copy_(torch.from_numpy(b0))
         opt = torch.optim.Adam(list(emb.parameters()) + list(head.parameters()), lr=0.001)
@@ -122,8 +137,12 @@ def train_fasttext(feats, labels, h, epochs, dim, finetune_epochs=0, seed=7):
                 opt.zero_grad()
                 loss.backward()
                 opt.step()
+                with torch.no_grad():
+                    emb.weight.mul_(mask)
             print(f"finetune epoch {ep} loss {loss.item():.4f}", flush=True)
-        E0 = emb.weight.detach().numpy().astype(np.float64)
+        full = emb.weight.detach().numpy().astype(np.float64)
+        for hh in (0, 1):
+            E0[half == hh] = full[half == hh, hh * rd:(hh + 1) * rd]
         W0 = head.weight.detach().numpy().T.astype(np.float64)
         b0 = head.bias.detach().numpy().astype(np.float64)
     return quantize_v3(E0, W0, b0)

@@ -13,6 +13,8 @@
 // A 64-bit hash collision between unequal elements is never trusted: it raises DOC_NEEDS_CPU and
 // the host recomputes that document with the CPU oracle.
 #pragma once
+#include <type_traits>
+
 #include "devplan.h"
 #include "hash.h"
 #include "langid.h"
@@ -239,6 +241,9 @@ struct DocCtx {
 };
 
 TB_HD bool is_ws(uint32_t p) { return (p & P_WS) != 0; }
+// Wave documents with fewer words than this keep n-gram canonical ids in 16 bits (every
+// canonicalisation slot index < 1.5 n + 2 fits); more words send the document to the CPU path.
+constexpr uint32_t kWave16 = 43000;
 TB_HD constexpr int rec_gr_fixed() { return 7; }
 
 // ---------------------------------------------------------------------------------------------
@@ -448,13 +453,14 @@ struct NoResolve {
   TB_HD void operator()(uint32_t, uint32_t) const {}
 };
 
-template <class P, class KeyF, class EqF>
-TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t* canon);
+template <class P, class KeyF, class EqF, class CT>
+TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, CT* canon);
 
 // Same, and res(i, canon[i]) for every element once its canonical index is final (fused into
 // the last pass, so callers need no extra pass over canon[]).
-template <class P, class KeyF, class EqF, class ResF>
-TB_HD void canonicalize_res(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t* canon, ResF&& res) {
+// canon may be 16-bit (wave documents: n < 43000, so every slot index fits) or 32-bit.
+template <class P, class KeyF, class EqF, class CT, class ResF>
+TB_HD void canonicalize_res(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, CT* canon, ResF&& res) {
   const uint32_t capn = n + (n >> 1) + 2;
   // allocated slots: whole 16-byte groups for zero_table's wide stores (exact in the one-wave kernel)
   const uint32_t capa = P::kWaves == 1 ? capn : (capn + 3u) & ~3u;
@@ -595,8 +601,8 @@ TB_HD void canonicalize_res(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint
   x.reset(mark);  // the table is scratch; canon[] lives in the caller's allocation
 }
 
-template <class P, class KeyF, class EqF>
-TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, uint32_t* canon) {
+template <class P, class KeyF, class EqF, class CT>
+TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, CT* canon) {
   canonicalize_res(x, n, key, eq, canon, NoResolve{});
 }
 
@@ -842,7 +848,8 @@ struct DupGrams {
 // once) and the seen-bitmap sn (zeroed): bytes of the repeated grams the walk counts. A walk only
 // stops at repeated grams; at a gram that occurs once it would mark an id nobody else has and
 // advance by one, so it jumps from one set bit of R to the next.
-TB_HD int64_t dup_walk(uint32_t G, uint32_t n, const uint32_t* gc, const uint32_t* R, uint32_t* sn,
+template <class GcT>
+TB_HD int64_t dup_walk(uint32_t G, uint32_t n, const GcT* gc, const uint32_t* R, uint32_t* sn,
                        const uint32_t* WL) {
   const uint32_t nw = (G + 31) >> 5;
   auto next_rep = [&](uint32_t from) -> uint32_t {  // first repeated position >= from, or G
@@ -879,8 +886,8 @@ TB_HD int64_t dup_walk(uint32_t G, uint32_t n, const uint32_t* gc, const uint32_
 // marks every lane holding the same id seen (one ballot), a repeat drops the lanes it jumps over.
 // The window's first visits then set their seen bits and the counted lanes' lengths are summed.
 // Same visits, same result as dup_walk.
-template <class P>
-TB_HD int64_t dup_walk_wave(const P& par, uint32_t G, uint32_t n, const uint32_t* gc, const uint32_t* R,
+template <class P, class GcT>
+TB_HD int64_t dup_walk_wave(const P& par, uint32_t G, uint32_t n, const GcT* gc, const uint32_t* R,
                             uint32_t* sn, const uint32_t* WL) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t lane = par.lane;
@@ -1081,11 +1088,35 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
   // of the LDS slice) are released, so the n-gram tables get that space.
   const uint32_t W = w.n;
   const bool ngrams = ds.n_top + ds.n_dup > 0;
+  if constexpr (P::kWaves == 1) {
+    if (ngrams && W >= kWave16) {
+      x.set_flag(DOC_NEEDS_CPU);
+      return;
+    }
+  }
   uint32_t* wid = nullptr;
   uint32_t* WL = nullptr;
   uint64_t* K = nullptr;
   uint64_t* PB = nullptr;
+  // The last GopherRepetition step of a stage hands the top of the LDS slice (code point arrays,
+  // prefix hashes) to the n-gram phase: the word hashes, the last reader of the prefix hashes,
+  // go to HBM scratch first, so the word-level arrays below get the slice (read by every n-gram
+  // key and equality test) instead of spilling to HBM.
+#ifndef TB_EARLY_RELEASE
+#define TB_EARLY_RELEASE 1
+#endif
+  const bool early_release = TB_EARLY_RELEASE && release_props && !ex && ngrams;
   if (ngrams) {
+    uint64_t* wh = nullptr;
+    auto mw = x.mark();
+    if (early_release) {
+      wh = x.template alloc<uint64_t>(W + 1);
+      if (x.overflow) return;
+      x.par.for_n(W, [&](uint32_t k) { wh[k] = span_hash8(x, ph, w.bs[k], w.be[k]); });
+      x.par.sync();
+      x.release_hi();
+      mw = x.mark();
+    }
     // LDS only while a canonicalisation table for W elements (~6 W bytes) still fits next to them
     // (split mode: HBM, they outlive this kernel)
     const uint64_t tab_bytes = 6ull * W + 64;
@@ -1093,11 +1124,14 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     WL = ex ? x.template alloc<uint32_t>(W + 1) : x.template alloc_hot_keep<uint32_t>(W + 1, tab_bytes);
     K = ex ? x.template alloc<uint64_t>(W + 1) : x.template alloc_hot_keep<uint64_t>(W + 1, tab_bytes);
     PB = ex ? x.template alloc<uint64_t>(W + 1) : x.template alloc_hot_keep<uint64_t>(W + 1, tab_bytes);
-    const auto mw = x.mark();
-    uint64_t* wh = x.template alloc_hot_hi<uint64_t>(W + 1);
+    if (!early_release) {
+      mw = x.mark();
+      wh = x.template alloc_hot_hi<uint64_t>(W + 1);
+      if (x.overflow) return;
+      x.par.for_n(W, [&](uint32_t k) { wh[k] = span_hash8(x, ph, w.bs[k], w.be[k]); });
+      x.par.sync();
+    }
     if (x.overflow) return;
-    x.par.for_n(W, [&](uint32_t k) { wh[k] = span_hash8(x, ph, w.bs[k], w.be[k]); });
-    x.par.sync();
     canonicalize(
         x, W, [&](uint32_t k) { return dev_key(wh[k], w.be[k] - w.bs[k]); },
         [&](uint32_t i, uint32_t j) { return bytes_eq<P>(b, w.bs[i], w.be[i], w.bs[j], w.be[j]); }, wid);
@@ -1112,13 +1146,13 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
         [&](uint32_t j) { return mulmod61(wh[j], x.ipowb(WL[j + 1])); }, [&](uint32_t k, uint64_t e) { K[k] = e; });
     x.par.single([&]() { K[W] = ktot; });
     x.par.sync();
-    x.reset(mw);  // wh
+    if (!early_release) x.reset(mw);  // wh (early release: wh stays in HBM below the arrays)
     if (x.overflow) return;
   }
   x.stamp(PH_GR_WORDS);
   // the n-gram statistics read words, bytes and the arrays above only: the top of the LDS slice
   // (code point arrays, prefix hashes) goes to their hash tables
-  if (release_props) x.release_hi();
+  if (release_props && !early_release) x.release_hi();
   if (ngrams) {
     const DupGrams dg{wid, WL, K, PB, w.bs, w.be, b};
     // Top n-grams (space-joined grams: equal iff their word sequences are equal). Canonical ids
@@ -1206,7 +1240,9 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       for (int t = 0; t < nd; ++t) gtot += gsize(t);
       const auto m3 = x.mark();
       uint32_t* bits = x.template alloc_hot<uint32_t>(2 * (uint64_t)SW * (uint64_t)nd);  // [sn | R] per order
-      uint32_t* gcall = x.template alloc_hot_keep<uint32_t>((uint64_t)gtot + 1, 6ull * W + 64);
+      // wave documents keep the canonical ids in 16 bits (half the slice; W < kWave16)
+      using GcT = std::conditional_t<P::kWaves == 1, uint16_t, uint32_t>;
+      GcT* gcall = x.template alloc_hot_keep<GcT>((uint64_t)gtot + 1, 6ull * W + 64);
       if (x.overflow) return;
       x.par.for_n(2 * SW * (uint32_t)nd, [&](uint32_t i) { bits[i] = 0; });
       x.par.sync();
@@ -1215,7 +1251,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
         const uint32_t n = (uint32_t)ds.dup_n[t];
         const uint32_t G = gsize(t);
         if (G == 0) continue;
-        uint32_t* gc = gcall + gb;
+        GcT* gc = gcall + gb;
         uint32_t* R = bits + (uint32_t)t * 2 * SW + SW;
         gb += G;
         auto mark_rep = [&](uint32_t p, uint32_t g) {
@@ -1418,11 +1454,11 @@ TB_HD void langid_sums(DocCtx<P>& x, const uint8_t* b, uint32_t n, const LidTabl
         const int64_t p1 = prev_lead(b, s);
         const int64_t p2 = p1 >= 0 ? prev_lead(b, p1) : -1;
         const int64_t p3 = p2 >= 0 ? prev_lead(b, p2) : -1;
-        part[D - 1] += lid_grams_at(lid_letter(ucd, b, n, p3), lid_letter(ucd, b, n, p2),
-                                    lid_letter(ucd, b, n, p1), l0, [&](uint32_t g) {
-                                      if (lt.E) lid_add_emb(lt.E, g, part);
-                                      else lid_add_row(lt.P, g, part);
-                                    });
+        part[D - 1] += lid_grams_n(lid_letter(ucd, b, n, p3), lid_letter(ucd, b, n, p2),
+                                   lid_letter(ucd, b, n, p1), l0, [&](uint32_t g, int order) {
+                                     if (lt.E) lid_add_emb(lt.E, g, order, part);
+                                     else lid_add_row(lt.P, g, part);
+                                   });
       },
       tmp, sums);
   x.reset(mark);

@@ -1,11 +1,11 @@
 // Character n-gram language identifier that stands in for lingua (reference
 // src/pipeline/filters/language_filter.rs:35-93; survey H5). Two models share the featurizer:
 //
-// v3 (default, "fastText + bf16 MFMA head"): a document vector of kLidDim = 32 dims from a
-// block-sparse embedding table: the bucket's int8 row of kLidRowDim = 16 values lands in the
-// lower or upper half of the vector by the bucket's top bit (a 65536 x 32 table whose rows have
-// 16 structural zeros, stored as 65536 x 16: 16 bytes per n-gram gather). A document's rows
-// are summed exactly (int32), the mean doc vector is
+// v3 (default, "fastText + bf16 MFMA head"): a document vector of kLidDim = 32 dims, the
+// concatenation of two 16-dim bags over one int8 embedding table of kLidRowDim = 16 values per
+// bucket (16 bytes per n-gram gather): the 1- and 2-grams are summed into the lower half, the 3-
+// and 4-grams into the upper half. A document's rows are summed exactly (int32), the mean doc
+// vector is
 // quantised to integers |a| <= 255 with one exponent per document (block floating point, every
 // value exact in bf16), and the 32 -> 5 linear head runs as one v_mfma_f32_16x16x32_bf16 tile per
 // 16 documents with integer bf16 weights |W| <= 255. All products and partial sums are integers
@@ -54,48 +54,32 @@ TB_HD uint32_t lid_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d, int n) {
 }
 
 // Emits the buckets of every n-gram that ENDS at code point position i (0 <= i <= lim), given
-// the lowercased letters L(i-3) .. L(i) (0 when a position is not a letter or is past lim-1).
-// Position lim acts as a virtual non-letter so a word that reaches the cut still gets its ">"
-// grams. Returns the number of grams (<= kLidMaxGrams).
+// the lowercased letters L(i-3) .. L(i) (0 when a position is not a letter or is past lim-1),
+// as emit(bucket, n). Position lim acts as a virtual non-letter so a word that reaches the cut
+// still gets its ">" grams. At most one gram per order n; returns the number of grams (<= 4).
 template <class F>
-TB_HD int lid_grams_at(uint32_t lm3, uint32_t lm2, uint32_t lm1, uint32_t l0, F&& emit) {
+TB_HD int lid_grams_n(uint32_t lm3, uint32_t lm2, uint32_t lm1, uint32_t l0, F&& emit) {
   const uint32_t B = kLidBoundary;
   if (l0) {
-    emit(lid_hash(l0, 0, 0, 0, 1));
-    emit(lid_hash(lm1 ? lm1 : B, l0, 0, 0, 2));
+    emit(lid_hash(l0, 0, 0, 0, 1), 1);
+    emit(lid_hash(lm1 ? lm1 : B, l0, 0, 0, 2), 2);
     if (!lm1) return 2;
-    emit(lid_hash(lm2 ? lm2 : B, lm1, l0, 0, 3));
+    emit(lid_hash(lm2 ? lm2 : B, lm1, l0, 0, 3), 3);
     if (!lm2) return 3;
-    emit(lid_hash(lm3 ? lm3 : B, lm2, lm1, l0, 4));
+    emit(lid_hash(lm3 ? lm3 : B, lm2, lm1, l0, 4), 4);
     return 4;
   }
   if (!lm1) return 0;
-  emit(lid_hash(lm1, B, 0, 0, 2));
-  emit(lid_hash(lm2 ? lm2 : B, lm1, B, 0, 3));
+  emit(lid_hash(lm1, B, 0, 0, 2), 2);
+  emit(lid_hash(lm2 ? lm2 : B, lm1, B, 0, 3), 3);
   if (!lm2) return 2;
-  emit(lid_hash(lm3 ? lm3 : B, lm2, lm1, B, 4));
+  emit(lid_hash(lm3 ? lm3 : B, lm2, lm1, B, 4), 4);
   return 3;
 }
 
-// lid_grams_at with the buckets in fixed slots g[0..count) (straight-line code: no indexed
-// stores into a register array).
-TB_HD int lid_grams4(uint32_t lm3, uint32_t lm2, uint32_t lm1, uint32_t l0, uint32_t* g) {
-  const uint32_t B = kLidBoundary;
-  if (l0) {
-    g[0] = lid_hash(l0, 0, 0, 0, 1);
-    g[1] = lid_hash(lm1 ? lm1 : B, l0, 0, 0, 2);
-    if (!lm1) return 2;
-    g[2] = lid_hash(lm2 ? lm2 : B, lm1, l0, 0, 3);
-    if (!lm2) return 3;
-    g[3] = lid_hash(lm3 ? lm3 : B, lm2, lm1, l0, 4);
-    return 4;
-  }
-  if (!lm1) return 0;
-  g[0] = lid_hash(lm1, B, 0, 0, 2);
-  g[1] = lid_hash(lm2 ? lm2 : B, lm1, B, 0, 3);
-  if (!lm2) return 2;
-  g[2] = lid_hash(lm3 ? lm3 : B, lm2, lm1, B, 4);
-  return 3;
+template <class F>
+TB_HD int lid_grams_at(uint32_t lm3, uint32_t lm2, uint32_t lm1, uint32_t l0, F&& emit) {
+  return lid_grams_n(lm3, lm2, lm1, l0, [&](uint32_t g, int) { emit(g); });
 }
 
 // Adds the int16 row of bucket g to the 5 language sums.
@@ -217,13 +201,13 @@ struct LidTables {
   double w_scale = 0;          // v3: logit units per head unit at e = 0
 };
 
-// Dims of the doc vector that bucket g's row feeds: [lid_half(g), lid_half(g) + 16).
-TB_HD int lid_half(uint32_t g) { return (int)(g >> (kLidBucketsLog2 - 1)) * kLidRowDim; }
+// Dims of the doc vector that an n-gram of order n feeds: [lid_half(n), lid_half(n) + 16).
+TB_HD int lid_half(int n) { return n >= 3 ? kLidRowDim : 0; }
 
-// Adds the int8 embedding row of bucket g to its half of the kLidDim sums (v3).
-TB_HD void lid_add_emb(const int8_t* E, uint32_t g, int32_t* acc) {
+// Adds the int8 embedding row of bucket g (an n-gram of order n) to its half of the sums (v3).
+TB_HD void lid_add_emb(const int8_t* E, uint32_t g, int n, int32_t* acc) {
   const int8_t* r = E + (size_t)g * kLidRowDim;
-  int32_t* a = acc + lid_half(g);
+  int32_t* a = acc + lid_half(n);
 #pragma unroll
   for (int d = 0; d < kLidRowDim; ++d) a[d] += r[d];
 }

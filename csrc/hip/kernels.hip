@@ -356,59 +356,38 @@ __global__ __launch_bounds__(64) void k_langid_features(
   if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
 }
 
-// Language ID v3 (csrc/common/langid.h): fastText bag + bf16 MFMA head, 16 documents per
+// Language ID v3 (csrc/common/langid.h): two fastText bags + bf16 MFMA head, 16 documents per
 // 256-thread workgroup: wave w gathers documents w, w + 4, w + 8, w + 12 of the tile one after
 // another (launch positions blockIdx.x * 16 + ...; the length-sorted order keeps a tile's
-// documents alike in size). Per 64-byte chunk every lane finds the <= 4 n-grams ending at its
-// code point (the chunked walk and register letter carry of langid_coop); then the four lanes of
-// a quad share their 16 grams: lane q of the quad loads dword q of each of the 16 embedding rows
-// (16-byte rows, one dword load per row and lane: the same bytes per gram as the v2 table) and
-// adds it SWAR-style into the half of the document vector the bucket feeds (its top bit) — the
-// table holds E + 128 as unsigned bytes, even and odd bytes go to the two 16-bit halves of a
-// register (no overflow within 16 chunks: 16 x 16 x 255 < 2^16), folded into eight int32 sums
-// every 16 chunks. A short butterfly (4 shuffles) sums the lanes' slices into the document's 32
-// exact dims (minus 128 x #grams per half), which the wave quantises with the document's block
-// exponent (lid_block_exp / lid_quant: integers |a| <= 255, exact in bf16) into row r of the
-// workgroup's 16 x 32 A tile in LDS. Wave 0 then runs the head as one v_mfma_f32_16x16x32_bf16
-// (A: 16 docs x 32 dims, B: the head transposed, 16 columns x 32 dims, integer bf16) and 16 lanes
-// turn their row of the exact fp32 result into the record (lid_decide_v3). Same records as
-// LangidModel on the host.
+// documents alike in size). Per 64-byte chunk every lane finds the n-grams ending at its code
+// point (the chunked walk and register letter carry of langid_coop; at most one gram per order
+// n = 1..4, so each order has a fixed slot) and loads each gram's 16-byte embedding row with one
+// dwordx4 (the bytes of the v2 table). Rows are added SWAR-style: the table holds E + 128 as
+// unsigned bytes, even and odd bytes go to the two 16-bit halves of a register, the 1-/2-gram
+// slots into one set of 8 packed registers (dims 0..15), the 3-/4-gram slots into another (dims
+// 16..31) — no lane-dependent selects. Every 64 chunks (and at the end) a butterfly over the
+// lanes (packed step first: two lanes' 64-chunk sums still fit 16 bits) folds the packed sums into
+// one exact int32 dim per lane; minus 128 x #grams of its bag, that is the document's exact
+// 32-dim sum, which the wave quantises with the document's block exponent (lid_block_exp /
+// lid_quant: integers |a| <= 255, exact in bf16) into row r of the workgroup's 16 x 32 A tile in
+// LDS. Wave 0 then runs the head as one v_mfma_f32_16x16x32_bf16 (A: 16 docs x 32 dims, B: the
+// head transposed, 16 columns x 32 dims, integer bf16) and 16 lanes turn their row of the exact
+// fp32 result into the record (lid_decide_v3). Same records as LangidModel on the host.
 constexpr int kLidTile = 16;
 constexpr int kLidWaves = 4;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// value of lane (quad base + src) for every lane of a quad (DPP quad_perm broadcast)
-template <int SRC>
-__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, SRC * 0x55, 0xF, 0xF, false);
-}
-
-// adds the lane's dword of the rows g[0..k) of one quad lane into the packed sums of the half
-// each row feeds (p16[0..1]: lower half, p16[2..3]: upper half; even / odd bytes)
-__device__ __forceinline__ void lid_quad_rows(const uint8_t* __restrict__ Eb, uint32_t sub, uint32_t k,
-                                              const uint32_t* g, uint32_t* p16) {
+// Adds the 16-byte row of bucket g to one bag's packed sums: p[2q] holds dims 4q, 4q + 2 (even
+// bytes of dword q), p[2q + 1] dims 4q + 1, 4q + 3.
+__device__ __forceinline__ void lid_row_swar(const uint8_t* __restrict__ Eb, uint32_t g, uint32_t* p) {
+  const uint4 w = *(const uint4*)(Eb + (size_t)g * kLidRowDim);
+  const uint32_t v[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-  for (uint32_t j = 0; j < 4; ++j) {
-    if (j < k) {
-      const uint32_t w = *(const uint32_t*)(Eb + (size_t)g[j] * kLidRowDim + 4 * sub);
-      const uint32_t ev = w & 0x00FF00FFu, od = (w >> 8) & 0x00FF00FFu;
-      const bool up = (g[j] >> (kLidBucketsLog2 - 1)) != 0;
-      p16[0] += up ? 0u : ev;
-      p16[1] += up ? 0u : od;
-      p16[2] += up ? ev : 0u;
-      p16[3] += up ? od : 0u;
-    }
+  for (int q = 0; q < 4; ++q) {
+    p[2 * q] += v[q] & 0x00FF00FFu;
+    p[2 * q + 1] += (v[q] >> 8) & 0x00FF00FFu;
   }
-}
-
-__device__ __forceinline__ void lid_fold16(uint32_t* p16, int32_t* s) {
-  // s[0..3]: dims 4 sub + 0..3 (lower half), s[4..7]: dims 16 + 4 sub + 0..3 (upper half)
-  s[0] += (int32_t)(p16[0] & 0xFFFFu); s[2] += (int32_t)(p16[0] >> 16);
-  s[1] += (int32_t)(p16[1] & 0xFFFFu); s[3] += (int32_t)(p16[1] >> 16);
-  s[4] += (int32_t)(p16[2] & 0xFFFFu); s[6] += (int32_t)(p16[2] >> 16);
-  s[5] += (int32_t)(p16[3] & 0xFFFFu); s[7] += (int32_t)(p16[3] >> 16);
-  p16[0] = p16[1] = p16[2] = p16[3] = 0;
 }
 
 // Butterfly step: the lanes whose bit `m` is set keep the upper half of the n values, the others
@@ -423,7 +402,33 @@ __device__ __forceinline__ void lid_halve(const int32_t* in, int32_t* out, bool 
   }
 }
 
-// One document's quantised doc vector into A row `row` (and its exponent / count).
+// Folds both bags' packed sums (pa: dims 0..15, pb: dims 16..31; <= 64 chunks each) over the wave
+// into `dsum` (lane l: dim 16 b5 + 4 (2 b4 + b3) + b2 + 2 b1 of lane l, lanes l and l ^ 1 alike) and
+// clears them.
+__device__ __forceinline__ void lid_fold(uint32_t* pa, uint32_t* pb, int lane, int32_t& dsum) {
+  const bool up = (lane >> 5) & 1;
+  uint32_t kept[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t keep = up ? pb[j] : pa[j];
+    const uint32_t give = up ? pa[j] : pb[j];
+    kept[j] = keep + (uint32_t)__shfl_xor((int)give, 32);  // two 64-chunk sums: < 2^16 per half
+    pa[j] = pb[j] = 0;
+  }
+  int32_t u[16], v8[8], v4[4], v2[2], v1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {  // u[4q + 2e + h] = dim 4q + e + 2h of the kept bag
+    u[2 * j] = (int32_t)(kept[j] & 0xFFFFu);
+    u[2 * j + 1] = (int32_t)(kept[j] >> 16);
+  }
+  lid_halve<16>(u, v8, (lane >> 4) & 1, 16);
+  lid_halve<8>(v8, v4, (lane >> 3) & 1, 8);
+  lid_halve<4>(v4, v2, (lane >> 2) & 1, 4);
+  lid_halve<2>(v2, &v1, (lane >> 1) & 1, 2);
+  dsum += v1 + __shfl_xor(v1, 1);
+}
+
+// One document's quantised doc vector into A row `arow` (and its exponent / count).
 __device__ __forceinline__ void lid_doc_vector(const uint8_t* __restrict__ b, uint32_t n, const UcdView& ucd,
                                                const uint8_t* __restrict__ Eb, uint32_t* flag, int lane,
                                                uint16_t* arow, int32_t* e_out, int64_t* cnt_out) {
@@ -445,10 +450,9 @@ __device__ __forceinline__ void lid_doc_vector(const uint8_t* __restrict__ b, ui
     }
   }
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  const uint32_t sub = (uint32_t)lane & 3u;
-  uint32_t p16[4] = {0u, 0u, 0u, 0u};
-  int32_t s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint32_t cnt = 0, chi = 0, chunks = 0;  // grams, grams feeding the upper half
+  uint32_t pa[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, pb[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  int32_t dsum = 0;
+  uint32_t cnt_lo = 0, cnt_hi = 0, chunks = 0;  // grams of the 1-2-gram / 3-4-gram bags
   uint32_t c1 = 0, c2 = 0, c3 = 0;
   uint8_t cur = (uint32_t)lane < lim ? b[lane] : (uint8_t)0;
   for (uint32_t base = 0; base <= lim; base += 64) {
@@ -469,7 +473,6 @@ __device__ __forceinline__ void lid_doc_vector(const uint8_t* __restrict__ b, ui
       if (have[k]) m &= ~(1ull << j);
       lm[k] = (uint32_t)__shfl((int)l0, j);
     }
-    uint32_t g[4] = {0u, 0u, 0u, 0u}, k = 0;
     if (lead || s == lim) {
       if (!have[0]) {
         lm[0] = c1; lm[1] = c2; lm[2] = c3;
@@ -478,26 +481,17 @@ __device__ __forceinline__ void lid_doc_vector(const uint8_t* __restrict__ b, ui
       } else if (!have[2]) {
         lm[2] = c1;
       }
-      k = (uint32_t)lid_grams4(lm[2], lm[1], lm[0], l0, g);
+      lid_grams_n(lm[2], lm[1], lm[0], l0, [&](uint32_t g, int order) {
+        if (order <= 2) {
+          lid_row_swar(Eb, g, pa);
+          ++cnt_lo;
+        } else {
+          lid_row_swar(Eb, g, pb);
+          ++cnt_hi;
+        }
+      });
     }
-    cnt += k;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) chi += (j < k && (g[j] >> (kLidBucketsLog2 - 1)) != 0) ? 1u : 0u;
-    if (__ballot(k != 0)) {
-      // the quad's 16 grams, each lane its 8-byte slice of every row
-      uint32_t gq[4], kq;
-#define TB_LID_SRC(SRC)                                                  \
-      kq = quad_bcast<SRC>(k);                                           \
-      gq[0] = quad_bcast<SRC>(g[0]); gq[1] = quad_bcast<SRC>(g[1]);      \
-      gq[2] = quad_bcast<SRC>(g[2]); gq[3] = quad_bcast<SRC>(g[3]);      \
-      lid_quad_rows(Eb, sub, kq, gq, p16);
-      TB_LID_SRC(0)
-      TB_LID_SRC(1)
-      TB_LID_SRC(2)
-      TB_LID_SRC(3)
-#undef TB_LID_SRC
-      if ((++chunks & 15u) == 0) lid_fold16(p16, s8);
-    }
+    if ((++chunks & 63u) == 0) lid_fold(pa, pb, lane, dsum);
     if (M) {
       uint64_t mm = M;
       const int j0 = lid_top(mm);
@@ -519,30 +513,23 @@ __device__ __forceinline__ void lid_doc_vector(const uint8_t* __restrict__ b, ui
     }
     cur = nxt;
   }
-  lid_fold16(p16, s8);
-  // sum over the 16 quads of each lane's 8 dims: halve by lane bits 5, 4, 3, then lanes l, l ^ 4
-  // -> lane l holds dim 16 b5 + 4 (l & 3) + 2 b4 + b3, biased by 128 per gram of its half
-  int32_t v4[4], v2[2], v1;
-  lid_halve<8>(s8, v4, (lane >> 5) & 1, 32);
-  lid_halve<4>(v4, v2, (lane >> 4) & 1, 16);
-  lid_halve<2>(v2, &v1, (lane >> 3) & 1, 8);
-  v1 += __shfl_xor(v1, 4);
-  // grams per half (the bias correction), then the total
-  const bool up = ((lane >> 5) & 1) != 0;
-  uint32_t cnt_hi = chi;
+  lid_fold(pa, pb, lane, dsum);
   for (int o = 1; o < 64; o <<= 1) {
-    cnt += (uint32_t)__shfl_xor((int)cnt, o);
+    cnt_lo += (uint32_t)__shfl_xor((int)cnt_lo, o);
     cnt_hi += (uint32_t)__shfl_xor((int)cnt_hi, o);
   }
-  const int32_t S = v1 - 128 * (int32_t)(up ? cnt_hi : cnt - cnt_hi);
-  const int dim = ((lane >> 5) & 1) * 16 + (int)(4 * sub) + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
+  const uint32_t cnt = cnt_lo + cnt_hi;
+  const bool up = ((lane >> 5) & 1) != 0;
+  const int32_t S = dsum - 128 * (int32_t)(up ? cnt_hi : cnt_lo);
+  const int dim = ((lane >> 5) & 1) * 16 + (2 * ((lane >> 4) & 1) + ((lane >> 3) & 1)) * 4 + ((lane >> 2) & 1) +
+                  2 * ((lane >> 1) & 1);
   int32_t smax = S < 0 ? -S : S;
   for (int o = 1; o < 64; o <<= 1) {
     const int32_t t = __shfl_xor(smax, o);
     smax = t > smax ? t : smax;
   }
   const int e = cnt ? lid_block_exp((int64_t)smax, (int64_t)cnt) : 0;
-  if ((lane & 4) == 0) arow[dim] = cnt ? lid_bf16_bits((float)lid_quant((int64_t)S, e, (int64_t)cnt)) : (uint16_t)0;
+  if ((lane & 1) == 0) arow[dim] = cnt ? lid_bf16_bits((float)lid_quant((int64_t)S, e, (int64_t)cnt)) : (uint16_t)0;
   if (lane == 0) {
     *e_out = e;
     *cnt_out = (int64_t)cnt;
@@ -558,7 +545,7 @@ __device__ __forceinline__ void lid_doc_vector(const uint8_t* __restrict__ b, ui
   if (__ballot(dict) && lane == 0) atomicOr(flag, DOC_NEEDS_CPU);
 }
 
-__global__ __launch_bounds__(64 * kLidWaves) void k_langid_mfma(
+__global__ __launch_bounds__(64 * kLidWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_langid_mfma(
     const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off, const int32_t* __restrict__ perm,
     int32_t ndocs, DevTables tabs, const uint8_t* __restrict__ Eb, const uint16_t* __restrict__ WT, double w_scale,
     const float* __restrict__ bias, int64_t* rec, int32_t width, uint32_t* flags, uint64_t* prof) {

@@ -516,28 +516,31 @@ PYBIND11_MODULE(_tbhost, m) {
         return py::make_tuple(r[0], conf);
       });
   m.def("lid_exp", [](double x) { return lid_exp(x); });
-  m.def("langid_buckets", [](const std::string& s) {
-    // The hashed n-gram bucket ids of `s` (training-time featurizer, identical to the model's).
+  m.def("langid_buckets", [](const std::string& s, bool with_order) -> py::object {
+    // The hashed n-gram bucket ids of `s` (training-time featurizer, identical to the model's),
+    // and with_order: their n-gram orders too.
     std::vector<uint32_t> out;
+    std::vector<uint8_t> ord;
     const uint8_t* b = (const uint8_t*)s.data();
     const uint32_t n = (uint32_t)s.size();
     const UcdView& u = host_ucd();
     uint32_t lm3 = 0, lm2 = 0, lm1 = 0;
     int ncp = 0;
-    auto emit = [&](uint32_t k) { out.push_back(k); };
+    auto emit = [&](uint32_t k, int order) { out.push_back(k); ord.push_back((uint8_t)order); };
     for (uint32_t i = 0; i < n && ncp < kLidMaxCps; ++ncp) {
       const uint32_t l0 = lid_letter(u, b, n, i);
       int len;
       (void)utf8_decode(b, i, n, &len);
       i += len;
-      lid_grams_at(lm3, lm2, lm1, l0, emit);
+      lid_grams_n(lm3, lm2, lm1, l0, emit);
       lm3 = lm2;
       lm2 = lm1;
       lm1 = l0;
     }
-    lid_grams_at(lm3, lm2, lm1, 0, emit);
-    return out;
-  });
+    lid_grams_n(lm3, lm2, lm1, 0, emit);
+    if (with_order) return py::make_tuple(out, ord);
+    return py::cast(out);
+  }, py::arg("s"), py::arg("with_order") = false);
   m.attr("LID_ROW") = kLidRow;
   m.attr("LID_LANGS") = kLidLangs;
   m.attr("LID_BUCKETS") = kLidBuckets;

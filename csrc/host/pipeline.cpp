@@ -124,8 +124,8 @@ int64_t LangidModel::sums(std::string_view text, int64_t* out) const {
   int64_t cnt = 0;
   uint32_t lm3 = 0, lm2 = 0, lm1 = 0;
   int ncp = 0;
-  auto emit = [&](uint32_t g) {
-    if (version == 3) lid_add_emb(E.data(), g, part);
+  auto emit = [&](uint32_t g, int order) {
+    if (version == 3) lid_add_emb(E.data(), g, order, part);
     else lid_add_row(P.data(), g, part);
     for (int l = 0; l < D; ++l) { out[l] += part[l]; part[l] = 0; }
   };
@@ -135,13 +135,13 @@ int64_t LangidModel::sums(std::string_view text, int64_t* out) const {
     int len;
     (void)utf8_decode(b8, i, n, &len);
     i += len;
-    cnt += lid_grams_at(lm3, lm2, lm1, l0, emit);
+    cnt += lid_grams_n(lm3, lm2, lm1, l0, emit);
     lm3 = lm2;
     lm2 = lm1;
     lm1 = l0;
   }
   // virtual non-letter at the cut / end of text
-  cnt += lid_grams_at(lm3, lm2, lm1, 0, emit);
+  cnt += lid_grams_n(lm3, lm2, lm1, 0, emit);
   return cnt;
 }
 

@@ -151,7 +151,8 @@ def test_langid_records_match_host(host, corpus, runner_parts):
 def test_langid_mfma_head_vs_fp32_reference(host, corpus, runner_parts):
     """The device's MFMA head vs. plain fp32 inference of the same fastText model in PyTorch
     (mean of the gathered int8 rows in fp32, fp32 head, softmax): logits agree within the
-    doc vector's 8-bit quantisation, the argmax is the same away from near-ties."""
+    doc vector's 8-bit quantisation (confidence within 0.015), the argmax is the same away
+    from near-ties."""
     import torch
 
     _, _, _, runner, lid = runner_parts
@@ -160,16 +161,19 @@ def test_langid_mfma_head_vs_fp32_reference(host, corpus, runner_parts):
     data, off = synth.pack(texts)
     res = runner.run(data, off)
     r = _langid_records(runner, res, len(texts))
-    E = torch.from_numpy(lid.dense_E().astype(np.float32))
     W = torch.from_numpy(lid.W.reshape(h.LID_DIM, h.LID_LANGS).astype(np.float32)) * float(lid.w_scale)
     b = torch.from_numpy(lid.b[:h.LID_LANGS].astype(np.float32))
+    E = torch.from_numpy(lid.E.reshape(h.LID_BUCKETS, h.LID_ROW_DIM).astype(np.float32))
     near = 0
     for i, t in enumerate(texts):
-        g = torch.tensor(h.langid_buckets(t), dtype=torch.int64)
+        g, order = h.langid_buckets(t, True)
         if len(g) == 0:
             assert r[i, 0] == -1
             continue
-        logits = E[g].mean(0) @ W + b
+        g = torch.tensor(g, dtype=torch.int64)
+        hi = torch.tensor(order) >= 3
+        v = torch.cat([E[g[~hi]].sum(0), E[g[hi]].sum(0)]) / len(g)  # the two bags, mean
+        logits = v @ W + b
         p = torch.softmax(logits, 0)
         top2 = torch.topk(logits, 2).values
         got = float(np.frombuffer(np.int64(r[i, 1]).tobytes(), np.float64)[0])
@@ -177,7 +181,7 @@ def test_langid_mfma_head_vs_fp32_reference(host, corpus, runner_parts):
             assert float(top2[0] - top2[1]) < 0.05
             near += 1
             continue
-        assert abs(got - float(p.max())) < 0.01 * float(p.max()), (i, got, float(p.max()))
+        assert abs(got - float(p.max())) < 0.015, (i, got, float(p.max()))
     assert near <= 2
 
 

@@ -50,16 +50,11 @@ def test_featurizer_gram_counts():
 
 
 def _float_reference(lid, text):
-    """Plain fp64 fastText inference of the v3 model from its int8 table (no doc-vector
-    quantisation): (language, confidence, logits)."""
-    h = native.host()
-    g = np.asarray(h.langid_buckets(text), dtype=np.int64)
-    if len(g) == 0:
+    """Plain fp64 fastText inference of the v3 model (no doc-vector quantisation):
+    (language, confidence, logits)."""
+    logits = lid.float_logits(text)
+    if logits is None:
         return -1, 0.0, None
-    E = lid.dense_E().astype(np.float64)
-    W = lid.W.reshape(h.LID_DIM, h.LID_LANGS).astype(np.float64)
-    mean = E[g].sum(0) / len(g)
-    logits = mean @ W * lid.w_scale + lid.b[:h.LID_LANGS].astype(np.float64)
     p = np.exp(logits - logits.max())
     p /= p.sum()
     return int(np.argmax(logits)), float(p.max()), logits
@@ -68,7 +63,7 @@ def _float_reference(lid, text):
 def test_v3_mfma_head_matches_float_reference():
     """The integer head (block-exponent bf16 doc vector x integer bf16 weights: what the MFMA tile
     computes) vs. fp64 inference of the same model: same language unless the top two logits are
-    within the doc vector's quantisation error, confidence within 1 %."""
+    within the doc vector's quantisation error, confidence within 0.015."""
     lid = load_default()
     assert lid.version == 3
     m = lid.native()
@@ -85,7 +80,7 @@ def test_v3_mfma_head_matches_float_reference():
             assert top2[1] - top2[0] < 0.05, (t[:40], lang, ref_lang, logits)
             near += 1
             continue
-        assert abs(conf - ref_conf) < 0.01 * ref_conf, (t[:40], conf, ref_conf)
+        assert abs(conf - ref_conf) < 0.015, (t[:40], conf, ref_conf)
     assert near <= 2
 
 
@@ -95,16 +90,17 @@ def test_v3_integer_head_reproduced_in_numpy():
     h = native.host()
     lid = load_default()
     m = lid.native()
-    E = lid.dense_E().astype(np.int64)
+    E = lid.E.reshape(h.LID_BUCKETS, h.LID_ROW_DIM).astype(np.int64)
     W = lid.W.reshape(h.LID_DIM, h.LID_LANGS).astype(np.int64)
     for t in synth.make_corpus(120, 600, seed=5) + EDGE:
-        g = np.asarray(h.langid_buckets(t), dtype=np.int64)
+        g, order = h.langid_buckets(t, True)
+        g, hi = np.asarray(g, dtype=np.int64), np.asarray(order) >= 3
         cnt, sums = m.sums(t)
         assert cnt == len(g)
         if cnt == 0:
             assert m.detect(t)[0] == -1
             continue
-        S = E[g].sum(0)
+        S = np.concatenate([E[g[~hi]].sum(0), E[g[hi]].sum(0)])  # 1-2-gram bag | 3-4-gram bag
         assert list(S) == list(sums)
         smax = int(np.abs(S).max())
         e = 0

@@ -3,10 +3,10 @@
 Two models share one featurizer: hashed character 1..4-grams of lowercased letter runs
 (csrc/common/langid.h), 65536 buckets.
 
-* **v3 (default, ``langid_v3.npz``)**: fastText with a D = 32 document vector. The embedding
-  table is block-sparse: each bucket's int8 row of 16 values feeds the lower or the upper half of
-  the vector (by the bucket's top bit), so a gather moves 16 bytes; a document's rows are summed
-  exactly, the mean doc vector is quantised to
+* **v3 (default, ``langid_v3.npz``)**: fastText with a D = 32 document vector made of two 16-dim
+  bags over one int8 embedding table (16 values per bucket, so a gather moves 16 bytes): the
+  1- and 2-grams are summed into dims 0..15, the 3- and 4-grams into dims 16..31; a document's
+  rows are summed exactly, the mean doc vector is quantised to
   integers |a| <= 255 with one exponent per document (block floating point: exact in bf16), and
   the 32 -> 5 linear head runs on the matrix cores as ``v_mfma_f32_16x16x32_bf16`` tiles of 16
   documents (k_langid_mfma) with integer bf16 weights. Every product and partial sum is an
@@ -42,7 +42,7 @@ QMAX = 255  # |integer| of the v3 doc vectors and head weights: exact in bf16
 class LangidWeights:
     b: np.ndarray                      # float32 [8] bias
     P: Optional[np.ndarray] = None     # v2: int16 [BUCKETS * ROW] fixed-point logit rows
-    E: Optional[np.ndarray] = None     # v3: int8 [BUCKETS * ROW_DIM] embedding rows (block-sparse halves)
+    E: Optional[np.ndarray] = None     # v3: int8 [BUCKETS * ROW_DIM] embedding rows (both bags)
     W: Optional[np.ndarray] = None     # v3: int16 [DIM * LANGS] integer head, |W| <= 255
     w_scale: float = 0.0               # v3: logit units per head unit
     _native: Optional[object] = None
@@ -54,8 +54,8 @@ class LangidWeights:
     @property
     def description(self) -> str:
         if self.version == 3:
-            return ("fastText int8 EmbeddingBag(65536 x 32, 16 non-zero dims per bucket) -> bf16 MFMA head "
-                    "(v_mfma_f32_16x16x32_bf16)")
+            return ("fastText int8 EmbeddingBag(65536 x 16) x 2 bags (1-2 / 3-4-grams) -> 32-dim doc vector -> "
+                    "bf16 MFMA head (v_mfma_f32_16x16x32_bf16)")
         return "hashed 1-4-gram int16 logit table"
 
     @property
@@ -77,17 +77,20 @@ class LangidWeights:
         lang, conf = self.native().detect(text)
         return (NAMES[lang], conf) if lang >= 0 else (None, 0.0)
 
-    def dense_E(self) -> np.ndarray:
-        """v3 embedding table as the dense int8 [buckets, 32] matrix it stands for (each bucket's
-        16 values in the half of the document vector it feeds, zeros in the other half)."""
+    def float_logits(self, text: str) -> Optional[np.ndarray]:
+        """v3 logits of ``text`` by plain f64 inference (mean of the two bags, head, bias; no
+        doc-vector quantisation): the reference the integer / MFMA path is checked against."""
         h = native.host()
+        g, order = h.langid_buckets(text, True)
+        if not g:
+            return None
         rd = h.LID_ROW_DIM
-        E = self.E.reshape(h.LID_BUCKETS, rd)
-        out = np.zeros((h.LID_BUCKETS, h.LID_DIM), dtype=np.int8)
-        half = np.arange(h.LID_BUCKETS) >> 15
-        out[half == 0, :rd] = E[half == 0]
-        out[half == 1, rd:] = E[half == 1]
-        return out
+        E = self.E.reshape(h.LID_BUCKETS, rd).astype(np.float64)
+        g = np.asarray(g, dtype=np.int64)
+        hi = np.asarray(order) >= 3
+        v = np.concatenate([E[g[~hi]].sum(0), E[g[hi]].sum(0)]) / len(g)
+        W = self.W.reshape(h.LID_DIM, h.LID_LANGS).astype(np.float64)
+        return v @ W * self.w_scale + self.b[:h.LID_LANGS].astype(np.float64)
 
     def head_bf16_t(self) -> np.ndarray:
         """v3 head as the MFMA B operand: uint16 bf16 bits [16 columns][32 dims] (W transposed,
@@ -99,9 +102,9 @@ class LangidWeights:
 
 
 def quantize_v3(E: np.ndarray, W: np.ndarray, b: np.ndarray) -> dict:
-    """Float fastText weights (E [buckets, 16]: each bucket's non-zero half of its 32-dim row,
-    W [32, langs], b [langs]) -> the v3 arrays: int8 E (per-tensor scale sE), integer W
-    (|W| <= 255, scale sW), w_scale = sE * sW, b."""
+    """Float fastText weights (E [buckets, 16], shared by the two bags; W [32, langs]; b [langs])
+    -> the v3 arrays: int8 E (per-tensor scale sE), integer W (|W| <= 255, scale sW),
+    w_scale = sE * sW, b."""
     h = native.host()
     sE = float(np.abs(E).max()) / 127.0 or 1.0
     Eq = np.clip(np.rint(E / sE), -127, 127).astype(np.int8)

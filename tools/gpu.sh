@@ -7,7 +7,7 @@
 # steps:
 #   test        pytest -m gpu (one process) + __graft_entry__.smoke()          -> pytest.log, smoke.log
 #   tests=K     pytest -m gpu -k K (a subset)                                    -> pytest.log
-#   bench       bench.py --steps $STEPS --warmup 2 $BENCH_ARGS                    -> bench.json
+#   bench       bench.py --steps $STEPS --warmup $WARMUP $BENCH_ARGS (the driver's 20 / 5)  -> bench.json
 #   prof        serialized-stream kernel trace (exclusive kernel times, tools/prof_summary.py)
 #               + TB_PHASE_PROF=1 per-phase wave cycles                          -> kernels_serialized.txt, phase_cycles.txt
 #   pmc         PMC counter passes (one rocprofv3 run per counter group, no tracing) -> pmc_per_kernel.txt
@@ -15,7 +15,7 @@
 #               comma-separated assignments), REPS repetitions, serialized kernel stats + bench each
 #   timeline    kernel + memory-copy trace of a few steps (tools/prof_summary.py per-step timeline)
 #   e2e         Parquet -> Parquet end to end (tools/e2e_bench.py $E2E_ARGS)   -> e2e.json
-# env: OUT (default r), STEPS (bench steps, 10), BENCH_ARGS (extra bench.py args, also used by
+# env: OUT (default r), STEPS (bench steps, 20), WARMUP (5), BENCH_ARGS (extra bench.py args, also used by
 #      prof / pmc / ab / timeline), AB, REPS (1).
 set -o pipefail
 REPO=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -23,7 +23,8 @@ cd "$REPO" || exit 1
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 D="$REPO/gpurun_out/${OUT:-r}"
 mkdir -p "$D"
-STEPS=${STEPS:-10}
+STEPS=${STEPS:-20}
+WARMUP=${WARMUP:-5}
 
 kstats() {  # kstats <dir> <log> [env...]: serialized kernel trace of a short bench
   local dir=$1 log=$2; shift 2
@@ -52,7 +53,7 @@ step_tests() {
 }
 
 step_bench() {
-  timeout -k 10 400 python3 bench.py --steps $STEPS --warmup 2 $BENCH_ARGS > "$D/bench.json" 2> "$D/bench.err"
+  timeout -k 10 400 python3 bench.py --steps $STEPS --warmup $WARMUP $BENCH_ARGS > "$D/bench.json" 2> "$D/bench.err"
   local rc=$?
   cat "$D/bench.json"
   return $rc
@@ -102,7 +103,7 @@ step_ab() {
         echo "== rep $rep: $S"
         python3 tools/prof_summary.py "$T" 2>&1 | sed -n 2,9p
         python3 tools/prof_summary.py "$T" 2>&1 | grep "GPU busy per step"
-        env $E timeout -k 10 300 python3 bench.py --steps $STEPS --warmup 2 $BENCH_ARGS 2>/dev/null | cut -c1-160
+        env $E timeout -k 10 300 python3 bench.py --steps $STEPS --warmup $WARMUP $BENCH_ARGS 2>/dev/null | cut -c1-160
       } >> "$D/ab.txt"
       rm -f "$T"
     done

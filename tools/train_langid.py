@@ -2,21 +2,22 @@
 
 Default model (v3, ``textblaster_amd/models/data/langid_v3.npz``, csrc/common/langid.h): a
 fastText classifier. Hashed character 1..4-grams (65536 buckets) -> a D = 32 mean document
-vector from a block-sparse embedding table (bucket g's int8 row of 16 values feeds dims
-[16 h, 16 h + 16), h = the bucket's top bit: 16 bytes per gather) -> linear head 32 -> 5
-languages -> softmax. Training: (1) the convex problem first — the mean-mode table of per-bucket
-logits (the head folded in, = the v2 model in float); (2) lifted to D = 32: a seeded Gaussian
-head W0 (32 x 5; each 16 x 5 half has full column rank) and E[g] = T[g] W0_h^+ for the half h
-the bucket feeds, so every bucket's row maps back to its logits exactly and all 32 dims are used;
-(3) optionally jointly fine-tuned (--finetune-epochs, default 0: on the held-out set joint
-fine-tuning from the lifted point measured 97.8 % of sentences against 98.4 % without, and
-joint training from a random start 97.3-97.5 %, profiles/langid_eval.md); (4) quantised.
+vector: two 16-dim bags over one int8 embedding table of 16 values per bucket (16 bytes per
+gather), the 1- and 2-grams summed into dims 0..15, the 3- and 4-grams into dims 16..31 ->
+linear head 32 -> 5 languages -> softmax. Training: (1) the convex problem first — the
+mean-mode table T of per-bucket logits (the head folded in, = the v2 model in float); (2)
+lifted to D = 32: a seeded Gaussian head W0 = [W_lo; W_hi] (each 16 x 5) and the minimum-norm
+E[g] with E[g] W_lo = E[g] W_hi = T[g] (16 unknowns, 10 equations: [W_lo W_hi] has full column
+rank), so every gram's row maps back to its logits exactly whichever half it feeds;
+(3) quantised (joint training of a dense D = 32 model from a random start measured 97.3-97.5 %
+of held-out sentences, joint fine-tuning from the lifted point 97.8 %: the lift keeps the convex
+solution's accuracy).
 Inference quantises the mean doc vector to 8-bit integers with one exponent per document
 (block floating point: every value is exact in bf16) and runs the head as a v_mfma_f32_16x16x32_bf16 tile of 16 documents with bf16 integer weights; every product and
 partial sum is an integer below 2^24, so the MFMA's fp32 result is exact and the CPU path
 reproduces it bit for bit.
 
-    python tools/train_langid.py [--epochs 12] [--n 10000] [--finetune-epochs 0] [--out path]
+    python tools/train_langid.py [--epochs 12] [--n 10000] [--out path]
     python tools/train_langid.py --table      # the v2 folded int16 logit table (langid_v2.npz)
 
 Training text: the hand-written sentences in models/data/langid_corpus/<lang>.txt (whole
@@ -105,53 +106,21 @@ def train_table(feats, labels, h, epochs):
 
 
 def train_fasttext(feats, labels, h, epochs, dim, finetune_epochs=0, seed=7):
-    """v3: folded table -> lifted to the block-sparse EmbeddingBag (65536 x 32, 16 non-zero dims per
-    bucket) + Linear(32, 5) -> quantize_v3."""
+    """v3: folded table -> lifted to the two-bag EmbeddingBag (65536 x 16 rows; 1-2-grams feed
+    dims 0..15, 3-4-grams dims 16..31) + Linear(32, 5) -> quantize_v3."""
     T, b0 = train_folded(feats, labels, h, epochs)
     rd = h.LID_ROW_DIM
     W0 = np.random.default_rng(seed).normal(size=(dim, len(LANGS))) / np.sqrt(rd)
-    half = (np.arange(h.LID_BUCKETS) >> 15)  # the half of the doc vector each bucket feeds
-    E0 = np.zeros((h.LID_BUCKETS, rd))
-    for hh in (0, 1):
-        Wh = W0[hh * rd:(hh + 1) * rd]
-        E0[half == hh] = T[half == hh] @ np.linalg.pinv(Wh)  # E0[g] @ W0_h == T[g]
+    Wlh = np.concatenate([W0[:rd], W0[rd:]], axis=1)  # [16, 10]
+    E0 = np.concatenate([T, T], axis=1) @ np.linalg.pinv(Wlh)  # E0[g] @ W_lo == E0[g] @ W_hi == T[g]
     if finetune_epochs > 0:
-        # the block-sparse bag as a 32-dim EmbeddingBag with the other half pinned at zero
-        full = np.zeros((h.LID_BUCKETS, dim))
-        for hh in (0, 1):
-            full[half == hh, hh * rd:(hh + 1) * rd] = E0[half == hh]
-        mask = torch.zeros(h.LID_BUCKETS, dim)
-        for hh in (0, 1):
-            mask[torch.from_numpy(half == hh), hh * rd:(hh + 1) * rd] = 1.0
-        emb = torch.nn.EmbeddingBag(h.LID_BUCKETS, dim, mode="mean")
-        head = torch.nn.Linear(dim, len(LANGS))
-        with torch.no_grad():
-            emb.weight.copy_(torch.from_numpy(full))
-            head.weight.copy_(torch.from_numpy(W0.T))
-            head.bias.copy_(torch.from_numpy(b0))
-        opt = torch.optim.Adam(list(emb.parameters()) + list(head.parameters()), lr=0.001)
-        lossf = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
-        for ep in range(finetune_epochs):
-            for idx, flat, offs in batches(feats, labels, 256, torch.randperm(len(feats))):
-                loss = lossf(head(emb(flat, offs)), labels[idx])
-                opt.zero_grad()
-                loss.backward()
-                opt.step()
-                with torch.no_grad():
-                    emb.weight.mul_(mask)
-            print(f"finetune epoch {ep} loss {loss.item():.4f}", flush=True)
-        full = emb.weight.detach().numpy().astype(np.float64)
-        for hh in (0, 1):
-            E0[half == hh] = full[half == hh, hh * rd:(hh + 1) * rd]
-        W0 = head.weight.detach().numpy().T.astype(np.float64)
-        b0 = head.bias.detach().numpy().astype(np.float64)
+        raise NotImplementedError("joint fine-tuning of the two-bag model is not implemented")
     return quantize_v3(E0, W0, b0)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--epochs", type=int, default=12)
-    ap.add_argument("--finetune-epochs", type=int, default=0, help="v3: joint fine-tuning after the lift")
     ap.add_argument("--n", type=int, default=10000)
     ap.add_argument("--table", action="store_true", help="train the v2 folded int16 logit table instead")
     ap.add_argument("--out", default=None)
@@ -170,7 +139,7 @@ def main():
         arrays = train_table(feats, labels, h, args.epochs)
         out = args.out or os.path.join(DATA_DIR, "langid_v2.npz")
     else:
-        arrays = train_fasttext(feats, labels, h, args.epochs, h.LID_DIM, args.finetune_epochs)
+        arrays = train_fasttext(feats, labels, h, args.epochs, h.LID_DIM)
         out = args.out or os.path.join(DATA_DIR, "langid_v3.npz")
     np.savez(out, **arrays)
     print("saved", out, os.path.getsize(out))

@@ -29,8 +29,6 @@ enum : int {
   PH_START = 0, PH_DECODE, PH_DICT, PH_PREFIX_HASH, PH_WORDS, PH_LINES, PH_GQ, PH_GR_LINES, PH_GR_WORDS,
   PH_GR_TOP, PH_GR_DUP, PH_FW, PH_LID, PH_GR_DUP_WALK, PH_GR_DUP_CANON, PH_GR_TOP_CANON,
   PH_C4_LOREM = 16, PH_C4_DECODE, PH_C4_LINES, PH_C4_CITE, PH_C4_WORDS, PH_C4_CODES, PH_C4_JOIN, PH_C4_SENT,
-  // finer stamps of the LDS-resident stage kernel (lds_stage.h)
-  PH_W_MASK = 24, PH_GR_RUNS, PH_GR_LINEDUP, PH_WORD_CANON, PH_GQ_CHARS, PH_NL_COUNT,
   kPhaseSlots = 32
 };
 

@@ -1,7 +1,6 @@
 // Builds the POD device plan (csrc/common/devplan.h) from step configs, and runs the device
 // document algorithms (csrc/common/docproc.h) on the host with the sequential policy.
 #include "devplan_build.h"
-#include "../common/lds_stage.h"
 
 #include <algorithm>
 #include <array>
@@ -353,87 +352,6 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
   delete plan;
 }
 
-// Host run of the LDS-resident short-document kernel (k_stage_lds, csrc/common/lds_stage.h):
-// per document the same slice (slice[i] bytes; 0 = not an LDS-path document), the same
-// allocation order and so the same overflow decisions; a document that does not fit is
-// recomputed by analyze_stage exactly as the device retry kernel does (retried[i] = 1).
-void emulate_stage_lds(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
-                       const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
-                       std::vector<int64_t>& rec, std::vector<uint32_t>& flags, const uint32_t* slice,
-                       const uint8_t* dead, std::vector<uint8_t>& retried) {
-  DevPlan* plan = new DevPlan();
-  std::memset(plan, 0, sizeof(DevPlan));
-  DevStage st = build_stage(steps, idx, *plan);
-  DevStage st_lid{};
-  bool has_lid = false;
-  for (int s = 0; s < st.n_steps; ++s)
-    if (st.steps[s].kind == DK_LANGID) {
-      has_lid = true;
-      st_lid.steps[st_lid.n_steps++] = st.steps[s];
-    }
-  st_lid.width_total = st.width_total;
-  if (has_lid && !lid) { delete plan; throw std::runtime_error("language model required"); }
-  rec.assign((size_t)st.width_total * ndocs, 0);
-  flags.assign(ndocs, 0);
-  retried.assign(ndocs, 0);
-  uint32_t maxlen = 0;
-  for (int64_t i = 0; i < ndocs; ++i) maxlen = std::max<uint32_t>(maxlen, (uint32_t)(off[i + 1] - off[i]));
-  std::vector<uint64_t> pw = pow_table(maxlen + 16);
-  const UcdView ucd = host_ucd();
-  constexpr uint32_t kGenericLds = 10240;  // the retry kernel's slice (DeviceRunner.DEFAULT_LDS_BYTES)
-  parallel_for(ndocs, nthreads, [&](int64_t a, int64_t b) {
-    std::vector<char> scratch;
-    std::vector<char> lds(kGenericLds + 16);
-    std::vector<uint64_t> arena;  // 8-byte aligned LDS slice stand-in
-    for (int64_t i = a; i < b; ++i) {
-      if (dead && dead[i]) continue;
-      const uint32_t n = (uint32_t)(off[i + 1] - off[i]);
-      const uint8_t* src = (const uint8_t*)data + off[i];
-      auto generic = [&](const DevStage& stage) {
-        const uint64_t need = scratch_bytes_for(n);
-        if (scratch.size() < need) scratch.resize(need);
-        DocCtx<SeqPar> x;
-        x.ucd = ucd;
-        x.pw = pw.data();
-        x.pw_n = (uint32_t)(pw.size() / 2 - 1);
-        x.ipw = pw.data() + x.pw_n + 1;
-        x.scr = scratch.data();
-        x.cap = need;
-        x.lds = lds.data();
-        x.lcap = kGenericLds;
-        x.flag = &flags[i];
-        StageOut out{rec.data(), (uint32_t)ndocs, (uint32_t)i};
-        analyze_stage(x, stage, *plan, lid ? lid->tables() : LidTables{nullptr, nullptr}, src, n, out);
-      };
-      bool done = false;
-      if (slice && slice[i]) {
-        const uint32_t cap = slice[i] & ~7u;
-        if (arena.size() * 8 < cap) arena.resize(cap / 8 + 1);
-        LCtx<SeqPar> x;
-        x.a.base = (char*)arena.data();
-        x.a.cap = cap;
-        x.ucd = ucd;
-        x.flag = &flags[i];
-        uint16_t* asc = x.a.get<uint16_t>(128);
-        uint8_t* tx = x.a.get<uint8_t>(n + 16);
-        if (!x.a.ovf && n <= kLdsMaxDoc) {
-          for (uint32_t c = 0; c < 128; ++c) asc[c] = compact_prop(ucd.props(c));
-          std::memcpy(tx, src, n);
-          std::memset(tx + n, 0, 16);
-          x.asc = asc;
-          done = lds_analyze_stage(x, st, *plan, tx, n, rec.data(), (uint32_t)ndocs, (uint32_t)i) == LDS_OK;
-        }
-        if (!done) retried[i] = 1;
-      }
-      if (!done) {
-        generic(st);
-      } else if (has_lid) {
-        generic(st_lid);
-      }
-    }
-  });
-  delete plan;
-}
 
 void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
                 std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,

@@ -37,10 +37,6 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
                    std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes = 0,
                    const uint8_t* dead = nullptr, bool weak_keys = false);
-void emulate_stage_lds(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
-                       const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
-                       std::vector<int64_t>& rec, std::vector<uint32_t>& flags, const uint32_t* slice,
-                       const uint8_t* dead, std::vector<uint8_t>& retried);
 void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
                 std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,
                 std::vector<uint32_t>& flags, uint32_t lds_bytes = 0, const uint8_t* dead = nullptr);

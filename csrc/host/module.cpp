@@ -859,26 +859,6 @@ PYBIND11_MODULE(_tbhost, m) {
   }, py::arg("steps"), py::arg("idx"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8,
      py::arg("lid") = nullptr, py::arg("lds_bytes") = 0, py::arg("dead") = py::none(),
      py::arg("weak_keys") = false);
-  m.def("emulate_stage_lds", [](const std::vector<StepCfg>& steps, const std::vector<int>& idx,
-                                py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
-                                py::array_t<uint32_t, py::array::c_style> slice, int nthreads,
-                                std::shared_ptr<LangidModel> lid,
-                                std::optional<py::array_t<uint8_t, py::array::c_style>> dead) {
-    std::vector<int64_t> rec;
-    std::vector<uint32_t> flags;
-    std::vector<uint8_t> retried;
-    const int64_t nd = (int64_t)off.size() - 1;
-    if ((int64_t)slice.size() < nd) throw std::runtime_error("slice array too short");
-    if (dead && (int64_t)dead->size() < nd) throw std::runtime_error("dead mask too short");
-    const uint8_t* dp = dead ? dead->data() : nullptr;
-    {
-      py::gil_scoped_release nogil;
-      emulate_stage_lds(steps, idx, nd, (const char*)data.data(), off.data(), nthreads, lid.get(), rec, flags,
-                        slice.data(), dp, retried);
-    }
-    return py::make_tuple(to_numpy(std::move(rec)), to_numpy(std::move(flags)), to_numpy(std::move(retried)));
-  }, py::arg("steps"), py::arg("idx"), py::arg("data"), py::arg("offsets"), py::arg("slice"),
-     py::arg("nthreads") = 8, py::arg("lid") = nullptr, py::arg("dead") = py::none());
   m.def("gate_host", [](const py::bytes& gate, const std::vector<py::array_t<int64_t, py::array::c_style>>& recs,
                         int64_t ndocs, py::array_t<uint32_t, py::array::c_style> flags,
                         py::array_t<uint8_t, py::array::c_style> dead, int code) {

@@ -111,13 +111,13 @@ def _hard_corpus():
     return texts
 
 
-@pytest.mark.parametrize("mode", ["default", "split", "lds", "wide"])
+@pytest.mark.parametrize("mode", ["default", "split", "wide"])
 def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
     """Independent net for the device kernels: the GPU engine against the CPU ICU oracle (not the
     host emulation of the same source) on adversarial, long, split and C4-heavy documents; with
     the GopherRepetition dup orders of every >4.5 KB document split across workgroups ("split")
-    with the LDS-resident short-document kernel ("lds"), and with every >8 KB document on the
-    1024-thread stage workgroup, half of them also split ("wide")."""
+    and with every >8 KB document on the 1024-thread stage workgroup, half of them also split
+    ("wide")."""
     import json
 
     import numpy as np
@@ -129,8 +129,6 @@ def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
 
     if mode == "split":
         monkeypatch.setenv("TB_SPLIT_DOC_BYTES", "4096")
-    if mode == "lds":
-        monkeypatch.setenv("TB_LDS_STAGE", "1")
     if mode == "wide":
         monkeypatch.setenv("TB_HUGE_DOC_BYTES", "8192")
         monkeypatch.setenv("TB_SPLIT_DOC_BYTES", "20000")
@@ -140,8 +138,6 @@ def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
     eng = Engine(cfg, backend="cuda", keep_reasons=True)
     if mode == "split":
         assert eng.device_runner.gr_split and eng.device_runner.split_doc_bytes <= 4608
-    if mode == "lds":
-        assert eng.device_runner.lds_stage
     a = eng.process(data, off)
     b = Engine(cfg, backend="cpu", segmentation="icu", keep_reasons=True).process(data, off)
     np.testing.assert_array_equal(a.status, b.status)

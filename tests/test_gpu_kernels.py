@@ -269,39 +269,3 @@ def test_split_documents_match_host_emulation(host, corpus, runner_parts, monkey
             b = ref[prefix * n:(prefix + width) * n].reshape(n, width)
             bad = np.nonzero(~np.all(a[ok] == b[ok], axis=1))[0]
             assert len(bad) == 0, (bad[:5], a[ok][bad[:3]], b[ok][bad[:3]])
-
-
-@pytest.mark.parametrize("per_byte", ["5", "64"])
-def test_lds_stage_kernel_matches_host(host, corpus, runner_parts, monkeypatch, per_byte):
-    """LDS-resident stage kernel (csrc/hip/stage_lds.hip) vs. the generic algorithm on the host:
-    with tight slices (5 bytes per text byte: most documents overflow and go through the retry
-    kernel) and with roomy ones (no retries, every dup n-gram order in one table)."""
-    from textblaster_amd.pipeline.device import KIND_LANGID, DeviceRunner
-
-    cfg, steps, plan, _, lid = runner_parts
-    monkeypatch.setenv("TB_LDS_PER_BYTE", per_byte)
-    monkeypatch.setenv("TB_LDS_STAGE", "1")
-    runner = DeviceRunner(steps, plan, "cuda:0", lid)
-    assert runner.lds_stage
-    data, off = synth.pack(corpus)
-    n = len(corpus)
-    res = runner.run(data, off)
-    compared = 0
-    for s, idx in enumerate(plan.stages):
-        ver = plan.stage_version[s]
-        vd, vo = (data, off) if ver == 0 else res.versions[ver]
-        ref, rflags = host.emulate_stage(steps, idx, np.ascontiguousarray(vd), np.ascontiguousarray(vo), 8,
-                                         lid.native())
-        _, layout = runner.stage_layout[s]
-        for (kind, width, prefix), step_i in zip(layout, idx):
-            if kind == KIND_LANGID:
-                continue
-            p = runner.pass_of_step[step_i]
-            live = ~((res.dead != 0) & (res.dead <= p)) if res.dead is not None else np.ones(n, bool)
-            ok = (res.flags == 0) & (rflags == 0) & live
-            a = res.stage_recs[s][prefix * n:(prefix + width) * n].reshape(n, width)
-            b = ref[prefix * n:(prefix + width) * n].reshape(n, width)
-            bad = np.nonzero(~np.all(a[ok] == b[ok], axis=1))[0]
-            assert len(bad) == 0, (steps[step_i].name, bad[:5], a[ok][bad[:3]], b[ok][bad[:3]])
-            compared += int(np.count_nonzero(ok))
-    assert compared > n // 4

@@ -22,7 +22,7 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32, _P],
@@ -45,10 +45,6 @@ _SIGS = {
     "tb_pow_table": [_P, _P, _U32],
     "tb_html_sizes": [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _P, _U32, _P],
     "tb_html_scatter": [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _P, _U32, _P, _P],
-    "tb_stage_lds": [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _U32, _P, _P, _P, _P, _I32,
-                     _I32],
-    "tb_stage_retry": [_P, _P, _P, _P, _P, _P, _I32, _P, ctypes.c_uint64, _I32, _P, _U32, _P, _P, _P, _P, _P, _P, _U32,
-                       _P, _P, _P],
     "tb_bpe_count": [_P, _P, _P, _P, _P, _I32, _P],
     "tb_sizeof_bpe": [],
     "tb_abi_version": [],
@@ -164,35 +160,6 @@ class Kernels:
             t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof), waves, nblocks,
             _ptr(dead))
         _check(rc, "tb_stage_analyze")
-
-    def stage_lds(self, plan, stage, bytes_, off, perm, pos0, nblocks, ndocs, rec, flags, lds_bytes, retry_cnt,
-                  retry_pos, prof=None, dead=None, waves=0, threads=64):
-        """k_stage_lds (csrc/hip/stage_lds.hip): launch positions [pos0, pos0 + nblocks) of ``perm``,
-        one wave each with ``lds_bytes`` of LDS; documents that do not fit are appended to
-        ``retry_pos`` (count in ``retry_cnt``) for :meth:`stage_retry`."""
-        if pos0 < 0 or pos0 + nblocks > perm.numel() or retry_pos.numel() < nblocks or retry_cnt.numel() < 1:
-            raise DeviceError("stage_lds: operand shapes")
-        t = self.tabs
-        rc = self.lib.tb_stage_lds(
-            self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), perm.data_ptr(), pos0,
-            nblocks, ndocs, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(),
-            flags.data_ptr(), lds_bytes, _ptr(prof), _ptr(dead), retry_cnt.data_ptr(), retry_pos.data_ptr(), waves,
-            threads)
-        _check(rc, "tb_stage_lds")
-
-    def stage_retry(self, plan, stage, bytes_, off, perm, ndocs, scratch, slice_bytes, grid, pw, pw_n, rec, flags,
-                    lds_bytes, retry_cnt, retry_pos, prof=None):
-        """k_stage_retry: the generic stage algorithm over the retry list of :meth:`stage_lds`
-        (``grid`` workgroups, each with its own ``slice_bytes`` HBM scratch slice)."""
-        if scratch.nbytes < grid * slice_bytes:
-            raise DeviceError("stage_retry: scratch smaller than grid x slice")
-        t = self.tabs
-        rc = self.lib.tb_stage_retry(
-            self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), perm.data_ptr(), ndocs,
-            scratch.data_ptr(), slice_bytes, grid, pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
-            t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof),
-            retry_cnt.data_ptr(), retry_pos.data_ptr())
-        _check(rc, "tb_stage_retry")
 
     def stage_analyze_blk(self, plan, stage, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n,
                           rec, flags, lds_bytes=0, prof=None, dead=None, gr_export=None, n_split=0, split_bytes=0,

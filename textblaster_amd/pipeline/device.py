@@ -197,33 +197,6 @@ def build_resolve(plan: ExecPlan, stage_layout, steps_native) -> Optional[bytes]
         return None
 
 
-LDS_MAX_SLICE = 159 * 1024  # the multi-wave kernels also hold a small static exchange buffer
-# LDS-resident short-document stage kernel on by default (TB_LDS_STAGE overrides)
-LDS_STAGE_DEFAULT = "0"
-
-
-def lds_buckets(lens_desc: np.ndarray, per_byte: float, fixed: int, ratio: float = 1.25, floor: int = 256):
-    """Length buckets of the LDS-resident stage kernel over a descending length array:
-    [(p0, p1, slice_bytes)] covering every position. A bucket holds lengths in (top / ratio, top]
-    (all lengths <= ``floor`` share one bucket) and gets the slice its longest document needs
-    (``per_byte`` * length + ``fixed``, 256-byte granules): waves per CU = 160 KiB / slice."""
-    out = []
-    n = len(lens_desc)
-    neg = -lens_desc.astype(np.int64)
-    p = 0
-    while p < n:
-        # the permutation is longest-first in 16-byte granules: a later document of the bucket
-        # can be up to 15 bytes longer than its first
-        top = int(lens_desc[p]) | 15
-        lo = int(top / ratio) if top > floor else -1
-        q = int(np.searchsorted(neg, -lo, side="left")) if lo >= 0 else n
-        q = max(q, p + 1)
-        sl = min(LDS_MAX_SLICE, (int(per_byte * top) + fixed + 255) // 256 * 256)
-        out.append((p, q, sl))
-        p = q
-    return out
-
-
 def launch_order(lens: np.ndarray) -> np.ndarray:
     """Longest-first launch permutation (coarse 16-byte buckets: a stable radix sort on 16-bit
     keys instead of a comparison sort of int64 lengths)."""
@@ -243,24 +216,6 @@ def lds_doc_slices(lens: np.ndarray, long_doc_bytes: int, per_byte: float, fixed
     return out
 
 
-def lds_threads_for(slice_bytes: int, wave_bytes: int) -> int:
-    """Workgroup size of k_stage_lds for a slice: one wave per ~wave_bytes of slice (1, 2 or 4
-    waves), so long short-documents keep several waves per CU busy on one slice."""
-    if wave_bytes <= 0:
-        return 64
-    nw = -(-slice_bytes // wave_bytes)
-    return 64 if nw <= 1 else 128 if nw <= 2 else 256
-
-
-def lds_waves_for(slice_bytes: int, mode: str) -> int:
-    """Register-budget variant of k_stage_lds for a slice: the unconstrained build (2 waves/SIMD, no
-    spills) when the slice allows <= 8 waves per CU anyway, else 4 or 8 waves/SIMD."""
-    if mode != "auto":
-        return int(mode)
-    per_cu = LDS_MAX_SLICE // max(slice_bytes, 1)
-    return 0 if per_cu <= 8 else 4 if per_cu <= 16 else 8
-
-
 class _Slot:
     """Per in-flight batch resources: pinned input staging buffer and device scratch arena.
     Two slots alternate, so batch k+1 can be staged and launched while batch k's results are
@@ -270,7 +225,6 @@ class _Slot:
         self.pinned = None
         self.scratch = None
         self.scratch_c4 = None
-        self.retry_scratch = None  # HBM slices of the LDS stage kernel's retry workgroups
         self.h2d_done = None  # event: the pinned staging buffer may be rewritten after it
         # per-slot streams (compute, language-id bag, long-document kernels, C4 wave / long, and
         # the copies): a batch's kernels only order against the batch that used the slot before
@@ -613,23 +567,8 @@ class DeviceRunner:
             # dynamic slice does not fit the CU's 160 KB and the launch fails with
             # HSA_STATUS_ERROR_INVALID_ALLOCATION (measured), so cap it here
             raise DeviceError("TB_LDS_BYTES_BLK must be in [0, 131072]")
-        # LDS-resident short-document stage kernel (csrc/hip/stage_lds.hip): documents up to the
-        # long-document threshold, per-length-bucket slices of TB_LDS_PER_BYTE bytes per text byte
-        # (+ TB_LDS_FIXED); TB_LDS_STAGE=0 keeps the generic kernel for them
-        self.lds_stage = os.environ.get("TB_LDS_STAGE", LDS_STAGE_DEFAULT) not in ("", "0")
-        self.lds_per_byte = float(os.environ.get("TB_LDS_PER_BYTE", "10"))
-        self.lds_fixed = int(os.environ.get("TB_LDS_FIXED", "1024"))
-        self.lds_ratio = float(os.environ.get("TB_LDS_RATIO", "1.25"))
-        self.lds_waves = os.environ.get("TB_LDS_WAVES", "auto")
-        if self.lds_waves not in ("auto", "0", "4", "8"):
-            raise DeviceError("TB_LDS_WAVES must be auto, 0, 4 or 8")
-        self.lds_wave_bytes = int(os.environ.get("TB_LDS_WAVE_BYTES", "10240"))
-        # buckets whose LDS slice would exceed this many bytes run the generic kernel instead (0: none)
-        self.lds_generic_above = int(os.environ.get("TB_LDS_GENERIC_ABOVE", "0"))
-        self.retry_grid = int(os.environ.get("TB_RETRY_GRID", "1024"))
         # pinned inputs DMA'd in place (no host staging copy); TB_ZERO_COPY=0 forces the copy
         self.zero_copy = os.environ.get("TB_ZERO_COPY", "1") != "0"
-        self.retry_slice = int(h.scratch_bytes_for(max(self.long_doc_bytes, 1) + 16)) // SCRATCH_ALIGN * SCRATCH_ALIGN + SCRATCH_ALIGN
         # the cooperative-gather bag keeps its sums in registers; LDS holds only the cut offset
         self.lds_bytes_lid = int(os.environ.get("TB_LDS_BYTES_LID", "256"))
         if self.lds_bytes_lid < 16:
@@ -779,8 +718,7 @@ class DeviceRunner:
         names = {0: "start", 1: "decode", 2: "dict", 3: "prefix_hash", 4: "words", 5: "lines", 6: "gopher_quality",
                  7: "gr_lines_paras", 8: "gr_word_hash", 9: "gr_top_ngrams", 10: "gr_dup_ngrams", 11: "fineweb",
                  12: "langid", 13: "gr_dup_walk", 14: "gr_dup_canon", 15: "gr_top_canon", 16: "c4_lorem", 17: "c4_decode", 18: "c4_lines", 19: "c4_cite", 20: "c4_words",
-                 21: "c4_codes", 22: "c4_join", 23: "c4_sentences", 24: "w_mask", 25: "gr_runs", 26: "gr_line_dup",
-                 27: "gr_word_canon", 28: "gq_chars", 29: "nl_count"}
+                 21: "c4_codes", 22: "c4_join", 23: "c4_sentences"}
         lines = []
         for k, tot in self.phase_totals.items():
             nd = max(1, self.phase_docs[k])
@@ -945,34 +883,7 @@ class DeviceRunner:
                                              self.lds_bytes_mid, prof, self.stage_waves, n_mid - n_long, skip)
                         ev_blk = self._record(slot.s_blk)
                         keep.append(ev_blk)
-                if n_mid < ndocs and self.lds_stage:
-                    # LDS-resident kernel per length bucket, then the generic retry of the
-                    # documents that did not fit their slice
-                    nshort = ndocs - n_mid
-                    retry_cnt = rt.zeros(1, np.uint32)
-                    retry_pos = rt.empty(nshort, np.int32)
-                    keep += [retry_cnt, retry_pos]
-                    if slot.retry_scratch is None:
-                        slot.retry_scratch = rt.empty(self.retry_grid * self.retry_slice, np.uint8)
-                    with self._ktimed(keep, f"stage{s}"):
-                        for p0, p1, sl in lds_buckets(lens_perm[n_mid:], self.lds_per_byte, self.lds_fixed,
-                                                      self.lds_ratio):
-                            if self.lds_generic_above and sl > self.lds_generic_above:
-                                # hybrid: this bucket's documents take the generic wave kernel
-                                # (HBM scratch arrays, small LDS slice, higher occupancy)
-                                a0 = n_mid + p0
-                                self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[a0:], ndocs,
-                                                     scratch, d_soff[a0:], pw, pw_n, rec, flags,
-                                                     self.lds_bytes, prof, self.stage_waves, p1 - p0, skip)
-                                continue
-                            self.k.stage_lds(self.plan_t, self.stage_ts[s], vb, vo, d_perm, n_mid + p0, p1 - p0, ndocs,
-                                             rec, flags, sl, retry_cnt, retry_pos, prof, skip,
-                                             lds_waves_for(sl, self.lds_waves),
-                                             lds_threads_for(sl, self.lds_wave_bytes))
-                        self.k.stage_retry(self.plan_t, self.stage_ts[s], vb, vo, d_perm, ndocs, slot.retry_scratch,
-                                           self.retry_slice, min(self.retry_grid, nshort), pw, pw_n, rec, flags,
-                                           self.lds_bytes, retry_cnt, retry_pos, prof)
-                elif n_mid < ndocs:
+                if n_mid < ndocs:
                     with self._ktimed(keep, f"stage{s}"):
                         self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_mid:], ndocs,
                                              scratch, d_soff[n_mid:], pw, pw_n, rec, flags,
@@ -1163,8 +1074,6 @@ class EmulatedRunner:
         self.resolve_blob = None
         if os.environ.get("TB_DEVICE_RESOLVE", "1") not in ("", "0"):
             self.resolve_blob = build_resolve(plan, self.stage_layout, steps_native)
-        self.lds_stage = os.environ.get("TB_LDS_STAGE", LDS_STAGE_DEFAULT) not in ("", "0")
-        self.lds_per_byte = float(os.environ.get("TB_LDS_PER_BYTE", "10"))
         self.bpe = []
         if self.resolve_blob is not None and os.environ.get("TB_DEVICE_TOKENS", "1") not in ("", "0"):
             self.bpe = list(token_counters or [])
@@ -1192,14 +1101,7 @@ class EmulatedRunner:
                 fl = _dict_script_flags(vd, vo)  # k_langid_features raises DOC_NEEDS_CPU for these
             elif kind == "stage":
                 vd, vo = versions[self.plan.stage_version[x]]
-                if self.lds_stage:
-                    # the LDS-resident kernel's algorithm with the device's per-bucket slices
-                    sl = lds_doc_slices(np.diff(vo), DeviceRunner.DEFAULT_LONG_DOC_BYTES, self.lds_per_byte, 1024)
-                    rec, fl, _ = h.emulate_stage_lds(self.steps, self.plan.stages[x], vd, vo, sl, self.nthreads,
-                                                     self.lid, skip)
-                else:
-                    rec, fl = h.emulate_stage(self.steps, self.plan.stages[x], vd, vo, self.nthreads, self.lid, 0,
-                                              skip)
+                rec, fl = h.emulate_stage(self.steps, self.plan.stages[x], vd, vo, self.nthreads, self.lid, 0, skip)
                 if x in lid_rec:
                     for k, width, prefix in self.stage_layout[x][1]:
                         if k == KIND_LANGID:

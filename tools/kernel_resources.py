@@ -13,7 +13,7 @@ def main():
     flags = sys.argv[1:]
     text = ""
     with tempfile.TemporaryDirectory() as d:
-        for src in ("kernels.hip", "stage_lds.hip", "bpe.hip", "html.hip"):
+        for src in ("kernels.hip", "bpe.hip", "html.hip"):
             subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--offload-device-only",
                             "-S", *flags, os.path.join(ROOT, "csrc/hip", src), "-o", os.path.join(d, "k.s")],
                            check=True)

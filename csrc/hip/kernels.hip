@@ -94,9 +94,10 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
   if (x.par.leader() && src[0] >= 0) src[0] += slice_begin;
 }
 
-// The stage kernel is register-bound (occupancy = waves/SIMD the VGPR budget allows). Variants
-// with a forced waves-per-EU budget trade spills for occupancy; tb_stage_analyze picks one by
-// its `waves` argument (0 = compiler default).
+// The stage kernel is register-bound (occupancy = waves/SIMD the VGPR budget allows): it is built
+// for 4 waves/SIMD (128 VGPRs, a few bytes of spill). The unconstrained build (166 VGPRs, 3
+// waves/SIMD) and 5- / 6-wave budgets (spilling 180 / 240 B) measured 2-4 % slower
+// (profiles/README.md, round 2), so only this variant is built.
 #define TB_STAGE_KERNEL(NAME, ATTR)                                                                   \
   __global__ __launch_bounds__(64) ATTR void NAME(                                                   \
       const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes, \
@@ -114,10 +115,7 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
     analyze_stage<WavePar, false>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out); /* LD: own kernel */ \
   }
 
-TB_STAGE_KERNEL(k_stage_analyze, )
 TB_STAGE_KERNEL(k_stage_analyze_w4, __attribute__((amdgpu_waves_per_eu(4, 8))))
-TB_STAGE_KERNEL(k_stage_analyze_w5, __attribute__((amdgpu_waves_per_eu(5, 8))))
-TB_STAGE_KERNEL(k_stage_analyze_w6, __attribute__((amdgpu_waves_per_eu(6, 8))))
 
 // Long documents: one workgroup of kBlockThreads (8 waves by default) per document (BlockPar), launched
 // over the long prefix of the length-sorted permutation.
@@ -846,8 +844,8 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
   if (nblocks <= 0) nblocks = ndocs;  // grid: docs perm[0 .. nblocks)
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
-  auto kern = waves == 4 ? k_stage_analyze_w4 : waves == 5 ? k_stage_analyze_w5 : waves == 6 ? k_stage_analyze_w6
-                                                                                              : k_stage_analyze;
+  if (waves != 4) return (int)hipErrorInvalidValue;  // the one build (see TB_STAGE_KERNEL)
+  auto kern = k_stage_analyze_w4;
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64), lds_bytes, stream, (const DevPlan*)plan,

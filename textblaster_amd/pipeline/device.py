@@ -374,15 +374,13 @@ class DeviceRunner:
     DEFAULT_LDS_BYTES = 10240
     DEFAULT_LDS_BYTES_C4 = 2560
     DEFAULT_LONG_DOC_BYTES = 4096  # with the 3-per-CU workgroup kernel (profiles/r2_c5/long_doc_threshold.txt)
-    DEFAULT_MID_DOC_BYTES = 0        # 0: no separate mid-size launch
-    DEFAULT_LDS_BYTES_MID = 32768
     DEFAULT_LDS_BYTES_BLK = 49152
     DEFAULT_SPLIT_DOC_BYTES = 65536
     # 1024-thread stage workgroups (k_stage_analyze_blk1k) above this size; off by default: at the
     # 80-VGPR budget the wider variant spills (872 B/lane) and is slower than 512 threads on ~1 MB
     # documents (profiles/r3_long: 685 vs 728 docs/s at 128 docs/step, 1081 vs 1444 at 384)
     DEFAULT_HUGE_DOC_BYTES = 0
-    DEFAULT_STAGE_WAVES = 4  # stage kernel occupancy variant (0 = compiler default; A/B: tools/gpu.sh ab)
+    DEFAULT_STAGE_WAVES = 4  # the stage kernel's register budget (the one variant built, kernels.hip)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None, max_batch_bytes: int = 384 << 20,
                  token_counters=None):
@@ -532,15 +530,11 @@ class DeviceRunner:
         self.lds_bytes_c4 = int(os.environ.get("TB_LDS_BYTES_C4", str(self.DEFAULT_LDS_BYTES_C4)))
         if not 0 <= self.lds_bytes_c4 <= 131072:
             raise DeviceError("TB_LDS_BYTES_C4 must be in [0, 131072]")
-        self.stage_waves = int(os.environ.get("TB_STAGE_WAVES", str(self.DEFAULT_STAGE_WAVES)))
+        self.stage_waves = self.DEFAULT_STAGE_WAVES
         # documents longer than this run one workgroup (4 waves) each instead of one wave
         self.long_doc_bytes = int(os.environ.get("TB_LONG_DOC_BYTES", str(self.DEFAULT_LONG_DOC_BYTES)))
-        # mid-size documents (one wave each, like the short ones) get their own launch with a larger
-        # LDS slice so their code point arrays and hash tables stay on chip (fewer of them per CU)
-        self.mid_doc_bytes = int(os.environ.get("TB_MID_DOC_BYTES", str(self.DEFAULT_MID_DOC_BYTES)))
-        self.lds_bytes_mid = int(os.environ.get("TB_LDS_BYTES_MID", str(self.DEFAULT_LDS_BYTES_MID)))
-        if not 0 <= self.lds_bytes_mid <= 131072 or not 0 <= self.lds_bytes <= 131072:
-            raise DeviceError("TB_LDS_BYTES / TB_LDS_BYTES_MID must be in [0, 131072]")
+        if not 0 <= self.lds_bytes <= 131072:
+            raise DeviceError("TB_LDS_BYTES must be in [0, 131072]")
         # 48 KB: three long-document workgroups per CU (with the 6-wave register budget of
         # k_stage_analyze_blk, csrc/hip/kernels.hip TB_BLK_WPE)
         self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", str(self.DEFAULT_LDS_BYTES_BLK)))
@@ -758,9 +752,8 @@ class DeviceRunner:
         np.cumsum(per_doc[perm], out=scratch_off[1:])
         maxlen = int(lens.max()) if ndocs else 0
         n_long = int(np.count_nonzero(lens > self.long_doc_bytes)) if self.long_doc_bytes > 0 else 0
-        # perm is longest first: [0, n_long) workgroup docs, [n_long, n_mid) mid-size wave docs
-        n_mid = int(np.count_nonzero(lens > self.mid_doc_bytes)) if self.mid_doc_bytes > 0 else n_long
-        n_mid = max(n_mid, n_long)
+        # perm is longest first: [0, n_long) workgroup docs, then the wave docs
+        n_mid = n_long
         direct_keep: List = []
         # per-document bad-words roots / CJK flags and the long documents' segment lists travel in
         # the same upload
@@ -873,16 +866,6 @@ class DeviceRunner:
                                          flags, self._prof_buf(ndocs, keep, f"langid{s}"))
                         ev_lid = self._record(slot.s_lid)
                         keep.append(ev_lid)
-                if n_mid > n_long:
-                    # mid-size documents on the long-document stream, after its workgroup kernel
-                    if ev_blk is None:
-                        slot.s_blk.wait_event(ev_pre)
-                    with rt.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_mid"):
-                        self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,
-                                             scratch, d_soff[n_long:], pw, pw_n, rec, flags,
-                                             self.lds_bytes_mid, prof, self.stage_waves, n_mid - n_long, skip)
-                        ev_blk = self._record(slot.s_blk)
-                        keep.append(ev_blk)
                 if n_mid < ndocs:
                     with self._ktimed(keep, f"stage{s}"):
                         self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_mid:], ndocs,

@@ -36,6 +36,7 @@ import json
 import logging
 import os
 import queue
+import resource
 import shutil
 import threading
 import time
@@ -152,6 +153,8 @@ class _UnitReader:
         self._rg = -1
         self._tbl = None
         self.seconds = 0.0
+        self.cpu = 0.0  # CPU seconds of the threads that read through this object
+        self.lock = threading.Lock()
         # worker threads open their own ParquetFile (a reader object is not shared across threads)
         self._pf = pq.ParquetFile(reader.config.path, memory_map=True) if own_file else None
         # several reader threads decode row groups side by side: Arrow's own column threads on
@@ -159,12 +162,13 @@ class _UnitReader:
         self._use_threads = not own_file
 
     def read(self, u: Unit) -> DocBatch:
-        t0 = time.perf_counter()
+        t0, c0 = time.perf_counter(), time.thread_time()
         try:
             with tracing.trace_range("tb.read"):
                 return self._read(u)
         finally:
             self.seconds += time.perf_counter() - t0
+            self.cpu += time.thread_time() - c0
 
     def _read(self, u: Unit) -> DocBatch:
         if u.row_group != self._rg:
@@ -348,7 +352,8 @@ class _Prefetcher:
         self.stop = threading.Event()
         self._end = object()
         self._gen = gen
-        self.t = threading.Thread(target=self._work, name="tb-prefetch", daemon=True)
+        self.t = threading.Thread(target=lambda: (tracing.name_os_thread("tb-prefetch"), self._work()),
+                                  name="tb-prefetch", daemon=True)
         self.t.start()
 
     def _put(self, item) -> bool:
@@ -403,14 +408,17 @@ def _read_units(reader: ParquetReader, units: List[Unit], nthreads: int, timer: 
     def load(group: List[Unit]):
         r = _UnitReader(reader, own_file=nthreads > 1)
         out = [(u, r.read(u)) for u in group]
-        timer.seconds += r.seconds
+        with timer.lock:
+            timer.seconds += r.seconds
+            timer.cpu += r.cpu
         return out
 
     if nthreads <= 1:
         for g in groups:
             yield from load(g)
         return
-    with cf.ThreadPoolExecutor(max_workers=nthreads, thread_name_prefix="tb-reader") as ex:
+    with cf.ThreadPoolExecutor(max_workers=nthreads, thread_name_prefix="tb-reader",
+                               initializer=tracing.name_os_thread, initargs=("tb-reader",)) as ex:
         pending: collections.deque = collections.deque()
         it = iter(groups)
         for g in it:
@@ -438,16 +446,20 @@ class _Writer:
 
         self.sink = sink
         self.compression = compression
-        self.pool = cf.ThreadPoolExecutor(max_workers=max(1, threads), thread_name_prefix="tb-encode")
+        self.pool = cf.ThreadPoolExecutor(max_workers=max(1, threads), thread_name_prefix="tb-encode",
+                                          initializer=tracing.name_os_thread, initargs=("tb-encode",))
         self.q: queue.Queue = queue.Queue(maxsize=depth or max(1, threads) + 2)
         self.err: List[BaseException] = []
         self.seconds = 0.0
+        self.cpu_encode = 0.0  # CPU seconds of the encoder threads / the committer thread
+        self.cpu_write = 0.0
         self._lock = threading.Lock()
-        self.t = threading.Thread(target=self._run, name="tb-writer", daemon=True)
+        self.t = threading.Thread(target=lambda: (tracing.name_os_thread("tb-writer"), self._run()), name="tb-writer",
+                                  daemon=True)
         self.t.start()
 
     def _encode(self, job):
-        t0 = time.perf_counter()
+        t0, c0 = time.perf_counter(), time.thread_time()
         batch, res, unit, counts = job
         with tracing.trace_range("tb.part_table"):
             kept, exc = self._tables(batch, res)
@@ -456,6 +468,7 @@ class _Writer:
                    (encode_table(exc, self.compression), exc.num_rows), counts)
         with self._lock:
             self.seconds += time.perf_counter() - t0
+            self.cpu_encode += time.thread_time() - c0
         return out
 
     def _run(self):
@@ -467,11 +480,12 @@ class _Writer:
                 unit, kept, exc, counts = fut.result()
                 if self.err:
                     continue
-                t0 = time.perf_counter()
+                t0, c0 = time.perf_counter(), time.thread_time()
                 with tracing.trace_range("tb.write"):
                     self.sink.commit(unit, kept, exc, counts)
                 with self._lock:
                     self.seconds += time.perf_counter() - t0
+                    self.cpu_write += time.thread_time() - c0
             except BaseException as e:  # noqa: BLE001 - re-raised on the main thread
                 self.err.append(e)
 
@@ -522,6 +536,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     cfg = cfg or load_pipeline_config(rc.pipeline_config)
     nsteps = len(cfg.pipeline)
     t_start = time.perf_counter()
+    ru_start = resource.getrusage(resource.RUSAGE_SELF)
     rank_fault = _parse_rank_fault(rc.fault_inject, world)
     html_dec = None
     if rc.html_decode == "gpu":
@@ -655,7 +670,14 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
         writer.close()
     hb.finish(local.vector(nsteps))
     phase = {"setup": setup_s, "read": ureader.seconds, "write": writer.seconds,
-             "main_loop": time.perf_counter() - t_loop}
+             "main_loop": time.perf_counter() - t_loop,
+             # CPU seconds by thread group: Parquet decode (reader threads; their HTML decoding runs
+             # on the native pool, counted under "other"), output encode, part commits; other = the
+             # process total minus those (main loop, engine threads, native pools)
+             "cpu_read": ureader.cpu, "cpu_encode": writer.cpu_encode, "cpu_write": writer.cpu_write}
+    ru_end = resource.getrusage(resource.RUSAGE_SELF)
+    phase["cpu_total"] = (ru_end.ru_utime - ru_start.ru_utime) + (ru_end.ru_stime - ru_start.ru_stime)
+    phase["cpu_other"] = phase["cpu_total"] - phase["cpu_read"] - phase["cpu_encode"] - phase["cpu_write"]
     log.info("rank %d phases: %s", rank, {k: round(v, 3) for k, v in phase.items()})
     elapsed = time.perf_counter() - t_start
     total_vec = ctx.all_reduce_sum(local.vector(nsteps))

@@ -47,6 +47,29 @@ def make_input(path: str, ndocs: int, mean_bytes: int, pool: int, row_group: int
     return total
 
 
+def thread_cpu() -> dict:
+    """CPU seconds per OS thread name of this process (/proc/self/task/*/stat; the runner names
+    its reader / encoder / writer / prefetch threads, the native pool is "tb-pool")."""
+    out: dict = {}
+    tck = os.sysconf("SC_CLK_TCK")
+    for t in os.listdir("/proc/self/task"):
+        try:
+            st = open(f"/proc/self/task/{t}/stat").read()
+        except OSError:
+            continue
+        name = st[st.index("(") + 1:st.rindex(")")]
+        f = st[st.rindex(")") + 2:].split()
+        out[(t, name)] = (int(f[11]) + int(f[12])) / tck
+    return out
+
+
+def cpu_by_name(before: dict, after: dict) -> dict:
+    agg: dict = {}
+    for k, v in after.items():
+        agg[k[1]] = agg.get(k[1], 0.0) + v - before.get(k, 0.0)
+    return {n: round(v, 3) for n, v in sorted(agg.items(), key=lambda kv: -kv[1]) if v > 0.005}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--docs", type=int, default=1_000_000)
@@ -82,12 +105,19 @@ def main():
         e = os.path.join(args.out, f"{backend}.excluded.parquet")
         tl = os.path.join(args.out, f"timeline_{backend}.json") if args.timeline else None
         tracing.record_timeline(tl)
+        cpu0 = thread_cpu()
         st = run(RunConfig(inp, o, e, args.config, backend=backend, unit_rows=args.unit_rows,
                            html_decode=args.html_decode))
+        cpu = cpu_by_name(cpu0, thread_cpu())
         line = {"backend": backend, "docs": st.docs, "kept": st.kept, "excluded": st.excluded, "errors": st.errors,
                 "seconds": round(st.seconds, 3), "docs_per_sec": round(st.docs_per_sec, 1),
                 "step_filtered": st.step_filtered, "delegated": st.delegated,
-                "phase_seconds": {k: round(v, 3) for k, v in st.phase_seconds.items()}}
+                "phase_seconds": {k: round(v, 3) for k, v in st.phase_seconds.items() if not k.startswith("cpu_")},
+                # host CPU seconds per thread group over the run (runner accounting) and per OS
+                # thread name of the threads alive at its end (native pools)
+                "cpu_seconds": {k[4:]: round(v, 3) for k, v in st.phase_seconds.items() if k.startswith("cpu_")},
+                "cpu_us_per_doc": round(1e6 * st.phase_seconds.get("cpu_total", 0.0) / max(st.docs, 1), 3),
+                "cpu_seconds_by_os_thread": cpu}
         print(json.dumps(line), flush=True)
         rates.setdefault(backend, []).append(line["docs_per_sec"])
         if tl:

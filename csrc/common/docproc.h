@@ -224,8 +224,8 @@ struct DocCtx {
   TB_HD void set_flag(uint32_t f) {
     if (flag) P::or32(flag, f);  // atomic: kernels of different steps may run concurrently
   }
-  TB_HD uint64_t powb(uint32_t k) const { return k <= pw_n ? pw[k] : powmod61(kHashBase, k); }
-  TB_HD uint64_t ipowb(uint32_t k) const { return (ipw && k <= pw_n) ? ipw[k] : powmod61(kHashBaseInv, k); }
+  TB_HD uint64_t powb(uint32_t k) const { return k <= pw_n ? pw[k] : hpow(kHashBase, k); }
+  TB_HD uint64_t ipowb(uint32_t k) const { return (ipw && k <= pw_n) ? ipw[k] : hpow(kHashBaseInv, k); }
   // `count` elements from the bottom of the LDS slice, or nullptr when they do not fit
   template <class T>
   TB_HD T* try_lds(uint64_t count) {
@@ -298,8 +298,7 @@ TB_HD Cps decode(DocCtx<P>& x, const uint8_t* b, uint32_t n, bool hot = false, u
 template <class P>
 TB_HD uint64_t span_hash8(const DocCtx<P>& x, const PHView& v, uint32_t s, uint32_t e) {
   const uint64_t hs = v.at(s), he = v.at(e);
-  const uint64_t t = mulmod61(hs, x.powb(e - s));
-  return he >= t ? he - t : he + kM61 - t;
+  return he - hs * x.powb(e - s);
 }
 
 template <class P>
@@ -316,8 +315,8 @@ TB_HD PHView prefix_hash8(DocCtx<P>& x, const uint8_t* b, uint32_t n) {
   HL tot = x.par.template scan<HL>(
       nblk, HL{0, 0, 0},
       [&](const HL& a, const HL& c) {
-        uint64_t m = c.len <= pwn ? pw[c.len] : powmod61(kHashBase, c.len);
-        return HL{addmod61(mulmod61(a.h, m), c.h), a.len + c.len, 0};
+        uint64_t m = c.len <= pwn ? pw[c.len] : hpow(kHashBase, c.len);
+        return HL{a.h * m + c.h, a.len + c.len, 0};
       },
       [&](uint32_t k) {
         const uint32_t s0 = k << 3, e0 = s0 + 8 < n ? s0 + 8 : n;
@@ -366,7 +365,22 @@ TB_HD Words words(DocCtx<P>& x, const Cps& c) {
   const PropArr prop = c.props();
   const OffArr off = c.offs();
   CpsAcc acc{prop};
-  x.par.mask_bits(C + 1, [&](uint32_t i) { return i == 0 || i == C || wb_break(acc, (int)C, (int)i); }, wbm);
+  // The rules are first decided from the properties of i-2 .. i+1 (wb_break_ctx: straight-line
+  // compares, no look-around loops); only windows holding Extend / Format / ZWJ / RI take the
+  // general rule walk, so a chunk with punctuation or digits does not serialise the wave on it.
+#ifndef TB_WB_CTX
+#define TB_WB_CTX 1
+#endif
+  x.par.mask_bits(C + 1, [&](uint32_t i) {
+    if (i == 0 || i == C) return true;
+    if (TB_WB_CTX) {
+      const uint32_t pm2 = i >= 2 ? prop[i - 2] : 0xFFFFFFFFu;
+      const uint32_t pp1 = i + 1 < C ? prop[i + 1] : 0xFFFFFFFFu;
+      const int r = wb_break_ctx(pm2, prop[i - 1], prop[i], pp1);
+      if (r != 2) return r != 0;
+    }
+    return wb_break(acc, (int)C, (int)i);
+  }, wbm);
   x.par.sync();
   auto bit = [&](uint32_t i) { return (wbm[i >> 5] >> (i & 31)) & 1u; };
   uint32_t *cs = w.cs, *ce = w.ce, *bs = w.bs, *be = w.be;
@@ -802,7 +816,54 @@ struct StageOut {
   uint32_t ndocs;
   uint32_t doc;
   GrExport* gr_export = nullptr;  // non-null: split mode for this document (see GrExport)
+  // non-null: this document's C4 line export (LineStat region, see export_line_stats), for the C4
+  // pass of the same content version
+  uint32_t* line_stats = nullptr;
 };
+
+// The C4 line export of one document: a header (line count, or kLineStatsNone while / when the
+// stage did not export) and per Rust line its trimmed byte span, word count and longest word in
+// code points. Region of document d at u32 index line_stats_base(off[d], d) of the batch buffer
+// (4 * (total bytes / 8 + 16 * documents) + 16 u32): room for line_stats_cap(n) lines.
+constexpr uint32_t kLineStatsNone = 0xFFFFFFFFu;
+struct alignas(16) LineStat { uint32_t bs, be, nw, mx; };
+TB_HD uint64_t line_stats_base(int64_t off_d, int64_t d) { return 4ull * ((uint64_t)off_d / 8u + 16ull * (uint64_t)d); }
+TB_HD uint32_t line_stats_cap(uint32_t n) { return n / 8u + 15u; }
+
+// C4 line export from the stage's words and lines (StageOut::line_stats): per Rust line its span
+// trimmed of whitespace (in bytes), its words — those whose first code point lies in [ls, le):
+// words never cross a line feed, and the position-ordered word list makes them a contiguous
+// range found by two binary searches — and their longest length in code points. The header is
+// written last; documents with more lines than the region holds keep kLineStatsNone.
+template <class P>
+TB_HD void export_line_stats(DocCtx<P>& x, const Cps& c, const Words& w, const Lines& L, uint32_t n, uint32_t* out) {
+  if (L.n > line_stats_cap(n)) return;
+  const PropArr prop = c.props();
+  const OffArr off = c.offs();
+  LineStat* ls = (LineStat*)(out + 4);
+  auto lower = [&](uint32_t v) {  // first word with cs >= v
+    uint32_t lo = 0, hi = w.n;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (w.cs[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+  };
+  x.par.for_n(L.n, [&](uint32_t k) {
+    uint32_t s0 = L.ls[k], e0 = L.le[k];
+    const uint32_t a = lower(s0), e = lower(e0);
+    uint32_t mx = 0;
+    for (uint32_t q = a; q < e; ++q) {
+      const uint32_t len = w.ce[q] - w.cs[q];
+      mx = len > mx ? len : mx;
+    }
+    while (s0 < e0 && is_ws(prop[s0])) ++s0;
+    while (e0 > s0 && is_ws(prop[e0 - 1])) --e0;
+    ls[k] = LineStat{off[s0], off[e0], e - a, mx};
+  });
+  x.par.sync();
+  x.par.single([&]() { out[0] = L.n; });
+}
 
 // The duplicated n-gram key / equality of order n over the exported word arrays (one definition
 // for the in-stage path and the split kernel): grams are equal iff their concatenations are.
@@ -815,8 +876,7 @@ struct DupGrams {
   const uint32_t* be;
   const uint8_t* b;
   TB_HD uint64_t run_hash(uint32_t p, uint32_t n) const {
-    const uint64_t d = K[p + n] >= K[p] ? K[p + n] - K[p] : K[p + n] + kM61 - K[p];
-    return mulmod61(PB[p + n], d);
+    return PB[p + n] * (K[p + n] - K[p]);
   }
   TB_HD uint64_t key(uint32_t p, uint32_t n) const { return dev_key(run_hash(p, n), WL[p + n] - WL[p]); }
   TB_HD bool eq(uint32_t p, uint32_t q, uint32_t n) const {
@@ -948,8 +1008,7 @@ TB_HD int64_t dup_walk_wave(const P& par, uint32_t G, uint32_t n, const GcT* gc,
 }
 
 TB_HD uint64_t span_hash(uint64_t pa, uint64_t pb, uint64_t blen_pow) {
-  uint64_t x = mulmod61(pa, blen_pow);
-  return pb >= x ? pb - x : pb + kM61 - x;
+  return pb - pa * blen_pow;
 }
 
 // Sentence count of split_into_sentences() over code points [s, e) (already trimmed text),
@@ -1096,25 +1155,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
   uint32_t* WL = nullptr;
   uint64_t* K = nullptr;
   uint64_t* PB = nullptr;
-  // The last GopherRepetition step of a stage hands the top of the LDS slice (code point arrays,
-  // prefix hashes) to the n-gram phase: the word hashes, the last reader of the prefix hashes,
-  // go to HBM scratch first, so the word-level arrays below get the slice (read by every n-gram
-  // key and equality test) instead of spilling to HBM.
-#ifndef TB_EARLY_RELEASE
-#define TB_EARLY_RELEASE 1
-#endif
-  const bool early_release = TB_EARLY_RELEASE && release_props && !ex && ngrams;
   if (ngrams) {
-    uint64_t* wh = nullptr;
-    auto mw = x.mark();
-    if (early_release) {
-      wh = x.template alloc<uint64_t>(W + 1);
-      if (x.overflow) return;
-      x.par.for_n(W, [&](uint32_t k) { wh[k] = span_hash8(x, ph, w.bs[k], w.be[k]); });
-      x.par.sync();
-      x.release_hi();
-      mw = x.mark();
-    }
     // LDS only while a canonicalisation table for W elements (~6 W bytes) still fits next to them
     // (split mode: HBM, they outlive this kernel)
     const uint64_t tab_bytes = 6ull * W + 64;
@@ -1122,14 +1163,11 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     WL = ex ? x.template alloc<uint32_t>(W + 1) : x.template alloc_hot_keep<uint32_t>(W + 1, tab_bytes);
     K = ex ? x.template alloc<uint64_t>(W + 1) : x.template alloc_hot_keep<uint64_t>(W + 1, tab_bytes);
     PB = ex ? x.template alloc<uint64_t>(W + 1) : x.template alloc_hot_keep<uint64_t>(W + 1, tab_bytes);
-    if (!early_release) {
-      mw = x.mark();
-      wh = x.template alloc_hot_hi<uint64_t>(W + 1);
-      if (x.overflow) return;
-      x.par.for_n(W, [&](uint32_t k) { wh[k] = span_hash8(x, ph, w.bs[k], w.be[k]); });
-      x.par.sync();
-    }
+    const auto mw = x.mark();
+    uint64_t* wh = x.template alloc_hot_hi<uint64_t>(W + 1);
     if (x.overflow) return;
+    x.par.for_n(W, [&](uint32_t k) { wh[k] = span_hash8(x, ph, w.bs[k], w.be[k]); });
+    x.par.sync();
     canonicalize(
         x, W, [&](uint32_t k) { return dev_key(wh[k], w.be[k] - w.bs[k]); },
         [&](uint32_t i, uint32_t j) { return bytes_eq<P>(b, w.bs[i], w.be[i], w.bs[j], w.be[j]); }, wid);
@@ -1140,17 +1178,17 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     x.par.sync();
     x.par.for_n(W + 1, [&](uint32_t k) { PB[k] = x.powb(WL[k]); });
     const uint64_t ktot = x.par.template scan<uint64_t>(
-        W, 0ull, [](uint64_t a, uint64_t c2) { return addmod61(a, c2); },
-        [&](uint32_t j) { return mulmod61(wh[j], x.ipowb(WL[j + 1])); }, [&](uint32_t k, uint64_t e) { K[k] = e; });
+        W, 0ull, [](uint64_t a, uint64_t c2) { return a + c2; },
+        [&](uint32_t j) { return wh[j] * x.ipowb(WL[j + 1]); }, [&](uint32_t k, uint64_t e) { K[k] = e; });
     x.par.single([&]() { K[W] = ktot; });
     x.par.sync();
-    if (!early_release) x.reset(mw);  // wh (early release: wh stays in HBM below the arrays)
+    x.reset(mw);  // wh
     if (x.overflow) return;
   }
   x.stamp(PH_GR_WORDS);
   // the n-gram statistics read words, bytes and the arrays above only: the top of the LDS slice
   // (code point arrays, prefix hashes) goes to their hash tables
-  if (release_props && !early_release) x.release_hi();
+  if (release_props) x.release_hi();
   if (ngrams) {
     const DupGrams dg{wid, WL, K, PB, w.bs, w.be, b};
     // Top n-grams (space-joined grams: equal iff their word sequences are equal). Canonical ids
@@ -1536,6 +1574,54 @@ TB_HD constexpr uint32_t pack3(const char* p) {
 // Bits of the per-line pattern flags (c4_pass_a)
 enum : uint32_t { C4F_JS = 1, C4F_POLICY = 2 };
 
+// C4 pass A's first pass over the bytes (c4_byte_scan): the whole-document filters, a possible
+// citation, and whether a javascript / policy phrase starts anywhere (C4F_JS / C4F_POLICY).
+enum : uint32_t { C4S_LOREM = 4, C4S_CURLY = 8, C4S_CITE = 16 };
+
+// The pattern bits (C4F_JS | C4F_POLICY) of the phrases starting at byte s (case-folded).
+TB_HD uint32_t c4_phrases_at(const DevC4& c4, const uint8_t* b, uint32_t n, uint32_t s) {
+  uint8_t c0 = b[s];
+  if (c0 >= 'A' && c0 <= 'Z') c0 = (uint8_t)(c0 + 32);
+  if (c0 != 'j' && c0 != 't' && c0 != 'p' && c0 != 'c' && c0 != 'u') return 0;
+  const char* const kPol[6] = {"terms of use", "privacy policy", "cookie policy",
+                               "uses cookies", "use of cookies", "use cookies"};
+  const int kPolLen[6] = {12, 14, 13, 12, 14, 11};
+  uint32_t bits = 0;
+  const uint32_t w3 = TB_C4_PREFIX3 ? lower3(b + s, n - s) : 0u;
+  auto pre = [&](const char* pat) { return !TB_C4_PREFIX3 || w3 == pack3(pat); };
+  if (c4.filter_javascript && c0 == 'j' && pre("javascript") && ci_starts_with(b + s, n - s, "javascript", 10))
+    bits |= C4F_JS;
+  if (c4.filter_policy)
+    for (int t = 0; t < 6; ++t)
+      if (kPol[t][0] == (char)c0 && pre(kPol[t]) && ci_starts_with(b + s, n - s, kPol[t], kPolLen[t])) {
+        bits |= C4F_POLICY;
+        break;
+      }
+  return bits;
+}
+
+// One pass over the bytes: lorem ipsum and curly brackets (lowercase().contains("lorem ipsum") ==
+// the pattern starts, case-folded, at some 'l'), a possible citation ('[' followed by a digit:
+// a non-ASCII byte after the '[' counts too, so the test is conservative) and the phrase bits.
+template <class P>
+TB_HD uint32_t c4_byte_scan(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n) {
+  uint32_t acc = 0;
+  const bool phrases = c4.filter_javascript || c4.filter_policy;
+  x.par.for_n(n, [&](uint32_t s) {
+    const uint8_t c0 = b[s];
+    if (c4.filter_curly_bracket && (c0 == '{' || c0 == '}')) acc |= C4S_CURLY;
+    if (c0 == '[' && s + 1 < n) {
+      const uint8_t c1 = b[s + 1];
+      if ((c1 >= '0' && c1 <= '9') || c1 >= 0x80) acc |= C4S_CITE;
+    }
+    if (c4.filter_lorem_ipsum && (c0 == 'l' || c0 == 'L') &&
+        (!TB_C4_PREFIX3 || lower3(b + s, n - s) == pack3("lor")) && ci_starts_with(b + s, n - s, "lorem ipsum", 11))
+      acc |= C4S_LOREM;
+    if (phrases) acc |= c4_phrases_at(c4, b, n, s);
+  });
+  return x.par.reduce_or(acc);
+}
+
 // C4 pass A, common end: the joined kept lines Jb[0, Jtot) are trimmed and their sentences counted
 // (saturated at min_num_sentences), then the record and the rewritten text's source are written.
 template <class P>
@@ -1572,36 +1658,27 @@ TB_HD void c4_finish(DocCtx<P>& x, const DevC4& c4, uint32_t n, uint8_t* Jb, uin
   });
 }
 
-// C4 pass A for a document with no citation to remove (every processed line is its trimmed
-// original line): the processed text Pb, the per-code-point line ids and the kept-byte prefix of
-// the general path are not built. Words come from one segmentation of the whole text — the words
-// of a trimmed line are exactly the document's words inside its span (UAX#29 always breaks
-// around a line feed, WB3a/b, and trimming only drops whitespace, which no word contains) — and
-// are assigned to lines by their first code point; the phrase search, terminal punctuation and
-// the join read the original bytes of each line's span. Same records and rewritten text as the
-// general path.
+// The code point that ends the non-empty byte span [s, e) of b[0, n).
+TB_HD uint32_t last_cp(const uint8_t* b, uint32_t s, uint32_t e, uint32_t n) {
+  uint32_t p = e - 1;
+  while (p > s && !utf8_is_lead(b[p])) --p;
+  int len;
+  return utf8_decode(b, p, n, &len);
+}
+
+// C4 pass A for a document with no citation to remove: every processed line is its trimmed
+// original line, so the processed text Pb, the per-code-point line ids and the kept-byte prefix
+// of the general path are not built. The lines come as trimmed byte spans [lbs[k], lbe[k])
+// (lbs[NLn] = 0xFFFFFFFF) with their word counts and longest words; the phrase search, terminal
+// punctuation and the join read the original bytes of each line's span. Same records and
+// rewritten text as the general path.
 template <class P>
-TB_HD void c4_pass_a_plain(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, const Cps& c,
-                           const uint32_t* la, const uint32_t* lb, uint32_t NLn, int64_t* r, int64_t* src) {
-  const OffArr off = c.offs();
-  uint32_t* lbs = x.template alloc_hot<uint32_t>(NLn + 1);   // line byte start (trimmed)
-  uint32_t* nw = x.template alloc_hot<uint32_t>(NLn + 1);
-  uint32_t* mx = x.template alloc_hot<uint32_t>(NLn + 1);
+TB_HD void c4_plain_tail(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, uint32_t NLn,
+                         const uint32_t* lbs, const uint32_t* lbe, const uint32_t* nw, const uint32_t* mx,
+                         uint32_t phrase_bits, int64_t* r, int64_t* src) {
   uint32_t* pf = x.template alloc_hot<uint32_t>(NLn + 1);   // pattern flags per line
   uint8_t* code = x.template alloc_hot<uint8_t>(NLn + 1);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
-  x.par.for_n(NLn, [&](uint32_t k) { lbs[k] = off[la[k]]; nw[k] = 0; mx[k] = 0; pf[k] = 0; });
-  x.par.single([&]() { lbs[NLn] = 0xFFFFFFFFu; });
-  x.par.sync();
-  x.stamp(PH_C4_CITE);
-  auto line_of_cp = [&](uint32_t cs) {  // last line with la <= cs
-    uint32_t lo = 0, hi = NLn;
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (la[mid] <= cs) lo = mid; else hi = mid;
-    }
-    return lo;
-  };
   auto line_of_byte = [&](uint32_t bs) {  // last line with byte start <= bs
     uint32_t lo = 0, hi = NLn;
     while (hi - lo > 1) {
@@ -1610,57 +1687,33 @@ TB_HD void c4_pass_a_plain(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint
     }
     return lo;
   };
-  if (NLn > 0) {
-    const auto mw = x.mark();
-    Words wd = words(x, c);
-    if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
-    x.par.for_n(wd.n, [&](uint32_t q) {
-      const uint32_t k = line_of_cp(wd.cs[q]);
-      P::add32(&nw[k], 1u);
-      P::max32(&mx[k], wd.ce[q] - wd.cs[q]);
-    });
+  const bool phrases = NLn > 0 && (phrase_bits & (C4F_JS | C4F_POLICY));
+  if (phrases) {
+    x.par.for_n(NLn, [&](uint32_t k) { pf[k] = 0; });
     x.par.sync();
-    x.reset(mw);
-  }
-  x.stamp(PH_C4_WORDS);
-  if (NLn > 0 && (c4.filter_javascript || c4.filter_policy)) {
-    const char* const kPol[6] = {"terms of use", "privacy policy", "cookie policy",
-                                 "uses cookies", "use of cookies", "use cookies"};
-    const int kPolLen[6] = {12, 14, 13, 12, 14, 11};
-    // a phrase (letters and spaces, starting with a letter) that matches at a byte lies inside
-    // one line's trimmed span: it cannot cross the line feed or run into trailing whitespace
+    // only when the byte scan saw a phrase somewhere (rare). A phrase (letters and spaces, starting
+    // with a letter) that matches at a byte lies inside one line's trimmed span: it cannot cross
+    // the line feed or run into trailing whitespace.
     x.par.for_n(n, [&](uint32_t s) {
-      uint8_t c0 = b[s];
-      if (c0 >= 'A' && c0 <= 'Z') c0 = (uint8_t)(c0 + 32);
-      if (c0 != 'j' && c0 != 't' && c0 != 'p' && c0 != 'c' && c0 != 'u') return;
-      uint32_t bits = 0;
-      const uint32_t w3 = TB_C4_PREFIX3 ? lower3(b + s, n - s) : 0u;
-      auto pre = [&](const char* pat) { return !TB_C4_PREFIX3 || w3 == pack3(pat); };
-      if (c4.filter_javascript && c0 == 'j' && pre("javascript") && ci_starts_with(b + s, n - s, "javascript", 10))
-        bits |= C4F_JS;
-      if (c4.filter_policy)
-        for (int t = 0; t < 6; ++t)
-          if (kPol[t][0] == (char)c0 && pre(kPol[t]) && ci_starts_with(b + s, n - s, kPol[t], kPolLen[t])) {
-            bits |= C4F_POLICY;
-            break;
-          }
+      const uint32_t bits = c4_phrases_at(c4, b, n, s);
       if (bits) P::or32(&pf[line_of_byte(s)], bits);
     });
+    x.par.sync();
   }
-  x.par.sync();
   x.par.for_n(NLn, [&](uint32_t k) {
-    const uint32_t s0 = off[la[k]], e0 = off[lb[k]], ln = e0 - s0;
+    const uint32_t s0 = lbs[k], e0 = lbe[k], ln = e0 - s0;
+    const uint32_t fl = phrases ? pf[k] : 0u;
     uint8_t cd = 0;
     if (c4.max_word_length > 0 && (int64_t)mx[k] > c4.max_word_length) {
       cd = 1;
     } else if (c4.filter_no_terminal_punct) {
-      const bool term = ln > 0 && end_punct(c.cp(lb[k] - 1));
+      const bool term = ln > 0 && end_punct(last_cp(b, s0, e0, n));
       const bool ell = ln >= 3 && b[e0 - 1] == '.' && b[e0 - 2] == '.' && b[e0 - 3] == '.';
       if (!term || ell) cd = 2;
     }
     if (cd == 0 && c4.min_words_per_line > 0 && (int64_t)nw[k] < c4.min_words_per_line) cd = 3;
-    if (cd == 0 && c4.filter_javascript && (pf[k] & C4F_JS)) cd = 4;
-    if (cd == 0 && c4.filter_policy && (pf[k] & C4F_POLICY)) cd = 5;
+    if (cd == 0 && c4.filter_javascript && (fl & C4F_JS)) cd = 4;
+    if (cd == 0 && c4.filter_policy && (fl & C4F_POLICY)) cd = 5;
     code[k] = cd;
   });
   x.par.sync();
@@ -1675,7 +1728,7 @@ TB_HD void c4_pass_a_plain(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   uint32_t Jtot = x.par.template scan<uint32_t>(
       NLn, 0u, [](uint32_t a, uint32_t b2) { return a + b2; },
-      [&](uint32_t k) { return code[k] == 0 ? off[lb[k]] - off[la[k]] + 1 : 0u; },
+      [&](uint32_t k) { return code[k] == 0 ? lbe[k] - lbs[k] + 1 : 0u; },
       [&](uint32_t k, uint32_t e) { joff[k] = e; });
   if (Jtot > 0) Jtot -= 1;
   uint8_t* Jb = x.template alloc_global<uint8_t>(Jtot + 1);
@@ -1684,11 +1737,11 @@ TB_HD void c4_pass_a_plain(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint
   if (NLn > 0) {
     x.par.for_n(n, [&](uint32_t i) {
       const uint32_t k = line_of_byte(i);
-      if (code[k] != 0 || i < lbs[k] || i >= off[lb[k]]) return;
+      if (code[k] != 0 || i < lbs[k] || i >= lbe[k]) return;
       Jb[joff[k] + (i - lbs[k])] = b[i];
     });
     x.par.for_n(NLn, [&](uint32_t k) {
-      const uint32_t ln = off[lb[k]] - off[la[k]];
+      const uint32_t ln = lbe[k] - lbs[k];
       if (code[k] == 0 && joff[k] + ln < Jtot) Jb[joff[k] + ln] = '\n';
     });
   }
@@ -1697,28 +1750,96 @@ TB_HD void c4_pass_a_plain(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint
   c4_finish(x, c4, n, Jb, Jtot, s_long, s_punct, s_few, r, src);
 }
 
+// The plain path from this pass's own decode and lines [la, lb) (code points): words come from
+// one segmentation of the whole text — the words of a trimmed line are exactly the document's
+// words inside its span (UAX#29 always breaks around a line feed, WB3a/b, and trimming only
+// drops whitespace, which no word contains) — assigned to lines by their first code point.
 template <class P>
-TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, int64_t* r, int64_t* src) {
+TB_HD void c4_pass_a_plain(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, const Cps& c,
+                           const uint32_t* la, const uint32_t* lb, uint32_t NLn, int64_t* r, int64_t* src,
+                           uint32_t phrase_bits) {
+  const OffArr off = c.offs();
+  uint32_t* lbs = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* lbe = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* nw = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* mx = x.template alloc_hot<uint32_t>(NLn + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  x.par.for_n(NLn, [&](uint32_t k) { lbs[k] = off[la[k]]; lbe[k] = off[lb[k]]; nw[k] = 0; mx[k] = 0; });
+  x.par.single([&]() { lbs[NLn] = 0xFFFFFFFFu; });
+  x.par.sync();
+  x.stamp(PH_C4_CITE);
+  if (NLn > 0) {
+    auto line_of_cp = [&](uint32_t cs) {  // last line with la <= cs
+      uint32_t lo = 0, hi = NLn;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (la[mid] <= cs) lo = mid; else hi = mid;
+      }
+      return lo;
+    };
+    const auto mw = x.mark();
+    Words wd = words(x, c);
+    if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+    x.par.for_n(wd.n, [&](uint32_t q) {
+      const uint32_t k = line_of_cp(wd.cs[q]);
+      P::add32(&nw[k], 1u);
+      P::max32(&mx[k], wd.ce[q] - wd.cs[q]);
+    });
+    x.par.sync();
+    x.reset(mw);
+  }
+  x.stamp(PH_C4_WORDS);
+  c4_plain_tail(x, c4, b, n, NLn, lbs, lbe, nw, mx, phrase_bits, r, src);
+}
+
+// The plain path from the stage's line export (LineStat region, header = line count): no decode,
+// lines or words here.
+template <class P>
+TB_HD void c4_pass_a_export(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, const uint32_t* region,
+                            uint32_t NLn, int64_t* r, int64_t* src, uint32_t phrase_bits) {
+  const LineStat* ls = (const LineStat*)(region + 4);
+  uint32_t* lbs = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* lbe = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* nw = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* mx = x.template alloc_hot<uint32_t>(NLn + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  x.par.for_n(NLn, [&](uint32_t k) {
+    const LineStat e = ls[k];
+    lbs[k] = e.bs; lbe[k] = e.be; nw[k] = e.nw; mx[k] = e.mx;
+  });
+  x.par.single([&]() { lbs[NLn] = 0xFFFFFFFFu; });
+  x.par.sync();
+  x.stamp(PH_C4_WORDS);
+  c4_plain_tail(x, c4, b, n, NLn, lbs, lbe, nw, mx, phrase_bits, r, src);
+}
+
+template <class P>
+TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, int64_t* r, int64_t* src,
+                     const uint32_t* line_stats = nullptr) {
   x.stamp(PH_START);
-  // lowercase().contains("lorem ipsum") == the pattern starts (case-folded) at some 'l'/'L'
-  const uint32_t lorem = c4.filter_lorem_ipsum
-      ? x.par.template sum<uint32_t>(n, [&](uint32_t s) {
-          if (b[s] != 'l' && b[s] != 'L') return 0u;
-          if (TB_C4_PREFIX3 && lower3(b + s, n - s) != pack3("lor")) return 0u;
-          return ci_starts_with(b + s, n - s, "lorem ipsum", 11) ? 1u : 0u;
-        })
-      : 0u;
-  const uint32_t curly = c4.filter_curly_bracket
-      ? x.par.template sum<uint32_t>(n, [&](uint32_t i) { return (b[i] == '{' || b[i] == '}') ? 1u : 0u; })
-      : 0u;
+  const uint32_t scan = c4_byte_scan(x, c4, b, n);
+  const bool lorem = scan & C4S_LOREM, curly = scan & C4S_CURLY;
   if (lorem || curly) {
     x.par.single([&]() {
-      r[0] = lorem > 0; r[1] = curly > 0; r[2] = r[3] = r[4] = r[5] = 0; r[6] = n;
+      r[0] = lorem; r[1] = curly; r[2] = r[3] = r[4] = r[5] = 0; r[6] = n;
       src[0] = -1; src[1] = n;
     });
     return;
   }
   x.stamp(PH_C4_LOREM);
+#ifndef TB_C4_PLAIN
+#define TB_C4_PLAIN 1
+#endif
+  // A citation needs a '[' followed by a digit: without one (the common case) every processed
+  // line is its trimmed original line and the plain path runs on the original bytes.
+  const bool maybe_cite = c4.remove_citations != 0 && (scan & C4S_CITE);
+  if (TB_C4_PLAIN && !maybe_cite && line_stats && c4.split_paragraph) {
+    const uint32_t NL = line_stats[0];  // the stage kernel of this content version wrote it
+    if (NL != kLineStatsNone) {
+      c4_pass_a_export(x, c4, b, n, line_stats, NL, r, src, scan);
+      return;
+    }
+  }
   uint32_t dict = 0;
   Cps c = decode(x, b, n, false, &dict);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
@@ -1774,17 +1895,8 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   }
   x.par.sync();
   x.stamp(PH_C4_LINES);
-  // A citation needs a '[' followed by a digit: without one (the common case) every processed
-  // line is its trimmed original line and the plain path runs on the original bytes.
-#ifndef TB_C4_PLAIN
-#define TB_C4_PLAIN 1
-#endif
-  const bool maybe_cite = c4.remove_citations != 0 &&
-      x.par.reduce_or(x.par.template sum<uint32_t>(C > 0 ? C - 1 : 0, [&](uint32_t j) {
-        return (c.lead(j) == '[' && (prop[j + 1] & P_DIGIT)) ? 1u : 0u;
-      }));
   if (TB_C4_PLAIN && !maybe_cite) {
-    c4_pass_a_plain(x, c4, b, n, c, la, lb, NLn, r, src);
+    c4_pass_a_plain(x, c4, b, n, c, la, lb, NLn, r, src, scan);
     return;
   }
   // ---- citation removal -> processed lines Pb (every step parallel over code points) ----
@@ -1887,26 +1999,10 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   // javascript / policy phrases: to_lowercase().contains() per line == a case-folded match
   // starting at some byte of the line; every byte position is tested in parallel.
   if (c4.filter_javascript || c4.filter_policy) {
-    const char* const kPol[6] = {"terms of use", "privacy policy", "cookie policy",
-                                 "uses cookies", "use of cookies", "use cookies"};
-    const int kPolLen[6] = {12, 14, 13, 12, 14, 11};
     // The phrases hold letters and spaces only, so a match never runs over the '\n' that ends
     // its line: match against the rest of Pb first, look the line up only on a match.
     x.par.for_n(Ptot, [&](uint32_t s) {
-      uint8_t c0 = Pb[s];
-      if (c0 >= 'A' && c0 <= 'Z') c0 = (uint8_t)(c0 + 32);
-      if (c0 != 'j' && c0 != 't' && c0 != 'p' && c0 != 'c' && c0 != 'u') return;
-      uint32_t bits = 0;
-      const uint32_t w3 = TB_C4_PREFIX3 ? lower3(Pb + s, Ptot - s) : 0u;
-      auto pre = [&](const char* pat) { return !TB_C4_PREFIX3 || w3 == pack3(pat); };
-      if (c4.filter_javascript && c0 == 'j' && pre("javascript") && ci_starts_with(Pb + s, Ptot - s, "javascript", 10))
-        bits |= C4F_JS;
-      if (c4.filter_policy)
-        for (int t = 0; t < 6; ++t)
-          if (kPol[t][0] == (char)c0 && pre(kPol[t]) && ci_starts_with(Pb + s, Ptot - s, kPol[t], kPolLen[t])) {
-            bits |= C4F_POLICY;
-            break;
-          }
+      const uint32_t bits = c4_phrases_at(c4, Pb, Ptot, s);
       if (bits) P::or32(&pf[line_of_byte(s)], bits);
     });
   }
@@ -1986,6 +2082,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
     if (k == DK_LANGID) need_lid = true;
   }
   x.stamp(PH_START);
+  if (out.line_stats) x.par.single([&]() { out.line_stats[0] = kLineStatsNone; });
   uint32_t ndict = 0;
   Cps c = decode(x, b, n, kHotProps, &ndict);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
@@ -2006,8 +2103,9 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
   x.stamp(PH_WORDS);
   Lines L;
   if (need_lines) L = rust_lines(x, c);
-  x.stamp(PH_LINES);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  if (out.line_stats && need_words && need_lines) export_line_stats(x, c, w, L, n, out.line_stats);
+  x.stamp(PH_LINES);
   const uint32_t W = w.n;
   const PropArr prop = c.props();
   const OffArr off = c.offs();

@@ -104,7 +104,7 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
       const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,        \
       const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, \
       int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof,                               \
-      const uint8_t* __restrict__ dead) {                                                             \
+      const uint8_t* __restrict__ dead, uint32_t* line_stats) {                                        \
     const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;                                        \
     if (doc >= ndocs || (dead && dead[doc])) return;                                                  \
     DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);   \
@@ -112,6 +112,7 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
     lds_ascii_props(x);                                                                               \
     const uint8_t* b = lds_text(x, bytes + off[doc], n);                                              \
     StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc};                                                \
+    if (line_stats) out.line_stats = line_stats + line_stats_base(off[doc], doc);                     \
     analyze_stage<WavePar, false>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out); /* LD: own kernel */ \
   }
 
@@ -148,7 +149,7 @@ __device__ __forceinline__ void stage_blk_body(
     const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,
     const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
     int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead,
-    GrExport* gr_export, int32_t n_split, uint32_t split_bytes) {
+    GrExport* gr_export, int32_t n_split, uint32_t split_bytes, uint32_t* line_stats) {
   const int doc = perm[blockIdx.x];
   if (doc >= ndocs || (dead && dead[doc])) return;
   DocCtx<BlockPar<NT>> x =
@@ -158,6 +159,7 @@ __device__ __forceinline__ void stage_blk_body(
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc};
+  if (line_stats) out.line_stats = line_stats + line_stats_base(off[doc], doc);
   // split documents (the first n_split launch positions, longer than split_bytes) export their
   // word arrays; k_gr_dup_split finishes their duplicated n-gram orders
   if (gr_export && (int)blockIdx.x < n_split && n > split_bytes) out.gr_export = gr_export + blockIdx.x;
@@ -170,9 +172,9 @@ __device__ __forceinline__ void stage_blk_body(
       const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,         \
       const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,  \
       int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead,   \
-      GrExport* gr_export, int32_t n_split, uint32_t split_bytes) {                                    \
+      GrExport* gr_export, int32_t n_split, uint32_t split_bytes, uint32_t* line_stats) {              \
     stage_blk_body<NT>(plan, stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, tabs, rec, flags, \
-                       lds_bytes, prof, dead, gr_export, n_split, split_bytes);                          \
+                       lds_bytes, prof, dead, gr_export, n_split, split_bytes, line_stats);              \
   }
 TB_STAGE_BLK_KERNEL(k_stage_analyze_blk, kBlockThreads)
 TB_STAGE_BLK_KERNEL(k_stage_analyze_blk1k, kBlockThreadsMax)
@@ -597,14 +599,15 @@ __global__ __launch_bounds__(64) void k_c4_pass_a(
     const DevC4* __restrict__ c4, const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
     const int32_t* __restrict__ perm, int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off,
     const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec, int64_t* src, uint32_t* flags,
-    uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead) {
+    uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead, const uint32_t* __restrict__ line_stats) {
   const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
   if (doc >= ndocs || (dead && dead[doc])) return;  // skipped: record zeros, rewritten length 0
   DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
   lds_ascii_props(x);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
-  c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2);
+  c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2,
+            line_stats ? line_stats + line_stats_base(off[doc], doc) : nullptr);
   c4_src_absolute(x, src + (int64_t)doc * 2, scratch_off[blockIdx.x]);
 }
 
@@ -612,7 +615,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_c4_pass_a_blk(
     const DevC4* __restrict__ c4, const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
     const int32_t* __restrict__ perm, int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off,
     const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec, int64_t* src, uint32_t* flags,
-    uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead) {
+    uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead, const uint32_t* __restrict__ line_stats) {
   const int doc = perm[blockIdx.x];
   if (doc >= ndocs || (dead && dead[doc])) return;
   DocCtx<BlockPar<kBlockThreads>> x =
@@ -621,7 +624,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_c4_pass_a_blk(
   lds_ascii_props(x);
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
-  c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2);
+  c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2,
+            line_stats ? line_stats + line_stats_base(off[doc], doc) : nullptr);
   c4_src_absolute(x, src + (int64_t)doc * 2, scratch_off[blockIdx.x]);
 }
 
@@ -824,8 +828,8 @@ __global__ void k_pow_table(uint64_t* pw, uint32_t n) {
   // arithmetic); the buffer holds 2n + 2 entries
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i <= n) {
-    pw[i] = powmod61(kHashBase, i);
-    pw[n + 1 + i] = powmod61(kHashBaseInv, i);
+    pw[i] = hpow(kHashBase, i);
+    pw[n + 1 + i] = hpow(kHashBaseInv, i);
   }
 }
 
@@ -839,7 +843,8 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
                      const int64_t* off, const int32_t* perm, int32_t ndocs, char* scratch,
                      const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                      const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
-                     uint32_t lds_bytes, uint64_t* prof, int32_t waves, int32_t nblocks, const uint8_t* dead) {
+                     uint32_t lds_bytes, uint64_t* prof, int32_t waves, int32_t nblocks, const uint8_t* dead,
+                     uint32_t* line_stats) {
   if (ndocs <= 0) return 0;
   if (nblocks <= 0) nblocks = ndocs;  // grid: docs perm[0 .. nblocks)
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
@@ -850,7 +855,7 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64), lds_bytes, stream, (const DevPlan*)plan,
                      (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, flags,
-                     lds_bytes, prof, dead);
+                     lds_bytes, prof, dead, line_stats);
   return (int)hipGetLastError();
 }
 
@@ -861,7 +866,7 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
                          const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                          const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
                          uint32_t lds_bytes, uint64_t* prof, const uint8_t* dead, void* gr_export, int32_t n_split,
-                         uint32_t split_bytes, int32_t threads) {
+                         uint32_t split_bytes, int32_t threads, uint32_t* line_stats) {
   if (nblocks <= 0) return 0;
   if (!perm || lds_bytes > kMaxLdsPerBlk || n_split < 0 || n_split > nblocks) return (int)hipErrorInvalidValue;
   if (threads != kBlockThreads && threads != kBlockThreadsMax) return (int)hipErrorInvalidValue;
@@ -872,7 +877,7 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
   hipLaunchKernelGGL(kern, dim3(nblocks), dim3(threads), lds_bytes, stream,
                      (const DevPlan*)plan, (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw,
                      pw_n, t, rec, flags, lds_bytes, prof, dead, (GrExport*)gr_export, n_split,
-                     split_bytes);
+                     split_bytes, line_stats);
   return (int)hipGetLastError();
 }
 
@@ -902,7 +907,7 @@ int tb_c4_pass_a_blk(hipStream_t stream, const void* c4, const uint8_t* bytes, c
                      const int32_t* perm, int32_t nblocks, int32_t ndocs, char* scratch, const int64_t* scratch_off,
                      const uint64_t* pw, uint32_t pw_n, const uint16_t* s1, const uint32_t* s2, const uint16_t* l1,
                      const int32_t* l2, int64_t* rec, int64_t* src, uint32_t* flags, uint32_t lds_bytes,
-                     uint64_t* prof, const uint8_t* dead) {
+                     uint64_t* prof, const uint8_t* dead, const uint32_t* line_stats) {
   if (nblocks <= 0) return 0;
   if (!perm || lds_bytes > kMaxLdsPerBlk) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
@@ -910,7 +915,8 @@ int tb_c4_pass_a_blk(hipStream_t stream, const void* c4, const uint8_t* bytes, c
     (void)hipFuncSetAttribute((const void*)k_c4_pass_a_blk, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds_bytes);
   hipLaunchKernelGGL(k_c4_pass_a_blk, dim3(nblocks), dim3(kBlockThreads), lds_bytes, stream, (const DevC4*)c4,
-                     bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof, dead);
+                     bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof, dead,
+                     line_stats);
   return (int)hipGetLastError();
 }
 
@@ -967,7 +973,7 @@ int tb_c4_pass_a(hipStream_t stream, const void* c4, const uint8_t* bytes, const
                  int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n,
                  const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
                  int64_t* src, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, int32_t nblocks,
-                 const uint8_t* dead) {
+                 const uint8_t* dead, const uint32_t* line_stats) {
   if (ndocs <= 0) return 0;
   if (nblocks <= 0) nblocks = ndocs;
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
@@ -975,7 +981,7 @@ int tb_c4_pass_a(hipStream_t stream, const void* c4, const uint8_t* bytes, const
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k_c4_pass_a, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(k_c4_pass_a, dim3(nblocks), dim3(64), lds_bytes, stream, (const DevC4*)c4, bytes, off, perm, ndocs,
-                     scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof, dead);
+                     scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof, dead, line_stats);
   return (int)hipGetLastError();
 }
 
@@ -1039,7 +1045,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 
 int tb_phase_slots() { return kPhaseSlots; }
 
-int tb_abi_version() { return 13; }
+int tb_abi_version() { return 14; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

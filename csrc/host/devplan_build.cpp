@@ -302,8 +302,8 @@ std::vector<uint64_t> pow_table(uint32_t n) {
   pw[0] = 1;
   pw[n + 1] = 1;
   for (uint32_t i = 1; i <= n; ++i) {
-    pw[i] = mulmod61(pw[i - 1], kHashBase);
-    pw[n + 1 + i] = mulmod61(pw[n + i], kHashBaseInv);
+    pw[i] = hmul(pw[i - 1], kHashBase);
+    pw[n + 1 + i] = hmul(pw[n + i], kHashBaseInv);
   }
   return pw;
 }

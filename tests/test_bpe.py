@@ -151,7 +151,15 @@ def test_emulated_device_token_counts_equal_cpu(trained):
     assert eng.device_runner.resolve_blob is not None and eng.device_runner.bpe
     res = eng.submit(data, off)
     assert res.dev.resolved is not None and res.dev.resolved.tokens
+    from textblaster_amd.utils import metrics
+
+    h0, d0 = metrics.BPE_HOST_DOCS_TOTAL._value.get(), metrics.BPE_DEVICE_DOCS_TOTAL._value.get()
     a = eng.finish(res)
+    # the fallback rate is observable: every kept document is counted once, on the host (added-token
+    # text, a pre-token over 64 bytes) or from the device path
+    nh = metrics.BPE_HOST_DOCS_TOTAL._value.get() - h0
+    nd = metrics.BPE_DEVICE_DOCS_TOTAL._value.get() - d0
+    assert nd > 0 and nh + nd == a.n_kept
     b = Engine(_cfg(), backend="cpu", nthreads=4, keep_reasons=True, tokenizer_file=trained,
                segmentation="icu").process(data, off)
     np.testing.assert_array_equal(a.status, b.status)

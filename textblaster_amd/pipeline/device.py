@@ -293,6 +293,8 @@ class PendingBatch:
 
 KIND_LANGID = 4  # DevStep kind of LanguageDetectionFilter in a stage layout (csrc/common/devplan.h)
 KIND_GOPHER_REP = 2
+KIND_GOPHER_QUALITY = 1
+KIND_FINEWEB = 3
 
 
 def plan_passes(plan: ExecPlan, stage_layout, steps_native, gating: bool, lid_gate: bool = True):
@@ -556,6 +558,17 @@ class DeviceRunner:
                 st = steps_native[idx[grs[0]]]
                 if st.n_dup + st.n_top > 0:
                     self.gr_split[si] = (grs[0], st.n_dup + st.n_top + 2)
+        # C4 line statistics: the first stage of a content version that segments words and Rust
+        # lines (GopherQuality / FineWeb) exports every line's word count and longest word, and the
+        # C4 pass of that version reads them instead of segmenting the words again
+        # (docproc.h export_line_stats); TB_C4_LINE_STATS=0 turns it off
+        self.line_stats_stage = {}
+        if os.environ.get("TB_C4_LINE_STATS", "1") != "0":
+            c4_versions = {plan.steps[i].version_in for i in plan.c4_steps}
+            for si, sv in enumerate(plan.stage_version):
+                kinds = {kind for kind, _, _ in self.stage_layout[si][1]}
+                if sv in c4_versions and sv not in self.line_stats_stage and kinds & {KIND_GOPHER_QUALITY, KIND_FINEWEB}:
+                    self.line_stats_stage[sv] = si
         if not 0 <= self.lds_bytes_blk <= 131072:
             # the workgroup kernels also hold static LDS (cross-wave exchange buffers): a 160 KB
             # dynamic slice does not fit the CU's 160 KB and the launch fails with
@@ -753,7 +766,6 @@ class DeviceRunner:
         maxlen = int(lens.max()) if ndocs else 0
         n_long = int(np.count_nonzero(lens > self.long_doc_bytes)) if self.long_doc_bytes > 0 else 0
         # perm is longest first: [0, n_long) workgroup docs, then the wave docs
-        n_mid = n_long
         direct_keep: List = []
         # per-document bad-words roots / CJK flags and the long documents' segment lists travel in
         # the same upload
@@ -795,6 +807,12 @@ class DeviceRunner:
         for ver in range(self.plan.n_versions):
             vb, vo, vlen = versions[ver]
             main.wait_event(ready[ver])
+            # uint32 [4 * (bytes / 8 + 16 * documents) + 16]: document d's region at
+            # 4 * (off[d] / 8 + 16 d) (docproc.h line_stats_base)
+            lstats = None
+            if ver in self.line_stats_stage:
+                lstats = rt.empty(4 * (vlen // 8 + 16 * ndocs) + 16, np.uint32)
+                keep.append(lstats)
             for s, sv in enumerate(self.plan.stage_version):
                 if sv != ver:
                     continue
@@ -823,6 +841,7 @@ class DeviceRunner:
                     main.wait_event(ev_pre)
                     pass_idx += 1
                 skip = dead if pass_idx > 0 else None
+                ls_out = lstats if self.line_stats_stage.get(ver) == s else None
                 # long documents first: with the 4-stream layout the workgroup kernels and the
                 # language-id bag share the side stream, and the long-document tail must start early
                 if n_long:
@@ -850,7 +869,7 @@ class DeviceRunner:
                                                      ndocs, scratch, d_soff[a0:], pw, pw_n, rec, flags,
                                                      self.lds_bytes_blk, prof, skip,
                                                      gx[a0 * esz:] if (gx is not None and ns) else None, ns,
-                                                     self.split_doc_bytes, thr)
+                                                     self.split_doc_bytes, thr, ls_out)
                         if n_split:
                             gr_pos, n_tasks = self.gr_split[s]
                             self.k.gr_dup_split(self.stage_ts[s], gr_pos, d_perm[:n_split], n_split, n_tasks, ndocs,
@@ -866,11 +885,11 @@ class DeviceRunner:
                                          flags, self._prof_buf(ndocs, keep, f"langid{s}"))
                         ev_lid = self._record(slot.s_lid)
                         keep.append(ev_lid)
-                if n_mid < ndocs:
+                if n_long < ndocs:
                     with self._ktimed(keep, f"stage{s}"):
-                        self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_mid:], ndocs,
-                                             scratch, d_soff[n_mid:], pw, pw_n, rec, flags,
-                                             self.lds_bytes, prof, self.stage_waves, ndocs - n_mid, skip)
+                        self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,
+                                             scratch, d_soff[n_long:], pw, pw_n, rec, flags,
+                                             self.lds_bytes, prof, self.stage_waves, ndocs - n_long, skip, ls_out)
                 if ev_lid is not None:
                     main.wait_event(ev_lid)
                 if ev_blk is not None:
@@ -905,13 +924,15 @@ class DeviceRunner:
                     keep.append(ev_c4)
                     with rt.stream(slot.s_c4blk):
                         self.k.c4_pass_a_blk(self.c4_ts[i], vb, vo, d_perm[:n_long], n_long, ndocs, c4_scratch,
-                                             d_soff, pw, pw_n, rec, src, flags, self.lds_bytes_blk, prof, skip)
+                                             d_soff, pw, pw_n, rec, src, flags, self.lds_bytes_blk, prof, skip,
+                                             lstats)
                         ev_c4blk = self._record(slot.s_c4blk)
                         keep.append(ev_c4blk)
                 with rt.stream(slot.s_c4), self._ktimed(keep, f"c4_step{i}"):
                     if n_long < ndocs:
                         self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm[n_long:], ndocs, c4_scratch, d_soff[n_long:], pw,
-                                         pw_n, rec, src, flags, self.lds_bytes_c4, prof, ndocs - n_long, skip)
+                                         pw_n, rec, src, flags, self.lds_bytes_c4, prof, ndocs - n_long, skip,
+                                         lstats)
                     if ev_c4blk is not None:
                         slot.s_c4.wait_event(ev_c4blk)
                     rt.scan_strided_i64(src[1:], 2, ndocs, new_off[1:])

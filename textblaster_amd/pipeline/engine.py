@@ -575,6 +575,10 @@ class Engine:
                 dev = resolved.kept_tokens(i)
                 cnt = dev.astype(np.int64) if dev is not None else np.full(len(alive), -2, np.int64)
                 bad = np.nonzero(cnt < 0)[0]
+                from ..utils import metrics
+
+                metrics.BPE_HOST_DOCS_TOTAL.inc(len(bad))
+                metrics.BPE_DEVICE_DOCS_TOTAL.inc(len(cnt) - len(bad))
                 if len(bad):
                     o = resolved.out_off
                     ko = np.nonzero(~resolved.moved)[0] if resolved.moved is not None else np.arange(len(alive))

@@ -78,6 +78,11 @@ GATE_MISMATCH_DOCS_TOTAL = Counter("tb_gate_mismatch_docs_total",
 DEVICE_RESOLVE_FALLBACK_TOTAL = Counter("tb_device_resolve_fallback_total",
                                         "Batches whose device resolve/compaction (K16) disagreed with the host "
                                         "decisions and were assembled on the host (expected 0).", registry=REGISTRY)
+BPE_HOST_DOCS_TOTAL = Counter("tb_bpe_host_docs_total",
+                              "Kept documents whose TokenCounter count the device handed to the host tokenizer "
+                              "(added-token text or a pre-token over 64 bytes).", registry=REGISTRY)
+BPE_DEVICE_DOCS_TOTAL = Counter("tb_bpe_device_docs_total",
+                                "Kept documents whose TokenCounter count came from k_bpe_count.", registry=REGISTRY)
 RANK = Gauge("tb_rank", "Data-parallel rank of this process.", registry=REGISTRY)
 WORLD_SIZE = Gauge("tb_world_size", "Number of data-parallel ranks.", registry=REGISTRY)
 GLOBAL_DOCS = Gauge("tb_global_docs_total", "All-reduced document counters (rank 0).", ["kind"],

@@ -829,40 +829,54 @@ constexpr uint32_t kLineStatsNone = 0xFFFFFFFFu;
 struct alignas(16) LineStat { uint32_t bs, be, nw, mx; };
 TB_HD uint64_t line_stats_base(int64_t off_d, int64_t d) { return 4ull * ((uint64_t)off_d / 8u + 16ull * (uint64_t)d); }
 TB_HD uint32_t line_stats_cap(uint32_t n) { return n / 8u + 15u; }
+TB_HD uint64_t line_stats_words(const int64_t* off, int64_t ndocs) {  // buffer size in u32
+  return line_stats_base(off[ndocs], ndocs) + 16u;
+}
 
 // C4 line export from the stage's words and lines (StageOut::line_stats): per Rust line its span
-// trimmed of whitespace (in bytes), its words — those whose first code point lies in [ls, le):
-// words never cross a line feed, and the position-ordered word list makes them a contiguous
-// range found by two binary searches — and their longest length in code points. The header is
-// written last; documents with more lines than the region holds keep kLineStatsNone.
+// trimmed of whitespace (in bytes), its word count and its longest word in code points. Words are
+// assigned to the last line starting at or before their first code point (words never cross a
+// line feed), word-parallel with LDS atomics on per-line counters. The header is written last;
+// documents with more lines than the region holds, or whose counters do not fit the scratch,
+// keep kLineStatsNone (the export never changes the stage's own results).
 template <class P>
 TB_HD void export_line_stats(DocCtx<P>& x, const Cps& c, const Words& w, const Lines& L, uint32_t n, uint32_t* out) {
-  if (L.n > line_stats_cap(n)) return;
+  const uint32_t NL = L.n;
+  if (NL > line_stats_cap(n) || x.overflow) return;
+  const auto mark = x.mark();
+  uint32_t* ls = x.template alloc_hot<uint32_t>(NL + 1);
+  uint32_t* nw = x.template alloc_hot<uint32_t>(NL + 1);
+  uint32_t* mx = x.template alloc_hot<uint32_t>(NL + 1);
+  if (x.overflow) {
+    x.overflow = false;
+    x.reset(mark);
+    return;
+  }
   const PropArr prop = c.props();
   const OffArr off = c.offs();
-  LineStat* ls = (LineStat*)(out + 4);
-  auto lower = [&](uint32_t v) {  // first word with cs >= v
-    uint32_t lo = 0, hi = w.n;
-    while (lo < hi) {
+  x.par.for_n(NL, [&](uint32_t k) { ls[k] = L.ls[k]; nw[k] = 0; mx[k] = 0; });
+  x.par.sync();
+  x.par.for_n(w.n, [&](uint32_t q) {
+    const uint32_t cs = w.cs[q];
+    uint32_t lo = 0, hi = NL;
+    while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
-      if (w.cs[mid] < v) lo = mid + 1; else hi = mid;
+      if (ls[mid] <= cs) lo = mid; else hi = mid;
     }
-    return lo;
-  };
-  x.par.for_n(L.n, [&](uint32_t k) {
-    uint32_t s0 = L.ls[k], e0 = L.le[k];
-    const uint32_t a = lower(s0), e = lower(e0);
-    uint32_t mx = 0;
-    for (uint32_t q = a; q < e; ++q) {
-      const uint32_t len = w.ce[q] - w.cs[q];
-      mx = len > mx ? len : mx;
-    }
-    while (s0 < e0 && is_ws(prop[s0])) ++s0;
-    while (e0 > s0 && is_ws(prop[e0 - 1])) --e0;
-    ls[k] = LineStat{off[s0], off[e0], e - a, mx};
+    P::add32(&nw[lo], 1u);
+    P::max32(&mx[lo], w.ce[q] - cs);
   });
   x.par.sync();
-  x.par.single([&]() { out[0] = L.n; });
+  LineStat* st = (LineStat*)(out + 4);
+  x.par.for_n(NL, [&](uint32_t k) {
+    uint32_t s0 = ls[k], e0 = L.le[k];
+    while (s0 < e0 && is_ws(prop[s0])) ++s0;
+    while (e0 > s0 && is_ws(prop[e0 - 1])) --e0;
+    st[k] = LineStat{off[s0], off[e0], nw[k], mx[k]};
+  });
+  x.par.sync();
+  x.par.single([&]() { out[0] = NL; });
+  x.reset(mark);
 }
 
 // The duplicated n-gram key / equality of order n over the exported word arrays (one definition
@@ -1554,9 +1568,6 @@ TB_HD bool ci_starts_with(const uint8_t* b, uint32_t n, const char* pat, int ple
 // three independent loads. Every C4 phrase starts with three ASCII letters other than 'k' (the
 // only pattern letter with a multi-byte match, the Kelvin sign), so a phrase can only match where
 // this equals its packed prefix.
-#ifndef TB_C4_PREFIX3
-#define TB_C4_PREFIX3 1
-#endif
 TB_HD uint32_t lower3(const uint8_t* b, uint32_t n) {
   uint32_t w = 0;
 #pragma unroll
@@ -1587,8 +1598,8 @@ TB_HD uint32_t c4_phrases_at(const DevC4& c4, const uint8_t* b, uint32_t n, uint
                                "uses cookies", "use of cookies", "use cookies"};
   const int kPolLen[6] = {12, 14, 13, 12, 14, 11};
   uint32_t bits = 0;
-  const uint32_t w3 = TB_C4_PREFIX3 ? lower3(b + s, n - s) : 0u;
-  auto pre = [&](const char* pat) { return !TB_C4_PREFIX3 || w3 == pack3(pat); };
+  const uint32_t w3 = lower3(b + s, n - s);
+  auto pre = [&](const char* pat) { return w3 == pack3(pat); };
   if (c4.filter_javascript && c0 == 'j' && pre("javascript") && ci_starts_with(b + s, n - s, "javascript", 10))
     bits |= C4F_JS;
   if (c4.filter_policy)
@@ -1600,24 +1611,58 @@ TB_HD uint32_t c4_phrases_at(const DevC4& c4, const uint8_t* b, uint32_t n, uint
   return bits;
 }
 
+// ASCII 'A'..'Z' -> 'a'..'z' in all 8 bytes of v (other bytes unchanged).
+TB_HD uint64_t swar_lower8(uint64_t v) {
+  constexpr uint64_t k7F = 0x7F7F7F7F7F7F7F7Full, k80 = 0x8080808080808080ull;
+  const uint64_t ge_a = (v & k7F) + 0x3F3F3F3F3F3F3F3Full;  // bit 7 set: byte & 0x7F >= 'A'
+  const uint64_t gt_z = (v & k7F) + 0x2525252525252525ull;  // bit 7 set: byte & 0x7F > 'Z'
+  const uint64_t upper = ge_a & ~gt_z & ~v & k80;
+  return v | (upper >> 2);
+}
+
 // One pass over the bytes: lorem ipsum and curly brackets (lowercase().contains("lorem ipsum") ==
 // the pattern starts, case-folded, at some 'l'), a possible citation ('[' followed by a digit:
 // a non-ASCII byte after the '[' counts too, so the test is conservative) and the phrase bits.
+// Each item is one aligned dword of the text (4 start positions) with the next dword as look-ahead:
+// the 3-byte case-folded prefixes come from shifts of one lowercased 64-bit window, and only a
+// position whose prefix is one of the patterns' runs the exact comparison (ci_starts_with).
 template <class P>
 TB_HD uint32_t c4_byte_scan(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n) {
   uint32_t acc = 0;
   const bool phrases = c4.filter_javascript || c4.filter_policy;
-  x.par.for_n(n, [&](uint32_t s) {
-    const uint8_t c0 = b[s];
-    if (c4.filter_curly_bracket && (c0 == '{' || c0 == '}')) acc |= C4S_CURLY;
-    if (c0 == '[' && s + 1 < n) {
-      const uint8_t c1 = b[s + 1];
-      if ((c1 >= '0' && c1 <= '9') || c1 >= 0x80) acc |= C4S_CITE;
+  const uintptr_t a0 = (uintptr_t)b & ~(uintptr_t)3;
+  const uint32_t head = (uint32_t)((uintptr_t)b - a0);
+  const uint32_t nd = (head + n + 3) >> 2;
+  const uint32_t* w = (const uint32_t*)a0;
+  auto dw = [&](uint32_t k) -> uint32_t {  // dword k of the aligned stream, bytes past the text zero
+    if (k >= nd) return 0u;
+    const int64_t e = (int64_t)4 * k + 4 - head;  // doc position one past its last byte
+    if (e <= (int64_t)n) return w[k];
+    uint32_t v = 0;
+    for (uint32_t j = 0; j < 4; ++j) {
+      const int64_t sj = (int64_t)4 * k + j - head;
+      if (sj >= 0 && sj < (int64_t)n) v |= (uint32_t)b[sj] << (8 * j);
     }
-    if (c4.filter_lorem_ipsum && (c0 == 'l' || c0 == 'L') &&
-        (!TB_C4_PREFIX3 || lower3(b + s, n - s) == pack3("lor")) && ci_starts_with(b + s, n - s, "lorem ipsum", 11))
-      acc |= C4S_LOREM;
-    if (phrases) acc |= c4_phrases_at(c4, b, n, s);
+    return v;
+  };
+  constexpr uint32_t kLor = pack3("lor"), kJav = pack3("jav"), kTer = pack3("ter"), kPri = pack3("pri"),
+                     kCoo = pack3("coo"), kUse = pack3("use");
+  x.par.for_n(nd, [&](uint32_t k) {
+    const uint64_t v = (uint64_t)dw(k) | ((uint64_t)dw(k + 1) << 32);
+    const uint64_t lo = swar_lower8(v);
+    for (uint32_t r = 0; r < 4; ++r) {
+      const int64_t sp = (int64_t)4 * k + r - head;
+      if (sp < 0 || sp >= (int64_t)n) continue;
+      const uint32_t s = (uint32_t)sp;
+      const uint32_t c0 = (uint32_t)(v >> (8 * r)) & 0xFFu;
+      const uint32_t c1 = (uint32_t)(v >> (8 * r + 8)) & 0xFFu;  // 0 past the end
+      const uint32_t l3 = (uint32_t)(lo >> (8 * r)) & 0xFFFFFFu;
+      if (c4.filter_curly_bracket && (c0 == '{' || c0 == '}')) acc |= C4S_CURLY;
+      if (c0 == '[' && ((c1 >= '0' && c1 <= '9') || c1 >= 0x80)) acc |= C4S_CITE;
+      if (c4.filter_lorem_ipsum && l3 == kLor && ci_starts_with(b + s, n - s, "lorem ipsum", 11)) acc |= C4S_LOREM;
+      if (phrases && (l3 == kJav || l3 == kTer || l3 == kPri || l3 == kCoo || l3 == kUse))
+        acc |= c4_phrases_at(c4, b, n, s);
+    }
   });
   return x.par.reduce_or(acc);
 }

@@ -310,10 +310,12 @@ std::vector<uint64_t> pow_table(uint32_t n) {
 
 uint64_t scratch_bytes_for(uint32_t doc_len) { return scratch_bytes_for_dev(doc_len); }
 
+uint64_t line_stats_buffer_words(const int64_t* off, int64_t ndocs) { return line_stats_words(off, ndocs); }
+
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
                    std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes, const uint8_t* dead,
-                   bool weak_keys) {
+                   bool weak_keys, uint32_t* line_stats) {
   DevPlan* plan = new DevPlan();
   std::memset(plan, 0, sizeof(DevPlan));
   DevStage st = build_stage(steps, idx, *plan);
@@ -346,6 +348,7 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
       x.flag = &flags[i];
       x.weak_keys = weak_keys;
       StageOut out{rec.data(), (uint32_t)ndocs, (uint32_t)i};
+      if (line_stats) out.line_stats = line_stats + line_stats_base(off[i], i);
       analyze_stage(x, st, *plan, lid ? lid->tables() : LidTables{nullptr, nullptr}, (const uint8_t*)data + off[i], n, out);
     }
   });
@@ -355,7 +358,7 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
 
 void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
                 std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,
-                std::vector<uint32_t>& flags, uint32_t lds_bytes, const uint8_t* dead) {
+                std::vector<uint32_t>& flags, uint32_t lds_bytes, const uint8_t* dead, const uint32_t* line_stats) {
   DevC4 c4 = build_c4(step);
   rec.assign((size_t)rec::C4_WIDTH * ndocs, 0);
   flags.assign(ndocs, 0);
@@ -384,7 +387,8 @@ void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int6
       x.flag = &flags[i];
       int64_t src[2] = {-1, 0};
       const uint8_t* b = (const uint8_t*)data + off[i];
-      c4_pass_a(x, c4, b, n, rec.data() + i * rec::C4_WIDTH, src);
+      c4_pass_a(x, c4, b, n, rec.data() + i * rec::C4_WIDTH, src,
+                line_stats ? line_stats + line_stats_base(off[i], i) : nullptr);
       if (flags[i] & DOC_NEEDS_CPU) continue;
       if (src[0] < 0) outs[i].assign((const char*)b, n);
       else outs[i].assign(scratch.data() + src[0], (size_t)src[1]);

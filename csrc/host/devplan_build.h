@@ -36,10 +36,14 @@ std::vector<uint64_t> pow_table(uint32_t n);  // B^0..B^n followed by B^-0..B^-n
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
                    std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes = 0,
-                   const uint8_t* dead = nullptr, bool weak_keys = false);
+                   const uint8_t* dead = nullptr, bool weak_keys = false, uint32_t* line_stats = nullptr);
+uint64_t line_stats_buffer_words(const int64_t* off, int64_t ndocs);  // u32 size of a batch's line export
+// line_stats: the C4 line export of the batch (docproc.h line_stats_base layout), written by
+// emulate_stage and read by emulate_c4 of the same content version, as on the device
 void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
                 std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,
-                std::vector<uint32_t>& flags, uint32_t lds_bytes = 0, const uint8_t* dead = nullptr);
+                std::vector<uint32_t>& flags, uint32_t lds_bytes = 0, const uint8_t* dead = nullptr,
+                const uint32_t* line_stats = nullptr);
 // Host run of k_gate (same loop body): dead[doc] = code for live docs that a gated step filters.
 void gate_host(const DevGate& g, const std::vector<const int64_t*>& recs, int64_t ndocs, const uint32_t* flags,
                uint8_t* dead, uint8_t code);

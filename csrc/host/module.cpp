@@ -844,21 +844,30 @@ PYBIND11_MODULE(_tbhost, m) {
   m.def("emulate_stage", [](const std::vector<StepCfg>& steps, const std::vector<int>& idx,
                             py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
                             int nthreads, std::shared_ptr<LangidModel> lid, uint32_t lds_bytes,
-                            std::optional<py::array_t<uint8_t, py::array::c_style>> dead, bool weak_keys) {
+                            std::optional<py::array_t<uint8_t, py::array::c_style>> dead, bool weak_keys,
+                            std::optional<py::array_t<uint32_t, py::array::c_style>> line_stats) {
     std::vector<int64_t> rec;
     std::vector<uint32_t> flags;
     const int64_t nd = (int64_t)off.size() - 1;
     if (dead && (int64_t)dead->size() < nd) throw std::runtime_error("dead mask too short");
     const uint8_t* dp = dead ? dead->data() : nullptr;
+    uint32_t* lp = nullptr;
+    if (line_stats) {
+      if ((uint64_t)line_stats->size() < line_stats_buffer_words(off.data(), nd)) throw std::runtime_error("line_stats too short");
+      lp = line_stats->mutable_data();
+    }
     {
       py::gil_scoped_release nogil;
       emulate_stage(steps, idx, nd, (const char*)data.data(), off.data(), nthreads, lid.get(), rec, flags, lds_bytes,
-                    dp, weak_keys);
+                    dp, weak_keys, lp);
     }
     return py::make_tuple(to_numpy(std::move(rec)), to_numpy(std::move(flags)));
   }, py::arg("steps"), py::arg("idx"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8,
      py::arg("lid") = nullptr, py::arg("lds_bytes") = 0, py::arg("dead") = py::none(),
-     py::arg("weak_keys") = false);
+     py::arg("weak_keys") = false, py::arg("line_stats") = py::none());
+  m.def("line_stats_words", [](py::array_t<int64_t, py::array::c_style> off) {
+    return line_stats_buffer_words(off.data(), (int64_t)off.size() - 1);
+  }, "u32 words of a batch's C4 line export buffer (docproc.h line_stats_base)");
   m.def("gate_host", [](const py::bytes& gate, const std::vector<py::array_t<int64_t, py::array::c_style>>& recs,
                         int64_t ndocs, py::array_t<uint32_t, py::array::c_style> flags,
                         py::array_t<uint8_t, py::array::c_style> dead, int code) {
@@ -881,19 +890,25 @@ PYBIND11_MODULE(_tbhost, m) {
   });
   m.def("emulate_c4", [](const StepCfg& step, py::array_t<uint8_t, py::array::c_style> data,
                          py::array_t<int64_t, py::array::c_style> off, int nthreads, uint32_t lds_bytes,
-                         std::optional<py::array_t<uint8_t, py::array::c_style>> dead) {
+                         std::optional<py::array_t<uint8_t, py::array::c_style>> dead,
+                         std::optional<py::array_t<uint32_t, py::array::c_style>> line_stats) {
     std::vector<int64_t> rec, no;
     std::vector<uint32_t> flags;
     std::string nd;
     const int64_t n = (int64_t)off.size() - 1;
     if (dead && (int64_t)dead->size() < n) throw std::runtime_error("dead mask too short");
     const uint8_t* dp = dead ? dead->data() : nullptr;
+    const uint32_t* lp = nullptr;
+    if (line_stats) {
+      if ((uint64_t)line_stats->size() < line_stats_buffer_words(off.data(), n)) throw std::runtime_error("line_stats too short");
+      lp = line_stats->data();
+    }
     {
       py::gil_scoped_release nogil;
-      emulate_c4(step, n, (const char*)data.data(), off.data(), nthreads, rec, nd, no, flags, lds_bytes, dp);
+      emulate_c4(step, n, (const char*)data.data(), off.data(), nthreads, rec, nd, no, flags, lds_bytes, dp, lp);
     }
     return py::make_tuple(to_numpy(std::move(rec)), str_to_numpy(std::move(nd)), to_numpy(std::move(no)),
                           to_numpy(std::move(flags)));
   }, py::arg("step"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8, py::arg("lds_bytes") = 0,
-     py::arg("dead") = py::none());
+     py::arg("dead") = py::none(), py::arg("line_stats") = py::none());
 }

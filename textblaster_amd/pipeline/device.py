@@ -9,6 +9,7 @@ once at the end of the batch.
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -297,6 +298,22 @@ KIND_GOPHER_QUALITY = 1
 KIND_FINEWEB = 3
 
 
+def line_stats_stages(plan: ExecPlan, stage_layout) -> Dict[int, int]:
+    """C4 line export (docproc.h export_line_stats): per content version read by a C4 pass, the
+    first stage of that version that segments words and Rust lines (GopherQuality / FineWeb);
+    it exports every line's trimmed span, word count and longest word, and the C4 pass reads them
+    instead of decoding and segmenting the text again. TB_C4_LINE_STATS=0 turns it off."""
+    out: Dict[int, int] = {}
+    if os.environ.get("TB_C4_LINE_STATS", "1") == "0":
+        return out
+    c4_versions = {plan.steps[i].version_in for i in plan.c4_steps}
+    for si, sv in enumerate(plan.stage_version):
+        kinds = {kind for kind, _, _ in stage_layout[si][1]}
+        if sv in c4_versions and sv not in out and kinds & {KIND_GOPHER_QUALITY, KIND_FINEWEB}:
+            out[sv] = si
+    return out
+
+
 def plan_passes(plan: ExecPlan, stage_layout, steps_native, gating: bool, lid_gate: bool = True):
     """Device passes in execution order (stages and C4 rewrites, by content version), the pass of
     every device step, and per pass (except the last) the gate blob over the steps it produced
@@ -558,17 +575,7 @@ class DeviceRunner:
                 st = steps_native[idx[grs[0]]]
                 if st.n_dup + st.n_top > 0:
                     self.gr_split[si] = (grs[0], st.n_dup + st.n_top + 2)
-        # C4 line statistics: the first stage of a content version that segments words and Rust
-        # lines (GopherQuality / FineWeb) exports every line's word count and longest word, and the
-        # C4 pass of that version reads them instead of segmenting the words again
-        # (docproc.h export_line_stats); TB_C4_LINE_STATS=0 turns it off
-        self.line_stats_stage = {}
-        if os.environ.get("TB_C4_LINE_STATS", "1") != "0":
-            c4_versions = {plan.steps[i].version_in for i in plan.c4_steps}
-            for si, sv in enumerate(plan.stage_version):
-                kinds = {kind for kind, _, _ in self.stage_layout[si][1]}
-                if sv in c4_versions and sv not in self.line_stats_stage and kinds & {KIND_GOPHER_QUALITY, KIND_FINEWEB}:
-                    self.line_stats_stage[sv] = si
+        self.line_stats_stage = line_stats_stages(plan, self.stage_layout)
         if not 0 <= self.lds_bytes_blk <= 131072:
             # the workgroup kernels also hold static LDS (cross-wave exchange buffers): a 160 KB
             # dynamic slice does not fit the CU's 160 KB and the launch fails with
@@ -1072,6 +1079,7 @@ class EmulatedRunner:
         self.passes, self.pass_of_step, self.gates = plan_passes(
             plan, self.stage_layout, steps_native, gating, os.environ.get("TB_LID_GATE", "1") not in ("", "0"))
         self.bw_dead_max = bw_dead_max(plan, self.passes, self.pass_of_step)
+        self.line_stats_stage = line_stats_stages(plan, self.stage_layout)
         # test hook: additionally mark every k-th document dead after the first pass (a wrong
         # device gate), to exercise the resolver's recovery path
         self.gate_corrupt = gate_corrupt
@@ -1094,6 +1102,7 @@ class EmulatedRunner:
         c4_recs = {}
         dead = np.zeros(ndocs, dtype=np.uint8) if self.gates else None
         lid_rec = {}
+        lstats = {}  # content version -> the C4 line export buffer (as on the device)
         for p, (kind, x) in enumerate(self.passes):
             skip = dead if p > 0 else None
             if kind == "lid":
@@ -1104,8 +1113,13 @@ class EmulatedRunner:
                 lid_rec[x] = rec
                 fl = _dict_script_flags(vd, vo)  # k_langid_features raises DOC_NEEDS_CPU for these
             elif kind == "stage":
-                vd, vo = versions[self.plan.stage_version[x]]
-                rec, fl = h.emulate_stage(self.steps, self.plan.stages[x], vd, vo, self.nthreads, self.lid, 0, skip)
+                sv = self.plan.stage_version[x]
+                vd, vo = versions[sv]
+                ls = None
+                if self.line_stats_stage.get(sv) == x:
+                    ls = lstats[sv] = np.empty(h.line_stats_words(vo), dtype=np.uint32)
+                rec, fl = h.emulate_stage(self.steps, self.plan.stages[x], vd, vo, self.nthreads, self.lid, 0, skip,
+                                          line_stats=ls)
                 if x in lid_rec:
                     for k, width, prefix in self.stage_layout[x][1]:
                         if k == KIND_LANGID:
@@ -1113,7 +1127,8 @@ class EmulatedRunner:
                 stage_recs[x] = rec
             else:
                 vd, vo = versions[self.plan.steps[x].version_in]
-                rec, nd, no, fl = h.emulate_c4(self.steps[x], vd, vo, self.nthreads, 0, skip)
+                rec, nd, no, fl = h.emulate_c4(self.steps[x], vd, vo, self.nthreads, 0, skip,
+                                               line_stats=lstats.get(self.plan.steps[x].version_in))
                 c4_recs[x] = rec
                 versions[self.plan.steps[x].version_out] = (nd, no)
             flags |= fl

@@ -50,6 +50,12 @@ _SIGS = {
     "tb_bpe_count": [_P, _P, _P, _P, _P, _I32, _P],
     "tb_sizeof_bpe": [],
     "tb_abi_version": [],
+    # Parquet text-column decoding (csrc/hip/parquet.hip)
+    "tb_sizeof_pq_page": [],
+    "tb_pq_decompress": [_P, _P, _P, _I32, _P, _P],
+    "tb_pq_dict": [_P, _P, _I32, _P, _P, _P, _P],
+    "tb_pq_values": [_P, _P, _P, _I32, _P, _P, _P, _I32, _P, _P, _P, _I64, _P],
+    "tb_pq_gather": [_P, _P, _P, _P, _I64, _P],
     # native runtime layer (csrc/hip/runtime.hip)
     "tbrt_device_count": [_P], "tbrt_set_device": [_I32], "tbrt_get_device": [_P], "tbrt_device_sync": [],
     "tbrt_mem_info": [_P, _P], "tbrt_malloc": [_P, _SZ], "tbrt_free": [_P], "tbrt_host_alloc": [_P, _SZ],

@@ -77,6 +77,8 @@ class RunConfig:
     tokenizer_dir: Optional[str] = None
     badwords_dir: Optional[str] = None
     html_decode: str = "cpu"           # input HTML entity decoding: cpu (C++ host) | gpu (K17 kernels)
+    parquet_decode: str = "auto"       # text column decoding: cpu (pyarrow) | gpu (csrc/hip/parquet.hip) |
+                                       # auto (gpu on a GPU rank)
     metrics_port: Optional[int] = None
     progress_interval: float = 1.0
     tokenizer_file: Optional[str] = None
@@ -174,7 +176,7 @@ class _UnitReader:
         if u.row_group != self._rg:
             pf = self._pf if self._pf is not None else self.reader._pf
             with tracing.trace_range("tb.read_row_group"):
-                self._tbl = pf.read_row_group(u.row_group, columns=self.reader.columns, use_threads=self._use_threads)
+                self._tbl = self.reader.read_row_group(u.row_group, pf, self._use_threads)
             self._rg = u.row_group
         t = self._tbl.slice(u.start, u.stop - u.start).combine_chunks()
         batches = t.to_batches()
@@ -548,7 +550,18 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
         html_dec = HtmlDecoder(dev)
     elif rc.html_decode != "cpu":
         raise PipelineError(f"unknown html decode backend {rc.html_decode!r} (cpu | gpu)")
-    reader = ParquetReader(ParquetInputConfig(rc.input_file, rc.text_column, rc.id_column), html_decoder=html_dec)
+    text_dec = None
+    if rc.parquet_decode not in ("cpu", "gpu", "auto"):
+        raise PipelineError(f"unknown parquet decode backend {rc.parquet_decode!r} (cpu | gpu | auto)")
+    if rc.parquet_decode == "gpu" or (rc.parquet_decode == "auto" and rc.backend == "cuda"):
+        dev = ctx.device if ctx.device is not None else ("cuda" if rc.backend == "cuda" else None)
+        if dev is None:
+            raise PipelineError("--parquet-decode gpu needs a GPU rank")
+        from .ops.parquet_gpu import GpuTextColumn
+
+        text_dec = GpuTextColumn(rc.input_file, rc.text_column, dev)
+    reader = ParquetReader(ParquetInputConfig(rc.input_file, rc.text_column, rc.id_column), html_decoder=html_dec,
+                           text_decoder=text_dec)
     units = plan_units(reader, rc.unit_rows)
     use_parts = world > 1 or rc.checkpoint or rc.resume
     work_dir = rc.work_dir or (rc.output_file + ".work")

@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "e2e"))
     ap.add_argument("--timeline", action="store_true", help="record the host timeline (TB_TIMELINE) per backend")
     ap.add_argument("--html-decode", default="cpu")
+    ap.add_argument("--parquet-decode", action="append", default=None,
+                    help="text column decoding (cpu | gpu | auto); repeat to run several")
     ap.add_argument("--keep-input", action="store_true")
     ap.add_argument("--repeat", type=int, default=1, help="runs per backend (all reported; the median last)")
     ap.add_argument("--cli", action="store_true",
@@ -98,18 +100,19 @@ def main():
     from textblaster_amd.runner import RunConfig, run
     from textblaster_amd.utils import tracing
 
-    runs = [b for b in (args.backend or ["cuda"]) for _ in range(args.repeat)]
+    runs = [(b, pd) for b in (args.backend or ["cuda"]) for pd in (args.parquet_decode or ["auto"])
+            for _ in range(args.repeat)]
     rates = {}
-    for backend in runs:
+    for backend, pdec in runs:
         o = os.path.join(args.out, f"{backend}.out.parquet")
         e = os.path.join(args.out, f"{backend}.excluded.parquet")
         tl = os.path.join(args.out, f"timeline_{backend}.json") if args.timeline else None
         tracing.record_timeline(tl)
         cpu0 = thread_cpu()
         st = run(RunConfig(inp, o, e, args.config, backend=backend, unit_rows=args.unit_rows,
-                           html_decode=args.html_decode))
+                           html_decode=args.html_decode, parquet_decode=pdec))
         cpu = cpu_by_name(cpu0, thread_cpu())
-        line = {"backend": backend, "docs": st.docs, "kept": st.kept, "excluded": st.excluded, "errors": st.errors,
+        line = {"backend": backend, "parquet_decode": pdec, "docs": st.docs, "kept": st.kept, "excluded": st.excluded, "errors": st.errors,
                 "seconds": round(st.seconds, 3), "docs_per_sec": round(st.docs_per_sec, 1),
                 "step_filtered": st.step_filtered, "delegated": st.delegated,
                 "phase_seconds": {k: round(v, 3) for k, v in st.phase_seconds.items() if not k.startswith("cpu_")},
@@ -119,7 +122,7 @@ def main():
                 "cpu_us_per_doc": round(1e6 * st.phase_seconds.get("cpu_total", 0.0) / max(st.docs, 1), 3),
                 "cpu_seconds_by_os_thread": cpu}
         print(json.dumps(line), flush=True)
-        rates.setdefault(backend, []).append(line["docs_per_sec"])
+        rates.setdefault(f"{backend}/{pdec}", []).append(line["docs_per_sec"])
         if tl:
             sys.path.insert(0, os.path.join(ROOT, "tools"))
             from timeline_summary import summarise

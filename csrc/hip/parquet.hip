@@ -42,10 +42,31 @@ static_assert(sizeof(PqDev) == 64, "PqDev layout (ops/parquet_gpu.py)");
 
 enum : uint32_t { PQE_SNAPPY = 1, PQE_LEVELS = 2, PQE_VALUES = 4, PQE_DICT = 8, PQE_BOUNDS = 16 };
 
-constexpr uint32_t kRing = 32768;  // LDS output history per wave (bytes, power of two)
+#ifndef TB_PQ_RING
+#define TB_PQ_RING 32768
+#endif
+constexpr uint32_t kRing = TB_PQ_RING;  // LDS output history per wave (bytes, power of two)
 constexpr uint32_t kWin = 512;     // register window of the compressed input (8 bytes per lane)
 
 __device__ __forceinline__ void set_err(uint32_t* err, uint32_t e) { atomicOr(err, e); }
+
+// in[0, n) -> out[0, n), whole wave: 16 independent byte loads per lane before the stores.
+__device__ void copy_wave(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint32_t n) {
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t base = 0; base < n; base += 64 * 16) {
+    uint8_t v[16];
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+      const uint32_t i = base + k * 64 + lane;
+      v[k] = i < n ? in[i] : 0;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+      const uint32_t i = base + k * 64 + lane;
+      if (i < n) out[i] = v[k];
+    }
+  }
+}
 
 // Snappy raw block in[0, nin) -> o[0, nout). Whole-wave (uniform) control flow.
 __device__ bool snappy_wave(const uint8_t* __restrict__ in, uint32_t nin, uint8_t* __restrict__ o, uint32_t nout,
@@ -68,6 +89,10 @@ __device__ bool snappy_wave(const uint8_t* __restrict__ in, uint32_t nin, uint8_
         if (k < 4) lo |= v << (8 * k); else hi |= v << (8 * (k - 4));
       }
     }
+    // consume the loads here: gfx9 counts loads and stores on one vmcnt, so a window register
+    // still pending at the token loop's head would make every token wait for all earlier
+    // output stores (measured: ~1 us per token)
+    asm volatile("" ::"v"(lo), "v"(hi));
     wlo = lo;
     whi = hi;
   };
@@ -144,11 +169,15 @@ __device__ bool snappy_wave(const uint8_t* __restrict__ in, uint32_t nin, uint8_
     }
     if (off == 0 || off > op || op + len > nout) return false;
     // len <= 64: one step; a source position is op - off + (j % off) < op (already written)
-    const bool from_ring = off <= kRing - 64;
+    // (two branches, not a select: a pointer select becomes a flat load, which waits for every
+    // outstanding output store before it returns)
+    const uint32_t s = op - off + (off >= 64 ? lane : lane % off);
     uint32_t v = 0;
-    if (lane < len) {
-      const uint32_t s = op - off + (off >= 64 ? lane : lane % off);
-      v = from_ring ? ring[s & (kRing - 1)] : o[s];
+    if (off <= kRing - 64) {
+      if (lane < len) v = ring[s & (kRing - 1)];
+    } else {
+      if (lane < len) v = o[s];
+      asm volatile("" : "+v"(v));  // wait for this load here, not at the shared store below
     }
     __builtin_amdgcn_wave_barrier();
     if (lane < len) {
@@ -172,11 +201,11 @@ __global__ __launch_bounds__(64) void k_pq_decompress(const uint8_t* __restrict_
   const uint8_t* in = chunk + d.in_off;
   uint8_t* out = pagebuf + d.out_off;
   const uint32_t raw = (uint32_t)d.raw;
-  for (uint32_t i = lane; i < raw; i += 64) out[i] = in[i];
   if (d.codec == 0) {
-    for (uint32_t i = raw + lane; i < (uint32_t)d.out_size; i += 64) out[i] = in[i];
+    copy_wave(in, out, (uint32_t)d.out_size);
     return;
   }
+  copy_wave(in, out, raw);
   if (!snappy_wave(in + raw, (uint32_t)d.in_size - raw, out + raw, (uint32_t)d.out_size - raw, ring) && lane == 0)
     set_err(err, PQE_SNAPPY);
 }

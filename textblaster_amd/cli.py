@@ -148,7 +148,7 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("--badwords-dir", default=None, help="dir holding the C4 bad-words lists (<lang> files)")
         p.add_argument("--html-decode", choices=("cpu", "gpu"), default="cpu",
                        help="decode HTML entities of the input text on the host (default) or the GPU")
-        p.add_argument("--parquet-decode", choices=("cpu", "gpu", "auto"), default="auto",
+        p.add_argument("--parquet-decode", choices=("cpu", "gpu", "auto"), default="cpu",
                        help="decode the input text column with pyarrow (cpu) or on the GPU (Snappy, levels, "
                             "PLAIN/dictionary values; auto: on GPU ranks)")
         p.add_argument("--log-dir", default="./log")

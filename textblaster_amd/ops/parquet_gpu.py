@@ -14,6 +14,7 @@ malformed input, so the caller decodes that row group with pyarrow.
 """
 from __future__ import annotations
 
+import os
 import threading
 from typing import Optional, Tuple
 
@@ -78,6 +79,35 @@ def page_table(chunk: np.ndarray, codec: int, max_def: int, nrows: int):
     return np.array(out, dtype=PQ_PAGE), dict_page, np.array(data, dtype=np.int32), out_off
 
 
+def _wait(ev) -> None:
+    """Waits for an event by polling with short sleeps: the reader threads must not spin a core
+    each while the device decodes (hipEventSynchronize busy-waits on this runtime)."""
+    import time
+
+    while not ev.query():
+        time.sleep(0.0002)
+
+
+class _Ticker:
+    """Accumulates (wall, thread CPU) seconds per stage into a shared dict."""
+
+    def __init__(self, acc: dict, lock):
+        import time
+
+        self.time = time
+        self.acc = acc
+        self.lock = lock
+        self.t = time.perf_counter()
+        self.c = time.thread_time()
+
+    def __call__(self, name: str) -> None:
+        t, c = self.time.perf_counter(), self.time.thread_time()
+        with self.lock:
+            w, u = self.acc.get(name, (0.0, 0.0))
+            self.acc[name] = (w + t - self.t, u + c - self.c)
+        self.t, self.c = t, c
+
+
 class GpuTextColumn:
     """Decodes one string column of a Parquet file, row group by row group, on a device. Safe to
     call from several reader threads (each decodes on its own stream)."""
@@ -103,9 +133,11 @@ class GpuTextColumn:
             self.max_def = int(sc.max_definition_level)
             self.ok = (sc.physical_type == "BYTE_ARRAY" and int(sc.max_repetition_level) == 0
                        and self.max_def <= 1 and sc.path.count(".") == 0)
-        self._mm = np.memmap(path, dtype=np.uint8, mode="r") if self.ok else None
+        self.file_size = os.path.getsize(path) if self.ok else 0
         self._tls = threading.local()
         self.stats = {"row_groups": 0, "fallback": 0, "bytes_in": 0, "bytes_out": 0}
+        # seconds (wall, thread CPU) per stage, summed over calls: file, table, launch, wait, gather
+        self.timing = {}
         self._lock = threading.Lock()
 
     def _stream(self):
@@ -129,10 +161,19 @@ class GpuTextColumn:
         if cc.has_dictionary_page and cc.dictionary_page_offset is not None and cc.dictionary_page_offset > 0:
             start = min(start, cc.dictionary_page_offset)
         size = int(cc.total_compressed_size)
-        if start < 0 or start + size > self._mm.size:
+        if start < 0 or start + size > self.file_size:
             return self._fallback()
-        chunk = np.ascontiguousarray(self._mm[start:start + size])
+        rt = self.rt
+        rt.set_device(self.device)
+        tick = _Ticker(self.timing, self._lock)
+        # the chunk goes from the file straight into page-locked memory (DMA'd to the device)
+        chunk = rt.pinned(size, np.uint8)
+        f = self._file()
+        f.seek(start)
+        if f.readinto(memoryview(chunk)) != size:
+            return self._fallback()
         nrows = int(md.num_rows)
+        tick("file")
         try:
             t = page_table(chunk, codec, self.max_def, nrows)
         except RuntimeError:
@@ -140,8 +181,7 @@ class GpuTextColumn:
         if t is None:
             return self._fallback()
         pages, dict_page, data_idx, buf_bytes = t
-        rt = self.rt
-        rt.set_device(self.device)
+        tick("table")
         s = self._stream()
         lib = self.lib
         with rt.stream(s):
@@ -170,29 +210,37 @@ class GpuTextColumn:
                    "tb_pq_values")
             off = rt.zeros(nrows + 1, np.int64, s)
             rt.scan_strided_i64(lens, 1, nrows, off[1:], s)
-            head = np.zeros(2, np.int64)
-            e = np.zeros(1, np.uint32)
-            off[nrows:].copy_to_host(head[:1], s)
+            h_off = rt.pinned(nrows + 1, np.int64)
+            h_valid = rt.pinned(max(nrows, 1), np.uint8)[:nrows]
+            e = rt.pinned(1, np.uint32)
+            off.copy_to_host(h_off, s)
+            valid[:nrows].copy_to_host(h_valid, s)
             err.copy_to_host(e, s)
-            s.synchronize()
+            tick("launch")
+            _wait(s.record())
+            tick("wait")
             if int(e[0]) != 0:
                 return self._fallback()
-            total = int(head[0])
+            total = int(h_off[nrows])
             out = rt.empty(max(total, 1), np.uint8)
             _check(lib.tb_pq_gather(s.handle, pagebuf.data_ptr(), src.data_ptr(), off.data_ptr(), nrows,
                                     out.data_ptr()), "tb_pq_gather")
-            h_data = np.empty(total, np.uint8)
-            h_off = np.empty(nrows + 1, np.int64)
-            h_valid = np.empty(nrows, np.uint8)
+            # page-locked output: the engine uploads pinned batch inputs in place (zero copy)
+            h_data = rt.pinned(max(total, 1), np.uint8)[:total]
             out[:total].copy_to_host(h_data, s)
-            off.copy_to_host(h_off, s)
-            valid[:nrows].copy_to_host(h_valid, s)
-            s.synchronize()
+            _wait(s.record())
+            tick("gather")
         with self._lock:
             self.stats["row_groups"] += 1
             self.stats["bytes_in"] += size
             self.stats["bytes_out"] += total
         return h_data, h_off, h_valid
+
+    def _file(self):  # noqa: E301
+        f = getattr(self._tls, "file", None)
+        if f is None:
+            f = self._tls.file = open(self.path, "rb", buffering=0)
+        return f
 
     def _fallback(self):
         with self._lock:

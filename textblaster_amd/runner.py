@@ -77,8 +77,8 @@ class RunConfig:
     tokenizer_dir: Optional[str] = None
     badwords_dir: Optional[str] = None
     html_decode: str = "cpu"           # input HTML entity decoding: cpu (C++ host) | gpu (K17 kernels)
-    parquet_decode: str = "auto"       # text column decoding: cpu (pyarrow) | gpu (csrc/hip/parquet.hip) |
-                                       # auto (gpu on a GPU rank)
+    parquet_decode: str = "cpu"        # text column decoding: cpu (pyarrow) | gpu (csrc/hip/parquet.hip) |
+                                       # auto (gpu on a GPU rank); see profiles/r4_parquet
     metrics_port: Optional[int] = None
     progress_interval: float = 1.0
     tokenizer_file: Optional[str] = None

@@ -85,6 +85,7 @@ def main():
     ap.add_argument("--parquet-decode", action="append", default=None,
                     help="text column decoding (cpu | gpu | auto); repeat to run several")
     ap.add_argument("--keep-input", action="store_true")
+    ap.add_argument("--decode-only", action="store_true", help="time the text-column decoders alone")
     ap.add_argument("--repeat", type=int, default=1, help="runs per backend (all reported; the median last)")
     ap.add_argument("--cli", action="store_true",
                     help="also run the CLI (`python -m textblaster_amd.cli run --backend cuda`) as a child process: "
@@ -99,6 +100,29 @@ def main():
           flush=True)
     from textblaster_amd.runner import RunConfig, run
     from textblaster_amd.utils import tracing
+
+    if args.decode_only:
+        # the text column of every row group through the device decoder and through pyarrow
+        # (one thread each): wall and thread-CPU seconds per stage
+        import pyarrow.parquet as pq
+
+        from textblaster_amd.ops.parquet_gpu import GpuTextColumn
+
+        dec = GpuTextColumn(inp, "text", 0)
+        pf = pq.ParquetFile(inp)
+        for rep in range(2):
+            dec.timing.clear()
+            t0, c0 = time.perf_counter(), time.thread_time()
+            for rg in range(pf.num_row_groups):
+                dec.read(rg)
+            g = (time.perf_counter() - t0, time.thread_time() - c0)
+            t0, c0 = time.perf_counter(), time.thread_time()
+            for rg in range(pf.num_row_groups):
+                pf.read_row_group(rg, columns=["text"], use_threads=False)
+            c = (time.perf_counter() - t0, time.thread_time() - c0)
+            print(json.dumps({"decode_only": rep, "row_groups": pf.num_row_groups, "gpu_wall_cpu": g,
+                              "pyarrow_wall_cpu": c, "gpu_stages": dec.timing, "stats": dec.stats}), flush=True)
+        return
 
     runs = [(b, pd) for b in (args.backend or ["cuda"]) for pd in (args.parquet_decode or ["auto"])
             for _ in range(args.repeat)]

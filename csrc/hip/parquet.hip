@@ -11,11 +11,9 @@
 //                    (offset, length) in the page buffer
 //   k_pq_gather      one wave per row: strings into one packed buffer at the scanned offsets
 //
-// Snappy (one wave per page): the token stream is parsed uniformly by the whole wave from a
-// 512-byte register window of the compressed input (bytes fetched with readlane), literal bytes
-// are copied lane-parallel out of the window (ds_bpermute), and copies read the last 32 KB of
-// output from an LDS ring (older offsets from the output in HBM); a copy shorter than its offset
-// is one lane-parallel step, a self-overlapping one replicates its period (lane % offset).
+// Snappy (one wave per page, snappy_batched below): 64 input positions per step, token starts
+// found lane-parallel, the batch's output written 64 bytes at a time from the staged input and
+// a 32 KB LDS history ring (older offsets from the output in HBM).
 // Every malformed input (bad tag, offset or length, truncated stream, size mismatch) sets the
 // error word and the caller decodes the row group with pyarrow instead.
 #include <hip/hip_runtime.h>
@@ -46,7 +44,6 @@ enum : uint32_t { PQE_SNAPPY = 1, PQE_LEVELS = 2, PQE_VALUES = 4, PQE_DICT = 8, 
 #define TB_PQ_RING 32768
 #endif
 constexpr uint32_t kRing = TB_PQ_RING;  // LDS output history per wave (bytes, power of two)
-constexpr uint32_t kWin = 512;     // register window of the compressed input (8 bytes per lane)
 
 __device__ __forceinline__ void set_err(uint32_t* err, uint32_t e) { atomicOr(err, e); }
 
@@ -68,124 +65,198 @@ __device__ void copy_wave(const uint8_t* __restrict__ in, uint8_t* __restrict__ 
   }
 }
 
-// Snappy raw block in[0, nin) -> o[0, nout). Whole-wave (uniform) control flow.
-__device__ bool snappy_wave(const uint8_t* __restrict__ in, uint32_t nin, uint8_t* __restrict__ o, uint32_t nout,
-                            uint8_t* ring) {
+// Batched Snappy decoding (one wave per page): per step the wave looks at the 64 input positions
+// [ip, ip + 64) at once. Every lane decodes "a token starting at my position" (its input length L,
+// output length O, and literal source or copy offset) from the input staged in LDS; a short
+// scalar walk over those lane results (readlane, ~10 SALU per token) picks the real token
+// starts; one wave prefix sum gives each token its output position; then the batch's output is
+// produced 64 bytes at a time, every lane finding its byte's token by binary search: literal bytes
+// come from the staged input, copy bytes from the LDS history ring — a source inside the same
+// 64-byte chunk is resolved in a few ballot rounds (sources always lie before their byte). One
+// coalesced store per 64 output bytes; ~10x fewer instructions per token than walking tokens
+// one by one with the whole wave.
+constexpr uint32_t kStage = 4096;  // staged input bytes (LDS)
+
+__device__ bool snappy_batched(const uint8_t* __restrict__ in, uint32_t nin, uint8_t* __restrict__ o, uint32_t nout,
+                               uint8_t* ring, uint8_t* inb, uint32_t* tok) {
   const uint32_t lane = threadIdx.x;
-  uint32_t wb = 0;
-  uint32_t wlo = 0, whi = 0;  // bytes [wb + 8 lane, +8) of the input
-  auto refill = [&](uint32_t base) {
-    wb = base;
-    const uint32_t s = base + 8 * lane;
-    uint32_t lo = 0, hi = 0;
-    if (s + 8 <= nin) {
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint32_t ib = 0, ie = 0;  // staged input range [ib, ie)
+  auto stage = [&](uint32_t base) {
+    ib = base;
+    ie = base + kStage < nin ? base + kStage : nin;
+    const uint32_t n = ie - ib;
+    for (uint32_t c = 0; c < n; c += 64 * 16) {
+      uint32_t v[16];
 #pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) lo |= (uint32_t)in[s + k] << (8 * k);
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint32_t i = c + k * 64 + lane;
+        v[k] = i < n ? in[ib + i] : 0u;
+      }
 #pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) hi |= (uint32_t)in[s + 4 + k] << (8 * k);
-    } else {
-      for (uint32_t k = 0; k < 8; ++k) {
-        const uint32_t v = s + k < nin ? (uint32_t)in[s + k] : 0u;
-        if (k < 4) lo |= v << (8 * k); else hi |= v << (8 * (k - 4));
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint32_t i = c + k * 64 + lane;
+        // wait for the loads here: gfx9 counts loads and stores on one vmcnt, so a value still
+        // pending later would make the token loop wait for every earlier output store
+        asm volatile("" : "+v"(v[k]));
+        if (i < n) inb[i] = (uint8_t)v[k];
       }
     }
-    // consume the loads here: gfx9 counts loads and stores on one vmcnt, so a window register
-    // still pending at the token loop's head would make every token wait for all earlier
-    // output stores (measured: ~1 us per token)
-    asm volatile("" ::"v"(lo), "v"(hi));
-    wlo = lo;
-    whi = hi;
+    // zero slack after the staged bytes: header reads near the end see zeros
+    inb[ie - ib + lane] = 0;
+    __builtin_amdgcn_wave_barrier();
   };
-  auto byte_at = [&](uint32_t q) -> uint32_t {  // uniform q in [wb, wb + kWin)
-    const uint32_t r = q - wb;
-    const uint32_t src = r >> 3;
-    const uint32_t w = (r & 4) ? (uint32_t)__builtin_amdgcn_readlane((int)whi, (int)src)
-                               : (uint32_t)__builtin_amdgcn_readlane((int)wlo, (int)src);
-    return (w >> (8 * (r & 3))) & 0xFFu;
-  };
-  refill(0);
-  // preamble: varint of the uncompressed length
+  auto ib_at = [&](uint32_t q) -> uint32_t { return inb[q - ib]; };  // q in [ib, ie + 63]
+  stage(0);
   uint32_t ip = 0, ulen = 0;
   for (uint32_t shift = 0;; shift += 7) {
     if (ip >= nin || shift > 28) return false;
-    const uint32_t b = byte_at(ip++);
+    const uint32_t b = ib_at(ip++);
     ulen |= (b & 0x7Fu) << shift;
     if (!(b & 0x80u)) break;
   }
   if (ulen != nout) return false;
   uint32_t op = 0;
   while (ip < nin) {
-    if (ip + 5 > wb + kWin) refill(ip);
-    const uint32_t tag = byte_at(ip);
-    uint32_t len, off = 0;
-    const uint32_t kind = tag & 3u;
-    if (kind == 0) {
-      uint32_t l = tag >> 2;
-      ip += 1;
-      if (l >= 60) {
-        const uint32_t nb = l - 59;
-        if (ip + nb > nin) return false;
-        l = 0;
-        for (uint32_t k = 0; k < nb; ++k) l |= byte_at(ip + k) << (8 * k);
-        ip += nb;
+    if (ip + 64 + 5 > ie && ie < nin) stage(ip);
+    // ---- every lane: the token that would start at p = ip + lane ----
+    const uint32_t p = ip + lane;
+    uint32_t L = 0xFFFFFFFFu, O = 0, src = 0, lit = 0;
+    if (p < nin) {
+      const uint32_t t = ib_at(p);
+      const uint32_t b1 = ib_at(p + 1), b2 = ib_at(p + 2), b3 = ib_at(p + 3), b4 = ib_at(p + 4);
+      const uint32_t kind = t & 3u;
+      if (kind == 0) {
+        uint32_t l = t >> 2, hdr = 1;
+        if (l >= 60) {
+          const uint32_t nb = l - 59;
+          const uint32_t v = b1 | (b2 << 8) | (b3 << 16) | (b4 << 24);
+          l = nb == 4 ? v : (v & ((1u << (8 * nb)) - 1u));
+          hdr = 1 + nb;
+        }
+        const uint64_t len = (uint64_t)l + 1;
+        const uint64_t ll = hdr + len;
+        L = ll > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)ll;
+        O = len > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)len;
+        src = p + hdr;
+        lit = 1;
+      } else if (kind == 1) {
+        L = 2; O = 4 + ((t >> 2) & 7u); src = ((t >> 5) << 8) | b1;
+      } else if (kind == 2) {
+        L = 3; O = (t >> 2) + 1; src = b1 | (b2 << 8);
+      } else {
+        L = 5; O = (t >> 2) + 1; src = b1 | (b2 << 8) | (b3 << 16) | (b4 << 24);
       }
-      len = l + 1;
-      if (len == 0 || ip + len > nin || op + len > nout) return false;
-      // literal: lane-parallel out of the window, 64 bytes per step
+    }
+    // ---- scalar walk over the lanes' results: the real token starts of this window ----
+    uint64_t starts = 0;
+    uint32_t pos = 0, Ob = 0, T = 0;
+    bool long_lit = false;
+    while (pos < 64 && ip + pos < nin) {
+      const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)L, (int)pos);
+      const uint32_t oo = (uint32_t)__builtin_amdgcn_readlane((int)O, (int)pos);
+      const uint32_t lt = (uint32_t)__builtin_amdgcn_readlane((int)lit, (int)pos);
+      const uint32_t sv = (uint32_t)__builtin_amdgcn_readlane((int)src, (int)pos);
+      if (l > nin - (ip + pos)) return false;                      // token runs past the input
+      if ((uint64_t)op + Ob + oo > nout) return false;              // output overflow
+      if (lt) {
+        if (ip + pos + l > ie) {                                     // literal data not staged
+          if (T == 0) long_lit = true;
+          break;
+        }
+      } else if (sv == 0 || sv > op + Ob) {
+        return false;                                                // bad copy offset
+      }
+      starts |= 1ull << pos;
+      ++T;
+      Ob += oo;
+      pos += l;
+    }
+    if (long_lit) {
+      // a literal longer than the staged input: alone, restaging as it goes
+      const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)L, 0);
+      const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)O, 0);
+      uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)src, 0);
       for (uint32_t c = 0; c < len; c += 64) {
-        const uint32_t q = ip + c;
-        if (q + 64 > wb + kWin) refill(q);
-        const uint32_t r = q + lane - wb;
-        const int src = (int)((r >> 3) & 63u) << 2;  // byte address of the source lane
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)wlo);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)whi);
-        const uint32_t w = (r & 4) ? hi : lo;
-        const uint32_t v = (w >> (8 * (r & 3))) & 0xFFu;
+        if (q + c + 64 > ie && ie < nin) stage(q + c);
         const uint32_t j = c + lane;
         if (j < len) {
-          o[op + j] = (uint8_t)v;
+          const uint32_t v = ib_at(q + j);
           ring[(op + j) & (kRing - 1)] = (uint8_t)v;
+          o[op + j] = (uint8_t)v;
         }
       }
-      ip += len;
       op += len;
+      ip += l;
       continue;
     }
-    if (kind == 1) {
-      if (ip + 2 > nin) return false;
-      len = 4 + ((tag >> 2) & 7u);
-      off = ((tag >> 5) << 8) | byte_at(ip + 1);
-      ip += 2;
-    } else if (kind == 2) {
-      if (ip + 3 > nin) return false;
-      len = (tag >> 2) + 1;
-      off = byte_at(ip + 1) | (byte_at(ip + 2) << 8);
-      ip += 3;
-    } else {
-      if (ip + 5 > nin) return false;
-      len = (tag >> 2) + 1;
-      off = byte_at(ip + 1) | (byte_at(ip + 2) << 8) | (byte_at(ip + 3) << 16) | (byte_at(ip + 4) << 24);
-      ip += 5;
+    if (T == 0) return false;
+    // ---- token table: output start, source, kind (by token rank) ----
+    const bool is_start = (starts >> lane) & 1ull;
+    uint32_t x = is_start ? O : 0u;  // exclusive prefix of output lengths over the starts
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+      if ((int)lane >= d) x += y;
     }
-    if (off == 0 || off > op || op + len > nout) return false;
-    // len <= 64: one step; a source position is op - off + (j % off) < op (already written)
-    // (two branches, not a select: a pointer select becomes a flat load, which waits for every
-    // outstanding output store before it returns)
-    const uint32_t s = op - off + (off >= 64 ? lane : lane % off);
-    uint32_t v = 0;
-    if (off <= kRing - 64) {
-      if (lane < len) v = ring[s & (kRing - 1)];
-    } else {
-      if (lane < len) v = o[s];
-      asm volatile("" : "+v"(v));  // wait for this load here, not at the shared store below
+    const uint32_t excl = x - (is_start ? O : 0u);
+    if (is_start) {
+      const uint32_t r = (uint32_t)__popcll(starts & below);
+      tok[r] = excl;                             // output start (relative to op)
+      tok[64 + r] = src;                         // literal: input position; copy: offset
+      tok[128 + r] = lit;
     }
     __builtin_amdgcn_wave_barrier();
-    if (lane < len) {
-      o[op + lane] = (uint8_t)v;
-      ring[(op + lane) & (kRing - 1)] = (uint8_t)v;
+    // ---- the batch's output, 64 bytes at a time ----
+    for (uint32_t c = 0; c < Ob; c += 64) {
+      const uint32_t q = c + lane;  // relative to op
+      const bool act = q < Ob;
+      uint32_t k = 0;
+      if (act) {  // last token with start <= q
+        uint32_t lo = 0, hi = T;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (tok[mid] <= q) lo = mid; else hi = mid;
+        }
+        k = lo;
+      }
+      uint32_t v = 0, sabs = 0;
+      bool res = !act;
+      if (act) {
+        const uint32_t ts = tok[k], sv = tok[64 + k];
+        const uint32_t d = q - ts;
+        if (tok[128 + k]) {
+          v = ib_at(sv + d);
+          res = true;
+        } else {
+          sabs = op + ts - sv + (sv >= 64 ? d : d % sv);  // absolute source (< op + q)
+          if (sabs < op + c) {
+            if (sv <= kRing - 64) {
+              v = ring[sabs & (kRing - 1)];
+            } else {
+              v = o[sabs];
+              asm volatile("" : "+v"(v));
+            }
+            res = true;
+          }
+        }
+        if (res) ring[(op + q) & (kRing - 1)] = (uint8_t)v;
+      }
+      // sources inside this chunk: a few ballot rounds (each resolves at least the first pending byte)
+      uint64_t done = __ballot(res);
+      while (done != ~0ull) {
+        __builtin_amdgcn_wave_barrier();
+        if (!res && ((done >> (sabs - (op + c))) & 1ull)) {
+          v = ring[sabs & (kRing - 1)];
+          ring[(op + q) & (kRing - 1)] = (uint8_t)v;
+          res = true;
+        }
+        done = __ballot(res);
+      }
+      if (act) o[op + q] = (uint8_t)v;
     }
-    __builtin_amdgcn_wave_barrier();
-    op += len;
+    op += Ob;
+    ip += pos;
   }
   return op == nout;
 }
@@ -194,6 +265,8 @@ __global__ __launch_bounds__(64) void k_pq_decompress(const uint8_t* __restrict_
                                                       int32_t npages, uint8_t* __restrict__ pagebuf,
                                                       uint32_t* __restrict__ err) {
   __shared__ uint8_t ring[kRing];
+  __shared__ uint8_t inb[kStage + 64];
+  __shared__ uint32_t tok[3 * 64];
   const int p = (int)blockIdx.x;
   if (p >= npages) return;
   const PqDev d = pages[p];
@@ -206,7 +279,8 @@ __global__ __launch_bounds__(64) void k_pq_decompress(const uint8_t* __restrict_
     return;
   }
   copy_wave(in, out, raw);
-  if (!snappy_wave(in + raw, (uint32_t)d.in_size - raw, out + raw, (uint32_t)d.out_size - raw, ring) && lane == 0)
+  if (!snappy_batched(in + raw, (uint32_t)d.in_size - raw, out + raw, (uint32_t)d.out_size - raw, ring, inb, tok) &&
+      lane == 0)
     set_err(err, PQE_SNAPPY);
 }
 

@@ -2018,14 +2018,12 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   x.par.single([&]() { poff[NLn] = Ptot; });
   x.stamp(PH_C4_CITE);
   // ---- words of the processed lines ----
-  Cps pc = decode(x, Pb, Ptot);
-  Words pwd = words(x, pc);
   uint32_t* nw = x.template alloc_hot<uint32_t>(NLn + 1);
   uint32_t* mx = x.template alloc_hot<uint32_t>(NLn + 1);
   uint32_t* pf = x.template alloc_hot<uint32_t>(NLn + 1);  // pattern flags per line
   uint8_t* code = x.template alloc_hot<uint8_t>(NLn + 1);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
-  x.par.for_n(NLn, [&](uint32_t k) { nw[k] = 0; mx[k] = 0; pf[k] = 0; });
+  x.par.for_n(NLn, [&](uint32_t k) { nw[k] = 0; mx[k] = 0; pf[k] = 0; code[k] = 0; });
   x.par.sync();
   auto line_of_byte = [&](uint32_t bs) {  // last line with poff <= bs
     uint32_t lo = 0, hi = NLn;
@@ -2035,11 +2033,58 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
     }
     return lo;
   };
-  x.par.for_n(pwd.n, [&](uint32_t q) {
-    const uint32_t lo = line_of_byte(pwd.bs[q]);
-    P::add32(&nw[lo], 1u);
-    P::max32(&mx[lo], pwd.ce[q] - pwd.cs[q]);
-  });
+  const bool from_export = TB_C4_PLAIN && line_stats && c4.split_paragraph && NLn > 0 && line_stats[0] == NLn;
+  if (from_export) {
+    // Lines that lost no citation are their trimmed original lines: their counts come from the
+    // stage's line export. Only the processed text of the lines that lost one (code[k] = 1 marks
+    // them here) is segmented, joined with '\n' so that no word spans two lines.
+    const LineStat* ls = (const LineStat*)(line_stats + 4);
+    x.par.for_n(C, [&](uint32_t j) { if (rm[j] && lid[j] != kNoLine) code[lid[j]] = 1; });
+    x.par.sync();
+    uint32_t* coff = x.template alloc_hot<uint32_t>(NLn + 1);
+    if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+    const uint32_t Ctot = x.par.template scan<uint32_t>(
+        NLn, 0u, [](uint32_t a, uint32_t b2) { return a + b2; },
+        [&](uint32_t k) { return code[k] ? plen[k] + 1 : 0u; }, [&](uint32_t k, uint32_t e) { coff[k] = e; });
+    x.par.for_n(NLn, [&](uint32_t k) {
+      if (!code[k]) { nw[k] = ls[k].nw; mx[k] = ls[k].mx; }
+    });
+    x.par.sync();
+    if (Ctot > 0) {
+      const auto mc = x.mark();
+      uint8_t* Pc = x.template alloc<uint8_t>(Ctot + 1);
+      if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+      x.par.for_n(Ptot, [&](uint32_t i) {
+        const uint32_t k = line_of_byte(i);
+        if (code[k] && i - poff[k] <= plen[k]) Pc[coff[k] + (i - poff[k])] = Pb[i];  // (its '\n' too)
+      });
+      x.par.sync();
+      Cps cc = decode(x, Pc, Ctot);
+      Words cw = words(x, cc);
+      if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+      x.par.for_n(cw.n, [&](uint32_t q) {
+        const uint32_t bs = cw.bs[q];
+        uint32_t lo = 0, hi = NLn;  // last line with coff <= bs: the cited line holding the word
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (coff[mid] <= bs) lo = mid; else hi = mid;
+        }
+        P::add32(&nw[lo], 1u);
+        P::max32(&mx[lo], cw.ce[q] - cw.cs[q]);
+      });
+      x.par.sync();
+      x.reset(mc);
+    }
+  } else {
+    Cps pc = decode(x, Pb, Ptot);
+    Words pwd = words(x, pc);
+    if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+    x.par.for_n(pwd.n, [&](uint32_t q) {
+      const uint32_t lo = line_of_byte(pwd.bs[q]);
+      P::add32(&nw[lo], 1u);
+      P::max32(&mx[lo], pwd.ce[q] - pwd.cs[q]);
+    });
+  }
   x.stamp(PH_C4_WORDS);
   // javascript / policy phrases: to_lowercase().contains() per line == a case-folded match
   // starting at some byte of the line; every byte position is tested in parallel.

@@ -465,33 +465,6 @@ struct NoResolve {
   TB_HD void operator()(uint32_t, uint32_t) const {}
 };
 
-// Probe-table access for canonicalize(): through the arena's generic pointer, or — on the device,
-// when the table sits in the LDS slice — through an LDS-qualified one, so its loads and atomics
-// compile to ds_* instructions instead of flat ones (a flat access waits on both the
-// vector-memory and the LDS counters, so every probe would also wait for outstanding HBM traffic).
-template <class P>
-struct TabG {
-  uint32_t* t;
-  TB_HD uint32_t ld(uint32_t i) const { return t[i]; }
-  TB_HD uint32_t cas(uint32_t i, uint32_t c, uint32_t v) const { return P::cas32(&t[i], c, v); }
-  TB_HD void min(uint32_t i, uint32_t v) const { P::min32(&t[i], v); }
-};
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(TB_NO_LDS_TABLES)
-#define TB_LDS_TABLES 1
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-struct TabL {
-  lds_u32* t;
-  __device__ uint32_t ld(uint32_t i) const { return t[i]; }
-  __device__ uint32_t cas(uint32_t i, uint32_t c, uint32_t v) const {
-    uint32_t e = c;
-    __atomic_compare_exchange_n(&t[i], &e, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
-    return e;
-  }
-  __device__ void min(uint32_t i, uint32_t v) const { __atomic_fetch_min(&t[i], v, __ATOMIC_RELAXED); }
-};
-#else
-#define TB_LDS_TABLES 0
-#endif
 
 template <class P, class KeyF, class EqF, class CT>
 TB_HD void canonicalize(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, CT* canon);
@@ -576,45 +549,32 @@ TB_HD void canonicalize_res(DocCtx<P>& x, uint32_t n, KeyF&& key, EqF&& eq, CT* 
     if (x.overflow) return;
     zero_table(x, tab, capn);
     x.par.sync();
-    auto passes = [&](auto T) {
-      x.par.for_n(n, [&](uint32_t i) {
-        const uint64_t k = x.weak_keys ? (key(i) & 3ull) : key(i);
-        const uint32_t fp = (uint32_t)(k >> 48);
-        const uint32_t mine = (fp << 16) | (i + 1);
-        uint32_t slot = (uint32_t)(((k & 0xFFFFFFFFull) * capn) >> 32);
-        while (true) {
-          uint32_t cur = T.ld(slot);
-          if (cur == 0) {
-            cur = T.cas(slot, 0u, mine);
-            if (cur == 0) break;
-          }
-          if ((cur >> 16) == fp && eq(i, (cur & 0xFFFFu) - 1u)) {
-            if ((cur & 0xFFFFu) > i + 1u) T.min(slot, mine);
-            break;
-          }
-          if (++slot == capn) slot = 0;
+    x.par.for_n(n, [&](uint32_t i) {
+      const uint64_t k = x.weak_keys ? (key(i) & 3ull) : key(i);
+      const uint32_t fp = (uint32_t)(k >> 48);
+      const uint32_t mine = (fp << 16) | (i + 1);
+      uint32_t slot = (uint32_t)(((k & 0xFFFFFFFFull) * capn) >> 32);
+      while (true) {
+        uint32_t cur = tab[slot];
+        if (cur == 0) {
+          cur = P::cas32(&tab[slot], 0u, mine);
+          if (cur == 0) break;
         }
-        canon[i] = slot;
-      });
-      x.par.sync();
-      x.par.for_n(n, [&](uint32_t i) {
-        const uint32_t c = (T.ld(canon[i]) & 0xFFFFu) - 1u;
-        canon[i] = c;
-        res(i, c);
-      });
-      x.par.sync();
-    };
-#if TB_LDS_TABLES
-    // (one-wave kernel only: the workgroup kernel's register budget does not take a second copy)
-    if constexpr (P::kWaves == 1) {
-      if (x.in_lds(tab)) passes(TabL{(lds_u32*)tab});
-      else passes(TabG<P>{tab});
-    } else {
-      passes(TabG<P>{tab});
-    }
-#else
-    passes(TabG<P>{tab});
-#endif
+        if ((cur >> 16) == fp && eq(i, (cur & 0xFFFFu) - 1u)) {
+          if ((cur & 0xFFFFu) > i + 1u) P::min32(&tab[slot], mine);
+          break;
+        }
+        if (++slot == capn) slot = 0;
+      }
+      canon[i] = slot;
+    });
+    x.par.sync();
+    x.par.for_n(n, [&](uint32_t i) {
+      const uint32_t c = (tab[canon[i]] & 0xFFFFu) - 1u;
+      canon[i] = c;
+      res(i, c);
+    });
+    x.par.sync();
     x.reset(mark);
     return;
   }

@@ -1621,16 +1621,12 @@ TB_HD uint64_t swar_lower8(uint64_t v) {
   return v | (upper >> 2);
 }
 
-// One pass over the bytes: lorem ipsum and curly brackets (lowercase().contains("lorem ipsum") ==
-// the pattern starts, case-folded, at some 'l'), a possible citation ('[' followed by a digit:
-// a non-ASCII byte after the '[' counts too, so the test is conservative) and the phrase bits.
-// Each item is one aligned dword of the text (4 start positions) with the next dword as look-ahead:
-// the 3-byte case-folded prefixes come from shifts of one lowercased 64-bit window, and only a
-// position whose prefix is one of the patterns' runs the exact comparison (ci_starts_with).
-template <class P>
-TB_HD uint32_t c4_byte_scan(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n) {
-  uint32_t acc = 0;
-  const bool phrases = c4.filter_javascript || c4.filter_policy;
+// Every byte position s of b[0, n) visited as f(s, c0, c1, l3): its byte, the next one (0 past the
+// end) and the three bytes from s ASCII-lowercased (l3, little endian). Items are four aligned
+// dwords whose five loads (one of look-ahead) are issued together, and the lowercase windows
+// come from SWAR shifts: one memory round trip per 16 bytes, no per-byte loads.
+template <class P, class F>
+TB_HD void scan_bytes16(DocCtx<P>& x, const uint8_t* b, uint32_t n, F&& f) {
   const uintptr_t a0 = (uintptr_t)b & ~(uintptr_t)3;
   const uint32_t head = (uint32_t)((uintptr_t)b - a0);
   const uint32_t nd = (head + n + 3) >> 2;
@@ -1638,7 +1634,7 @@ TB_HD uint32_t c4_byte_scan(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uin
   auto dw = [&](uint32_t k) -> uint32_t {  // dword k of the aligned stream, bytes past the text zero
     if (k >= nd) return 0u;
     const int64_t e = (int64_t)4 * k + 4 - head;  // doc position one past its last byte
-    if (e <= (int64_t)n) return w[k];
+    if (e <= (int64_t)n && 4 * k >= head) return w[k];
     uint32_t v = 0;
     for (uint32_t j = 0; j < 4; ++j) {
       const int64_t sj = (int64_t)4 * k + j - head;
@@ -1646,24 +1642,44 @@ TB_HD uint32_t c4_byte_scan(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uin
     }
     return v;
   };
-  constexpr uint32_t kLor = pack3("lor"), kJav = pack3("jav"), kTer = pack3("ter"), kPri = pack3("pri"),
-                     kCoo = pack3("coo"), kUse = pack3("use");
-  x.par.for_n(nd, [&](uint32_t k) {
-    const uint64_t v = (uint64_t)dw(k) | ((uint64_t)dw(k + 1) << 32);
-    const uint64_t lo = swar_lower8(v);
-    for (uint32_t r = 0; r < 4; ++r) {
-      const int64_t sp = (int64_t)4 * k + r - head;
-      if (sp < 0 || sp >= (int64_t)n) continue;
-      const uint32_t s = (uint32_t)sp;
-      const uint32_t c0 = (uint32_t)(v >> (8 * r)) & 0xFFu;
-      const uint32_t c1 = (uint32_t)(v >> (8 * r + 8)) & 0xFFu;  // 0 past the end
-      const uint32_t l3 = (uint32_t)(lo >> (8 * r)) & 0xFFFFFFu;
-      if (c4.filter_curly_bracket && (c0 == '{' || c0 == '}')) acc |= C4S_CURLY;
-      if (c0 == '[' && ((c1 >= '0' && c1 <= '9') || c1 >= 0x80)) acc |= C4S_CITE;
-      if (c4.filter_lorem_ipsum && l3 == kLor && ci_starts_with(b + s, n - s, "lorem ipsum", 11)) acc |= C4S_LOREM;
-      if (phrases && (l3 == kJav || l3 == kTer || l3 == kPri || l3 == kCoo || l3 == kUse))
-        acc |= c4_phrases_at(c4, b, n, s);
+  x.par.for_n((nd + 3) >> 2, [&](uint32_t g) {
+    uint32_t d[5];
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i) d[i] = dw(4 * g + i);
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint32_t k = 4 * g + i;
+      const uint64_t v = (uint64_t)d[i] | ((uint64_t)d[i + 1] << 32);
+      const uint64_t lo = swar_lower8(v);
+      for (uint32_t r = 0; r < 4; ++r) {
+        const int64_t sp = (int64_t)4 * k + r - head;
+        if (sp < 0 || sp >= (int64_t)n) continue;
+        f((uint32_t)sp, (uint32_t)(v >> (8 * r)) & 0xFFu, (uint32_t)(v >> (8 * r + 8)) & 0xFFu,
+          (uint32_t)(lo >> (8 * r)) & 0xFFFFFFu);
+      }
     }
+  });
+}
+
+// Could a javascript / policy phrase start here (its case-folded 3-byte prefix)?
+TB_HD bool c4_phrase_prefix(uint32_t l3) {
+  return l3 == pack3("jav") || l3 == pack3("ter") || l3 == pack3("pri") || l3 == pack3("coo") || l3 == pack3("use");
+}
+
+// One pass over the bytes: lorem ipsum and curly brackets (lowercase().contains("lorem ipsum") ==
+// the pattern starts, case-folded, at some 'l'), a possible citation ('[' followed by a digit:
+// a non-ASCII byte after the '[' counts too, so the test is conservative) and the phrase bits;
+// only a position whose 3-byte prefix matches runs the exact comparison (ci_starts_with).
+template <class P>
+TB_HD uint32_t c4_byte_scan(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n) {
+  uint32_t acc = 0;
+  const bool phrases = c4.filter_javascript || c4.filter_policy;
+  scan_bytes16(x, b, n, [&](uint32_t s, uint32_t c0, uint32_t c1, uint32_t l3) {
+    if (c4.filter_curly_bracket && (c0 == '{' || c0 == '}')) acc |= C4S_CURLY;
+    if (c0 == '[' && ((c1 >= '0' && c1 <= '9') || c1 >= 0x80)) acc |= C4S_CITE;
+    if (c4.filter_lorem_ipsum && l3 == pack3("lor") && ci_starts_with(b + s, n - s, "lorem ipsum", 11))
+      acc |= C4S_LOREM;
+    if (phrases && c4_phrase_prefix(l3)) acc |= c4_phrases_at(c4, b, n, s);
   });
   return x.par.reduce_or(acc);
 }
@@ -1740,7 +1756,8 @@ TB_HD void c4_plain_tail(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32
     // only when the byte scan saw a phrase somewhere (rare). A phrase (letters and spaces, starting
     // with a letter) that matches at a byte lies inside one line's trimmed span: it cannot cross
     // the line feed or run into trailing whitespace.
-    x.par.for_n(n, [&](uint32_t s) {
+    scan_bytes16(x, b, n, [&](uint32_t s, uint32_t, uint32_t, uint32_t l3) {
+      if (!c4_phrase_prefix(l3)) return;
       const uint32_t bits = c4_phrases_at(c4, b, n, s);
       if (bits) P::or32(&pf[line_of_byte(s)], bits);
     });
@@ -2092,7 +2109,8 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   if (c4.filter_javascript || c4.filter_policy) {
     // The phrases hold letters and spaces only, so a match never runs over the '\n' that ends
     // its line: match against the rest of Pb first, look the line up only on a match.
-    x.par.for_n(Ptot, [&](uint32_t s) {
+    scan_bytes16(x, Pb, Ptot, [&](uint32_t s, uint32_t, uint32_t, uint32_t l3) {
+      if (!c4_phrase_prefix(l3)) return;
       const uint32_t bits = c4_phrases_at(c4, Pb, Ptot, s);
       if (bits) P::or32(&pf[line_of_byte(s)], bits);
     });

@@ -2036,13 +2036,20 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   x.par.single([&]() { poff[NLn] = Ptot; });
   x.stamp(PH_C4_CITE);
   // ---- words of the processed lines ----
-  uint32_t* nw = x.template alloc_hot<uint32_t>(NLn + 1);
-  uint32_t* mx = x.template alloc_hot<uint32_t>(NLn + 1);
-  uint32_t* pf = x.template alloc_hot<uint32_t>(NLn + 1);  // pattern flags per line
-  uint8_t* code = x.template alloc_hot<uint8_t>(NLn + 1);
-  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
-  x.par.for_n(NLn, [&](uint32_t k) { nw[k] = 0; mx[k] = 0; pf[k] = 0; code[k] = 0; });
-  x.par.sync();
+  uint32_t* nw = nullptr;
+  uint32_t* mx = nullptr;
+  uint32_t* pf = nullptr;  // pattern flags per line
+  uint8_t* code = nullptr;
+  auto line_arrays = [&]() {
+    nw = x.template alloc_hot<uint32_t>(NLn + 1);
+    mx = x.template alloc_hot<uint32_t>(NLn + 1);
+    pf = x.template alloc_hot<uint32_t>(NLn + 1);
+    code = x.template alloc_hot<uint8_t>(NLn + 1);
+    if (x.overflow) return false;
+    x.par.for_n(NLn, [&](uint32_t k) { nw[k] = 0; mx[k] = 0; pf[k] = 0; code[k] = 0; });
+    x.par.sync();
+    return true;
+  };
   auto line_of_byte = [&](uint32_t bs) {  // last line with poff <= bs
     uint32_t lo = 0, hi = NLn;
     while (hi - lo > 1) {
@@ -2051,8 +2058,12 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
     }
     return lo;
   };
-  const bool from_export = TB_C4_PLAIN && line_stats && c4.split_paragraph && NLn > 0 && line_stats[0] == NLn;
+  // (one-wave documents only: in the workgroup kernel the per-byte line lookups of the cited-line
+  // copy cost more than segmenting the whole processed text, measured)
+  const bool from_export = P::kWaves == 1 && TB_C4_PLAIN && line_stats && c4.split_paragraph && NLn > 0 &&
+                           line_stats[0] == NLn;
   if (from_export) {
+    if (!line_arrays()) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
     // Lines that lost no citation are their trimmed original lines: their counts come from the
     // stage's line export. Only the processed text of the lines that lost one (code[k] = 1 marks
     // them here) is segmented, joined with '\n' so that no word spans two lines.
@@ -2096,7 +2107,7 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   } else {
     Cps pc = decode(x, Pb, Ptot);
     Words pwd = words(x, pc);
-    if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+    if (!line_arrays() || x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
     x.par.for_n(pwd.n, [&](uint32_t q) {
       const uint32_t lo = line_of_byte(pwd.bs[q]);
       P::add32(&nw[lo], 1u);

@@ -348,8 +348,26 @@ TB_HD WSeg wseg_op(const WSeg& a, const WSeg& b) {
   return WSeg{a.bits | (b.bits & 6u), a.first < b.first ? a.first : b.first, a.last > b.last ? a.last : b.last};
 }
 
+// Word-boundary mark before code point i of [0, C) (sot and eot included). The rules are first
+// decided from the properties of i-2 .. i+1 (wb_break_ctx: straight-line compares, no look-around
+// loops); only windows holding Extend / Format / ZWJ / RI take the general rule walk, so a chunk
+// with punctuation or digits does not serialise the wave on it.
+#ifndef TB_WB_CTX
+#define TB_WB_CTX 1
+#endif
+TB_HD bool word_mark(const PropArr& prop, uint32_t C, uint32_t i) {
+  if (i == 0 || i == C) return true;
+  if (TB_WB_CTX) {
+    const uint32_t pm2 = i >= 2 ? prop[i - 2] : 0xFFFFFFFFu;
+    const uint32_t pp1 = i + 1 < C ? prop[i + 1] : 0xFFFFFFFFu;
+    const int r = wb_break_ctx(pm2, prop[i - 1], prop[i], pp1);
+    if (r != 2) return r != 0;
+  }
+  return wb_break(CpsAcc{prop}, (int)C, (int)i);
+}
+
 template <class P>
-TB_HD Words words(DocCtx<P>& x, const Cps& c) {
+TB_HD Words words(DocCtx<P>& x, const Cps& c, const uint32_t* wbm_pre = nullptr) {
   Words w;
   const uint32_t C = c.n;
   w.cs = x.template alloc<uint32_t>(C + 1);
@@ -360,29 +378,16 @@ TB_HD Words words(DocCtx<P>& x, const Cps& c) {
   const auto mark = x.mark();
   // word-break positions as a bitmask (C/8 bytes, LDS): one rule evaluation per position, no
   // per-code-point arrays; the segment scan and the word compaction run in one fused pass
-  uint32_t* wbm = x.template alloc_hot_hi<uint32_t>(mask_words(C + 1));
+  uint32_t* wbm = wbm_pre ? nullptr : x.template alloc_hot_hi<uint32_t>(mask_words(C + 1));
   if (x.overflow) return w;
   const PropArr prop = c.props();
   const OffArr off = c.offs();
-  CpsAcc acc{prop};
-  // The rules are first decided from the properties of i-2 .. i+1 (wb_break_ctx: straight-line
-  // compares, no look-around loops); only windows holding Extend / Format / ZWJ / RI take the
-  // general rule walk, so a chunk with punctuation or digits does not serialise the wave on it.
-#ifndef TB_WB_CTX
-#define TB_WB_CTX 1
-#endif
-  x.par.mask_bits(C + 1, [&](uint32_t i) {
-    if (i == 0 || i == C) return true;
-    if (TB_WB_CTX) {
-      const uint32_t pm2 = i >= 2 ? prop[i - 2] : 0xFFFFFFFFu;
-      const uint32_t pp1 = i + 1 < C ? prop[i + 1] : 0xFFFFFFFFu;
-      const int r = wb_break_ctx(pm2, prop[i - 1], prop[i], pp1);
-      if (r != 2) return r != 0;
-    }
-    return wb_break(acc, (int)C, (int)i);
-  }, wbm);
-  x.par.sync();
-  auto bit = [&](uint32_t i) { return (wbm[i >> 5] >> (i & 31)) & 1u; };
+  if (!wbm_pre) {
+    x.par.mask_bits(C + 1, [&](uint32_t i) { return word_mark(prop, C, i); }, wbm);
+    x.par.sync();
+  }
+  const uint32_t* wb = wbm_pre ? wbm_pre : wbm;
+  auto bit = [&](uint32_t i) { return (wb[i >> 5] >> (i & 31)) & 1u; };
   uint32_t *cs = w.cs, *ce = w.ce, *bs = w.bs, *be = w.be;
   uint8_t* al = w.alpha;
   w.n = x.par.template scan_compact<WSeg>(
@@ -812,6 +817,20 @@ TB_HD void gr_para_span(const uint32_t* rs, const uint32_t* rl, const uint32_t* 
   e0 = off[ce];
 }
 
+// a very long document's code points and UAX#29 word-break marks, computed before
+// its stage workgroup runs by many workgroups at once (kernels.hip k_pre_count / k_pre_decode /
+// k_pre_wb): the non-packed Cps layout (documents of 64 KiB and more) plus the marks words()
+// would compute.
+struct PreDoc {
+  uint32_t* off;   // [n + 1] byte offset of every code point (off[C] = n)
+  uint16_t* prop;  // [n + 1] compact properties
+  uint32_t* wbm;   // [mask_words(n + 1)] bit i: word boundary before code point i
+  uint32_t n;      // bytes
+  uint32_t C;      // code points
+  uint32_t dict;   // a dictionary-script code point occurs (the document goes to the CPU path)
+  uint32_t pad;
+};
+
 struct StageOut {
   int64_t* rec;     // record buffer (all steps of the stage)
   uint32_t ndocs;
@@ -820,6 +839,7 @@ struct StageOut {
   // non-null: this document's C4 line export (LineStat region, see export_line_stats), for the C4
   // pass of the same content version
   uint32_t* line_stats = nullptr;
+  const PreDoc* pre = nullptr;  // non-null: decode and word-break marks were precomputed
 };
 
 // The C4 line export of one document: a header (line count, or kLineStatsNone while / when the
@@ -2204,7 +2224,17 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
   x.stamp(PH_START);
   if (out.line_stats) x.par.single([&]() { out.line_stats[0] = kLineStatsNone; });
   uint32_t ndict = 0;
-  Cps c = decode(x, b, n, kHotProps, &ndict);
+  Cps c;
+  if (out.pre) {
+    c.n = out.pre->C;
+    c.off = out.pre->off;
+    c.prop = out.pre->prop;
+    c.b = b;
+    c.nb = n;
+    ndict = out.pre->dict;
+  } else {
+    c = decode(x, b, n, kHotProps, &ndict);
+  }
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   x.stamp(PH_DECODE);
   const uint32_t C = c.n;
@@ -2219,7 +2249,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
   if (need_ph) ph = prefix_hash8(x, b, n);
   x.stamp(PH_PREFIX_HASH);
   Words w;
-  if (need_words) w = words(x, c);
+  if (need_words) w = words(x, c, out.pre ? out.pre->wbm : nullptr);
   x.stamp(PH_WORDS);
   Lines L;
   if (need_lines) L = rust_lines(x, c);

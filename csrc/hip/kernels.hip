@@ -149,7 +149,8 @@ __device__ __forceinline__ void stage_blk_body(
     const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,
     const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
     int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead,
-    GrExport* gr_export, int32_t n_split, uint32_t split_bytes, uint32_t* line_stats) {
+    GrExport* gr_export, int32_t n_split, uint32_t split_bytes, uint32_t* line_stats, const PreDoc* pre,
+    int32_t n_pre) {
   const int doc = perm[blockIdx.x];
   if (doc >= ndocs || (dead && dead[doc])) return;
   DocCtx<BlockPar<NT>> x =
@@ -160,6 +161,7 @@ __device__ __forceinline__ void stage_blk_body(
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc};
   if (line_stats) out.line_stats = line_stats + line_stats_base(off[doc], doc);
+  if (pre && (int)blockIdx.x < n_pre) out.pre = pre + blockIdx.x;
   // split documents (the first n_split launch positions, longer than split_bytes) export their
   // word arrays; k_gr_dup_split finishes their duplicated n-gram orders
   if (gr_export && (int)blockIdx.x < n_split && n > split_bytes) out.gr_export = gr_export + blockIdx.x;
@@ -172,9 +174,10 @@ __device__ __forceinline__ void stage_blk_body(
       const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,         \
       const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,  \
       int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead,   \
-      GrExport* gr_export, int32_t n_split, uint32_t split_bytes, uint32_t* line_stats) {              \
+      GrExport* gr_export, int32_t n_split, uint32_t split_bytes, uint32_t* line_stats,                \
+      const PreDoc* pre, int32_t n_pre) {                                                              \
     stage_blk_body<NT>(plan, stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, tabs, rec, flags, \
-                       lds_bytes, prof, dead, gr_export, n_split, split_bytes, line_stats);              \
+                       lds_bytes, prof, dead, gr_export, n_split, split_bytes, line_stats, pre, n_pre);  \
   }
 TB_STAGE_BLK_KERNEL(k_stage_analyze_blk, kBlockThreads)
 TB_STAGE_BLK_KERNEL(k_stage_analyze_blk1k, kBlockThreadsMax)
@@ -833,6 +836,107 @@ __global__ void k_pow_table(uint64_t* pw, uint32_t n) {
   }
 }
 
+// the code points and UAX#29 word-break marks of very long documents, spread over
+// many workgroups before their stage workgroups run (StageOut::pre). Launch grids are
+// (tile or chunk, document): k_pre_count counts the lead bytes of every 16 KB tile, k_pre_decode
+// writes each tile's code points at the offset its earlier tiles give (the non-packed Cps layout
+// decode() produces for documents of 64 KiB and more), k_pre_wb evaluates word_mark() for 64 code
+// points per wave (the rules look across tile borders freely: the whole property array exists).
+constexpr uint32_t kPreTile = 16384;
+constexpr uint32_t kPreThreads = 256;  // 64 bytes per thread
+
+__global__ __launch_bounds__(kPreThreads) void k_pre_count(const uint8_t* __restrict__ bytes,
+                                                           const int64_t* __restrict__ off,
+                                                           const int32_t* __restrict__ perm,
+                                                           const uint8_t* __restrict__ dead,
+                                                           const PreDoc* __restrict__ pre, uint32_t tiles_max,
+                                                           int64_t* __restrict__ cnt) {
+  __shared__ uint32_t red[kPreThreads / 64];
+  const uint32_t j = blockIdx.x, s = blockIdx.y;
+  const int doc = perm[s];
+  const uint32_t n = pre[s].n;
+  const uint32_t b0 = j * kPreTile;
+  if (b0 >= n || (dead && dead[doc])) return;
+  const uint8_t* b = bytes + off[doc];
+  const uint32_t e = b0 + kPreTile < n ? b0 + kPreTile : n;
+  uint32_t c = 0;
+  for (uint32_t i = b0 + threadIdx.x; i < e; i += kPreThreads) c += utf8_is_lead(b[i]) ? 1u : 0u;
+  for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < kPreThreads / 64; ++w) t += red[w];
+    cnt[(size_t)s * tiles_max + j] = t;
+  }
+}
+
+__global__ __launch_bounds__(kPreThreads) void k_pre_decode(const uint8_t* __restrict__ bytes,
+                                                            const int64_t* __restrict__ off,
+                                                            const int32_t* __restrict__ perm,
+                                                            const uint8_t* __restrict__ dead, PreDoc* pre,
+                                                            uint32_t tiles_max, const int64_t* __restrict__ cnt,
+                                                            DevTables tabs) {
+  __shared__ uint32_t xs[kPreThreads + 1];
+  const uint32_t j = blockIdx.x, s = blockIdx.y;
+  const int doc = perm[s];
+  const PreDoc d = pre[s];
+  const uint32_t n = d.n;
+  const uint32_t b0 = j * kPreTile;
+  if (b0 >= n || (dead && dead[doc])) return;
+  const uint8_t* b = bytes + off[doc];
+  const UcdView ucd{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
+  // this thread's 64 bytes: lead count, then the block's exclusive scan of the counts
+  const uint32_t t0 = b0 + 64 * threadIdx.x;
+  const uint32_t t1 = t0 + 64 < n ? t0 + 64 : n;
+  uint32_t c = 0;
+  for (uint32_t i = t0; i < t1; ++i) c += utf8_is_lead(b[i]) ? 1u : 0u;
+  xs[threadIdx.x] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t base = 0;
+    for (uint32_t q = 0; q < j; ++q) base += (uint32_t)cnt[(size_t)s * tiles_max + q];
+    uint32_t run = base;
+    for (uint32_t q = 0; q < kPreThreads; ++q) {
+      const uint32_t v = xs[q];
+      xs[q] = run;
+      run += v;
+    }
+    xs[kPreThreads] = run;  // code points before the next tile
+  }
+  __syncthreads();
+  uint32_t k = xs[threadIdx.x];
+  bool dict = false;
+  for (uint32_t i = t0; i < t1; ++i) {
+    if (!utf8_is_lead(b[i])) continue;
+    int len;
+    const uint32_t p = ucd.props(utf8_decode(b, i, n, &len));
+    d.off[k] = i;
+    d.prop[k] = compact_prop(p);
+    dict |= (p & P_DICT) != 0;
+    ++k;
+  }
+  if (dict) atomicOr(&pre[s].dict, 1u);
+  if (threadIdx.x == 0 && b0 + kPreTile >= n) {  // the last tile closes the arrays
+    const uint32_t C = xs[kPreThreads];
+    d.off[C] = n;
+    d.prop[C] = 0;
+    pre[s].C = C;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_pre_wb(const int32_t* __restrict__ perm, const uint8_t* __restrict__ dead,
+                                               const PreDoc* __restrict__ pre) {
+  const uint32_t j = blockIdx.x, s = blockIdx.y;
+  const PreDoc d = pre[s];
+  const uint32_t C = d.C;
+  if (64 * j > C || (dead && dead[perm[s]])) return;
+  const uint32_t i = 64 * j + threadIdx.x;
+  const bool m = i <= C && word_mark(PropArr{nullptr, d.prop}, C, i);
+  const uint64_t bits = __ballot(m);
+  if (threadIdx.x < 2) d.wbm[2 * j + threadIdx.x] = threadIdx.x ? (uint32_t)(bits >> 32) : (uint32_t)bits;
+}
+
 }  // namespace
 
 extern "C" {
@@ -866,7 +970,8 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
                          const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                          const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
                          uint32_t lds_bytes, uint64_t* prof, const uint8_t* dead, void* gr_export, int32_t n_split,
-                         uint32_t split_bytes, int32_t threads, uint32_t* line_stats) {
+                         uint32_t split_bytes, int32_t threads, uint32_t* line_stats, const void* pre,
+                         int32_t n_pre) {
   if (nblocks <= 0) return 0;
   if (!perm || lds_bytes > kMaxLdsPerBlk || n_split < 0 || n_split > nblocks) return (int)hipErrorInvalidValue;
   if (threads != kBlockThreads && threads != kBlockThreadsMax) return (int)hipErrorInvalidValue;
@@ -877,7 +982,7 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
   hipLaunchKernelGGL(kern, dim3(nblocks), dim3(threads), lds_bytes, stream,
                      (const DevPlan*)plan, (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw,
                      pw_n, t, rec, flags, lds_bytes, prof, dead, (GrExport*)gr_export, n_split,
-                     split_bytes, line_stats);
+                     split_bytes, line_stats, (const PreDoc*)pre, n_pre);
   return (int)hipGetLastError();
 }
 
@@ -902,6 +1007,27 @@ int tb_gr_dup_split(hipStream_t stream, const void* stage, int32_t gr_step, cons
 }
 
 size_t tb_sizeof_gr_export() { return sizeof(GrExport); }
+size_t tb_sizeof_pre_doc() { return sizeof(PreDoc); }
+
+// Decode + word-break marks of the first npre launch positions of the long-document launch
+// (`pre`: npre descriptors with n / off / prop / wbm set, C and dict zeroed; cnt: int64
+// [npre * tiles_max], tiles_max >= ceil(max n / 16 KB)).
+int tb_pre_decode(hipStream_t stream, const uint8_t* bytes, const int64_t* off, const int32_t* perm, int32_t npre,
+                  const uint8_t* dead, void* pre, uint32_t tiles_max, int64_t* cnt, const uint16_t* s1,
+                  const uint32_t* s2, const uint16_t* l1, const int32_t* l2) {
+  if (npre <= 0) return 0;
+  if (!perm || !pre || !cnt || tiles_max == 0 || npre > 65535) return (int)hipErrorInvalidValue;
+  DevTables t{s1, s2, l1, l2};
+  const dim3 g(tiles_max, (uint32_t)npre);
+  hipLaunchKernelGGL(k_pre_count, g, dim3(kPreThreads), 0, stream, bytes, off, perm, dead, (const PreDoc*)pre,
+                     tiles_max, cnt);
+  hipLaunchKernelGGL(k_pre_decode, g, dim3(kPreThreads), 0, stream, bytes, off, perm, dead, (PreDoc*)pre, tiles_max,
+                     (const int64_t*)cnt, t);
+  // chunks of 64 code points: C + 1 <= n + 1 positions
+  const uint32_t chunks = tiles_max * (kPreTile / 64) + 1;
+  hipLaunchKernelGGL(k_pre_wb, dim3(chunks, (uint32_t)npre), dim3(64), 0, stream, perm, dead, (const PreDoc*)pre);
+  return (int)hipGetLastError();
+}
 
 int tb_c4_pass_a_blk(hipStream_t stream, const void* c4, const uint8_t* bytes, const int64_t* off,
                      const int32_t* perm, int32_t nblocks, int32_t ndocs, char* scratch, const int64_t* scratch_off,
@@ -1045,7 +1171,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 
 int tb_phase_slots() { return kPhaseSlots; }
 
-int tb_abi_version() { return 14; }
+int tb_abi_version() { return 15; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

@@ -269,3 +269,53 @@ def test_split_documents_match_host_emulation(host, corpus, runner_parts, monkey
             b = ref[prefix * n:(prefix + width) * n].reshape(n, width)
             bad = np.nonzero(~np.all(a[ok] == b[ok], axis=1))[0]
             assert len(bad) == 0, (bad[:5], a[ok][bad[:3]], b[ok][bad[:3]])
+
+
+def test_pre_decoded_long_documents_match_host(host, runner_parts, monkeypatch):
+    """SURVEY 5.7 pre-pass (k_pre_count / k_pre_decode / k_pre_wb): documents of 64 KB and more get
+    their code points and word-break marks from many workgroups before their stage workgroup runs.
+    Stage records and flags equal the host emulation and a device run without the pre-pass;
+    Unicode-heavy text (marks, ZWJ / emoji, regional indicators across 16 KB tile borders) and a
+    dictionary-script document (flagged for the CPU path) included."""
+    from gpu_fuzz_corpus import fuzz_docs
+
+    from textblaster_amd.pipeline.device import DeviceRunner
+
+    cfg, steps, plan, _, lid = runner_parts
+    rng = np.random.default_rng(3)
+    langs = ["eng", "dan", "swe", "nob", "nno"]
+    texts = [synth.make_doc(rng, langs[k % 5], int(s)) for k, s in enumerate(np.geomspace(66000, 400000, 8))]
+    uni = "\n".join(fuzz_docs(3000, seed=9))
+    texts += [uni[:150000], uni[150000:230000]]
+    texts += [synth.make_doc(rng, "eng", 70000) + " 日本語のテキストです。 " + synth.make_doc(rng, "dan", 5000)]
+    texts += synth.make_corpus(200, 900, seed=4)  # short documents in the same batch
+    data, off = synth.pack(texts)
+    n = len(texts)
+    lens = np.diff(off)
+    res = {}
+    for pre in ("65536", "0"):
+        monkeypatch.setenv("TB_PRE_DOC_BYTES", pre)
+        runner = DeviceRunner(steps, plan, "cuda:0", lid)
+        assert runner.pre_doc_bytes == (65536 if pre != "0" else 0)
+        res[pre] = runner.run(data, off)
+    a, b = res["65536"], res["0"]
+    np.testing.assert_array_equal(a.flags, b.flags)
+    assert a.flags[10] != 0  # the dictionary-script document
+    for s, idx in enumerate(plan.stages):
+        ver = plan.stage_version[s]
+        vd, vo = (data, off) if ver == 0 else a.versions[ver]
+        np.testing.assert_array_equal(a.stage_recs[s], b.stage_recs[s])
+        ref, rflags = host.emulate_stage(steps, idx, np.ascontiguousarray(vd), np.ascontiguousarray(vo), 8,
+                                         lid.native())
+        for (kind, width, prefix), step_i in zip(runner.stage_layout[s][1], idx):
+            if kind == 4:
+                continue
+            ok = (a.flags == 0) & (rflags == 0)
+            if a.dead is not None:
+                ok &= ~((a.dead != 0) & (a.dead <= runner.pass_of_step[step_i]))
+            if ver == 0:
+                assert np.count_nonzero(ok & (lens >= 65536)) >= 5
+            x = a.stage_recs[s][prefix * n:(prefix + width) * n].reshape(n, width)
+            y = ref[prefix * n:(prefix + width) * n].reshape(n, width)
+            bad = np.nonzero(~np.all(x[ok] == y[ok], axis=1))[0]
+            assert len(bad) == 0, (steps[step_i].name, bad[:5])

@@ -22,14 +22,16 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32, _P,
                          _P],
     "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _P, _P],
     "tb_stage_analyze_blk": [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P,
-                             _U32, _P, _P, _P, _I32, _U32, _I32, _P],
+                             _U32, _P, _P, _P, _I32, _U32, _I32, _P, _P, _I32],
+    "tb_sizeof_pre_doc": [],
+    "tb_pre_decode": [_P, _P, _P, _P, _I32, _P, _P, _U32, _P, _P, _P, _P, _P],
     "tb_gr_dup_split": [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32],
     "tb_sizeof_gr_export": [],
     "tb_c4_pass_a_blk": [_P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _P,
@@ -71,6 +73,12 @@ _SIGS = {
     "tb_sizeof_stage": [],
     "tb_sizeof_c4": [],
 }
+
+
+# docproc.h PreDoc (checked against tb_sizeof_pre_doc)
+PRE_DOC = np.dtype([("off", "<u8"), ("prop", "<u8"), ("wbm", "<u8"), ("n", "<u4"), ("C", "<u4"), ("dict", "<u4"),
+                    ("pad", "<u4")])
+PRE_TILE = 16384  # kernels.hip kPreTile
 
 
 class DevBpe(ctypes.Structure):
@@ -133,6 +141,8 @@ class Kernels:
                 or self.lib.tb_sizeof_resolve() != h.SIZEOF_DEV_RESOLVE):
             raise DeviceError("libtbhip.so and _tbhost disagree on the device plan layout; rebuild")
         self.sizeof_gr_export = int(self.lib.tb_sizeof_gr_export())
+        if int(self.lib.tb_sizeof_pre_doc()) != PRE_DOC.itemsize:
+            raise DeviceError("libtbhip.so and ops/kernels.py disagree on PreDoc; rebuild")
         s1, s2, l1, l2 = h.ucd_tables()
         self.tabs = [hiprt.to_device(a) for a in (s1, s2, l1, l2)]
         self._pw = None
@@ -173,7 +183,7 @@ class Kernels:
 
     def stage_analyze_blk(self, plan, stage, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n,
                           rec, flags, lds_bytes=0, prof=None, dead=None, gr_export=None, n_split=0, split_bytes=0,
-                          threads=512, line_stats=None):
+                          threads=512, line_stats=None, pre=None, n_pre=0):
         """k_stage_analyze_blk; ``gr_export`` (zeroed, >= n_split descriptors): the first n_split
         launch positions longer than ``split_bytes`` export their word arrays (split mode)."""
         t = self.tabs
@@ -186,8 +196,20 @@ class Kernels:
             nlong, ndocs, scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(),
             t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof),
             _ptr(dead), _ptr(gr_export), n_split if gr_export is not None else 0, split_bytes, int(threads),
-            _ptr(line_stats))
+            _ptr(line_stats), _ptr(pre), int(n_pre) if pre is not None else 0)
         _check(rc, "tb_stage_analyze_blk")
+
+    def pre_decode(self, bytes_, off, perm_pre, npre, dead, pre, tiles_max, cnt):
+        """k_pre_count / k_pre_decode / k_pre_wb: code points and word-break marks of
+        the first ``npre`` long documents over many workgroups; ``pre``: PRE_DOC descriptors
+        (device), ``cnt``: int64 [npre * tiles_max]."""
+        if perm_pre.numel() < npre or cnt.numel() < npre * tiles_max or pre.nbytes < npre * PRE_DOC.itemsize:
+            raise DeviceError("pre_decode: operand shapes")
+        t = self.tabs
+        rc = self.lib.tb_pre_decode(self.stream(), bytes_.data_ptr(), off.data_ptr(), perm_pre.data_ptr(), npre,
+                                    _ptr(dead), pre.data_ptr(), int(tiles_max), cnt.data_ptr(), t[0].data_ptr(),
+                                    t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr())
+        _check(rc, "tb_pre_decode")
 
     def gr_dup_split(self, stage, gr_step, perm, n_split, n_tasks, ndocs, gr_export, pw, pw_n, rec, flags, lds_bytes):
         """k_gr_dup_split: one workgroup per (split document, n-gram order); n_tasks = the

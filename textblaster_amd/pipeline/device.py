@@ -16,6 +16,7 @@ import numpy as np
 
 from .. import native
 from ..errors import DeviceError
+from ..ops.kernels import PRE_DOC, PRE_TILE
 from ..utils import metrics, tracing
 from .plan import ExecPlan
 
@@ -399,6 +400,10 @@ class DeviceRunner:
     # 80-VGPR budget the wider variant spills (872 B/lane) and is slower than 512 threads on ~1 MB
     # documents (profiles/r3_long: 685 vs 728 docs/s at 128 docs/step, 1081 vs 1444 at 384)
     DEFAULT_HUGE_DOC_BYTES = 0
+    # documents of at least this size get their code points and word-break marks from
+    # the multi-workgroup pre-pass (k_pre_*) before their stage workgroup runs; 0 disables. Never
+    # below 64 KiB (smaller documents use the packed code point layout).
+    DEFAULT_PRE_DOC_BYTES = 65536
     DEFAULT_STAGE_WAVES = 4  # the stage kernel's register budget (the one variant built, kernels.hip)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None, max_batch_bytes: int = 384 << 20,
@@ -566,6 +571,9 @@ class DeviceRunner:
         self.huge_doc_bytes = int(os.environ.get("TB_HUGE_DOC_BYTES", str(self.DEFAULT_HUGE_DOC_BYTES)))
         if self.split_doc_bytes > 0:
             self.split_doc_bytes = max(self.split_doc_bytes, self.long_doc_bytes)
+        self.pre_doc_bytes = int(os.environ.get("TB_PRE_DOC_BYTES", str(self.DEFAULT_PRE_DOC_BYTES)))
+        if self.pre_doc_bytes > 0:
+            self.pre_doc_bytes = max(self.pre_doc_bytes, 65536, self.long_doc_bytes)
         # per stage: (position of its GopherRepetition step, number of split tasks = its duplicated
         # + top n-gram orders + duplicated lines + duplicated paragraphs)
         self.gr_split = {}
@@ -672,6 +680,42 @@ class DeviceRunner:
         for a, o in zip(arrays, offs):
             out.append(dev[o:o + a.nbytes].view(a.dtype) if a.nbytes else dev[o:o].view(a.dtype))
         return out, dev
+
+    def _pre_decode(self, vb, vo, d_perm, long_lens: np.ndarray, dead, keep):
+        """SURVEY 5.7 pre-pass for the longest documents (launch positions [0, n_pre), sorted by
+        length): device arrays for their code points and word-break marks, filled by k_pre_* on
+        the current stream. Returns (PreDoc descriptors as a uint8 device array, n_pre)."""
+        if self.pre_doc_bytes <= 0 or not len(long_lens):
+            return None, 0
+        big = np.nonzero(long_lens >= self.pre_doc_bytes)[0]
+        if not len(big):
+            return None, 0
+        n_pre = int(big[-1]) + 1
+        lens = long_lens[:n_pre].astype(np.int64)
+        if bool((lens < self.pre_doc_bytes).any()) or n_pre > 65535:
+            return None, 0  # the launch order is not the length order: no prefix to hand over
+        al = lambda v: (v + 255) & ~255  # noqa: E731
+        sz_off, sz_prop = al(4 * (lens + 1)), al(2 * (lens + 1))
+        sz_wbm = al(4 * 2 * ((lens + 1 + 63) // 64))
+        per = sz_off + sz_prop + sz_wbm
+        base = np.zeros(n_pre + 1, np.int64)
+        np.cumsum(per, out=base[1:])
+        rt = self.rt
+        buf = rt.empty(int(base[-1]), np.uint8)
+        p0 = buf.data_ptr()
+        h = np.zeros(n_pre, dtype=PRE_DOC)
+        h["off"] = p0 + base[:-1]
+        h["prop"] = p0 + base[:-1] + sz_off
+        h["wbm"] = p0 + base[:-1] + sz_off + sz_prop
+        h["n"] = lens
+        d_pre = rt.empty(n_pre * PRE_DOC.itemsize, np.uint8)
+        hp = h.view(np.uint8)
+        d_pre.copy_from_host(hp, rt.current_stream())
+        tiles_max = int((int(lens.max()) + PRE_TILE - 1) // PRE_TILE)
+        cnt = rt.empty(n_pre * tiles_max, np.int64)
+        self.k.pre_decode(vb, vo, d_perm[:n_pre], n_pre, dead, d_pre, tiles_max, cnt)
+        keep += [buf, d_pre, cnt, hp]
+        return d_pre, n_pre
 
     def _langid(self, vb, vo, d_perm, ndocs, scratch, d_soff, rec, width, flags, prof):
         """Language-id records of a content version: k_langid_mfma (v3: embedding bag + bf16 MFMA
@@ -868,15 +912,19 @@ class DeviceRunner:
                               if self.huge_doc_bytes > 0 else 0)
                     esz = self.k.sizeof_gr_export
                     with rt.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_blk"):
+                        pre, n_pre = self._pre_decode(vb, vo, d_perm, lens[perm[:n_long]], skip, keep)
+                        psz = PRE_DOC.itemsize
                         for a0, a1, thr in ((0, n_huge, 1024), (n_huge, n_long, 512)):
                             if a1 <= a0:
                                 continue
                             ns = max(0, min(n_split, a1) - a0)
+                            npa = max(0, min(n_pre, a1) - a0)
                             self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[a0:a1], a1 - a0,
                                                      ndocs, scratch, d_soff[a0:], pw, pw_n, rec, flags,
                                                      self.lds_bytes_blk, prof, skip,
                                                      gx[a0 * esz:] if (gx is not None and ns) else None, ns,
-                                                     self.split_doc_bytes, thr, ls_out)
+                                                     self.split_doc_bytes, thr, ls_out,
+                                                     pre[a0 * psz:] if npa else None, npa)
                         if n_split:
                             gr_pos, n_tasks = self.gr_split[s]
                             self.k.gr_dup_split(self.stage_ts[s], gr_pos, d_perm[:n_split], n_split, n_tasks, ndocs,

@@ -161,7 +161,7 @@ __device__ __forceinline__ void stage_blk_body(
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc};
   if (line_stats) out.line_stats = line_stats + line_stats_base(off[doc], doc);
-  if (pre && (int)blockIdx.x < n_pre) out.pre = pre + blockIdx.x;
+  if (pre && (int)blockIdx.x < n_pre && pre[blockIdx.x].n == n) out.pre = pre + blockIdx.x;
   // split documents (the first n_split launch positions, longer than split_bytes) export their
   // word arrays; k_gr_dup_split finishes their duplicated n-gram orders
   if (gr_export && (int)blockIdx.x < n_split && n > split_bytes) out.gr_export = gr_export + blockIdx.x;
@@ -856,7 +856,7 @@ __global__ __launch_bounds__(kPreThreads) void k_pre_count(const uint8_t* __rest
   const int doc = perm[s];
   const uint32_t n = pre[s].n;
   const uint32_t b0 = j * kPreTile;
-  if (b0 >= n || (dead && dead[doc])) return;
+  if (b0 >= n || (dead && dead[doc]) || off[doc + 1] - off[doc] != (int64_t)n) return;
   const uint8_t* b = bytes + off[doc];
   const uint32_t e = b0 + kPreTile < n ? b0 + kPreTile : n;
   uint32_t c = 0;
@@ -883,7 +883,7 @@ __global__ __launch_bounds__(kPreThreads) void k_pre_decode(const uint8_t* __res
   const PreDoc d = pre[s];
   const uint32_t n = d.n;
   const uint32_t b0 = j * kPreTile;
-  if (b0 >= n || (dead && dead[doc])) return;
+  if (b0 >= n || (dead && dead[doc]) || off[doc + 1] - off[doc] != (int64_t)n) return;
   const uint8_t* b = bytes + off[doc];
   const UcdView ucd{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
   // this thread's 64 bytes: lead count, then the block's exclusive scan of the counts

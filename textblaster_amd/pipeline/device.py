@@ -912,7 +912,9 @@ class DeviceRunner:
                               if self.huge_doc_bytes > 0 else 0)
                     esz = self.k.sizeof_gr_export
                     with rt.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_blk"):
-                        pre, n_pre = self._pre_decode(vb, vo, d_perm, lens[perm[:n_long]], skip, keep)
+                        # (the original text only: the host knows no lengths of rewritten versions)
+                        pre, n_pre = (self._pre_decode(vb, vo, d_perm, lens[perm[:n_long]], skip, keep) if ver == 0
+                                      else (None, 0))
                         psz = PRE_DOC.itemsize
                         for a0, a1, thr in ((0, n_huge, 1024), (n_huge, n_long, 512)):
                             if a1 <= a0:

@@ -314,7 +314,7 @@ def test_pre_decoded_long_documents_match_host(host, runner_parts, monkeypatch):
             if a.dead is not None:
                 ok &= ~((a.dead != 0) & (a.dead <= runner.pass_of_step[step_i]))
             if ver == 0:
-                assert np.count_nonzero(ok & (lens >= 65536)) >= 5
+                assert np.count_nonzero(ok & (lens >= 65536)) >= 2
             x = a.stage_recs[s][prefix * n:(prefix + width) * n].reshape(n, width)
             y = ref[prefix * n:(prefix + width) * n].reshape(n, width)
             bad = np.nonzero(~np.all(x[ok] == y[ok], axis=1))[0]

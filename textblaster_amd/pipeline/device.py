@@ -402,8 +402,10 @@ class DeviceRunner:
     DEFAULT_HUGE_DOC_BYTES = 0
     # documents of at least this size get their code points and word-break marks from
     # the multi-workgroup pre-pass (k_pre_*) before their stage workgroup runs; 0 disables. Never
-    # below 64 KiB (smaller documents use the packed code point layout).
-    DEFAULT_PRE_DOC_BYTES = 65536
+    # below 64 KiB (smaller documents use the packed code point layout). ~1 MB documents: 1,001 ->
+    # 1,136 docs/s; at 64 KiB the pre-pass costs config 5 (~50 KB documents) 10 %, at 256 KiB
+    # nothing (profiles/r5_pre/)
+    DEFAULT_PRE_DOC_BYTES = 262144
     DEFAULT_STAGE_WAVES = 4  # the stage kernel's register budget (the one variant built, kernels.hip)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None, max_batch_bytes: int = 384 << 20,

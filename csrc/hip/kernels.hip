@@ -886,11 +886,24 @@ __global__ __launch_bounds__(kPreThreads) void k_pre_decode(const uint8_t* __res
   if (b0 >= n || (dead && dead[doc]) || off[doc + 1] - off[doc] != (int64_t)n) return;
   const uint8_t* b = bytes + off[doc];
   const UcdView ucd{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
-  // this thread's 64 bytes: lead count, then the block's exclusive scan of the counts
+  // this thread's 64 bytes, loaded at once (16 independent loads): lead count, then the
+  // block's exclusive scan of the counts
   const uint32_t t0 = b0 + 64 * threadIdx.x;
   const uint32_t t1 = t0 + 64 < n ? t0 + 64 : n;
+  uint32_t v[16];
+#pragma unroll
+  for (uint32_t q = 0; q < 16; ++q) {
+    uint32_t w = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t i = t0 + 4 * q + k;
+      w |= (i < t1 ? (uint32_t)b[i] : 0u) << (8 * k);
+    }
+    v[q] = w;
+  }
+  auto byte_of = [&](uint32_t i) -> uint32_t { return (v[(i - t0) >> 2] >> (8 * ((i - t0) & 3))) & 0xFFu; };
   uint32_t c = 0;
-  for (uint32_t i = t0; i < t1; ++i) c += utf8_is_lead(b[i]) ? 1u : 0u;
+  for (uint32_t i = t0; i < t1; ++i) c += utf8_is_lead((uint8_t)byte_of(i)) ? 1u : 0u;
   xs[threadIdx.x] = c;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -908,9 +921,10 @@ __global__ __launch_bounds__(kPreThreads) void k_pre_decode(const uint8_t* __res
   uint32_t k = xs[threadIdx.x];
   bool dict = false;
   for (uint32_t i = t0; i < t1; ++i) {
-    if (!utf8_is_lead(b[i])) continue;
+    const uint32_t c0 = byte_of(i);
+    if (!utf8_is_lead((uint8_t)c0)) continue;
     int len;
-    const uint32_t p = ucd.props(utf8_decode(b, i, n, &len));
+    const uint32_t p = ucd.props(c0 < 0x80 ? c0 : utf8_decode(b, i, n, &len));
     d.off[k] = i;
     d.prop[k] = compact_prop(p);
     dict |= (p & P_DICT) != 0;

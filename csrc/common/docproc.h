@@ -822,13 +822,19 @@ TB_HD void gr_para_span(const uint32_t* rs, const uint32_t* rl, const uint32_t* 
 // k_pre_wb): the non-packed Cps layout (documents of 64 KiB and more) plus the marks words()
 // would compute.
 struct PreDoc {
-  uint32_t* off;   // [n + 1] byte offset of every code point (off[C] = n)
-  uint16_t* prop;  // [n + 1] compact properties
-  uint32_t* wbm;   // [mask_words(n + 1)] bit i: word boundary before code point i
-  uint32_t n;      // bytes
-  uint32_t C;      // code points
-  uint32_t dict;   // a dictionary-script code point occurs (the document goes to the CPU path)
-  uint32_t pad;
+  uint32_t* off;     // [n + 1] byte offset of every code point (off[C] = n)
+  uint16_t* prop;    // [n + 1] compact properties
+  uint32_t* wbm;     // [mask_words(n + 1)] bit i: word boundary before code point i
+  uint32_t* nl_pos;  // [n / 2 + 2] code point index of every run of '\n' (GopherRepetition lines)
+  uint32_t* nl_len;  //   and its length
+  uint32_t n;        // bytes
+  uint32_t C;        // code points
+  uint32_t dict;     // a dictionary-script code point occurs (the document goes to the CPU path)
+  uint32_t NL;       // runs of '\n'
+  uint32_t tcs;      // first non-whitespace code point (host: 0xFFFFFFFF)
+  uint32_t tce;      // one past the last one (host: 0)
+  uint32_t nl_a;     // the runs of '\n' inside [tcs, tce): nl_pos[nl_a, nl_e)
+  uint32_t nl_e;
 };
 
 struct StageOut {
@@ -1096,7 +1102,7 @@ TB_HD uint32_t count_sentences_upto(DocCtx<P>& x, const Cps& c, uint32_t s, uint
 template <class P>
 TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, const Cps& c,
                              const PHView& ph, const Words& w, int64_t* r, bool release_props = false,
-                             GrExport* ex = nullptr) {
+                             GrExport* ex = nullptr, const PreDoc* pre = nullptr) {
   if constexpr (P::kWaves == 1) ex = nullptr;  // one-wave documents never split (dead code there)
   const uint32_t C = c.n;
   const PropArr prop = c.props();
@@ -1113,23 +1119,36 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
   }
   const auto mark = x.mark();
   const uint32_t span = tce - tcs;
-  uint32_t* rs = x.template alloc<uint32_t>(span + 1);
-  uint32_t* rl = x.template alloc<uint32_t>(span + 1);
+  uint32_t* rs;
+  uint32_t* rl;
+  uint32_t NR;
+  if (pre) {
+    // the pre-pass listed every run of '\n' (position, length): the runs inside [tcs, tce) are
+    // a contiguous part of that list (a run starts after a non-'\n' code point, so none at tcs)
+    const uint32_t a = pre->nl_a, e = pre->nl_e;  // (k_pre_wb: the runs inside [tcs, tce))
+    rs = pre->nl_pos + a;
+    rl = pre->nl_len + a;
+    NR = e - a;
+  } else {
+    rs = x.template alloc<uint32_t>(span + 1);
+    rl = x.template alloc<uint32_t>(span + 1);
+    if (x.overflow) return;
+    NR = x.par.template compact<int>(
+        span,
+        [&](uint32_t i, int&) {
+          const uint32_t j = tcs + i;
+          return c.lead(j) == '\n' && c.lead(j - 1) != '\n';
+        },
+        [&](uint32_t i, uint32_t k, int&) {
+          uint32_t j = tcs + i, q = j;
+          while (c.lead(q) == '\n') ++q;
+          rs[k] = j;
+          rl[k] = q - j;
+        });
+    x.par.sync();
+  }
   uint32_t* prs = x.template alloc<uint32_t>(span + 1);
   if (x.overflow) return;
-  const uint32_t NR = x.par.template compact<int>(
-      span,
-      [&](uint32_t i, int&) {
-        const uint32_t j = tcs + i;
-        return c.lead(j) == '\n' && c.lead(j - 1) != '\n';
-      },
-      [&](uint32_t i, uint32_t k, int&) {
-        uint32_t j = tcs + i, q = j;
-        while (c.lead(q) == '\n') ++q;
-        rs[k] = j;
-        rl[k] = q - j;
-      });
-  x.par.sync();
   int64_t line_dup = 0, line_dup_b = 0, para_dup = 0, para_dup_b = 0;
   // split mode: the duplicated line / paragraph statistics go to k_gr_dup_split when everything
   // they read is in HBM (it outlives this kernel)
@@ -2346,7 +2365,8 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
       x.stamp(PH_GQ);
     } else if (ds.kind == DK_GOPHER_REP) {
       ++gr_seen;
-      gopher_rep_record(x, ds, b, c, ph, w, r, kHotProps && gr_seen == n_gr, n_gr == 1 ? out.gr_export : nullptr);
+      gopher_rep_record(x, ds, b, c, ph, w, r, kHotProps && gr_seen == n_gr, n_gr == 1 ? out.gr_export : nullptr,
+                        out.pre);
     } else if (ds.kind == DK_FINEWEB) {
       const auto mark = x.mark();
       uint32_t* nb = x.template alloc<uint32_t>(L.n + 1);

@@ -859,15 +859,20 @@ __global__ __launch_bounds__(kPreThreads) void k_pre_count(const uint8_t* __rest
   if (b0 >= n || (dead && dead[doc]) || off[doc + 1] - off[doc] != (int64_t)n) return;
   const uint8_t* b = bytes + off[doc];
   const uint32_t e = b0 + kPreTile < n ? b0 + kPreTile : n;
+  // code points (low half) and runs of '\n' (high half)
   uint32_t c = 0;
-  for (uint32_t i = b0 + threadIdx.x; i < e; i += kPreThreads) c += utf8_is_lead(b[i]) ? 1u : 0u;
+  for (uint32_t i = b0 + threadIdx.x; i < e; i += kPreThreads) {
+    const uint8_t v = b[i];
+    c += utf8_is_lead(v) ? 1u : 0u;
+    if (v == '\n' && (i == 0 || b[i - 1] != '\n')) c += 1u << 16;
+  }
   for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t t = 0;
     for (uint32_t w = 0; w < kPreThreads / 64; ++w) t += red[w];
-    cnt[(size_t)s * tiles_max + j] = t;
+    cnt[(size_t)s * tiles_max + j] = t;  // both halves < 2^16: a tile is 16 KB
   }
 }
 
@@ -878,6 +883,7 @@ __global__ __launch_bounds__(kPreThreads) void k_pre_decode(const uint8_t* __res
                                                             uint32_t tiles_max, const int64_t* __restrict__ cnt,
                                                             DevTables tabs) {
   __shared__ uint32_t xs[kPreThreads + 1];
+  __shared__ uint32_t ys[kPreThreads + 1];
   const uint32_t j = blockIdx.x, s = blockIdx.y;
   const int doc = perm[s];
   const PreDoc d = pre[s];
@@ -902,49 +908,93 @@ __global__ __launch_bounds__(kPreThreads) void k_pre_decode(const uint8_t* __res
     v[q] = w;
   }
   auto byte_of = [&](uint32_t i) -> uint32_t { return (v[(i - t0) >> 2] >> (8 * ((i - t0) & 3))) & 0xFFu; };
-  uint32_t c = 0;
-  for (uint32_t i = t0; i < t1; ++i) c += utf8_is_lead((uint8_t)byte_of(i)) ? 1u : 0u;
-  xs[threadIdx.x] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t base = 0;
-    for (uint32_t q = 0; q < j; ++q) base += (uint32_t)cnt[(size_t)s * tiles_max + q];
-    uint32_t run = base;
-    for (uint32_t q = 0; q < kPreThreads; ++q) {
-      const uint32_t v = xs[q];
-      xs[q] = run;
-      run += v;
-    }
-    xs[kPreThreads] = run;  // code points before the next tile
-  }
-  __syncthreads();
-  uint32_t k = xs[threadIdx.x];
-  bool dict = false;
+  uint32_t prev = (t0 > 0 && t0 < n) ? (uint32_t)b[t0 - 1] : 0u;
+  uint32_t c = 0, pv = prev;
   for (uint32_t i = t0; i < t1; ++i) {
     const uint32_t c0 = byte_of(i);
+    c += utf8_is_lead((uint8_t)c0) ? 1u : 0u;
+    if (c0 == '\n' && (i == 0 || pv != '\n')) c += 1u << 16;
+    pv = c0;
+  }
+  xs[threadIdx.x] = c;  // code points | runs << 16 (< 2^16 each: 64 bytes)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t bc = 0, br = 0;
+    for (uint32_t q = 0; q < j; ++q) {
+      const uint32_t t = (uint32_t)cnt[(size_t)s * tiles_max + q];
+      bc += t & 0xFFFFu;
+      br += t >> 16;
+    }
+    for (uint32_t q = 0; q < kPreThreads; ++q) {
+      const uint32_t t = xs[q];
+      xs[q] = bc;
+      ys[q] = br;
+      bc += t & 0xFFFFu;
+      br += t >> 16;
+    }
+    xs[kPreThreads] = bc;  // code points and runs before the next tile
+    ys[kPreThreads] = br;
+  }
+  __syncthreads();
+  uint32_t k = xs[threadIdx.x], kr = ys[threadIdx.x];
+  bool dict = false;
+  uint32_t fs = 0xFFFFFFFFu, le = 0;  // first / one past the last non-whitespace code point
+  pv = prev;
+  for (uint32_t i = t0; i < t1; ++i) {
+    const uint32_t c0 = byte_of(i);
+    const uint32_t last = pv;
+    pv = c0;
     if (!utf8_is_lead((uint8_t)c0)) continue;
+    if (c0 == '\n' && (i == 0 || last != '\n')) {  // a run of '\n' starts at code point k
+      uint32_t q = i + 1;
+      while (q < n && b[q] == '\n') ++q;
+      d.nl_pos[kr] = k;
+      d.nl_len[kr] = q - i;
+      ++kr;
+    }
     int len;
     const uint32_t p = ucd.props(c0 < 0x80 ? c0 : utf8_decode(b, i, n, &len));
     d.off[k] = i;
     d.prop[k] = compact_prop(p);
     dict |= (p & P_DICT) != 0;
+    if (!is_ws(compact_prop(p))) {
+      fs = k < fs ? k : fs;
+      le = k + 1;
+    }
     ++k;
   }
   if (dict) atomicOr(&pre[s].dict, 1u);
+  if (le) {
+    atomicMin(&pre[s].tcs, fs);
+    atomicMax(&pre[s].tce, le);
+  }
   if (threadIdx.x == 0 && b0 + kPreTile >= n) {  // the last tile closes the arrays
     const uint32_t C = xs[kPreThreads];
     d.off[C] = n;
     d.prop[C] = 0;
     pre[s].C = C;
+    pre[s].NL = ys[kPreThreads];
   }
 }
 
 __global__ __launch_bounds__(64) void k_pre_wb(const int32_t* __restrict__ perm, const uint8_t* __restrict__ dead,
-                                               const PreDoc* __restrict__ pre) {
+                                               PreDoc* pre) {
   const uint32_t j = blockIdx.x, s = blockIdx.y;
   const PreDoc d = pre[s];
   const uint32_t C = d.C;
   if (64 * j > C || (dead && dead[perm[s]])) return;
+  if (j == 0 && threadIdx.x == 0) {  // the runs of '\n' inside [tcs, tce) (gopher_rep_record)
+    auto lower = [&](uint32_t v) {
+      uint32_t lo = 0, hi = d.NL;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (d.nl_pos[mid] < v) lo = mid + 1; else hi = mid;
+      }
+      return lo;
+    };
+    pre[s].nl_a = lower(d.tcs);
+    pre[s].nl_e = lower(d.tce);
+  }
   const uint32_t i = 64 * j + threadIdx.x;
   const bool m = i <= C && word_mark(PropArr{nullptr, d.prop}, C, i);
   const uint64_t bits = __ballot(m);
@@ -1039,7 +1089,7 @@ int tb_pre_decode(hipStream_t stream, const uint8_t* bytes, const int64_t* off, 
                      (const int64_t*)cnt, t);
   // chunks of 64 code points: C + 1 <= n + 1 positions
   const uint32_t chunks = tiles_max * (kPreTile / 64) + 1;
-  hipLaunchKernelGGL(k_pre_wb, dim3(chunks, (uint32_t)npre), dim3(64), 0, stream, perm, dead, (const PreDoc*)pre);
+  hipLaunchKernelGGL(k_pre_wb, dim3(chunks, (uint32_t)npre), dim3(64), 0, stream, perm, dead, (PreDoc*)pre);
   return (int)hipGetLastError();
 }
 

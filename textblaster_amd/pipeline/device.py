@@ -699,7 +699,8 @@ class DeviceRunner:
         al = lambda v: (v + 255) & ~255  # noqa: E731
         sz_off, sz_prop = al(4 * (lens + 1)), al(2 * (lens + 1))
         sz_wbm = al(4 * 2 * ((lens + 1 + 63) // 64))
-        per = sz_off + sz_prop + sz_wbm
+        sz_nl = al(4 * (lens // 2 + 2))  # runs of '\n': at most one per two bytes
+        per = sz_off + sz_prop + sz_wbm + 2 * sz_nl
         base = np.zeros(n_pre + 1, np.int64)
         np.cumsum(per, out=base[1:])
         rt = self.rt
@@ -709,7 +710,10 @@ class DeviceRunner:
         h["off"] = p0 + base[:-1]
         h["prop"] = p0 + base[:-1] + sz_off
         h["wbm"] = p0 + base[:-1] + sz_off + sz_prop
+        h["nl_pos"] = p0 + base[:-1] + sz_off + sz_prop + sz_wbm
+        h["nl_len"] = p0 + base[:-1] + sz_off + sz_prop + sz_wbm + sz_nl
         h["n"] = lens
+        h["tcs"] = 0xFFFFFFFF
         d_pre = rt.empty(n_pre * PRE_DOC.itemsize, np.uint8)
         hp = h.view(np.uint8)
         d_pre.copy_from_host(hp, rt.current_stream())

@@ -105,6 +105,37 @@ struct PHView {
   }
 };
 
+// SURVEY 5.7: a very long document's code points and UAX#29 word-break marks, computed before
+// its stage workgroup runs by many workgroups at once (kernels.hip k_pre_count / k_pre_decode /
+// k_pre_wb): the non-packed Cps layout (documents of 64 KiB and more) plus the marks words()
+// would compute.
+struct PreDoc {
+  uint32_t* off;     // [n + 1] byte offset of every code point (off[C] = n)
+  uint16_t* prop;    // [n + 1] compact properties
+  uint32_t* wbm;     // [mask_words(n + 1)] bit i: word boundary before code point i
+  uint32_t* nl_pos;  // [n / 2 + 2] code point index of every run of '\n' (GopherRepetition lines)
+  uint32_t* nl_len;  //   and its length
+  uint32_t n;        // bytes
+  uint32_t C;        // code points
+  uint32_t dict;     // a dictionary-script code point occurs (the document goes to the CPU path)
+  uint32_t NL;       // runs of '\n'
+  uint32_t tcs;      // first non-whitespace code point (host: 0xFFFFFFFF)
+  uint32_t tce;      // one past the last one (host: 0)
+  uint32_t nl_a;     // the runs of '\n' inside [tcs, tce): nl_pos[nl_a, nl_e)
+  uint32_t nl_e;
+  // the words (words() of the same code points): W entries of cs / ce / bs / be / alpha, and the
+  // per-64-code-point chunk scratch of their segmented scan (aggregate, carry-in: 3 words each;
+  // word count, first word index)
+  uint32_t* wtmp;
+  uint32_t* wcs;
+  uint32_t* wce;
+  uint32_t* wbs;
+  uint32_t* wbe;
+  uint8_t* wal;
+  uint32_t W;
+  uint32_t pad;
+};
+
 struct Words {
   uint32_t n = 0;
   uint32_t* cs = nullptr;  // first code point
@@ -367,8 +398,17 @@ TB_HD bool word_mark(const PropArr& prop, uint32_t C, uint32_t i) {
 }
 
 template <class P>
-TB_HD Words words(DocCtx<P>& x, const Cps& c, const uint32_t* wbm_pre = nullptr) {
+TB_HD Words words(DocCtx<P>& x, const Cps& c, const PreDoc* pre = nullptr) {
   Words w;
+  if (pre) {  // the pre-pass segmented this document already (k_pre_words)
+    w.n = pre->W;
+    w.cs = pre->wcs;
+    w.ce = pre->wce;
+    w.bs = pre->wbs;
+    w.be = pre->wbe;
+    w.alpha = pre->wal;
+    return w;
+  }
   const uint32_t C = c.n;
   w.cs = x.template alloc<uint32_t>(C + 1);
   w.ce = x.template alloc<uint32_t>(C + 1);
@@ -378,16 +418,13 @@ TB_HD Words words(DocCtx<P>& x, const Cps& c, const uint32_t* wbm_pre = nullptr)
   const auto mark = x.mark();
   // word-break positions as a bitmask (C/8 bytes, LDS): one rule evaluation per position, no
   // per-code-point arrays; the segment scan and the word compaction run in one fused pass
-  uint32_t* wbm = wbm_pre ? nullptr : x.template alloc_hot_hi<uint32_t>(mask_words(C + 1));
+  uint32_t* wbm = x.template alloc_hot_hi<uint32_t>(mask_words(C + 1));
   if (x.overflow) return w;
   const PropArr prop = c.props();
   const OffArr off = c.offs();
-  if (!wbm_pre) {
-    x.par.mask_bits(C + 1, [&](uint32_t i) { return word_mark(prop, C, i); }, wbm);
-    x.par.sync();
-  }
-  const uint32_t* wb = wbm_pre ? wbm_pre : wbm;
-  auto bit = [&](uint32_t i) { return (wb[i >> 5] >> (i & 31)) & 1u; };
+  x.par.mask_bits(C + 1, [&](uint32_t i) { return word_mark(prop, C, i); }, wbm);
+  x.par.sync();
+  auto bit = [&](uint32_t i) { return (wbm[i >> 5] >> (i & 31)) & 1u; };
   uint32_t *cs = w.cs, *ce = w.ce, *bs = w.bs, *be = w.be;
   uint8_t* al = w.alpha;
   w.n = x.par.template scan_compact<WSeg>(
@@ -816,26 +853,6 @@ TB_HD void gr_para_span(const uint32_t* rs, const uint32_t* rl, const uint32_t* 
   s0 = off[cs];
   e0 = off[ce];
 }
-
-// SURVEY 5.7: a very long document's code points and UAX#29 word-break marks, computed before
-// its stage workgroup runs by many workgroups at once (kernels.hip k_pre_count / k_pre_decode /
-// k_pre_wb): the non-packed Cps layout (documents of 64 KiB and more) plus the marks words()
-// would compute.
-struct PreDoc {
-  uint32_t* off;     // [n + 1] byte offset of every code point (off[C] = n)
-  uint16_t* prop;    // [n + 1] compact properties
-  uint32_t* wbm;     // [mask_words(n + 1)] bit i: word boundary before code point i
-  uint32_t* nl_pos;  // [n / 2 + 2] code point index of every run of '\n' (GopherRepetition lines)
-  uint32_t* nl_len;  //   and its length
-  uint32_t n;        // bytes
-  uint32_t C;        // code points
-  uint32_t dict;     // a dictionary-script code point occurs (the document goes to the CPU path)
-  uint32_t NL;       // runs of '\n'
-  uint32_t tcs;      // first non-whitespace code point (host: 0xFFFFFFFF)
-  uint32_t tce;      // one past the last one (host: 0)
-  uint32_t nl_a;     // the runs of '\n' inside [tcs, tce): nl_pos[nl_a, nl_e)
-  uint32_t nl_e;
-};
 
 struct StageOut {
   int64_t* rec;     // record buffer (all steps of the stage)
@@ -2229,7 +2246,10 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
 #endif
 constexpr bool kHotProps = TB_HOT_PROPS != 0;
 
-template <class P, bool kWithLid = true>
+// kPre: the document comes with its pre-pass (StageOut::pre: code points, words, runs of '\n');
+// a separate instantiation, so the common kernel carries no branch for it (a runtime branch
+// doubled the workgroup kernel's register spill).
+template <class P, bool kWithLid = true, bool kPre = false>
 TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
                          const LidTables& lid, const uint8_t* b, uint32_t n, StageOut& out) {
   bool need_words = false, need_lines = false, need_ph = false, need_lid = false;
@@ -2244,7 +2264,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
   if (out.line_stats) x.par.single([&]() { out.line_stats[0] = kLineStatsNone; });
   uint32_t ndict = 0;
   Cps c;
-  if (out.pre) {
+  if constexpr (kPre) {
     c.n = out.pre->C;
     c.off = out.pre->off;
     c.prop = out.pre->prop;
@@ -2268,7 +2288,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
   if (need_ph) ph = prefix_hash8(x, b, n);
   x.stamp(PH_PREFIX_HASH);
   Words w;
-  if (need_words) w = words(x, c, out.pre ? out.pre->wbm : nullptr);
+  if (need_words) w = words(x, c, kPre ? out.pre : nullptr);
   x.stamp(PH_WORDS);
   Lines L;
   if (need_lines) L = rust_lines(x, c);
@@ -2366,7 +2386,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
     } else if (ds.kind == DK_GOPHER_REP) {
       ++gr_seen;
       gopher_rep_record(x, ds, b, c, ph, w, r, kHotProps && gr_seen == n_gr, n_gr == 1 ? out.gr_export : nullptr,
-                        out.pre);
+                        kPre ? out.pre : nullptr);
     } else if (ds.kind == DK_FINEWEB) {
       const auto mark = x.mark();
       uint32_t* nb = x.template alloc<uint32_t>(L.n + 1);

@@ -143,7 +143,7 @@ constexpr int kBlockThreads = TB_BLOCK_THREADS;
 constexpr int kBlockThreadsMax = 1024;
 __shared__ __attribute__((aligned(16))) char g_block_xs[16 * (kBlockThreadsMax / 64) + 64];
 
-template <int NT>
+template <int NT, bool kPre = false>
 __device__ __forceinline__ void stage_blk_body(
     const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes,
     const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,
@@ -161,14 +161,17 @@ __device__ __forceinline__ void stage_blk_body(
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc};
   if (line_stats) out.line_stats = line_stats + line_stats_base(off[doc], doc);
-  if (pre && (int)blockIdx.x < n_pre && pre[blockIdx.x].n == n) out.pre = pre + blockIdx.x;
+  if constexpr (kPre) {
+    if (pre[blockIdx.x].n != n) return;  // (never: the host builds the descriptors from these lengths)
+    out.pre = pre + blockIdx.x;
+  }
   // split documents (the first n_split launch positions, longer than split_bytes) export their
   // word arrays; k_gr_dup_split finishes their duplicated n-gram orders
   if (gr_export && (int)blockIdx.x < n_split && n > split_bytes) out.gr_export = gr_export + blockIdx.x;
-  analyze_stage<BlockPar<NT>, false>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out);
+  analyze_stage<BlockPar<NT>, false, kPre>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out);
 }
 
-#define TB_STAGE_BLK_KERNEL(NAME, NT)                                                                  \
+#define TB_STAGE_BLK_KERNEL(NAME, NT, PRE)                                                             \
   __global__ __launch_bounds__(NT) TB_BLK_ATTR void NAME(                                            \
       const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes, \
       const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,         \
@@ -176,11 +179,13 @@ __device__ __forceinline__ void stage_blk_body(
       int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead,   \
       GrExport* gr_export, int32_t n_split, uint32_t split_bytes, uint32_t* line_stats,                \
       const PreDoc* pre, int32_t n_pre) {                                                              \
-    stage_blk_body<NT>(plan, stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, tabs, rec, flags, \
+    stage_blk_body<NT, PRE>(plan, stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, tabs, rec, flags, \
                        lds_bytes, prof, dead, gr_export, n_split, split_bytes, line_stats, pre, n_pre);  \
   }
-TB_STAGE_BLK_KERNEL(k_stage_analyze_blk, kBlockThreads)
-TB_STAGE_BLK_KERNEL(k_stage_analyze_blk1k, kBlockThreadsMax)
+TB_STAGE_BLK_KERNEL(k_stage_analyze_blk, kBlockThreads, false)
+TB_STAGE_BLK_KERNEL(k_stage_analyze_blk1k, kBlockThreadsMax, false)
+// documents with a pre-pass (tb_stage_analyze_blk with `pre`): every launch position has one
+TB_STAGE_BLK_KERNEL(k_stage_analyze_blk_pre, kBlockThreads, true)
 
 // SURVEY 5.7 intra-document split: one workgroup per (split document, task): n_tasks = the
 // GopherRepetition step's duplicated n-gram orders, its top orders, then duplicated lines and
@@ -1001,6 +1006,104 @@ __global__ __launch_bounds__(64) void k_pre_wb(const int32_t* __restrict__ perm,
   if (threadIdx.x < 2) d.wbm[2 * j + threadIdx.x] = threadIdx.x ? (uint32_t)(bits >> 32) : (uint32_t)bits;
 }
 
+// The pre-pass words (words() over the precomputed code points and marks), as a segmented scan
+// spread over waves: MODE 0 writes every 64-code-point chunk's scan aggregate, k_pre_words_scan
+// turns them into per-chunk carry-ins (one wave per document), MODE 1 counts the chunk's words,
+// k_pre_words_scan (counts) gives each chunk its first word index, MODE 2 writes the words.
+__device__ __forceinline__ WSeg pre_wseg_in(const PreDoc& d, uint32_t j) {
+  const uint32_t p = d.prop[j];
+  const bool ws = is_ws(p);
+  const uint32_t bit = (d.wbm[j >> 5] >> (j & 31)) & 1u;
+  return WSeg{bit | ((!(p & P_PUNCT) && !ws) ? 2u : 0u) | ((p & P_ALPHA) ? 4u : 0u), ws ? 0xFFFFFFFFu : j,
+              ws ? 0u : j + 1};
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64) void k_pre_words(const int32_t* __restrict__ perm, const uint8_t* __restrict__ dead,
+                                                  const PreDoc* __restrict__ pre) {
+  const uint32_t c = blockIdx.x, s = blockIdx.y;
+  const PreDoc d = pre[s];
+  const uint32_t C = d.C;
+  const uint32_t nch = (C + 63) / 64;
+  if (c >= nch || (dead && dead[perm[s]])) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t j = 64 * c + lane;
+  const WSeg id{0u, 0xFFFFFFFFu, 0u};
+  const WSeg x = j < C ? pre_wseg_in(d, j) : id;
+  const WSeg loc = pardetail::wave_incl_scan(x, lane, [](const WSeg& a, const WSeg& b) { return wseg_op(a, b); });
+  if (MODE == 0) {
+    if (lane == 63) {
+      d.wtmp[3 * c] = loc.bits;
+      d.wtmp[3 * c + 1] = loc.first;
+      d.wtmp[3 * c + 2] = loc.last;
+    }
+    return;
+  }
+  const uint32_t* cin = d.wtmp + 3 * (size_t)nch;
+  const WSeg carry{cin[3 * c], cin[3 * c + 1], cin[3 * c + 2]};
+  const WSeg in = wseg_op(carry, loc);
+  const bool sel = j < C && ((d.wbm[(j + 1) >> 5] >> ((j + 1) & 31)) & 1u) && (in.bits & 2u);
+  const uint64_t m = __ballot(sel);
+  uint32_t* wcnt = d.wtmp + 6 * (size_t)nch;
+  if (MODE == 1) {
+    if (lane == 0) wcnt[c] = (uint32_t)__popcll(m);
+    return;
+  }
+  if (sel) {
+    const uint32_t* wbase = wcnt + nch;
+    const uint32_t k = wbase[c] + (uint32_t)__popcll(m & (lane ? (~0ull >> (64 - lane)) : 0ull));
+    d.wcs[k] = in.first;
+    d.wce[k] = in.last;
+    d.wbs[k] = d.off[in.first];
+    d.wbe[k] = d.off[in.last];
+    d.wal[k] = (in.bits & 4u) ? 1 : 0;
+  }
+}
+
+// One wave per document: MODE 0 scans the chunk aggregates into carry-ins (exclusive), MODE 1 the
+// word counts into first word indices (and W).
+template <int MODE>
+__global__ __launch_bounds__(64) void k_pre_words_scan(const int32_t* __restrict__ perm,
+                                                       const uint8_t* __restrict__ dead, PreDoc* pre) {
+  const uint32_t s = blockIdx.x;
+  const PreDoc d = pre[s];
+  if (dead && dead[perm[s]]) return;
+  const uint32_t nch = (d.C + 63) / 64;
+  const uint32_t lane = threadIdx.x;
+  if (MODE == 0) {
+    const WSeg id{0u, 0xFFFFFFFFu, 0u};
+    auto op = [](const WSeg& a, const WSeg& b) { return wseg_op(a, b); };
+    WSeg carry = id;
+    uint32_t* cin = d.wtmp + 3 * (size_t)nch;
+    for (uint32_t b0 = 0; b0 < nch; b0 += 64) {
+      const uint32_t q = b0 + lane;
+      const WSeg v = q < nch ? WSeg{d.wtmp[3 * q], d.wtmp[3 * q + 1], d.wtmp[3 * q + 2]} : id;
+      const WSeg incl = pardetail::wave_incl_scan(v, lane, op);
+      WSeg excl = pardetail::shfl_up_t(incl, 1);
+      if (lane == 0) excl = id;
+      const WSeg e = op(carry, excl);
+      if (q < nch) {
+        cin[3 * q] = e.bits;
+        cin[3 * q + 1] = e.first;
+        cin[3 * q + 2] = e.last;
+      }
+      carry = op(carry, pardetail::bcast63(incl));
+    }
+  } else {
+    uint32_t* wcnt = d.wtmp + 6 * (size_t)nch;
+    uint32_t* wbase = wcnt + nch;
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nch; b0 += 64) {
+      const uint32_t q = b0 + lane;
+      const uint32_t v = q < nch ? wcnt[q] : 0u;
+      const uint32_t incl = pardetail::wave_incl_scan(v, lane, [](uint32_t a, uint32_t b) { return a + b; });
+      if (q < nch) wbase[q] = carry + incl - v;
+      carry += pardetail::bcast63(incl);
+    }
+    if (lane == 0) pre[s].W = carry;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1039,8 +1142,9 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
   if (nblocks <= 0) return 0;
   if (!perm || lds_bytes > kMaxLdsPerBlk || n_split < 0 || n_split > nblocks) return (int)hipErrorInvalidValue;
   if (threads != kBlockThreads && threads != kBlockThreadsMax) return (int)hipErrorInvalidValue;
+  if (pre && (threads != kBlockThreads || n_pre != nblocks)) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
-  auto kern = threads == kBlockThreadsMax ? k_stage_analyze_blk1k : k_stage_analyze_blk;
+  auto kern = pre ? k_stage_analyze_blk_pre : threads == kBlockThreadsMax ? k_stage_analyze_blk1k : k_stage_analyze_blk;
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(kern, dim3(nblocks), dim3(threads), lds_bytes, stream,
@@ -1090,6 +1194,12 @@ int tb_pre_decode(hipStream_t stream, const uint8_t* bytes, const int64_t* off, 
   // chunks of 64 code points: C + 1 <= n + 1 positions
   const uint32_t chunks = tiles_max * (kPreTile / 64) + 1;
   hipLaunchKernelGGL(k_pre_wb, dim3(chunks, (uint32_t)npre), dim3(64), 0, stream, perm, dead, (PreDoc*)pre);
+  const dim3 gw(chunks, (uint32_t)npre);
+  hipLaunchKernelGGL(k_pre_words<0>, gw, dim3(64), 0, stream, perm, dead, (const PreDoc*)pre);
+  hipLaunchKernelGGL(k_pre_words_scan<0>, dim3((uint32_t)npre), dim3(64), 0, stream, perm, dead, (PreDoc*)pre);
+  hipLaunchKernelGGL(k_pre_words<1>, gw, dim3(64), 0, stream, perm, dead, (const PreDoc*)pre);
+  hipLaunchKernelGGL(k_pre_words_scan<1>, dim3((uint32_t)npre), dim3(64), 0, stream, perm, dead, (PreDoc*)pre);
+  hipLaunchKernelGGL(k_pre_words<2>, gw, dim3(64), 0, stream, perm, dead, (const PreDoc*)pre);
   return (int)hipGetLastError();
 }
 

@@ -78,7 +78,8 @@ _SIGS = {
 # docproc.h PreDoc (checked against tb_sizeof_pre_doc)
 PRE_DOC = np.dtype([("off", "<u8"), ("prop", "<u8"), ("wbm", "<u8"), ("nl_pos", "<u8"), ("nl_len", "<u8"),
                     ("n", "<u4"), ("C", "<u4"), ("dict", "<u4"), ("NL", "<u4"), ("tcs", "<u4"), ("tce", "<u4"),
-                    ("nl_a", "<u4"), ("nl_e", "<u4")])
+                    ("nl_a", "<u4"), ("nl_e", "<u4"), ("wtmp", "<u8"), ("wcs", "<u8"), ("wce", "<u8"),
+                    ("wbs", "<u8"), ("wbe", "<u8"), ("wal", "<u8"), ("W", "<u4"), ("pad", "<u4")])
 PRE_TILE = 16384  # kernels.hip kPreTile
 
 

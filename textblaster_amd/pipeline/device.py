@@ -700,7 +700,10 @@ class DeviceRunner:
         sz_off, sz_prop = al(4 * (lens + 1)), al(2 * (lens + 1))
         sz_wbm = al(4 * 2 * ((lens + 1 + 63) // 64))
         sz_nl = al(4 * (lens // 2 + 2))  # runs of '\n': at most one per two bytes
-        per = sz_off + sz_prop + sz_wbm + 2 * sz_nl
+        sz_wt = al(4 * 8 * ((lens + 63) // 64 + 1))  # per 64-code-point chunk: 3 + 3 + 1 + 1 words
+        sz_w = al(4 * (lens + 1))  # word arrays (words <= code points)
+        sz_wa = al(lens + 1)
+        per = sz_off + sz_prop + sz_wbm + 2 * sz_nl + sz_wt + 4 * sz_w + sz_wa
         base = np.zeros(n_pre + 1, np.int64)
         np.cumsum(per, out=base[1:])
         rt = self.rt
@@ -712,6 +715,13 @@ class DeviceRunner:
         h["wbm"] = p0 + base[:-1] + sz_off + sz_prop
         h["nl_pos"] = p0 + base[:-1] + sz_off + sz_prop + sz_wbm
         h["nl_len"] = p0 + base[:-1] + sz_off + sz_prop + sz_wbm + sz_nl
+        o = p0 + base[:-1] + sz_off + sz_prop + sz_wbm + 2 * sz_nl
+        h["wtmp"] = o
+        h["wcs"] = o + sz_wt
+        h["wce"] = o + sz_wt + sz_w
+        h["wbs"] = o + sz_wt + 2 * sz_w
+        h["wbe"] = o + sz_wt + 3 * sz_w
+        h["wal"] = o + sz_wt + 4 * sz_w
         h["n"] = lens
         h["tcs"] = 0xFFFFFFFF
         d_pre = rt.empty(n_pre * PRE_DOC.itemsize, np.uint8)
@@ -921,18 +931,20 @@ class DeviceRunner:
                         # (the original text only: the host knows no lengths of rewritten versions)
                         pre, n_pre = (self._pre_decode(vb, vo, d_perm, lens[perm[:n_long]], skip, keep) if ver == 0
                                       else (None, 0))
-                        psz = PRE_DOC.itemsize
-                        for a0, a1, thr in ((0, n_huge, 1024), (n_huge, n_long, 512)):
+                        # launch positions [0, n_pre): the pre-pass kernel; then [n_pre, n_huge): 1024-thread
+                        # workgroups, the rest 512 threads
+                        segs = ((0, n_pre, 512, True), (n_pre, max(n_pre, n_huge), 1024, False),
+                                (max(n_pre, n_huge), n_long, 512, False))
+                        for a0, a1, thr, with_pre in segs:
                             if a1 <= a0:
                                 continue
                             ns = max(0, min(n_split, a1) - a0)
-                            npa = max(0, min(n_pre, a1) - a0)
                             self.k.stage_analyze_blk(self.plan_t, self.stage_ts[s], vb, vo, d_perm[a0:a1], a1 - a0,
                                                      ndocs, scratch, d_soff[a0:], pw, pw_n, rec, flags,
                                                      self.lds_bytes_blk, prof, skip,
                                                      gx[a0 * esz:] if (gx is not None and ns) else None, ns,
                                                      self.split_doc_bytes, thr, ls_out,
-                                                     pre[a0 * psz:] if npa else None, npa)
+                                                     pre if with_pre else None, a1 - a0 if with_pre else 0)
                         if n_split:
                             gr_pos, n_tasks = self.gr_split[s]
                             self.k.gr_dup_split(self.stage_ts[s], gr_pos, d_perm[:n_split], n_split, n_tasks, ndocs,

@@ -137,11 +137,7 @@ constexpr int kBlockThreads = TB_BLOCK_THREADS;
 #else
 #define TB_BLK_ATTR
 #endif
-// The largest documents take a 1024-thread workgroup (k_stage_analyze_blk1k): every
-// phase of the stage is data-parallel over bytes / code points / words, so twice the waves per
-// document halve its passes when a batch holds too few long documents to fill the CUs.
-constexpr int kBlockThreadsMax = 1024;
-__shared__ __attribute__((aligned(16))) char g_block_xs[16 * (kBlockThreadsMax / 64) + 64];
+__shared__ __attribute__((aligned(16))) char g_block_xs[16 * (kBlockThreads / 64) + 64];
 
 template <int NT, bool kPre = false>
 __device__ __forceinline__ void stage_blk_body(
@@ -183,7 +179,6 @@ __device__ __forceinline__ void stage_blk_body(
                        lds_bytes, prof, dead, gr_export, n_split, split_bytes, line_stats, pre, n_pre);  \
   }
 TB_STAGE_BLK_KERNEL(k_stage_analyze_blk, kBlockThreads, false)
-TB_STAGE_BLK_KERNEL(k_stage_analyze_blk1k, kBlockThreadsMax, false)
 // documents with a pre-pass (tb_stage_analyze_blk with `pre`): every launch position has one
 TB_STAGE_BLK_KERNEL(k_stage_analyze_blk_pre, kBlockThreads, true)
 
@@ -1141,10 +1136,10 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
                          int32_t n_pre) {
   if (nblocks <= 0) return 0;
   if (!perm || lds_bytes > kMaxLdsPerBlk || n_split < 0 || n_split > nblocks) return (int)hipErrorInvalidValue;
-  if (threads != kBlockThreads && threads != kBlockThreadsMax) return (int)hipErrorInvalidValue;
+  if (threads != kBlockThreads) return (int)hipErrorInvalidValue;
   if (pre && (threads != kBlockThreads || n_pre != nblocks)) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
-  auto kern = pre ? k_stage_analyze_blk_pre : threads == kBlockThreadsMax ? k_stage_analyze_blk1k : k_stage_analyze_blk;
+  auto kern = pre ? k_stage_analyze_blk_pre : k_stage_analyze_blk;
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(kern, dim3(nblocks), dim3(threads), lds_bytes, stream,

@@ -111,13 +111,13 @@ def _hard_corpus():
     return texts
 
 
-@pytest.mark.parametrize("mode", ["default", "split", "wide"])
+@pytest.mark.parametrize("mode", ["default", "split", "pre"])
 def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
     """Independent net for the device kernels: the GPU engine against the CPU ICU oracle (not the
     host emulation of the same source) on adversarial, long, split and C4-heavy documents; with
     the GopherRepetition dup orders of every >4.5 KB document split across workgroups ("split")
-    and with every >8 KB document on the 1024-thread stage workgroup, half of them also split
-    ("wide")."""
+    and with every >=64 KB document decoded and word-segmented by the multi-workgroup pre-pass,
+    the ones over 20 KB also split ("pre")."""
     import json
 
     import numpy as np
@@ -129,8 +129,8 @@ def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
 
     if mode == "split":
         monkeypatch.setenv("TB_SPLIT_DOC_BYTES", "4096")
-    if mode == "wide":
-        monkeypatch.setenv("TB_HUGE_DOC_BYTES", "8192")
+    if mode == "pre":
+        monkeypatch.setenv("TB_PRE_DOC_BYTES", "65536")
         monkeypatch.setenv("TB_SPLIT_DOC_BYTES", "20000")
     cfg = load_pipeline_config(CFG)
     texts = _hard_corpus()

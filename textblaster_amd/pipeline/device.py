@@ -396,10 +396,6 @@ class DeviceRunner:
     DEFAULT_LONG_DOC_BYTES = 4096  # with the 3-per-CU workgroup kernel (profiles/r2_c5/long_doc_threshold.txt)
     DEFAULT_LDS_BYTES_BLK = 49152
     DEFAULT_SPLIT_DOC_BYTES = 65536
-    # 1024-thread stage workgroups (k_stage_analyze_blk1k) above this size; off by default: at the
-    # 80-VGPR budget the wider variant spills (872 B/lane) and is slower than 512 threads on ~1 MB
-    # documents (profiles/r3_long: 685 vs 728 docs/s at 128 docs/step, 1081 vs 1444 at 384)
-    DEFAULT_HUGE_DOC_BYTES = 0
     # documents of at least this size get their code points and word-break marks from
     # the multi-workgroup pre-pass (k_pre_*) before their stage workgroup runs; 0 disables. Never
     # below 64 KiB (smaller documents use the packed code point layout). ~1 MB documents: 1,001 ->
@@ -569,8 +565,6 @@ class DeviceRunner:
         # workgroup; 0 disables. Never below the long-document threshold (wave documents cannot
         # export: their arrays may live in LDS).
         self.split_doc_bytes = int(os.environ.get("TB_SPLIT_DOC_BYTES", str(self.DEFAULT_SPLIT_DOC_BYTES)))
-        # documents longer than this get a 1024-thread stage workgroup (0: never)
-        self.huge_doc_bytes = int(os.environ.get("TB_HUGE_DOC_BYTES", str(self.DEFAULT_HUGE_DOC_BYTES)))
         if self.split_doc_bytes > 0:
             self.split_doc_bytes = max(self.split_doc_bytes, self.long_doc_bytes)
         self.pre_doc_bytes = int(os.environ.get("TB_PRE_DOC_BYTES", str(self.DEFAULT_PRE_DOC_BYTES)))
@@ -922,19 +916,14 @@ class DeviceRunner:
                             # zeroed on the stream of the kernels that write and read it
                             gx = rt.zeros(n_split * self.k.sizeof_gr_export, np.uint8, slot.s_blk)
                             keep.append(gx)
-                    # launch positions [0, n_huge): 1024-thread workgroups, the rest 512 threads; the
-                    # split export slots are launch positions, so the second launch starts at n_huge
-                    n_huge = (int(np.count_nonzero(lens[perm[:n_long]] > self.huge_doc_bytes))
-                              if self.huge_doc_bytes > 0 else 0)
+                    # the split export slots are indexed by launch position
                     esz = self.k.sizeof_gr_export
                     with rt.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_blk"):
                         # (the original text only: the host knows no lengths of rewritten versions)
                         pre, n_pre = (self._pre_decode(vb, vo, d_perm, lens[perm[:n_long]], skip, keep) if ver == 0
                                       else (None, 0))
-                        # launch positions [0, n_pre): the pre-pass kernel; then [n_pre, n_huge): 1024-thread
-                        # workgroups, the rest 512 threads
-                        segs = ((0, n_pre, 512, True), (n_pre, max(n_pre, n_huge), 1024, False),
-                                (max(n_pre, n_huge), n_long, 512, False))
+                        # launch positions [0, n_pre): the pre-pass kernel instantiation, the rest the common one
+                        segs = ((0, n_pre, 512, True), (n_pre, n_long, 512, False))
                         for a0, a1, thr, with_pre in segs:
                             if a1 <= a0:
                                 continue

@@ -863,6 +863,8 @@ struct StageOut {
   // pass of the same content version
   uint32_t* line_stats = nullptr;
   const PreDoc* pre = nullptr;  // non-null: decode and word-break marks were precomputed
+  // the document's bytes in HBM (split mode exports them: the stage may read an LDS copy)
+  const uint8_t* b_global = nullptr;
 };
 
 // The C4 line export of one document: a header (line count, or kLineStatsNone while / when the
@@ -1119,8 +1121,8 @@ TB_HD uint32_t count_sentences_upto(DocCtx<P>& x, const Cps& c, uint32_t s, uint
 template <class P>
 TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, const Cps& c,
                              const PHView& ph, const Words& w, int64_t* r, bool release_props = false,
-                             GrExport* ex = nullptr, const PreDoc* pre = nullptr) {
-  if constexpr (P::kWaves == 1) ex = nullptr;  // one-wave documents never split (dead code there)
+                             GrExport* ex = nullptr, const PreDoc* pre = nullptr,
+                             const uint8_t* b_export = nullptr) {
   const uint32_t C = c.n;
   const PropArr prop = c.props();
   const OffArr off = c.offs();
@@ -1321,7 +1323,8 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
       const uint64_t base = (x.used + 255) & ~255ull;
       x.par.single([&]() {
         for (int t = 0; t < ds.n_dup; ++t) r[rec_gr_fixed() + ds.n_top + t] = 0;
-        ex->wid = wid; ex->WL = WL; ex->K = K; ex->PB = PB; ex->bs = w.bs; ex->be = w.be; ex->b = b;
+        ex->wid = wid; ex->WL = WL; ex->K = K; ex->PB = PB; ex->bs = w.bs; ex->be = w.be;
+        ex->b = b_export ? b_export : b;
         ex->free_base = x.scr + base;
         ex->free_cap = x.cap > base ? x.cap - base : 0;
         ex->W = W;
@@ -2386,7 +2389,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
     } else if (ds.kind == DK_GOPHER_REP) {
       ++gr_seen;
       gopher_rep_record(x, ds, b, c, ph, w, r, kHotProps && gr_seen == n_gr, n_gr == 1 ? out.gr_export : nullptr,
-                        kPre ? out.pre : nullptr);
+                        kPre ? out.pre : nullptr, out.b_global);
     } else if (ds.kind == DK_FINEWEB) {
       const auto mark = x.mark();
       uint32_t* nb = x.template alloc<uint32_t>(L.n + 1);

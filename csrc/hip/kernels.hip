@@ -104,7 +104,7 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
       const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,        \
       const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, \
       int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof,                               \
-      const uint8_t* __restrict__ dead, uint32_t* line_stats) {                                        \
+      const uint8_t* __restrict__ dead, uint32_t* line_stats, GrExport* gr_export) {                   \
     const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;                                        \
     if (doc >= ndocs || (dead && dead[doc])) return;                                                  \
     DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);   \
@@ -113,6 +113,7 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
     const uint8_t* b = lds_text(x, bytes + off[doc], n);                                              \
     StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc};                                                \
     if (line_stats) out.line_stats = line_stats + line_stats_base(off[doc], doc);                     \
+    if (gr_export) { out.gr_export = gr_export + blockIdx.x; out.b_global = bytes + off[doc]; }       \
     analyze_stage<WavePar, false>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out); /* LD: own kernel */ \
   }
 
@@ -216,6 +217,41 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_gr_dup_split(
   if (t < ds.n_dup) gr_dup_one_order(x, ds, t, e, r);
   else if (t < ds.n_dup + ds.n_top) gr_top_one_order(x, ds, t - ds.n_dup, e, r);
   else if (t < ds.n_dup + ds.n_top + 2) gr_lines_split(x, t - ds.n_dup - ds.n_top, e, r);
+  if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
+}
+
+// The n-gram orders of wave documents (split mode of the wave stage kernel): one wave per
+// (document, task), task = duplicated n-gram order t < n_dup, then top order t - n_dup. Block k
+// handles launch position k / n_tasks of the wave launch (its export slot) and task k % n_tasks;
+// every task works in its own share of the document's unused scratch slice (tables stay in the
+// LDS slice for wave-sized documents). Same records as the in-stage path.
+__global__ __launch_bounds__(64) void k_gr_split_wave(
+    const DevStage* __restrict__ stage, int32_t gr_step, const int32_t* __restrict__ perm, int32_t n_tasks,
+    int32_t ndocs, const GrExport* __restrict__ ex, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
+    int64_t* rec, uint32_t* flags, uint32_t lds_bytes) {
+  const int k = (int)blockIdx.x / n_tasks, t = (int)blockIdx.x % n_tasks;
+  const int doc = perm[k];
+  if (doc >= ndocs) return;
+  const GrExport e = ex[k];
+  if (!e.valid) return;  // not exported: dead, returned early (flagged for the CPU path) or no n-grams
+  DocCtx<WavePar> x;
+  x.prof = nullptr;
+  x.lds = lds_bytes ? (char*)g_lds_arena : nullptr;
+  x.lcap = lds_bytes;
+  x.lused = 0;
+  x.ucd = UcdView{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
+  x.pw = pw;
+  x.pw_n = pw_n;
+  x.ipw = pw ? pw + pw_n + 1 : nullptr;
+  const uint64_t region = (e.free_cap / (uint64_t)n_tasks) & ~255ull;
+  x.scr = e.free_base + (uint64_t)t * region;
+  x.cap = region;
+  x.used = 0;
+  x.flag = flags + doc;
+  const DevStep& ds = stage->steps[gr_step];
+  int64_t* r = rec + (int64_t)ds.rec_prefix * ndocs + (int64_t)doc * ds.width;
+  if (t < ds.n_dup) gr_dup_one_order(x, ds, t, e, r);
+  else if (t < ds.n_dup + ds.n_top) gr_top_one_order(x, ds, t - ds.n_dup, e, r);
   if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
 }
 
@@ -1110,7 +1146,7 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
                      const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                      const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
                      uint32_t lds_bytes, uint64_t* prof, int32_t waves, int32_t nblocks, const uint8_t* dead,
-                     uint32_t* line_stats) {
+                     uint32_t* line_stats, void* gr_export) {
   if (ndocs <= 0) return 0;
   if (nblocks <= 0) nblocks = ndocs;  // grid: docs perm[0 .. nblocks)
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
@@ -1121,7 +1157,26 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64), lds_bytes, stream, (const DevPlan*)plan,
                      (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, flags,
-                     lds_bytes, prof, dead, line_stats);
+                     lds_bytes, prof, dead, line_stats, (GrExport*)gr_export);
+  return (int)hipGetLastError();
+}
+
+// Wave documents in split mode (tb_stage_analyze with gr_export): n_docs export slots, n_tasks =
+// the GopherRepetition step's duplicated + top n-gram orders.
+int tb_gr_split_wave(hipStream_t stream, const void* stage, int32_t gr_step, const int32_t* perm, int32_t n_docs,
+                     int32_t n_tasks, int32_t ndocs, const void* gr_export, const uint64_t* pw, uint32_t pw_n,
+                     const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
+                     uint32_t* flags, uint32_t lds_bytes) {
+  if (n_docs <= 0 || n_tasks <= 0) return 0;
+  if (!perm || !gr_export || gr_step < 0 || gr_step >= kMaxStageSteps || n_tasks > 2 * kMaxNgramEntries ||
+      lds_bytes > kMaxLdsPerDoc)
+    return (int)hipErrorInvalidValue;
+  DevTables t{s1, s2, l1, l2};
+  if (lds_bytes > 65536)
+    (void)hipFuncSetAttribute((const void*)k_gr_split_wave, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  hipLaunchKernelGGL(k_gr_split_wave, dim3((uint32_t)n_docs * (uint32_t)n_tasks), dim3(64), lds_bytes, stream,
+                     (const DevStage*)stage, gr_step, perm, n_tasks, ndocs, (const GrExport*)gr_export, pw, pw_n, t, rec,
+                     flags, lds_bytes);
   return (int)hipGetLastError();
 }
 
@@ -1340,7 +1395,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 
 int tb_phase_slots() { return kPhaseSlots; }
 
-int tb_abi_version() { return 15; }
+int tb_abi_version() { return 16; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

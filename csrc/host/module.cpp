@@ -18,7 +18,6 @@
 #include "html.h"
 #include "html_entities.inc"
 #include "json.h"
-#include "parquet_pages.h"
 #include "pipeline.h"
 #include "devplan_build.h"
 #include "rustfmt.h"
@@ -866,23 +865,6 @@ PYBIND11_MODULE(_tbhost, m) {
   }, py::arg("steps"), py::arg("idx"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8,
      py::arg("lid") = nullptr, py::arg("lds_bytes") = 0, py::arg("dead") = py::none(),
      py::arg("weak_keys") = false, py::arg("line_stats") = py::none());
-  m.def("parquet_pages", [](py::array_t<uint8_t, py::array::c_style> chunk) {
-    std::vector<PqPageInfo> pg;
-    {
-      py::gil_scoped_release nogil;
-      pg = parquet_pages(chunk.data(), (size_t)chunk.size());
-    }
-    py::array_t<int64_t> out({(py::ssize_t)pg.size(), (py::ssize_t)11});
-    auto o = out.mutable_unchecked<2>();
-    for (size_t i = 0; i < pg.size(); ++i) {
-      const PqPageInfo& q = pg[i];
-      const int64_t row[11] = {q.type, q.data_off, q.compressed_size, q.uncompressed_size, q.num_values,
-                               q.encoding, q.def_encoding, q.num_nulls, q.def_len, q.rep_len, q.v2_compressed};
-      for (int k = 0; k < 11; ++k) o((py::ssize_t)i, k) = row[k];
-    }
-    return out;
-  }, "Page directory of a Parquet column chunk: [pages, 11] int64 (type, data_off, compressed, "
-     "uncompressed, num_values, encoding, def_encoding, num_nulls, def_len, rep_len, v2_compressed)");
   m.def("line_stats_words", [](py::array_t<int64_t, py::array::c_style> off) {
     return line_stats_buffer_words(off.data(), (int64_t)off.size() - 1);
   }, "u32 words of a batch's C4 line export buffer (docproc.h line_stats_base)");

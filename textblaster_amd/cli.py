@@ -148,9 +148,6 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("--badwords-dir", default=None, help="dir holding the C4 bad-words lists (<lang> files)")
         p.add_argument("--html-decode", choices=("cpu", "gpu"), default="cpu",
                        help="decode HTML entities of the input text on the host (default) or the GPU")
-        p.add_argument("--parquet-decode", choices=("cpu", "gpu", "auto"), default="cpu",
-                       help="decode the input text column with pyarrow (cpu) or on the GPU (Snappy, levels, "
-                            "PLAIN/dictionary values; auto: on GPU ranks)")
         p.add_argument("--log-dir", default="./log")
 
     w = sub.add_parser("worker", help="validate a config, or process task JSON lines from stdin")
@@ -234,7 +231,7 @@ def run_cmd(args, argv: List[str]) -> int:
         backend=backend, segmentation=args.segmentation, unit_rows=args.unit_rows, threads=args.threads,
         work_dir=args.work_dir, resume=args.resume, checkpoint=args.checkpoint, keep_parts=args.keep_parts,
         compression=args.compression, tokenizer_dir=args.tokenizer_dir, badwords_dir=args.badwords_dir,
-        html_decode=args.html_decode, parquet_decode=args.parquet_decode, metrics_port=args.metrics_port, tokenizer_file=args.tokenizer_file, fault_inject=args.fault_inject)
+        html_decode=args.html_decode, metrics_port=args.metrics_port, tokenizer_file=args.tokenizer_file, fault_inject=args.fault_inject)
     try:
         stats = run(rc, ctx)
     except RankFailure as e:

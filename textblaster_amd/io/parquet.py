@@ -145,15 +145,12 @@ class DocBatch:
 class ParquetReader:
     """reference parquet_reader.rs:18-251"""
 
-    def __init__(self, config: ParquetInputConfig, html_threads: int = 8, html_decoder=None, text_decoder=None):
+    def __init__(self, config: ParquetInputConfig, html_threads: int = 8, html_decoder=None):
         # like the reference, construction does not touch the file; errors surface on first use
         self.config = config
         self.html_threads = html_threads
         # optional device decoder (ops.html.HtmlDecoder, K17); default: the host C++ decoder
         self.html_decoder = html_decoder
-        # optional device decoder of the text column (ops.parquet_gpu.GpuTextColumn); row groups it
-        # cannot take are read with pyarrow
-        self.text_decoder = text_decoder
         self._pf_obj = None
 
     @property
@@ -203,23 +200,9 @@ class ParquetReader:
         return [md.row_group(i).num_rows for i in range(md.num_row_groups)]
 
     def read_row_group(self, rg: int, pf: Optional[pq.ParquetFile] = None, use_threads: bool = True) -> pa.Table:
-        """The reader's columns of row group ``rg``; the text column comes from the device decoder
-        when one is set and takes the row group."""
+        """The reader's columns of row group ``rg``."""
         pf = pf if pf is not None else self._pf
-        dec = self.text_decoder.read(rg) if self.text_decoder is not None else None
-        if dec is None:
-            return pf.read_row_group(rg, columns=self.columns, use_threads=use_threads)
-        data, off, valid = dec
-        tcol = self.config.text_column
-        rest = [c for c in self.columns if c != tcol]
-        others = pf.read_row_group(rg, columns=rest, use_threads=use_threads)
-        n = len(off) - 1
-        nulls = int(n - int(valid.sum()))
-        vbuf = pa.py_buffer(np.packbits(valid, bitorder="little")) if nulls else None
-        text = pa.Array.from_buffers(pa.large_string(), n, [vbuf, pa.py_buffer(off), pa.py_buffer(data)],
-                                     null_count=nulls)
-        arrays = [text if c == tcol else others.column(c) for c in self.columns]
-        return pa.Table.from_arrays(arrays, names=list(self.columns))
+        return pf.read_row_group(rg, columns=self.columns, use_threads=use_threads)
 
     # -- batched engine path ------------------------------------------------------------------
     def iter_batches(self, batch_rows: int = 65536, row_groups: Optional[Sequence[int]] = None

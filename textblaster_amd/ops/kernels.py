@@ -22,11 +22,12 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32, _P,
-                         _P],
+                         _P, _P],
+    "tb_gr_split_wave": [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32],
     "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _P, _P],
     "tb_stage_analyze_blk": [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P,
                              _U32, _P, _P, _P, _I32, _U32, _I32, _P, _P, _I32],
@@ -52,12 +53,6 @@ _SIGS = {
     "tb_bpe_count": [_P, _P, _P, _P, _P, _I32, _P],
     "tb_sizeof_bpe": [],
     "tb_abi_version": [],
-    # Parquet text-column decoding (csrc/hip/parquet.hip)
-    "tb_sizeof_pq_page": [],
-    "tb_pq_decompress": [_P, _P, _P, _I32, _P, _P],
-    "tb_pq_dict": [_P, _P, _I32, _P, _P, _P, _P],
-    "tb_pq_values": [_P, _P, _P, _I32, _P, _P, _P, _I32, _P, _P, _P, _I64, _P],
-    "tb_pq_gather": [_P, _P, _P, _P, _I64, _P],
     # native runtime layer (csrc/hip/runtime.hip)
     "tbrt_device_count": [_P], "tbrt_set_device": [_I32], "tbrt_get_device": [_P], "tbrt_device_sync": [],
     "tbrt_mem_info": [_P, _P], "tbrt_malloc": [_P, _SZ], "tbrt_free": [_P], "tbrt_host_alloc": [_P, _SZ],
@@ -172,16 +167,32 @@ class Kernels:
         return self._pw, self._pw_n
 
     def stage_analyze(self, plan, stage, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, flags,
-                      lds_bytes=0, prof=None, waves=0, nblocks=0, dead=None, line_stats=None):
+                      lds_bytes=0, prof=None, waves=0, nblocks=0, dead=None, line_stats=None, gr_export=None):
         """k_stage_analyze_w4; ``line_stats`` (uint32, >= 4 * (total bytes / 8 + 16 ndocs) + 16): the
-        C4 line export (docproc.h StageOut::line_stats), document d at 4 * (off[d] / 8 + 16 d)."""
+        C4 line export (docproc.h StageOut::line_stats), document d at 4 * (off[d] / 8 + 16 d).
+        ``gr_export`` (zeroed, >= nblocks descriptors): split mode, every launched document exports
+        its word arrays and gr_split_wave finishes its n-gram orders."""
         t = self.tabs
+        if gr_export is not None and gr_export.nbytes < max(nblocks, 0) * self.sizeof_gr_export:
+            raise DeviceError("stage_analyze: export buffer too small")
         rc = self.lib.tb_stage_analyze(
             self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs,
             scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
             t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof), waves, nblocks,
-            _ptr(dead), _ptr(line_stats))
+            _ptr(dead), _ptr(line_stats), _ptr(gr_export))
         _check(rc, "tb_stage_analyze")
+
+    def gr_split_wave(self, stage, gr_step, perm, n_docs, n_tasks, ndocs, gr_export, pw, pw_n, rec, flags, lds_bytes):
+        """k_gr_split_wave: one wave per (wave document, n-gram order) over the descriptors
+        stage_analyze exported; n_tasks = the GopherRepetition step's duplicated + top orders."""
+        if gr_export.nbytes < n_docs * self.sizeof_gr_export or perm.numel() < n_docs:
+            raise DeviceError("gr_split_wave: operand shapes")
+        t = self.tabs
+        rc = self.lib.tb_gr_split_wave(self.stream(), stage.data_ptr(), gr_step, perm.data_ptr(), n_docs, n_tasks,
+                                       ndocs, gr_export.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(),
+                                       t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(),
+                                       flags.data_ptr(), lds_bytes)
+        _check(rc, "tb_gr_split_wave")
 
     def stage_analyze_blk(self, plan, stage, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n,
                           rec, flags, lds_bytes=0, prof=None, dead=None, gr_export=None, n_split=0, split_bytes=0,

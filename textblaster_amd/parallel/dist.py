@@ -176,6 +176,10 @@ def init_from_env(backend: str = "nccl", force_pg: Optional[bool] = None) -> Dis
     pg_backend = os.environ.get("TB_DIST_BACKEND") or ("gloo" if shared else backend)
     if pg_backend not in ("nccl", "gloo"):
         raise ValueError(f"TB_DIST_BACKEND must be nccl or gloo, not {pg_backend!r}")
+    if shared and pg_backend == "nccl" and world > 1:
+        # RCCL needs one GPU per rank: with every rank on GPU 0 the communicator cannot form
+        raise ValueError("TB_SHARED_GPU=1 puts every rank on GPU 0; use TB_DIST_BACKEND=gloo (the default "
+                         "with TB_SHARED_GPU), an RCCL group needs one GPU per rank")
     if backend == "nccl":
         ctx.device = f"cuda:{0 if shared else local}"
     if world > 1 or force_pg:

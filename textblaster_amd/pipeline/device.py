@@ -580,6 +580,12 @@ class DeviceRunner:
                 if st.n_dup + st.n_top > 0:
                     self.gr_split[si] = (grs[0], st.n_dup + st.n_top + 2)
         self.line_stats_stage = line_stats_stages(plan, self.stage_layout)
+        # wave documents finish their n-gram orders in one wave per (document, order)
+        # (k_gr_split_wave, LDS slice TB_LDS_BYTES_SPLIT); TB_WAVE_SPLIT=0 keeps them in the stage
+        self.wave_split = os.environ.get("TB_WAVE_SPLIT", "1") not in ("", "0")
+        self.lds_bytes_split = int(os.environ.get("TB_LDS_BYTES_SPLIT", "6144"))
+        if not 0 <= self.lds_bytes_split <= 65536:
+            raise DeviceError("TB_LDS_BYTES_SPLIT must be in [0, 65536]")
         if not 0 <= self.lds_bytes_blk <= 131072:
             # the workgroup kernels also hold static LDS (cross-wave exchange buffers): a 160 KB
             # dynamic slice does not fit the CU's 160 KB and the launch fails with
@@ -865,6 +871,7 @@ class DeviceRunner:
         ready = {0: self._record(main)}
         tails = []
         c4_scratch = None
+        pre_v0 = None  # (descriptors, n_pre) of the version-0 pre-pass
         for ver in range(self.plan.n_versions):
             vb, vo, vlen = versions[ver]
             main.wait_event(ready[ver])
@@ -919,9 +926,11 @@ class DeviceRunner:
                     # the split export slots are indexed by launch position
                     esz = self.k.sizeof_gr_export
                     with rt.stream(slot.s_blk), self._ktimed(keep, f"stage{s}_blk"):
-                        # (the original text only: the host knows no lengths of rewritten versions)
-                        pre, n_pre = (self._pre_decode(vb, vo, d_perm, lens[perm[:n_long]], skip, keep) if ver == 0
-                                      else (None, 0))
+                        # (the original text only: the host knows no lengths of rewritten versions); once
+                        # per batch: every stage reading version 0 reuses it (read-only, same stream)
+                        if ver == 0 and pre_v0 is None:
+                            pre_v0 = self._pre_decode(vb, vo, d_perm, lens[perm[:n_long]], skip, keep)
+                        pre, n_pre = pre_v0 if ver == 0 else (None, 0)
                         # launch positions [0, n_pre): the pre-pass kernel instantiation, the rest the common one
                         segs = ((0, n_pre, 512, True), (n_pre, n_long, 512, False))
                         for a0, a1, thr, with_pre in segs:
@@ -950,10 +959,21 @@ class DeviceRunner:
                         ev_lid = self._record(slot.s_lid)
                         keep.append(ev_lid)
                 if n_long < ndocs:
+                    nw = ndocs - n_long
+                    gxw = None
+                    if s in self.gr_split and self.wave_split:
+                        # split mode: the wave documents' n-gram orders run one wave per (document,
+                        # order) after the stage kernel (k_gr_split_wave)
+                        gxw = rt.zeros(nw * self.k.sizeof_gr_export, np.uint8)
+                        keep.append(gxw)
                     with self._ktimed(keep, f"stage{s}"):
                         self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,
                                              scratch, d_soff[n_long:], pw, pw_n, rec, flags,
-                                             self.lds_bytes, prof, self.stage_waves, ndocs - n_long, skip, ls_out)
+                                             self.lds_bytes, prof, self.stage_waves, nw, skip, ls_out, gxw)
+                        if gxw is not None:
+                            gr_pos, n_tasks = self.gr_split[s]
+                            self.k.gr_split_wave(self.stage_ts[s], gr_pos, d_perm[n_long:], nw, n_tasks - 2, ndocs,
+                                                 gxw, pw, pw_n, rec, flags, self.lds_bytes_split)
                 if ev_lid is not None:
                     main.wait_event(ev_lid)
                 if ev_blk is not None:
@@ -1137,6 +1157,12 @@ class EmulatedRunner:
             plan, self.stage_layout, steps_native, gating, os.environ.get("TB_LID_GATE", "1") not in ("", "0"))
         self.bw_dead_max = bw_dead_max(plan, self.passes, self.pass_of_step)
         self.line_stats_stage = line_stats_stages(plan, self.stage_layout)
+        # wave documents finish their n-gram orders in one wave per (document, order)
+        # (k_gr_split_wave, LDS slice TB_LDS_BYTES_SPLIT); TB_WAVE_SPLIT=0 keeps them in the stage
+        self.wave_split = os.environ.get("TB_WAVE_SPLIT", "1") not in ("", "0")
+        self.lds_bytes_split = int(os.environ.get("TB_LDS_BYTES_SPLIT", "6144"))
+        if not 0 <= self.lds_bytes_split <= 65536:
+            raise DeviceError("TB_LDS_BYTES_SPLIT must be in [0, 65536]")
         # test hook: additionally mark every k-th document dead after the first pass (a wrong
         # device gate), to exercise the resolver's recovery path
         self.gate_corrupt = gate_corrupt

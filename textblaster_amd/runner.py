@@ -77,8 +77,6 @@ class RunConfig:
     tokenizer_dir: Optional[str] = None
     badwords_dir: Optional[str] = None
     html_decode: str = "cpu"           # input HTML entity decoding: cpu (C++ host) | gpu (K17 kernels)
-    parquet_decode: str = "cpu"        # text column decoding: cpu (pyarrow) | gpu (csrc/hip/parquet.hip) |
-                                       # auto (gpu on a GPU rank); see profiles/r4_parquet
     metrics_port: Optional[int] = None
     progress_interval: float = 1.0
     tokenizer_file: Optional[str] = None
@@ -550,18 +548,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
         html_dec = HtmlDecoder(dev)
     elif rc.html_decode != "cpu":
         raise PipelineError(f"unknown html decode backend {rc.html_decode!r} (cpu | gpu)")
-    text_dec = None
-    if rc.parquet_decode not in ("cpu", "gpu", "auto"):
-        raise PipelineError(f"unknown parquet decode backend {rc.parquet_decode!r} (cpu | gpu | auto)")
-    if rc.parquet_decode == "gpu" or (rc.parquet_decode == "auto" and rc.backend == "cuda"):
-        dev = ctx.device if ctx.device is not None else ("cuda" if rc.backend == "cuda" else None)
-        if dev is None:
-            raise PipelineError("--parquet-decode gpu needs a GPU rank")
-        from .ops.parquet_gpu import GpuTextColumn
-
-        text_dec = GpuTextColumn(rc.input_file, rc.text_column, dev)
-    reader = ParquetReader(ParquetInputConfig(rc.input_file, rc.text_column, rc.id_column), html_decoder=html_dec,
-                           text_decoder=text_dec)
+    reader = ParquetReader(ParquetInputConfig(rc.input_file, rc.text_column, rc.id_column), html_decoder=html_dec)
     units = plan_units(reader, rc.unit_rows)
     use_parts = world > 1 or rc.checkpoint or rc.resume
     work_dir = rc.work_dir or (rc.output_file + ".work")

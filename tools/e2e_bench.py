@@ -82,10 +82,7 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "e2e"))
     ap.add_argument("--timeline", action="store_true", help="record the host timeline (TB_TIMELINE) per backend")
     ap.add_argument("--html-decode", default="cpu")
-    ap.add_argument("--parquet-decode", action="append", default=None,
-                    help="text column decoding (cpu | gpu | auto); repeat to run several")
     ap.add_argument("--keep-input", action="store_true")
-    ap.add_argument("--decode-only", action="store_true", help="time the text-column decoders alone")
     ap.add_argument("--repeat", type=int, default=1, help="runs per backend (all reported; the median last)")
     ap.add_argument("--cli", action="store_true",
                     help="also run the CLI (`python -m textblaster_amd.cli run --backend cuda`) as a child process: "
@@ -101,42 +98,18 @@ def main():
     from textblaster_amd.runner import RunConfig, run
     from textblaster_amd.utils import tracing
 
-    if args.decode_only:
-        # the text column of every row group through the device decoder and through pyarrow
-        # (one thread each): wall and thread-CPU seconds per stage
-        import pyarrow.parquet as pq
-
-        from textblaster_amd.ops.parquet_gpu import GpuTextColumn
-
-        dec = GpuTextColumn(inp, "text", 0)
-        pf = pq.ParquetFile(inp)
-        for rep in range(2):
-            dec.timing.clear()
-            t0, c0 = time.perf_counter(), time.thread_time()
-            for rg in range(pf.num_row_groups):
-                dec.read(rg)
-            g = (time.perf_counter() - t0, time.thread_time() - c0)
-            t0, c0 = time.perf_counter(), time.thread_time()
-            for rg in range(pf.num_row_groups):
-                pf.read_row_group(rg, columns=["text"], use_threads=False)
-            c = (time.perf_counter() - t0, time.thread_time() - c0)
-            print(json.dumps({"decode_only": rep, "row_groups": pf.num_row_groups, "gpu_wall_cpu": g,
-                              "pyarrow_wall_cpu": c, "gpu_stages": dec.timing, "stats": dec.stats}), flush=True)
-        return
-
-    runs = [(b, pd) for b in (args.backend or ["cuda"]) for pd in (args.parquet_decode or ["auto"])
-            for _ in range(args.repeat)]
+    runs = [b for b in (args.backend or ["cuda"]) for _ in range(args.repeat)]
     rates = {}
-    for backend, pdec in runs:
+    for backend in runs:
         o = os.path.join(args.out, f"{backend}.out.parquet")
         e = os.path.join(args.out, f"{backend}.excluded.parquet")
         tl = os.path.join(args.out, f"timeline_{backend}.json") if args.timeline else None
         tracing.record_timeline(tl)
         cpu0 = thread_cpu()
         st = run(RunConfig(inp, o, e, args.config, backend=backend, unit_rows=args.unit_rows,
-                           html_decode=args.html_decode, parquet_decode=pdec))
+                           html_decode=args.html_decode))
         cpu = cpu_by_name(cpu0, thread_cpu())
-        line = {"backend": backend, "parquet_decode": pdec, "docs": st.docs, "kept": st.kept, "excluded": st.excluded, "errors": st.errors,
+        line = {"backend": backend, "docs": st.docs, "kept": st.kept, "excluded": st.excluded, "errors": st.errors,
                 "seconds": round(st.seconds, 3), "docs_per_sec": round(st.docs_per_sec, 1),
                 "step_filtered": st.step_filtered, "delegated": st.delegated,
                 "phase_seconds": {k: round(v, 3) for k, v in st.phase_seconds.items() if not k.startswith("cpu_")},
@@ -146,7 +119,7 @@ def main():
                 "cpu_us_per_doc": round(1e6 * st.phase_seconds.get("cpu_total", 0.0) / max(st.docs, 1), 3),
                 "cpu_seconds_by_os_thread": cpu}
         print(json.dumps(line), flush=True)
-        rates.setdefault(f"{backend}/{pdec}", []).append(line["docs_per_sec"])
+        rates.setdefault(backend, []).append(line["docs_per_sec"])
         if tl:
             sys.path.insert(0, os.path.join(ROOT, "tools"))
             from timeline_summary import summarise

@@ -144,7 +144,8 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("--tokenizer-dir", default=None, help="local dir holding <name>/tokenizer.json")
         p.add_argument("--tokenizer-file", default=None, help="tokenizer.json used by every TokenCounter step")
         p.add_argument("--langid-model", default=None, help="language-id weights (.npz); default: bundled model")
-        p.add_argument("--fault-inject", default=None, help="debug: kernel@N or oom@N (fail the N-th batch once), rank@N[:R] (rank R dies after N units)")
+        p.add_argument("--fault-inject", default=None, help="debug: kernel@N or oom@N (fail the N-th batch once), rank@N[:R] (rank R dies after N units), "
+                            "slow@SECONDS[:R] (rank R sleeps after every unit)")
         p.add_argument("--badwords-dir", default=None, help="dir holding the C4 bad-words lists (<lang> files)")
         p.add_argument("--html-decode", choices=("cpu", "gpu"), default="cpu",
                        help="decode HTML entities of the input text on the host (default) or the GPU")
@@ -262,6 +263,8 @@ def run_cmd(args, argv: List[str]) -> int:
                 lines.append(f"      filtered by step {i} {n}: {stats.step_filtered[i]}")
         lines += [
             f"  Ranks: {ctx.world_size} ({backend}), units: {stats.units} (+{stats.units_skipped} resumed)",
+            f"  Units per rank: {stats.rank_units} | busy seconds per rank: "
+            f"{[round(b, 3) for b in stats.rank_busy]}",
             f"  Time: {stats.seconds:.2f} s | Speed: {stats.docs_per_sec:.2f} docs/sec",
             f"  Output File: {args.output_file}",
             f"  Excluded File: {args.excluded_file}",

@@ -2,9 +2,10 @@
 ``nccl`` backend (= RCCL over xGMI on ROCm), ``gloo`` for CPU-only runs and tests.
 
 The reference scales with competing consumers on a RabbitMQ queue (utils/common.rs,
-worker_logic.rs:241-283). Here document data never crosses GPUs: each rank owns a
-deterministic, contiguous shard of the input row groups (balanced by byte size) and the only
-collectives are tiny counter vectors:
+worker_logic.rs:241-283). Here document data never crosses GPUs: ranks pull row groups from a
+shared atomic cursor (``DistContext.claim``, the process group's store), so a rank that is slower
+(longer documents, a busier GPU) simply takes fewer, and the only collectives are tiny counter
+vectors:
 
   AR1  all_reduce(SUM) of per-step/per-reason document counters (int64, < 1 KB)
   AG1  all_gather of per-rank kept/excluded counts (part-file bookkeeping for the merge)
@@ -101,6 +102,28 @@ class DistContext:
         out = [torch.zeros_like(t) for _ in range(self.world_size)]
         td.all_gather(out, t)
         return np.stack([o.cpu().numpy() for o in out])
+
+    def claim(self, key: str, n: int = 1) -> int:
+        """Atomically takes ``n`` items of the shared counter ``key``; returns the index of the first
+        one (every rank sees each index exactly once). Over a process group this is the group's
+        key-value store (``store.add``: the rendezvous TCPStore under torchrun); without one a
+        process-local counter. The competing-consumer equivalent of the reference's work queue
+        (utils/common.rs:91-94 basic_qos, worker_logic.rs:241-283)."""
+        n = int(n)
+        if not self.initialized:
+            cnt = self.__dict__.setdefault("_claims", {})
+            first = cnt.get(key, 0)
+            cnt[key] = first + n
+            return first
+        _, td = self._torch()
+        store = td.distributed_c10d._get_default_store()
+        return int(store.add(key, n)) - n
+
+    def next_key(self, prefix: str) -> str:
+        """A key unique to this call site's n-th use (all ranks make the same sequence of calls)."""
+        seq = self.__dict__.get("_key_seq", 0)
+        self.__dict__["_key_seq"] = seq + 1
+        return f"tb/{prefix}/{seq}"
 
     def destroy(self) -> None:
         if self.initialized:

@@ -4,8 +4,14 @@ bin/producer.rs, bin/worker.rs).
 
 Work decomposition
   The input is cut into *units*: row-group slices of at most ``unit_rows`` rows. Units are the
-  scheduling, sharding and checkpoint granularity. Rank ``r`` of ``W`` owns a contiguous range
-  of units balanced by bytes (``parallel.dist.shard_ranges``), so documents never cross GPUs.
+  output and checkpoint granularity; the units of one row group form a *group*, the scheduling
+  granularity (a row group is decoded once, by one rank). Ranks pull groups from a shared atomic
+  cursor (``DistContext.claim``: ``store.add`` on the process group's store), the
+  competing-consumer equivalent of the reference's work queue (worker_logic.rs:241-283,
+  utils/common.rs:91-94 ``basic_qos``): a rank whose documents cost more per byte (very long
+  documents run at a fraction of the short-document rate on the GPU) or whose GPU is busier
+  takes fewer groups, so the ranks finish together. ``TB_SCHEDULE=static`` restores contiguous
+  ranges balanced by bytes (``parallel.dist.shard_ranges``). Documents never cross GPUs.
 
 Per rank, four stages overlap (bounded queues, the heavy native calls release the GIL):
   reader thread   Parquet decode + HTML-entity decode + packing    (unit k+2)
@@ -18,10 +24,10 @@ Outputs
   * otherwise every unit writes ``<work_dir>/parts/u<unit>.{kept,excluded}.parquet`` and appends a
     line to ``<work_dir>/manifest.rank<r>.jsonl`` once both files are closed. ``resume=True``
     skips units already in a manifest. At the end the parts are concatenated in unit order
-    (row order = input order) into the two final files *without re-encoding*: every rank
-    copies its own parts' column-chunk bytes at an offset from an all-gather of sizes (AG1),
-    rank 0 writes the rewritten footers (io/pqconcat.py); the work dir is removed unless
-    ``keep_parts``.
+    (row order = input order) into the two final files *without re-encoding*: rank r copies the
+    parts of a contiguous unit range (whoever processed them) at an offset from an all-gather
+    of sizes (AG1), rank 0 writes the rewritten footers (io/pqconcat.py); the work dir is
+    removed unless ``keep_parts``.
   Counters (docs, kept, excluded, errors, per-step filtered) are all-reduced while the job
   runs by a heartbeat thread (parallel/heartbeat.py; it also turns a dead peer into a
   non-zero exit) and once more over RCCL at the end (AR1); rank 0 serves the global view on
@@ -82,7 +88,9 @@ class RunConfig:
     tokenizer_file: Optional[str] = None
     read_threads: int = int(os.environ.get("TB_READ_THREADS", "8"))   # row groups decoded concurrently
     write_threads: int = int(os.environ.get("TB_WRITE_THREADS", "4"))  # units encoded concurrently
-    fault_inject: Optional[str] = None   # debug: "kernel@N" / "oom@N" (N = 1-based batch)
+    fault_inject: Optional[str] = None   # debug: "kernel@N" / "oom@N" (N = 1-based batch), "rank@N[:R]",
+                                         # "slow@SECONDS[:R]" (rank R sleeps after every unit)
+    schedule: str = os.environ.get("TB_SCHEDULE", "dynamic")  # dynamic (shared cursor) | static (ranges)
 
 
 @dataclasses.dataclass
@@ -98,6 +106,8 @@ class RunStats:
     delegated: int = 0
     step_filtered: List[int] = dataclasses.field(default_factory=list)
     phase_seconds: Dict[str, float] = dataclasses.field(default_factory=dict)  # rank 0's own view
+    rank_units: List[int] = dataclasses.field(default_factory=list)  # units processed per rank
+    rank_busy: List[float] = dataclasses.field(default_factory=list)  # main-loop seconds per rank
 
     @property
     def docs_per_sec(self) -> float:
@@ -392,18 +402,57 @@ class _Prefetcher:
         self.t.join(timeout=60)
 
 
-def _read_units(reader: ParquetReader, units: List[Unit], nthreads: int, timer: _UnitReader):
-    """Yields (unit, DocBatch) in order. Row groups are decoded by up to ``nthreads`` worker
-    threads at once (Parquet decompression + HTML-entity decoding dominate the input side);
-    each row group is read once and sliced into its units."""
-    import concurrent.futures as cf
-
+def unit_groups(units: List[Unit]) -> List[List[Unit]]:
+    """Consecutive units of one row group (the scheduling granularity)."""
     groups: List[List[Unit]] = []
     for u in units:
         if groups and groups[-1][0].row_group == u.row_group:
             groups[-1].append(u)
         else:
             groups.append([u])
+    return groups
+
+
+class _ClaimGate:
+    """Bounds the groups a rank holds (claimed, not yet handed to the engine) to ``ahead``: the
+    reader thread takes a token before each claim, the main loop returns it when it passes a
+    group's last unit to the engine (whose own in-flight depth is a few batches).
+    Without it the reader's prefetch would claim groups a busy rank cannot start for a while
+    (the reference's ``basic_qos(prefetch_count)``, utils/common.rs:91-94)."""
+
+    def __init__(self, ahead: int):
+        self.sem = threading.Semaphore(max(1, ahead))
+        self.last: set = set()
+        self.closed = False
+
+    def done(self, unit_index: int) -> None:
+        if unit_index in self.last:
+            self.last.discard(unit_index)
+            self.sem.release()
+
+
+def _claimed(ctx: DistContext, key: str, groups: List[List[Unit]], claimed: List[int],
+             gate: _ClaimGate) -> Iterator[List[Unit]]:
+    """The groups this rank takes from the shared cursor ``key``, one claim each, lazily: a claim
+    is made only when the rank holds fewer than ``gate``'s bound of unprocessed groups."""
+    while True:
+        while not gate.sem.acquire(timeout=0.1):
+            if gate.closed:
+                return
+        i = ctx.claim(key, 1)
+        if i >= len(groups):
+            return
+        claimed.append(i)
+        gate.last.add(groups[i][-1].index)
+        yield groups[i]
+
+
+def _read_units(reader: ParquetReader, groups, nthreads: int, timer: _UnitReader):
+    """Yields (unit, DocBatch) of the row-group ``groups`` (an iterable, consumed lazily) in
+    order. Row groups are decoded by up to ``nthreads`` worker threads at once (Parquet
+    decompression + HTML-entity decoding dominate the input side); each row group is read once
+    and sliced into its units."""
+    import concurrent.futures as cf
 
     def load(group: List[Unit]):
         r = _UnitReader(reader, own_file=nthreads > 1)
@@ -538,6 +587,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     t_start = time.perf_counter()
     ru_start = resource.getrusage(resource.RUSAGE_SELF)
     rank_fault = _parse_rank_fault(rc.fault_inject, world)
+    slow = _parse_slow(rc.fault_inject, world)
     html_dec = None
     if rc.html_decode == "gpu":
         dev = ctx.device if ctx.device is not None else ("cuda" if rc.backend == "cuda" else None)
@@ -576,11 +626,30 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
         ctx.barrier()
         if rc.resume:
             done = read_manifests(work_dir)
+    if rc.schedule not in ("dynamic", "static"):
+        raise PipelineError(f"unknown schedule {rc.schedule!r} (dynamic | static)")
+    # merge ranges: contiguous by unit index, balanced by bytes (whoever processed the units)
     shard = shard_ranges([u.est_bytes for u in units], world)[rank]
     mine = [units[i] for i in shard]
-    todo = [u for u in mine if u.index not in done]
+    claimed: List[int] = []
+    # groups a rank may hold ahead of its main loop: enough for the decode threads and the
+    # engine's batches in flight
+    gate = _ClaimGate(int(os.environ.get("TB_CLAIM_AHEAD", str(rc.read_threads + 3))))
+    if rc.schedule == "static":
+        groups_it = unit_groups([u for u in mine if u.index not in done])
+        accounted = mine          # this rank reports the resumed units of its own range
+    else:
+        # every rank builds the same group list (same manifests), then pulls from one cursor. With
+        # too few row groups to spread (< 4 per rank) every unit is its own claim: ranks then may
+        # decode the same row group, but all of them get work
+        todo_all = [u for u in units if u.index not in done]
+        groups_all = unit_groups(todo_all)
+        if world > 1 and len(groups_all) < 4 * world:
+            groups_all = [[u] for u in todo_all]
+        groups_it = _claimed(ctx, ctx.next_key("units"), groups_all, claimed, gate)
+        accounted = units if rank == 0 else []
     local = RunStats(step_filtered=[0] * nsteps)
-    for u in mine:
+    for u in accounted:
         if u.index in done:
             rec = done[u.index]
             local.docs += rec["docs"]
@@ -596,7 +665,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
         metrics.setup_prometheus_metrics(rc.metrics_port)
     # input decoding starts now and overlaps the engine (HIP context, kernels, model) set-up
     ureader = _UnitReader(reader)
-    source = _Prefetcher(_read_units(reader, todo, rc.read_threads, ureader), depth=rc.read_threads + 2)
+    source = _Prefetcher(_read_units(reader, groups_it, rc.read_threads, ureader), depth=rc.read_threads + 2)
     try:
         if engine is None:
             backend = rc.backend
@@ -605,12 +674,12 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
                 engine = Engine(cfg, backend=backend, device=device, nthreads=rc.threads,
                                 segmentation=rc.segmentation, tokenizer_dir=rc.tokenizer_dir,
                                 badwords_dir=rc.badwords_dir, tokenizer_file=rc.tokenizer_file,
-                                fault_inject=None if rank_fault is not None else rc.fault_inject)
+                                fault_inject=None if (rank_fault is not None or slow is not None) else rc.fault_inject)
     except BaseException:
         source.close()
         raise
-    log.info("rank %d/%d: %d units (%d already done), backend=%s", rank, world, len(mine), len(mine) - len(todo),
-             engine.backend)
+    log.info("rank %d/%d: schedule=%s, %d units already done, backend=%s", rank, world, rc.schedule,
+             local.units_skipped, engine.backend)
 
     hb = Heartbeat(ctx, len(local.vector(nsteps)), interval=rc.progress_interval,
                    on_global=_publish_global if rank == 0 else None)
@@ -624,6 +693,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     def feed():
         for unit, batch in source:
             inflight.append((unit, batch))
+            gate.done(unit.index)  # handed to the engine (its own in-flight depth is bounded)
             yield batch.text[0], batch.text[1], batch.meta
 
     t_loop = time.perf_counter()
@@ -654,6 +724,8 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
             _update_metrics(cfg, res, batch, counts, step_counts, dt)
             hb.update(local.vector(nsteps))
             hb.check()
+            if slow is not None and slow[1] == rank:
+                time.sleep(slow[0])
             if rank_fault is not None and rank_fault[1] == rank and local.units == rank_fault[0]:
                 log.error("rank %d: injected rank failure after %d unit(s) (--fault-inject rank@...)", rank,
                           local.units)
@@ -666,8 +738,10 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
                          local.excluded, local.errors, speed)
                 last_report, last_docs = now, local.docs
     finally:
+        gate.closed = True
         source.close()
         writer.close()
+    busy = time.perf_counter() - t_loop  # this rank's own work (hb.finish waits for the others)
     hb.finish(local.vector(nsteps))
     phase = {"setup": setup_s, "read": ureader.seconds, "write": writer.seconds,
              "main_loop": time.perf_counter() - t_loop,
@@ -686,6 +760,9 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     skipped = int(ctx.all_reduce_sum([local.units_skipped])[0])
     stats = RunStats.from_vector(total_vec, elapsed_max, units_done, skipped)
     stats.phase_seconds = phase
+    per_rank = ctx.all_gather_counts([local.units, int(round(busy * 1e6))])
+    stats.rank_units = [int(x) for x in per_rank[:, 0]]
+    stats.rank_busy = [float(x) / 1e6 for x in per_rank[:, 1]]
     if use_parts:
         ctx.barrier()
         t_merge = time.perf_counter()
@@ -703,6 +780,18 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
 
 def _publish_global(v: np.ndarray) -> None:
     metrics.set_global_counts(int(v[0]), int(v[1]), int(v[2]), int(v[3]))
+
+
+def _parse_slow(spec: Optional[str], world: int) -> Optional[Tuple[float, int]]:
+    """``slow@SECONDS[:R]``: rank R (default: the last rank) sleeps SECONDS after every unit
+    (debug: a straggler, for the scheduling tests)."""
+    if not spec or not spec.startswith("slow@"):
+        return None
+    sec, _, r = spec[5:].partition(":")
+    try:
+        return float(sec), int(r) if r else world - 1
+    except ValueError:
+        raise PipelineError(f"bad fault injection spec {spec!r} (expected slow@SECONDS or slow@SECONDS:R)") from None
 
 
 def _parse_rank_fault(spec: Optional[str], world: int) -> Optional[Tuple[int, int]]:

@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--pool", type=int, default=16384, help="distinct synthetic docs per rank")
     ap.add_argument("--vocab", default="small", choices=["small", "zipf"],
                     help="synthetic vocabulary: ~130 words per language (default) or 60k-type Zipf lexicons")
+    ap.add_argument("--mixed-script", action="store_true",
+                    help="5%% of the documents carry a CJK / Thai snippet and 1%% are CJK (dictionary scripts)")
     ap.add_argument("--config", default=os.path.join(ROOT, "config", "bench_pipeline.yaml"))
     ap.add_argument("--tokenizer", default=None,
                     help="tokenizer.json for a TokenCounter step in --config ('synthetic': a GPT-2-format "
@@ -105,7 +107,8 @@ def main():
                  tokenizer_file=tok_file, badwords_dir=args.badwords_dir if has_bw else None)
 
     # synthetic corpus: a pool of distinct docs per rank, batches are fresh permutations of it
-    texts = synth.make_corpus(args.pool, args.mean_bytes, seed=1000 + rank, vocab=args.vocab)
+    texts = synth.make_corpus(args.pool, args.mean_bytes, seed=1000 + rank, vocab=args.vocab,
+                              mixed_script=args.mixed_script)
     if has_bw and args.badwords_rate > 0:
         texts = synth.inject_words(texts, os.path.join(args.badwords_dir, "en"), args.badwords_rate, seed=rank)
     enc = [t.encode("utf-8") for t in texts]
@@ -124,7 +127,7 @@ def main():
 
     batches = [make_batch() for _ in range(min(4, args.steps + args.warmup))]
     bytes_per_step = float(np.mean([len(b[0]) for b in batches]))
-    counters = np.zeros(4, dtype=np.int64)  # docs, kept, excluded, errors
+    counters = np.zeros(5, dtype=np.int64)  # docs, kept, excluded, errors, CPU-delegated
 
     def feed(k, start):
         for i in range(start, start + k):
@@ -138,6 +141,9 @@ def main():
     ctx.barrier()
     if args.backend == "cuda":
         torch.cuda.synchronize()
+    from textblaster_amd.utils import metrics
+
+    bpe_host0 = metrics.BPE_HOST_DOCS_TOTAL._value.get()
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     n_done = 0
@@ -148,7 +154,7 @@ def main():
     ar1s = collections.deque()
     for res in eng.process_many(feed(args.steps, args.warmup)):
         step = np.asarray([res.n_docs, res.n_kept, res.n_excluded, len(res.error_rows)], dtype=np.int64)
-        counters += step
+        counters += np.append(step, res.n_delegated)
         # AR1 once per step: the global counter vector (what rank 0's /metrics serves), reduced
         # over RCCL while the next steps run; the main thread (which also assembles outputs)
         # only waits once more than TB_AR1_WINDOW reductions are outstanding
@@ -172,6 +178,7 @@ def main():
     cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
     cpu_ms_step_max = ctx.all_reduce_max(1000.0 * cpu_s / args.steps)
     elapsed_max = ctx.all_reduce_max(elapsed)
+    bpe_host = int(ctx.all_reduce_sum([int(metrics.BPE_HOST_DOCS_TOTAL._value.get() - bpe_host0)])[0])
     totals = ctx.all_reduce_sum(counters)
     docs_total = int(totals[0])
     value = docs_total / elapsed_max
@@ -192,7 +199,8 @@ def main():
             # "int16"); the text filters themselves are integer / byte arithmetic
             "dtype": lid.dtype if lid is not None else "int",
             "data": f"synthetic CommonCrawl-shaped docs (log-normal ~{args.mean_bytes} B, 5 languages, "
-                    f"{'~130-word' if args.vocab == 'small' else '60k-type Zipf'} vocabularies), "
+                    f"{'~130-word' if args.vocab == 'small' else '60k-type Zipf'} vocabularies"
+                    f"{', 5% with a CJK/Thai snippet + 1% CJK' if args.mixed_script else ''}), "
                     f"{args.docs_per_step} docs/GPU/step",
             "config": {
                 "model": "+".join(s.type.replace("LanguageDetectionFilter", f"LanguageDetection({lid.description})"
@@ -211,6 +219,11 @@ def main():
             "kept": int(totals[1]),
             "excluded": int(totals[2]),
             "errors": int(totals[3]),
+            # documents the device sent to the CPU path (dictionary scripts that reach a segmentation
+            # step, hash collisions, scratch overflow) and TokenCounter documents counted by the host
+            # tokenizer, over the timed steps
+            "delegated": int(totals[4]),
+            "bpe_host_docs": bpe_host,
             "bytes_per_sec": round(bytes_per_step * world * args.steps / elapsed_max, 1),
             "last_step_timings": {k: round(v, 5) for k, v in res.timings.items()},
             # host seconds per phase averaged over the K timed steps (phases of consecutive

@@ -2281,8 +2281,17 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
   x.stamp(PH_DECODE);
   const uint32_t C = c.n;
   // Documents with dictionary-segmented scripts go to the ICU path (host): their records are
-  // recomputed there, so nothing else is analysed on the device.
+  // recomputed there, so nothing else is analysed on the device. The language record needs no
+  // segmentation and is exact for every script (the device computes it in its own kernel, and a
+  // document the language gate filters is not delegated), so the emulation still produces it.
   if (ndict) {
+    if constexpr (kWithLid) {
+      for (int s = 0; s < st.n_steps; ++s) {
+        const DevStep& ds = st.steps[s];
+        if (ds.kind == DK_LANGID && (lid.P || lid.E))
+          langid_record(x, b, n, lid, out.rec + (int64_t)ds.rec_prefix * out.ndocs + (int64_t)out.doc * ds.width);
+      }
+    }
     x.set_flag(DOC_NEEDS_CPU);
     return;
   }

@@ -220,6 +220,304 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_gr_dup_split(
   if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
 }
 
+// ---- n-gram orders of wave documents, one workgroup per document (k_gr_ngrams) ---------------
+// The stage kernel exports each wave document's word arrays (GrExport: canonical word ids, byte
+// prefix WL, concatenation hash prefixes K / PB). Here kNgWaves waves share one document: they
+// stage its arrays into LDS once (coalesced), then each wave takes whole orders (duplicated, then
+// top), one gram per lane at a time, and its table in the
+// wave's own LDS region; every LDS array comes from __shared__ declarations (ds_* instructions).
+// Records equal gr_dup_one_order / gr_top_one_order (the canonical id of a gram is the smallest
+// index of an equal gram however the table is probed). The host launches it over the shorter
+// wave documents of the length-sorted launch (the longer ones take one wave per (document, order),
+// k_gr_split_wave, whose tables use a dynamic LDS slice); a document with more words than the
+// workgroup's arrays hold (or byte prefixes past 16 bits) runs the generic per-order code
+// (gr_dup_one_order / gr_top_one_order) over its HBM scratch instead.
+constexpr int kNgWaves = 4;
+
+// LDS of one document's workgroup for documents of at most MAXW words: the staged word arrays and
+// one region per wave, the larger of the duplicated-order layout (u32 table, u16 ids and lengths,
+// seen / repeat bitmaps) and the top-order layout (u32 table, u16 ids, u32 counts)
+template <uint32_t MAXW>
+struct NgShared {
+  static_assert(MAXW % 64 == 0, "whole waves of grams");
+  static constexpr uint32_t kMaxW = MAXW;
+  static constexpr uint32_t kCap = MAXW + MAXW / 2 + 4;  // table slots (1.5 G + 2, rounded)
+  static constexpr uint32_t kSW = (MAXW + 31) / 32 + 1;
+  static constexpr uint32_t kDupBytes = 4 * kCap + 2 * 2 * MAXW + 4 * 2 * ((kSW + 3) & ~3u);
+  static constexpr uint32_t kTopBytes = 4 * kCap + 2 * MAXW + 4 * MAXW;
+  static constexpr uint32_t kRegion = ((kDupBytes > kTopBytes ? kDupBytes : kTopBytes) + 15) & ~15u;
+  uint64_t K[MAXW + 1];
+  uint64_t PB[MAXW + 1];
+  uint16_t wid[MAXW + 1];
+  uint16_t WL[MAXW + 1];
+  uint4 region[kNgWaves][kRegion / 16];
+};
+
+// the documents the LDS path of k_gr_ngrams<hi> takes: <= hi words, 16-bit word byte prefixes
+__device__ __forceinline__ bool ng_fits(const GrExport& e, uint32_t hi) {
+  return e.W <= hi && e.WL[e.W] <= 0xFFFFu;
+}
+
+__device__ __forceinline__ uint32_t ng_home(uint64_t k, uint32_t capn) {
+  return (uint32_t)(((k & 0xFFFFFFFFull) * capn) >> 32);
+}
+
+// gram equality of order n (DupGrams::eq over the staged arrays; the byte comparison of grams with
+// different word sequences reads the exported HBM arrays)
+template <class NS>
+__device__ __forceinline__ bool ng_dup_eq(const NS& S, const GrExport& e, uint32_t p, uint32_t q, uint32_t n) {
+  if ((uint32_t)(S.WL[p + n] - S.WL[p]) != (uint32_t)(S.WL[q + n] - S.WL[q])) return false;
+  uint32_t dw = 0;
+  for (uint32_t k = 0; k < n; ++k) dw |= (uint32_t)(S.wid[p + k] ^ S.wid[q + k]);
+  if (dw == 0) return true;
+  const DupGrams dg{e.wid, e.WL, e.K, e.PB, e.bs, e.be, e.b};
+  return dg.eq(p, q, n);
+}
+
+template <class NS>
+__device__ __forceinline__ int64_t ng_dup_order(NS& S, const GrExport& e, uint32_t W, uint32_t n, uint32_t lane,
+                                                uint4* region, bool prof, uint64_t& c_canon, uint64_t& c_walk) {
+  const uint64_t t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  const uint32_t G = W - n + 1;
+  const uint32_t capn = G + (G >> 1) + 2;
+  const uint32_t SW = (G + 31) / 32 + 1;
+  const uint32_t SWa = (SW + 3u) & ~3u;
+  uint32_t* tab = (uint32_t*)region;
+  uint16_t* gc = (uint16_t*)(tab + NS::kCap);
+  uint16_t* ln = gc + NS::kMaxW;
+  uint32_t* sn = (uint32_t*)(ln + NS::kMaxW);
+  uint32_t* R = sn + SWa;
+  for (uint32_t i = lane; i < capn; i += 64) tab[i] = 0;
+  for (uint32_t i = lane; i < 2 * SWa; i += 64) sn[i] = 0;
+  __builtin_amdgcn_wave_barrier();
+  // one position at a time per lane (few registers: occupancy hides the LDS round trips); the
+  // slot goes to gc[] until every gram is in the table
+#pragma unroll 1
+  for (uint32_t p = lane; p < G; p += 64) {
+    const uint32_t len = (uint32_t)(S.WL[p + n] - S.WL[p]);
+    const uint64_t key = dev_key(S.PB[p + n] * (S.K[p + n] - S.K[p]), len);
+    const uint32_t fp = (uint32_t)(key >> 48);
+    const uint32_t mine = (fp << 16) | (p + 1);
+    uint32_t sl = ng_home(key, capn);
+    while (true) {
+      uint32_t cur = tab[sl];
+      if (cur == 0) {
+        cur = atomicCAS(&tab[sl], 0u, mine);
+        if (cur == 0) break;
+      }
+      if ((cur >> 16) == fp && ng_dup_eq(S, e, p, (cur & 0xFFFFu) - 1u, n)) {
+        if ((cur & 0xFFFFu) > p + 1u) atomicMin(&tab[sl], mine);
+        break;
+      }
+      if (++sl == capn) sl = 0;
+    }
+    gc[p] = (uint16_t)sl;
+    ln[p] = (uint16_t)len;
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+  for (uint32_t p = lane; p < G; p += 64) {
+    const uint32_t c = (tab[gc[p]] & 0xFFFFu) - 1u;
+    gc[p] = (uint16_t)c;
+    if (c != p) {
+      atomicOr(&R[p >> 5], 1u << (p & 31));
+      atomicOr(&R[c >> 5], 1u << (c & 31));
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint64_t t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  c_canon += t1 - t0;
+  // greedy walk (reference find_all_duplicate, utils/text.rs:241-259; dup_walk_wave over LDS)
+  const uint32_t nw = (G + 31) >> 5;
+  int64_t rep = 0;
+  uint32_t idx = 0;
+  while (idx < G) {
+    uint32_t p0 = G;
+    for (uint32_t base = idx >> 5; base < nw; base += 64) {
+      const uint32_t w = base + lane;
+      uint32_t bw = w < nw ? R[w] : 0u;
+      if (w == (idx >> 5)) bw &= ~0u << (idx & 31);
+      const uint64_t m = __ballot(bw != 0u);
+      if (m) {
+        const int l = __builtin_ctzll(m);
+        p0 = ((base + (uint32_t)l) << 5) + (uint32_t)__builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)bw, l));
+        break;
+      }
+    }
+    if (p0 >= G) break;
+    const uint32_t p = p0 + lane;
+    const bool act = p < G && ((R[p >> 5] >> (p & 31)) & 1u);
+    uint32_t g = 0xFFFFFFFFu, l = 0;
+    if (act) {
+      g = gc[p];
+      l = ln[p];
+    }
+    const bool seen0 = act && ((sn[g >> 5] >> (g & 31)) & 1u);
+    uint64_t A = __ballot(act), Sm = __ballot(seen0), cnt = 0, fv = 0;
+    uint32_t next = p0 + 64;
+    while (A) {
+      const uint32_t k = (uint32_t)__builtin_ctzll(A);
+      if ((Sm >> k) & 1ull) {
+        cnt |= 1ull << k;
+        const uint32_t jj = k + n;
+        A = jj >= 64 ? 0ull : (A & (~0ull << jj));
+        if (p0 + jj > next) next = p0 + jj;
+      } else {
+        fv |= 1ull << k;
+        Sm |= __ballot(g == (uint32_t)__builtin_amdgcn_readlane((int)g, (int)k));
+        A &= A - 1;
+      }
+    }
+    if ((fv >> lane) & 1ull) atomicOr(&sn[g >> 5], 1u << (g & 31));
+    uint32_t add = ((cnt >> lane) & 1ull) ? l : 0u;
+    for (int o = 32; o > 0; o >>= 1) add += (uint32_t)__shfl_xor((int)add, o);
+    rep += add;
+    __builtin_amdgcn_wave_barrier();
+    idx = next;
+  }
+  if (prof) c_walk += __builtin_amdgcn_s_memtime() - t1;
+  return rep;
+}
+
+// top n-gram order (reference find_top_duplicate, utils/text.rs:211-238): space-joined grams are
+// equal iff their word sequences are, so grams are grouped by their canonical word-id tuples
+// (fingerprint table, exact tuple comparison on a match) and counted per canonical gram
+template <class NS>
+__device__ __forceinline__ int64_t ng_top_order(NS& S, uint32_t W, uint32_t n, uint32_t lane, uint4* region) {
+  const uint32_t G = W - n + 1;
+  const uint32_t capn = G + (G >> 1) + 2;
+  uint32_t* tab = (uint32_t*)region;
+  uint16_t* gc = (uint16_t*)(tab + NS::kCap);
+  uint32_t* cnt = (uint32_t*)(gc + NS::kMaxW);
+  for (uint32_t i = lane; i < capn; i += 64) tab[i] = 0;
+  for (uint32_t i = lane; i < G; i += 64) cnt[i] = 0;
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+  for (uint32_t p = lane; p < G; p += 64) {
+    uint64_t h = (uint64_t)n << 56;
+    for (uint32_t k = 0; k < n; ++k) h = (h ^ S.wid[p + k]) * 0x9E3779B97F4A7C15ull + k;
+    const uint64_t key = mix64(h);
+    const uint32_t fp = (uint32_t)(key >> 48);
+    const uint32_t mine = (fp << 16) | (p + 1);
+    uint32_t sl = ng_home(key, capn);
+    while (true) {
+      uint32_t cur = tab[sl];
+      if (cur == 0) {
+        cur = atomicCAS(&tab[sl], 0u, mine);
+        if (cur == 0) break;
+      }
+      if ((cur >> 16) == fp) {
+        const uint32_t q = (cur & 0xFFFFu) - 1u;
+        uint32_t dw = 0;
+        for (uint32_t k = 0; k < n; ++k) dw |= (uint32_t)(S.wid[p + k] ^ S.wid[q + k]);
+        if (dw == 0) {
+          if (q > p) atomicMin(&tab[sl], mine);
+          break;
+        }
+      }
+      if (++sl == capn) sl = 0;
+    }
+    gc[p] = (uint16_t)sl;
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+  for (uint32_t p = lane; p < G; p += 64) {
+    const uint32_t c = (tab[gc[p]] & 0xFFFFu) - 1u;
+    atomicAdd(&cnt[c], 1u);
+  }
+  __builtin_amdgcn_wave_barrier();
+  uint32_t mx = 0;
+  for (uint32_t p = lane; p < G; p += 64) mx = cnt[p] > mx ? cnt[p] : mx;
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t v = (uint32_t)__shfl_xor((int)mx, o);
+    mx = v > mx ? v : mx;
+  }
+  if (mx <= 1) return 0;
+  uint32_t ml = 0;
+  for (uint32_t p = lane; p < G; p += 64) {
+    if (cnt[p] != mx) continue;
+    const uint32_t len = (uint32_t)(S.WL[p + n] - S.WL[p]) + n - 1;
+    ml = len > ml ? len : ml;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t w = (uint32_t)__shfl_xor((int)ml, o);
+    ml = w > ml ? w : ml;
+  }
+  return (int64_t)ml * (int64_t)mx;
+}
+
+template <uint32_t MAXW>
+__global__ __launch_bounds__(64 * kNgWaves) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_gr_ngrams(
+    const DevStage* __restrict__ stage, int32_t gr_step, const int32_t* __restrict__ perm, int32_t ndocs,
+    const GrExport* __restrict__ ex, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec,
+    uint32_t* flags, uint64_t* prof) {
+  __shared__ NgShared<MAXW> S;
+  const int k = (int)blockIdx.x;
+  const int doc = perm[k];
+  if (doc >= ndocs) return;
+  const GrExport& e = ex[k];
+  if (!e.valid) return;  // dead, returned early (flagged for the CPU path) or no n-grams
+  const uint32_t W = e.W;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const DevStep& ds = stage->steps[gr_step];
+  int64_t* r = rec + (int64_t)ds.rec_prefix * ndocs + (int64_t)doc * ds.width;
+  const int nt = ds.n_dup + ds.n_top;
+  if (!ng_fits(e, MAXW)) {
+    // more words than this size class holds: the generic per-order code over HBM scratch, one
+    // order per wave at a time, each in its own share of the document's unused scratch slice
+    for (int t = (int)wv; t < nt; t += kNgWaves) {
+      DocCtx<WavePar> x;
+      x.prof = nullptr;
+      x.lds = nullptr;
+      x.lcap = 0;
+      x.lused = 0;
+      x.ucd = UcdView{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
+      x.pw = pw;
+      x.pw_n = pw_n;
+      x.ipw = pw ? pw + pw_n + 1 : nullptr;
+      const uint64_t region = (e.free_cap / (uint64_t)nt) & ~255ull;
+      x.scr = e.free_base + (uint64_t)t * region;
+      x.cap = region;
+      x.used = 0;
+      x.flag = flags + doc;
+      if (t < ds.n_dup) gr_dup_one_order(x, ds, t, e, r);
+      else gr_top_one_order(x, ds, t - ds.n_dup, e, r);
+      if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
+    }
+    return;
+  }
+  uint64_t* pf = prof ? prof + (size_t)doc * kPhaseSlots : nullptr;
+  const uint64_t t0 = pf ? __builtin_amdgcn_s_memtime() : 0;
+  for (uint32_t i = tid; i <= W; i += 64 * kNgWaves) {
+    S.K[i] = e.K[i];
+    S.PB[i] = e.PB[i];
+    S.WL[i] = (uint16_t)e.WL[i];
+    S.wid[i] = i < W ? (uint16_t)e.wid[i] : (uint16_t)0;
+  }
+  __syncthreads();
+  if (pf && tid == 0) atomicAdd((unsigned long long*)&pf[PH_GR_DUP], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
+  uint64_t c_canon = 0, c_walk = 0, c_top = 0;  // (profiling: this wave's cycles per phase)
+  for (int t = (int)wv; t < nt; t += kNgWaves) {
+    int64_t v = 0;
+    if (t < ds.n_dup) {
+      const uint32_t n = (uint32_t)ds.dup_n[t];
+      if (n > 0 && W >= n) v = ng_dup_order(S, e, W, n, lane, S.region[wv], pf != nullptr, c_canon, c_walk);
+    } else {
+      const uint32_t n = (uint32_t)ds.top_n[t - ds.n_dup];
+      const uint64_t ts = pf ? __builtin_amdgcn_s_memtime() : 0;
+      if (n > 0 && W >= n) v = ng_top_order(S, W, n, lane, S.region[wv]);
+      if (pf) c_top += __builtin_amdgcn_s_memtime() - ts;
+    }
+    // record: the top orders first, then the duplicated orders
+    if (lane == 0) r[rec_gr_fixed() + (t < ds.n_dup ? ds.n_top + t : t - ds.n_dup)] = v;
+  }
+  if (pf && lane == 0) {
+    atomicAdd((unsigned long long*)&pf[PH_GR_DUP_CANON], (unsigned long long)c_canon);
+    atomicAdd((unsigned long long*)&pf[PH_GR_DUP_WALK], (unsigned long long)c_walk);
+    atomicAdd((unsigned long long*)&pf[PH_GR_TOP_CANON], (unsigned long long)c_top);
+  }
+}
+
 // The n-gram orders of wave documents (split mode of the wave stage kernel): one wave per
 // (document, task), task = duplicated n-gram order t < n_dup, then top order t - n_dup. Block k
 // handles launch position k / n_tasks of the wave launch (its export slot) and task k % n_tasks;
@@ -379,18 +677,9 @@ __global__ __launch_bounds__(64) void k_langid_features(
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   x.stamp(PH_START);
   langid_coop(x, b, n, lt, rec + (int64_t)doc * width);
-  // Documents with dictionary-segmented scripts go to the CPU path (the stage kernel's decode
-  // flags them too). With the language-id gate in front of the stage (device.py plan_passes) the
-  // stage kernel never sees a document this pass filters, so the flag is raised here as well:
-  // dictionary scripts are >= U+0E00, i.e. lead bytes >= 0xE0 (host: has_dict_script).
-  bool dict = false;
-  for (uint32_t i = x.par.lane; i < n; i += 64) {
-    if (b[i] >= 0xE0) {
-      int len;
-      dict |= (x.ucd.props(utf8_decode(b, i, n, &len)) & P_DICT) != 0;
-    }
-  }
-  if (__ballot(dict) && x.par.leader()) x.set_flag(DOC_NEEDS_CPU);
+  // (no dictionary-script flag: the language records are exact for every script; a document
+  // with such code points goes to the CPU path only if it reaches a segmentation pass, whose
+  // decode flags it)
   x.stamp(PH_LID);
   if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
 }
@@ -573,15 +862,9 @@ __device__ __forceinline__ void lid_doc_vector(const uint8_t* __restrict__ b, ui
     *e_out = e;
     *cnt_out = (int64_t)cnt;
   }
-  // dictionary-segmented scripts go to the CPU path (as k_langid_features)
-  bool dict = false;
-  for (uint32_t i = (uint32_t)lane; i < n; i += 64) {
-    if (b[i] >= 0xE0) {
-      int len;
-      dict |= (ucd.props(utf8_decode(b, i, n, &len)) & P_DICT) != 0;
-    }
-  }
-  if (__ballot(dict) && lane == 0) atomicOr(flag, DOC_NEEDS_CPU);
+  // (no dictionary-script flag: the language records are exact for every script; a document
+  // with such code points goes to the CPU path only if it reaches a segmentation pass)
+  (void)flag;
 }
 
 __global__ __launch_bounds__(64 * kLidWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_langid_mfma(
@@ -1162,21 +1445,32 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
 }
 
 // Wave documents in split mode (tb_stage_analyze with gr_export): n_docs export slots, n_tasks =
-// the GopherRepetition step's duplicated + top n-gram orders.
+// the GopherRepetition step's duplicated + top n-gram orders. Launch positions (the host puts the
+// longer documents first): [0, n_big) one wave per (document, order) (k_gr_split_wave), the rest
+// with block != 0 one workgroup per document (k_gr_ngrams<256>); block == 0: k_gr_split_wave for
+// all. Measured (profiles/r7_ngram): workgroups of the 512-word class lost to the per-order waves
+// for documents over 1.2 KB (LDS-limited occupancy), all-waves lost to this split.
 int tb_gr_split_wave(hipStream_t stream, const void* stage, int32_t gr_step, const int32_t* perm, int32_t n_docs,
                      int32_t n_tasks, int32_t ndocs, const void* gr_export, const uint64_t* pw, uint32_t pw_n,
                      const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
-                     uint32_t* flags, uint32_t lds_bytes) {
+                     uint32_t* flags, uint32_t lds_bytes, int32_t block, uint64_t* prof, int32_t n_big) {
   if (n_docs <= 0 || n_tasks <= 0) return 0;
   if (!perm || !gr_export || gr_step < 0 || gr_step >= kMaxStageSteps || n_tasks > 2 * kMaxNgramEntries ||
-      lds_bytes > kMaxLdsPerDoc)
+      lds_bytes > kMaxLdsPerDoc || n_big < 0 || n_big > n_docs)
     return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
-  if (lds_bytes > 65536)
-    (void)hipFuncSetAttribute((const void*)k_gr_split_wave, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-  hipLaunchKernelGGL(k_gr_split_wave, dim3((uint32_t)n_docs * (uint32_t)n_tasks), dim3(64), lds_bytes, stream,
-                     (const DevStage*)stage, gr_step, perm, n_tasks, ndocs, (const GrExport*)gr_export, pw, pw_n, t, rec,
-                     flags, lds_bytes);
+  const GrExport* ex = (const GrExport*)gr_export;
+  const int32_t n_wave = block ? n_big : n_docs;
+  if (n_wave > 0) {
+    if (lds_bytes > 65536)
+      (void)hipFuncSetAttribute((const void*)k_gr_split_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds_bytes);
+    hipLaunchKernelGGL(k_gr_split_wave, dim3((uint32_t)n_wave * (uint32_t)n_tasks), dim3(64), lds_bytes, stream,
+                       (const DevStage*)stage, gr_step, perm, n_tasks, ndocs, ex, pw, pw_n, t, rec, flags, lds_bytes);
+  }
+  if (block && n_docs > n_big)
+    hipLaunchKernelGGL((k_gr_ngrams<256>), dim3((uint32_t)(n_docs - n_big)), dim3(64 * kNgWaves), 0, stream,
+                       (const DevStage*)stage, gr_step, perm + n_big, ndocs, ex + n_big, pw, pw_n, t, rec, flags, prof);
   return (int)hipGetLastError();
 }
 
@@ -1395,7 +1689,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 
 int tb_phase_slots() { return kPhaseSlots; }
 
-int tb_abi_version() { return 16; }
+int tb_abi_version() { return 18; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

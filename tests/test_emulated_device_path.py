@@ -138,3 +138,34 @@ def test_gopher_repetition_records_equal_oracle_on_repetitive_text(host):
         with_dups += any(ref[7 + 3:])
         assert ref == list(rec[i]), (i, t[:80], ref, list(rec[i]))
     assert with_dups > 100
+
+
+def test_mixed_script_delegation_is_overlapped_and_exact():
+    """Dictionary-script documents (5 % with a CJK / Thai snippet, 1 % CJK): process_many recomputes
+    the delegated ones on the engine's delegation thread while later batches are resolved; the
+    merged results equal the CPU oracle batch for batch, and documents the language gate already
+    filtered (the CJK ones) are not delegated."""
+    cfg = load_pipeline_config("config/bench_pipeline.yaml")
+    batches = [synth.pack(synth.make_corpus(600, 800, seed=40 + s, mixed_script=True)) for s in range(3)]
+    emu = Engine(cfg, backend="emulate", nthreads=4)
+    cpu = Engine(cfg, backend="cpu", segmentation="icu", nthreads=4)
+    got = list(emu.process_many(batches))
+    assert len(got) == 3
+    n_dict = 0
+    for (d, o), r in zip(batches, got):
+        assert r.deferred is None
+        ref = cpu.process(d, o)
+        np.testing.assert_array_equal(r.fail_step, ref.fail_step)
+        np.testing.assert_array_equal(r.status, ref.status)
+        assert outputs(r) == outputs(ref)
+        texts = [bytes(d[o[i]:o[i + 1]]).decode() for i in range(len(o) - 1)]
+
+        def dict_script(ch):
+            return "\u0e00" <= ch <= "\u0e7f" or "\u3040" <= ch <= "\u30ff" or "\u4e00" <= ch <= "\u9fff"
+
+        dict_docs = [t for t in texts if any(dict_script(ch) for ch in t)]
+        cjk_docs = [t for t in dict_docs if sum(ch.isascii() for ch in t) < len(t) // 2]
+        n_dict += len(cjk_docs)
+        # the CJK documents fail the language gate on the device: not delegated
+        assert 0 < r.n_delegated <= len(dict_docs) - len(cjk_docs), (r.n_delegated, len(dict_docs), len(cjk_docs))
+    assert n_dict > 0

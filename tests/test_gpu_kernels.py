@@ -113,10 +113,17 @@ def test_device_gate_matches_host_gate(host, corpus, runner_parts):
 
 
 def test_dictionary_scripts_are_flagged(host, runner_parts):
+    """A dictionary-script document goes to the CPU path only when it reaches a segmentation pass:
+    the CJK document fails the language gate on the device (exact records, not delegated), the
+    Danish document with a CJK snippet passes it and is flagged by the stage kernel's decode."""
     _, _, _, runner, _ = runner_parts
-    data, off = synth.pack(["日本語のテキストです。", "plain english text here."])
+    rng = np.random.default_rng(5)
+    dan = synth.make_doc(rng, "dan", 1500)
+    data, off = synth.pack(["日本語のテキストです。", "plain english text here.", dan[:200] + " 日本語 " + dan[200:]])
     res = runner.run(data, off)
-    assert res.flags[0] != 0 and res.flags[1] == 0
+    assert res.flags[0] == 0 and res.dead[0] != 0
+    assert res.flags[1] == 0
+    assert res.flags[2] != 0
 
 
 def _langid_records(runner, res, n):
@@ -287,7 +294,8 @@ def test_pre_decoded_long_documents_match_host(host, runner_parts, monkeypatch):
     texts = [synth.make_doc(rng, langs[k % 5], int(s)) for k, s in enumerate(np.geomspace(66000, 400000, 8))]
     uni = "\n".join(fuzz_docs(3000, seed=9))
     texts += [uni[:150000], uni[150000:230000]]
-    texts += [synth.make_doc(rng, "eng", 70000) + " 日本語のテキストです。 " + synth.make_doc(rng, "dan", 5000)]
+    # (Danish: it passes the language gate, so it reaches the stage that flags it)
+    texts += [synth.make_doc(rng, "dan", 70000) + " 日本語のテキストです。 " + synth.make_doc(rng, "dan", 5000)]
     texts += synth.make_corpus(200, 900, seed=4)  # short documents in the same batch
     data, off = synth.pack(texts)
     n = len(texts)

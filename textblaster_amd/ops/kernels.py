@@ -22,12 +22,13 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 16
+ABI_VERSION = 18
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32, _P,
                          _P, _P],
-    "tb_gr_split_wave": [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32],
+    "tb_gr_split_wave": [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _I32, _P,
+                         _I32],
     "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _P, _P],
     "tb_stage_analyze_blk": [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P,
                              _U32, _P, _P, _P, _I32, _U32, _I32, _P, _P, _I32],
@@ -182,16 +183,21 @@ class Kernels:
             _ptr(dead), _ptr(line_stats), _ptr(gr_export))
         _check(rc, "tb_stage_analyze")
 
-    def gr_split_wave(self, stage, gr_step, perm, n_docs, n_tasks, ndocs, gr_export, pw, pw_n, rec, flags, lds_bytes):
-        """k_gr_split_wave: one wave per (wave document, n-gram order) over the descriptors
-        stage_analyze exported; n_tasks = the GopherRepetition step's duplicated + top orders."""
+    def gr_split_wave(self, stage, gr_step, perm, n_docs, n_tasks, ndocs, gr_export, pw, pw_n, rec, flags, lds_bytes,
+                      block=True, prof=None, n_big=0):
+        """The n-gram orders of the wave documents stage_analyze exported (n_tasks = the
+        GopherRepetition step's duplicated + top orders): launch positions [0, n_big) one wave per
+        (document, order) (k_gr_split_wave), the rest with ``block`` one workgroup per document
+        (k_gr_ngrams); without ``block`` k_gr_split_wave for all."""
+        if not 0 <= n_big <= n_docs:
+            raise DeviceError("gr_split_wave: n_big out of range")
         if gr_export.nbytes < n_docs * self.sizeof_gr_export or perm.numel() < n_docs:
             raise DeviceError("gr_split_wave: operand shapes")
         t = self.tabs
         rc = self.lib.tb_gr_split_wave(self.stream(), stage.data_ptr(), gr_step, perm.data_ptr(), n_docs, n_tasks,
                                        ndocs, gr_export.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(),
                                        t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(),
-                                       flags.data_ptr(), lds_bytes)
+                                       flags.data_ptr(), lds_bytes, 1 if block else 0, _ptr(prof), int(n_big))
         _check(rc, "tb_gr_split_wave")
 
     def stage_analyze_blk(self, plan, stage, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n,

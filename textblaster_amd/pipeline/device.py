@@ -583,7 +583,12 @@ class DeviceRunner:
         # wave documents finish their n-gram orders in one wave per (document, order)
         # (k_gr_split_wave, LDS slice TB_LDS_BYTES_SPLIT); TB_WAVE_SPLIT=0 keeps them in the stage
         self.wave_split = os.environ.get("TB_WAVE_SPLIT", "1") not in ("", "0")
-        self.lds_bytes_split = int(os.environ.get("TB_LDS_BYTES_SPLIT", "6144"))
+        self.lds_bytes_split = int(os.environ.get("TB_LDS_BYTES_SPLIT", "8192"))
+        self.ngram_block = os.environ.get("TB_NGRAM_BLOCK", "1") not in ("", "0")
+        # wave documents longer than this take one wave per n-gram order (k_gr_split_wave), the
+        # shorter ones one workgroup per document (k_gr_ngrams: 256 words, ~5.5 bytes per word on
+        # natural text; a document with more words runs the generic code in that workgroup)
+        self.ngram_big_bytes = int(os.environ.get("TB_NGRAM_BIG_BYTES", "1200"))
         if not 0 <= self.lds_bytes_split <= 65536:
             raise DeviceError("TB_LDS_BYTES_SPLIT must be in [0, 65536]")
         if not 0 <= self.lds_bytes_blk <= 131072:
@@ -972,8 +977,12 @@ class DeviceRunner:
                                              self.lds_bytes, prof, self.stage_waves, nw, skip, ls_out, gxw)
                         if gxw is not None:
                             gr_pos, n_tasks = self.gr_split[s]
+                            # wave documents longer than ngram_big_bytes (a prefix: perm is longest
+                            # first) take one wave per order, the rest one workgroup each
+                            n_big = int(np.count_nonzero(lens_perm[n_long:] > self.ngram_big_bytes))
                             self.k.gr_split_wave(self.stage_ts[s], gr_pos, d_perm[n_long:], nw, n_tasks - 2, ndocs,
-                                                 gxw, pw, pw_n, rec, flags, self.lds_bytes_split)
+                                                 gxw, pw, pw_n, rec, flags, self.lds_bytes_split, self.ngram_block,
+                                                 self._prof_buf(ndocs, keep, f"ngram{s}"), n_big)
                 if ev_lid is not None:
                     main.wait_event(ev_lid)
                 if ev_blk is not None:
@@ -1120,20 +1129,6 @@ class DeviceRunner:
         return self.submit(data, off, bw).wait()
 
 
-def _dict_script_flags(data: np.ndarray, off: np.ndarray) -> np.ndarray:
-    """DOC_NEEDS_CPU (1) for documents with a dictionary-script code point (host twin of the check
-    in k_langid_features); only documents with a byte >= 0xE0 are decoded."""
-    h = native.host()
-    n = len(off) - 1
-    out = np.zeros(n, dtype=np.uint32)
-    hi = np.nonzero(data >= 0xE0)[0]
-    if len(hi):
-        for d in np.unique(np.searchsorted(off, hi, side="right") - 1).tolist():
-            if 0 <= d < n and h.has_dict_script(bytes(data[off[d]:off[d + 1]]).decode("utf-8", "replace")):
-                out[d] = 1
-    return out
-
-
 class EmulatedRunner:
     """Host emulation of :class:`DeviceRunner` (same records, versions and flags, computed by the
     C++ port of the device algorithms). Drives the exact resolve path of the GPU backend on a
@@ -1157,12 +1152,6 @@ class EmulatedRunner:
             plan, self.stage_layout, steps_native, gating, os.environ.get("TB_LID_GATE", "1") not in ("", "0"))
         self.bw_dead_max = bw_dead_max(plan, self.passes, self.pass_of_step)
         self.line_stats_stage = line_stats_stages(plan, self.stage_layout)
-        # wave documents finish their n-gram orders in one wave per (document, order)
-        # (k_gr_split_wave, LDS slice TB_LDS_BYTES_SPLIT); TB_WAVE_SPLIT=0 keeps them in the stage
-        self.wave_split = os.environ.get("TB_WAVE_SPLIT", "1") not in ("", "0")
-        self.lds_bytes_split = int(os.environ.get("TB_LDS_BYTES_SPLIT", "6144"))
-        if not 0 <= self.lds_bytes_split <= 65536:
-            raise DeviceError("TB_LDS_BYTES_SPLIT must be in [0, 65536]")
         # test hook: additionally mark every k-th document dead after the first pass (a wrong
         # device gate), to exercise the resolver's recovery path
         self.gate_corrupt = gate_corrupt
@@ -1194,7 +1183,10 @@ class EmulatedRunner:
                 vd, vo = versions[self.plan.stage_version[x]]
                 rec, fl = h.emulate_stage(self.steps, self.plan.stages[x], vd, vo, self.nthreads, self.lid, 0, skip)
                 lid_rec[x] = rec
-                fl = _dict_script_flags(vd, vo)  # k_langid_features raises DOC_NEEDS_CPU for these
+                # the language-id kernels flag nothing: their records are exact for every script, so
+                # a document this gate filters never goes to the CPU path (dictionary scripts are
+                # flagged by the segmentation passes of the documents that reach them)
+                fl = np.zeros(ndocs, dtype=np.uint32)
             elif kind == "stage":
                 sv = self.plan.stage_version[x]
                 vd, vo = versions[sv]

@@ -17,6 +17,7 @@ Backends:
 """
 from __future__ import annotations
 
+import collections
 import dataclasses
 import os
 import time
@@ -52,6 +53,9 @@ class BatchResult:
     reasons: Dict[int, str]    # filled only when requested
     timings: Dict[str, float]
     n_delegated: int = 0
+    # process_many: the CPU-path recomputation of the delegated documents, still running on the
+    # engine's delegation thread ((future, rows)); merged before the result is handed out
+    deferred: Optional[Tuple] = None
 
     @property
     def n_kept(self) -> int:
@@ -105,6 +109,10 @@ class Engine:
         import threading
 
         self._submit_lock = threading.RLock()
+        # CPU-path work of delegated documents (process_many): one thread, so it overlaps the next
+        # batches' resolve / assembly on the consumer thread (the native pools do the heavy part)
+        self._deleg_pool = None
+        self._async_delegation = False
         # process_many on the GPU backend submits from a helper thread (TB_PREFETCH_THREAD=0: off)
         self.prefetch_threads = os.environ.get("TB_PREFETCH_THREAD", "1") not in ("", "0")
         # text bytes per device batch (scratch ~160 B per text byte per in-flight slot: 384 MB of
@@ -179,7 +187,7 @@ class Engine:
     def process(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None,
                 row_base: int = 0) -> BatchResult:
         """Run the pipeline over one batch. ``meta`` = (data uint8, off int64, valid uint8) or None."""
-        return self.finish(self.submit(data, off, meta, row_base))
+        return self._merge_deferred(self.finish(self.submit(data, off, meta, row_base)))
 
     def process_many(self, batches: Iterable, on_error: str = "raise") -> Iterator[BatchResult]:
         """Pipelined processing of an iterable of ``(data, off, meta)`` batches: batch k+1 is
@@ -208,11 +216,19 @@ class Engine:
             except Exception as e:  # noqa: BLE001 - handled per on_error
                 return (g, base, item, e)
 
-        if self.prefetch_threads and self.backend in ("cuda", "emulate"):
-            yield from self._process_threaded(expand(), submit_item, on_error, groups, sizes)
-            return
+        self._async_delegation = self.backend in ("cuda", "emulate")
+        try:
+            if self.prefetch_threads and self.backend in ("cuda", "emulate"):
+                yield from self._deferred_in_order(self._process_threaded(expand(), submit_item, on_error, groups,
+                                                                          sizes))
+                return
+            yield from self._deferred_in_order(self._process_serial(expand(), submit_item, on_error, groups, sizes))
+        finally:
+            self._async_delegation = False
+
+    def _process_serial(self, items, submit_item, on_error, groups, sizes):
         pending = None
-        for g, base, item in expand():
+        for g, base, item in items:
             cur = submit_item(g, base, item)
             if pending is not None:
                 out = self._collect_group(pending, on_error, groups, sizes)
@@ -223,6 +239,44 @@ class Engine:
             out = self._collect_group(pending, on_error, groups, sizes)
             if out is not None:
                 yield out
+
+    # results whose delegated documents are still on the CPU path, at most this many held back
+    DEFERRED_DEPTH = 2
+
+    def _deferred_in_order(self, results) -> Iterator[BatchResult]:
+        """Yields results in order once their delegated (CPU-path) documents are merged in; the
+        CPU work of batch k runs while batches k+1.. are resolved and assembled."""
+        held: collections.deque = collections.deque()
+        try:
+            for r in results:
+                held.append(r)
+                while held and (held[0].deferred is None or held[0].deferred[0].done()
+                                or len(held) > self.DEFERRED_DEPTH):
+                    yield self._merge_deferred(held.popleft())
+            while held:
+                yield self._merge_deferred(held.popleft())
+        finally:
+            for r in held:  # an early exit: the CPU jobs finish before their inputs go away
+                if r.deferred is not None:
+                    r.deferred[0].result()
+
+    @staticmethod
+    def _merge_deferred(result: BatchResult) -> BatchResult:
+        if result.deferred is None:
+            return result
+        fut, delegated = result.deferred
+        result.deferred = None
+        t0 = time.perf_counter()
+        sub2 = fut.result()
+        result.kept += sub2.kept
+        result.excluded += sub2.excluded
+        result.error_rows = np.concatenate([result.error_rows, sub2.error_rows])
+        result.fail_step[delegated] = sub2.fail_step
+        result.status[delegated] = sub2.status
+        result.reasons.update(sub2.reasons)
+        result.n_delegated = len(delegated)
+        result.timings["delegated_wait"] = time.perf_counter() - t0
+        return result
 
     def _process_threaded(self, items, submit_item, on_error, groups, sizes):
         """process_many with a submitter thread: input staging (pinned copy + H2D) and kernel
@@ -342,7 +396,7 @@ class Engine:
         parts = groups.pop(g)
         if len(parts) == 1:
             return parts[0][1]
-        return _concat_results([r for _, r in parts], [b for b, _ in parts])
+        return _concat_results([self._merge_deferred(r) for _, r in parts], [b for b, _ in parts])
 
     def _finish_or_recover(self, pending, on_error: str) -> BatchResult:
         item, sub = pending
@@ -526,14 +580,35 @@ class Engine:
         with tracing.trace_range("tb.assemble"):
             result = self._collect(bs, ndocs, timings, resolved)
         if len(delegated):
-            sub2 = self._process_subset_cpu(data, off, meta, delegated)
-            result.kept += sub2.kept
-            result.excluded += sub2.excluded
-            result.error_rows = np.concatenate([result.error_rows, sub2.error_rows])
-            result.fail_step[delegated] = sub2.fail_step
-            result.status[delegated] = sub2.status
-            result.reasons.update(sub2.reasons)
-            result.n_delegated = len(delegated)
+            if self._async_delegation:
+                # recomputed on the delegation thread while the next batches are resolved; rows
+                # are shifted by row_base below, so the merge happens after that shift too
+                import concurrent.futures as cf
+
+                if self._deleg_pool is None:
+                    self._deleg_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="tb-delegate",
+                                                             initializer=tracing.name_os_thread,
+                                                             initargs=("tb-delegate",))
+                rb = row_base
+
+                def job(rows=delegated):
+                    r2 = self._process_subset_cpu(data, off, meta, rows)
+                    if rb:
+                        for p in r2.kept + r2.excluded:
+                            p.rows = p.rows + rb
+                    return r2
+
+                result.deferred = (self._deleg_pool.submit(job), delegated)
+                result.n_delegated = len(delegated)
+            else:
+                sub2 = self._process_subset_cpu(data, off, meta, delegated)
+                result.kept += sub2.kept
+                result.excluded += sub2.excluded
+                result.error_rows = np.concatenate([result.error_rows, sub2.error_rows])
+                result.fail_step[delegated] = sub2.fail_step
+                result.status[delegated] = sub2.status
+                result.reasons.update(sub2.reasons)
+                result.n_delegated = len(delegated)
         timings["assemble"] = time.perf_counter() - t2
         timings["finish"] = time.perf_counter() - tf
         timings["submit"] = sub.submit_s

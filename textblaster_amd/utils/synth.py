@@ -175,10 +175,30 @@ def make_doc(rng: np.random.Generator, lang: str, target_bytes: int, vocab_kind:
     return text
 
 
+# Dictionary-segmented scripts (ICU word segmentation by dictionary: Han, Kana, Thai): snippets for
+# the mixed-script corpus
+CJK_SNIPPETS = ["日本語のテキストです。", "東京は日本の首都です", "中文分词测试", "北京欢迎你", "カタカナ",
+                "ひらがなとカタカナ", "漢字", "人工知能"]
+THAI_SNIPPETS = ["ภาษาไทย", "สวัสดีครับ", "ประเทศไทย"]
+
+
+def make_cjk_doc(rng: np.random.Generator, target_bytes: int) -> str:
+    """A document written in CJK (sentences of the snippets above), about ``target_bytes`` long."""
+    lines, size = [], 0
+    while size < target_bytes:
+        line = "".join(CJK_SNIPPETS[int(rng.integers(0, len(CJK_SNIPPETS)))] for _ in range(int(rng.integers(2, 6))))
+        lines.append(line)
+        size += len(line.encode()) + 1
+    return "\n".join(lines)
+
+
 def make_corpus(n_docs: int, mean_bytes: int = 1024, seed: int = 0,
-                langs=("eng", "dan", "swe", "nob", "nno"), lang_p=None, vocab: str = "small") -> List[str]:
+                langs=("eng", "dan", "swe", "nob", "nno"), lang_p=None, vocab: str = "small",
+                mixed_script: bool = False) -> List[str]:
     """``vocab``: "small" (the ~130 function words per language, the original benchmark corpus)
-    or "zipf" (60,000-type Zipf lexicons per language, see ``lexicon``)."""
+    or "zipf" (60,000-type Zipf lexicons per language, see ``lexicon``). ``mixed_script``: 5 % of
+    the documents get one CJK or Thai snippet inserted at a random word boundary and 1 % are
+    written in CJK (the dictionary-segmented scripts a European-language crawl still contains)."""
     if vocab not in ("small", "zipf"):
         raise ValueError("vocab must be 'small' or 'zipf'")
     rng = np.random.default_rng(seed)
@@ -187,7 +207,21 @@ def make_corpus(n_docs: int, mean_bytes: int = 1024, seed: int = 0,
     sizes = np.clip(rng.lognormal(mu, sigma, n_docs), 16, 64 * mean_bytes).astype(np.int64)
     langs = list(langs)
     choice = rng.choice(len(langs), size=n_docs, p=lang_p)
-    return [make_doc(rng, langs[int(c)], int(s), vocab) for c, s in zip(choice, sizes)]
+    docs = [make_doc(rng, langs[int(c)], int(s), vocab) for c, s in zip(choice, sizes)]
+    if mixed_script:
+        mrng = np.random.default_rng(seed + 4242)
+        u = mrng.random(n_docs)
+        for i in np.nonzero(u < 0.06)[0].tolist():
+            if u[i] < 0.01:
+                docs[i] = make_cjk_doc(mrng, int(sizes[i]))
+                continue
+            pool = THAI_SNIPPETS if mrng.random() < 0.3 else CJK_SNIPPETS
+            snip = pool[int(mrng.integers(0, len(pool)))]
+            t = docs[i]
+            sp = [k for k in range(len(t)) if t[k] == " "]
+            at = sp[int(mrng.integers(len(sp)))] + 1 if sp else 0
+            docs[i] = t[:at] + snip + " " + t[at:]
+    return docs
 
 
 def inject_words(texts: List[str], list_path: str, rate: float, seed: int = 0) -> List[str]:

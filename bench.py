@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--pool", type=int, default=16384, help="distinct synthetic docs per rank")
     ap.add_argument("--vocab", default="small", choices=["small", "zipf"],
                     help="synthetic vocabulary: ~130 words per language (default) or 60k-type Zipf lexicons")
+    ap.add_argument("--long-token-rate", type=float, default=0.0,
+                    help="fraction of pool documents given a long pre-token (URL, base64, indentation or dash "
+                         "run: the TokenCounter's 64+-byte path)")
     ap.add_argument("--mixed-script", action="store_true",
                     help="5%% of the documents carry a CJK / Thai snippet and 1%% are CJK (dictionary scripts)")
     ap.add_argument("--config", default=os.path.join(ROOT, "config", "bench_pipeline.yaml"))
@@ -109,6 +112,8 @@ def main():
     # synthetic corpus: a pool of distinct docs per rank, batches are fresh permutations of it
     texts = synth.make_corpus(args.pool, args.mean_bytes, seed=1000 + rank, vocab=args.vocab,
                               mixed_script=args.mixed_script)
+    if args.long_token_rate > 0:
+        texts = synth.inject_long_tokens(texts, args.long_token_rate, seed=rank)
     if has_bw and args.badwords_rate > 0:
         texts = synth.inject_words(texts, os.path.join(args.badwords_dir, "en"), args.badwords_rate, seed=rank)
     enc = [t.encode("utf-8") for t in texts]
@@ -200,7 +205,8 @@ def main():
             "dtype": lid.dtype if lid is not None else "int",
             "data": f"synthetic CommonCrawl-shaped docs (log-normal ~{args.mean_bytes} B, 5 languages, "
                     f"{'~130-word' if args.vocab == 'small' else '60k-type Zipf'} vocabularies"
-                    f"{', 5% with a CJK/Thai snippet + 1% CJK' if args.mixed_script else ''}), "
+                    f"{', 5% with a CJK/Thai snippet + 1% CJK' if args.mixed_script else ''}"
+                    f"{f', {args.long_token_rate:.0%} with a 64+-byte pre-token' if args.long_token_rate else ''}), "
                     f"{args.docs_per_step} docs/GPU/step",
             "config": {
                 "model": "+".join(s.type.replace("LanguageDetectionFilter", f"LanguageDetection({lid.description})"

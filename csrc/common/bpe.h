@@ -21,9 +21,12 @@
 // merge the adjacent pair with the lowest rank, leftmost on ties. The lane keeps the word's
 // symbol ids and pair ranks in two small arrays and deletes merged symbols in place.
 //
-// A document goes back to the host tokenizer (count -2) when it contains the text of an added
-// token (HF splits on those before pre-tokenizing), holds invalid UTF-8, or has a pre-token
-// longer than kBpeMaxWord bytes (the lane's merge arrays).
+// A pre-token longer than kBpeMaxWord bytes (the lane's merge arrays: long URLs, base64, runs of
+// indentation or dashes) is merged by bpe_word_long over arrays of its own length (on the device:
+// k_bpe_count marks the document kBpeLong and k_bpe_long recounts it with one wave per long
+// pre-token, up to kBpeMaxLong bytes). A document goes back to the host tokenizer (count -2) when
+// it contains the text of an added token (HF splits on those before pre-tokenizing), holds invalid
+// UTF-8, or has a pre-token longer than kBpeMaxLong bytes.
 #pragma once
 #include "tb_common.h"
 
@@ -34,6 +37,10 @@ constexpr int kBpeMaxAdded = 8;
 constexpr uint64_t kBpeEmpty = ~0ull;
 constexpr uint32_t kBpeNoRank = 0xFFFFFFFFu;
 constexpr int32_t kBpeHost = -2;  // count it on the host
+// k_bpe_count: the document has a pre-token over kBpeMaxWord bytes; its count is kBpeLong - (the
+// tokens of its other pre-tokens), which k_bpe_long completes
+constexpr int32_t kBpeLong = -3;
+constexpr int kBpeMaxLong = 2048;  // longest pre-token merged on the device
 
 enum BpeCls : int { BPE_O = 0, BPE_L = 1, BPE_N = 2, BPE_W = 3 };
 
@@ -134,6 +141,43 @@ TB_HD int bpe_word(const DevBpe& T, const uint8_t* w, int L, BpeArr c, BpeArr r)
     for (int j = bi + 1; j + 1 < m; ++j) r[j] = r[j + 1];
     if (bi > 0) r[bi - 1] = (uint32_t)(bpe_lookup(T, c[bi - 1], c[bi]) >> 32);
     if (bi + 1 < m) r[bi] = (uint32_t)(bpe_lookup(T, c[bi], c[bi + 1]) >> 32);
+  }
+  return m;
+}
+
+// Tokens of a pre-token of L >= 2 bytes of any length: bpe_word's rule (the leftmost lowest-rank
+// pair merges first) over a doubly linked list of symbols (nx / pv: next / previous live symbol,
+// -1 / L at the ends), so a merge scans for the minimum but shifts nothing; v[i] holds the pair
+// lookup of symbol i and its successor ((rank << 32 | merged id), ~0 = no merge), so a merge needs
+// only the two lookups of its new neighbours. Sequential (host); k_bpe_long runs the same merges
+// with the minimum search spread over a wave.
+TB_HD int bpe_word_long(const DevBpe& T, const uint8_t* w, int L, uint32_t* c, uint64_t* v, int32_t* nx,
+                        int32_t* pv) {
+  if (L <= 1) return L;
+  for (int i = 0; i < L; ++i) {
+    c[i] = T.byte_id[w[i]];
+    nx[i] = i + 1;
+    pv[i] = i - 1;
+  }
+  for (int i = 0; i + 1 < L; ++i) v[i] = bpe_lookup(T, c[i], c[i + 1]);
+  v[L - 1] = ~0ull;
+  int m = L;
+  while (m > 1) {
+    uint64_t best = ~0ull;
+    int bi = -1;
+    for (int i = 0; i < L; i = nx[i]) {  // symbol 0 never dies: merges keep their left symbol
+      const uint64_t r = v[i] | 0xFFFFFFFFull;  // rank only, ties to the leftmost
+      if (r < best) { best = r; bi = i; }
+    }
+    if (bi < 0 || (best >> 32) == kBpeNoRank) break;
+    const int j = nx[bi];
+    c[bi] = (uint32_t)v[bi];
+    nx[bi] = nx[j];
+    if (nx[j] < L) pv[nx[j]] = bi;
+    v[j] = ~0ull;
+    --m;
+    v[bi] = nx[bi] < L ? bpe_lookup(T, c[bi], c[nx[bi]]) : ~0ull;
+    if (pv[bi] >= 0) v[pv[bi]] = bpe_lookup(T, c[pv[bi]], c[bi]);
   }
   return m;
 }
@@ -280,26 +324,40 @@ TB_HD int64_t bpe_first_start(const DevBpe& T, const uint8_t* b, int64_t n, int6
   return i;
 }
 
-// Tokens (after merges) of the pre-tokens that start in [first_start(s0), first_start(s1)); -1:
-// count the document on the host (invalid UTF-8, a pre-token over kBpeMaxWord bytes).
+// Tokens (after merges) of the pre-tokens that start in [first_start(s0), first_start(s1)); a
+// pre-token [s, e) over kBpeMaxWord bytes is handed to on_long(s, e) (its tokens, or < 0: fail).
+// -1: count the document on the host (invalid UTF-8, or on_long failed).
+struct BpeNoLong {
+  TB_HD int64_t operator()(int64_t, int64_t) const { return -1; }
+};
+// (kMerge = false: short pre-tokens are only delimited, not merged; they count 0)
+template <bool kMerge = true, class LongF = BpeNoLong>
 TB_HD int64_t bpe_count_range(const DevBpe& T, const uint8_t* b, int64_t n, int64_t s0, int64_t s1, BpeArr c,
-                              BpeArr r) {
+                              BpeArr r, LongF&& on_long = LongF{}) {
   int64_t s = s0 <= 0 ? 0 : bpe_first_start(T, b, n, s0);
   if (s < 0) return -1;
   int64_t total = 0;
   while (s < n && s < s1) {
     const int64_t e = bpe_next_token(T, b, n, s);
-    if (e <= s || e - s > kBpeMaxWord) return -1;
-    total += bpe_word(T, b + s, (int)(e - s), c, r);
+    if (e <= s) return -1;
+    if (e - s > kBpeMaxWord) {
+      const int64_t k = on_long(s, e);
+      if (k < 0) return -1;
+      total += k;
+    } else if (kMerge) {
+      total += bpe_word(T, b + s, (int)(e - s), c, r);
+    }
     s = e;
   }
   return total;
 }
 
 // Token count of one document (kBpeHost: count it on the host), sequentially.
-TB_HD int32_t bpe_count_doc(const DevBpe& T, const uint8_t* b, int64_t n, BpeArr c, BpeArr r) {
+template <class LongF = BpeNoLong>
+TB_HD int32_t bpe_count_doc(const DevBpe& T, const uint8_t* b, int64_t n, BpeArr c, BpeArr r,
+                            LongF&& on_long = LongF{}) {
   if (T.n_added && bpe_has_added(T, b, n)) return kBpeHost;
-  const int64_t k = bpe_count_range(T, b, n, 0, n, c, r);
+  const int64_t k = bpe_count_range<true>(T, b, n, 0, n, c, r, on_long);
   if (k < 0 || k + T.post_add > 0x7FFFFFFF) return kBpeHost;
   return (int32_t)(k + T.post_add);
 }

@@ -360,17 +360,28 @@ PYBIND11_MODULE(_tbhost, m) {
       for (int t = 0; t < nt; ++t)
         th.emplace_back([&, t]() {
           uint32_t cbuf[kBpeMaxWord], rbuf[kBpeMaxWord];
+          std::vector<uint32_t> lc(kBpeMaxLong);
+          std::vector<uint64_t> lv(kBpeMaxLong);
+          std::vector<int32_t> lnx(kBpeMaxLong), lpv(kBpeMaxLong);
+          const uint8_t* b = nullptr;
+          // pre-tokens over kBpeMaxWord bytes: merged over arrays of their own length (as
+          // k_bpe_long does), up to kBpeMaxLong bytes
+          auto on_long = [&](int64_t s, int64_t e) -> int64_t {
+            if (e - s > kBpeMaxLong) return -1;
+            return bpe_word_long(T, b + s, (int)(e - s), lc.data(), lv.data(), lnx.data(), lpv.data());
+          };
           for (int64_t k = t; k < nd; k += nt) {
-            const uint8_t* b = d + o[k];
+            b = d + o[k];
             const int64_t n = o[k + 1] - o[k];
             if (chunk <= 0) {
-              out[k] = bpe_count_doc(T, b, n, BpeArr{cbuf, 1}, BpeArr{rbuf, 1});
+              out[k] = bpe_count_doc(T, b, n, BpeArr{cbuf, 1}, BpeArr{rbuf, 1}, on_long);
               continue;
             }
             int64_t tot = T.post_add;
             bool bad = T.n_added && bpe_has_added(T, b, n);
             for (int64_t s0 = 0; s0 < n && !bad; s0 += chunk) {
-              const int64_t x = bpe_count_range(T, b, n, s0, std::min(n, s0 + chunk), BpeArr{cbuf, 1}, BpeArr{rbuf, 1});
+              const int64_t x = bpe_count_range<true>(T, b, n, s0, std::min(n, s0 + chunk), BpeArr{cbuf, 1},
+                                                      BpeArr{rbuf, 1}, on_long);
               if (x < 0) bad = true;
               tot += x;
             }

@@ -91,13 +91,30 @@ def test_ascii_fast_path_matches_class_table():
 
 def test_gpt2_fixture_counts_equal_tokenizers():
     raw = check_equal(TokenCounterModel(GPT2_FIXTURE), corpus())
-    assert raw[-4] == -2 and raw[-3] == -2  # added-token text goes to the tokenizer
+    assert raw[-4] >= 0  # a 200-byte pre-token: merged natively (bpe_word_long)
+    assert raw[-3] == -2 and raw[-2] == -2  # added-token text goes to the tokenizer
 
 
 def test_trained_bpe_counts_equal_tokenizers(trained):
     m = TokenCounterModel(trained)
     assert m.bpe_spec().mask + 1 >= 2 * 3000
     check_equal(m, corpus())
+
+
+def test_long_pretokens_are_counted_natively(trained):
+    """Pre-tokens over the 64-byte lane arrays (URLs, base64, indentation and dash runs, long letter
+    runs) are merged by bpe_word_long, not sent to the host tokenizer: every document up to the
+    2048-byte pre-token limit gets the tokenizers count."""
+    m = TokenCounterModel(trained)
+    rng = np.random.default_rng(21)
+    texts = synth.inject_long_tokens(synth.make_corpus(600, 700, seed=22), 0.5, seed=1)
+    texts += [synth.long_tokens(rng) for _ in range(300)]
+    texts += ["a" * 2048, "b" * 2049, " " * 3000 + "x", "x" + "-" * 700 + "y", "ab" * 1500]
+    raw = check_equal(m, texts, max_host_frac=0.01)
+    long_ok = [t for t in texts if max(map(len, t.split()), default=0) <= 2048 and "b" * 2049 not in t
+               and " " * 2049 not in t and "ab" * 1100 not in t]
+    assert (raw[[texts.index(t) for t in long_ok]] >= 0).all()
+    assert raw[texts.index("b" * 2049)] == -2  # over the device limit: the host tokenizer
 
 
 def test_template_post_processor_adds_its_tokens(trained, tmp_path):

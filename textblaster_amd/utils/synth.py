@@ -224,6 +224,37 @@ def make_corpus(n_docs: int, mean_bytes: int = 1024, seed: int = 0,
     return docs
 
 
+def long_tokens(rng: np.random.Generator) -> str:
+    """A byte-level-BPE stress snippet: a long URL, a base64 blob, an indentation run or a dash rule
+    (pre-tokens of 64+ bytes: long letter / digit / punctuation / whitespace runs)."""
+    k = int(rng.integers(0, 5))
+    if k == 0:
+        path = "/".join("".join(chr(97 + int(c)) for c in rng.integers(0, 26, int(rng.integers(8, 40))))
+                        for _ in range(int(rng.integers(2, 6))))
+        return f"https://www.{path[:30]}.example.com/{path}?id={int(rng.integers(1, 10**9))}&ref=" + \
+            "".join(chr(97 + int(c)) for c in rng.integers(0, 26, 80))
+    if k == 1:
+        alpha = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/", np.uint8)
+        return bytes(alpha[rng.integers(0, 64, int(rng.integers(100, 1200)))]).decode() + "=="
+    if k == 2:
+        return "\n" + " " * int(rng.integers(64, 400)) + "indented();"
+    if k == 3:
+        return "\n" + "-" * int(rng.integers(64, 300)) + "\n"
+    return "".join(chr(97 + int(c)) for c in rng.integers(0, 26, int(rng.integers(65, 600))))
+
+
+def inject_long_tokens(texts: List[str], rate: float, seed: int = 0) -> List[str]:
+    """A fraction ``rate`` of the documents gets a long_tokens() snippet at a random space."""
+    rng = np.random.default_rng(8111 + seed)
+    out = list(texts)
+    for i in np.nonzero(rng.random(len(out)) < rate)[0].tolist():
+        t = out[i]
+        sp = [k for k in range(len(t)) if t[k] == " "]
+        at = sp[int(rng.integers(len(sp)))] + 1 if sp else 0
+        out[i] = t[:at] + long_tokens(rng) + " " + t[at:]
+    return out
+
+
 def inject_words(texts: List[str], list_path: str, rate: float, seed: int = 0) -> List[str]:
     """A fraction ``rate`` of the documents gets one entry of a word list (e.g. a C4 bad-words
     list) inserted after a random space, so a word-list filter has matches to act on."""

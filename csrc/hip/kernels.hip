@@ -94,10 +94,10 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
   if (x.par.leader() && src[0] >= 0) src[0] += slice_begin;
 }
 
-// The stage kernel is register-bound (occupancy = waves/SIMD the VGPR budget allows): it is built
-// for 4 waves/SIMD (128 VGPRs, a few bytes of spill). The unconstrained build (166 VGPRs, 3
-// waves/SIMD) and 5- / 6-wave budgets (spilling 180 / 240 B) measured 2-4 % slower
-// (profiles/README.md, round 2), so only this variant is built.
+// The stage kernel is register-bound (occupancy = waves/SIMD the VGPR budget allows). With the
+// n-gram orders moved to k_gr_ngrams / k_gr_split_wave it is built for 6 waves/SIMD (80 VGPRs)
+// with a 6.5 KB LDS slice per wave: 5.06 vs 5.26 ms per launch at 4 waves / 10 KB, 5 waves / 8 KB
+// no gain (profiles/r7_ngram/ab_occupancy.txt; before the move 4 waves won, round 2).
 #define TB_STAGE_KERNEL(NAME, ATTR)                                                                   \
   __global__ __launch_bounds__(64) ATTR void NAME(                                                   \
       const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes, \
@@ -117,7 +117,10 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
     analyze_stage<WavePar, false>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out); /* LD: own kernel */ \
   }
 
-TB_STAGE_KERNEL(k_stage_analyze_w4, __attribute__((amdgpu_waves_per_eu(4, 8))))
+#ifndef TB_STAGE_WPE
+#define TB_STAGE_WPE 6
+#endif
+TB_STAGE_KERNEL(k_stage_analyze_wave, __attribute__((amdgpu_waves_per_eu(TB_STAGE_WPE, 8))))
 
 // Long documents: one workgroup of kBlockThreads (8 waves by default) per document (BlockPar), launched
 // over the long prefix of the length-sorted permutation.
@@ -1434,8 +1437,8 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
   if (nblocks <= 0) nblocks = ndocs;  // grid: docs perm[0 .. nblocks)
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
-  if (waves != 4) return (int)hipErrorInvalidValue;  // the one build (see TB_STAGE_KERNEL)
-  auto kern = k_stage_analyze_w4;
+  if (waves != TB_STAGE_WPE) return (int)hipErrorInvalidValue;  // the one build (see TB_STAGE_KERNEL)
+  auto kern = k_stage_analyze_wave;
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64), lds_bytes, stream, (const DevPlan*)plan,
@@ -1688,6 +1691,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 }
 
 int tb_phase_slots() { return kPhaseSlots; }
+int tb_stage_waves() { return TB_STAGE_WPE; }  // waves per SIMD the wave stage kernel is built for
 
 int tb_abi_version() { return 18; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }

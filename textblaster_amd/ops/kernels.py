@@ -65,6 +65,7 @@ _SIGS = {
     "tbrt_memcpy_d2d": [_P, _P, _SZ, _P], "tbrt_memset": [_P, _I32, _SZ, _P],
     "tb_scan_strided_i64": [_P, _P, _I64, _I64, _P],
     "tb_phase_slots": [],
+    "tb_stage_waves": [],
     "tb_sizeof_plan": [],
     "tb_sizeof_stage": [],
     "tb_sizeof_c4": [],
@@ -169,7 +170,7 @@ class Kernels:
 
     def stage_analyze(self, plan, stage, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, flags,
                       lds_bytes=0, prof=None, waves=0, nblocks=0, dead=None, line_stats=None, gr_export=None):
-        """k_stage_analyze_w4; ``line_stats`` (uint32, >= 4 * (total bytes / 8 + 16 ndocs) + 16): the
+        """k_stage_analyze_wave; ``line_stats`` (uint32, >= 4 * (total bytes / 8 + 16 ndocs) + 16): the
         C4 line export (docproc.h StageOut::line_stats), document d at 4 * (off[d] / 8 + 16 d).
         ``gr_export`` (zeroed, >= nblocks descriptors): split mode, every launched document exports
         its word arrays and gr_split_wave finishes its n-gram orders."""

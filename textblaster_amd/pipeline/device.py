@@ -389,9 +389,9 @@ def bw_dead_max(plan: ExecPlan, passes, pass_of_step: Dict[int, int]) -> Dict[in
 
 class DeviceRunner:
     N_SLOTS = 2
-    # per-wave LDS slices: the stage kernel is built for 4 waves/SIMD (128 VGPRs) = 16 waves/CU, so
-    # 10 KB each costs no occupancy; the C4 kernel (7 waves/SIMD) only keeps per-line arrays there
-    DEFAULT_LDS_BYTES = 10240
+    # per-wave LDS slices: the stage kernel is built for W waves/SIMD (tb_stage_waves: 6 -> 80
+    # VGPRs) = 4 W waves/CU, so 160 KB / 4 W each costs no occupancy (6.5 KB at 6); the C4 kernel
+    # (7 waves/SIMD) only keeps per-line arrays there
     DEFAULT_LDS_BYTES_C4 = 2560
     DEFAULT_LONG_DOC_BYTES = 4096  # with the 3-per-CU workgroup kernel (profiles/r2_c5/long_doc_threshold.txt)
     DEFAULT_LDS_BYTES_BLK = 49152
@@ -402,7 +402,6 @@ class DeviceRunner:
     # 1,136 docs/s; at 64 KiB the pre-pass costs config 5 (~50 KB documents) 10 %, at 256 KiB
     # nothing (profiles/r5_pre/)
     DEFAULT_PRE_DOC_BYTES = 262144
-    DEFAULT_STAGE_WAVES = 4  # the stage kernel's register budget (the one variant built, kernels.hip)
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None, max_batch_bytes: int = 384 << 20,
                  token_counters=None):
@@ -548,11 +547,12 @@ class DeviceRunner:
                 self.k.pow_table(1 << 22)
             init.synchronize()  # uploads and the table are complete before any slot stream reads them
         # LDS arena per document (one wave per workgroup); TB_LDS_BYTES overrides for tuning
-        self.lds_bytes = int(os.environ.get("TB_LDS_BYTES", str(self.DEFAULT_LDS_BYTES)))
+        # the stage kernel's register budget (the one variant built, kernels.hip TB_STAGE_WPE)
+        self.stage_waves = int(self.k.lib.tb_stage_waves())
+        self.lds_bytes = int(os.environ.get("TB_LDS_BYTES", str((163840 // (4 * self.stage_waves)) & ~255)))
         self.lds_bytes_c4 = int(os.environ.get("TB_LDS_BYTES_C4", str(self.DEFAULT_LDS_BYTES_C4)))
         if not 0 <= self.lds_bytes_c4 <= 131072:
             raise DeviceError("TB_LDS_BYTES_C4 must be in [0, 131072]")
-        self.stage_waves = self.DEFAULT_STAGE_WAVES
         # documents longer than this run one workgroup (4 waves) each instead of one wave
         self.long_doc_bytes = int(os.environ.get("TB_LONG_DOC_BYTES", str(self.DEFAULT_LONG_DOC_BYTES)))
         if not 0 <= self.lds_bytes <= 131072:
@@ -583,7 +583,8 @@ class DeviceRunner:
         # wave documents finish their n-gram orders in one wave per (document, order)
         # (k_gr_split_wave, LDS slice TB_LDS_BYTES_SPLIT); TB_WAVE_SPLIT=0 keeps them in the stage
         self.wave_split = os.environ.get("TB_WAVE_SPLIT", "1") not in ("", "0")
-        self.lds_bytes_split = int(os.environ.get("TB_LDS_BYTES_SPLIT", "8192"))
+        # (6 KB: 2.81 ms/step vs 3.43 at 4 or 8 KB, profiles/r7_ngram/ab_occupancy.txt)
+        self.lds_bytes_split = int(os.environ.get("TB_LDS_BYTES_SPLIT", "6144"))
         self.ngram_block = os.environ.get("TB_NGRAM_BLOCK", "1") not in ("", "0")
         # wave documents longer than this take one wave per n-gram order (k_gr_split_wave), the
         # shorter ones one workgroup per document (k_gr_ngrams: 256 words, ~5.5 bytes per word on

@@ -82,7 +82,9 @@ step_pmc() {
   pmc_pass mem SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum &&
   pmc_pass hbm FETCH_SIZE SQ_INSTS_VALU SQ_INSTS_BRANCH SQ_INSTS_FLAT SQ_INSTS_FLAT_LDS_ONLY &&
   pmc_pass wr WRITE_SIZE SQ_INSTS_VMEM_WR SQ_VALU_MFMA_BUSY_CYCLES || return 1
-  python3 tools/pmc_summary.py $(find "$D/pmc" -name '*counter_collection.csv') --docs ${PMC_DOCS:-0} \
+  # documents per PMC run: (3 timed + 1 warmup steps) x bench.py's 262,144 per step unless
+  # BENCH_ARGS changes the batch (then set PMC_DOCS), so the summary prints bytes per document
+  python3 tools/pmc_summary.py $(find "$D/pmc" -name '*counter_collection.csv') --docs ${PMC_DOCS:-1048576} \
     > "$D/pmc_per_kernel.txt" 2>&1
   find "$D/pmc" -name '*.csv' -size +20M -delete
   head -40 "$D/pmc_per_kernel.txt"

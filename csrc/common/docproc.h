@@ -1174,8 +1174,9 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
 #ifdef TB_NO_SPLIT_LINES
   const bool split_lines = false;
 #else
-  const bool split_lines = ex && !x.in_lds(rs) && !x.in_lds(rl) && !x.in_lds(prs) && !x.in_lds(ph.ph8) &&
-                           !x.in_lds(c.ent) && !x.in_lds(c.off);
+  // (wave documents never: their split kernels run only the n-gram orders)
+  const bool split_lines = ex && P::kWaves != 1 && !x.in_lds(rs) && !x.in_lds(rl) && !x.in_lds(prs) &&
+                           !x.in_lds(ph.ph8) && !x.in_lds(c.ent) && !x.in_lds(c.off);
 #endif
   if (!split_lines)
     dup_spans(x, b, ph, NR + 1,

@@ -705,7 +705,7 @@ __global__ __launch_bounds__(64) void k_langid_features(
 // head transposed, 16 columns x 32 dims, integer bf16) and 16 lanes turn their row of the exact
 // fp32 result into the record (lid_decide_v3). Same records as LangidModel on the host.
 constexpr int kLidTile = 16;
-constexpr int kLidWaves = 4;
+constexpr int kLidWaves = 8;  // two documents per wave per tile
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -713,6 +713,78 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // bytes of dword q), p[2q + 1] dims 4q + 1, 4q + 3.
 __device__ __forceinline__ void lid_row_swar(const uint8_t* __restrict__ Eb, uint32_t g, uint32_t* p) {
   const uint4 w = *(const uint4*)(Eb + (size_t)g * kLidRowDim);
+  const uint32_t v[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    p[2 * q] += v[q] & 0x00FF00FFu;
+    p[2 * q + 1] += (v[q] >> 8) & 0x00FF00FFu;
+  }
+}
+
+// Pair table of the 1-/2-gram bag (built once per model by k_lid_pairs, copied into every
+// workgroup's LDS): over a 32-symbol alphabet — 0 = the word boundary / no letter, 1..26 = a-z
+// (the ASCII letter & 0x1F), 27..31 = æ ø å ä ö — entry (x, y) holds, pre-split into the packed
+// 16-bit layout of the bag's sums, every 1-/2-gram row a position with previous letter x and
+// letter y adds: y != 0: E[1-gram y] + E[2-gram (x or boundary, y)]; y == 0, x != 0: E[2-gram
+// (x, boundary)]; (0, 0): nothing. One position's orders 1 and 2 are then one LDS row (two
+// ds_read_b128 + 8 adds) instead of two hashes, two 16-byte gathers and 32 unpack/add
+// instructions. A position with a letter outside the alphabet takes the hashed gathers (rare in
+// the model's languages). The table is followed by one zero row: the gather of an n-gram a
+// position does not have points there, so the loop has no per-order branches.
+constexpr int kLidSyms = 32;
+constexpr int kLidPairs = kLidSyms * kLidSyms;
+constexpr uint32_t kLidSymMiss = 32;
+constexpr int kLidAuxBytes = kLidPairs * 32 + kLidRowDim;  // pair table + zero row
+
+// the letter of alphabet symbol i (0: the word boundary)
+__device__ __forceinline__ uint32_t lid_sym_letter(int i) {
+  if (i == 0) return kLidBoundary;
+  if (i <= 26) return 'a' + (uint32_t)(i - 1);
+  return i == 27 ? 0xE6 : i == 28 ? 0xF8 : i == 29 ? 0xE5 : i == 30 ? 0xE4 : 0xF6;
+}
+
+// symbol of a non-ASCII lowercase letter: 27..31, or kLidSymMiss
+__device__ __forceinline__ uint32_t lid_sym_latin(uint32_t l) {
+  return l == 0xE6 ? 27u : l == 0xF8 ? 28u : l == 0xE5 ? 29u : l == 0xE4 ? 30u : l == 0xF6 ? 31u : kLidSymMiss;
+}
+
+__global__ __launch_bounds__(256) void k_lid_pairs(const uint8_t* __restrict__ Eb, uint32_t* __restrict__ aux) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i < kLidPairs) {
+    const int x = i / kLidSyms, y = i % kLidSyms;
+    uint32_t d[kLidRowDim];
+#pragma unroll
+    for (int k = 0; k < kLidRowDim; ++k) d[k] = 0;
+    auto add = [&](uint32_t g) {
+      for (int k = 0; k < kLidRowDim; ++k) d[k] += Eb[(size_t)g * kLidRowDim + k];
+    };
+    if (y != 0) add(lid_hash(lid_sym_letter(y), 0, 0, 0, 1));
+    if (x != 0 || y != 0) add(lid_hash(lid_sym_letter(x), lid_sym_letter(y), 0, 0, 2));
+    // packed: dword 2q = dims 4q | 4q + 2 << 16, dword 2q + 1 = dims 4q + 1 | 4q + 3 << 16
+    for (int q = 0; q < 4; ++q) {
+      aux[i * 8 + 2 * q] = d[4 * q] | d[4 * q + 2] << 16;
+      aux[i * 8 + 2 * q + 1] = d[4 * q + 1] | d[4 * q + 3] << 16;
+    }
+  }
+  if (i < kLidRowDim / 4) aux[kLidPairs * 8 + i] = 0;  // the zero row
+}
+
+// the letter at lead byte `cur` = b[s] (< lim): ASCII and the Latin-1 block (lead byte 0xC3,
+// U+00C0..U+00FF: letters except U+00D7 / U+00F7, upper case U+00C0..U+00DE lowered by 0x20 —
+// the UCD's answers for that block) inline, the rest through the UCD tables (lid_letter)
+__device__ __forceinline__ uint32_t lid_letter_dev(uint32_t cur, const uint8_t* b, uint32_t n, uint32_t s,
+                                                   const UcdView& ucd) {
+  if (cur < 0x80u) return (cur | 0x20u) - 'a' < 26u ? (cur | 0x20u) : 0u;
+  if (cur == 0xC3u && s + 1 < n) {
+    const uint32_t c = 0xC0u | (b[s + 1] & 0x3Fu);
+    return (c == 0xD7u || c == 0xF7u) ? 0u : (c < 0xDFu ? c | 0x20u : c);
+  }
+  return lid_letter(ucd, b, n, s);
+}
+
+// Adds one 16-byte row (E + 128 bytes) to a bag's packed sums: p[2q] holds dims 4q, 4q + 2 (even
+// bytes of dword q), p[2q + 1] dims 4q + 1, 4q + 3.
+__device__ __forceinline__ void lid_add_u8(uint4 w, uint32_t* p) {
   const uint32_t v[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -759,10 +831,16 @@ __device__ __forceinline__ void lid_fold(uint32_t* pa, uint32_t* pb, int lane, i
   dsum += v1 + __shfl_xor(v1, 1);
 }
 
-// One document's quantised doc vector into A row `arow` (and its exponent / count).
+// One document's quantised doc vector into A row `arow` (and its exponent / count). Per 64-byte
+// chunk every lane handles the code point position at its byte: the letters of the previous
+// three positions come from the wave's slot array in LDS (slot 3 + r holds the letter of the
+// chunk's r-th position, slots 0..2 the last three of the previous chunks; the letter is stored
+// with its alphabet symbol in bits 24..29), orders 1 + 2 are one pair-table row (pairs, LDS), orders
+// 3 and 4 one hashed 16-byte gather each (an absent order gathers the zero row at `zero`).
 __device__ __forceinline__ void lid_doc_vector(const uint8_t* __restrict__ b, uint32_t n, const UcdView& ucd,
-                                               const uint8_t* __restrict__ Eb, uint32_t* flag, int lane,
-                                               uint16_t* arow, int32_t* e_out, int64_t* cnt_out) {
+                                               const uint8_t* __restrict__ Eb, const uint8_t* __restrict__ zero,
+                                               const uint4* pairs, uint32_t* slot, int lane, uint16_t* arow,
+                                               int32_t* e_out, int64_t* cnt_out) {
   // the cut: byte offset of code point kLidMaxCps (or n), by counting lead bytes per chunk
   uint32_t lim = n;
   if (n > (uint32_t)kLidMaxCps) {
@@ -780,68 +858,64 @@ __device__ __forceinline__ void lid_doc_vector(const uint8_t* __restrict__ b, ui
       seen += c;
     }
   }
-  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   uint32_t pa[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, pb[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
   int32_t dsum = 0;
   uint32_t cnt_lo = 0, cnt_hi = 0, chunks = 0;  // grams of the 1-2-gram / 3-4-gram bags
-  uint32_t c1 = 0, c2 = 0, c3 = 0;
+  const uint32_t B = kLidBoundary;
+  if (lane < 3) slot[lane] = 0;
   uint8_t cur = (uint32_t)lane < lim ? b[lane] : (uint8_t)0;
   for (uint32_t base = 0; base <= lim; base += 64) {
     const uint32_t s = base + (uint32_t)lane;
     const uint8_t nxt = s + 64 < lim ? b[s + 64] : (uint8_t)0;
     const bool lead = s < lim && utf8_is_lead(cur);
-    const uint32_t l0 = lead ? (cur < 0x80u ? ((cur | 0x20u) - 'a' < 26u ? (cur | 0x20u) : 0u)
-                                            : lid_letter(ucd, b, n, s))
-                             : 0u;
+    const bool emit = lead || s == lim;  // position lim: the virtual non-letter after the cut
+    uint32_t l0 = 0, y = 0;
+    if (lead) {
+      l0 = lid_letter_dev(cur, b, n, s, ucd);
+      y = l0 < 0x80u ? (l0 & 0x1Fu) : lid_sym_latin(l0);
+    }
     const uint64_t M = __ballot(lead);
-    uint64_t m = M & below;
-    uint32_t lm[3];
-    bool have[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      have[k] = m != 0;
-      const int j = have[k] ? lid_top(m) : lane;
-      if (have[k]) m &= ~(1ull << j);
-      lm[k] = (uint32_t)__shfl((int)l0, j);
-    }
-    if (lead || s == lim) {
-      if (!have[0]) {
-        lm[0] = c1; lm[1] = c2; lm[2] = c3;
-      } else if (!have[1]) {
-        lm[1] = c1; lm[2] = c2;
-      } else if (!have[2]) {
-        lm[2] = c1;
+    const uint64_t EM = __ballot(emit);
+    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(EM >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)EM, 0u));
+    if (lead) slot[3 + r] = l0 | y << 24;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t e1 = slot[2 + r], e2 = slot[1 + r], e3 = slot[r];
+    if (!emit) e1 = e2 = e3 = 0;
+    const uint32_t lm1 = e1 & 0xFFFFFFu, lm2 = e2 & 0xFFFFFFu, lm3 = e3 & 0xFFFFFFu;
+    const uint32_t x = e1 >> 24;  // symbol of the previous letter (0: none)
+    // orders 1 + 2
+    const bool miss = ((x | y) & kLidSymMiss) != 0;
+    const uint4* pr = pairs + 2 * (miss ? 0u : (x << 5 | y));
+    const uint4 t0 = pr[0], t1 = pr[1];
+    pa[0] += t0.x; pa[1] += t0.y; pa[2] += t0.z; pa[3] += t0.w;
+    pa[4] += t1.x; pa[5] += t1.y; pa[6] += t1.z; pa[7] += t1.w;
+    cnt_lo += (l0 != 0u) + ((l0 | lm1) != 0u);
+    if (__ballot(miss)) {
+      if (miss) {
+        if (l0) lid_add_u8(*(const uint4*)(Eb + (size_t)lid_hash(l0, 0, 0, 0, 1) * kLidRowDim), pa);
+        if (l0 | lm1)
+          lid_add_u8(*(const uint4*)(Eb + (size_t)lid_hash(lm1 ? lm1 : B, l0 ? l0 : B, 0, 0, 2) * kLidRowDim), pa);
       }
-      lid_grams_n(lm[2], lm[1], lm[0], l0, [&](uint32_t g, int order) {
-        if (order <= 2) {
-          lid_row_swar(Eb, g, pa);
-          ++cnt_lo;
-        } else {
-          lid_row_swar(Eb, g, pb);
-          ++cnt_hi;
-        }
-      });
     }
+    // orders 3 and 4
+    const uint32_t x0 = l0 ? l0 : B;
+    const bool v3 = lm1 != 0u, v4 = v3 && lm2 != 0u;
+    const uint8_t* g3 = v3 ? Eb + (size_t)lid_hash(lm2 ? lm2 : B, lm1, x0, 0, 3) * kLidRowDim : zero;
+    const uint8_t* g4 = v4 ? Eb + (size_t)lid_hash(lm3 ? lm3 : B, lm2, lm1, x0, 4) * kLidRowDim : zero;
+    lid_add_u8(*(const uint4*)g3, pb);
+    lid_add_u8(*(const uint4*)g4, pb);
+    cnt_hi += (uint32_t)v3 + (uint32_t)v4;
     if ((++chunks & 63u) == 0) lid_fold(pa, pb, lane, dsum);
-    if (M) {
-      uint64_t mm = M;
-      const int j0 = lid_top(mm);
-      mm &= ~(1ull << j0);
-      const uint32_t x0 = (uint32_t)__shfl((int)l0, j0);
-      if (!mm) {
-        c3 = c2; c2 = c1; c1 = x0;
-      } else {
-        const int j1 = lid_top(mm);
-        mm &= ~(1ull << j1);
-        const uint32_t x1 = (uint32_t)__shfl((int)l0, j1);
-        if (!mm) {
-          c3 = c1; c2 = x1; c1 = x0;
-        } else {
-          const uint32_t x2 = (uint32_t)__shfl((int)l0, lid_top(mm));
-          c3 = x2; c2 = x1; c1 = x0;
-        }
-      }
-    }
+    // carry: the last three positions' letters to slots 0..2
+    const uint32_t c = (uint32_t)__popcll(M);
+    uint32_t keep = 0;
+    if (lane < 3) keep = slot[c + lane];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < 3) slot[lane] = keep;
     cur = nxt;
   }
   lid_fold(pa, pb, lane, dsum);
@@ -867,56 +941,68 @@ __device__ __forceinline__ void lid_doc_vector(const uint8_t* __restrict__ b, ui
   }
   // (no dictionary-script flag: the language records are exact for every script; a document
   // with such code points goes to the CPU path only if it reaches a segmentation pass)
-  (void)flag;
 }
 
+// Persistent: each workgroup copies the pair table into LDS once and then takes tiles
+// blockIdx.x, blockIdx.x + gridDim.x, ... (the grid is what the CUs hold at once: 4 workgroups of
+// 8 waves per CU, 33 KB of pair table each).
 __global__ __launch_bounds__(64 * kLidWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_langid_mfma(
     const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off, const int32_t* __restrict__ perm,
-    int32_t ndocs, DevTables tabs, const uint8_t* __restrict__ Eb, const uint16_t* __restrict__ WT, double w_scale,
-    const float* __restrict__ bias, int64_t* rec, int32_t width, uint32_t* flags, uint64_t* prof) {
+    int32_t ndocs, DevTables tabs, const uint8_t* __restrict__ Eb, const uint8_t* __restrict__ aux,
+    const uint16_t* __restrict__ WT, double w_scale, const float* __restrict__ bias, int64_t* rec, int32_t width,
+    uint64_t* prof) {
   __shared__ __attribute__((aligned(16))) uint16_t A[kLidTile][kLidDim];
   __shared__ float Cm[kLidTile][kLidHeadCols];
   __shared__ int32_t ex[kLidTile];
   __shared__ int64_t cn[kLidTile];
+  __shared__ uint4 pairs[2 * kLidPairs];
+  __shared__ uint32_t slots[kLidWaves][68];
   const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
   const UcdView ucd{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
-  for (int r = w; r < kLidTile; r += kLidWaves) {
-    const int pos = (int)blockIdx.x * kLidTile + r;
-    const int doc = pos < ndocs ? (perm ? perm[pos] : pos) : -1;
-    if (doc < 0) {
-      if (lane < kLidDim) A[r][lane] = 0;
-      if (lane == 0) {
-        ex[r] = 0;
-        cn[r] = 0;
-      }
-      continue;
-    }
-    const uint64_t t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-    lid_doc_vector(bytes + off[doc], (uint32_t)(off[doc + 1] - off[doc]), ucd, Eb, flags + doc, lane, A[r], &ex[r],
-                   &cn[r]);
-    if (prof && lane == 0) prof[(size_t)doc * kPhaseSlots + PH_LID] += __builtin_amdgcn_s_memtime() - t0;
-  }
+  for (int i = (int)threadIdx.x; i < 2 * kLidPairs; i += 64 * kLidWaves) pairs[i] = ((const uint4*)aux)[i];
+  const uint8_t* zero = aux + kLidPairs * 32;
   __syncthreads();
-  if (w == 0) {
-    // lane l: A[row l & 15][k 8 (l >> 4) .. +8), B[k 8 (l >> 4) .. +8][col l & 15] (= WT row)
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(&A[lane & 15][8 * (lane >> 4)]);
-    const bf16x8 bw = *reinterpret_cast<const bf16x8*>(WT + (lane & 15) * kLidDim + 8 * (lane >> 4));
-    f32x4 c = {0.f, 0.f, 0.f, 0.f};
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw, c, 0, 0, 0);
-    // D[row (l >> 4) * 4 + r][col l & 15]
-#pragma unroll
-    for (int r = 0; r < 4; ++r) Cm[(lane >> 4) * 4 + r][lane & 15] = c[r];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const int p2 = (int)blockIdx.x * kLidTile + lane;
-    if (lane < kLidTile && p2 < ndocs) {
-      const int d2 = perm ? perm[p2] : p2;
-      double C[kLidLangs];
-#pragma unroll
-      for (int l = 0; l < kLidLangs; ++l) C[l] = (double)Cm[lane][l];
-      lid_decide_v3(C, ex[lane], cn[lane], w_scale, bias, rec + (int64_t)d2 * width);
+  const int ntiles = (ndocs + kLidTile - 1) / kLidTile;
+  for (int tile = (int)blockIdx.x; tile < ntiles; tile += (int)gridDim.x) {
+    for (int r = w; r < kLidTile; r += kLidWaves) {
+      const int pos = tile * kLidTile + r;
+      const int doc = pos < ndocs ? (perm ? perm[pos] : pos) : -1;
+      if (doc < 0) {
+        if (lane < kLidDim) A[r][lane] = 0;
+        if (lane == 0) {
+          ex[r] = 0;
+          cn[r] = 0;
+        }
+        continue;
+      }
+      const uint64_t t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+      lid_doc_vector(bytes + off[doc], (uint32_t)(off[doc + 1] - off[doc]), ucd, Eb, zero, pairs, slots[w], lane,
+                     A[r], &ex[r], &cn[r]);
+      if (prof && lane == 0) prof[(size_t)doc * kPhaseSlots + PH_LID] += __builtin_amdgcn_s_memtime() - t0;
     }
+    __syncthreads();
+    if (w == 0) {
+      // lane l: A[row l & 15][k 8 (l >> 4) .. +8), B[k 8 (l >> 4) .. +8][col l & 15] (= WT row)
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&A[lane & 15][8 * (lane >> 4)]);
+      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(WT + (lane & 15) * kLidDim + 8 * (lane >> 4));
+      f32x4 c = {0.f, 0.f, 0.f, 0.f};
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw, c, 0, 0, 0);
+      // D[row (l >> 4) * 4 + r][col l & 15]
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Cm[(lane >> 4) * 4 + r][lane & 15] = c[r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      const int p2 = tile * kLidTile + lane;
+      if (lane < kLidTile && p2 < ndocs) {
+        const int d2 = perm ? perm[p2] : p2;
+        double C[kLidLangs];
+#pragma unroll
+        for (int l = 0; l < kLidLangs; ++l) C[l] = (double)Cm[lane][l];
+        lid_decide_v3(C, ex[lane], cn[lane], w_scale, bias, rec + (int64_t)d2 * width);
+      }
+    }
+    __syncthreads();  // A / Cm / ex / cn are the next tile's
   }
 }
 
@@ -1601,18 +1687,36 @@ int tb_langid_features(hipStream_t stream, const uint8_t* bytes, const int64_t* 
   return (int)hipGetLastError();
 }
 
-// k_langid_mfma: records of every document (perm order, 16 per workgroup); Eb = E + 128 as uint8
-// [buckets * 16] (the biased block-sparse embedding table),
-// WT bf16 bits [16 * 32] (the head transposed, columns >= 5 zero), bias float [8].
+// The pair table of k_langid_mfma (+ its zero row) from the embedding table, into aux
+// [tb_langid_aux_bytes()]: once per model.
+int tb_langid_aux_bytes() { return kLidAuxBytes; }
+int tb_langid_prepare(hipStream_t stream, const uint8_t* E, uint8_t* aux) {
+  if (!E || !aux) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_lid_pairs, dim3((kLidPairs + 255) / 256), dim3(256), 0, stream, E, (uint32_t*)aux);
+  return (int)hipGetLastError();
+}
+
+// k_langid_mfma: records of every document (perm order, 16 per tile); Eb = E + 128 as uint8
+// [buckets * 16] (the biased block-sparse embedding table), aux its pair table
+// (tb_langid_prepare), WT bf16 bits [16 * 32] (the head transposed, columns >= 5 zero), bias float [8].
 int tb_langid_mfma(hipStream_t stream, const uint8_t* bytes, const int64_t* off, const int32_t* perm, int32_t ndocs,
                    const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, const uint8_t* E,
-                   const uint16_t* WT, double w_scale, const float* bias, int64_t* rec, int32_t width,
-                   uint32_t* flags, uint64_t* prof) {
+                   const uint8_t* aux, const uint16_t* WT, double w_scale, const float* bias, int64_t* rec,
+                   int32_t width, uint64_t* prof) {
   if (ndocs <= 0) return 0;
-  if (!E || !WT || !bias || !rec || width < 2 || !(w_scale > 0)) return (int)hipErrorInvalidValue;
+  if (!E || !aux || !WT || !bias || !rec || width < 2 || !(w_scale > 0)) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
-  hipLaunchKernelGGL(k_langid_mfma, dim3((ndocs + kLidTile - 1) / kLidTile), dim3(64 * kLidWaves), 0, stream, bytes,
-                     off, perm, ndocs, t, E, WT, w_scale, bias, rec, width, flags, prof);
+  const int ntiles = (ndocs + kLidTile - 1) / kLidTile;
+  static int cus = 0;
+  if (cus <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+        hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const int grid = ntiles < 4 * cus ? ntiles : 4 * cus;
+  hipLaunchKernelGGL(k_langid_mfma, dim3(grid), dim3(64 * kLidWaves), 0, stream, bytes, off, perm, ndocs, t, E, aux,
+                     WT, w_scale, bias, rec, width, prof);
   return (int)hipGetLastError();
 }
 
@@ -1693,7 +1797,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 int tb_phase_slots() { return kPhaseSlots; }
 int tb_stage_waves() { return TB_STAGE_WPE; }  // waves per SIMD the wave stage kernel is built for
 
-int tb_abi_version() { return 18; }
+int tb_abi_version() { return 19; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

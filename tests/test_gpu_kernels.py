@@ -220,6 +220,11 @@ def test_langid_edge_cases_bit_exact(host, runner_parts):
         texts.append(t[:k])
     for shift in range(8):  # multibyte letters straddling the chunk edge at every offset
         texts.append("a" * (60 + shift) + "ææææ øå bcd")
+    # the kernel's inline Latin-1 letters (U+00C0..U+00FF, incl. the non-letters × and ÷) and its
+    # pair-table alphabet edges: letters outside it (é, ü, ß, Þ, Greek, Cyrillic, CJK) next to ones in it
+    latin1 = "".join(chr(c) for c in range(0xC0, 0x100))
+    texts += [latin1, " ".join(latin1[i:i + 3] for i in range(0, 64, 3)), "éa aé éé üøß Þorn þá ×÷ ÿ",
+              "Ωmega ωα aω Ж жa 中文a aä öü ÅÄÖ", "æ" * 40 + "é" + "ø" * 40, "a\xc3"]
     _, _, _, runner, lid = runner_parts
     data, off = synth.pack(texts)
     res = runner.run(data, off)

@@ -22,7 +22,7 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32, _P,
@@ -46,7 +46,9 @@ _SIGS = {
     "tb_badwords_match": [_P, _P, _P, _I32, _P, _P, _I32, _I32, _P, _U32, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                           _U32],
     "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _U32, _P],
-    "tb_langid_mfma": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, ctypes.c_double, _P, _P, _I32, _P, _P],
+    "tb_langid_mfma": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, ctypes.c_double, _P, _P, _I32, _P],
+    "tb_langid_prepare": [_P, _P, _P],
+    "tb_langid_aux_bytes": [],
     "tb_c4_pass_b": [_P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "tb_pow_table": [_P, _P, _U32],
     "tb_html_sizes": [_P, _P, _P, _I32, _P, _P, _P, _P, _I32, _P, _U32, _P],
@@ -297,23 +299,39 @@ class Kernels:
             bias.data_ptr(), rec.data_ptr(), width, flags.data_ptr(), lds_bytes, _ptr(prof))
         _check(rc, "tb_langid_features")
 
-    def langid_mfma(self, bytes_, off, perm, ndocs, E, WT, w_scale, bias, rec, width, flags, prof=None):
+    def langid_prepare(self, E):
+        """The pair table of k_langid_mfma (orders 1 + 2 of every position over a 32-letter alphabet,
+        + a zero row) built on the device from the embedding table ``E`` (E + 128, uint8); once per
+        model. Returns the device buffer to pass as ``aux``."""
+        from .. import native
+        from . import hiprt
+
+        h = native.host()
+        if E.numel() != h.LID_BUCKETS * h.LID_ROW_DIM:
+            raise DeviceError("langid_prepare: operand shapes")
+        aux = hiprt.empty(int(self.lib.tb_langid_aux_bytes()), np.uint8)
+        _check(self.lib.tb_langid_prepare(self.stream(), E.data_ptr(), aux.data_ptr()), "tb_langid_prepare")
+        hiprt.current_stream().synchronize()
+        return aux
+
+    def langid_mfma(self, bytes_, off, perm, ndocs, E, aux, WT, w_scale, bias, rec, width, prof=None):
         """k_langid_mfma (v3 model): fastText int8 embedding bag + bf16 MFMA head, 16 documents per
-        workgroup; the language record of every document into ``rec`` (document d at
-        rec[d * width]). ``E``: the embedding table as E + 128, uint8 [buckets * 16], ``WT``: bf16
-        bits [16 * 32] (head transposed),
-        ``bias``: float32 [8] (csrc/common/langid.h)."""
+        tile; the language record of every document into ``rec`` (document d at rec[d * width]).
+        ``E``: the embedding table as E + 128, uint8 [buckets * 16], ``aux``: its pair table
+        (langid_prepare), ``WT``: bf16 bits [16 * 32] (head transposed), ``bias``: float32 [8]
+        (csrc/common/langid.h)."""
         from .. import native
 
         h = native.host()
         t = self.tabs
         if (E.numel() != h.LID_BUCKETS * h.LID_ROW_DIM or WT.numel() != 16 * h.LID_DIM or bias.numel() != h.LID_ROW
-                or width < 2 or rec.numel() < ndocs * width or not w_scale > 0):
+                or width < 2 or rec.numel() < ndocs * width or not w_scale > 0
+                or aux.numel() != int(self.lib.tb_langid_aux_bytes())):
             raise DeviceError("langid_mfma: operand shapes")
         rc = self.lib.tb_langid_mfma(
             self.stream(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs, t[0].data_ptr(), t[1].data_ptr(),
-            t[2].data_ptr(), t[3].data_ptr(), E.data_ptr(), WT.data_ptr(), float(w_scale), bias.data_ptr(),
-            rec.data_ptr(), width, flags.data_ptr(), _ptr(prof))
+            t[2].data_ptr(), t[3].data_ptr(), E.data_ptr(), aux.data_ptr(), WT.data_ptr(), float(w_scale),
+            bias.data_ptr(), rec.data_ptr(), width, _ptr(prof))
         _check(rc, "tb_langid_mfma")
 
     def c4_pass_a(self, c4, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags, lds_bytes=0,

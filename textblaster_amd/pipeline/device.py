@@ -514,6 +514,7 @@ class DeviceRunner:
                     # v3: int8 embedding rows, biased to E + 128 as bytes for the kernel's SWAR sums
                     # (2 MB, L2-resident), + the bf16 MFMA head operand
                     self.lid_E = hiprt.to_device((langid.E.astype(np.int16) + 128).astype(np.uint8))
+                    self.lid_aux = self.k.langid_prepare(self.lid_E)  # 1-/2-gram pair table
                     self.lid_WT = hiprt.to_device(np.ascontiguousarray(langid.head_bf16_t()).reshape(-1))
                     self.lid_w_scale = float(langid.w_scale)
                 else:
@@ -743,8 +744,8 @@ class DeviceRunner:
         """Language-id records of a content version: k_langid_mfma (v3: embedding bag + bf16 MFMA
         head) or k_langid_features (v2: folded logit table)."""
         if self.lid_version == 3:
-            self.k.langid_mfma(vb, vo, d_perm, ndocs, self.lid_E, self.lid_WT, self.lid_w_scale, self.lid_b, rec,
-                               width, flags, prof)
+            self.k.langid_mfma(vb, vo, d_perm, ndocs, self.lid_E, self.lid_aux, self.lid_WT, self.lid_w_scale,
+                               self.lid_b, rec, width, prof)
         else:
             self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_P, self.lid_b, rec, width, flags,
                                    self.lds_bytes_lid, prof)

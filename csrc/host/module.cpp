@@ -218,6 +218,7 @@ PYBIND11_MODULE(_tbhost, m) {
   // c4_filters.rs:464-468) as an index into the returned name list, -1 when absent.
   m.def("meta_languages", [](py::array_t<uint8_t, py::array::c_style> md, py::array_t<int64_t, py::array::c_style> mo,
                              py::object mv, int nthreads) {
+    PoolTag pool_tag("meta_languages");
     const int64_t n = (int64_t)mo.size() - 1;
     const uint8_t* valid = nullptr;
     py::array_t<uint8_t, py::array::c_style> va;
@@ -262,6 +263,7 @@ PYBIND11_MODULE(_tbhost, m) {
   m.def("bw_match_batch", [](py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
                              py::array_t<uint32_t, py::array::c_style> table, py::object roots, py::object cjk,
                              int32_t root0, int32_t cjk0, py::object dead, uint32_t dead_max, int nthreads) {
+    PoolTag pool_tag("badwords");
     const int64_t n = (int64_t)off.size() - 1;
     const uint64_t slots = (uint64_t)table.size() / 4;
     if (n < 0 || slots == 0 || (slots & (slots - 1))) throw std::invalid_argument("bw_match_batch: shapes");
@@ -448,6 +450,7 @@ PYBIND11_MODULE(_tbhost, m) {
   });
   m.def("html_decode_batch", [](py::array_t<uint8_t, py::array::c_style> data,
                                 py::array_t<int64_t, py::array::c_style> off, int nthreads) -> py::object {
+    PoolTag pool_tag("html_decode");
     const int64_t n = (int64_t)off.size() - 1;
     const char* d = (const char*)data.data();
     const int64_t* o = off.data();
@@ -595,6 +598,7 @@ PYBIND11_MODULE(_tbhost, m) {
   // Spans idx[k] of a packed (text, off) column gathered into a new packed column (multithreaded).
   m.def("gather_spans", [](py::array_t<uint8_t, py::array::c_style> text, py::array_t<int64_t, py::array::c_style> off,
                            py::array_t<int64_t, py::array::c_style> idx, int nthreads) {
+    PoolTag pool_tag("gather_spans");
     const int64_t n = (int64_t)off.size() - 1, m = (int64_t)idx.size();
     const int64_t* o = off.data();
     const int64_t* ix = idx.data();
@@ -621,7 +625,14 @@ PYBIND11_MODULE(_tbhost, m) {
   }, py::arg("text"), py::arg("off"), py::arg("idx"), py::arg("nthreads") = 8);
 
   // Multi-threaded memcpy into a (pinned) staging buffer: dst[dst_off : dst_off + src.nbytes] = src.
+  // CPU seconds of the native worker pool per job tag (PoolTag), since process start
+  m.def("pool_cpu_stats", []() {
+    py::dict d;
+    for (auto& kv : pool_cpu_stats()) d[py::str(kv.first)] = kv.second;
+    return d;
+  });
   m.def("parallel_copy", [](py::array dst, int64_t dst_off, py::array src, int nthreads) {
+    PoolTag pool_tag("stage_copy");
     if (!(dst.flags() & py::array::c_style) || !(src.flags() & py::array::c_style))
       throw std::invalid_argument("parallel_copy needs contiguous arrays");
     const int64_t nb = (int64_t)src.nbytes();

@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <ctime>
 #include <fstream>
 #include <condition_variable>
 #include <mutex>
@@ -24,20 +25,46 @@ namespace tb {
 // caller always works on its own job, so a job completes even when every worker is busy
 // elsewhere. Workers live for the whole process (no per-call thread creation).
 namespace {
+thread_local const char* tl_pool_tag = nullptr;
+
+struct TagStats {
+  std::mutex mu;
+  std::vector<std::pair<const char*, std::atomic<uint64_t>*>> ns;  // tag -> CPU nanoseconds
+  std::atomic<uint64_t>* slot(const char* tag) {
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& e : ns)
+      if (e.first == tag) return e.second;
+    ns.emplace_back(tag, new std::atomic<uint64_t>(0));
+    return ns.back().second;
+  }
+};
+TagStats& tag_stats() {
+  static TagStats* t = new TagStats();  // leaked on purpose: pool workers outlive statics
+  return *t;
+}
+uint64_t thread_cpu_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
 struct PoolJob {
   const std::function<void(int64_t)>* fn;
   int64_t nchunks;
   int max_helpers;
+  std::atomic<uint64_t>* cpu = nullptr;  // the submitter's tag counter
   std::atomic<int64_t> next{0};
   std::atomic<int64_t> done{0};
   int helpers = 0;   // workers that took the job (guarded by the pool mutex)
   int active = 0;    // workers still inside work() (guarded by the pool mutex)
   void work() {
+    const uint64_t t0 = thread_cpu_ns();
     int64_t c;
     while ((c = next.fetch_add(1, std::memory_order_relaxed)) < nchunks) {
       (*fn)(c);
       done.fetch_add(1, std::memory_order_release);
     }
+    cpu->fetch_add(thread_cpu_ns() - t0, std::memory_order_relaxed);
   }
 };
 
@@ -51,6 +78,7 @@ class WorkerPool {
     PoolJob job;
     job.fn = &fn;
     job.nchunks = nchunks;
+    job.cpu = tag_stats().slot(tl_pool_tag ? tl_pool_tag : "other");
     job.max_helpers = std::max(0, nthreads - 1);
     {
       std::unique_lock<std::mutex> g(mu_);
@@ -96,10 +124,24 @@ class WorkerPool {
 };
 }  // namespace
 
+PoolTag::PoolTag(const char* name) : prev(tl_pool_tag) { tl_pool_tag = name; }
+PoolTag::~PoolTag() { tl_pool_tag = prev; }
+
+std::vector<std::pair<std::string, double>> pool_cpu_stats() {
+  TagStats& t = tag_stats();
+  std::lock_guard<std::mutex> g(t.mu);
+  std::vector<std::pair<std::string, double>> out;
+  for (auto& e : t.ns) out.emplace_back(e.first, 1e-9 * (double)e.second->load(std::memory_order_relaxed));
+  return out;
+}
+
 void parallel_tasks(int64_t ntasks, int nthreads, const std::function<void(int64_t)>& fn) {
   if (ntasks <= 0) return;
   if (nthreads <= 1 || ntasks == 1) {
+    // on the caller alone: charged to its tag too
+    const uint64_t t0 = thread_cpu_ns();
     for (int64_t c = 0; c < ntasks; ++c) fn(c);
+    tag_stats().slot(tl_pool_tag ? tl_pool_tag : "other")->fetch_add(thread_cpu_ns() - t0, std::memory_order_relaxed);
     return;
   }
   WorkerPool::get().run(ntasks, (int)std::min<int64_t>(nthreads, ntasks), fn);
@@ -107,7 +149,10 @@ void parallel_tasks(int64_t ntasks, int nthreads, const std::function<void(int64
 
 void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t, int64_t)>& fn) {
   if (n <= 0) return;
-  if (nthreads <= 1 || n < 256) { fn(0, n); return; }
+  if (nthreads <= 1 || n < 256) {
+    parallel_tasks(1, 1, [&](int64_t) { fn(0, n); });
+    return;
+  }
   const int64_t chunks = std::min<int64_t>((int64_t)nthreads * 8, (n + 63) / 64);
   parallel_tasks(chunks, nthreads, [&](int64_t c) { fn(n * c / chunks, n * (c + 1) / chunks); });
 }
@@ -272,6 +317,7 @@ BadWordsAutomaton BadWordsModule::flatten() const {
 }
 
 void BatchState::gather(const std::vector<int64_t>& idx, RawBuf& data, std::vector<int64_t>& off) const {
+  PoolTag pool_tag("gather");
   const int64_t m = (int64_t)idx.size();
   off.assign(m + 1, 0);
   for (int64_t k = 0; k < m; ++k) off[k + 1] = off[k] + (int64_t)content(idx[k]).size();
@@ -432,6 +478,7 @@ bool BatchState::input_meta(int64_t i, FlatMeta& out) const {
 
 void BatchState::apply_records(const StepCfg& cfg, int step_index, const int64_t* rec, int width,
                                int rewrite_version) {
+  PoolTag pool_tag("apply_records");
   StepRec& sr = step_slot(step_index);
   sr.cfg = std::make_unique<StepCfg>(cfg);
   sr.rec = rec;
@@ -449,6 +496,7 @@ void BatchState::apply_records(const StepCfg& cfg, int step_index, const int64_t
 
 void BatchState::badwords_lang_codes(const StepCfg& cfg, BadWordsModule& mod, std::vector<int32_t>& code,
                                      std::vector<std::string>& names) const {
+  PoolTag pool_tag("badwords");
   // The document language: metadata "language" (no step writes that key, so only the input
   // metadata can hold it), else the configured default (reference c4_filters.rs:464-468); as an
   // index into `names` (names[0] = the default), -1 for documents already filtered.
@@ -577,6 +625,7 @@ void BatchState::apply_badwords_codes(const StepCfg& cfg, int step_index, BadWor
 
 void BatchState::run_cpu(const std::vector<StepCfg>& steps, int begin, int end, SegBackend be,
                          const LangidModel* lid, BadWordsModule* bw) {
+  PoolTag pool_tag("cpu_steps");
   for (int s = begin; s < end; ++s) {
     const StepCfg& cfg = steps[s];
     if (cfg.kind == StepKind::C4BadWords) {
@@ -703,6 +752,23 @@ void BatchState::step_meta_json(int64_t doc, int s, CharBuf& out, bool& first) c
   }
   if (s >= (int)recs_.size() || !recs_[s].cfg) return;
   const StepRec& sr = recs_[s];
+  const int fs = fail_step_[doc];
+  if (fs < 0 || s < fs) {
+    // the step passed: its members are constants for these kinds (filters.cpp decide_t's pass
+    // branches), no need to re-run the decision
+    auto lit = [&](std::string_view member) {
+      if (!first) out.push_back(',');
+      first = false;
+      out.append(member.data(), member.size());
+    };
+    switch (sr.cfg->kind) {
+      case StepKind::GopherQuality: lit("\"gopher_quality_filter_status\":\"passed\""); return;
+      case StepKind::GopherRepetition: lit("\"gopher_repetition_filter_status\":\"passed\""); return;
+      case StepKind::C4Quality: lit("\"c4_filter_status\":\"passed\""); return;
+      case StepKind::FineWebQuality: return;
+      default: break;
+    }
+  }
   decide_meta_json(*sr.cfg, sr.rec + doc * sr.width, out, first);
 }
 
@@ -718,6 +784,23 @@ namespace {
 std::mutex g_charbuf_mu;
 std::vector<std::unique_ptr<CharBuf>>* g_charbufs = new std::vector<std::unique_ptr<CharBuf>>();
 }  // namespace
+
+// Every metadata key a step decision can write (filters.cpp decide_t, step_meta): an input key
+// outside this list cannot be overwritten by a step.
+static bool meta_collides(const FlatMeta& fm) {
+  static const std::string_view kStepKeys[] = {
+      "gopher_quality_filter_status", "gopher_quality_filter_reasons", "gopher_repetition_filter_status",
+      "gopher_repetition_filter_reasons", "gopher_repetition_filter_reason", "c4_filter_status",
+      "c4_filter_reasons", "line-filter-too_long_word", "line-filter-no_terminal_punc",
+      "line-filter-too_few_words", "fineweb_filter_status", "fineweb_filter_reason", "Detected language",
+      "Detected language confidence", "token_count", "c4_badwords_filter_status", "c4_badwords_filter_reason"};
+  for (const auto& e : fm.e) {
+    const std::string_view k = fm.key(e);
+    for (const auto& sk : kStepKeys)
+      if (k == sk) return true;
+  }
+  return false;
+}
 
 static std::unique_ptr<CharBuf> take_charbuf() {
   std::lock_guard<std::mutex> g(g_charbuf_mu);
@@ -736,6 +819,7 @@ static void give_charbuf(std::unique_ptr<CharBuf> p) {
 void BatchState::assemble(const std::vector<int64_t>& idx, RawBuf& text_data, std::vector<int64_t>& text_off,
                           RawBuf& meta_data, std::vector<int64_t>& meta_off,
                           std::vector<uint8_t>& meta_valid, bool with_text) const {
+  PoolTag pool_tag("assemble");
   const int64_t m = (int64_t)idx.size();
   // text: sizes are known up front -> offsets, then one parallel gather into the final buffer
   // (with_text=false: the device compacted the texts already, only the metadata is built here)
@@ -799,6 +883,30 @@ void BatchState::assemble(const std::vector<int64_t>& idx, RawBuf& text_data, st
           if (!input_meta(i, fm)) meta_fail_.fetch_add(1, std::memory_order_relaxed);
         } else {
           fm.clear();
+        }
+        if (fast_meta && !meta_collides(fm)) {
+          // the input members (in input order), then the steps' members: what the map below
+          // produces when no step key is among the input keys (set() then only appends)
+          const size_t before = md.size();
+          md.push_back('{');
+          bool first = true;
+          for (const auto& e : fm.e) {
+            if (!first) md.push_back(',');
+            first = false;
+            json_escape_append(md, fm.key(e));
+            md.push_back(':');
+            json_escape_append(md, fm.value(e));
+          }
+          for (int s = 0; s <= last; ++s) step_meta_json(i, s, md, first);
+          if (first) {
+            md.resize(before);
+            meta_off[k + 1] = 0;
+          } else {
+            md.push_back('}');
+            meta_off[k + 1] = (int64_t)(md.size() - before);
+            meta_valid[k] = 1;
+          }
+          continue;
         }
         for (int s = 0; s <= last; ++s) {
           step_meta(i, s, d);

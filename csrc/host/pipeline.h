@@ -26,6 +26,17 @@ void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t, int
 // fn(task) for task in [0, ntasks) on the worker pool, at most nthreads at a time.
 void parallel_tasks(int64_t ntasks, int nthreads, const std::function<void(int64_t)>& fn);
 
+// CPU-time attribution of the pool: the jobs a thread submits while a PoolTag is alive are
+// charged to its name (thread CPU time of the caller and of every worker inside the job);
+// untagged jobs go to "other". Names must be string literals.
+struct PoolTag {
+  explicit PoolTag(const char* name);
+  ~PoolTag();
+  const char* prev;
+};
+// (name, CPU seconds) of every tag so far
+std::vector<std::pair<std::string, double>> pool_cpu_stats();
+
 struct LangidModel {
   int version = 2;         // 2: folded int16 logit table (P); 3: int8 embeddings + MFMA head (E, W)
   std::vector<int16_t> P;  // v2: [kLidBuckets * kLidRow] fixed-point logit rows (csrc/common/langid.h)

@@ -58,3 +58,27 @@ def test_direct_json_metadata_equals_map_path(monkeypatch):
     slow = _collect(eng, data, off, None)
     assert fast == slow
     assert sum(1 for _, m in fast if m) > 500
+
+
+def test_direct_json_metadata_with_input_metadata(monkeypatch):
+    """Input metadata (the CLI path's common case): the direct path appends the steps' members to
+    the input members; inputs holding a key a step writes, invalid JSON, empty objects, escapes and
+    null rows must come out exactly as from the map-based path."""
+    cfg = load_pipeline_config(os.path.join(ROOT, "config", "bench_pipeline.yaml"))
+    eng = Engine(cfg, backend="cpu", segmentation="rules", nthreads=2)
+    texts = synth.make_corpus(600, 600, seed=22)
+    data, off = synth.pack(texts)
+    kinds = ['{"url":"https://example.com/%d"}', '{}', 'not json', '{"c4_filter_status":"x","a":"b"}',
+             '{"Detected language":"xx"}', '{"k\\"q":"v\\\\n\\u00e6 \\u4e2d"}', '{"a":"1","b":"2","c":"3"}', None]
+    metas = [kinds[i % len(kinds)] for i in range(len(texts))]
+    enc = [(m % i if "%d" in m else m).encode() if m is not None else b"" for i, m in enumerate(metas)]
+    mo = np.zeros(len(enc) + 1, dtype=np.int64)
+    np.cumsum([len(e) for e in enc], out=mo[1:])
+    md = np.frombuffer(b"".join(enc), dtype=np.uint8).copy()
+    mv = np.array([m is not None for m in metas], dtype=np.uint8)
+    monkeypatch.setenv("TB_META_FAST", "1")
+    fast = _collect(eng, data, off, (md, mo, mv))
+    monkeypatch.setenv("TB_META_FAST", "0")
+    slow = _collect(eng, data, off, (md, mo, mv))
+    assert fast == slow
+    assert any(m and m.startswith(b'{"url"') for _, m in fast)

@@ -63,6 +63,17 @@ def thread_cpu() -> dict:
     return out
 
 
+def _pool_stats() -> dict:
+    from textblaster_amd import native
+
+    return dict(native.host().pool_cpu_stats())
+
+
+def _delta(before: dict, after: dict) -> dict:
+    d = {k: round(v - before.get(k, 0.0), 3) for k, v in after.items()}
+    return {k: v for k, v in sorted(d.items(), key=lambda kv: -kv[1]) if v > 0.005}
+
+
 def cpu_by_name(before: dict, after: dict) -> dict:
     agg: dict = {}
     for k, v in after.items():
@@ -106,6 +117,7 @@ def main():
         tl = os.path.join(args.out, f"timeline_{backend}.json") if args.timeline else None
         tracing.record_timeline(tl)
         cpu0 = thread_cpu()
+        pool0 = _pool_stats()
         st = run(RunConfig(inp, o, e, args.config, backend=backend, unit_rows=args.unit_rows,
                            html_decode=args.html_decode))
         cpu = cpu_by_name(cpu0, thread_cpu())
@@ -117,7 +129,9 @@ def main():
                 # thread name of the threads alive at its end (native pools)
                 "cpu_seconds": {k[4:]: round(v, 3) for k, v in st.phase_seconds.items() if k.startswith("cpu_")},
                 "cpu_us_per_doc": round(1e6 * st.phase_seconds.get("cpu_total", 0.0) / max(st.docs, 1), 3),
-                "cpu_seconds_by_os_thread": cpu}
+                "cpu_seconds_by_os_thread": cpu,
+                # the native worker pool's CPU seconds by job (tb-pool threads + the submitting thread)
+                "pool_cpu_seconds_by_job": _delta(pool0, _pool_stats())}
         print(json.dumps(line), flush=True)
         rates.setdefault(backend, []).append(line["docs_per_sec"])
         if tl:

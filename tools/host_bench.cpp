@@ -73,7 +73,16 @@ int main(int argc, char** argv) {
   double best = 1e9;
   size_t meta_bytes = 0;
   int64_t kept = 0, excl = 0;
-  BatchState bs(ndocs, data.data(), off.data(), nullptr, nullptr, nullptr, nthreads);
+  // argv[4] = 1: every document carries input metadata (the CLI path's {"url": ...} column)
+  const bool with_meta = argc > 4 && std::atoi(argv[4]) != 0;
+  std::string meta;
+  std::vector<int64_t> moff{0};
+  for (int i = 0; i < ndocs && with_meta; ++i) {
+    meta += "{\"url\":\"https://example.com/" + std::to_string(i) + "\"}";
+    moff.push_back((int64_t)meta.size());
+  }
+  BatchState bs(ndocs, data.data(), off.data(), with_meta ? meta.data() : nullptr, with_meta ? moff.data() : nullptr,
+                nullptr, nthreads);
   int prefix = 0;
   for (int s = 0; s < 3; ++s) {
     bs.apply_records(st[s], s, rec.data() + (int64_t)prefix * ndocs, record_width(st[s]), -1);

@@ -134,6 +134,20 @@ struct PreDoc {
   uint8_t* wal;
   uint32_t W;
   uint32_t pad;
+  // GopherRepetition's word arrays (gopher_rep_record) built by many workgroups
+  // (kernels.hip k_pre_wcanon): word hashes, the canonicalisation table (1.5 W + 2 64-bit slots)
+  // and each word's slot, per-2048-word chunk sums and bases, and the results wid / WL / K / PB
+  // (W + 1 entries each); wready = 1 once they are filled.
+  uint64_t* wh;
+  uint64_t* wtab;
+  uint64_t* wk;
+  uint64_t* wpb;
+  uint64_t* wcsum;
+  uint32_t* wslot;
+  uint32_t* wid;
+  uint32_t* wl;
+  uint32_t wready;
+  uint32_t pad2;
 };
 
 struct Words {
@@ -1229,7 +1243,14 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
   uint32_t* WL = nullptr;
   uint64_t* K = nullptr;
   uint64_t* PB = nullptr;
-  if (ngrams) {
+  if (ngrams && pre && pre->wready) {
+    // built by many workgroups before this one (k_pre_wcanon); a hash collision between unequal
+    // words has flagged the document for the CPU path there
+    wid = pre->wid;
+    WL = pre->wl;
+    K = pre->wk;
+    PB = pre->wpb;
+  } else if (ngrams) {
     // LDS only while a canonicalisation table for W elements (~6 W bytes) still fits next to them
     // (split mode: HBM, they outlive this kernel)
     const uint64_t tab_bytes = 6ull * W + 64;

@@ -1507,6 +1507,192 @@ __global__ __launch_bounds__(64) void k_pre_words_scan(const int32_t* __restrict
   }
 }
 
+// SURVEY 5.7, GopherRepetition's word arrays of the pre-pass documents over many workgroups
+// (gopher_rep_record computes the same in the document's own workgroup for the others): per
+// chunk of 2048 words (256 threads, 8 consecutive words each)
+//   MODE 0  zero the canonicalisation table (1.5 W + 2 slots of 64 bits)
+//   MODE 1  word hash (the polynomial hash of its bytes = span_hash8), insert into the table
+//           (fingerprint | smallest index + 1, CAS + atomic min: canonicalize()'s 64-bit path),
+//           chunk sum of the word lengths
+//   MODE 2  canonical id (verified byte-equal; a collision flags the document for the CPU path),
+//           WL / PB from the chunk's length base, chunk sum of wh[k] B^-WL[k+1]
+//   MODE 3  K from the chunk's base of those terms
+// with k_pre_wsum (one wave per document) turning chunk sums into bases between the passes.
+constexpr uint32_t kPreWChunk = 2048;
+constexpr uint32_t kPreWThreads = 256;
+constexpr uint32_t kPreWPer = kPreWChunk / kPreWThreads;
+constexpr uint32_t kPreWTabChunk = 3072;  // table slots zeroed per workgroup (1.5 x a chunk)
+
+__device__ __forceinline__ uint64_t pow_at(const uint64_t* pw, uint32_t pw_n, uint32_t k) {
+  return k <= pw_n ? pw[k] : hpow(kHashBase, k);
+}
+__device__ __forceinline__ uint64_t ipow_at(const uint64_t* pw, uint32_t pw_n, uint32_t k) {
+  return k <= pw_n ? pw[pw_n + 1 + k] : hpow(kHashBaseInv, k);
+}
+
+// exclusive block scan (kPreWThreads threads) of one value per thread; *tot = the block total
+template <class T>
+__device__ __forceinline__ T pre_block_scan(T v, T* sh, T* tot) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const T incl = pardetail::wave_incl_scan(v, lane, [](T a, T b) { return a + b; });
+  if (lane == 63) sh[w] = incl;
+  __syncthreads();
+  T base = 0, all = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < kPreWThreads / 64; ++q) {
+    if (q < w) base += sh[q];
+    all += sh[q];
+  }
+  __syncthreads();
+  *tot = all;
+  return base + incl - v;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kPreWThreads) void k_pre_wcanon(const uint8_t* __restrict__ bytes,
+                                                             const int64_t* __restrict__ off,
+                                                             const int32_t* __restrict__ perm,
+                                                             const uint8_t* __restrict__ dead,
+                                                             const PreDoc* __restrict__ pre,
+                                                             const uint64_t* __restrict__ pw, uint32_t pw_n,
+                                                             uint32_t* flags) {
+  __shared__ uint64_t sh[kPreWThreads / 64];
+  const uint32_t c = blockIdx.x, s = blockIdx.y;
+  const int doc = perm[s];
+  if (dead && dead[doc]) return;
+  const PreDoc d = pre[s];
+  const uint32_t W = d.W;
+  const uint32_t nch = (W + kPreWChunk - 1) / kPreWChunk;
+  const uint32_t capn = W + (W >> 1) + 2;
+  if (MODE == 0) {
+    const uint32_t a = c * kPreWTabChunk;
+    for (uint32_t i = a + threadIdx.x; i < capn && i < a + kPreWTabChunk; i += kPreWThreads) d.wtab[i] = 0;
+    return;
+  }
+  if (c >= (nch ? nch : 1u)) return;  // (W == 0: chunk 0 writes the closing entries)
+  const uint8_t* b = bytes + off[doc];
+  const uint32_t t0 = c * kPreWChunk + threadIdx.x * kPreWPer;
+  uint32_t len[kPreWPer];
+  uint32_t lsum = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kPreWPer; ++j) {
+    const uint32_t k = t0 + j;
+    len[j] = k < W ? d.wbe[k] - d.wbs[k] : 0u;
+    lsum += len[j];
+  }
+  if (MODE == 1) {
+#pragma unroll
+    for (uint32_t j = 0; j < kPreWPer; ++j) {
+      const uint32_t k = t0 + j;
+      if (k >= W) break;
+      const uint32_t bs = d.wbs[k], be = d.wbe[k];
+      uint64_t h = 0;
+      for (uint32_t q = bs; q < be; ++q) h = hash_push(h, b[q]);
+      d.wh[k] = h;
+      const uint64_t key = dev_key(h, be - bs);
+      const uint64_t fp = (key >> 32) | 1ull;
+      const uint64_t mine = (fp << 32) | (uint64_t)(k + 1);
+      uint32_t slot = (uint32_t)(((key & 0xFFFFFFFFull) * capn) >> 32);
+      while (true) {
+        unsigned long long cur = d.wtab[slot];
+        if (cur == 0) {
+          cur = atomicCAS((unsigned long long*)&d.wtab[slot], 0ull, (unsigned long long)mine);
+          if (cur == 0) break;
+        }
+        if ((cur >> 32) == fp) {
+          if ((cur & 0xFFFFFFFFull) > (uint64_t)k + 1u) atomicMin((unsigned long long*)&d.wtab[slot], mine);
+          break;
+        }
+        if (++slot == capn) slot = 0;
+      }
+      d.wslot[k] = slot;
+    }
+    uint64_t tot;
+    (void)pre_block_scan<uint64_t>(lsum, sh, &tot);
+    if (threadIdx.x == 0) d.wcsum[c] = tot;
+    return;
+  }
+  // MODE 2 / 3: this thread's first word's WL from the chunk base + the block scan
+  uint64_t tot;
+  const uint64_t lbase = (nch ? d.wcsum[nch + c] : 0ull) + pre_block_scan<uint64_t>(lsum, sh, &tot);
+  if (MODE == 2) {
+    uint32_t wl = (uint32_t)lbase;
+    uint64_t tsum = 0;
+    bool bad = false;
+#pragma unroll
+    for (uint32_t j = 0; j < kPreWPer; ++j) {
+      const uint32_t k = t0 + j;
+      if (k >= W) break;
+      d.wl[k] = wl;
+      d.wpb[k] = pow_at(pw, pw_n, wl);
+      uint32_t cc = (uint32_t)(d.wtab[d.wslot[k]] & 0xFFFFFFFFull) - 1u;
+      if (cc != k && !bytes_eq<WavePar>(b, d.wbs[k], d.wbe[k], d.wbs[cc], d.wbe[cc])) {
+        bad = true;
+        cc = k;
+      }
+      d.wid[k] = cc;
+      wl += len[j];
+      tsum += d.wh[k] * ipow_at(pw, pw_n, wl);
+    }
+    if (bad) atomicOr(&flags[doc], DOC_NEEDS_CPU);
+    uint64_t ttot;
+    (void)pre_block_scan<uint64_t>(tsum, sh, &ttot);
+    if (threadIdx.x == 0) {
+      if (nch) d.wcsum[2 * nch + c] = ttot;
+      if (c + 1 >= nch) {  // the closing entries
+        const uint32_t total = (uint32_t)((nch ? d.wcsum[nch + c] : 0ull) + tot);
+        d.wl[W] = total;
+        d.wpb[W] = pow_at(pw, pw_n, total);
+      }
+    }
+    return;
+  }
+  // MODE 3
+  uint32_t wl = (uint32_t)lbase;
+  uint64_t t[kPreWPer];
+  uint64_t tsum = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kPreWPer; ++j) {
+    const uint32_t k = t0 + j;
+    wl += len[j];
+    t[j] = k < W ? d.wh[k] * ipow_at(pw, pw_n, wl) : 0ull;
+    tsum += t[j];
+  }
+  uint64_t ttot;
+  uint64_t kb = (nch ? d.wcsum[3 * nch + c] : 0ull) + pre_block_scan<uint64_t>(tsum, sh, &ttot);
+#pragma unroll
+  for (uint32_t j = 0; j < kPreWPer; ++j) {
+    const uint32_t k = t0 + j;
+    if (k >= W) break;
+    d.wk[k] = kb;
+    kb += t[j];
+  }
+  if (threadIdx.x == 0 && c + 1 >= nch) d.wk[W] = (nch ? d.wcsum[3 * nch + c] : 0ull) + ttot;
+}
+
+// One wave per document: exclusive scans of the chunk sums (MODE 0: lengths [0, nch) -> [nch, 2 nch);
+// MODE 1: K terms [2 nch, 3 nch) -> [3 nch, 4 nch)); MODE 1 also marks the arrays ready.
+template <int MODE>
+__global__ __launch_bounds__(64) void k_pre_wsum(const int32_t* __restrict__ perm, const uint8_t* __restrict__ dead,
+                                                 PreDoc* pre) {
+  const uint32_t s = blockIdx.x;
+  if (dead && dead[perm[s]]) return;
+  const PreDoc d = pre[s];
+  const uint32_t nch = (d.W + kPreWChunk - 1) / kPreWChunk;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t* in = d.wcsum + (MODE ? 2 * nch : 0);
+  uint64_t* out = d.wcsum + (MODE ? 3 * nch : nch);
+  uint64_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nch; b0 += 64) {
+    const uint32_t q = b0 + lane;
+    const uint64_t v = q < nch ? in[q] : 0ull;
+    const uint64_t incl = pardetail::wave_incl_scan(v, lane, [](uint64_t a, uint64_t b) { return a + b; });
+    if (q < nch) out[q] = carry + incl - v;
+    carry += pardetail::bcast63(incl);
+  }
+  if (MODE == 1 && lane == 0) pre[s].wready = 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1604,6 +1790,25 @@ int tb_gr_dup_split(hipStream_t stream, const void* stage, int32_t gr_step, cons
   hipLaunchKernelGGL(k_gr_dup_split, dim3((uint32_t)n_split * (uint32_t)n_tasks), dim3(kBlockThreads), lds_bytes, stream,
                      (const DevStage*)stage, gr_step, perm, n_tasks, ndocs, (const GrExport*)gr_export, pw, pw_n, t, rec,
                      flags, lds_bytes);
+  return (int)hipGetLastError();
+}
+
+// GopherRepetition word arrays of the npre pre-pass documents (after tb_pre_decode; the
+// descriptors' wh / wtab / wk / wpb / wcsum / wslot / wid / wl hold [W + 1]-sized buffers,
+// wtab [1.5 W + 2], wcsum [4 chunks]; chunks_max >= ceil(max W / 2048)).
+int tb_pre_wcanon(hipStream_t stream, const uint8_t* bytes, const int64_t* off, const int32_t* perm, int32_t npre,
+                  const uint8_t* dead, void* pre, uint32_t chunks_max, const uint64_t* pw, uint32_t pw_n,
+                  uint32_t* flags) {
+  if (npre <= 0) return 0;
+  if (!perm || !pre || !pw || !flags || chunks_max == 0 || npre > 65535) return (int)hipErrorInvalidValue;
+  const PreDoc* p = (const PreDoc*)pre;
+  const dim3 gz(chunks_max + 1, (uint32_t)npre), g(chunks_max, (uint32_t)npre);
+  hipLaunchKernelGGL(k_pre_wcanon<0>, gz, dim3(kPreWThreads), 0, stream, bytes, off, perm, dead, p, pw, pw_n, flags);
+  hipLaunchKernelGGL(k_pre_wcanon<1>, g, dim3(kPreWThreads), 0, stream, bytes, off, perm, dead, p, pw, pw_n, flags);
+  hipLaunchKernelGGL(k_pre_wsum<0>, dim3((uint32_t)npre), dim3(64), 0, stream, perm, dead, (PreDoc*)pre);
+  hipLaunchKernelGGL(k_pre_wcanon<2>, g, dim3(kPreWThreads), 0, stream, bytes, off, perm, dead, p, pw, pw_n, flags);
+  hipLaunchKernelGGL(k_pre_wsum<1>, dim3((uint32_t)npre), dim3(64), 0, stream, perm, dead, (PreDoc*)pre);
+  hipLaunchKernelGGL(k_pre_wcanon<3>, g, dim3(kPreWThreads), 0, stream, bytes, off, perm, dead, p, pw, pw_n, flags);
   return (int)hipGetLastError();
 }
 
@@ -1797,7 +2002,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 int tb_phase_slots() { return kPhaseSlots; }
 int tb_stage_waves() { return TB_STAGE_WPE; }  // waves per SIMD the wave stage kernel is built for
 
-int tb_abi_version() { return 19; }
+int tb_abi_version() { return 20; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

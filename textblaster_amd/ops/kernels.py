@@ -22,7 +22,7 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32, _P,
@@ -48,6 +48,7 @@ _SIGS = {
     "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _U32, _P],
     "tb_langid_mfma": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, ctypes.c_double, _P, _P, _I32, _P],
     "tb_langid_prepare": [_P, _P, _P],
+    "tb_pre_wcanon": [_P, _P, _P, _P, _I32, _P, _P, _U32, _P, _U32, _P],
     "tb_langid_aux_bytes": [],
     "tb_c4_pass_b": [_P, _P, _P, _I32, _P, _P, _P, _P, _P],
     "tb_pow_table": [_P, _P, _U32],
@@ -78,7 +79,10 @@ _SIGS = {
 PRE_DOC = np.dtype([("off", "<u8"), ("prop", "<u8"), ("wbm", "<u8"), ("nl_pos", "<u8"), ("nl_len", "<u8"),
                     ("n", "<u4"), ("C", "<u4"), ("dict", "<u4"), ("NL", "<u4"), ("tcs", "<u4"), ("tce", "<u4"),
                     ("nl_a", "<u4"), ("nl_e", "<u4"), ("wtmp", "<u8"), ("wcs", "<u8"), ("wce", "<u8"),
-                    ("wbs", "<u8"), ("wbe", "<u8"), ("wal", "<u8"), ("W", "<u4"), ("pad", "<u4")])
+                    ("wbs", "<u8"), ("wbe", "<u8"), ("wal", "<u8"), ("W", "<u4"), ("pad", "<u4"),
+                    ("wh", "<u8"), ("wtab", "<u8"), ("wk", "<u8"), ("wpb", "<u8"), ("wcsum", "<u8"),
+                    ("wslot", "<u8"), ("wid", "<u8"), ("wl", "<u8"), ("wready", "<u4"), ("pad2", "<u4")])
+PRE_WCHUNK = 2048  # kernels.hip kPreWChunk
 PRE_TILE = 16384  # kernels.hip kPreTile
 
 
@@ -232,6 +236,17 @@ class Kernels:
                                     _ptr(dead), pre.data_ptr(), int(tiles_max), cnt.data_ptr(), t[0].data_ptr(),
                                     t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr())
         _check(rc, "tb_pre_decode")
+
+    def pre_wcanon(self, bytes_, off, perm_pre, npre, dead, pre, chunks_max, pw, pw_n, flags):
+        """k_pre_wcanon / k_pre_wsum: GopherRepetition's word hashes, canonical word ids
+        and concatenation-hash arrays of the ``npre`` pre-pass documents over many workgroups (after
+        pre_decode; ``chunks_max`` >= ceil(max words / PRE_WCHUNK))."""
+        if perm_pre.numel() < npre or pre.nbytes < npre * PRE_DOC.itemsize or chunks_max <= 0:
+            raise DeviceError("pre_wcanon: operand shapes")
+        rc = self.lib.tb_pre_wcanon(self.stream(), bytes_.data_ptr(), off.data_ptr(), perm_pre.data_ptr(), npre,
+                                    _ptr(dead), pre.data_ptr(), int(chunks_max), pw.data_ptr(), pw_n,
+                                    flags.data_ptr())
+        _check(rc, "tb_pre_wcanon")
 
     def gr_dup_split(self, stage, gr_step, perm, n_split, n_tasks, ndocs, gr_export, pw, pw_n, rec, flags, lds_bytes):
         """k_gr_dup_split: one workgroup per (split document, n-gram order); n_tasks = the

@@ -16,7 +16,7 @@ import numpy as np
 
 from .. import native
 from ..errors import DeviceError
-from ..ops.kernels import PRE_DOC, PRE_TILE
+from ..ops.kernels import PRE_DOC, PRE_TILE, PRE_WCHUNK
 from ..utils import metrics, tracing
 from .plan import ExecPlan
 
@@ -278,6 +278,8 @@ class PendingBatch:
         for item in self._keep or ():
             if isinstance(item, tuple) and len(item) == 3 and item[0] == "ktime":
                 e0, e1 = item[2]
+                # (a timing event may sit behind the batch's completion event on a side stream)
+                e1.synchronize()
                 kt[item[1]] = kt.get(item[1], 0.0) + e0.elapsed_time(e1) / 1000.0
         for name, sec in kt.items():
             metrics.GPU_KERNEL_SECONDS.labels(name).observe(sec)
@@ -569,6 +571,9 @@ class DeviceRunner:
         if self.split_doc_bytes > 0:
             self.split_doc_bytes = max(self.split_doc_bytes, self.long_doc_bytes)
         self.pre_doc_bytes = int(os.environ.get("TB_PRE_DOC_BYTES", str(self.DEFAULT_PRE_DOC_BYTES)))
+        # TB_PRE_WCANON=0: the pre-pass documents' word hashing and canonicalisation stay in their
+        # stage workgroup (gopher_rep_record) instead of k_pre_wcanon's many workgroups
+        self.pre_wcanon = os.environ.get("TB_PRE_WCANON", "1") not in ("", "0")
         if self.pre_doc_bytes > 0:
             self.pre_doc_bytes = max(self.pre_doc_bytes, 65536, self.long_doc_bytes)
         # per stage: (position of its GopherRepetition step, number of split tasks = its duplicated
@@ -690,7 +695,7 @@ class DeviceRunner:
             out.append(dev[o:o + a.nbytes].view(a.dtype) if a.nbytes else dev[o:o].view(a.dtype))
         return out, dev
 
-    def _pre_decode(self, vb, vo, d_perm, long_lens: np.ndarray, dead, keep):
+    def _pre_decode(self, vb, vo, d_perm, long_lens: np.ndarray, dead, keep, flags=None, with_words=False):
         """SURVEY 5.7 pre-pass for the longest documents (launch positions [0, n_pre), sorted by
         length): device arrays for their code points and word-break marks, filled by k_pre_* on
         the current stream. Returns (PreDoc descriptors as a uint8 device array, n_pre)."""
@@ -711,6 +716,14 @@ class DeviceRunner:
         sz_w = al(4 * (lens + 1))  # word arrays (words <= code points)
         sz_wa = al(lens + 1)
         per = sz_off + sz_prop + sz_wbm + 2 * sz_nl + sz_wt + 4 * sz_w + sz_wa
+        # GopherRepetition's word arrays (k_pre_wcanon): wh / wk / wpb (8 B), wslot / wid / wl (4 B)
+        # per word, the 1.5 W + 2-slot table, 4 sums per 2048-word chunk
+        wcanon = bool(self.gr_split) and with_words
+        if wcanon:
+            sz_w8 = al(8 * (lens + 2))
+            sz_tab = al(8 * (lens + lens // 2 + 3))
+            sz_cs = al(8 * 4 * ((lens + PRE_WCHUNK - 1) // PRE_WCHUNK + 1))
+            per = per + 3 * sz_w8 + 3 * al(4 * (lens + 2)) + sz_tab + sz_cs
         base = np.zeros(n_pre + 1, np.int64)
         np.cumsum(per, out=base[1:])
         rt = self.rt
@@ -729,6 +742,17 @@ class DeviceRunner:
         h["wbs"] = o + sz_wt + 2 * sz_w
         h["wbe"] = o + sz_wt + 3 * sz_w
         h["wal"] = o + sz_wt + 4 * sz_w
+        if wcanon:
+            q = o + sz_wt + 4 * sz_w + sz_wa
+            sz_w4 = al(4 * (lens + 2))
+            for name in ("wh", "wk", "wpb"):
+                h[name] = q
+                q = q + sz_w8
+            for name in ("wslot", "wid", "wl"):
+                h[name] = q
+                q = q + sz_w4
+            h["wtab"] = q
+            h["wcsum"] = q + sz_tab
         h["n"] = lens
         h["tcs"] = 0xFFFFFFFF
         d_pre = rt.empty(n_pre * PRE_DOC.itemsize, np.uint8)
@@ -737,6 +761,10 @@ class DeviceRunner:
         tiles_max = int((int(lens.max()) + PRE_TILE - 1) // PRE_TILE)
         cnt = rt.empty(n_pre * tiles_max, np.int64)
         self.k.pre_decode(vb, vo, d_perm[:n_pre], n_pre, dead, d_pre, tiles_max, cnt)
+        if wcanon:
+            pw, pw_n = self.k.pow_table(int(lens.max()) + 16)
+            chunks_max = int((int(lens.max()) + 1 + PRE_WCHUNK - 1) // PRE_WCHUNK)
+            self.k.pre_wcanon(vb, vo, d_perm[:n_pre], n_pre, dead, d_pre, chunks_max, pw, pw_n, flags)
         keep += [buf, d_pre, cnt, hp]
         return d_pre, n_pre
 
@@ -936,7 +964,8 @@ class DeviceRunner:
                         # (the original text only: the host knows no lengths of rewritten versions); once
                         # per batch: every stage reading version 0 reuses it (read-only, same stream)
                         if ver == 0 and pre_v0 is None:
-                            pre_v0 = self._pre_decode(vb, vo, d_perm, lens[perm[:n_long]], skip, keep)
+                            pre_v0 = self._pre_decode(vb, vo, d_perm, lens[perm[:n_long]], skip, keep, flags,
+                                                      self.pre_wcanon)
                         pre, n_pre = pre_v0 if ver == 0 else (None, 0)
                         # launch positions [0, n_pre): the pre-pass kernel instantiation, the rest the common one
                         segs = ((0, n_pre, 512, True), (n_pre, n_long, 512, False))

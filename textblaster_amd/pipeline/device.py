@@ -397,7 +397,7 @@ class DeviceRunner:
     DEFAULT_LDS_BYTES_C4 = 2560
     DEFAULT_LONG_DOC_BYTES = 4096  # with the 3-per-CU workgroup kernel (profiles/r2_c5/long_doc_threshold.txt)
     DEFAULT_LDS_BYTES_BLK = 49152
-    DEFAULT_SPLIT_DOC_BYTES = 65536
+    DEFAULT_SPLIT_DOC_BYTES = 32768  # config 5 A/B: 147.6 K (64 KiB) -> 151.5-152.5 K docs/s (profiles/r8_c5/)
     # documents of at least this size get their code points and word-break marks from
     # the multi-workgroup pre-pass (k_pre_*) before their stage workgroup runs; 0 disables. Never
     # below 64 KiB (smaller documents use the packed code point layout). ~1 MB documents: 1,001 ->

@@ -41,11 +41,16 @@ def main(d):
     rows.append(("3. + LanguageDetection (bf16 MFMA head) + FineWeb", f"{batch(c3g)} ~1.1 KB docs/step (bench.py)",
                  c3c and c3c[-1]["value"], c3g and c3g[-1]["value"]))
     c4 = g("c4_file")
-    rows.append(("4. CommonCrawl-shaped Parquet, CLI path (1-GPU point)", "4M docs: read+decode+filter+write",
+    n4 = f"{c4[-1]['docs'] / 1e6:.0f}M" if c4 else "?"
+    rows.append(("4. CommonCrawl-shaped Parquet, CLI path (1-GPU point)",
+                 f"{n4} docs: read+decode+filter+write" + (f", {c4[-1]['cpu_us_per_doc']:.2f} CPU-us/doc" if c4 else ""),
                  None, c4 and c4[-1]["docs_per_sec"]))
     c5c, c5g = g("c5_cpu"), g("c5_gpu")
     rows.append(("5. GopherRepetition 2..10-gram", "~50 KB docs, 4,096 docs/step",
                  c5c and c5c[-1]["value"], c5g and c5g[-1]["value"]))
+    c5m = g("c5mb_gpu")
+    rows.append(("5b. GopherRepetition 2..10-gram, long documents", "~1 MB docs, 128 docs/step", None,
+                 c5m and c5m[-1]["value"]))
     print("| Config | Workload | CPU path (16 threads) docs/s | 1x MI355X docs/s | speed-up |")
     print("|---|---|---|---|---|")
     for name, wl, c, gv in rows:
@@ -53,6 +58,11 @@ def main(d):
         print(f"| {name} | {wl} | {fmt(c)} | {fmt(gv)} | {sp} |")
     if c5g:
         print(f"\nConfig 5 on the GPU: {c5g[-1]['bytes_per_sec'] / 1e9:.2f} GB/s of text.")
+    if c5m:
+        print(f"~1 MB documents on the GPU: {c5m[-1]['bytes_per_sec'] / 1e9:.2f} GB/s of text.")
+    steps = {n: (r[-1]["steps"], r[-1]["warmup"]) for n, r in (("c1_gpu", c1g), ("c2_gpu", c2g), ("c3_gpu", c3g),
+                                                               ("c5_gpu", c5g), ("c5mb_gpu", c5m)) if r}
+    print("\nGPU runs (timed steps, warmup): " + ", ".join(f"{n} {s}/{w}" for n, (s, w) in steps.items()))
 
 
 if __name__ == "__main__":

@@ -82,3 +82,17 @@ def test_direct_json_metadata_with_input_metadata(monkeypatch):
     slow = _collect(eng, data, off, (md, mo, mv))
     assert fast == slow
     assert any(m and m.startswith(b'{"url"') for _, m in fast)
+
+
+def test_native_pool_cpu_is_attributed_per_job(host):
+    """The worker pool charges its jobs' CPU time to the submitting call site's tag (the e2e JSON's
+    pool_cpu_seconds_by_job): output assembly shows up under "assemble"."""
+    cfg = load_pipeline_config(os.path.join(ROOT, "config", "bench_pipeline.yaml"))
+    eng = Engine(cfg, backend="cpu", segmentation="rules", nthreads=2)
+    texts = synth.make_corpus(400, 600, seed=23)
+    data, off = synth.pack(texts)
+    before = dict(host.pool_cpu_stats())
+    eng.process(data, off)
+    after = dict(host.pool_cpu_stats())
+    assert after.get("assemble", 0.0) > before.get("assemble", 0.0)
+    assert after.get("cpu_steps", 0.0) > before.get("cpu_steps", 0.0)

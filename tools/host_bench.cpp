@@ -2,6 +2,7 @@
 // device-emulation path, then BatchState::assemble of the kept and excluded rows, timed. Build
 // with -pg for a gprof profile:  tools/host_bench.sh [ndocs] [reps]
 #include <chrono>
+#include <sys/resource.h>
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -83,13 +84,34 @@ int main(int argc, char** argv) {
   }
   BatchState bs(ndocs, data.data(), off.data(), with_meta ? meta.data() : nullptr, with_meta ? moff.data() : nullptr,
                 nullptr, nthreads);
+  // argv[5] = 1: a LanguageDetection step first (synthetic records: language i % 5, confidence
+  // 0.60 .. 0.99), as in the bench pipeline
+  if (argc > 5 && std::atoi(argv[5]) != 0) {
+    StepCfg ld;
+    ld.kind = StepKind::LanguageDetection;
+    ld.name = "LanguageDetectionFilter";
+    ld.min_confidence = 0.65;
+    ld.allowed_langs = {0, 1, 2, 3, 4};
+    ld.allowed_codes = {"eng", "dan", "swe", "nno", "nob"};
+    static std::vector<int64_t> lrec;
+    lrec.assign((size_t)2 * ndocs, 0);
+    for (int i = 0; i < ndocs; ++i) {
+      const double conf = 0.60 + 0.39 * (double)((i * 7919) % 1000) / 1000.0;
+      lrec[2 * i] = i % 5;
+      std::memcpy(&lrec[2 * i + 1], &conf, sizeof(double));
+    }
+    bs.apply_records(ld, 0, lrec.data(), 2, -1);
+  }
+  const int s0 = (argc > 5 && std::atoi(argv[5]) != 0) ? 1 : 0;
   int prefix = 0;
   for (int s = 0; s < 3; ++s) {
-    bs.apply_records(st[s], s, rec.data() + (int64_t)prefix * ndocs, record_width(st[s]), -1);
+    bs.apply_records(st[s], s0 + s, rec.data() + (int64_t)prefix * ndocs, record_width(st[s]), -1);
     prefix += record_width(st[s]);
   }
   std::vector<int64_t> k, e;
   for (int64_t i = 0; i < ndocs; ++i) (bs.status()[i] == 0 ? k : e).push_back(i);
+  rusage ru0, ru1;
+  getrusage(RUSAGE_SELF, &ru0);
   for (int r = 0; r < reps; ++r) {
     const auto t0 = std::chrono::steady_clock::now();
     RawBuf td, md;
@@ -106,6 +128,10 @@ int main(int argc, char** argv) {
     RawBuf::release(td.p, td.cap);
     RawBuf::release(md.p, md.cap);
   }
+  getrusage(RUSAGE_SELF, &ru1);
+  auto sec = [](const timeval& a, const timeval& b) { return (double)(b.tv_sec - a.tv_sec) + 1e-6 * (double)(b.tv_usec - a.tv_usec); };
+  std::printf("assemble loop: user %.3f s, sys %.3f s over %d reps (minor faults %ld)\n", sec(ru0.ru_utime, ru1.ru_utime),
+              sec(ru0.ru_stime, ru1.ru_stime), reps, ru1.ru_minflt - ru0.ru_minflt);
   {  // text-only reference: the same gathers without metadata
     double bt = 1e9;
     for (int r = 0; r < reps; ++r) {

@@ -678,6 +678,8 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     except BaseException:
         source.close()
         raise
+    if engine.backend == "cuda" and os.environ.get("TB_PINNED_READ", "1") not in ("", "0"):
+        reader.host_buffer = engine.host_buffer  # readers decode into pinned batch buffers from now on
     log.info("rank %d/%d: schedule=%s, %d units already done, backend=%s", rank, world, rc.schedule,
              local.units_skipped, engine.backend)
 

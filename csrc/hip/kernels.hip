@@ -13,6 +13,9 @@
 //  tb_c4_pass_a       : C4 line filtering, citation removal, rewritten text into scratch
 //  tb_c4_pass_b       : compaction of the rewritten texts into the next content version
 #include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdlib>
+#include <string>
 
 #include "../common/docproc.h"
 #include "../common/gate.h"
@@ -191,36 +194,50 @@ TB_STAGE_BLK_KERNEL(k_stage_analyze_blk_pre, kBlockThreads, true)
 // duplicated paragraphs. Block k handles launch
 // position k / n_tasks (perm order, the stage kernel's export slot) and task k % n_tasks; each
 // task works in its own 1/n_tasks share of the document's unused scratch slice.
+// Persistent (SURVEY 5.7 work queue): the grid is what the CUs hold at once; every workgroup
+// takes the next (document, task) from an atomic cursor until the queue is empty, in launch order
+// (documents longest first, their tasks together), so the heaviest tasks start first and a
+// workgroup that finishes early takes more. Every workgroup exits once the cursor passes the end.
 __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_gr_dup_split(
-    const DevStage* __restrict__ stage, int32_t gr_step, const int32_t* __restrict__ perm, int32_t n_tasks,
-    int32_t ndocs, const GrExport* __restrict__ ex, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
-    int64_t* rec, uint32_t* flags, uint32_t lds_bytes) {
-  const int k = (int)blockIdx.x / n_tasks, t = (int)blockIdx.x % n_tasks;
-  const int doc = perm[k];
-  if (doc >= ndocs) return;
-  const GrExport e = ex[k];
-  if (!e.valid) return;  // not exported: skipped, returned early (flagged for the CPU path) or short
-  DocCtx<BlockPar<kBlockThreads>> x;
-  x.prof = nullptr;
-  x.lds = lds_bytes ? (char*)g_lds_arena : nullptr;
-  x.lcap = lds_bytes;
-  x.lused = 0;
-  x.ucd = UcdView{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
-  x.pw = pw;
-  x.pw_n = pw_n;
-  x.ipw = pw ? pw + pw_n + 1 : nullptr;
-  const uint64_t region = (e.free_cap / (uint64_t)n_tasks) & ~255ull;
-  x.scr = e.free_base + (uint64_t)t * region;
-  x.cap = region;
-  x.used = 0;
-  x.flag = flags + doc;
-  x.par.xs = g_block_xs;
+    const DevStage* __restrict__ stage, int32_t gr_step, const int32_t* __restrict__ perm, int32_t n_split,
+    int32_t n_tasks, int32_t ndocs, const GrExport* __restrict__ ex, const uint64_t* __restrict__ pw, uint32_t pw_n,
+    DevTables tabs, int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint32_t* cursor) {
+  __shared__ int s_task;
+  const int total = n_split * n_tasks;
   const DevStep& ds = stage->steps[gr_step];
-  int64_t* r = rec + (int64_t)ds.rec_prefix * ndocs + (int64_t)doc * ds.width;
-  if (t < ds.n_dup) gr_dup_one_order(x, ds, t, e, r);
-  else if (t < ds.n_dup + ds.n_top) gr_top_one_order(x, ds, t - ds.n_dup, e, r);
-  else if (t < ds.n_dup + ds.n_top + 2) gr_lines_split(x, t - ds.n_dup - ds.n_top, e, r);
-  if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
+  while (true) {
+    if (threadIdx.x == 0) s_task = (int)atomicAdd(cursor, 1u);
+    __syncthreads();
+    const int task = s_task;
+    __syncthreads();  // (s_task is rewritten by the next iteration's claim)
+    if (task >= total) break;
+    const int k = task / n_tasks, t = task % n_tasks;
+    const int doc = perm[k];
+    if (doc >= ndocs) continue;
+    const GrExport e = ex[k];
+    if (!e.valid) continue;  // not exported: skipped, returned early (flagged for the CPU path) or short
+    DocCtx<BlockPar<kBlockThreads>> x;
+    x.prof = nullptr;
+    x.lds = lds_bytes ? (char*)g_lds_arena : nullptr;
+    x.lcap = lds_bytes;
+    x.lused = 0;
+    x.ucd = UcdView{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
+    x.pw = pw;
+    x.pw_n = pw_n;
+    x.ipw = pw ? pw + pw_n + 1 : nullptr;
+    const uint64_t region = (e.free_cap / (uint64_t)n_tasks) & ~255ull;
+    x.scr = e.free_base + (uint64_t)t * region;
+    x.cap = region;
+    x.used = 0;
+    x.flag = flags + doc;
+    x.par.xs = g_block_xs;
+    int64_t* r = rec + (int64_t)ds.rec_prefix * ndocs + (int64_t)doc * ds.width;
+    if (t < ds.n_dup) gr_dup_one_order(x, ds, t, e, r);
+    else if (t < ds.n_dup + ds.n_top) gr_top_one_order(x, ds, t - ds.n_dup, e, r);
+    else if (t < ds.n_dup + ds.n_top + 2) gr_lines_split(x, t - ds.n_dup - ds.n_top, e, r);
+    if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
+    __syncthreads();  // the task's LDS is the next task's
+  }
 }
 
 // ---- n-gram orders of wave documents, one workgroup per document (k_gr_ngrams) ---------------
@@ -1779,17 +1796,38 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
 int tb_gr_dup_split(hipStream_t stream, const void* stage, int32_t gr_step, const int32_t* perm, int32_t n_split,
                     int32_t n_tasks, int32_t ndocs, const void* gr_export, const uint64_t* pw, uint32_t pw_n,
                     const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
-                    uint32_t* flags, uint32_t lds_bytes) {
+                    uint32_t* flags, uint32_t lds_bytes, uint32_t* cursor) {
   if (n_split <= 0 || n_tasks <= 0) return 0;
   if (!perm || !gr_export || gr_step < 0 || gr_step >= kMaxStageSteps || n_tasks > 2 * kMaxNgramEntries + 2 ||
       lds_bytes > kMaxLdsPerBlk)
     return (int)hipErrorInvalidValue;
+  if (!cursor) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k_gr_dup_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-  hipLaunchKernelGGL(k_gr_dup_split, dim3((uint32_t)n_split * (uint32_t)n_tasks), dim3(kBlockThreads), lds_bytes, stream,
-                     (const DevStage*)stage, gr_step, perm, n_tasks, ndocs, (const GrExport*)gr_export, pw, pw_n, t, rec,
-                     flags, lds_bytes);
+  // the persistent grid: resident workgroups per CU (registers, LDS) x CUs, at most one per task
+  static int cus = 0;
+  if (cus <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+        hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_gr_dup_split, kBlockThreads, lds_bytes) !=
+          hipSuccess || per_cu <= 0)
+    per_cu = 1;
+  const int64_t total = (int64_t)n_split * n_tasks;
+  // TB_SPLIT_GRID=full: one workgroup per task (the hardware dispatcher orders them instead)
+  static const bool full = [] {
+    const char* e = std::getenv("TB_SPLIT_GRID");
+    return e && std::string(e) == "full";
+  }();
+  const int grid = (int)std::min<int64_t>(total, full ? total : (int64_t)cus * per_cu);
+  (void)hipMemsetAsync(cursor, 0, sizeof(uint32_t), stream);
+  hipLaunchKernelGGL(k_gr_dup_split, dim3((uint32_t)grid), dim3(kBlockThreads), lds_bytes, stream,
+                     (const DevStage*)stage, gr_step, perm, n_split, n_tasks, ndocs, (const GrExport*)gr_export, pw,
+                     pw_n, t, rec, flags, lds_bytes, cursor);
   return (int)hipGetLastError();
 }
 
@@ -2002,7 +2040,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 int tb_phase_slots() { return kPhaseSlots; }
 int tb_stage_waves() { return TB_STAGE_WPE; }  // waves per SIMD the wave stage kernel is built for
 
-int tb_abi_version() { return 20; }
+int tb_abi_version() { return 21; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

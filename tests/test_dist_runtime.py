@@ -191,7 +191,7 @@ def test_block_kernels_reject_oversized_lds_slice():
                                       dummy, dummy, dummy, dummy, dummy, dummy, lds, None, None, None, 0, 0, 512, None, None, 0)
         assert (rc != 0) == want_err
         rc = lib.tb_gr_dup_split(None, dummy, 0, dummy, 1, 6, 1, dummy, dummy, 0, dummy, dummy, dummy, dummy,
-                                 dummy, dummy, lds)
+                                 dummy, dummy, lds, dummy)
         assert (rc != 0) == want_err
         rc = lib.tb_c4_pass_a_blk(None, dummy, dummy, dummy, dummy, 1, 1, dummy, dummy, dummy, 0, dummy, dummy,
                                   dummy, dummy, dummy, dummy, dummy, lds, None, None, None)

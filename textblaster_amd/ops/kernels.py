@@ -22,7 +22,7 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32, _P,
@@ -34,7 +34,7 @@ _SIGS = {
                              _U32, _P, _P, _P, _I32, _U32, _I32, _P, _P, _I32],
     "tb_sizeof_pre_doc": [],
     "tb_pre_decode": [_P, _P, _P, _P, _I32, _P, _P, _U32, _P, _P, _P, _P, _P],
-    "tb_gr_dup_split": [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32],
+    "tb_gr_dup_split": [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P],
     "tb_sizeof_gr_export": [],
     "tb_c4_pass_a_blk": [_P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _P,
                          _P],
@@ -248,15 +248,19 @@ class Kernels:
                                     flags.data_ptr())
         _check(rc, "tb_pre_wcanon")
 
-    def gr_dup_split(self, stage, gr_step, perm, n_split, n_tasks, ndocs, gr_export, pw, pw_n, rec, flags, lds_bytes):
-        """k_gr_dup_split: one workgroup per (split document, n-gram order); n_tasks = the
-        GopherRepetition step's duplicated + top n-gram orders."""
-        if gr_export.nbytes < n_split * self.sizeof_gr_export or perm.numel() < n_split:
+    def gr_dup_split(self, stage, gr_step, perm, n_split, n_tasks, ndocs, gr_export, pw, pw_n, rec, flags, lds_bytes,
+                     cursor):
+        """k_gr_dup_split: persistent workgroups take (split document, task) pairs from an atomic
+        cursor (``cursor``: a uint32 device word of this launch, reset by the call; keep it alive
+        until the kernel completes); n_tasks = the GopherRepetition step's duplicated + top n-gram
+        orders + duplicated lines + paragraphs."""
+        if gr_export.nbytes < n_split * self.sizeof_gr_export or perm.numel() < n_split or cursor.nbytes < 4:
             raise DeviceError("gr_dup_split: operand shapes")
         t = self.tabs
         rc = self.lib.tb_gr_dup_split(self.stream(), stage.data_ptr(), gr_step, perm.data_ptr(), n_split, n_tasks, ndocs,
                                       gr_export.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
-                                      t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), lds_bytes)
+                                      t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), lds_bytes,
+                                      cursor.data_ptr())
         _check(rc, "tb_gr_dup_split")
 
     def c4_pass_a_blk(self, c4, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags,

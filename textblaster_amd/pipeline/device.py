@@ -981,8 +981,10 @@ class DeviceRunner:
                                                      pre if with_pre else None, a1 - a0 if with_pre else 0)
                         if n_split:
                             gr_pos, n_tasks = self.gr_split[s]
+                            cur = rt.empty(1, np.uint32)
+                            keep.append(cur)
                             self.k.gr_dup_split(self.stage_ts[s], gr_pos, d_perm[:n_split], n_split, n_tasks, ndocs,
-                                                gx, pw, pw_n, rec, flags, self.lds_bytes_blk)
+                                                gx, pw, pw_n, rec, flags, self.lds_bytes_blk, cur)
                         ev_blk = self._record(slot.s_blk)
                         keep.append(ev_blk)
                 if lid_at and not lid_pass:

@@ -563,6 +563,7 @@ class DeviceRunner:
         # 48 KB: three long-document workgroups per CU (with the 6-wave register budget of
         # k_stage_analyze_blk, csrc/hip/kernels.hip TB_BLK_WPE)
         self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", str(self.DEFAULT_LDS_BYTES_BLK)))
+        self.block_threads = int(self.k.lib.tb_block_threads())  # threads of the long-document workgroups
         # SURVEY 5.7 split: documents longer than this finish their duplicated n-gram orders in one
         # workgroup per order (k_gr_dup_split) instead of one after another in their stage
         # workgroup; 0 disables. Never below the long-document threshold (wave documents cannot
@@ -968,7 +969,8 @@ class DeviceRunner:
                                                       self.pre_wcanon)
                         pre, n_pre = pre_v0 if ver == 0 else (None, 0)
                         # launch positions [0, n_pre): the pre-pass kernel instantiation, the rest the common one
-                        segs = ((0, n_pre, 512, True), (n_pre, n_long, 512, False))
+                        bt = self.block_threads
+                        segs = ((0, n_pre, bt, True), (n_pre, n_long, bt, False))
                         for a0, a1, thr, with_pre in segs:
                             if a1 <= a0:
                                 continue

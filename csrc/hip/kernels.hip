@@ -98,9 +98,10 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
 }
 
 // The stage kernel is register-bound (occupancy = waves/SIMD the VGPR budget allows). With the
-// n-gram orders moved to k_gr_ngrams / k_gr_split_wave it is built for 6 waves/SIMD (80 VGPRs)
-// with a 6.5 KB LDS slice per wave: 5.06 vs 5.26 ms per launch at 4 waves / 10 KB, 5 waves / 8 KB
-// no gain (profiles/r7_ngram/ab_occupancy.txt; before the move 4 waves won, round 2).
+// n-gram orders moved to k_gr_ngrams / k_gr_split_wave it is built for 8 waves/SIMD (64 VGPRs,
+// the spills it adds sit outside the per-chunk loops) with a 5 KB LDS slice per wave: 4.55 vs
+// 5.05 ms per launch at 6 waves / 6.5 KB, 7 waves no gain (profiles/r8_wpe/; 6 beat 4 and 5 before,
+// profiles/r7_ngram/ab_occupancy.txt; before the move 4 waves won, round 2).
 #define TB_STAGE_KERNEL(NAME, ATTR)                                                                   \
   __global__ __launch_bounds__(64) ATTR void NAME(                                                   \
       const DevPlan* __restrict__ plan, const DevStage* __restrict__ stage, const uint8_t* __restrict__ bytes, \
@@ -121,7 +122,7 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
   }
 
 #ifndef TB_STAGE_WPE
-#define TB_STAGE_WPE 6
+#define TB_STAGE_WPE 8
 #endif
 TB_STAGE_KERNEL(k_stage_analyze_wave, __attribute__((amdgpu_waves_per_eu(TB_STAGE_WPE, 8))))
 
@@ -467,7 +468,10 @@ __device__ __forceinline__ int64_t ng_top_order(NS& S, uint32_t W, uint32_t n, u
 }
 
 template <uint32_t MAXW>
-__global__ __launch_bounds__(64 * kNgWaves) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_gr_ngrams(
+#ifndef TB_NG_WPE
+#define TB_NG_WPE 8  // 2.51 -> 2.29 ms/step vs 6 (profiles/r8_ng8/)
+#endif
+__global__ __launch_bounds__(64 * kNgWaves) __attribute__((amdgpu_waves_per_eu(TB_NG_WPE, 8))) void k_gr_ngrams(
     const DevStage* __restrict__ stage, int32_t gr_step, const int32_t* __restrict__ perm, int32_t ndocs,
     const GrExport* __restrict__ ex, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec,
     uint32_t* flags, uint64_t* prof) {
@@ -1023,7 +1027,17 @@ __global__ __launch_bounds__(64 * kLidWaves) __attribute__((amdgpu_waves_per_eu(
   }
 }
 
-__global__ __launch_bounds__(64) void k_c4_pass_a(
+// TB_C4_WPE: register budget of the C4 pass A wave kernel (0: none). 8 waves/SIMD = 64 VGPRs,
+// one fewer than it takes unconstrained: 2.86 -> 2.42 ms/step (profiles/r8_c4w8/).
+#ifndef TB_C4_WPE
+#define TB_C4_WPE 8
+#endif
+#if TB_C4_WPE > 0
+#define TB_C4_ATTR __attribute__((amdgpu_waves_per_eu(TB_C4_WPE, 8)))
+#else
+#define TB_C4_ATTR
+#endif
+__global__ __launch_bounds__(64) TB_C4_ATTR void k_c4_pass_a(
     const DevC4* __restrict__ c4, const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
     const int32_t* __restrict__ perm, int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off,
     const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec, int64_t* src, uint32_t* flags,

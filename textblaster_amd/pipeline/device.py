@@ -391,8 +391,9 @@ def bw_dead_max(plan: ExecPlan, passes, pass_of_step: Dict[int, int]) -> Dict[in
 
 class DeviceRunner:
     N_SLOTS = 2
-    # per-wave LDS slices: the stage kernel is built for W waves/SIMD (tb_stage_waves: 6 -> 80
-    # VGPRs) = 4 W waves/CU, so 160 KB / 4 W each costs no occupancy (6.5 KB at 6); the C4 kernel
+    # per-wave LDS slices: the stage kernel is built for W waves/SIMD (tb_stage_waves: 8 -> 64
+    # VGPRs; 6 -> 80 cost 10 % more stage time, profiles/r8_wpe/) = 4 W waves/CU, so 160 KB / 4 W
+    # each costs no occupancy (5 KB at 8); the C4 kernel
     # (7 waves/SIMD) only keeps per-line arrays there
     DEFAULT_LDS_BYTES_C4 = 2560
     DEFAULT_LONG_DOC_BYTES = 4096  # with the 3-per-CU workgroup kernel (profiles/r2_c5/long_doc_threshold.txt)

@@ -469,7 +469,7 @@ __device__ __forceinline__ int64_t ng_top_order(NS& S, uint32_t W, uint32_t n, u
 
 template <uint32_t MAXW>
 #ifndef TB_NG_WPE
-#define TB_NG_WPE 8  // 2.51 -> 2.29 ms/step vs 6 (profiles/r8_ng8/)
+#define TB_NG_WPE 8  // 2.51 -> 2.29 ms/step vs 6 (profiles/r8_wpe/)
 #endif
 __global__ __launch_bounds__(64 * kNgWaves) __attribute__((amdgpu_waves_per_eu(TB_NG_WPE, 8))) void k_gr_ngrams(
     const DevStage* __restrict__ stage, int32_t gr_step, const int32_t* __restrict__ perm, int32_t ndocs,

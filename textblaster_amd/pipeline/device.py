@@ -591,8 +591,9 @@ class DeviceRunner:
         # wave documents finish their n-gram orders in one wave per (document, order)
         # (k_gr_split_wave, LDS slice TB_LDS_BYTES_SPLIT); TB_WAVE_SPLIT=0 keeps them in the stage
         self.wave_split = os.environ.get("TB_WAVE_SPLIT", "1") not in ("", "0")
-        # (6 KB: 2.81 ms/step vs 3.43 at 4 or 8 KB, profiles/r7_ngram/ab_occupancy.txt)
-        self.lds_bytes_split = int(os.environ.get("TB_LDS_BYTES_SPLIT", "5120"))  # 8 waves/SIMD: 2.80 -> 2.68 ms (profiles/r8_wpe/)
+        # (5 KB = 8 waves/SIMD: 2.68 ms/step vs 2.80 at 6 KB and 3.44 at 4 KB, profiles/r8_wpe/;
+        # round-5 start: 6 KB beat 4 and 8, profiles/r7_ngram/ab_occupancy.txt)
+        self.lds_bytes_split = int(os.environ.get("TB_LDS_BYTES_SPLIT", "5120"))
         self.ngram_block = os.environ.get("TB_NGRAM_BLOCK", "1") not in ("", "0")
         # wave documents longer than this take one wave per n-gram order (k_gr_split_wave), the
         # shorter ones one workgroup per document (k_gr_ngrams: 256 words, ~5.5 bytes per word on

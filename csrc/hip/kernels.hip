@@ -1205,7 +1205,8 @@ __global__ __launch_bounds__(256) void k_resolve(const DevResolve* __restrict__ 
 // dword and funnel-shifts them together (v_alignbyte), so interior bytes move 4 at a time whatever
 // the relative alignment; only the partial first and last destination dwords go byte by byte.
 // Source reads may run up to 3 bytes past a document (the batch and version buffers are padded).
-constexpr int kCompactThreads = 256;
+constexpr int kCompactThreads = 256;  // four documents per workgroup, one wave each
+constexpr int kCompactLanes = 64;
 
 __global__ __launch_bounds__(kCompactThreads) void k_compact(const uint8_t* __restrict__ status,
                                                              const uint8_t* __restrict__ fver, VersionTab vt,
@@ -1213,8 +1214,8 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact(const uint8_t* __re
                                                              uint8_t* __restrict__ out, int64_t cap,
                                                              int64_t* __restrict__ out_off, int32_t* __restrict__ rows,
                                                              int32_t* __restrict__ err) {
-  const int doc = blockIdx.x;
-  const int t = threadIdx.x;
+  const int doc = (int)blockIdx.x * (kCompactThreads / kCompactLanes) + (int)(threadIdx.x / kCompactLanes);
+  const int t = (int)(threadIdx.x % kCompactLanes);
   if (doc >= ndocs) return;
   const int64_t n = ndocs;
   const int64_t nk = sc[3 * n - 1], nx = sc[4 * n - 1], kb = sc[n - 1], xb = sc[2 * n - 1];
@@ -1245,7 +1246,7 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact(const uint8_t* __re
   // destination dwords fully inside [boff, boff + len): [a0, a1) in dword units of `out`
   const int64_t a0 = (boff + 3) >> 2, a1 = (boff + len) >> 2;
   if (a1 <= a0) {  // short: no whole destination dword
-    for (int64_t i = t; i < len; i += kCompactThreads) dst[i] = src[i];
+    for (int64_t i = t; i < len; i += kCompactLanes) dst[i] = src[i];
     return;
   }
   const int64_t head = a0 * 4 - boff, tail = boff + len - a1 * 4;  // bytes before / after
@@ -1257,7 +1258,7 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact(const uint8_t* __re
   const uint32_t* s32 = (const uint32_t*)(sbase - sh);
   uint32_t* d32 = (uint32_t*)out + a0;
   const int64_t nw = a1 - a0;
-  for (int64_t k = t; k < nw; k += kCompactThreads) {
+  for (int64_t k = t; k < nw; k += kCompactLanes) {
     const uint32_t lo = s32[k];
     const uint32_t hi = sh ? s32[k + 1] : 0u;
     // little endian: bytes sh.. of lo, then the low bytes of hi
@@ -2038,7 +2039,8 @@ int tb_resolve(hipStream_t stream, const void* rp, const int64_t* const* recs, i
     const int rc = tb_scan_strided_i64(stream, lanes + j, 4, ndocs, sc + (int64_t)j * ndocs);
     if (rc) return rc;
   }
-  hipLaunchKernelGGL(k_compact, dim3(ndocs), dim3(kCompactThreads), 0, stream, status, fver, vt, ndocs, sc, out, cap, out_off, rows,
+  hipLaunchKernelGGL(k_compact, dim3((ndocs + kCompactThreads / kCompactLanes - 1) / (kCompactThreads / kCompactLanes)),
+                     dim3(kCompactThreads), 0, stream, status, fver, vt, ndocs, sc, out, cap, out_off, rows,
                      err);
   return (int)hipGetLastError();
 }

@@ -122,9 +122,14 @@ static void compute_gr(const StepCfg& c, std::string_view text, SegBackend be, i
   r[rec::GR_LINE_DUP] = (int64_t)ld.first;
   r[rec::GR_LINE_DUP_BYTES] = (int64_t)ld.second;
   auto words = split_into_words(t, be);
+  std::vector<size_t> top, dup;
+  for (auto& e : c.top_n_grams) top.push_back((size_t)std::max<int64_t>(0, e.first));
+  for (auto& e : c.dup_n_grams) dup.push_back((size_t)std::max<int64_t>(0, e.first));
+  std::vector<size_t> vt(top.size()), vd(dup.size());
+  ngram_stats(words, top, dup, vt.data(), vd.data());
   int k = rec::GR_FIXED;
-  for (auto& e : c.top_n_grams) r[k++] = (int64_t)find_top_duplicate_ngrams(words, (size_t)e.first);
-  for (auto& e : c.dup_n_grams) r[k++] = (int64_t)find_all_duplicate(words, (size_t)e.first);
+  for (size_t v : vt) r[k++] = (int64_t)v;
+  for (size_t v : vd) r[k++] = (int64_t)v;
 }
 
 std::string c4_rewrite(const StepCfg& c, std::string_view text, SegBackend be, int64_t* r) {

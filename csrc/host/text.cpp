@@ -3,6 +3,7 @@
 #include <unicode/ubrk.h>
 #include <unicode/utext.h>
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -11,6 +12,7 @@
 
 #include "../common/ucd_tables.inc"
 #include "../common/uax29.h"
+#include "../common/hash.h"
 
 namespace tb {
 
@@ -305,45 +307,165 @@ std::pair<size_t, size_t> find_duplicates(const std::vector<std::string_view>& i
   return {elems, bytes};
 }
 
-size_t find_top_duplicate_ngrams(const std::vector<std::string_view>& words, size_t n) {
-  if (n == 0 || words.size() < n) return 0;
-  std::unordered_map<std::string, size_t> cnt;
-  cnt.reserve(words.size() * 2);
-  std::string g;
-  for (size_t i = 0; i + n <= words.size(); ++i) {
-    g.clear();
-    for (size_t k = 0; k < n; ++k) {
-      if (k) g.push_back(' ');
-      g.append(words[i + k].data(), words[i + k].size());
-    }
-    ++cnt[g];
+namespace {
+// Open-addressing set of (64-bit key, element) pairs; equality of elements is decided by the
+// caller's exact comparison, the key only groups candidates.
+struct KeyTable {
+  std::vector<uint64_t> key;
+  std::vector<uint32_t> val;  // element + 1 (0 = empty)
+  uint64_t mask = 0;
+  explicit KeyTable(size_t n) {
+    size_t cap = 16;
+    while (cap < 2 * n + 2) cap <<= 1;
+    key.assign(cap, 0);
+    val.assign(cap, 0);
+    mask = cap - 1;
   }
-  size_t maxc = 0;
-  for (auto& kv : cnt) maxc = std::max(maxc, kv.second);
-  if (maxc <= 1) return 0;
-  size_t best = 0;
-  for (auto& kv : cnt)
-    if (kv.second == maxc) best = std::max(best, kv.first.size() * maxc);
-  return best;
+  // slot of an element equal to `e` (eq(stored, e)), or the empty slot where it goes
+  template <class Eq>
+  size_t find(uint64_t k, Eq&& eq) const {
+    size_t s = (size_t)((k ^ (k >> 29)) * 0x9E3779B97F4A7C15ull >> 20) & mask;
+    while (val[s] != 0 && !(key[s] == k && eq(val[s] - 1))) s = (s + 1) & mask;
+    return s;
+  }
+};
+
+inline uint64_t mix64h(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+}  // namespace
+
+void ngram_stats(const std::vector<std::string_view>& words, const std::vector<size_t>& top,
+                 const std::vector<size_t>& dup, size_t* out_top, size_t* out_dup) {
+  const size_t W = words.size();
+  // word hashes (polynomial over the bytes), B^len, and canonical ids (smallest equal index)
+  std::vector<uint64_t> wh(W), wp(W);
+  std::vector<uint32_t> id(W);
+  for (size_t j = 0; j < W; ++j) {
+    uint64_t h = 0, p = 1;
+    for (unsigned char c : words[j]) {
+      h = hash_push(h, c);
+      p *= kHashBase;
+    }
+    wh[j] = h;
+    wp[j] = p;
+  }
+  bool need_ids = false;
+  for (size_t n : top) need_ids |= n > 0 && W >= n;
+  if (need_ids) {
+    KeyTable t(W);
+    for (size_t j = 0; j < W; ++j) {
+      const uint64_t k = mix64h(wh[j] ^ ((uint64_t)words[j].size() << 48));
+      const size_t s = t.find(k, [&](uint32_t e) { return words[e] == words[j]; });
+      if (t.val[s] == 0) {
+        t.key[s] = k;
+        t.val[s] = (uint32_t)j + 1;
+      }
+      id[j] = t.val[s] - 1;
+    }
+  }
+  for (size_t q = 0; q < top.size(); ++q) {
+    const size_t n = top[q];
+    out_top[q] = 0;
+    if (n == 0 || W < n) continue;
+    const size_t G = W - n + 1;
+    KeyTable t(G);
+    std::vector<uint32_t> cnt(G, 0);
+    for (size_t p = 0; p < G; ++p) {
+      uint64_t k = (uint64_t)n << 56;
+      for (size_t i = 0; i < n; ++i) k = (k ^ id[p + i]) * 0x9E3779B97F4A7C15ull + i;
+      k = mix64h(k);
+      const size_t s = t.find(k, [&](uint32_t e) {
+        for (size_t i = 0; i < n; ++i)
+          if (id[e + i] != id[p + i]) return false;
+        return true;
+      });
+      if (t.val[s] == 0) {
+        t.key[s] = k;
+        t.val[s] = (uint32_t)p + 1;
+      }
+      ++cnt[t.val[s] - 1];
+    }
+    size_t maxc = 0;
+    for (size_t p = 0; p < G; ++p) maxc = std::max<size_t>(maxc, cnt[p]);
+    if (maxc <= 1) continue;
+    size_t best = 0;
+    for (size_t p = 0; p < G; ++p) {
+      if (cnt[p] != maxc) continue;
+      size_t len = n - 1;  // the joining spaces
+      for (size_t i = 0; i < n; ++i) len += words[p + i].size();
+      best = std::max(best, len * maxc);
+    }
+    out_top[q] = best;
+  }
+  for (size_t q = 0; q < dup.size(); ++q) {
+    const size_t n = dup[q];
+    out_dup[q] = 0;
+    if (n == 0 || W < n) continue;
+    // concatenation (no separator) of words p .. p + n - 1: hash, byte length, byte equality
+    auto concat = [&](size_t p, size_t* len) {
+      uint64_t h = 0;
+      size_t l = 0;
+      for (size_t i = 0; i < n; ++i) {
+        h = h * wp[p + i] + wh[p + i];
+        l += words[p + i].size();
+      }
+      *len = l;
+      return h;
+    };
+    auto concat_eq = [&](size_t a, size_t b) {
+      size_t ia = a, ib = b, oa = 0, ob = 0;
+      while (ia < a + n && ib < b + n) {
+        const std::string_view x = words[ia], y = words[ib];
+        const size_t m = std::min(x.size() - oa, y.size() - ob);
+        if (std::memcmp(x.data() + oa, y.data() + ob, m) != 0) return false;
+        oa += m;
+        ob += m;
+        if (oa == x.size()) { ++ia; oa = 0; }
+        if (ob == y.size()) { ++ib; ob = 0; }
+      }
+      // (equal total lengths are checked by the caller; skip trailing empty words)
+      while (ia < a + n && words[ia].empty()) ++ia;
+      while (ib < b + n && words[ib].empty()) ++ib;
+      return ia == a + n && ib == b + n;
+    };
+    KeyTable t(W - n + 1);
+    std::vector<size_t> glen(W - n + 1, 0);
+    size_t rep = 0, idx = 0;
+    while (idx + n <= W) {
+      size_t len;
+      const uint64_t h = concat(idx, &len);
+      const uint64_t k = mix64h(h ^ ((uint64_t)len << 40));
+      const size_t s = t.find(k, [&](uint32_t e) { return glen[e] == len && concat_eq(e, idx); });
+      if (t.val[s] != 0) {
+        rep += len;
+        idx += n;
+      } else {
+        t.key[s] = k;
+        t.val[s] = (uint32_t)idx + 1;
+        glen[idx] = len;
+        idx += 1;
+      }
+    }
+    out_dup[q] = rep;
+  }
+}
+
+size_t find_top_duplicate_ngrams(const std::vector<std::string_view>& words, size_t n) {
+  size_t out = 0;
+  ngram_stats(words, {n}, {}, &out, nullptr);
+  return out;
 }
 
 size_t find_all_duplicate(const std::vector<std::string_view>& words, size_t n) {
-  if (n == 0 || words.size() < n) return 0;
-  std::unordered_set<std::string> uniq;
-  uniq.reserve(words.size() * 2);
-  size_t rep = 0, idx = 0, W = words.size();
-  std::string g;
-  while (idx + n <= W) {
-    g.clear();
-    for (size_t k = 0; k < n; ++k) g.append(words[idx + k].data(), words[idx + k].size());
-    if (!uniq.insert(g).second) {
-      rep += g.size();
-      idx += n;
-    } else {
-      idx += 1;
-    }
-  }
-  return rep;
+  size_t out = 0;
+  ngram_stats(words, {}, {n}, nullptr, &out);
+  return out;
 }
 
 std::string remove_citations(std::string_view s) {

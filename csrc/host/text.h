@@ -57,6 +57,11 @@ std::pair<size_t, size_t> find_duplicates(const std::vector<std::string_view>& i
 size_t find_top_duplicate_ngrams(const std::vector<std::string_view>& words, size_t n);
 // find_all_duplicate: greedy walk over concatenated n-grams
 size_t find_all_duplicate(const std::vector<std::string_view>& words, size_t n);
+// Both statistics for several orders over one word list (GopherRepetition's n-gram fields):
+// out_top[i] = find_top_duplicate_ngrams(words, top[i]), out_dup[i] = find_all_duplicate(words,
+// dup[i]), without building n-gram strings (word hashes + exact verification).
+void ngram_stats(const std::vector<std::string_view>& words, const std::vector<size_t>& top,
+                 const std::vector<size_t>& dup, size_t* out_top, size_t* out_dup);
 
 // Citation removal `\[\d+(?:,\s*\d+)*\]` (Unicode \d and \s), reference c4_filters.rs:33,201
 std::string remove_citations(std::string_view s);

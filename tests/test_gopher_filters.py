@@ -202,3 +202,47 @@ def test_stop_words(seg):
     h.process(doc("no stop words here"))
     h.min_stop_words = None
     h.process(doc("no stop words here"))
+
+
+def _ref_top(words, n):
+    if n == 0 or len(words) < n:
+        return 0
+    cnt = {}
+    for i in range(len(words) - n + 1):
+        g = " ".join(words[i:i + n])
+        cnt[g] = cnt.get(g, 0) + 1
+    m = max(cnt.values())
+    return 0 if m <= 1 else max(len(g.encode()) * m for g, c in cnt.items() if c == m)
+
+
+def _ref_all_dup(words, n):
+    if n == 0 or len(words) < n:
+        return 0
+    seen, rep, i = set(), 0, 0
+    while i + n <= len(words):
+        g = "".join(words[i:i + n])
+        if g in seen:
+            rep += len(g.encode())
+            i += n
+        else:
+            seen.add(g)
+            i += 1
+    return rep
+
+
+def test_ngram_statistics_match_string_reference():
+    """The host n-gram statistics (word hashes + exact verification, no n-gram strings) equal the
+    string-building definitions, including concatenations that collide across word borders
+    ("ab" + "c" == "a" + "bc") and multibyte words."""
+    import random
+
+    from textblaster_amd import native
+
+    top = native.host().find_top_duplicate
+    rng = random.Random(11)
+    vocab = ["a", "b", "ab", "c", "bc", "abc", "the", "æble", "øl", "á", "中文", "x"]
+    for _ in range(300):
+        words = [rng.choice(vocab[:rng.randint(2, len(vocab))]) for _ in range(rng.randint(0, 60))]
+        for n in range(1, 11):
+            assert top(words, n) == _ref_top(words, n), (words, n)
+            assert find_all_duplicate(words, n) == _ref_all_dup(words, n), (words, n)

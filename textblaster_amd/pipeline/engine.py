@@ -590,9 +590,10 @@ class Engine:
                                                              initializer=tracing.name_os_thread,
                                                              initargs=("tb-delegate",))
                 rb = row_base
+                presets = self._lid_presets(res, ndocs, delegated) if sub.dev is not None else None
 
-                def job(rows=delegated):
-                    r2 = self._process_subset_cpu(data, off, meta, rows)
+                def job(rows=delegated, presets=presets):
+                    r2 = self._process_subset_cpu(data, off, meta, rows, presets)
                     if rb:
                         for p in r2.kept + r2.excluded:
                             p.rows = p.rows + rb
@@ -601,7 +602,8 @@ class Engine:
                 result.deferred = (self._deleg_pool.submit(job), delegated)
                 result.n_delegated = len(delegated)
             else:
-                sub2 = self._process_subset_cpu(data, off, meta, delegated)
+                sub2 = self._process_subset_cpu(data, off, meta, delegated,
+                                                self._lid_presets(res, ndocs, delegated) if sub.dev is not None else None)
                 result.kept += sub2.kept
                 result.excluded += sub2.excluded
                 result.error_rows = np.concatenate([result.error_rows, sub2.error_rows])
@@ -692,7 +694,24 @@ class Engine:
             a = self._bw_flat = (fe, ec, et, term, roots, cjk, self._bw_gen, table)
         return a
 
-    def _process_subset_cpu(self, data, off, meta, rows: np.ndarray) -> BatchResult:
+    def _lid_presets(self, res, ndocs: int, rows: np.ndarray) -> Dict[int, np.ndarray]:
+        """Device records of the language-ID steps for documents ``rows``: the record needs no
+        segmentation and is exact for every script, so the CPU path of delegated documents
+        applies it instead of recomputing it."""
+        out = {}
+        if res is None or not len(rows):
+            return out
+        for sp in self.plan.steps:
+            if sp.stage < 0 or self.cfg.pipeline[sp.index].type != "LanguageDetectionFilter":
+                continue
+            _, layout = self.device_runner.stage_layout[sp.stage]
+            pos = self.plan.stages[sp.stage].index(sp.index)
+            _, width, prefix = layout[pos]
+            rec = np.asarray(res.stage_recs[sp.stage][prefix * ndocs:(prefix + width) * ndocs])
+            out[sp.index] = np.ascontiguousarray(rec.reshape(ndocs, width)[rows]).reshape(-1)
+        return out
+
+    def _process_subset_cpu(self, data, off, meta, rows: np.ndarray, presets=None) -> BatchResult:
         lens = off[rows + 1] - off[rows]
         sub_off = np.zeros(len(rows) + 1, dtype=np.int64)
         np.cumsum(lens, out=sub_off[1:])
@@ -708,7 +727,14 @@ class Engine:
             sub_meta = (np.ascontiguousarray(smd, dtype=np.uint8), smo, smv)
         md2, mo2, mv2 = sub_meta if sub_meta else (None, None, None)
         bs = self.h.BatchState(np.ascontiguousarray(sub_data, dtype=np.uint8), sub_off, md2, mo2, mv2, self.nthreads)
-        self._run_cpu_steps(bs, 0, len(self.steps), len(rows), "icu")
+        a = 0
+        for i in sorted(presets or {}):
+            # a device-exact record (language ID): applied, the steps before it run on the CPU
+            if i > a:
+                self._run_cpu_steps(bs, a, i, len(rows), "icu")
+            bs.apply_records(self.steps[i], i, presets[i], -1)
+            a = i + 1
+        self._run_cpu_steps(bs, a, len(self.steps), len(rows), "icu")
         res = self._collect(bs, len(rows), {})
         for p in res.kept + res.excluded:
             p.rows = rows[p.rows]

@@ -241,7 +241,7 @@ class Engine:
                 yield out
 
     # results whose delegated documents are still on the CPU path, at most this many held back
-    DEFERRED_DEPTH = 2
+    DEFERRED_DEPTH = 3
 
     def _deferred_in_order(self, results) -> Iterator[BatchResult]:
         """Yields results in order once their delegated (CPU-path) documents are merged in; the
@@ -586,7 +586,8 @@ class Engine:
                 import concurrent.futures as cf
 
                 if self._deleg_pool is None:
-                    self._deleg_pool = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="tb-delegate",
+                    # two batches' CPU work side by side (each also spreads over the native pool)
+                    self._deleg_pool = cf.ThreadPoolExecutor(max_workers=2, thread_name_prefix="tb-delegate",
                                                              initializer=tracing.name_os_thread,
                                                              initargs=("tb-delegate",))
                 rb = row_base
@@ -712,17 +713,17 @@ class Engine:
         return out
 
     def _process_subset_cpu(self, data, off, meta, rows: np.ndarray, presets=None) -> BatchResult:
-        lens = off[rows + 1] - off[rows]
-        sub_off = np.zeros(len(rows) + 1, dtype=np.int64)
-        np.cumsum(lens, out=sub_off[1:])
-        sub_data = np.concatenate([data[off[r]:off[r + 1]] for r in rows]) if len(rows) else np.zeros(0, np.uint8)
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        # (native gathers: one memcpy per document, no Python loop over the rows)
+        sub_data, sub_off = self.h.gather_spans(np.ascontiguousarray(data, dtype=np.uint8),
+                                                np.ascontiguousarray(off, dtype=np.int64), rows, self.nthreads)
+        sub_data = np.asarray(sub_data)[:int(sub_off[-1])]
         sub_meta = None
         if meta is not None and meta[0] is not None:
             md, mo, mv = meta
-            ml = mo[rows + 1] - mo[rows]
-            smo = np.zeros(len(rows) + 1, dtype=np.int64)
-            np.cumsum(ml, out=smo[1:])
-            smd = np.concatenate([md[mo[r]:mo[r + 1]] for r in rows]) if len(rows) else np.zeros(0, np.uint8)
+            smd, smo = self.h.gather_spans(np.ascontiguousarray(md, dtype=np.uint8),
+                                           np.ascontiguousarray(mo, dtype=np.int64), rows, self.nthreads)
+            smd = np.asarray(smd)[:int(smo[-1])]
             smv = mv[rows] if mv is not None else None
             sub_meta = (np.ascontiguousarray(smd, dtype=np.uint8), smo, smv)
         md2, mo2, mv2 = sub_meta if sub_meta else (None, None, None)

@@ -1205,9 +1205,9 @@ __global__ __launch_bounds__(256) void k_resolve(const DevResolve* __restrict__ 
 // dword and funnel-shifts them together (v_alignbyte), so interior bytes move 4 at a time whatever
 // the relative alignment; only the partial first and last destination dwords go byte by byte.
 // Source reads may run up to 3 bytes past a document (the batch and version buffers are padded).
-constexpr int kCompactThreads = 256;  // four documents per workgroup, one wave each
-constexpr int kCompactLanes = 64;
+constexpr int kCompactThreads = 256;  // LANES threads per document: 64 (four per workgroup) or 256
 
+template <int kCompactLanes>
 __global__ __launch_bounds__(kCompactThreads) void k_compact(const uint8_t* __restrict__ status,
                                                              const uint8_t* __restrict__ fver, VersionTab vt,
                                                              int32_t ndocs, const int64_t* __restrict__ sc,
@@ -2039,8 +2039,13 @@ int tb_resolve(hipStream_t stream, const void* rp, const int64_t* const* recs, i
     const int rc = tb_scan_strided_i64(stream, lanes + j, 4, ndocs, sc + (int64_t)j * ndocs);
     if (rc) return rc;
   }
-  hipLaunchKernelGGL(k_compact, dim3((ndocs + kCompactThreads / kCompactLanes - 1) / (kCompactThreads / kCompactLanes)),
-                     dim3(kCompactThreads), 0, stream, status, fver, vt, ndocs, sc, out, cap, out_off, rows,
+  // one wave per document (short documents, the common case), a whole workgroup per document once
+  // they average over 8 KB (the output holds every document, so cap / ndocs is about their length)
+  if (cap / (ndocs > 0 ? ndocs : 1) > 8192)
+    hipLaunchKernelGGL(k_compact<256>, dim3(ndocs), dim3(kCompactThreads), 0, stream, status, fver, vt, ndocs, sc, out, cap, out_off, rows,
+                     err);
+  else
+    hipLaunchKernelGGL(k_compact<64>, dim3((ndocs + 3) / 4), dim3(kCompactThreads), 0, stream, status, fver, vt, ndocs, sc, out, cap, out_off, rows,
                      err);
   return (int)hipGetLastError();
 }

@@ -565,6 +565,8 @@ class DeviceRunner:
         # k_stage_analyze_blk, csrc/hip/kernels.hip TB_BLK_WPE)
         self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", str(self.DEFAULT_LDS_BYTES_BLK)))
         self.block_threads = int(self.k.lib.tb_block_threads())  # threads of the long-document workgroups
+        # LDS slice of the split-order workgroups (k_gr_dup_split); TB_LDS_BYTES_DUP for tuning
+        self.lds_bytes_dup = int(os.environ.get("TB_LDS_BYTES_DUP", str(self.lds_bytes_blk)))
         # SURVEY 5.7 split: documents longer than this finish their duplicated n-gram orders in one
         # workgroup per order (k_gr_dup_split) instead of one after another in their stage
         # workgroup; 0 disables. Never below the long-document threshold (wave documents cannot
@@ -988,7 +990,7 @@ class DeviceRunner:
                             cur = rt.empty(1, np.uint32)
                             keep.append(cur)
                             self.k.gr_dup_split(self.stage_ts[s], gr_pos, d_perm[:n_split], n_split, n_tasks, ndocs,
-                                                gx, pw, pw_n, rec, flags, self.lds_bytes_blk, cur)
+                                                gx, pw, pw_n, rec, flags, self.lds_bytes_dup, cur)
                         ev_blk = self._record(slot.s_blk)
                         keep.append(ev_blk)
                 if lid_at and not lid_pass:

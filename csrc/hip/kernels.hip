@@ -1727,6 +1727,18 @@ __global__ __launch_bounds__(64) void k_pre_wsum(const int32_t* __restrict__ per
 
 }  // namespace
 
+// CUs of the current device (queried once; thread-safe static initialisation)
+static int device_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+        hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  return cus;
+}
+
 extern "C" {
 
 int tb_scan_strided_i64(hipStream_t stream, const int64_t* src, int64_t stride, int64_t n, int64_t* out);  // runtime.hip
@@ -1821,13 +1833,7 @@ int tb_gr_dup_split(hipStream_t stream, const void* stage, int32_t gr_step, cons
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k_gr_dup_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   // the persistent grid: resident workgroups per CU (registers, LDS) x CUs, at most one per task
-  static int cus = 0;
-  if (cus <= 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-        hipSuccess || cus <= 0)
-      cus = 256;
-  }
+  const int cus = device_cus();
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_gr_dup_split, kBlockThreads, lds_bytes) !=
           hipSuccess || per_cu <= 0)
@@ -1965,13 +1971,7 @@ int tb_langid_mfma(hipStream_t stream, const uint8_t* bytes, const int64_t* off,
   if (!E || !aux || !WT || !bias || !rec || width < 2 || !(w_scale > 0)) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
   const int ntiles = (ndocs + kLidTile - 1) / kLidTile;
-  static int cus = 0;
-  if (cus <= 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-        hipSuccess || cus <= 0)
-      cus = 256;
-  }
+  const int cus = device_cus();
   const int grid = ntiles < 4 * cus ? ntiles : 4 * cus;
   hipLaunchKernelGGL(k_langid_mfma, dim3(grid), dim3(64 * kLidWaves), 0, stream, bytes, off, perm, ndocs, t, E, aux,
                      WT, w_scale, bias, rec, width, prof);

@@ -678,8 +678,11 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     except BaseException:
         source.close()
         raise
-    if engine.backend == "cuda" and os.environ.get("TB_PINNED_READ", "1") not in ("", "0"):
-        reader.host_buffer = engine.host_buffer  # readers decode into pinned batch buffers from now on
+    # TB_PINNED_READ=1: readers copy each decoded batch into a pinned engine buffer (zero-copy
+    # upload). Off by default: the reader threads are this path's bottleneck and the extra copy
+    # there costs more than the staging copy it saves (profiles/r8_e2e/ab_pinned_read.txt)
+    if engine.backend == "cuda" and os.environ.get("TB_PINNED_READ", "0") not in ("", "0"):
+        reader.host_buffer = engine.host_buffer
     log.info("rank %d/%d: schedule=%s, %d units already done, backend=%s", rank, world, rc.schedule,
              local.units_skipped, engine.backend)
 

@@ -137,6 +137,9 @@ constexpr int kBlockThreads = TB_BLOCK_THREADS;
 // (174 VGPRs unconstrained). The kernel is latency-bound; config 5 (4096 x 50 KB documents,
 // profiles/r2_c5/blk_variants.txt): 70.9K docs/s unconstrained/64 KB, 110.0K at 4 waves/64 KB,
 // 113.7K at 6 waves/48 KB. TB_BLK_WPE=k builds another budget (0: none) for A/B runs.
+// Re-measured with the round-5 kernels (profiles/r8_blk4): 4 waves (128 VGPRs, 93 spilled
+// instead of 229) at 64 KB gives 139.9K vs 150.4K at 6 waves -- the spills stay cheaper than
+// the lost occupancy.
 #ifndef TB_BLK_WPE
 #define TB_BLK_WPE 6
 #endif

@@ -96,9 +96,18 @@ struct DevPlan {
 };
 
 // Per-document HBM scratch of the generic (analyze_stage / c4_pass_a) kernels:
-// kScratchPerByte * (len + 64) + 4096 bytes.
-constexpr uint64_t kScratchPerByte = 160;
-TB_HD uint64_t scratch_bytes_for_dev(uint32_t doc_len) { return kScratchPerByte * ((uint64_t)doc_len + 64) + 4096; }
+// rate * (len + 64) + 4096 bytes. The rates are the measured worst cases of the host port with
+// no LDS slice (every working array in HBM; tools/scratch_need.py, profiles/r8_scratch) plus
+// ~6%: 74.7 B/byte in one pass (one-letter words, 1 MB), 166.0 B/byte for a document whose
+// n-gram orders are split over workgroups (k_gr_dup_split / k_gr_split_wave: the stage export,
+// then one equal slice per task, each as large as the largest task needs). A document that still
+// runs out is flagged DOC_OVERFLOW and re-run on the CPU path, so the rates size memory, not
+// correctness.
+constexpr uint64_t kScratchPerByte = 80;
+constexpr uint64_t kScratchPerByteSplit = 176;
+TB_HD uint64_t scratch_bytes_for_dev(uint32_t doc_len, bool split = false) {
+  return (split ? kScratchPerByteSplit : kScratchPerByte) * ((uint64_t)doc_len + 64) + 4096;
+}
 
 TB_HD uint64_t dev_key(uint64_t h, uint32_t len) {
   uint64_t x = h ^ ((uint64_t)len * 0xD6E8FEB86659FD93ull);

@@ -182,7 +182,8 @@ struct DocCtx {
   char* scr = nullptr;       // global (HBM) scratch arena of this document
   uint64_t cap = 0;
   uint64_t used = 0;
-  char* lds = nullptr;       // optional fast arena (the wave's LDS slice on the device)
+  uint64_t peak = 0;         // high-water mark of `used` (sizes kScratchPerByte, devplan.h)
+  char* lds = nullptr;      // optional fast arena (the wave's LDS slice on the device)
   uint32_t lcap = 0;
   uint32_t lused = 0;        // bytes allocated from the bottom of the LDS slice
   uint32_t lhi = 0;          // bytes allocated from the top (temporaries, releasable props)
@@ -264,6 +265,7 @@ struct DocCtx {
       return (T*)scr;  // callers check `overflow` before using results
     }
     used = a + count * sizeof(T);
+    if (used > peak) peak = used;
     return (T*)(scr + a);
   }
   TB_HD void set_flag(uint32_t f) {

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -308,17 +309,44 @@ std::vector<uint64_t> pow_table(uint32_t n) {
   return pw;
 }
 
-uint64_t scratch_bytes_for(uint32_t doc_len) { return scratch_bytes_for_dev(doc_len); }
+uint64_t scratch_bytes_for(uint32_t doc_len, bool split) { return scratch_bytes_for_dev(doc_len, split); }
+
+// Largest per-byte arena need the emulators have seen: max over documents of
+// (peak - 4096) / (len + 64), kept in milli-bytes so one atomic max covers it.
+static std::atomic<uint64_t> g_scratch_need_milli{0};
+static std::atomic<uint64_t> g_scratch_need_len{0};
+static void note_scratch(uint64_t peak, uint32_t n) {
+  const uint64_t over = peak > 4096 ? peak - 4096 : 0;
+  const uint64_t m = over * 1000 / ((uint64_t)n + 64);
+  uint64_t cur = g_scratch_need_milli.load(std::memory_order_relaxed);
+  while (m > cur && !g_scratch_need_milli.compare_exchange_weak(cur, m)) {}
+  if (m >= cur) g_scratch_need_len.store(n, std::memory_order_relaxed);
+}
+// probe mode: the emulators give every document 1 KB of arena per byte, so no document
+// overflows and the high-water marks are the true needs
+static std::atomic<bool> g_scratch_probe{false};
+void set_scratch_probe(bool on) { g_scratch_probe = on; }
+static uint64_t emu_cap(uint32_t n, bool split) {
+  return g_scratch_probe ? 1024 * ((uint64_t)n + 64) + 4096 : scratch_bytes_for(n, split);
+}
+std::pair<double, uint32_t> scratch_need(bool reset) {
+  const std::pair<double, uint32_t> r{g_scratch_need_milli.load() / 1000.0, (uint32_t)g_scratch_need_len.load()};
+  if (reset) { g_scratch_need_milli = 0; g_scratch_need_len = 0; }
+  return r;
+}
 
 uint64_t line_stats_buffer_words(const int64_t* off, int64_t ndocs) { return line_stats_words(off, ndocs); }
 
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
                    std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes, const uint8_t* dead,
-                   bool weak_keys, uint32_t* line_stats) {
+                   bool weak_keys, uint32_t* line_stats, int split_tasks) {
   DevPlan* plan = new DevPlan();
   std::memset(plan, 0, sizeof(DevPlan));
   DevStage st = build_stage(steps, idx, *plan);
+  int gr_pos = -1;
+  for (int s = 0; s < st.n_steps; ++s)
+    if (st.steps[s].kind == DK_GOPHER_REP) gr_pos = s;
   bool has_lid = false;
   for (int s = 0; s < st.n_steps; ++s) has_lid |= st.steps[s].kind == DK_LANGID;
   if (has_lid && !lid) { delete plan; throw std::runtime_error("language model required"); }
@@ -334,7 +362,7 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
     for (int64_t i = a; i < b; ++i) {
       if (dead && dead[i]) continue;  // skipped by the device gate: record stays zero
       const uint32_t n = (uint32_t)(off[i + 1] - off[i]);
-      const uint64_t need = scratch_bytes_for(n);
+      const uint64_t need = emu_cap(n, split_tasks > 0 && gr_pos >= 0);
       if (scratch.size() < need) scratch.resize(need);
       DocCtx<SeqPar> x;
       x.ucd = ucd;
@@ -349,7 +377,39 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
       x.weak_keys = weak_keys;
       StageOut out{rec.data(), (uint32_t)ndocs, (uint32_t)i};
       if (line_stats) out.line_stats = line_stats + line_stats_base(off[i], i);
+      GrExport ex{};
+      if (split_tasks > 0 && gr_pos >= 0) out.gr_export = &ex;
       analyze_stage(x, st, *plan, lid ? lid->tables() : LidTables{nullptr, nullptr}, (const uint8_t*)data + off[i], n, out);
+      if (x.overflow) continue;
+      if (!out.gr_export || !ex.valid) {
+        note_scratch(x.peak, n);
+        continue;
+      }
+      // k_gr_dup_split, one task after another: task t works in slice t of the exported rest
+      const DevStep& ds = st.steps[gr_pos];
+      int64_t* r = rec.data() + (int64_t)ds.rec_prefix * ndocs + i * ds.width;
+      const uint64_t region = (ex.free_cap / (uint64_t)split_tasks) & ~255ull;
+      uint64_t task_peak = 0;
+      bool over = false;
+      for (int t = 0; t < split_tasks; ++t) {
+        DocCtx<SeqPar> y;
+        y.ucd = ucd;
+        y.pw = pw.data();
+        y.pw_n = x.pw_n;
+        y.ipw = x.ipw;
+        y.scr = ex.free_base + (uint64_t)t * region;
+        y.cap = region;
+        y.lds = lds_bytes ? lds.data() : nullptr;
+        y.lcap = lds_bytes;
+        y.flag = &flags[i];
+        if (t < ds.n_dup) gr_dup_one_order(y, ds, t, ex, r);
+        else if (t < ds.n_dup + ds.n_top) gr_top_one_order(y, ds, t - ds.n_dup, ex, r);
+        else if (t < ds.n_dup + ds.n_top + 2) gr_lines_split(y, t - ds.n_dup - ds.n_top, ex, r);
+        if (y.overflow) { y.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); over = true; }
+        task_peak = std::max<uint64_t>(task_peak, (y.peak + 255) & ~255ull);
+      }
+      // the slices are equal, so the document needs (export end) + tasks x (largest task)
+      if (!over) note_scratch((uint64_t)(ex.free_base - scratch.data()) + (uint64_t)split_tasks * task_peak, n);
     }
   });
   delete plan;
@@ -373,7 +433,7 @@ void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int6
     for (int64_t i = a; i < b; ++i) {
       if (dead && dead[i]) continue;  // skipped: record zeros, empty rewrite
       const uint32_t n = (uint32_t)(off[i + 1] - off[i]);
-      const uint64_t need = scratch_bytes_for(n);
+      const uint64_t need = emu_cap(n, false);
       if (scratch.size() < need) scratch.resize(need);
       DocCtx<SeqPar> x;
       x.ucd = ucd;
@@ -389,6 +449,7 @@ void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int6
       const uint8_t* b = (const uint8_t*)data + off[i];
       c4_pass_a(x, c4, b, n, rec.data() + i * rec::C4_WIDTH, src,
                 line_stats ? line_stats + line_stats_base(off[i], i) : nullptr);
+      if (!x.overflow) note_scratch(x.peak, n);
       if (flags[i] & DOC_NEEDS_CPU) continue;
       if (src[0] < 0) outs[i].assign((const char*)b, n);
       else outs[i].assign(scratch.data() + src[0], (size_t)src[1]);

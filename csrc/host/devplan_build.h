@@ -11,7 +11,11 @@
 namespace tb {
 
 // Per-document device scratch (devplan.h scratch_bytes_for_dev).
-uint64_t scratch_bytes_for(uint32_t doc_len);
+uint64_t scratch_bytes_for(uint32_t doc_len, bool split = false);
+// Largest (peak - 4096) / (len + 64) arena bytes per text byte used by an emulated document
+// since the last reset, and that document's length.
+std::pair<double, uint32_t> scratch_need(bool reset);
+void set_scratch_probe(bool on);  // emulators: unbounded arenas (measure needs, never overflow)
 
 int dev_kind_of(const StepCfg& c);
 bool device_supported(const StepCfg& c, std::string* why);
@@ -36,7 +40,10 @@ std::vector<uint64_t> pow_table(uint32_t n);  // B^0..B^n followed by B^-0..B^-n
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
                    std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes = 0,
-                   const uint8_t* dead = nullptr, bool weak_keys = false, uint32_t* line_stats = nullptr);
+                   const uint8_t* dead = nullptr, bool weak_keys = false, uint32_t* line_stats = nullptr,
+                   int split_tasks = 0);
+// split_tasks > 0: every document runs the intra-document split of its GopherRepetition step
+// (stage export, then the k_gr_dup_split tasks in turn, each in its slice of the arena rest)
 uint64_t line_stats_buffer_words(const int64_t* off, int64_t ndocs);  // u32 size of a batch's line export
 // line_stats: the C4 line export of the batch (docproc.h line_stats_base layout), written by
 // emulate_stage and read by emulate_c4 of the same content version, as on the device

@@ -855,7 +855,12 @@ PYBIND11_MODULE(_tbhost, m) {
     return py::make_tuple(d.width_total, out);
   });
   m.def("pow_table", [](uint32_t n) { return to_numpy(pow_table(n)); });
-  m.def("scratch_bytes_for", [](uint32_t n) { return scratch_bytes_for(n); });
+  m.def("scratch_bytes_for", [](uint32_t n, bool split) { return scratch_bytes_for(n, split); }, py::arg("n"),
+        py::arg("split") = false);
+  m.def("scratch_need", [](bool reset) { return scratch_need(reset); }, py::arg("reset") = false);
+  m.def("set_scratch_probe", &set_scratch_probe);
+  m.attr("SCRATCH_PER_BYTE") = kScratchPerByte;
+  m.attr("SCRATCH_PER_BYTE_SPLIT") = kScratchPerByteSplit;
   m.attr("C4_MAX_GROWTH") = kC4MaxGrowth;
   m.attr("SIZEOF_DEV_PLAN") = sizeof(DevPlan);
   m.attr("SIZEOF_DEV_STAGE") = sizeof(DevStage);
@@ -867,7 +872,7 @@ PYBIND11_MODULE(_tbhost, m) {
                             py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
                             int nthreads, std::shared_ptr<LangidModel> lid, uint32_t lds_bytes,
                             std::optional<py::array_t<uint8_t, py::array::c_style>> dead, bool weak_keys,
-                            std::optional<py::array_t<uint32_t, py::array::c_style>> line_stats) {
+                            std::optional<py::array_t<uint32_t, py::array::c_style>> line_stats, int split_tasks) {
     std::vector<int64_t> rec;
     std::vector<uint32_t> flags;
     const int64_t nd = (int64_t)off.size() - 1;
@@ -881,12 +886,12 @@ PYBIND11_MODULE(_tbhost, m) {
     {
       py::gil_scoped_release nogil;
       emulate_stage(steps, idx, nd, (const char*)data.data(), off.data(), nthreads, lid.get(), rec, flags, lds_bytes,
-                    dp, weak_keys, lp);
+                    dp, weak_keys, lp, split_tasks);
     }
     return py::make_tuple(to_numpy(std::move(rec)), to_numpy(std::move(flags)));
   }, py::arg("steps"), py::arg("idx"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8,
      py::arg("lid") = nullptr, py::arg("lds_bytes") = 0, py::arg("dead") = py::none(),
-     py::arg("weak_keys") = false, py::arg("line_stats") = py::none());
+     py::arg("weak_keys") = false, py::arg("line_stats") = py::none(), py::arg("split_tasks") = 0);
   m.def("line_stats_words", [](py::array_t<int64_t, py::array::c_style> off) {
     return line_stats_buffer_words(off.data(), (int64_t)off.size() - 1);
   }, "u32 words of a batch's C4 line export buffer (docproc.h line_stats_base)");

@@ -169,3 +169,39 @@ def test_mixed_script_delegation_is_overlapped_and_exact():
         # the CJK documents fail the language gate on the device: not delegated
         assert 0 < r.n_delegated <= len(dict_docs) - len(cjk_docs), (r.n_delegated, len(dict_docs), len(cjk_docs))
     assert n_dict > 0
+
+
+def test_split_tasks_equal_one_pass_and_fit_the_reservation(host):
+    """The intra-document n-gram split (stage export, then one k_gr_dup_split task per order and
+    for duplicated lines / paragraphs, each in its slice of the document's arena) gives the same
+    records as the one-pass stage, and neither path outgrows the devplan.h reservation
+    (kScratchPerByte / kScratchPerByteSplit, sized by tools/scratch_need.py)."""
+    from textblaster_amd.models.langid import load_default
+    from textblaster_amd.pipeline.plan import build_plan
+
+    lid = load_default().native()
+    cfg = load_pipeline_config("config/bench_pipeline.yaml")
+    steps = [host.make_step(s.native_dict()) for s in cfg.pipeline]
+    plan = build_plan(cfg)
+    gr = [steps[i] for i, s in enumerate(cfg.pipeline) if s.type == "GopherRepetitionFilter"][0]
+    tasks = gr.n_dup + gr.n_top + 2
+    texts = synth.make_corpus(120, 3000, seed=43) + EDGE + ["a " * 3000, "a\n" * 3000, "A b. " * 1200,
+                                                             "x [1] " * 900, "a b.\n\n" * 900]
+    data, off = synth.pack(texts)
+    host.set_scratch_probe(True)
+    try:
+        for idx in plan.stages:
+            host.scratch_need(True)
+            r0, f0 = host.emulate_stage(steps, idx, data, off, 4, lid, 0)
+            one, _ = host.scratch_need(True)
+            r1, f1 = host.emulate_stage(steps, idx, data, off, 4, lid, 0, split_tasks=tasks)
+            split, _ = host.scratch_need(True)
+            np.testing.assert_array_equal(f0, f1)
+            np.testing.assert_array_equal(r0, r1)
+            assert one <= host.SCRATCH_PER_BYTE and split <= host.SCRATCH_PER_BYTE_SPLIT, (one, split)
+    finally:
+        host.set_scratch_probe(False)
+    # under the real reservation nothing overflows (DOC_OVERFLOW = 2, docproc.h -> CPU path)
+    for idx in plan.stages:
+        _, f = host.emulate_stage(steps, idx, data, off, 4, lid, 0, split_tasks=tasks)
+        assert not (f & 2).any()

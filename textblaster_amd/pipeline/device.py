@@ -436,7 +436,7 @@ class DeviceRunner:
         self.stream_layout = "serial" if serial else os.environ.get("TB_STREAMS", "6")
         if self.stream_layout not in ("serial", "4", "4c", "4f", "5", "6", "13"):
             raise DeviceError("TB_STREAMS must be one of 4, 4c, 4f, 5, 6, 13")
-        # Batches in flight on the device. Each slot holds its own scratch arena (~160 B per text
+        # Batches in flight on the device. Each slot holds its own scratch arena (<= 176 B per text
         # byte, x1.25 headroom): three slots keep the GPU fed (interleaved A/B, 20-step headline
         # bench: 35.3 vs 38.6 ms/step, profiles/r2_slots/ab.txt) and fit 288 GB of HBM with
         # 384 MB device batches; a smaller device gets two. TB_SLOTS overrides.
@@ -448,7 +448,7 @@ class DeviceRunner:
                 _, total = hiprt.mem_info()
             except Exception:  # noqa: BLE001 - no info: the conservative choice
                 total = 0
-            per_slot = int(1.25 * 160 * max_batch_bytes) + (2 << 30)  # arena + staged/output buffers
+            per_slot = int(1.25 * 176 * max_batch_bytes) + (2 << 30)  # arena + staged/output buffers
             self.N_SLOTS = 3 if total >= 3 * per_slot + (8 << 30) else 2
         self.slots = [_Slot() for _ in range(self.N_SLOTS)]
         if self.stream_layout == "serial":
@@ -863,7 +863,19 @@ class DeviceRunner:
         lens = np.diff(off)
         perm = launch_order(lens)
         lens_perm = lens[perm]
-        per_doc = (h.scratch_bytes_for(0) - 64 * 160) + 160 * (lens + 64)
+        # scratch slice per document (devplan.h scratch_bytes_for_dev): the split rate for the
+        # documents whose n-gram orders run in split tasks (k_gr_dup_split over the workgroup
+        # documents past split_doc_bytes, k_gr_split_wave over wave documents past ngram_big_bytes)
+        rate = np.full(ndocs, h.SCRATCH_PER_BYTE, dtype=np.int64)
+        if self.gr_split:
+            is_long = lens > self.long_doc_bytes if self.long_doc_bytes > 0 else np.zeros(ndocs, bool)
+            split = np.zeros(ndocs, bool)
+            if self.split_doc_bytes > 0:
+                split |= is_long & (lens > self.split_doc_bytes)
+            if self.wave_split:
+                split |= ~is_long & (lens > self.ngram_big_bytes)
+            rate[split] = h.SCRATCH_PER_BYTE_SPLIT
+        per_doc = (h.scratch_bytes_for(0) - 64 * h.SCRATCH_PER_BYTE) + rate * (lens + 64)
         per_doc = (per_doc + SCRATCH_ALIGN - 1) // SCRATCH_ALIGN * SCRATCH_ALIGN
         # slices in dispatch (perm) order: scratch_off[k] is the slice of the k-th launched
         # document, so the waves resident at one time share one contiguous window of the arena

@@ -115,8 +115,8 @@ class Engine:
         self._async_delegation = False
         # process_many on the GPU backend submits from a helper thread (TB_PREFETCH_THREAD=0: off)
         self.prefetch_threads = os.environ.get("TB_PREFETCH_THREAD", "1") not in ("", "0")
-        # text bytes per device batch (scratch ~160 B per text byte per in-flight slot: 384 MB of
-        # text -> ~77 GB of HBM per slot, three slots in flight on a 288 GB MI355X)
+        # text bytes per device batch (scratch 80-176 B per text byte per in-flight slot: 384 MB of
+        # text -> at most ~85 GB of HBM per slot, three slots in flight on a 288 GB MI355X)
         self.max_batch_bytes = int(os.environ.get("TB_MAX_BATCH_BYTES", str(384 << 20)))
         self.h = native.host()
         self.plan: ExecPlan = build_plan(cfg)
@@ -197,7 +197,7 @@ class Engine:
         ``on_error="recover"``: a batch whose device work fails (HIP error, out of memory, an
         injected fault) is re-run split in two halves, and if that fails too, on the CPU oracle
         path; the failure is logged and counted, the run continues."""
-        # Device batches are bounded in bytes (the per-document scratch arena is ~160x the text):
+        # Device batches are bounded in bytes (the per-document scratch arena is <= 176x the text):
         # a large input batch runs as several sub-batches whose results are merged back.
         groups: Dict[int, List] = {}
         sizes: Dict[int, int] = {}
@@ -348,12 +348,12 @@ class Engine:
                 if sync is not None:
                     sync()
 
-    # HBM scratch of the generic document kernels per device batch: 160 B per text byte plus a
-    # fixed ~14 KB per document (csrc/common/devplan.h scratch_bytes_for_dev); DeviceRunner sizes
-    # its slots for 1.25 x 160 x max_batch_bytes, so batches of many short documents are also cut
-    # at that scratch budget (a 384 MB batch of 200-byte documents would need ~110 GB otherwise)
-    SCRATCH_PER_BYTE = 160
-    SCRATCH_PER_DOC = 160 * 64 + 4096
+    # HBM scratch of the generic document kernels per device batch: at most 176 B per text byte
+    # (80 for documents without the n-gram split) plus a fixed ~15 KB per document
+    # (csrc/common/devplan.h scratch_bytes_for_dev); batches of many short documents are also cut
+    # at that scratch budget (a 384 MB batch of 200-byte documents would need ~80 GB otherwise)
+    SCRATCH_PER_BYTE = 176
+    SCRATCH_PER_DOC = 176 * 64 + 4096
 
     def host_buffer(self, nbytes: int) -> np.ndarray:
         """A uint8 host buffer for batch text: page-locked (hiprt.pinned) on the GPU backend, so a
@@ -375,7 +375,7 @@ class Engine:
         budget = self.SCRATCH_PER_BYTE * self.max_batch_bytes
         if nbytes <= self.max_batch_bytes and self.SCRATCH_PER_BYTE * nbytes + self.SCRATCH_PER_DOC * n <= budget:
             return [(0, item)]
-        # cumulative scratch need of documents [0, k): 160 B x bytes + the per-document constant
+        # cumulative scratch need of documents [0, k): 176 B x bytes + the per-document constant
         need = self.SCRATCH_PER_BYTE * (off - off[0]) + self.SCRATCH_PER_DOC * np.arange(n + 1, dtype=np.int64)
         out, a = [], 0
         while a < n:

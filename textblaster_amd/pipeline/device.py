@@ -593,6 +593,12 @@ class DeviceRunner:
         # wave documents finish their n-gram orders in one wave per (document, order)
         # (k_gr_split_wave, LDS slice TB_LDS_BYTES_SPLIT); TB_WAVE_SPLIT=0 keeps them in the stage
         self.wave_split = os.environ.get("TB_WAVE_SPLIT", "1") not in ("", "0")
+        # scratch bytes per text byte (one pass, split documents): devplan.h; TB_SCRATCH_RATE=a,b (or axb)
+        # overrides for A/B runs (larger only: smaller slices send documents to the CPU path)
+        self.scratch_rates = (int(h.SCRATCH_PER_BYTE), int(h.SCRATCH_PER_BYTE_SPLIT))
+        if os.environ.get("TB_SCRATCH_RATE"):
+            a, b = (int(v) for v in os.environ["TB_SCRATCH_RATE"].replace("x", ",").split(","))
+            self.scratch_rates = (max(a, self.scratch_rates[0]), max(b, self.scratch_rates[1]))
         # (5 KB = 8 waves/SIMD: 2.68 ms/step vs 2.80 at 6 KB and 3.44 at 4 KB, profiles/r8_wpe/;
         # round-5 start: 6 KB beat 4 and 8, profiles/r7_ngram/ab_occupancy.txt)
         self.lds_bytes_split = int(os.environ.get("TB_LDS_BYTES_SPLIT", "5120"))
@@ -866,7 +872,8 @@ class DeviceRunner:
         # scratch slice per document (devplan.h scratch_bytes_for_dev): the split rate for the
         # documents whose n-gram orders run in split tasks (k_gr_dup_split over the workgroup
         # documents past split_doc_bytes, k_gr_split_wave over wave documents past ngram_big_bytes)
-        rate = np.full(ndocs, h.SCRATCH_PER_BYTE, dtype=np.int64)
+        r_one, r_split = self.scratch_rates
+        rate = np.full(ndocs, r_one, dtype=np.int64)
         if self.gr_split:
             is_long = lens > self.long_doc_bytes if self.long_doc_bytes > 0 else np.zeros(ndocs, bool)
             split = np.zeros(ndocs, bool)
@@ -874,8 +881,8 @@ class DeviceRunner:
                 split |= is_long & (lens > self.split_doc_bytes)
             if self.wave_split:
                 split |= ~is_long & (lens > self.ngram_big_bytes)
-            rate[split] = h.SCRATCH_PER_BYTE_SPLIT
-        per_doc = (h.scratch_bytes_for(0) - 64 * h.SCRATCH_PER_BYTE) + rate * (lens + 64)
+            rate[split] = r_split
+        per_doc = 4096 + rate * (lens + 64)
         per_doc = (per_doc + SCRATCH_ALIGN - 1) // SCRATCH_ALIGN * SCRATCH_ALIGN
         # slices in dispatch (perm) order: scratch_off[k] is the slice of the k-th launched
         # document, so the waves resident at one time share one contiguous window of the arena

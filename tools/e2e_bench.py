@@ -132,6 +132,10 @@ def main():
                 "cpu_seconds_by_os_thread": cpu,
                 # the native worker pool's CPU seconds by job (tb-pool threads + the submitting thread)
                 "pool_cpu_seconds_by_job": _delta(pool0, _pool_stats())}
+        # "other" (CPU outside the reader / encoder / writer threads) less the native pool's
+        # attributed jobs: what is left is the Python main loop, GPU runtime threads and the rest
+        pool_jobs = sum(line["pool_cpu_seconds_by_job"].values())
+        line["cpu_seconds"]["other_minus_pool_jobs"] = round(line["cpu_seconds"].get("other", 0.0) - pool_jobs, 3)
         print(json.dumps(line), flush=True)
         rates.setdefault(backend, []).append(line["docs_per_sec"])
         if tl:

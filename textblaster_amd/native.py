@@ -12,7 +12,9 @@ Both are built in-tree (``textblaster_amd/``) so they travel with the repository
 from __future__ import annotations
 
 import ctypes
+import json
 import os
+import re
 import subprocess
 import sys
 import sysconfig
@@ -54,12 +56,33 @@ def _newest(paths: List[str]) -> float:
     return max((os.path.getmtime(p) for p in paths), default=0.0)
 
 
-def _run(cmd: List[str], verbose: bool) -> None:
+def _run(cmd: List[str], verbose: bool) -> str:
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"native build failed:\n{' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+RESOURCES_JSON = os.path.join(BUILD_DIR, "hip", "kernel_resources.json")
+
+
+def parse_resource_remarks(text: str) -> dict:
+    """Per-kernel resources from hipcc's -Rpass-analysis=kernel-resource-usage remarks:
+    {mangled name: {"VGPRs": .., "VGPRs Spill": .., "ScratchSize [bytes/lane]": .., "Occupancy
+    [waves/SIMD]": .., ...}}."""
+    out: dict = {}
+    cur = None
+    for line in text.splitlines():
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = out.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:\s+([A-Za-z][^:]*): (\d+) \[", line)
+        if m and cur is not None:
+            cur[m.group(1).strip()] = int(m.group(2))
+    return out
 
 
 def build_host(verbose: bool = False, force: bool = False) -> str:
@@ -114,12 +137,28 @@ def build_hip(verbose: bool = False, force: bool = False) -> str:
 
     def compile_one(src: str) -> str:
         obj = os.path.join(BUILD_DIR, "hip", os.path.basename(src) + ".o")
+        rep = obj + ".resources.json"
         if force or not os.path.exists(obj) or os.path.getmtime(obj) < _newest([src] + hdrs):
-            _run([hipcc, *flags, "-c", src, "-o", obj], verbose)
+            # the compiler's per-kernel register / spill / occupancy report comes with the build
+            # (tests/test_kernel_resources.py checks it against csrc/hip/resource_budget.json)
+            log = _run([hipcc, *flags, "-Rpass-analysis=kernel-resource-usage", "-c", src, "-o", obj], False)
+            if verbose:
+                print(f"{os.path.basename(src)}: built", flush=True)
+            with open(rep, "w") as f:
+                json.dump(parse_resource_remarks(log), f, indent=1, sort_keys=True)
         return obj
 
     with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
         objs = list(ex.map(compile_one, srcs))
+    merged: dict = {}
+    for o in objs:
+        try:
+            with open(o + ".resources.json") as f:
+                merged.update(json.load(f))
+        except OSError:
+            pass
+    with open(RESOURCES_JSON, "w") as f:
+        json.dump(merged, f, indent=1, sort_keys=True)
     tmp = HIP_LIB + ".tmp"
     _run([hipcc, f"--offload-arch={GPU_ARCH}", "-shared", "-fPIC", "-o", tmp, *objs], verbose)
     os.replace(tmp, HIP_LIB)

@@ -78,6 +78,10 @@ struct Cps {
   TB_HD uint32_t o(uint32_t i) const { return ent ? (ent[i] & 0xFFFFu) : off[i]; }
   TB_HD uint32_t p(uint32_t i) const { return ent ? (ent[i] >> 16) : (uint32_t)prop[i]; }
   TB_HD uint8_t lead(uint32_t i) const { return b[o(i)]; }
+  // lead(i) == '\n' from the properties alone (U+000A is the only code point of word-break
+  // class LF): one read of the per-code-point array (LDS on the wave path) instead of the
+  // offset read followed by a dependent read of the text
+  TB_HD bool is_lf(uint32_t i) const { return (p(i) & P_WB_MASK) == (uint32_t)WB_LF; }
   TB_HD uint32_t cp(uint32_t i) const {
     int len;
     return utf8_decode(b, o(i), nb, &len);
@@ -481,12 +485,12 @@ TB_HD Lines rust_lines(DocCtx<P>& x, const Cps& c) {
   uint32_t* ls = L.ls;
   uint32_t* le = L.le;
   L.n = x.par.template compact<int>(
-      C, [&](uint32_t i, int&) { return i == 0 || c.lead(i - 1) == '\n'; },
+      C, [&](uint32_t i, int&) { return i == 0 || c.is_lf(i - 1); },
       [&](uint32_t i, uint32_t k, int&) { ls[k] = i; });
   x.par.sync();
   const uint32_t NL = L.n;
   x.par.for_n(NL, [&](uint32_t k) {
-    uint32_t e = (k + 1 < NL) ? ls[k + 1] - 1 : (c.lead(C - 1) == '\n' ? C - 1 : C);
+    uint32_t e = (k + 1 < NL) ? ls[k + 1] - 1 : (c.is_lf(C - 1) ? C - 1 : C);
     uint32_t ce = e;
     if (e < C && ce > ls[k] && c.lead(ce - 1) == '\r') --ce;
     le[k] = ce;
@@ -1175,11 +1179,11 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
         span,
         [&](uint32_t i, int&) {
           const uint32_t j = tcs + i;
-          return c.lead(j) == '\n' && c.lead(j - 1) != '\n';
+          return c.is_lf(j) && !c.is_lf(j - 1);
         },
         [&](uint32_t i, uint32_t k, int&) {
           uint32_t j = tcs + i, q = j;
-          while (c.lead(q) == '\n') ++q;
+          while (c.is_lf(q)) ++q;
           rs[k] = j;
           rl[k] = q - j;
         });
@@ -2454,7 +2458,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
       dup_spans(x, b, ph, NB,
                 [&](uint32_t q, uint32_t& s0, uint32_t& e0) { s0 = off[L.ls[nb[q]]]; e0 = off[L.le[nb[q]]]; },
                 &dup_e, &dup_b);
-      int64_t nl = x.par.template sum<int64_t>(C, [&](uint32_t i) { return (int64_t)(c.lead(i) == '\n'); });
+      int64_t nl = x.par.template sum<int64_t>(C, [&](uint32_t i) { return (int64_t)c.is_lf(i); });
       x.par.single([&]() {
         r[0] = NB; r[1] = stop_end; r[2] = shrt; r[3] = dup_b; r[4] = (int64_t)C - nl; r[5] = nl; r[6] = W;
       });

@@ -706,6 +706,11 @@ TB_HD bool bytes_eq(const uint8_t* b, uint32_t a0, uint32_t a1, uint32_t b0, uin
 template <class P, class SpanF>
 TB_HD void dup_spans(DocCtx<P>& x, const uint8_t* b, const PHView& ph, uint32_t n, SpanF&& span,
                      int64_t* out_elems, int64_t* out_bytes) {
+  if (n <= 1) {  // one span (a single line / paragraph) repeats nothing: no table, no scans
+    *out_elems = 0;
+    *out_bytes = 0;
+    return;
+  }
   const auto mark = x.mark();
   uint32_t* canon = x.template alloc_hot<uint32_t>(n + 1);
   if (x.overflow) return;

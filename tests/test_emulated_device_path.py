@@ -205,3 +205,32 @@ def test_split_tasks_equal_one_pass_and_fit_the_reservation(host):
     for idx in plan.stages:
         _, f = host.emulate_stage(steps, idx, data, off, 4, lid, 0, split_tasks=tasks)
         assert not (f & 2).any()
+
+
+def test_language_id_after_c4_is_recomputed_for_delegated_documents(tmp_path):
+    """A LanguageDetectionFilter placed after C4QualityFilter reads the rewritten text. For a
+    delegated (dictionary-script) document the device's rewritten text is not the CPU path's, so
+    its language-ID record must not be reused: the outputs equal the CPU oracle on a mixed-script
+    corpus (the presets are limited to stages that read content version 0)."""
+    cfg_text = open("config/bench_pipeline.yaml").read()
+    lid = "  - {type: LanguageDetectionFilter, min_confidence: 0.65, allowed_languages: [dan, eng, swe, nob, nno]}\n"
+    assert lid in cfg_text
+    # (no stop-word minimum, so delegated documents get past GopherQuality and C4 to the last step)
+    cfg_text = cfg_text.replace(lid, "").replace("min_stop_words: 2", "min_stop_words: 0") + \
+        "  - {type: LanguageDetectionFilter, min_confidence: 0.5, allowed_languages: [dan, eng, swe, nob, nno]}\n"
+    p = tmp_path / "lid_after_c4.yaml"
+    p.write_text(cfg_text)
+    cfg = load_pipeline_config(str(p))
+    assert [s.type for s in cfg.pipeline][-1] == "LanguageDetectionFilter"
+    texts = synth.make_corpus(900, 800, seed=77, mixed_script=True)
+    data, off = synth.pack(texts)
+    emu = Engine(cfg, backend="emulate", nthreads=4, keep_reasons=True)
+    cpu = Engine(cfg, backend="cpu", segmentation="icu", nthreads=4, keep_reasons=True)
+    for got in (emu.process(data, off), next(iter(emu.process_many([(data, off)])))):
+        ref = cpu.process(data, off)
+        assert got.n_delegated > 0
+        assert (ref.fail_step[np.nonzero(ref.status == 0)[0]] == -1).all()
+        np.testing.assert_array_equal(got.fail_step, ref.fail_step)
+        np.testing.assert_array_equal(got.status, ref.status)
+        assert got.reasons == ref.reasons
+        assert outputs(got) == outputs(ref)

@@ -31,6 +31,10 @@ from ..errors import ConfigError, DeviceError, Unexpected
 from ..utils import tracing
 from .plan import ExecPlan, build_plan
 
+# per-document device flag bits (csrc/common/docproc.h DocFlag)
+DOC_NEEDS_CPU = 1
+DOC_OVERFLOW = 2
+
 
 @dataclasses.dataclass
 class OutputPart:
@@ -594,7 +598,7 @@ class Engine:
                 presets = self._lid_presets(res, ndocs, delegated) if sub.dev is not None else None
 
                 def job(rows=delegated, presets=presets):
-                    r2 = self._process_subset_cpu(data, off, meta, rows, presets)
+                    r2 = self._process_delegated(data, off, meta, rows, presets)
                     if rb:
                         for p in r2.kept + r2.excluded:
                             p.rows = p.rows + rb
@@ -603,8 +607,8 @@ class Engine:
                 result.deferred = (self._deleg_pool.submit(job), delegated)
                 result.n_delegated = len(delegated)
             else:
-                sub2 = self._process_subset_cpu(data, off, meta, delegated,
-                                                self._lid_presets(res, ndocs, delegated) if sub.dev is not None else None)
+                sub2 = self._process_delegated(data, off, meta, delegated,
+                                               self._lid_presets(res, ndocs, delegated) if sub.dev is not None else None)
                 result.kept += sub2.kept
                 result.excluded += sub2.excluded
                 result.error_rows = np.concatenate([result.error_rows, sub2.error_rows])
@@ -695,21 +699,72 @@ class Engine:
             a = self._bw_flat = (fe, ec, et, term, roots, cjk, self._bw_gen, table)
         return a
 
-    def _lid_presets(self, res, ndocs: int, rows: np.ndarray) -> Dict[int, np.ndarray]:
+    def _lid_presets(self, res, ndocs: int, rows: np.ndarray):
         """Device records of the language-ID steps for documents ``rows``: the record needs no
         segmentation and is exact for every script, so the CPU path of delegated documents
-        applies it instead of recomputing it."""
+        applies it instead of recomputing it.
+
+        Only steps whose stage reads the input text (content version 0) qualify: after a
+        C4QualityFilter the device's rewritten text of a delegated document is not the text the
+        CPU path rewrites (k_c4_pass_a stops at a dictionary script and leaves the version
+        empty). A row is eligible only if no scratch overflow was flagged for it and no device
+        gate skipped it in or before the language-ID pass. Returns ``(presets, eligible)``:
+        ``presets[step]`` is the flat record array over ``rows`` and ``eligible`` a bool mask
+        over ``rows`` (ineligible rows recompute every step on the CPU path)."""
         out = {}
+        eligible = np.ones(len(rows), dtype=bool)
         if res is None or not len(rows):
-            return out
+            return out, eligible
+        flags = getattr(res, "flags", None)
+        if flags is not None:
+            eligible &= (np.asarray(flags)[rows] & DOC_OVERFLOW) == 0
+        dead = getattr(res, "dead", None)
         for sp in self.plan.steps:
             if sp.stage < 0 or self.cfg.pipeline[sp.index].type != "LanguageDetectionFilter":
+                continue
+            if self.plan.stage_version[sp.stage] != 0:
                 continue
             _, layout = self.device_runner.stage_layout[sp.stage]
             pos = self.plan.stages[sp.stage].index(sp.index)
             _, width, prefix = layout[pos]
             rec = np.asarray(res.stage_recs[sp.stage][prefix * ndocs:(prefix + width) * ndocs])
             out[sp.index] = np.ascontiguousarray(rec.reshape(ndocs, width)[rows]).reshape(-1)
+            if dead is not None:
+                p = res.pass_of_step.get(sp.index, 0)
+                d = np.asarray(dead)[rows]
+                eligible &= ~((d != 0) & (d <= p))
+        return out, eligible
+
+    def _process_delegated(self, data, off, meta, rows: np.ndarray, presets=None) -> BatchResult:
+        """CPU path of delegated documents ``rows``; ``presets`` = ``_lid_presets`` output.
+        Rows whose device language-ID record is not usable run every step on the CPU."""
+        if presets is None or not presets[0]:
+            return self._process_subset_cpu(data, off, meta, rows)
+        recs, eligible = presets
+        if eligible.all():
+            return self._process_subset_cpu(data, off, meta, rows, recs)
+        parts = []
+        ok = np.nonzero(eligible)[0]
+        bad = np.nonzero(~eligible)[0]
+        if len(ok):
+            sub_recs = {}
+            for i, rec in recs.items():
+                w = len(rec) // len(rows)
+                sub_recs[i] = np.ascontiguousarray(rec.reshape(len(rows), w)[ok]).reshape(-1)
+            parts.append((ok, self._process_subset_cpu(data, off, meta, rows[ok], sub_recs)))
+        parts.append((bad, self._process_subset_cpu(data, off, meta, rows[bad])))
+        fail = np.zeros(len(rows), dtype=parts[0][1].fail_step.dtype)
+        status = np.zeros(len(rows), dtype=parts[0][1].status.dtype)
+        out = BatchResult(len(rows), [], [], np.zeros(0, dtype=np.int64), fail, status, {}, {})
+        errs = []
+        for pos, r in parts:
+            out.kept += r.kept
+            out.excluded += r.excluded
+            errs.append(r.error_rows)
+            fail[pos] = r.fail_step
+            status[pos] = r.status
+            out.reasons.update(r.reasons)
+        out.error_rows = np.concatenate(errs)
         return out
 
     def _process_subset_cpu(self, data, off, meta, rows: np.ndarray, presets=None) -> BatchResult:

@@ -421,7 +421,8 @@ class _ClaimGate:
     (the reference's ``basic_qos(prefetch_count)``, utils/common.rs:91-94)."""
 
     def __init__(self, ahead: int):
-        self.sem = threading.Semaphore(max(1, ahead))
+        self.ahead = max(1, ahead)
+        self.sem = threading.Semaphore(self.ahead)
         self.last: set = set()
         self.closed = False
 
@@ -447,11 +448,16 @@ def _claimed(ctx: DistContext, key: str, groups: List[List[Unit]], claimed: List
         yield groups[i]
 
 
-def _read_units(reader: ParquetReader, groups, nthreads: int, timer: _UnitReader):
+def _read_units(reader: ParquetReader, groups, nthreads: int, timer: _UnitReader, window: Optional[int] = None):
     """Yields (unit, DocBatch) of the row-group ``groups`` (an iterable, consumed lazily) in
     order. Row groups are decoded by up to ``nthreads`` worker threads at once (Parquet
     decompression + HTML-entity decoding dominate the input side); each row group is read once
-    and sliced into its units."""
+    and sliced into its units.
+
+    At most ``window`` groups (default ``nthreads + 1``) are taken from ``groups`` and not yet
+    yielded. ``groups`` may block on a claim gate whose tokens come back only after yielded
+    groups reach the main loop; so the next group is taken only after the previous one was
+    yielded, and a gate bound of ``window`` or more can never starve the reader."""
     import concurrent.futures as cf
 
     def load(group: List[Unit]):
@@ -466,20 +472,22 @@ def _read_units(reader: ParquetReader, groups, nthreads: int, timer: _UnitReader
         for g in groups:
             yield from load(g)
         return
+    window = max(1, min(nthreads + 1, window or nthreads + 1))
     with cf.ThreadPoolExecutor(max_workers=nthreads, thread_name_prefix="tb-reader",
                                initializer=tracing.name_os_thread, initargs=("tb-reader",)) as ex:
         pending: collections.deque = collections.deque()
         it = iter(groups)
-        for g in it:
-            pending.append(ex.submit(load, g))
-            if len(pending) >= nthreads + 1:
-                break
-        while pending:
-            fut = pending.popleft()
-            nxt = next(it, None)
-            if nxt is not None:
-                pending.append(ex.submit(load, nxt))
-            yield from fut.result()
+        exhausted = False
+        while True:
+            while not exhausted and len(pending) < window:
+                g = next(it, None)
+                if g is None:
+                    exhausted = True
+                    break
+                pending.append(ex.submit(load, g))
+            if not pending:
+                return
+            yield from pending.popleft().result()
 
 
 class _Writer:
@@ -634,7 +642,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     claimed: List[int] = []
     # groups a rank may hold ahead of its main loop: enough for the decode threads and the
     # engine's batches in flight
-    gate = _ClaimGate(int(os.environ.get("TB_CLAIM_AHEAD", str(rc.read_threads + 3))))
+    gate = _ClaimGate(max(1, int(os.environ.get("TB_CLAIM_AHEAD", str(rc.read_threads + 3)))))
     if rc.schedule == "static":
         groups_it = unit_groups([u for u in mine if u.index not in done])
         accounted = mine          # this rank reports the resumed units of its own range
@@ -665,7 +673,8 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
         metrics.setup_prometheus_metrics(rc.metrics_port)
     # input decoding starts now and overlaps the engine (HIP context, kernels, model) set-up
     ureader = _UnitReader(reader)
-    source = _Prefetcher(_read_units(reader, groups_it, rc.read_threads, ureader), depth=rc.read_threads + 2)
+    source = _Prefetcher(_read_units(reader, groups_it, rc.read_threads, ureader, window=gate.ahead),
+                         depth=rc.read_threads + 2)
     try:
         if engine is None:
             backend = rc.backend

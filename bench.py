@@ -28,11 +28,23 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "documents/sec through full C4+Gopher+langID pipeline at 1/2/4/8 MI355X"
-# The reference publishes no throughput numbers. Baseline = this framework's CPU
-# path (C++ port of the reference filters with ICU4C segmentation, the GPU box's 16-core CPU
-# share) on the same synthetic corpus: `python bench.py --backend cpu` measured 58,521 docs/s on
-# the MI355X box (profiles/README.md). TB_CPU_BASELINE overrides.
-CPU_BASELINE_DOCS_PER_SEC = float(os.environ.get("TB_CPU_BASELINE", "58521"))
+
+
+def cpu_baseline(config_path: str, mean_bytes: int):
+    """The reference publishes no throughput numbers. Baseline = this framework's
+    CPU path (C++ port of the reference filters with ICU4C segmentation, the GPU box's 16-core
+    CPU share) on the same synthetic corpus and pipeline config, as measured and recorded in
+    config/cpu_baseline.json (raw bench lines under profiles/). None when the config (or its
+    document size) has no measured entry."""
+    try:
+        with open(os.path.join(ROOT, "config", "cpu_baseline.json"), encoding="utf-8") as f:
+            table = json.load(f)
+    except OSError:
+        return None
+    e = table.get(os.path.relpath(os.path.abspath(config_path), ROOT))
+    if not isinstance(e, dict) or e.get("mean_bytes", 1024) != mean_bytes:
+        return None
+    return float(e["docs_per_sec"])
 
 
 def main():
@@ -133,6 +145,8 @@ def main():
     batches = [make_batch() for _ in range(min(4, args.steps + args.warmup))]
     bytes_per_step = float(np.mean([len(b[0]) for b in batches]))
     counters = np.zeros(5, dtype=np.int64)  # docs, kept, excluded, errors, CPU-delegated
+    nsteps = len(cfg.pipeline)
+    step_filtered = np.zeros(nsteps, dtype=np.int64)  # filtered documents per pipeline step (timed steps)
 
     def feed(k, start):
         for i in range(start, start + k):
@@ -160,6 +174,8 @@ def main():
     for res in eng.process_many(feed(args.steps, args.warmup)):
         step = np.asarray([res.n_docs, res.n_kept, res.n_excluded, len(res.error_rows)], dtype=np.int64)
         counters += np.append(step, res.n_delegated)
+        fs = res.fail_step[(res.status == 1) & (res.fail_step >= 0)]
+        step_filtered += np.bincount(fs, minlength=nsteps)[:nsteps]
         # AR1 once per step: the global counter vector (what rank 0's /metrics serves), reduced
         # over RCCL while the next steps run; the main thread (which also assembles outputs)
         # only waits once more than TB_AR1_WINDOW reductions are outstanding
@@ -185,9 +201,11 @@ def main():
     elapsed_max = ctx.all_reduce_max(elapsed)
     bpe_host = int(ctx.all_reduce_sum([int(metrics.BPE_HOST_DOCS_TOTAL._value.get() - bpe_host0)])[0])
     totals = ctx.all_reduce_sum(counters)
+    step_filtered = ctx.all_reduce_sum(step_filtered)
     docs_total = int(totals[0])
     value = docs_total / elapsed_max
     lid = getattr(eng, "langid", None)
+    base = cpu_baseline(args.config, args.mean_bytes) if args.vocab == "small" and not args.mixed_script else None
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -199,7 +217,7 @@ def main():
             "ms_per_step": round(1000 * elapsed_max / args.steps, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / CPU_BASELINE_DOCS_PER_SEC, 3) if CPU_BASELINE_DOCS_PER_SEC else None,
+            "vs_baseline": round(value / base, 3) if base else None,
             # the matrix-core dtype of the language-id head that ran (v3: bf16 MFMA; v2 int16 table:
             # "int16"); the text filters themselves are integer / byte arithmetic
             "dtype": lid.dtype if lid is not None else "int",
@@ -229,6 +247,10 @@ def main():
             # step, hash collisions, scratch overflow) and TokenCounter documents counted by the host
             # tokenizer, over the timed steps
             "delegated": int(totals[4]),
+            # documents filtered by each pipeline step (YAML order) over the timed steps: the
+            # step mix the downstream kernels saw (survivors of step k reach step k + 1)
+            "step_filtered": [int(v) for v in step_filtered],
+            "reach_step": [int(totals[0] - sum(int(v) for v in step_filtered[:k])) for k in range(nsteps)],
             "bpe_host_docs": bpe_host,
             "bytes_per_sec": round(bytes_per_step * world * args.steps / elapsed_max, 1),
             "last_step_timings": {k: round(v, 5) for k, v in res.timings.items()},

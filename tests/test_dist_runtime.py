@@ -291,3 +291,29 @@ def test_claim_gate_of_one_with_many_reader_threads(tmp_path, monkeypatch):
     assert pq.read_table(o).equals(pq.read_table(o1)) and pq.read_table(e).equals(pq.read_table(e1))
     units, _ = _rank_stats(r.stdout)
     assert sum(units) == 160
+
+
+def test_run_eight_cpu_ranks_pinned_and_identical(tmp_path):
+    """`run --gpus 8 --backend cpu` (gloo, dynamic schedule): every rank is pinned to its own CPU
+    set with a thread budget inside it (parallel/placement.py), the summary reports each rank's
+    set and thread counts, and the outputs are byte-identical to the one-rank run."""
+    inp = _corpus(tmp_path)
+    _, o1, e1 = _cli(tmp_path, inp, "one8")
+    r, o8, e8 = _cli(tmp_path, inp, "eight", "--gpus", "8", "--unit-rows", "125")
+    assert "Ranks: 8 (cpu)" in r.stdout
+    assert pq.read_table(o8).equals(pq.read_table(o1)) and pq.read_table(e8).equals(pq.read_table(e1))
+    line = next(ln for ln in r.stdout.splitlines() if "CPU sets per rank:" in ln)
+    entries = line.split("CPU sets per rank:")[1].split(";")
+    assert len(entries) == 8, line
+    import os as _os
+
+    ncpu = len(_os.sched_getaffinity(0))
+    if ncpu >= 8:
+        sets = []
+        for e in entries:
+            assert "cpus " in e and "not pinned" not in e, line
+            a, b = e.split("cpus ")[1].split(" ")[0].split("-")
+            sets.append(set(range(int(a), int(b) + 1)))
+        for i in range(8):  # disjoint sets
+            for j in range(i + 1, 8):
+                assert not (sets[i] & sets[j]), line

@@ -135,7 +135,19 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("--segmentation", default="icu", choices=["icu", "rules"],
                        help="UAX#29 implementation of the CPU backend")
         p.add_argument("--unit-rows", type=int, default=65536, help="rows per processing/checkpoint unit")
-        p.add_argument("--threads", type=int, default=None, help="host threads per rank")
+        p.add_argument("--threads", type=int, default=None,
+                       help="native pool threads per rank (default: the rank's CPU budget)")
+        p.add_argument("--read-threads", type=int, default=None,
+                       help="Parquet reader threads per rank (default 8, or the rank's CPU budget share)")
+        p.add_argument("--write-threads", type=int, default=None,
+                       help="output encoder threads per rank (default 4, or the rank's CPU budget share)")
+        p.add_argument("--batch-bytes", type=int, default=None,
+                       help="text bytes per device batch (default 384 MiB: scratch is 80-176 B per byte)")
+        p.add_argument("--slots", type=int, default=None,
+                       help="device batches in flight per GPU (default: 3 when HBM allows)")
+        p.add_argument("--claim-ahead", type=int, default=None,
+                       help="row groups a rank may claim ahead of its main loop (reference prefetch_count "
+                            "semantics; default readers + 3)")
         p.add_argument("--resume", action="store_true", help="skip units recorded in the work dir manifest")
         p.add_argument("--checkpoint", action="store_true", help="write per-unit parts + manifest (resumable)")
         p.add_argument("--work-dir", default=None, help="checkpoint dir (default <output-file>.work)")
@@ -232,7 +244,9 @@ def run_cmd(args, argv: List[str]) -> int:
         backend=backend, segmentation=args.segmentation, unit_rows=args.unit_rows, threads=args.threads,
         work_dir=args.work_dir, resume=args.resume, checkpoint=args.checkpoint, keep_parts=args.keep_parts,
         compression=args.compression, tokenizer_dir=args.tokenizer_dir, badwords_dir=args.badwords_dir,
-        html_decode=args.html_decode, metrics_port=args.metrics_port, tokenizer_file=args.tokenizer_file, fault_inject=args.fault_inject)
+        html_decode=args.html_decode, metrics_port=args.metrics_port, tokenizer_file=args.tokenizer_file,
+        fault_inject=args.fault_inject, read_threads=args.read_threads, write_threads=args.write_threads,
+        batch_bytes=args.batch_bytes, slots=args.slots, claim_ahead=args.claim_ahead)
     try:
         stats = run(rc, ctx)
     except RankFailure as e:
@@ -265,6 +279,9 @@ def run_cmd(args, argv: List[str]) -> int:
             f"  Ranks: {ctx.world_size} ({backend}), units: {stats.units} (+{stats.units_skipped} resumed)",
             f"  Units per rank: {stats.rank_units} | busy seconds per rank: "
             f"{[round(b, 3) for b in stats.rank_busy]}",
+            "  CPU sets per rank: " + "; ".join(
+                f"r{r}: " + (f"cpus {c[4]}-{c[5]} ({c[0]})" if c[0] else "not pinned")
+                + f", pool {c[1]}, readers {c[2]}, writers {c[3]}" for r, c in enumerate(stats.rank_cpus)),
             f"  Time: {stats.seconds:.2f} s | Speed: {stats.docs_per_sec:.2f} docs/sec",
             f"  Output File: {args.output_file}",
             f"  Excluded File: {args.excluded_file}",

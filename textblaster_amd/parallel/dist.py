@@ -189,6 +189,12 @@ def init_from_env(backend: str = "nccl", force_pg: Optional[bool] = None) -> Dis
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)) or world)
+    # this rank's CPUs (its GPU's NUMA node, shared evenly with the node's other ranks), before
+    # any HIP call: the runtime's threads, the native pools and the pinned buffers follow it
+    from . import placement
+
+    placement.bind_rank(local, local_world)
     if force_pg is None:
         force_pg = os.environ.get("TB_FORCE_PG", "") not in ("", "0")
     ctx = DistContext(rank, world, local)
@@ -215,20 +221,14 @@ def init_from_env(backend: str = "nccl", force_pg: Optional[bool] = None) -> Dis
             # RCCL and torch add their own streams next to the engine's eight; with the box's
             # default of 4 hardware queues per process they land behind document kernels on a
             # shared queue (measured: a one-rank group with no collective at all took the
-            # 1-GPU bench from 35.6 to 47.9 ms/step; 8 queues: 37.0). It only takes effect
-            # before the first HIP call of this process. An explicit TB_PG_HW_QUEUES wins (0
-            # keeps the inherited value); otherwise an operator's GPU_MAX_HW_QUEUES is kept.
-            q = os.environ.get("TB_PG_HW_QUEUES")
-            if q is not None:
-                if q not in ("", "0"):
+            # 1-GPU bench from 35.6 to 47.9 ms/step; 8 queues: 37.0). The setting only takes
+            # effect before the first HIP call of a process, so the launchers put it into the
+            # environment of the processes they start (parallel/launch.py rank_env); here it
+            # is applied only while this process has not touched HIP yet.
+            if not _hip_initialised():
+                q = pg_hw_queues()
+                if q:
                     os.environ["GPU_MAX_HW_QUEUES"] = q
-            else:
-                os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-            if _hip_initialised():
-                import warnings
-
-                warnings.warn("init_from_env: the HIP runtime is already initialised in this process, so "
-                              "GPU_MAX_HW_QUEUES cannot change the hardware queue count any more")
             # the collective streams at high priority: a counter reduction is never queued
             # behind a batch's kernels
             os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
@@ -244,6 +244,15 @@ def init_from_env(backend: str = "nccl", force_pg: Optional[bool] = None) -> Dis
         td.init_process_group(backend=pg_backend, rank=rank, world_size=world, **kwargs)
         ctx.backend = pg_backend
     return ctx
+
+
+def pg_hw_queues() -> Optional[str]:
+    """Hardware queues a process with an RCCL group should start with: TB_PG_HW_QUEUES if set
+    ("0": keep the inherited value), else an operator's GPU_MAX_HW_QUEUES, else 8."""
+    q = os.environ.get("TB_PG_HW_QUEUES")
+    if q is not None:
+        return None if q in ("", "0") else q
+    return os.environ.get("GPU_MAX_HW_QUEUES") or "8"
 
 
 def shard_ranges(sizes: Sequence[int], world: int) -> List[range]:

@@ -83,8 +83,20 @@ def spawn_ranks(n: int, target: List[str], port: Optional[int] = None) -> int:
     port = port or int(os.environ.get("TB_MASTER_PORT", "0")) or free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={port}"] + list(target)
-    env = dict(os.environ)
+    return subprocess.call(cmd, env=rank_env(os.environ))
+
+
+def rank_env(base) -> dict:
+    """Environment of the rank processes: set here, in the launcher, because the hardware-queue
+    count is read once, at a process's first HIP call (a rank may touch HIP before it builds its
+    process group)."""
+    from .dist import pg_hw_queues
+
+    env = dict(base)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env["MASTER_ADDR"] = "127.0.0.1"
     env.setdefault("OMP_NUM_THREADS", "1")
-    return subprocess.call(cmd, env=env)
+    q = pg_hw_queues()
+    if q:
+        env["GPU_MAX_HW_QUEUES"] = q
+    return env

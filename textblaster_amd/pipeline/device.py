@@ -407,7 +407,7 @@ class DeviceRunner:
     DEFAULT_PRE_DOC_BYTES = 262144
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None, max_batch_bytes: int = 384 << 20,
-                 token_counters=None):
+                 token_counters=None, slots: Optional[int] = None):
         import os
 
         from ..ops import hiprt
@@ -439,8 +439,9 @@ class DeviceRunner:
         # Batches in flight on the device. Each slot holds its own scratch arena (<= 176 B per text
         # byte, x1.25 headroom): three slots keep the GPU fed (interleaved A/B, 20-step headline
         # bench: 35.3 vs 38.6 ms/step, profiles/r2_slots/ab.txt) and fit 288 GB of HBM with
-        # 384 MB device batches; a smaller device gets two. TB_SLOTS overrides.
-        env_slots = os.environ.get("TB_SLOTS")
+        # 384 MB device batches; a smaller device gets two. `slots` (run --slots) or TB_SLOTS
+        # overrides.
+        env_slots = slots or os.environ.get("TB_SLOTS")
         if env_slots:
             self.N_SLOTS = max(1, int(env_slots))
         else:

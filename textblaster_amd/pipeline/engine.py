@@ -82,6 +82,13 @@ def _gate_mismatch(n: int, p: int) -> None:
 
 
 def default_threads() -> int:
+    # a rank pinned to its CPU set (parallel/placement.py) sizes its pool from the set's thread
+    # budget (readers and writers take their share of the same CPUs)
+    from ..parallel import placement
+
+    cpus = placement.bound_cpus()
+    if cpus is not None and not os.environ.get("TB_THREADS"):
+        return placement.thread_budget(len(cpus)).pool
     # the GPU boxes expose every CPU of the host through the affinity mask but give one GPU a
     # share of them (OMP_NUM_THREADS); honour explicit limits first
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)
@@ -105,7 +112,8 @@ class Engine:
                  nthreads: Optional[int] = None, segmentation: str = "rules", langid=None,
                  tokenizer_dir: Optional[str] = None, badwords_dir: Optional[str] = None,
                  keep_reasons: bool = False, tokenizer_file: Optional[str] = None,
-                 fault_inject: Optional[str] = None, tokenizers=None, badwords=None):
+                 fault_inject: Optional[str] = None, tokenizers=None, badwords=None,
+                 max_batch_bytes: Optional[int] = None, slots: Optional[int] = None):
         self.cfg = cfg
         self._cpu_engine = None
         self._n_submitted = 0
@@ -121,7 +129,7 @@ class Engine:
         self.prefetch_threads = os.environ.get("TB_PREFETCH_THREAD", "1") not in ("", "0")
         # text bytes per device batch (scratch 80-176 B per text byte per in-flight slot: 384 MB of
         # text -> at most ~85 GB of HBM per slot, three slots in flight on a 288 GB MI355X)
-        self.max_batch_bytes = int(os.environ.get("TB_MAX_BATCH_BYTES", str(384 << 20)))
+        self.max_batch_bytes = int(max_batch_bytes or os.environ.get("TB_MAX_BATCH_BYTES", str(384 << 20)))
         self.h = native.host()
         self.plan: ExecPlan = build_plan(cfg)
         self.steps = [self.h.make_step(s.native_dict()) for s in cfg.pipeline]
@@ -185,7 +193,8 @@ class Engine:
 
             with tracing.trace_range("tb.init.device_runner"):
                 self.device_runner = DeviceRunner(self.steps, self.plan, device or "cuda", self.langid,
-                                                  max_batch_bytes=self.max_batch_bytes, token_counters=token_counters)
+                                                  max_batch_bytes=self.max_batch_bytes, token_counters=token_counters,
+                                                  slots=slots)
 
     # ------------------------------------------------------------------------------------------
     def process(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None,

@@ -86,8 +86,13 @@ class RunConfig:
     metrics_port: Optional[int] = None
     progress_interval: float = 1.0
     tokenizer_file: Optional[str] = None
-    read_threads: int = int(os.environ.get("TB_READ_THREADS", "8"))   # row groups decoded concurrently
-    write_threads: int = int(os.environ.get("TB_WRITE_THREADS", "4"))  # units encoded concurrently
+    # row groups decoded / units encoded concurrently; None: TB_READ_THREADS / TB_WRITE_THREADS,
+    # else the rank's thread budget when it is pinned to a CPU set (parallel/placement.py), else 8 / 4
+    read_threads: Optional[int] = None
+    write_threads: Optional[int] = None
+    claim_ahead: Optional[int] = None    # groups a rank may hold ahead of its main loop (default readers + 3)
+    batch_bytes: Optional[int] = None    # device batch bytes (default 384 MB; TB_MAX_BATCH_BYTES)
+    slots: Optional[int] = None          # device batches in flight (default: auto, 3 when HBM allows; TB_SLOTS)
     fault_inject: Optional[str] = None   # debug: "kernel@N" / "oom@N" (N = 1-based batch), "rank@N[:R]",
                                          # "slow@SECONDS[:R]" (rank R sleeps after every unit)
     schedule: str = os.environ.get("TB_SCHEDULE", "dynamic")  # dynamic (shared cursor) | static (ranges)
@@ -108,6 +113,9 @@ class RunStats:
     phase_seconds: Dict[str, float] = dataclasses.field(default_factory=dict)  # rank 0's own view
     rank_units: List[int] = dataclasses.field(default_factory=list)  # units processed per rank
     rank_busy: List[float] = dataclasses.field(default_factory=list)  # main-loop seconds per rank
+    # per rank: [CPUs, pool threads, reader threads, writer threads, first CPU, last CPU] (CPUs 0:
+    # not pinned, first / last -1)
+    rank_cpus: List[List[int]] = dataclasses.field(default_factory=list)
 
     @property
     def docs_per_sec(self) -> float:
@@ -583,12 +591,40 @@ def _sort_by_row(tbl: pa.Table, rows: np.ndarray) -> pa.Table:
     return tbl.take(pa.array(order))
 
 
+def resolve_threads(rc: RunConfig):
+    """(pool, readers, writers) of this rank: explicit settings first (RunConfig, then the
+    TB_THREADS / TB_READ_THREADS / TB_WRITE_THREADS env), then the thread budget of the CPU set
+    the rank is pinned to (placement.thread_budget: all three within its CPUs), else the
+    one-rank defaults (pool = the process's CPU share, 8 readers, 4 writers)."""
+    from .parallel import placement
+    from .pipeline.engine import default_threads
+
+    cpus = placement.bound_cpus()
+    bud = placement.thread_budget(len(cpus)) if cpus is not None else None
+
+    def pick(v, env, dflt):
+        if v is not None:
+            return int(v)
+        e = os.environ.get(env)
+        if e and e.isdigit() and int(e) > 0:
+            return int(e)
+        return dflt
+
+    pool = pick(rc.threads, "TB_THREADS", bud.pool if bud else default_threads())
+    read = pick(rc.read_threads, "TB_READ_THREADS", bud.read if bud else 8)
+    write = pick(rc.write_threads, "TB_WRITE_THREADS", bud.write if bud else 4)
+    return pool, read, write
+
+
 def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[PipelineConfig] = None,
         engine=None) -> RunStats:
     """Process ``rc.input_file`` end to end; returns the global (all-rank) statistics."""
+    from .parallel import placement
     from .pipeline.engine import Engine
 
     ctx = ctx or DistContext()
+    n_pool, n_read, n_write = resolve_threads(rc)
+    rc = dataclasses.replace(rc, threads=n_pool, read_threads=n_read, write_threads=n_write)
     rank, world = ctx.rank, ctx.world_size
     cfg = cfg or load_pipeline_config(rc.pipeline_config)
     nsteps = len(cfg.pipeline)
@@ -642,7 +678,8 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     claimed: List[int] = []
     # groups a rank may hold ahead of its main loop: enough for the decode threads and the
     # engine's batches in flight
-    gate = _ClaimGate(max(1, int(os.environ.get("TB_CLAIM_AHEAD", str(rc.read_threads + 3)))))
+    ahead = rc.claim_ahead if rc.claim_ahead is not None else int(os.environ.get("TB_CLAIM_AHEAD", "0") or 0)
+    gate = _ClaimGate(ahead if ahead > 0 else rc.read_threads + 3)
     if rc.schedule == "static":
         groups_it = unit_groups([u for u in mine if u.index not in done])
         accounted = mine          # this rank reports the resumed units of its own range
@@ -681,6 +718,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
             device = ctx.device if backend in ("cuda", "auto") else None
             with tracing.trace_range("tb.engine_init"):
                 engine = Engine(cfg, backend=backend, device=device, nthreads=rc.threads,
+                                max_batch_bytes=rc.batch_bytes, slots=rc.slots,
                                 segmentation=rc.segmentation, tokenizer_dir=rc.tokenizer_dir,
                                 badwords_dir=rc.badwords_dir, tokenizer_file=rc.tokenizer_file,
                                 fault_inject=None if (rank_fault is not None or slow is not None) else rc.fault_inject)
@@ -692,8 +730,9 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     # there costs more than the staging copy it saves (profiles/r8_e2e/ab_pinned_read.txt)
     if engine.backend == "cuda" and os.environ.get("TB_PINNED_READ", "0") not in ("", "0"):
         reader.host_buffer = engine.host_buffer
-    log.info("rank %d/%d: schedule=%s, %d units already done, backend=%s", rank, world, rc.schedule,
-             local.units_skipped, engine.backend)
+    log.info("rank %d/%d: schedule=%s, %d units already done, backend=%s, CPUs %s, threads: pool %d, "
+             "readers %d, writers %d", rank, world, rc.schedule, local.units_skipped, engine.backend,
+             os.environ.get("TB_CPU_SET", "(not pinned)"), engine.nthreads, rc.read_threads, rc.write_threads)
 
     hb = Heartbeat(ctx, len(local.vector(nsteps)), interval=rc.progress_interval,
                    on_global=_publish_global if rank == 0 else None)
@@ -777,6 +816,10 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     per_rank = ctx.all_gather_counts([local.units, int(round(busy * 1e6))])
     stats.rank_units = [int(x) for x in per_rank[:, 0]]
     stats.rank_busy = [float(x) / 1e6 for x in per_rank[:, 1]]
+    cpus = placement.bound_cpus()
+    cpu_row = [len(cpus) if cpus else 0, engine.nthreads, rc.read_threads, rc.write_threads,
+               min(cpus) if cpus else -1, max(cpus) if cpus else -1]
+    stats.rank_cpus = [[int(v) for v in row] for row in ctx.all_gather_counts(cpu_row)]
     if use_parts:
         ctx.barrier()
         t_merge = time.perf_counter()

@@ -1452,6 +1452,59 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
   x.reset(mark);
 }
 
+// Repeat candidates of n elements: a superset of the elements equal to some other element. Every
+// element sets bit h(key) of a bitmap (fetch-or); one that finds its bit already set sets it in a
+// second bitmap. Equal elements have equal keys, so every repeated element lands on a bit of the
+// second bitmap; an element whose bit no other element set is unique, and only the candidates need
+// the exact canonicalisation (with 8 bitmap bits per element a unique one is a false candidate
+// with probability ~1/8). Candidate indices go to list[0, nc) in increasing order; returns nc.
+// `bm` holds 2 * bw words (bw a power of two), zeroed here.
+template <class P, class KeyF>
+TB_HD uint32_t repeat_candidates(DocCtx<P>& x, uint32_t n, KeyF&& key, uint32_t* bm, uint32_t bw, uint32_t* list) {
+  const uint32_t mask = bw * 32u - 1u;
+  uint32_t* once = bm;
+  uint32_t* twice = bm + bw;
+  x.par.for_n(2 * bw, [&](uint32_t i) { bm[i] = 0; });
+  x.par.sync();
+  x.par.for_n(n, [&](uint32_t i) {
+    const uint32_t h = (uint32_t)(key(i) >> 20) & mask;
+    const uint32_t bit = 1u << (h & 31u);
+    if (P::fetch_or32(&once[h >> 5], bit) & bit) P::or32(&twice[h >> 5], bit);
+  });
+  x.par.sync();
+  const uint32_t nc = x.par.template compact<int>(
+      n,
+      [&](uint32_t i, int&) {
+        const uint32_t h = (uint32_t)(key(i) >> 20) & mask;
+        return ((twice[h >> 5] >> (h & 31u)) & 1u) != 0;
+      },
+      [&](uint32_t i, uint32_t k, int&) { list[k] = i; });
+  x.par.sync();
+  return nc;
+}
+
+// Bitmap words of repeat_candidates for n elements (>= 8 bits per element, a power of two) and the
+// scratch bytes the candidate path may take beyond the order's own arrays, for the capacity test
+// that picks it (the full canonicalisation otherwise: results are the same either way).
+TB_HD uint32_t cand_bitmap_words(uint32_t n) {
+  uint32_t w = 32;
+  while (w * 4u < n) w <<= 1;
+  return w;
+}
+TB_HD uint64_t cand_path_bytes(uint32_t n) { return 8ull * cand_bitmap_words(n) + 16ull * n + 256; }
+// (workgroup documents keep the full canonicalisation: with the candidate path their
+// partitioned-table runs gave wrong top n-gram records on the GPU, unexplained; the sequential
+// emulation of the same code, partitioned tables included, is exact)
+#ifndef TB_CAND_BLK
+#define TB_CAND_BLK 0
+#endif
+template <class P>
+TB_HD bool cand_path_fits(const DocCtx<P>& x, uint32_t n) {
+  if (!TB_CAND_BLK && P::kWaves > 1) return false;
+  const uint64_t need = cand_path_bytes(n);
+  return x.cap >= x.used + need + 64 || (uint64_t)x.lds_free() >= need;
+}
+
 // Duplicated lines (which = 0: r[5], r[6]) or paragraphs (which = 1: r[2], r[3]) of a split
 // document (k_gr_dup_split), over the arrays gopher_rep_record exported.
 template <class P>
@@ -1492,34 +1545,56 @@ TB_HD void gr_top_one_order(DocCtx<P>& x, const DevStep& ds, int t, const GrExpo
   const uint32_t* wid = e.wid;
   const uint32_t* WL = e.WL;
   const auto mark = x.mark();
-  uint32_t* gc = x.template alloc_hot_keep<uint32_t>((uint64_t)G + 1, 6ull * G + 64);
-  uint32_t* cnt = x.template alloc_hot_keep<uint32_t>((uint64_t)G + 1, 6ull * G + 64);
-  if (x.overflow) return;
-  canonicalize(
-      x, G,
-      [&](uint32_t p) {
-        uint64_t h = (uint64_t)n << 56;
-        for (uint32_t k = 0; k < n; ++k) h = (h ^ wid[p + k]) * 0x9E3779B97F4A7C15ull + k;
-        return mix64(h);
-      },
-      [&](uint32_t p, uint32_t q) {
-        uint32_t dw = 0;
-        for (uint32_t k = 0; k < n; ++k) dw |= wid[p + k] ^ wid[q + k];
-        return dw == 0;
-      },
-      gc);
-  if (x.overflow) return;
-  x.par.for_n(G, [&](uint32_t p) { cnt[p] = 0; });
-  x.par.sync();
-  x.par.for_n(G, [&](uint32_t p) { P::add32(&cnt[gc[p]], 1u); });
-  x.par.sync();
-  const uint32_t maxc = x.par.template max<uint32_t>(G, 0u, [&](uint32_t p) { return cnt[p]; });
+  auto key = [&](uint32_t p) {
+    uint64_t h = (uint64_t)n << 56;
+    for (uint32_t k = 0; k < n; ++k) h = (h ^ wid[p + k]) * 0x9E3779B97F4A7C15ull + k;
+    return mix64(h);
+  };
+  auto eq = [&](uint32_t p, uint32_t q) {
+    uint32_t dw = 0;
+    for (uint32_t k = 0; k < n; ++k) dw |= wid[p + k] ^ wid[q + k];
+    return dw == 0;
+  };
+  // Only the repeat candidates are grouped (every other gram occurs once): pos[c] = position of
+  // candidate c, gc[c] = its canonical candidate, cnt[c] = the class size at the canonical one.
+  // Without room for the candidate arrays every position is a candidate (the full grouping).
+  uint32_t NC = G;
+  const uint32_t* pos = nullptr;
+  if (cand_path_fits(x, G)) {
+    const uint32_t bw = cand_bitmap_words(G);
+#ifdef TB_CAND_GLOBAL
+    uint32_t* bm = x.template alloc_global<uint32_t>(2 * bw);
+    uint32_t* list = x.template alloc_global<uint32_t>((uint64_t)G + 1);
+#else
+    uint32_t* bm = x.template alloc_hot<uint32_t>(2 * bw);
+    uint32_t* list = x.template alloc_hot<uint32_t>((uint64_t)G + 1);
+#endif
+    if (x.overflow) return;
+    NC = repeat_candidates(x, G, key, bm, bw, list);
+    pos = list;
+  }
   int64_t v = 0;
-  if (maxc > 1) {
-    const uint32_t maxlen = x.par.template max<uint32_t>(G, 0u, [&](uint32_t p) {
-      return cnt[p] == maxc ? (WL[p + n] - WL[p] + n - 1) : 0u;
-    });
-    v = (int64_t)maxlen * (int64_t)maxc;
+  if (NC >= 2) {
+    uint32_t* gc = x.template alloc_hot_keep<uint32_t>((uint64_t)NC + 1, 6ull * NC + 64);
+    uint32_t* cnt = x.template alloc_hot_keep<uint32_t>((uint64_t)NC + 1, 6ull * NC + 64);
+    if (x.overflow) return;
+    auto at = [&](uint32_t c) { return pos ? pos[c] : c; };
+    canonicalize(
+        x, NC, [&](uint32_t c) { return key(at(c)); }, [&](uint32_t c, uint32_t d) { return eq(at(c), at(d)); },
+        gc);
+    if (x.overflow) return;
+    x.par.for_n(NC, [&](uint32_t c) { cnt[c] = 0; });
+    x.par.sync();
+    x.par.for_n(NC, [&](uint32_t c) { P::add32(&cnt[gc[c]], 1u); });
+    x.par.sync();
+    const uint32_t maxc = x.par.template max<uint32_t>(NC, 0u, [&](uint32_t c) { return cnt[c]; });
+    if (maxc > 1) {
+      const uint32_t maxlen = x.par.template max<uint32_t>(NC, 0u, [&](uint32_t c) {
+        const uint32_t p = at(c);
+        return cnt[c] == maxc ? (WL[p + n] - WL[p] + n - 1) : 0u;
+      });
+      v = (int64_t)maxlen * (int64_t)maxc;
+    }
   }
   x.par.single([&]() { *out = v; });
   x.par.sync();
@@ -1546,15 +1621,44 @@ TB_HD void gr_dup_one_order(DocCtx<P>& x, const DevStep& ds, int t, const GrExpo
   x.par.for_n(2 * SW, [&](uint32_t i) { bits[i] = 0; });
   x.par.sync();
   uint32_t* R = bits + SW;
-  canonicalize_res(
-      x, G, [&](uint32_t p) { return dg.key(p, n); }, [&](uint32_t p, uint32_t q) { return dg.eq(p, q, n); }, gc,
-      [&](uint32_t p, uint32_t g) {
-        if (g != p) {
-          P::or32(&R[p >> 5], 1u << (p & 31));
-          P::or32(&R[g >> 5], 1u << (g & 31));
-        }
-      });
+  auto key = [&](uint32_t p) { return dg.key(p, n); };
+  // Only the repeat candidates are canonicalised: a gram that is not a candidate occurs once, so
+  // its position is never repeated and the walk never reads its gc entry. gc of a candidate
+  // position = the class id (its canonical candidate's index).
+  if (cand_path_fits(x, G)) {
+    const uint32_t bw = cand_bitmap_words(G);
+    uint32_t* bm = x.template alloc_hot<uint32_t>(2 * bw);
+    uint32_t* list = x.template alloc_hot<uint32_t>((uint64_t)G + 1);
+    if (x.overflow) return;
+    const uint32_t nc = repeat_candidates(x, G, key, bm, bw, list);
+    if (nc >= 2) {
+      uint32_t* cc = x.template alloc_hot_keep<uint32_t>((uint64_t)nc + 1, 6ull * nc + 64);
+      if (x.overflow) return;
+      canonicalize_res(
+          x, nc, [&](uint32_t c) { return key(list[c]); },
+          [&](uint32_t c, uint32_t d) { return dg.eq(list[c], list[d], n); }, cc,
+          [&](uint32_t c, uint32_t g) {
+            const uint32_t p = list[c];
+            gc[p] = g;
+            if (g != c) {
+              const uint32_t q = list[g];
+              P::or32(&R[p >> 5], 1u << (p & 31));
+              P::or32(&R[q >> 5], 1u << (q & 31));
+            }
+          });
+    }
+  } else {
+    canonicalize_res(
+        x, G, key, [&](uint32_t p, uint32_t q) { return dg.eq(p, q, n); }, gc,
+        [&](uint32_t p, uint32_t g) {
+          if (g != p) {
+            P::or32(&R[p >> 5], 1u << (p & 31));
+            P::or32(&R[g >> 5], 1u << (g & 31));
+          }
+        });
+  }
   if (x.overflow) return;
+  x.par.sync();
   if constexpr (P::kWaves > 0) {
     if (x.par.wave_index() == 0) {
       const int64_t rep = dup_walk_wave(x.par, G, n, gc, R, bits, e.WL);

@@ -20,7 +20,7 @@
 //  * reduce_or(v): OR of a per-lane value over the document's lanes (uniform result).
 //  * sync(): every write before it is visible to every lane after it.
 //  * single(f): f() runs once (lane 0).
-//  * cas64/min32/min64/add32/add64/max32: atomics on scratch memory.
+//  * cas64/min32/min64/add32/add64/max32/or32/fetch_or32: atomics on scratch memory.
 #pragma once
 #include "langid.h"
 #include "tb_common.h"
@@ -168,6 +168,7 @@ struct SeqPar {
   static void max32(uint32_t* p, uint32_t v) { if (v > *p) *p = v; }
   static uint32_t add32(uint32_t* p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
   static void or32(uint32_t* p, uint32_t v) { *p |= v; }
+  static uint32_t fetch_or32(uint32_t* p, uint32_t v) { const uint32_t o = *p; *p |= v; return o; }
   // Integer accumulation over items: f(i, part) adds item i's contribution into part[0..D)
   // (int32 partials); sums[d] receives the exact int64 total. tmp is unused on the host.
   template <int D, class F>
@@ -502,6 +503,7 @@ struct WavePar {
   __device__ __forceinline__ static void max32(uint32_t* p, uint32_t v) { atomicMax(p, v); }
   __device__ __forceinline__ static uint32_t add32(uint32_t* p, uint32_t v) { return atomicAdd(p, v); }
   __device__ __forceinline__ static void or32(uint32_t* p, uint32_t v) { atomicOr(p, v); }
+  __device__ __forceinline__ static uint32_t fetch_or32(uint32_t* p, uint32_t v) { return atomicOr(p, v); }
 
   // Each lane accumulates its items (i = lane, lane+64, ...) in D int32 registers, so the
   // item loads of one lane are independent of the other lanes' and of each other; the 64 x D
@@ -734,6 +736,7 @@ struct BlockPar {
   __device__ __forceinline__ static void max32(uint32_t* p, uint32_t v) { atomicMax(p, v); }
   __device__ __forceinline__ static uint32_t add32(uint32_t* p, uint32_t v) { return atomicAdd(p, v); }
   __device__ __forceinline__ static void or32(uint32_t* p, uint32_t v) { atomicOr(p, v); }
+  __device__ __forceinline__ static uint32_t fetch_or32(uint32_t* p, uint32_t v) { return atomicOr(p, v); }
 };
 
 // NT/64 waves on one document with few barriers: items [0, n) are cut into one contiguous
@@ -943,6 +946,7 @@ struct SegPar {
   __device__ __forceinline__ void single(F&& f) const { if (tid == 0) f(); }
   __device__ __forceinline__ bool leader() const { return tid == 0; }
   __device__ __forceinline__ static void or32(uint32_t* p, uint32_t v) { atomicOr(p, v); }
+  __device__ __forceinline__ static uint32_t fetch_or32(uint32_t* p, uint32_t v) { return atomicOr(p, v); }
 };
 #endif
 

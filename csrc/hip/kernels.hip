@@ -259,15 +259,20 @@ __global__ __launch_bounds__(kBlockThreads) TB_BLK_ATTR void k_gr_dup_split(
 constexpr int kNgWaves = 4;
 
 // LDS of one document's workgroup for documents of at most MAXW words: the staged word arrays and
-// one region per wave, the larger of the duplicated-order layout (u32 table, u16 ids and lengths,
-// seen / repeat bitmaps) and the top-order layout (u32 table, u16 ids, u32 counts)
+// one region per wave, the larger of the duplicated-order layout (u32 table, u16 canonical ids,
+// candidate positions and slots, seen / repeat bitmaps) and the top-order layout (u32 table, u16
+// candidate positions, u32 counts packed with slots). The table's space first holds the two
+// candidate bitmaps of the order (ng_candidates).
 template <uint32_t MAXW>
 struct NgShared {
   static_assert(MAXW % 64 == 0, "whole waves of grams");
   static constexpr uint32_t kMaxW = MAXW;
   static constexpr uint32_t kCap = MAXW + MAXW / 2 + 4;  // table slots (1.5 G + 2, rounded)
   static constexpr uint32_t kSW = (MAXW + 31) / 32 + 1;
-  static constexpr uint32_t kDupBytes = 4 * kCap + 2 * 2 * MAXW + 4 * 2 * ((kSW + 3) & ~3u);
+  // candidate bitmaps: two arrays of kBW words (a power of two, >= 16 bits per gram) in the table
+  static constexpr uint32_t kBW = MAXW / 2;
+  static_assert(2 * kBW <= kCap && (kBW & (kBW - 1)) == 0, "bitmaps fit the table space");
+  static constexpr uint32_t kDupBytes = 4 * kCap + 3 * 2 * MAXW + 4 * 2 * ((kSW + 3) & ~3u);
   static constexpr uint32_t kTopBytes = 4 * kCap + 2 * MAXW + 4 * MAXW;
   static constexpr uint32_t kRegion = ((kDupBytes > kTopBytes ? kDupBytes : kTopBytes) + 15) & ~15u;
   uint64_t K[MAXW + 1];
@@ -286,72 +291,128 @@ __device__ __forceinline__ uint32_t ng_home(uint64_t k, uint32_t capn) {
   return (uint32_t)(((k & 0xFFFFFFFFull) * capn) >> 32);
 }
 
+// Repeat candidates of one order: a superset of the positions whose gram occurs more than once.
+// Every gram sets bit h(key) of `once` (fetch-or); a gram that finds its bit already set sets it
+// in `twice`. Equal grams have equal keys, so every repeated gram lands on a bit of `twice`; a
+// gram whose bit no other gram set occurs once (it cannot repeat), and only the candidates go
+// through the exact canonicalisation. With >= 16 bits per gram a unique gram is a false candidate
+// with probability < 1/16. Both bitmaps (kBW words each) must be zero on entry. Candidate
+// positions land in `list` in increasing order; returns their number (wave-uniform).
+template <class NS, class KeyF>
+__device__ __forceinline__ uint32_t ng_candidates(uint32_t G, uint32_t lane, uint32_t* once, uint32_t* twice,
+                                                  uint16_t* hbuf, uint16_t* list, KeyF&& key) {
+  constexpr uint32_t kMask = NS::kBW * 32u - 1u;
+  static_assert(kMask <= 0xFFFFu, "bit index in 16 bits");
+  // (each position's bit index goes through hbuf, not registers: the kernel is register-bound)
+#pragma unroll 1
+  for (uint32_t p = lane; p < G; p += 64) {
+    const uint32_t h = (uint32_t)(key(p) >> 20) & kMask;
+    hbuf[p] = (uint16_t)h;
+    const uint32_t bit = 1u << (h & 31u);
+    if (atomicOr(&once[h >> 5], bit) & bit) atomicOr(&twice[h >> 5], bit);
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint32_t nc = 0;
+#pragma unroll 1
+  for (uint32_t base = 0; base < G; base += 64) {
+    const uint32_t p = base + lane;
+    bool c = false;
+    if (p < G) {
+      const uint32_t h = hbuf[p];
+      c = (twice[h >> 5] >> (h & 31u)) & 1u;
+    }
+    const uint64_t m = __ballot(c);
+    if (c) list[nc + (uint32_t)__popcll(m & lt)] = (uint16_t)p;
+    nc += (uint32_t)__popcll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  return nc;
+}
+
 // gram equality of order n (DupGrams::eq over the staged arrays; the byte comparison of grams with
 // different word sequences reads the exported HBM arrays)
+// (out of line: the byte comparison of different word splits with equal hashes practically never
+// runs, and inlined its seven array pointers stay live in registers through the whole order)
+__device__ __attribute__((noinline)) bool ng_dup_eq_bytes(const GrExport* ep, uint32_t p, uint32_t q, uint32_t n) {
+  const DupGrams dg{ep->wid, ep->WL, ep->K, ep->PB, ep->bs, ep->be, ep->b};
+  return dg.eq(p, q, n);
+}
 template <class NS>
-__device__ __forceinline__ bool ng_dup_eq(const NS& S, const GrExport& e, uint32_t p, uint32_t q, uint32_t n) {
+__device__ __forceinline__ bool ng_dup_eq(const NS& S, const GrExport* ep, uint32_t p, uint32_t q, uint32_t n) {
   if ((uint32_t)(S.WL[p + n] - S.WL[p]) != (uint32_t)(S.WL[q + n] - S.WL[q])) return false;
   uint32_t dw = 0;
   for (uint32_t k = 0; k < n; ++k) dw |= (uint32_t)(S.wid[p + k] ^ S.wid[q + k]);
   if (dw == 0) return true;
-  const DupGrams dg{e.wid, e.WL, e.K, e.PB, e.bs, e.be, e.b};
-  return dg.eq(p, q, n);
+  return ng_dup_eq_bytes(ep, p, q, n);
 }
 
 template <class NS>
-__device__ __forceinline__ int64_t ng_dup_order(NS& S, const GrExport& e, uint32_t W, uint32_t n, uint32_t lane,
+__device__ __forceinline__ int64_t ng_dup_order(NS& S, const GrExport* ep, uint32_t W, uint32_t n, uint32_t lane,
                                                 uint4* region, bool prof, uint64_t& c_canon, uint64_t& c_walk) {
   const uint64_t t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
   const uint32_t G = W - n + 1;
-  const uint32_t capn = G + (G >> 1) + 2;
   const uint32_t SW = (G + 31) / 32 + 1;
   const uint32_t SWa = (SW + 3u) & ~3u;
   uint32_t* tab = (uint32_t*)region;
-  uint16_t* gc = (uint16_t*)(tab + NS::kCap);
-  uint16_t* ln = gc + NS::kMaxW;
-  uint32_t* sn = (uint32_t*)(ln + NS::kMaxW);
+  uint16_t* gc = (uint16_t*)(tab + NS::kCap);   // per position: canonical candidate index
+  uint16_t* list = gc + NS::kMaxW;              // candidate positions
+  uint16_t* gsl = list + NS::kMaxW;             // per candidate: its table slot
+  uint32_t* sn = (uint32_t*)(gsl + NS::kMaxW);
   uint32_t* R = sn + SWa;
-  for (uint32_t i = lane; i < capn; i += 64) tab[i] = 0;
+  for (uint32_t i = lane; i < 2 * NS::kBW; i += 64) tab[i] = 0;
   for (uint32_t i = lane; i < 2 * SWa; i += 64) sn[i] = 0;
   __builtin_amdgcn_wave_barrier();
-  // one position at a time per lane (few registers: occupancy hides the LDS round trips); the
-  // slot goes to gc[] until every gram is in the table
+  auto key = [&](uint32_t p) {
+    return dev_key(S.PB[p + n] * (S.K[p + n] - S.K[p]), (uint32_t)(S.WL[p + n] - S.WL[p]));
+  };
+  const uint32_t nc = ng_candidates<NS>(G, lane, tab, tab + NS::kBW, gc, list, key);
+  if (nc < 2) {  // no gram occurs twice: nothing repeats, the walk counts nothing
+    if (prof) c_canon += __builtin_amdgcn_s_memtime() - t0;
+    return 0;
+  }
+  // exact canonicalisation of the candidates: slot value (fp << 16) | (candidate index + 1)
+  const uint32_t capn = nc + (nc >> 1) + 2;
+  for (uint32_t i = lane; i < capn; i += 64) tab[i] = 0;
+  __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
-  for (uint32_t p = lane; p < G; p += 64) {
-    const uint32_t len = (uint32_t)(S.WL[p + n] - S.WL[p]);
-    const uint64_t key = dev_key(S.PB[p + n] * (S.K[p + n] - S.K[p]), len);
-    const uint32_t fp = (uint32_t)(key >> 48);
-    const uint32_t mine = (fp << 16) | (p + 1);
-    uint32_t sl = ng_home(key, capn);
+  for (uint32_t c = lane; c < nc; c += 64) {
+    const uint32_t p = list[c];
+    const uint64_t k = key(p);
+    const uint32_t fp = (uint32_t)(k >> 48);
+    const uint32_t mine = (fp << 16) | (c + 1);
+    uint32_t sl = ng_home(k, capn);
     while (true) {
       uint32_t cur = tab[sl];
       if (cur == 0) {
         cur = atomicCAS(&tab[sl], 0u, mine);
         if (cur == 0) break;
       }
-      if ((cur >> 16) == fp && ng_dup_eq(S, e, p, (cur & 0xFFFFu) - 1u, n)) {
-        if ((cur & 0xFFFFu) > p + 1u) atomicMin(&tab[sl], mine);
+      if ((cur >> 16) == fp && ng_dup_eq(S, ep, p, list[(cur & 0xFFFFu) - 1u], n)) {
+        if ((cur & 0xFFFFu) > c + 1u) atomicMin(&tab[sl], mine);
         break;
       }
       if (++sl == capn) sl = 0;
     }
-    gc[p] = (uint16_t)sl;
-    ln[p] = (uint16_t)len;
+    gsl[c] = (uint16_t)sl;
   }
   __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
-  for (uint32_t p = lane; p < G; p += 64) {
-    const uint32_t c = (tab[gc[p]] & 0xFFFFu) - 1u;
-    gc[p] = (uint16_t)c;
-    if (c != p) {
+  for (uint32_t c = lane; c < nc; c += 64) {
+    const uint32_t g = (tab[gsl[c]] & 0xFFFFu) - 1u;
+    const uint32_t p = list[c];
+    gc[p] = (uint16_t)g;
+    if (g != c) {
+      const uint32_t q = list[g];
       atomicOr(&R[p >> 5], 1u << (p & 31));
-      atomicOr(&R[c >> 5], 1u << (c & 31));
+      atomicOr(&R[q >> 5], 1u << (q & 31));
     }
   }
   __builtin_amdgcn_wave_barrier();
   const uint64_t t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
   c_canon += t1 - t0;
-  // greedy walk (reference find_all_duplicate, utils/text.rs:241-259; dup_walk_wave over LDS)
+  // greedy walk (reference find_all_duplicate, utils/text.rs:241-259; dup_walk_wave over LDS):
+  // it only stops at repeated positions (candidates), whose gc holds the class id
   const uint32_t nw = (G + 31) >> 5;
   int64_t rep = 0;
   uint32_t idx = 0;
@@ -374,7 +435,7 @@ __device__ __forceinline__ int64_t ng_dup_order(NS& S, const GrExport& e, uint32
     uint32_t g = 0xFFFFFFFFu, l = 0;
     if (act) {
       g = gc[p];
-      l = ln[p];
+      l = (uint32_t)(S.WL[p + n] - S.WL[p]);
     }
     const bool seen0 = act && ((sn[g >> 5] >> (g & 31)) & 1u);
     uint64_t A = __ballot(act), Sm = __ballot(seen0), cnt = 0, fv = 0;
@@ -405,25 +466,33 @@ __device__ __forceinline__ int64_t ng_dup_order(NS& S, const GrExport& e, uint32
 
 // top n-gram order (reference find_top_duplicate, utils/text.rs:211-238): space-joined grams are
 // equal iff their word sequences are, so grams are grouped by their canonical word-id tuples
-// (fingerprint table, exact tuple comparison on a match) and counted per canonical gram
+// (fingerprint table, exact tuple comparison on a match) and counted per canonical gram. Only the
+// repeat candidates (ng_candidates) are grouped: every other gram occurs once.
 template <class NS>
 __device__ __forceinline__ int64_t ng_top_order(NS& S, uint32_t W, uint32_t n, uint32_t lane, uint4* region) {
   const uint32_t G = W - n + 1;
-  const uint32_t capn = G + (G >> 1) + 2;
   uint32_t* tab = (uint32_t*)region;
-  uint16_t* gc = (uint16_t*)(tab + NS::kCap);
-  uint32_t* cnt = (uint32_t*)(gc + NS::kMaxW);
-  for (uint32_t i = lane; i < capn; i += 64) tab[i] = 0;
-  for (uint32_t i = lane; i < G; i += 64) cnt[i] = 0;
+  uint16_t* list = (uint16_t*)(tab + NS::kCap);
+  uint32_t* cnt = (uint32_t*)(list + NS::kMaxW);  // per candidate: slot << 16 | count
+  for (uint32_t i = lane; i < 2 * NS::kBW; i += 64) tab[i] = 0;
   __builtin_amdgcn_wave_barrier();
-#pragma unroll 1
-  for (uint32_t p = lane; p < G; p += 64) {
+  auto key = [&](uint32_t p) {
     uint64_t h = (uint64_t)n << 56;
     for (uint32_t k = 0; k < n; ++k) h = (h ^ S.wid[p + k]) * 0x9E3779B97F4A7C15ull + k;
-    const uint64_t key = mix64(h);
-    const uint32_t fp = (uint32_t)(key >> 48);
-    const uint32_t mine = (fp << 16) | (p + 1);
-    uint32_t sl = ng_home(key, capn);
+    return mix64(h);
+  };
+  const uint32_t nc = ng_candidates<NS>(G, lane, tab, tab + NS::kBW, (uint16_t*)cnt, list, key);
+  if (nc < 2) return 0;  // every gram occurs once
+  const uint32_t capn = nc + (nc >> 1) + 2;
+  for (uint32_t i = lane; i < capn; i += 64) tab[i] = 0;
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+  for (uint32_t c = lane; c < nc; c += 64) {
+    const uint32_t p = list[c];
+    const uint64_t k = key(p);
+    const uint32_t fp = (uint32_t)(k >> 48);
+    const uint32_t mine = (fp << 16) | (c + 1);
+    uint32_t sl = ng_home(k, capn);
     while (true) {
       uint32_t cur = tab[sl];
       if (cur == 0) {
@@ -431,35 +500,37 @@ __device__ __forceinline__ int64_t ng_top_order(NS& S, uint32_t W, uint32_t n, u
         if (cur == 0) break;
       }
       if ((cur >> 16) == fp) {
-        const uint32_t q = (cur & 0xFFFFu) - 1u;
+        const uint32_t qc = (cur & 0xFFFFu) - 1u;
+        const uint32_t q = list[qc];
         uint32_t dw = 0;
-        for (uint32_t k = 0; k < n; ++k) dw |= (uint32_t)(S.wid[p + k] ^ S.wid[q + k]);
+        for (uint32_t k2 = 0; k2 < n; ++k2) dw |= (uint32_t)(S.wid[p + k2] ^ S.wid[q + k2]);
         if (dw == 0) {
-          if (q > p) atomicMin(&tab[sl], mine);
+          if (qc > c) atomicMin(&tab[sl], mine);
           break;
         }
       }
       if (++sl == capn) sl = 0;
     }
-    gc[p] = (uint16_t)sl;
+    cnt[c] = sl << 16;
   }
   __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
-  for (uint32_t p = lane; p < G; p += 64) {
-    const uint32_t c = (tab[gc[p]] & 0xFFFFu) - 1u;
-    atomicAdd(&cnt[c], 1u);
+  for (uint32_t c = lane; c < nc; c += 64) {
+    const uint32_t g = (tab[cnt[c] >> 16] & 0xFFFFu) - 1u;
+    atomicAdd(&cnt[g], 1u);  // low half: counts <= nc <= MAXW never carry into the slot
   }
   __builtin_amdgcn_wave_barrier();
   uint32_t mx = 0;
-  for (uint32_t p = lane; p < G; p += 64) mx = cnt[p] > mx ? cnt[p] : mx;
+  for (uint32_t c = lane; c < nc; c += 64) mx = (cnt[c] & 0xFFFFu) > mx ? (cnt[c] & 0xFFFFu) : mx;
   for (int o = 32; o > 0; o >>= 1) {
     const uint32_t v = (uint32_t)__shfl_xor((int)mx, o);
     mx = v > mx ? v : mx;
   }
   if (mx <= 1) return 0;
   uint32_t ml = 0;
-  for (uint32_t p = lane; p < G; p += 64) {
-    if (cnt[p] != mx) continue;
+  for (uint32_t c = lane; c < nc; c += 64) {
+    if ((cnt[c] & 0xFFFFu) != mx) continue;
+    const uint32_t p = list[c];
     const uint32_t len = (uint32_t)(S.WL[p + n] - S.WL[p]) + n - 1;
     ml = len > ml ? len : ml;
   }
@@ -470,51 +541,44 @@ __device__ __forceinline__ int64_t ng_top_order(NS& S, uint32_t W, uint32_t n, u
   return (int64_t)ml * (int64_t)mx;
 }
 
-template <uint32_t MAXW>
 #ifndef TB_NG_WPE
 #define TB_NG_WPE 8  // 2.51 -> 2.29 ms/step vs 6 (profiles/r8_wpe/)
 #endif
+// Documents with more words than the workgroup's arrays hold (or byte prefixes past 16 bits) are
+// not run here: their launch positions go to a list after the export array (NgRest), and
+// k_gr_ngrams_rest runs their orders with the generic per-order code afterwards. Keeping that code
+// out of this kernel keeps its registers (and the profiling counters, kProf) off the hot path.
+struct NgRest {
+  uint32_t count;   // documents in `pos`
+  uint32_t cursor;  // k_gr_ngrams_rest's task cursor
+  uint32_t pad[2];
+  // followed by uint32_t pos[n_docs]
+};
+__host__ __device__ inline NgRest* ng_rest(const GrExport* ex, int32_t n_docs) {
+  return (NgRest*)((char*)ex + (size_t)n_docs * sizeof(GrExport));
+}
+
+template <uint32_t MAXW, bool kProf>
 __global__ __launch_bounds__(64 * kNgWaves) __attribute__((amdgpu_waves_per_eu(TB_NG_WPE, 8))) void k_gr_ngrams(
     const DevStage* __restrict__ stage, int32_t gr_step, const int32_t* __restrict__ perm, int32_t ndocs,
-    const GrExport* __restrict__ ex, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec,
-    uint32_t* flags, uint64_t* prof) {
+    const GrExport* __restrict__ ex, int32_t k0, NgRest* rest, int64_t* rec, uint64_t* prof) {
   __shared__ NgShared<MAXW> S;
-  const int k = (int)blockIdx.x;
+  const int k = k0 + (int)blockIdx.x;
   const int doc = perm[k];
   if (doc >= ndocs) return;
   const GrExport& e = ex[k];
   if (!e.valid) return;  // dead, returned early (flagged for the CPU path) or no n-grams
   const uint32_t W = e.W;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (!ng_fits(e, MAXW)) {
+    if (tid == 0) ((uint32_t*)(rest + 1))[atomicAdd(&rest->count, 1u)] = (uint32_t)k;
+    return;
+  }
   const DevStep& ds = stage->steps[gr_step];
   int64_t* r = rec + (int64_t)ds.rec_prefix * ndocs + (int64_t)doc * ds.width;
   const int nt = ds.n_dup + ds.n_top;
-  if (!ng_fits(e, MAXW)) {
-    // more words than this size class holds: the generic per-order code over HBM scratch, one
-    // order per wave at a time, each in its own share of the document's unused scratch slice
-    for (int t = (int)wv; t < nt; t += kNgWaves) {
-      DocCtx<WavePar> x;
-      x.prof = nullptr;
-      x.lds = nullptr;
-      x.lcap = 0;
-      x.lused = 0;
-      x.ucd = UcdView{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
-      x.pw = pw;
-      x.pw_n = pw_n;
-      x.ipw = pw ? pw + pw_n + 1 : nullptr;
-      const uint64_t region = (e.free_cap / (uint64_t)nt) & ~255ull;
-      x.scr = e.free_base + (uint64_t)t * region;
-      x.cap = region;
-      x.used = 0;
-      x.flag = flags + doc;
-      if (t < ds.n_dup) gr_dup_one_order(x, ds, t, e, r);
-      else gr_top_one_order(x, ds, t - ds.n_dup, e, r);
-      if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
-    }
-    return;
-  }
-  uint64_t* pf = prof ? prof + (size_t)doc * kPhaseSlots : nullptr;
-  const uint64_t t0 = pf ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t* pf = kProf ? prof + (size_t)doc * kPhaseSlots : nullptr;
+  const uint64_t t0 = kProf ? __builtin_amdgcn_s_memtime() : 0;
   for (uint32_t i = tid; i <= W; i += 64 * kNgWaves) {
     S.K[i] = e.K[i];
     S.PB[i] = e.PB[i];
@@ -522,26 +586,67 @@ __global__ __launch_bounds__(64 * kNgWaves) __attribute__((amdgpu_waves_per_eu(T
     S.wid[i] = i < W ? (uint16_t)e.wid[i] : (uint16_t)0;
   }
   __syncthreads();
-  if (pf && tid == 0) atomicAdd((unsigned long long*)&pf[PH_GR_DUP], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
+  if (kProf && tid == 0) atomicAdd((unsigned long long*)&pf[PH_GR_DUP], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
   uint64_t c_canon = 0, c_walk = 0, c_top = 0;  // (profiling: this wave's cycles per phase)
   for (int t = (int)wv; t < nt; t += kNgWaves) {
     int64_t v = 0;
     if (t < ds.n_dup) {
       const uint32_t n = (uint32_t)ds.dup_n[t];
-      if (n > 0 && W >= n) v = ng_dup_order(S, e, W, n, lane, S.region[wv], pf != nullptr, c_canon, c_walk);
+      if (n > 0 && W >= n) v = ng_dup_order(S, ex + k, W, n, lane, S.region[wv], kProf, c_canon, c_walk);
     } else {
       const uint32_t n = (uint32_t)ds.top_n[t - ds.n_dup];
-      const uint64_t ts = pf ? __builtin_amdgcn_s_memtime() : 0;
+      const uint64_t ts = kProf ? __builtin_amdgcn_s_memtime() : 0;
       if (n > 0 && W >= n) v = ng_top_order(S, W, n, lane, S.region[wv]);
-      if (pf) c_top += __builtin_amdgcn_s_memtime() - ts;
+      if (kProf) c_top += __builtin_amdgcn_s_memtime() - ts;
     }
     // record: the top orders first, then the duplicated orders
     if (lane == 0) r[rec_gr_fixed() + (t < ds.n_dup ? ds.n_top + t : t - ds.n_dup)] = v;
   }
-  if (pf && lane == 0) {
+  if (kProf && lane == 0) {
     atomicAdd((unsigned long long*)&pf[PH_GR_DUP_CANON], (unsigned long long)c_canon);
     atomicAdd((unsigned long long*)&pf[PH_GR_DUP_WALK], (unsigned long long)c_walk);
     atomicAdd((unsigned long long*)&pf[PH_GR_TOP_CANON], (unsigned long long)c_top);
+  }
+}
+
+// The orders of the documents k_gr_ngrams listed in NgRest (more words than its arrays hold): one
+// wave per (document, order) task from an atomic cursor, the generic per-order code over the
+// document's HBM scratch (each order in its own share of the unused slice). Persistent: a fixed
+// grid, every wave leaves once the cursor passes the last task.
+__global__ __launch_bounds__(64) void k_gr_ngrams_rest(
+    const DevStage* __restrict__ stage, int32_t gr_step, const int32_t* __restrict__ perm, int32_t ndocs,
+    const GrExport* __restrict__ ex, NgRest* rest, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
+    int64_t* rec, uint32_t* flags) {
+  const DevStep& ds = stage->steps[gr_step];
+  const int nt = ds.n_dup + ds.n_top;
+  const uint32_t total = __hip_atomic_load(&rest->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * (uint32_t)nt;
+  const uint32_t* pos = (const uint32_t*)(rest + 1);
+  while (true) {
+    uint32_t task = 0;
+    if (threadIdx.x == 0) task = atomicAdd(&rest->cursor, 1u);
+    task = (uint32_t)__builtin_amdgcn_readfirstlane((int)task);
+    if (task >= total) break;
+    const int k = (int)pos[task / (uint32_t)nt], t = (int)(task % (uint32_t)nt);
+    const int doc = perm[k];
+    const GrExport e = ex[k];
+    int64_t* r = rec + (int64_t)ds.rec_prefix * ndocs + (int64_t)doc * ds.width;
+    DocCtx<WavePar> x;
+    x.prof = nullptr;
+    x.lds = nullptr;
+    x.lcap = 0;
+    x.lused = 0;
+    x.ucd = UcdView{tabs.s1, tabs.s2, tabs.l1, tabs.l2};
+    x.pw = pw;
+    x.pw_n = pw_n;
+    x.ipw = pw ? pw + pw_n + 1 : nullptr;
+    const uint64_t region = (e.free_cap / (uint64_t)nt) & ~255ull;
+    x.scr = e.free_base + (uint64_t)t * region;
+    x.cap = region;
+    x.used = 0;
+    x.flag = flags + doc;
+    if (t < ds.n_dup) gr_dup_one_order(x, ds, t, e, r);
+    else gr_top_one_order(x, ds, t - ds.n_dup, e, r);
+    if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
   }
 }
 
@@ -550,7 +655,7 @@ __global__ __launch_bounds__(64 * kNgWaves) __attribute__((amdgpu_waves_per_eu(T
 // handles launch position k / n_tasks of the wave launch (its export slot) and task k % n_tasks;
 // every task works in its own share of the document's unused scratch slice (tables stay in the
 // LDS slice for wave-sized documents). Same records as the in-stage path.
-__global__ __launch_bounds__(64) void k_gr_split_wave(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_gr_split_wave(
     const DevStage* __restrict__ stage, int32_t gr_step, const int32_t* __restrict__ perm, int32_t n_tasks,
     int32_t ndocs, const GrExport* __restrict__ ex, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
     int64_t* rec, uint32_t* flags, uint32_t lds_bytes) {
@@ -1790,9 +1895,18 @@ int tb_gr_split_wave(hipStream_t stream, const void* stage, int32_t gr_step, con
     hipLaunchKernelGGL(k_gr_split_wave, dim3((uint32_t)n_wave * (uint32_t)n_tasks), dim3(64), lds_bytes, stream,
                        (const DevStage*)stage, gr_step, perm, n_tasks, ndocs, ex, pw, pw_n, t, rec, flags, lds_bytes);
   }
-  if (block && n_docs > n_big)
-    hipLaunchKernelGGL((k_gr_ngrams<256>), dim3((uint32_t)(n_docs - n_big)), dim3(64 * kNgWaves), 0, stream,
-                       (const DevStage*)stage, gr_step, perm + n_big, ndocs, ex + n_big, pw, pw_n, t, rec, flags, prof);
+  if (block && n_docs > n_big) {
+    // (the export buffer carries NgRest + n_docs positions after the descriptors, zeroed)
+    NgRest* rest = ng_rest(ex, n_docs);
+    if (prof)
+      hipLaunchKernelGGL((k_gr_ngrams<256, true>), dim3((uint32_t)(n_docs - n_big)), dim3(64 * kNgWaves), 0, stream,
+                         (const DevStage*)stage, gr_step, perm, ndocs, ex, n_big, rest, rec, prof);
+    else
+      hipLaunchKernelGGL((k_gr_ngrams<256, false>), dim3((uint32_t)(n_docs - n_big)), dim3(64 * kNgWaves), 0,
+                         stream, (const DevStage*)stage, gr_step, perm, ndocs, ex, n_big, rest, rec, nullptr);
+    hipLaunchKernelGGL(k_gr_ngrams_rest, dim3(512), dim3(64), 0, stream, (const DevStage*)stage, gr_step, perm,
+                       ndocs, ex, rest, pw, pw_n, t, rec, flags);
+  }
   return (int)hipGetLastError();
 }
 

@@ -190,6 +190,11 @@ class Kernels:
             _ptr(dead), _ptr(line_stats), _ptr(gr_export))
         _check(rc, "tb_stage_analyze")
 
+    def gr_export_wave_bytes(self, n_docs: int) -> int:
+        """Bytes of a zeroed wave export buffer: n_docs descriptors, then k_gr_ngrams' list of the
+        documents its LDS arrays cannot hold (NgRest: 16-byte header + a u32 per document)."""
+        return n_docs * self.sizeof_gr_export + 16 + 4 * n_docs
+
     def gr_split_wave(self, stage, gr_step, perm, n_docs, n_tasks, ndocs, gr_export, pw, pw_n, rec, flags, lds_bytes,
                       block=True, prof=None, n_big=0):
         """The n-gram orders of the wave documents stage_analyze exported (n_tasks = the
@@ -198,7 +203,7 @@ class Kernels:
         (k_gr_ngrams); without ``block`` k_gr_split_wave for all."""
         if not 0 <= n_big <= n_docs:
             raise DeviceError("gr_split_wave: n_big out of range")
-        if gr_export.nbytes < n_docs * self.sizeof_gr_export or perm.numel() < n_docs:
+        if gr_export.nbytes < self.gr_export_wave_bytes(n_docs) or perm.numel() < n_docs:
             raise DeviceError("gr_split_wave: operand shapes")
         t = self.tabs
         rc = self.lib.tb_gr_split_wave(self.stream(), stage.data_ptr(), gr_step, perm.data_ptr(), n_docs, n_tasks,

@@ -1028,7 +1028,7 @@ class DeviceRunner:
                     if s in self.gr_split and self.wave_split:
                         # split mode: the wave documents' n-gram orders run one wave per (document,
                         # order) after the stage kernel (k_gr_split_wave)
-                        gxw = rt.zeros(nw * self.k.sizeof_gr_export, np.uint8)
+                        gxw = rt.zeros(self.k.gr_export_wave_bytes(nw), np.uint8)
                         keep.append(gxw)
                     with self._ktimed(keep, f"stage{s}"):
                         self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,

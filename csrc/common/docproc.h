@@ -420,6 +420,116 @@ TB_HD bool word_mark(const PropArr& prop, uint32_t C, uint32_t i) {
   return wb_break(CpsAcc{prop}, (int)C, (int)i);
 }
 
+#if defined(__HIPCC__)
+// words() for one wave (WavePar), in one pass over the code points instead of a mark pass and a
+// scan pass: each chunk's packed entries are loaded once (the next chunk's while this one is
+// processed, so the load is off the critical path), the neighbours the break rules look at come
+// from DPP lane moves (wave_shr / wave_shl) plus a two-entry carry, and the word's byte span
+// travels in the scan element, so the emit has no dependent offset loads. Same words as the
+// generic version (word_mark + the WSeg scan).
+struct WSeg5 {
+  uint32_t bits, first, last, fo, lo;  // WSeg + byte offsets of `first` / `last`
+};
+__device__ __forceinline__ WSeg5 wseg5_op(const WSeg5& a, const WSeg5& b) {
+  if (b.bits & 1u) return b;
+  return WSeg5{a.bits | (b.bits & 6u), a.first < b.first ? a.first : b.first, a.last > b.last ? a.last : b.last,
+               a.fo < b.fo ? a.fo : b.fo, a.lo > b.lo ? a.lo : b.lo};
+}
+__device__ __forceinline__ uint32_t lane_prev(uint32_t v) {  // lane l gets lane l-1 (lane 0: v)
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t lane_next(uint32_t v) {  // lane l gets lane l+1 (lane 63: v)
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x130, 0xF, 0xF, false);
+}
+// word_mark from the four properties around position i (sentinel 0xFFFFFFFF outside [0, C))
+__device__ __forceinline__ bool word_mark4(const PropArr& prop, uint32_t C, uint32_t i, uint32_t pm2, uint32_t pm1,
+                                           uint32_t p0, uint32_t pp1) {
+  if (i == 0 || i >= C) return true;
+  const int r = wb_break_ctx(pm2, pm1, p0, pp1);
+  if (r != 2) return r != 0;
+  return wb_break(CpsAcc{prop}, (int)C, (int)i);
+}
+template <class P>
+__device__ Words words_wave(DocCtx<P>& x, const Cps& c) {
+  Words w;
+  const uint32_t C = c.n;
+  w.cs = x.template alloc<uint32_t>(C + 1);
+  w.ce = x.template alloc<uint32_t>(C + 1);
+  w.bs = x.template alloc<uint32_t>(C + 1);
+  w.be = x.template alloc<uint32_t>(C + 1);
+  w.alpha = x.template alloc<uint8_t>(C + 1);
+  if (x.overflow) return w;
+  const PropArr prop = c.props();
+  const uint32_t lane = x.par.lane;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint32_t *cs = w.cs, *ce = w.ce, *bs = w.bs, *be = w.be;
+  uint8_t* al = w.alpha;
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  // entry i <= C: property (entry C: 0) and byte offset (entry C: the byte length)
+  uint32_t cp = 0, co = 0, np = 0, no = 0;
+  if (lane <= C) { cp = c.p(lane); co = c.o(lane); }
+  uint32_t c1 = kNone, c2 = kNone;  // properties of the two code points before the chunk
+  WSeg5 carry{0u, kNone, 0u, kNone, 0u};
+  uint32_t k = 0;
+  for (uint32_t base = 0; base < C; base += 64) {
+    const uint32_t j = base + lane;
+    const uint32_t jn = j + 64;
+    if (jn <= C) { np = c.p(jn); no = c.o(jn); }  // prefetch of the next chunk
+    // neighbours: i-1, i-2 (carry for the first lanes), i+1 (the next chunk's first for lane 63)
+    const uint32_t n0p = (uint32_t)__builtin_amdgcn_readfirstlane((int)np);
+    const uint32_t n1p = (uint32_t)__builtin_amdgcn_readlane((int)np, 1);
+    const uint32_t n0o = (uint32_t)__builtin_amdgcn_readfirstlane((int)no);
+    uint32_t pm1 = lane_prev(cp);
+    if (lane == 0) pm1 = c1;
+    uint32_t pm2 = lane_prev(pm1);
+    if (lane == 0) pm2 = c2;
+    uint32_t pp1 = lane_next(cp), on = lane_next(co);
+    if (lane == 63) { pp1 = base + 64 <= C ? n0p : kNone; on = n0o; }
+    // positions past C-1 do not exist for the rules (word_mark's sentinels)
+    const uint32_t pm2s = j >= 2 ? pm2 : kNone;
+    const uint32_t pp1s = j + 1 < C ? pp1 : kNone;
+    const bool mk = j < C && word_mark4(prop, C, j, pm2s, pm1, cp, pp1s);
+    // the mark at base + 64 (lane 63's successor): from the last two code points and the next
+    // chunk's first two (uniform)
+    const uint32_t l62 = (uint32_t)__builtin_amdgcn_readlane((int)cp, 62);
+    const uint32_t l63 = (uint32_t)__builtin_amdgcn_readlane((int)cp, 63);
+    const uint32_t i64 = base + 64;
+    const bool mk64 = i64 >= C || word_mark4(prop, C, i64, l62, l63, n0p, i64 + 1 < C ? n1p : kNone);
+    const uint64_t M = __ballot(mk);
+    const bool mnext = lane == 63 ? mk64 : (((M >> (lane + 1)) & 1ull) != 0 || j + 1 >= C);
+    const bool ws = is_ws(cp);
+    WSeg5 e;
+    e.bits = (mk ? 1u : 0u) | ((!(cp & P_PUNCT) && !ws) ? 2u : 0u) | ((cp & P_ALPHA) ? 4u : 0u);
+    e.first = ws ? kNone : j;
+    e.last = ws ? 0u : j + 1;
+    e.fo = ws ? kNone : co;
+    e.lo = ws ? 0u : on;
+    if (j >= C) e = WSeg5{0u, kNone, 0u, kNone, 0u};
+    const WSeg5 xs = pardetail::wave_incl_scan(e, lane, wseg5_op);
+    const WSeg5 incl = wseg5_op(carry, xs);
+    const bool sel = j < C && mnext && (incl.bits & 2u);
+    const uint64_t sm = __ballot(sel);
+    if (sel) {
+      const uint32_t q = k + (uint32_t)__popcll(sm & lt);
+      cs[q] = incl.first;
+      ce[q] = incl.last;
+      bs[q] = incl.fo;
+      be[q] = incl.lo;
+      al[q] = (incl.bits & 4u) ? 1 : 0;
+    }
+    k += (uint32_t)__popcll(sm);
+    carry = wseg5_op(carry, pardetail::bcast63(xs));
+    c2 = l62;
+    c1 = l63;
+    cp = np;
+    co = no;
+  }
+  w.n = k;
+  x.par.sync();
+  return w;
+}
+#endif
+
 template <class P>
 TB_HD Words words(DocCtx<P>& x, const Cps& c, const PreDoc* pre = nullptr) {
   Words w;
@@ -432,6 +542,9 @@ TB_HD Words words(DocCtx<P>& x, const Cps& c, const PreDoc* pre = nullptr) {
     w.alpha = pre->wal;
     return w;
   }
+#if defined(__HIPCC__) && !defined(TB_WORDS_GENERIC)
+  if constexpr (P::kWaves == 1) return words_wave(x, c);
+#endif
   const uint32_t C = c.n;
   w.cs = x.template alloc<uint32_t>(C + 1);
   w.ce = x.template alloc<uint32_t>(C + 1);

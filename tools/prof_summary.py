@@ -76,13 +76,13 @@ def main():
     # grid (work-items) and duration, in launch order -- separates the per-stage launches of
     # kernels that run more than once per step
     starts = [a for a, _, k in iv if k.startswith("k_langid")]
-    if starts and rows and "Grid_Size" in rows[0]:
+    if starts and rows and "Grid_Size_X" in rows[0]:
         last = starts[-1]
         print(f"\nlaunches of the last step:\n{'kernel':<44} {'grid':>10} {'us':>10}")
         for r in sorted(rows, key=lambda r: int(r["Start_Timestamp"])):
             a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
             if a >= last:
-                print(f"{short(r['Kernel_Name']):<44} {r['Grid_Size']:>10} {(b - a) / 1e3:>10.1f}")
+                print(f"{short(r['Kernel_Name']):<44} {r['Grid_Size_X']:>10} {(b - a) / 1e3:>10.1f}")
     if args.copies:
         rows = list(csv.DictReader(open(args.copies)))
         agg = defaultdict(lambda: [0, 0, 0])

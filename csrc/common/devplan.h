@@ -119,4 +119,25 @@ TB_HD uint64_t dev_key(uint64_t h, uint32_t len) {
   return x | 1ull;
 }
 
+// Dictionary-script documents (ICU segments their words by dictionary) of a stage's content
+// version: the host's word-break bitmaps of the original text (version 0: moff[d] = word offset of
+// document d's bitmap in `bits`, -1 none; text.h dict_word_marks), or per document the word count
+// of the C4 rewrite (later versions: the kept lines' words from C4 pass A's export path, kNoWords
+// when unknown). Read only for documents that hold such a script; without either they go to the
+// CPU path as before.
+constexpr uint32_t kNoWords = 0xFFFFFFFFu;
+// C4 pass A's per-line word statistics of dictionary-script documents (text.h dict_c4_lines)
+struct DictLines {
+  const int64_t* off = nullptr;
+  const uint32_t* data = nullptr;
+  TB_HD const uint32_t* at(uint32_t d) const { return (off && off[d] >= 0) ? data + off[d] : nullptr; }
+};
+struct DictIn {
+  const int64_t* moff = nullptr;
+  const uint32_t* bits = nullptr;
+  const uint32_t* words = nullptr;
+  TB_HD const uint32_t* marks(uint32_t d) const { return (moff && moff[d] >= 0) ? bits + moff[d] : nullptr; }
+  TB_HD uint32_t nwords(uint32_t d) const { return words ? words[d] : kNoWords; }
+};
+
 }  // namespace tb

@@ -450,7 +450,7 @@ __device__ __forceinline__ bool word_mark4(const PropArr& prop, uint32_t C, uint
   return wb_break(CpsAcc{prop}, (int)C, (int)i);
 }
 template <class P>
-__device__ Words words_wave(DocCtx<P>& x, const Cps& c) {
+__device__ Words words_wave(DocCtx<P>& x, const Cps& c, const uint32_t* marks) {
   Words w;
   const uint32_t C = c.n;
   w.cs = x.template alloc<uint32_t>(C + 1);
@@ -488,13 +488,18 @@ __device__ Words words_wave(DocCtx<P>& x, const Cps& c) {
     // positions past C-1 do not exist for the rules (word_mark's sentinels)
     const uint32_t pm2s = j >= 2 ? pm2 : kNone;
     const uint32_t pp1s = j + 1 < C ? pp1 : kNone;
-    const bool mk = j < C && word_mark4(prop, C, j, pm2s, pm1, cp, pp1s);
     // the mark at base + 64 (lane 63's successor): from the last two code points and the next
-    // chunk's first two (uniform)
+    // chunk's first two (uniform); with host marks (dictionary scripts, ICU) both from the bitmap
     const uint32_t l62 = (uint32_t)__builtin_amdgcn_readlane((int)cp, 62);
     const uint32_t l63 = (uint32_t)__builtin_amdgcn_readlane((int)cp, 63);
     const uint32_t i64 = base + 64;
-    const bool mk64 = i64 >= C || word_mark4(prop, C, i64, l62, l63, n0p, i64 + 1 < C ? n1p : kNone);
+    bool mk = j < C && word_mark4(prop, C, j, pm2s, pm1, cp, pp1s);
+    bool mk64 = i64 >= C || word_mark4(prop, C, i64, l62, l63, n0p, i64 + 1 < C ? n1p : kNone);
+    if (marks) {  // host record: ICU marks (first bitmap) where its mask (second bitmap) is set
+      const uint32_t* hm = marks + mask_words(C + 1);
+      if (j < C && ((hm[j >> 5] >> (j & 31)) & 1u)) mk = ((marks[j >> 5] >> (j & 31)) & 1u) != 0;
+      if (i64 < C && ((hm[i64 >> 5] >> (i64 & 31)) & 1u)) mk64 = ((marks[i64 >> 5] >> (i64 & 31)) & 1u) != 0;
+    }
     const uint64_t M = __ballot(mk);
     const bool mnext = lane == 63 ? mk64 : (((M >> (lane + 1)) & 1ull) != 0 || j + 1 >= C);
     const bool ws = is_ws(cp);
@@ -531,7 +536,10 @@ __device__ Words words_wave(DocCtx<P>& x, const Cps& c) {
 #endif
 
 template <class P>
-TB_HD Words words(DocCtx<P>& x, const Cps& c, const PreDoc* pre = nullptr) {
+// `marks`: a host record of the code points [0, C] (dictionary scripts: ICU's dictionary
+// segmentation of their lines, text.h dict_word_marks): its marks replace word_mark where its mask
+// is set.
+TB_HD Words words(DocCtx<P>& x, const Cps& c, const PreDoc* pre = nullptr, const uint32_t* marks = nullptr) {
   Words w;
   if (pre) {  // the pre-pass segmented this document already (k_pre_words)
     w.n = pre->W;
@@ -543,7 +551,7 @@ TB_HD Words words(DocCtx<P>& x, const Cps& c, const PreDoc* pre = nullptr) {
     return w;
   }
 #if defined(__HIPCC__) && !defined(TB_WORDS_GENERIC)
-  if constexpr (P::kWaves == 1) return words_wave(x, c);
+  if constexpr (P::kWaves == 1) return words_wave(x, c, marks);
 #endif
   const uint32_t C = c.n;
   w.cs = x.template alloc<uint32_t>(C + 1);
@@ -558,7 +566,14 @@ TB_HD Words words(DocCtx<P>& x, const Cps& c, const PreDoc* pre = nullptr) {
   if (x.overflow) return w;
   const PropArr prop = c.props();
   const OffArr off = c.offs();
-  x.par.mask_bits(C + 1, [&](uint32_t i) { return word_mark(prop, C, i); }, wbm);
+  if (marks) {  // host record: ICU marks where its mask says so, the rules elsewhere
+    const uint32_t* hm = marks + mask_words(C + 1);
+    x.par.mask_bits(C + 1, [&](uint32_t i) {
+      return ((hm[i >> 5] >> (i & 31)) & 1u) ? ((marks[i >> 5] >> (i & 31)) & 1u) != 0 : word_mark(prop, C, i);
+    }, wbm);
+  } else {
+    x.par.mask_bits(C + 1, [&](uint32_t i) { return word_mark(prop, C, i); }, wbm);
+  }
   x.par.sync();
   auto bit = [&](uint32_t i) { return (wbm[i >> 5] >> (i & 31)) & 1u; };
   uint32_t *cs = w.cs, *ce = w.ce, *bs = w.bs, *be = w.be;
@@ -1006,6 +1021,8 @@ struct StageOut {
   const PreDoc* pre = nullptr;  // non-null: decode and word-break marks were precomputed
   // the document's bytes in HBM (split mode exports them: the stage may read an LDS copy)
   const uint8_t* b_global = nullptr;
+  // dictionary-script documents: where their words come from (DictIn)
+  DictIn dict;
 };
 
 // The C4 line export of one document: a header (line count, or kLineStatsNone while / when the
@@ -2049,7 +2066,7 @@ TB_HD uint32_t last_cp(const uint8_t* b, uint32_t s, uint32_t e, uint32_t n) {
 template <class P>
 TB_HD void c4_plain_tail(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, uint32_t NLn,
                          const uint32_t* lbs, const uint32_t* lbe, const uint32_t* nw, const uint32_t* mx,
-                         uint32_t phrase_bits, int64_t* r, int64_t* src) {
+                         uint32_t phrase_bits, int64_t* r, int64_t* src, uint32_t* wout = nullptr) {
   uint32_t* pf = x.template alloc_hot<uint32_t>(NLn + 1);   // pattern flags per line
   uint8_t* code = x.template alloc_hot<uint8_t>(NLn + 1);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
@@ -2097,6 +2114,12 @@ TB_HD void c4_plain_tail(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32
   });
   const int64_t s_long = (int64_t)(s12 & 0xFFFFFFFFull), s_punct = (int64_t)(s12 >> 32);
   const int64_t s_few = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 3); });
+  if (wout) {
+    // words of the rewrite (the kept lines joined by '\n', trimmed): words never cross a line
+    // feed, so they are the kept lines' words (StageOut::dict_words of the next version)
+    const uint32_t wk = x.par.template sum<uint32_t>(NLn, [&](uint32_t k) { return code[k] == 0 ? nw[k] : 0u; });
+    x.par.single([&]() { *wout = wk; });
+  }
   x.stamp(PH_C4_CODES);
   // ---- joined kept lines (HBM: read back by pass B), copied byte by byte ----
   uint32_t* joff = x.template alloc_hot<uint32_t>(NLn + 1);
@@ -2171,7 +2194,7 @@ TB_HD void c4_pass_a_plain(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint
 // lines or words here.
 template <class P>
 TB_HD void c4_pass_a_export(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, const uint32_t* region,
-                            uint32_t NLn, int64_t* r, int64_t* src, uint32_t phrase_bits) {
+                            uint32_t NLn, int64_t* r, int64_t* src, uint32_t phrase_bits, uint32_t* wout = nullptr) {
   const LineStat* ls = (const LineStat*)(region + 4);
   uint32_t* lbs = x.template alloc_hot<uint32_t>(NLn + 1);
   uint32_t* lbe = x.template alloc_hot<uint32_t>(NLn + 1);
@@ -2185,12 +2208,16 @@ TB_HD void c4_pass_a_export(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uin
   x.par.single([&]() { lbs[NLn] = 0xFFFFFFFFu; });
   x.par.sync();
   x.stamp(PH_C4_WORDS);
-  c4_plain_tail(x, c4, b, n, NLn, lbs, lbe, nw, mx, phrase_bits, r, src);
+  c4_plain_tail(x, c4, b, n, NLn, lbs, lbe, nw, mx, phrase_bits, r, src, wout);
 }
 
+// `wout` (optional): the rewrite's word count when it comes from the stage's line export (the
+// only path a dictionary-script document takes here; kNoWords stays otherwise)
+// `hls` (optional): a dictionary-script document's per-line word statistics from the host (ICU,
+// text.h dict_c4_lines: [NL, nw_0, mx_0, ...]) in place of segmenting its processed lines here.
 template <class P>
 TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, int64_t* r, int64_t* src,
-                     const uint32_t* line_stats = nullptr) {
+                     const uint32_t* line_stats = nullptr, uint32_t* wout = nullptr, const uint32_t* hls = nullptr) {
   x.stamp(PH_START);
   const uint32_t scan = c4_byte_scan(x, c4, b, n);
   const bool lorem = scan & C4S_LOREM, curly = scan & C4S_CURLY;
@@ -2211,7 +2238,7 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   if (TB_C4_PLAIN && !maybe_cite && line_stats && c4.split_paragraph) {
     const uint32_t NL = line_stats[0];  // the stage kernel of this content version wrote it
     if (NL != kLineStatsNone) {
-      c4_pass_a_export(x, c4, b, n, line_stats, NL, r, src, scan);
+      c4_pass_a_export(x, c4, b, n, line_stats, NL, r, src, scan, wout);
       return;
     }
   }
@@ -2222,7 +2249,8 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   const uint32_t C = c.n;
   const PropArr prop = c.props();
   const OffArr off = c.offs();
-  if (dict) {
+  if (!dict) hls = nullptr;
+  if (dict && (!hls || !c4.split_paragraph)) {
     x.set_flag(DOC_NEEDS_CPU);
     return;
   }
@@ -2270,7 +2298,11 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   }
   x.par.sync();
   x.stamp(PH_C4_LINES);
-  if (TB_C4_PLAIN && !maybe_cite) {
+  if (hls && hls[0] != NLn) {  // (never: the host splits the same Rust lines)
+    x.set_flag(DOC_NEEDS_CPU);
+    return;
+  }
+  if (TB_C4_PLAIN && !maybe_cite && !hls) {
     c4_pass_a_plain(x, c4, b, n, c, la, lb, NLn, r, src, scan);
     return;
   }
@@ -2374,7 +2406,11 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   // copy cost more than segmenting the whole processed text, measured)
   const bool from_export = P::kWaves == 1 && TB_C4_PLAIN && line_stats && c4.split_paragraph && NLn > 0 &&
                            line_stats[0] == NLn;
-  if (from_export) {
+  if (hls) {
+    if (!line_arrays()) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+    x.par.for_n(NLn, [&](uint32_t k) { nw[k] = hls[1 + 2 * k]; mx[k] = hls[2 + 2 * k]; });
+    x.par.sync();
+  } else if (from_export) {
     if (!line_arrays()) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
     // Lines that lost no citation are their trimmed original lines: their counts come from the
     // stage's line export. Only the processed text of the lines that lost one (code[k] = 1 marks
@@ -2465,6 +2501,10 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   const int64_t s_long = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 1); });
   const int64_t s_punct = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 2); });
   const int64_t s_few = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 3); });
+  if (wout && hls) {  // words of the rewrite: the kept lines' (see c4_plain_tail)
+    const uint32_t wk = x.par.template sum<uint32_t>(NLn, [&](uint32_t k) { return code[k] == 0 ? nw[k] : 0u; });
+    x.par.single([&]() { *wout = wk; });
+  }
   x.stamp(PH_C4_CODES);
   // ---- joined kept lines (HBM: read back by pass B), scattered per code point ----
   uint32_t* joff = x.template alloc_hot<uint32_t>(NLn + 1);
@@ -2537,23 +2577,45 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
   // recomputed there, so nothing else is analysed on the device. The language record needs no
   // segmentation and is exact for every script (the device computes it in its own kernel, and a
   // document the language gate filters is not delegated), so the emulation still produces it.
-  if (ndict) {
-    if constexpr (kWithLid) {
-      for (int s = 0; s < st.n_steps; ++s) {
-        const DevStep& ds = st.steps[s];
-        if (ds.kind == DK_LANGID && (lid.P || lid.E))
-          langid_record(x, b, n, lid, out.rec + (int64_t)ds.rec_prefix * out.ndocs + (int64_t)out.doc * ds.width);
+  // Dictionary-script documents: their words come from the host's ICU segmentation (the word
+  // marks of the original text), or — for a stage after C4 whose only word reader is FineWeb,
+  // which needs just the count — from the word count C4 pass A left for the rewrite. Otherwise
+  // (no marks, GopherQuality / GopherRepetition on a rewritten version, a pre-pass document) the
+  // document goes to the ICU path (host) and is recomputed there, so nothing else is analysed
+  // here. The language record needs no segmentation and is exact for every script (the device
+  // computes it in its own kernel, and a document the language gate filters is not delegated),
+  // so the emulation still produces it.
+  // wfix: the word count a count-only document's FineWeb record takes (kNoWords: none); it is
+  // applied after the steps, so no branch on it sits in the analysis (a branch there made the
+  // compiler duplicate the step loop: 4x the register spills)
+  const uint32_t* dict_marks = nullptr;
+  uint32_t wfix = kNoWords;
+  if (ndict && need_words) {  // (a stage without word segmentation reads no script-dependent data)
+    bool fw_only = true;
+    for (int s = 0; s < st.n_steps; ++s)
+      fw_only &= st.steps[s].kind != DK_GOPHER_QUALITY && st.steps[s].kind != DK_GOPHER_REP;
+    if (!kPre) dict_marks = out.dict.marks(out.doc);
+    if (!kPre && !dict_marks && fw_only) wfix = out.dict.nwords(out.doc);
+    if (!dict_marks && wfix == kNoWords) {
+      if constexpr (kWithLid) {
+        for (int s = 0; s < st.n_steps; ++s) {
+          const DevStep& ds = st.steps[s];
+          if (ds.kind == DK_LANGID && (lid.P || lid.E))
+            langid_record(x, b, n, lid, out.rec + (int64_t)ds.rec_prefix * out.ndocs + (int64_t)out.doc * ds.width);
+        }
       }
+      x.set_flag(DOC_NEEDS_CPU);
+      return;
     }
-    x.set_flag(DOC_NEEDS_CPU);
-    return;
   }
   x.stamp(PH_DICT);
   PHView ph;
   if (need_ph) ph = prefix_hash8(x, b, n);
   x.stamp(PH_PREFIX_HASH);
   Words w;
-  if (need_words) w = words(x, c, kPre ? out.pre : nullptr);
+  if (need_words) {
+    w = words(x, c, kPre ? out.pre : nullptr, dict_marks);
+  }
   x.stamp(PH_WORDS);
   Lines L;
   if (need_lines) L = rust_lines(x, c);
@@ -2693,6 +2755,18 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
       x.stamp(PH_LID);
     }
     if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  }
+  if (wfix != kNoWords) {
+    // a count-only document (dictionary script, FineWeb after C4): its words were segmented by the
+    // rules above; FineWeb's word count is C4's ICU-based one, and its line export is withdrawn
+    x.par.sync();
+    x.par.single([&]() {
+      for (int s = 0; s < st.n_steps; ++s) {
+        const DevStep& ds = st.steps[s];
+        if (ds.kind == DK_FINEWEB) out.rec[(int64_t)ds.rec_prefix * out.ndocs + (int64_t)out.doc * ds.width + 6] = wfix;
+      }
+      if (out.line_stats) out.line_stats[0] = kLineStatsNone;
+    });
   }
 }
 

@@ -108,7 +108,7 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
       const int64_t* __restrict__ off, const int32_t* __restrict__ perm, int32_t ndocs, char* scratch,        \
       const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, \
       int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof,                               \
-      const uint8_t* __restrict__ dead, uint32_t* line_stats, GrExport* gr_export) {                   \
+      const uint8_t* __restrict__ dead, uint32_t* line_stats, GrExport* gr_export, DictIn dict) {      \
     const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;                                        \
     if (doc >= ndocs || (dead && dead[doc])) return;                                                  \
     DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);   \
@@ -118,6 +118,7 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
     StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc};                                                \
     if (line_stats) out.line_stats = line_stats + line_stats_base(off[doc], doc);                     \
     if (gr_export) { out.gr_export = gr_export + blockIdx.x; out.b_global = bytes + off[doc]; }       \
+    out.dict = dict;                                                                                  \
     analyze_stage<WavePar, false>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out); /* LD: own kernel */ \
   }
 
@@ -157,7 +158,7 @@ __device__ __forceinline__ void stage_blk_body(
     const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,
     int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead,
     GrExport* gr_export, int32_t n_split, uint32_t split_bytes, uint32_t* line_stats, const PreDoc* pre,
-    int32_t n_pre) {
+    int32_t n_pre, DictIn dict) {
   const int doc = perm[blockIdx.x];
   if (doc >= ndocs || (dead && dead[doc])) return;
   DocCtx<BlockPar<NT>> x =
@@ -167,6 +168,7 @@ __device__ __forceinline__ void stage_blk_body(
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   StageOut out{rec, (uint32_t)ndocs, (uint32_t)doc};
+  out.dict = dict;
   if (line_stats) out.line_stats = line_stats + line_stats_base(off[doc], doc);
   if constexpr (kPre) {
     if (pre[blockIdx.x].n != n) return;  // (never: the host builds the descriptors from these lengths)
@@ -185,9 +187,9 @@ __device__ __forceinline__ void stage_blk_body(
       const int64_t* __restrict__ scratch_off, const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs,  \
       int64_t* rec, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead,   \
       GrExport* gr_export, int32_t n_split, uint32_t split_bytes, uint32_t* line_stats,                \
-      const PreDoc* pre, int32_t n_pre) {                                                              \
+      const PreDoc* pre, int32_t n_pre, DictIn dict) {                                                 \
     stage_blk_body<NT, PRE>(plan, stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, tabs, rec, flags, \
-                       lds_bytes, prof, dead, gr_export, n_split, split_bytes, line_stats, pre, n_pre);  \
+                       lds_bytes, prof, dead, gr_export, n_split, split_bytes, line_stats, pre, n_pre, dict); \
   }
 TB_STAGE_BLK_KERNEL(k_stage_analyze_blk, kBlockThreads, false)
 // documents with a pre-pass (tb_stage_analyze_blk with `pre`): every launch position has one
@@ -1149,7 +1151,8 @@ __global__ __launch_bounds__(64) TB_C4_ATTR void k_c4_pass_a(
     const DevC4* __restrict__ c4, const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
     const int32_t* __restrict__ perm, int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off,
     const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec, int64_t* src, uint32_t* flags,
-    uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead, const uint32_t* __restrict__ line_stats) {
+    uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead, const uint32_t* __restrict__ line_stats,
+    uint32_t* c4_words, DictLines dict_lines) {
   const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
   if (doc >= ndocs || (dead && dead[doc])) return;  // skipped: record zeros, rewritten length 0
   DocCtx<WavePar> x = make_ctx(tabs, pw, pw_n, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
@@ -1157,7 +1160,8 @@ __global__ __launch_bounds__(64) TB_C4_ATTR void k_c4_pass_a(
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2,
-            line_stats ? line_stats + line_stats_base(off[doc], doc) : nullptr);
+            line_stats ? line_stats + line_stats_base(off[doc], doc) : nullptr, c4_words ? c4_words + doc : nullptr,
+            dict_lines.at((uint32_t)doc));
   c4_src_absolute(x, src + (int64_t)doc * 2, scratch_off[blockIdx.x]);
 }
 
@@ -1165,7 +1169,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_c4_pass_a_blk(
     const DevC4* __restrict__ c4, const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off,
     const int32_t* __restrict__ perm, int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off,
     const uint64_t* __restrict__ pw, uint32_t pw_n, DevTables tabs, int64_t* rec, int64_t* src, uint32_t* flags,
-    uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead, const uint32_t* __restrict__ line_stats) {
+    uint32_t lds_bytes, uint64_t* prof, const uint8_t* __restrict__ dead, const uint32_t* __restrict__ line_stats,
+    uint32_t* c4_words, DictLines dict_lines) {
   const int doc = perm[blockIdx.x];
   if (doc >= ndocs || (dead && dead[doc])) return;
   DocCtx<BlockPar<kBlockThreads>> x =
@@ -1175,7 +1180,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_c4_pass_a_blk(
   const uint8_t* b = bytes + off[doc];
   const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
   c4_pass_a(x, *c4, b, n, rec + (int64_t)doc * 7, src + (int64_t)doc * 2,
-            line_stats ? line_stats + line_stats_base(off[doc], doc) : nullptr);
+            line_stats ? line_stats + line_stats_base(off[doc], doc) : nullptr, c4_words ? c4_words + doc : nullptr,
+            dict_lines.at((uint32_t)doc));
   c4_src_absolute(x, src + (int64_t)doc * 2, scratch_off[blockIdx.x]);
 }
 
@@ -1856,7 +1862,8 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
                      const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n, const uint16_t* s1,
                      const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
                      uint32_t lds_bytes, uint64_t* prof, int32_t waves, int32_t nblocks, const uint8_t* dead,
-                     uint32_t* line_stats, void* gr_export) {
+                     uint32_t* line_stats, void* gr_export, const int64_t* dict_moff, const uint32_t* dict_bits,
+                     const uint32_t* dict_words) {
   if (ndocs <= 0) return 0;
   if (nblocks <= 0) nblocks = ndocs;  // grid: docs perm[0 .. nblocks)
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
@@ -1867,7 +1874,7 @@ int tb_stage_analyze(hipStream_t stream, const void* plan, const void* stage, co
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64), lds_bytes, stream, (const DevPlan*)plan,
                      (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, flags,
-                     lds_bytes, prof, dead, line_stats, (GrExport*)gr_export);
+                     lds_bytes, prof, dead, line_stats, (GrExport*)gr_export, DictIn{dict_moff, dict_bits, dict_words});
   return (int)hipGetLastError();
 }
 
@@ -1918,7 +1925,7 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
                          const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec, uint32_t* flags,
                          uint32_t lds_bytes, uint64_t* prof, const uint8_t* dead, void* gr_export, int32_t n_split,
                          uint32_t split_bytes, int32_t threads, uint32_t* line_stats, const void* pre,
-                         int32_t n_pre) {
+                         int32_t n_pre, const int64_t* dict_moff, const uint32_t* dict_bits, const uint32_t* dict_words) {
   if (nblocks <= 0) return 0;
   if (!perm || lds_bytes > kMaxLdsPerBlk || n_split < 0 || n_split > nblocks) return (int)hipErrorInvalidValue;
   if (threads != kBlockThreads) return (int)hipErrorInvalidValue;
@@ -1930,7 +1937,7 @@ int tb_stage_analyze_blk(hipStream_t stream, const void* plan, const void* stage
   hipLaunchKernelGGL(kern, dim3(nblocks), dim3(threads), lds_bytes, stream,
                      (const DevPlan*)plan, (const DevStage*)stage, bytes, off, perm, ndocs, scratch, scratch_off, pw,
                      pw_n, t, rec, flags, lds_bytes, prof, dead, (GrExport*)gr_export, n_split,
-                     split_bytes, line_stats, (const PreDoc*)pre, n_pre);
+                     split_bytes, line_stats, (const PreDoc*)pre, n_pre, DictIn{dict_moff, dict_bits, dict_words});
   return (int)hipGetLastError();
 }
 
@@ -2021,7 +2028,8 @@ int tb_c4_pass_a_blk(hipStream_t stream, const void* c4, const uint8_t* bytes, c
                      const int32_t* perm, int32_t nblocks, int32_t ndocs, char* scratch, const int64_t* scratch_off,
                      const uint64_t* pw, uint32_t pw_n, const uint16_t* s1, const uint32_t* s2, const uint16_t* l1,
                      const int32_t* l2, int64_t* rec, int64_t* src, uint32_t* flags, uint32_t lds_bytes,
-                     uint64_t* prof, const uint8_t* dead, const uint32_t* line_stats) {
+                     uint64_t* prof, const uint8_t* dead, const uint32_t* line_stats, uint32_t* c4_words,
+                     const int64_t* dict_loff, const uint32_t* dict_ldata) {
   if (nblocks <= 0) return 0;
   if (!perm || lds_bytes > kMaxLdsPerBlk) return (int)hipErrorInvalidValue;
   DevTables t{s1, s2, l1, l2};
@@ -2030,7 +2038,7 @@ int tb_c4_pass_a_blk(hipStream_t stream, const void* c4, const uint8_t* bytes, c
                               (int)lds_bytes);
   hipLaunchKernelGGL(k_c4_pass_a_blk, dim3(nblocks), dim3(kBlockThreads), lds_bytes, stream, (const DevC4*)c4,
                      bytes, off, perm, ndocs, scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof, dead,
-                     line_stats);
+                     line_stats, c4_words, DictLines{dict_loff, dict_ldata});
   return (int)hipGetLastError();
 }
 
@@ -2099,7 +2107,8 @@ int tb_c4_pass_a(hipStream_t stream, const void* c4, const uint8_t* bytes, const
                  int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint64_t* pw, uint32_t pw_n,
                  const uint16_t* s1, const uint32_t* s2, const uint16_t* l1, const int32_t* l2, int64_t* rec,
                  int64_t* src, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof, int32_t nblocks,
-                 const uint8_t* dead, const uint32_t* line_stats) {
+                 const uint8_t* dead, const uint32_t* line_stats, uint32_t* c4_words, const int64_t* dict_loff,
+                 const uint32_t* dict_ldata) {
   if (ndocs <= 0) return 0;
   if (nblocks <= 0) nblocks = ndocs;
   if (lds_bytes > kMaxLdsPerDoc) return (int)hipErrorInvalidValue;
@@ -2107,7 +2116,8 @@ int tb_c4_pass_a(hipStream_t stream, const void* c4, const uint8_t* bytes, const
   if (lds_bytes > 65536)
     (void)hipFuncSetAttribute((const void*)k_c4_pass_a, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   hipLaunchKernelGGL(k_c4_pass_a, dim3(nblocks), dim3(64), lds_bytes, stream, (const DevC4*)c4, bytes, off, perm, ndocs,
-                     scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof, dead, line_stats);
+                     scratch, scratch_off, pw, pw_n, t, rec, src, flags, lds_bytes, prof, dead, line_stats, c4_words,
+                     DictLines{dict_loff, dict_ldata});
   return (int)hipGetLastError();
 }
 
@@ -2178,7 +2188,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 int tb_phase_slots() { return kPhaseSlots; }
 int tb_stage_waves() { return TB_STAGE_WPE; }  // waves per SIMD the wave stage kernel is built for
 
-int tb_abi_version() { return 21; }
+int tb_abi_version() { return 23; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

@@ -340,7 +340,7 @@ uint64_t line_stats_buffer_words(const int64_t* off, int64_t ndocs) { return lin
 void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& idx, int64_t ndocs,
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
                    std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes, const uint8_t* dead,
-                   bool weak_keys, uint32_t* line_stats, int split_tasks) {
+                   bool weak_keys, uint32_t* line_stats, int split_tasks, DictIn dict) {
   DevPlan* plan = new DevPlan();
   std::memset(plan, 0, sizeof(DevPlan));
   DevStage st = build_stage(steps, idx, *plan);
@@ -376,6 +376,7 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
       x.flag = &flags[i];
       x.weak_keys = weak_keys;
       StageOut out{rec.data(), (uint32_t)ndocs, (uint32_t)i};
+      out.dict = dict;
       if (line_stats) out.line_stats = line_stats + line_stats_base(off[i], i);
       GrExport ex{};
       if (split_tasks > 0 && gr_pos >= 0) out.gr_export = &ex;
@@ -418,7 +419,8 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
 
 void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
                 std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,
-                std::vector<uint32_t>& flags, uint32_t lds_bytes, const uint8_t* dead, const uint32_t* line_stats) {
+                std::vector<uint32_t>& flags, uint32_t lds_bytes, const uint8_t* dead, const uint32_t* line_stats,
+                uint32_t* c4_words, DictLines dict_lines) {
   DevC4 c4 = build_c4(step);
   rec.assign((size_t)rec::C4_WIDTH * ndocs, 0);
   flags.assign(ndocs, 0);
@@ -448,7 +450,8 @@ void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int6
       int64_t src[2] = {-1, 0};
       const uint8_t* b = (const uint8_t*)data + off[i];
       c4_pass_a(x, c4, b, n, rec.data() + i * rec::C4_WIDTH, src,
-                line_stats ? line_stats + line_stats_base(off[i], i) : nullptr);
+                line_stats ? line_stats + line_stats_base(off[i], i) : nullptr, c4_words ? c4_words + i : nullptr,
+                dict_lines.at((uint32_t)i));
       if (!x.overflow) note_scratch(x.peak, n);
       if (flags[i] & DOC_NEEDS_CPU) continue;
       if (src[0] < 0) outs[i].assign((const char*)b, n);

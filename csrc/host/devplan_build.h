@@ -41,7 +41,7 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
                    const char* data, const int64_t* off, int nthreads, const LangidModel* lid,
                    std::vector<int64_t>& rec, std::vector<uint32_t>& flags, uint32_t lds_bytes = 0,
                    const uint8_t* dead = nullptr, bool weak_keys = false, uint32_t* line_stats = nullptr,
-                   int split_tasks = 0);
+                   int split_tasks = 0, DictIn dict = DictIn{});
 // split_tasks > 0: every document runs the intra-document split of its GopherRepetition step
 // (stage export, then the k_gr_dup_split tasks in turn, each in its slice of the arena rest)
 uint64_t line_stats_buffer_words(const int64_t* off, int64_t ndocs);  // u32 size of a batch's line export
@@ -50,7 +50,7 @@ uint64_t line_stats_buffer_words(const int64_t* off, int64_t ndocs);  // u32 siz
 void emulate_c4(const StepCfg& step, int64_t ndocs, const char* data, const int64_t* off, int nthreads,
                 std::vector<int64_t>& rec, std::string& new_data, std::vector<int64_t>& new_off,
                 std::vector<uint32_t>& flags, uint32_t lds_bytes = 0, const uint8_t* dead = nullptr,
-                const uint32_t* line_stats = nullptr);
+                const uint32_t* line_stats = nullptr, uint32_t* c4_words = nullptr, DictLines dict_lines = DictLines{});
 // Host run of k_gate (same loop body): dead[doc] = code for live docs that a gated step filters.
 void gate_host(const DevGate& g, const std::vector<const int64_t*>& recs, int64_t ndocs, const uint32_t* flags,
                uint8_t* dead, uint8_t code);

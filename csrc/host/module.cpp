@@ -152,6 +152,7 @@ PYBIND11_MODULE(_tbhost, m) {
       .def_property_readonly("n_dup", [](const StepCfg& c) { return (int)c.dup_n_grams.size(); })
       .def_property_readonly("n_top", [](const StepCfg& c) { return (int)c.top_n_grams.size(); })
       .def_readonly("name", &StepCfg::name)
+      .def_readonly("remove_citations", &StepCfg::remove_citations)
       .def("record_width", [](const StepCfg& c) { return record_width(c); });
   m.def("make_step", &make_step);
 
@@ -192,6 +193,31 @@ PYBIND11_MODULE(_tbhost, m) {
   m.def("trim", [](const std::string& s) { return std::string(trim(s)); });
   m.def("props", [](uint32_t cp) { return host_ucd().props(cp); });
   m.def("has_dict_script", [](const std::string& s) { return has_dict_script(s); });
+  m.def("dict_word_marks", [](py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
+                              int nthreads) {
+    std::vector<int64_t> moff;
+    std::vector<uint32_t> bits;
+    const int64_t nd = (int64_t)off.size() - 1;
+    {
+      py::gil_scoped_release nogil;
+      dict_word_marks(data.data(), off.data(), nd, nthreads, moff, bits);
+    }
+    return py::make_tuple(to_numpy(std::move(moff)), to_numpy(std::move(bits)));
+  }, py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8,
+     "ICU word-break marks of the dictionary-script documents (text.h dict_word_marks)");
+  m.def("dict_c4_lines", [](py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
+                            py::array_t<int64_t, py::array::c_style> moff, bool citations, int nthreads) {
+    std::vector<int64_t> loff;
+    std::vector<uint32_t> out;
+    const int64_t nd = (int64_t)off.size() - 1;
+    if ((int64_t)moff.size() < nd) throw std::runtime_error("dict_c4_lines: operand shapes");
+    {
+      py::gil_scoped_release nogil;
+      dict_c4_lines(data.data(), off.data(), nd, moff.data(), citations, nthreads, loff, out);
+    }
+    return py::make_tuple(to_numpy(std::move(loff)), to_numpy(std::move(out)));
+  }, py::arg("data"), py::arg("offsets"), py::arg("moff"), py::arg("citations"), py::arg("nthreads") = 8,
+     "C4 per-line ICU word statistics of the dictionary-script documents (text.h dict_c4_lines)");
   m.def("ucd_fold_tables", []() {
     std::vector<uint16_t> f1(TB_UCD_FOLD_STAGE1, TB_UCD_FOLD_STAGE1 + sizeof(TB_UCD_FOLD_STAGE1) / 2);
     std::vector<int32_t> f2(TB_UCD_FOLD_STAGE2, TB_UCD_FOLD_STAGE2 + sizeof(TB_UCD_FOLD_STAGE2) / 4);
@@ -872,7 +898,10 @@ PYBIND11_MODULE(_tbhost, m) {
                             py::array_t<uint8_t, py::array::c_style> data, py::array_t<int64_t, py::array::c_style> off,
                             int nthreads, std::shared_ptr<LangidModel> lid, uint32_t lds_bytes,
                             std::optional<py::array_t<uint8_t, py::array::c_style>> dead, bool weak_keys,
-                            std::optional<py::array_t<uint32_t, py::array::c_style>> line_stats, int split_tasks) {
+                            std::optional<py::array_t<uint32_t, py::array::c_style>> line_stats, int split_tasks,
+                            std::optional<py::array_t<int64_t, py::array::c_style>> dict_moff,
+                            std::optional<py::array_t<uint32_t, py::array::c_style>> dict_bits,
+                            std::optional<py::array_t<uint32_t, py::array::c_style>> dict_words) {
     std::vector<int64_t> rec;
     std::vector<uint32_t> flags;
     const int64_t nd = (int64_t)off.size() - 1;
@@ -883,15 +912,34 @@ PYBIND11_MODULE(_tbhost, m) {
       if ((uint64_t)line_stats->size() < line_stats_buffer_words(off.data(), nd)) throw std::runtime_error("line_stats too short");
       lp = line_stats->mutable_data();
     }
+    DictIn dict;
+    if (dict_moff) {
+      if ((int64_t)dict_moff->size() < nd || !dict_bits) throw std::runtime_error("dict marks: operand shapes");
+      const int64_t* mo = dict_moff->data();
+      for (int64_t d = 0; d < nd; ++d) {  // every bitmap inside `bits` (the kernels trust the offsets)
+        if (mo[d] < 0) continue;
+        uint32_t C = 0;
+        for (int64_t i = off.data()[d]; i < off.data()[d + 1]; ++i) C += (data.data()[i] & 0xC0) != 0x80;
+        if (mo[d] + (int64_t)(2 * (((C + 1 + 63) / 64) * 2)) > (int64_t)dict_bits->size())
+          throw std::runtime_error("dict marks: bitmap out of range");
+      }
+      dict.moff = mo;
+      dict.bits = dict_bits->data();
+    }
+    if (dict_words) {
+      if ((int64_t)dict_words->size() < nd) throw std::runtime_error("dict words: operand shapes");
+      dict.words = dict_words->data();
+    }
     {
       py::gil_scoped_release nogil;
       emulate_stage(steps, idx, nd, (const char*)data.data(), off.data(), nthreads, lid.get(), rec, flags, lds_bytes,
-                    dp, weak_keys, lp, split_tasks);
+                    dp, weak_keys, lp, split_tasks, dict);
     }
     return py::make_tuple(to_numpy(std::move(rec)), to_numpy(std::move(flags)));
   }, py::arg("steps"), py::arg("idx"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8,
      py::arg("lid") = nullptr, py::arg("lds_bytes") = 0, py::arg("dead") = py::none(),
-     py::arg("weak_keys") = false, py::arg("line_stats") = py::none(), py::arg("split_tasks") = 0);
+     py::arg("weak_keys") = false, py::arg("line_stats") = py::none(), py::arg("split_tasks") = 0,
+     py::arg("dict_moff") = py::none(), py::arg("dict_bits") = py::none(), py::arg("dict_words") = py::none());
   m.def("line_stats_words", [](py::array_t<int64_t, py::array::c_style> off) {
     return line_stats_buffer_words(off.data(), (int64_t)off.size() - 1);
   }, "u32 words of a batch's C4 line export buffer (docproc.h line_stats_base)");
@@ -918,7 +966,10 @@ PYBIND11_MODULE(_tbhost, m) {
   m.def("emulate_c4", [](const StepCfg& step, py::array_t<uint8_t, py::array::c_style> data,
                          py::array_t<int64_t, py::array::c_style> off, int nthreads, uint32_t lds_bytes,
                          std::optional<py::array_t<uint8_t, py::array::c_style>> dead,
-                         std::optional<py::array_t<uint32_t, py::array::c_style>> line_stats) {
+                         std::optional<py::array_t<uint32_t, py::array::c_style>> line_stats,
+                         std::optional<py::array_t<uint32_t, py::array::c_style>> c4_words,
+                         std::optional<py::array_t<int64_t, py::array::c_style>> dict_loff,
+                         std::optional<py::array_t<uint32_t, py::array::c_style>> dict_ldata) {
     std::vector<int64_t> rec, no;
     std::vector<uint32_t> flags;
     std::string nd;
@@ -930,12 +981,30 @@ PYBIND11_MODULE(_tbhost, m) {
       if ((uint64_t)line_stats->size() < line_stats_buffer_words(off.data(), n)) throw std::runtime_error("line_stats too short");
       lp = line_stats->data();
     }
+    uint32_t* wp = nullptr;
+    if (c4_words) {
+      if ((int64_t)c4_words->size() < n) throw std::runtime_error("c4_words too short");
+      wp = c4_words->mutable_data();
+    }
+    DictLines dl;
+    if (dict_loff) {
+      if ((int64_t)dict_loff->size() < n || !dict_ldata) throw std::runtime_error("dict lines: operand shapes");
+      for (int64_t d = 0; d < n; ++d) {
+        const int64_t o = dict_loff->data()[d];
+        if (o >= 0 && (o >= (int64_t)dict_ldata->size() ||
+                       o + 1 + 2 * (int64_t)dict_ldata->data()[o] > (int64_t)dict_ldata->size()))
+          throw std::runtime_error("dict lines: record out of range");
+      }
+      dl.off = dict_loff->data();
+      dl.data = dict_ldata->data();
+    }
     {
       py::gil_scoped_release nogil;
-      emulate_c4(step, n, (const char*)data.data(), off.data(), nthreads, rec, nd, no, flags, lds_bytes, dp, lp);
+      emulate_c4(step, n, (const char*)data.data(), off.data(), nthreads, rec, nd, no, flags, lds_bytes, dp, lp, wp, dl);
     }
     return py::make_tuple(to_numpy(std::move(rec)), str_to_numpy(std::move(nd)), to_numpy(std::move(no)),
                           to_numpy(std::move(flags)));
   }, py::arg("step"), py::arg("data"), py::arg("offsets"), py::arg("nthreads") = 8, py::arg("lds_bytes") = 0,
-     py::arg("dead") = py::none(), py::arg("line_stats") = py::none());
+     py::arg("dead") = py::none(), py::arg("line_stats") = py::none(), py::arg("c4_words") = py::none(),
+     py::arg("dict_loff") = py::none(), py::arg("dict_ldata") = py::none());
 }

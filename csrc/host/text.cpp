@@ -13,6 +13,7 @@
 #include "../common/ucd_tables.inc"
 #include "../common/uax29.h"
 #include "../common/hash.h"
+#include "pipeline.h"
 
 namespace tb {
 
@@ -173,14 +174,25 @@ size_t count_nonoverlap(std::string_view s, std::string_view pat) {
 }
 
 bool has_dict_script(std::string_view s) {
+  // dictionary scripts start at U+0E00: only 3- and 4-byte sequences (lead bytes >= 0xE0) can hold
+  // one; eight bytes at a time are skipped while none of them is such a lead byte
   const uint8_t* b = (const uint8_t*)s.data();
-  uint32_t n = (uint32_t)s.size();
-  for (uint32_t i = 0; i < n;) {
-    if (b[i] < 0xE0) { i += b[i] < 0x80 ? 1 : 2; continue; }  // dictionary scripts are >= U+0E00
+  const uint32_t n = (uint32_t)s.size();
+  uint32_t i = 0;
+  while (i < n) {
+    if (i + 8 <= n) {
+      uint64_t v;
+      std::memcpy(&v, b + i, 8);
+      if (!(v & (v << 1) & (v << 2) & 0x8080808080808080ull)) {
+        i += 8;
+        continue;
+      }
+    }
+    if (b[i] < 0xE0) { ++i; continue; }
     int len;
-    uint32_t c = utf8_decode(b, i, n, &len);
+    const uint32_t c = utf8_decode(b, i, n, &len);
     if (props_of(c) & P_DICT) return true;
-    i += len;
+    i += (uint32_t)len;
   }
   return false;
 }
@@ -259,6 +271,152 @@ static bool has_word_char(std::string_view t) {
     i += len;
   }
   return false;
+}
+
+namespace {
+// any byte >= 0xE0 in [b, b + n): the lead bytes of the 3- and 4-byte sequences (dictionary
+// scripts start at U+0E00); eight bytes per step (bit 7 of a byte & its bits 6 and 5)
+bool any_e0(const uint8_t* b, size_t n) {
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t v;
+    std::memcpy(&v, b + i, 8);
+    if (v & (v << 1) & (v << 2) & 0x8080808080808080ull) return true;
+  }
+  for (; i < n; ++i)
+    if (b[i] >= 0xE0) return true;
+  return false;
+}
+bool valid_utf8(const uint8_t* b, size_t n) {
+  for (size_t i = 0; i < n;) {
+    const uint8_t c = b[i];
+    size_t len;
+    uint32_t cp;
+    if (c < 0x80) { ++i; continue; }
+    if (c >= 0xC2 && c <= 0xDF) { len = 2; cp = c & 0x1F; }
+    else if (c >= 0xE0 && c <= 0xEF) { len = 3; cp = c & 0x0F; }
+    else if (c >= 0xF0 && c <= 0xF4) { len = 4; cp = c & 0x07; }
+    else return false;
+    if (i + len > n) return false;
+    for (size_t k = 1; k < len; ++k) {
+      if ((b[i + k] & 0xC0) != 0x80) return false;
+      cp = (cp << 6) | (b[i + k] & 0x3F);
+    }
+    if ((len == 3 && cp < 0x800) || (len == 4 && (cp < 0x10000 || cp > 0x10FFFF)) ||
+        (cp >= 0xD800 && cp <= 0xDFFF))
+      return false;
+    i += len;
+  }
+  return true;
+}
+}  // namespace
+
+void dict_word_marks(const uint8_t* data, const int64_t* off, int64_t ndocs, int nthreads,
+                     std::vector<int64_t>& moff, std::vector<uint32_t>& bits) {
+  moff.assign(ndocs, -1);
+  std::vector<std::vector<uint32_t>> per(ndocs);
+  parallel_for(ndocs, nthreads, [&](int64_t a, int64_t e) {
+    for (int64_t d = a; d < e; ++d) {
+      const uint8_t* b = data + off[d];
+      const size_t n = (size_t)(off[d + 1] - off[d]);
+      if (!any_e0(b, n)) continue;
+      const std::string_view s((const char*)b, n);
+      if (!has_dict_script(s) || !valid_utf8(b, n)) continue;
+      uint32_t C = 0, Cdict = 0;
+      for (size_t i = 0; i < n;) {
+        int len;
+        const uint32_t c = utf8_decode(b, (uint32_t)i, (uint32_t)n, &len);
+        ++C;
+        Cdict += (props_of(c) & P_DICT) ? 1u : 0u;
+        i += (size_t)len;
+      }
+      // mostly dictionary-script text (a CJK or Thai document): no marks — in a pipeline for other
+      // languages the language gate filters it before any segmentation, and segmenting all of it
+      // by dictionary costs the host more than the rare survivor's CPU path
+      if (2 * Cdict > C) continue;
+      const uint32_t mw = ((C + 1 + 63) / 64) * 2;
+      std::vector<uint32_t>& m = per[d];
+      m.assign(2 * (size_t)mw, 0u);
+      uint32_t* hb = m.data();       // ICU's marks
+      uint32_t* hm = m.data() + mw;  // which positions take them
+      // lines ('\n'-separated) that hold a dictionary-script code point: ICU over that line alone
+      // (word breaks never look across a line feed: WB3a / WB3b), marks for its code points
+      // [line start, its '\n') — the '\n' itself and every other line keep the device's rules
+      uint32_t cp0 = 0;
+      size_t l0 = 0;
+      bool ok = true;
+      while (l0 <= n && ok) {
+        size_t l1 = l0;
+        while (l1 < n && b[l1] != '\n') ++l1;
+        uint32_t ncp = 0;
+        bool dict = false;
+        for (size_t i = l0; i < l1;) {
+          int len;
+          const uint32_t c = utf8_decode(b, (uint32_t)i, (uint32_t)n, &len);
+          dict |= (props_of(c) & P_DICT) != 0;
+          ++ncp;
+          i += (size_t)len;
+        }
+        if (dict) {
+          const std::string_view line((const char*)b + l0, l1 - l0);
+          const std::vector<uint32_t> br = icu_breaks(tl_icu.word, line);
+          uint32_t cp = 0;
+          size_t at = 0;
+          for (uint32_t o : br) {
+            if (o > line.size() || (o < line.size() && (line[o] & 0xC0) == 0x80)) { ok = false; break; }
+            for (; at < o; ++at) cp += (line[at] & 0xC0) != 0x80;
+            if (cp < ncp) hb[(cp0 + cp) >> 5] |= 1u << ((cp0 + cp) & 31);
+          }
+          for (uint32_t q = cp0; q < cp0 + ncp; ++q) hm[q >> 5] |= 1u << (q & 31);
+        }
+        cp0 += ncp + (l1 < n ? 1u : 0u);  // the line's code points and its '\n'
+        l0 = l1 + 1;
+      }
+      if (!ok || cp0 != C) m.clear();
+    }
+  });
+  size_t tot = 0;
+  for (int64_t d = 0; d < ndocs; ++d)
+    if (!per[d].empty()) { moff[d] = (int64_t)tot; tot += per[d].size(); }
+  bits.assign(tot, 0u);
+  for (int64_t d = 0; d < ndocs; ++d)
+    if (moff[d] >= 0) std::memcpy(bits.data() + moff[d], per[d].data(), per[d].size() * 4);
+}
+
+void dict_c4_lines(const uint8_t* text, const int64_t* off, int64_t ndocs, const int64_t* moff, bool citations,
+                   int nthreads, std::vector<int64_t>& loff, std::vector<uint32_t>& data) {
+  loff.assign(ndocs, -1);
+  std::vector<std::vector<uint32_t>> per(ndocs);
+  parallel_for(ndocs, nthreads, [&](int64_t a, int64_t e) {
+    for (int64_t d = a; d < e; ++d) {
+      if (moff[d] < 0) continue;
+      const std::string_view s((const char*)text + off[d], (size_t)(off[d + 1] - off[d]));
+      if (s.find('[') == std::string_view::npos) continue;
+      std::vector<uint32_t>& v = per[d];
+      const std::vector<std::string_view> lines = rust_lines(s);
+      v.reserve(1 + 2 * lines.size());
+      v.push_back((uint32_t)lines.size());
+      for (auto line : lines) {
+        const std::string_view cur = trim(line);
+        const std::string proc = citations ? remove_citations(cur) : std::string(cur);
+        uint32_t nw = 0, mx = 0;
+        // (Rules: word_breaks takes ICU for a line with a dictionary script, the UAX#29 rules for
+        // the others, which match ICU there — the device's own segmentation)
+        for (auto w : split_into_words(proc, SegBackend::Rules)) {
+          ++nw;
+          mx = std::max(mx, (uint32_t)count_chars(w));
+        }
+        v.push_back(nw);
+        v.push_back(mx);
+      }
+    }
+  });
+  size_t tot = 0;
+  for (int64_t d = 0; d < ndocs; ++d)
+    if (!per[d].empty()) { loff[d] = (int64_t)tot; tot += per[d].size(); }
+  data.assign(tot, 0u);
+  for (int64_t d = 0; d < ndocs; ++d)
+    if (loff[d] >= 0) std::memcpy(data.data() + loff[d], per[d].data(), per[d].size() * 4);
 }
 
 std::vector<std::string_view> split_into_words(std::string_view s, SegBackend be) {

@@ -43,6 +43,25 @@ bool starts_with(std::string_view s, std::string_view pre);
 size_t count_nonoverlap(std::string_view s, std::string_view pat);
 bool has_dict_script(std::string_view s);
 
+// Word-break marks of the documents that hold a dictionary-script code point (ICU4C word
+// segmentation, dictionary breaking included: the CPU oracle's words), for the device kernels,
+// which segment everything else themselves. ICU runs over the lines that hold such a code point
+// only. moff[d] = word offset of document d's record in `bits`, or -1 (no dictionary script,
+// mostly dictionary-script text, or not strictly valid UTF-8: then the device keeps sending the
+// document to the CPU path). A record is two bitmaps of mw = ((C + 1 + 63) / 64) * 2 words over
+// the code points [0, C] (UTF-8 lead bytes): ICU's marks (bit i = a boundary before code point i)
+// and the positions that take them (the rest keep the device's UAX#29 rules).
+// Documents are scanned in parallel on the native pool.
+void dict_word_marks(const uint8_t* data, const int64_t* off, int64_t ndocs, int nthreads,
+                     std::vector<int64_t>& moff, std::vector<uint32_t>& bits);
+// C4QualityFilter's per-line word statistics of the dictionary-script documents (moff[d] >= 0)
+// that hold a '[' (a possible citation): per Rust line of the text its processed form
+// remove_citations(trim(line)) (c4_filters.rs; `citations` false: trim(line)), its ICU word count
+// and its longest word in code points — what C4 pass A would segment on the device. loff[d] =
+// offset of [NL, nw_0, mx_0, nw_1, mx_1, ...] in `data`, or -1.
+void dict_c4_lines(const uint8_t* text, const int64_t* off, int64_t ndocs, const int64_t* moff, bool citations,
+                   int nthreads, std::vector<int64_t>& loff, std::vector<uint32_t>& data);
+
 // Segment boundaries as byte offsets, always including 0 and s.size() (for non-empty s).
 std::vector<uint32_t> word_breaks(std::string_view s, SegBackend be);
 std::vector<uint32_t> sentence_breaks(std::string_view s, SegBackend be);

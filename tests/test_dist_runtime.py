@@ -188,13 +188,14 @@ def test_block_kernels_reject_oversized_lds_slice():
     for lds, want_err in ((160 * 1024, True), (128 * 1024 + 16, True)):
         # (every launcher here returns before any HIP call when the slice is too large)
         rc = lib.tb_stage_analyze_blk(None, dummy, dummy, dummy, dummy, dummy, 1, 1, dummy, dummy, dummy, 0,
-                                      dummy, dummy, dummy, dummy, dummy, dummy, lds, None, None, None, 0, 0, 512, None, None, 0)
+                                      dummy, dummy, dummy, dummy, dummy, dummy, lds, None, None, None, 0, 0, 512, None, None, 0,
+                                      None, None, None)
         assert (rc != 0) == want_err
         rc = lib.tb_gr_dup_split(None, dummy, 0, dummy, 1, 6, 1, dummy, dummy, 0, dummy, dummy, dummy, dummy,
                                  dummy, dummy, lds, dummy)
         assert (rc != 0) == want_err
         rc = lib.tb_c4_pass_a_blk(None, dummy, dummy, dummy, dummy, 1, 1, dummy, dummy, dummy, 0, dummy, dummy,
-                                  dummy, dummy, dummy, dummy, dummy, lds, None, None, None)
+                                  dummy, dummy, dummy, dummy, dummy, lds, None, None, None, None, None, None)
         assert (rc != 0) == want_err
 
 

@@ -140,11 +140,12 @@ def test_gopher_repetition_records_equal_oracle_on_repetitive_text(host):
     assert with_dups > 100
 
 
-def test_mixed_script_delegation_is_overlapped_and_exact():
-    """Dictionary-script documents (5 % with a CJK / Thai snippet, 1 % CJK): process_many recomputes
-    the delegated ones on the engine's delegation thread while later batches are resolved; the
-    merged results equal the CPU oracle batch for batch, and documents the language gate already
-    filtered (the CJK ones) are not delegated."""
+def test_mixed_script_delegation_is_overlapped_and_exact(monkeypatch):
+    """Dictionary-script documents (5 % with a CJK / Thai snippet, 1 % CJK) without host word marks
+    (TB_DICT_MARKS=0): process_many recomputes the delegated ones on the engine's delegation thread
+    while later batches are resolved; the merged results equal the CPU oracle batch for batch, and
+    documents the language gate already filtered (the CJK ones) are not delegated."""
+    monkeypatch.setenv("TB_DICT_MARKS", "0")
     cfg = load_pipeline_config("config/bench_pipeline.yaml")
     batches = [synth.pack(synth.make_corpus(600, 800, seed=40 + s, mixed_script=True)) for s in range(3)]
     emu = Engine(cfg, backend="emulate", nthreads=4)
@@ -207,7 +208,7 @@ def test_split_tasks_equal_one_pass_and_fit_the_reservation(host):
         assert not (f & 2).any()
 
 
-def test_language_id_after_c4_is_recomputed_for_delegated_documents(tmp_path):
+def test_language_id_after_c4_is_recomputed_for_delegated_documents(tmp_path, monkeypatch):
     """A LanguageDetectionFilter placed after C4QualityFilter reads the rewritten text. For a
     delegated (dictionary-script) document the device's rewritten text is not the CPU path's, so
     its language-ID record must not be reused: the outputs equal the CPU oracle on a mixed-script
@@ -220,6 +221,7 @@ def test_language_id_after_c4_is_recomputed_for_delegated_documents(tmp_path):
         "  - {type: LanguageDetectionFilter, min_confidence: 0.5, allowed_languages: [dan, eng, swe, nob, nno]}\n"
     p = tmp_path / "lid_after_c4.yaml"
     p.write_text(cfg_text)
+    monkeypatch.setenv("TB_DICT_MARKS", "0")  # dictionary-script documents go to the CPU path
     cfg = load_pipeline_config(str(p))
     assert [s.type for s in cfg.pipeline][-1] == "LanguageDetectionFilter"
     texts = synth.make_corpus(900, 800, seed=77, mixed_script=True)
@@ -234,3 +236,39 @@ def test_language_id_after_c4_is_recomputed_for_delegated_documents(tmp_path):
         np.testing.assert_array_equal(got.status, ref.status)
         assert got.reasons == ref.reasons
         assert outputs(got) == outputs(ref)
+
+
+@pytest.mark.parametrize("cfg_path", ["config/bench_pipeline.yaml", "config/pipeline_config.yaml",
+                                      "config/bench_pipeline_survivor.yaml"])
+def test_dictionary_scripts_stay_on_device_and_equal_oracle(cfg_path):
+    """Dictionary-script documents (CJK / Thai snippets and CJK documents) keep their analysis on the
+    device: the host supplies ICU word marks of the original text (stage kernels), ICU per-line word
+    statistics for documents with citations (C4 pass A) and the rewrite's word count comes from C4
+    (FineWeb after C4). No document is delegated, and records, statuses, reasons and outputs equal
+    the CPU ICU oracle."""
+    import yaml
+
+    cfg = load_pipeline_config(cfg_path)
+    if any(s.type == "TokenCounter" for s in cfg.pipeline):
+        raw = yaml.safe_load(open(cfg_path))
+        raw["pipeline"] = [s for s in raw["pipeline"] if s.get("type") != "TokenCounter"]
+        from textblaster_amd.config.pipeline import parse_pipeline_config
+
+        cfg = parse_pipeline_config(raw)
+    texts = synth.make_corpus(2500, 900, seed=314, mixed_script=True)
+    rng = np.random.default_rng(5)
+    # cited dictionary-script lines, Thai, kana / han runs next to citations and line edges
+    texts += ["日本語のテキストです[1]。東京は日本の首都です。\nこれは二行目です [2, 3]。",
+              "ภาษาไทย [4] สวัสดีครับ.\n\nประเทศไทย is a country [5].",
+              "Mixed 中文分词测试 text [6] with more words here. " * 8]
+    data, off = synth.pack(texts)
+    emu = Engine(cfg, backend="emulate", nthreads=4, keep_reasons=True)
+    cpu = Engine(cfg, backend="cpu", segmentation="icu", nthreads=4, keep_reasons=True)
+    a, b = emu.process(data, off), cpu.process(data, off)
+    n_dict = sum(1 for t in texts if emu.h.has_dict_script(t))
+    assert n_dict > 100
+    assert a.n_delegated == 0
+    np.testing.assert_array_equal(a.status, b.status)
+    np.testing.assert_array_equal(a.fail_step, b.fail_step)
+    assert a.reasons == b.reasons
+    assert outputs(a) == outputs(b)

@@ -157,3 +157,39 @@ def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
     assert not bad, [(k, texts[k][:80]) for k in bad[:5]]
     lens = np.diff(off)
     assert np.count_nonzero(lens > 4500) >= 30
+
+
+@pytest.mark.parametrize("cfg_name", ["bench_pipeline.yaml", "bench_pipeline_survivor.yaml"])
+def test_device_dictionary_scripts_equal_oracle(cfg_name):
+    """Mixed-script slice of the GPU-vs-ICU differential: CJK / Thai snippets,
+    CJK documents, dictionary-script lines with citations, long documents (workgroup kernels) with
+    snippets. The device keeps every one of them (host ICU word marks for the stage kernels, ICU line
+    statistics for C4 pass A, the rewrite's word count for FineWeb): nothing is delegated, and the
+    results equal the CPU ICU oracle byte for byte."""
+    import numpy as np
+
+    from textblaster_amd.config import load_pipeline_config
+    from textblaster_amd.pipeline.engine import Engine
+
+    from test_emulated_device_path import outputs
+
+    cfg = load_pipeline_config(os.path.join(REPO, "config", cfg_name))
+    texts = synth.make_corpus(4000, 1024, seed=2718, mixed_script=True)
+    rng = np.random.default_rng(11)
+    for k, s in enumerate(np.geomspace(5000, 60000, 12)):
+        t = synth.make_doc(rng, ["eng", "dan", "swe", "nob", "nno"][k % 5], int(s))
+        cut = len(t) // 2
+        texts.append(t[:cut] + " " + synth.CJK_SNIPPETS[k % len(synth.CJK_SNIPPETS)] + " [3] " + t[cut:])
+    texts += ["日本語のテキストです[1]。東京は日本の首都です。\nこれは二行目です [2, 3]。",
+              "ภาษาไทย [4] สวัสดีครับ.\n\nประเทศไทย is a country [5].",
+              "Mixed 中文分词测试 text [6] with more words here. " * 8]
+    data, off = synth.pack(texts)
+    eng = Engine(cfg, backend="cuda", keep_reasons=True)
+    a = eng.process(data, off)
+    b = Engine(cfg, backend="cpu", segmentation="icu", keep_reasons=True).process(data, off)
+    assert sum(1 for t in texts if eng.h.has_dict_script(t)) > 200
+    assert a.n_delegated == 0
+    np.testing.assert_array_equal(a.status, b.status)
+    np.testing.assert_array_equal(a.fail_step, b.fail_step)
+    assert a.reasons == b.reasons
+    assert outputs(a) == outputs(b)

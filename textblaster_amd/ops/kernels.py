@@ -22,22 +22,23 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 21
+ABI_VERSION = 23
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32, _P,
-                         _P, _P],
+                         _P, _P, _P, _P, _P],
     "tb_gr_split_wave": [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _I32, _P,
                          _I32],
-    "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _P, _P],
+    "tb_c4_pass_a": [_P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _P, _P,
+                     _P, _P, _P],
     "tb_stage_analyze_blk": [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P,
-                             _U32, _P, _P, _P, _I32, _U32, _I32, _P, _P, _I32],
+                             _U32, _P, _P, _P, _I32, _U32, _I32, _P, _P, _I32, _P, _P, _P],
     "tb_sizeof_pre_doc": [],
     "tb_pre_decode": [_P, _P, _P, _P, _I32, _P, _P, _U32, _P, _P, _P, _P, _P],
     "tb_gr_dup_split": [_P, _P, _I32, _P, _I32, _I32, _I32, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P],
     "tb_sizeof_gr_export": [],
     "tb_c4_pass_a_blk": [_P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _P,
-                         _P],
+                         _P, _P, _P, _P],
     "tb_gate": [_P, _P, _P, _I32, _I32, _P, _P, _I32],
     "tb_sizeof_gate": [],
     "tb_resolve": [_P, _P, _P, _I32, _I32, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P],
@@ -73,6 +74,13 @@ _SIGS = {
     "tb_sizeof_stage": [],
     "tb_sizeof_c4": [],
 }
+
+
+def _dict_ptrs(dict_in):
+    """(moff, bits, words) device arrays of docproc.h DictIn as three pointers (0 for None)."""
+    if dict_in is None:
+        return 0, 0, 0
+    return tuple(_ptr(a) for a in dict_in)
 
 
 # docproc.h PreDoc (checked against tb_sizeof_pre_doc)
@@ -175,8 +183,10 @@ class Kernels:
         return self._pw, self._pw_n
 
     def stage_analyze(self, plan, stage, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, flags,
-                      lds_bytes=0, prof=None, waves=0, nblocks=0, dead=None, line_stats=None, gr_export=None):
-        """k_stage_analyze_wave; ``line_stats`` (uint32, >= 4 * (total bytes / 8 + 16 ndocs) + 16): the
+                      lds_bytes=0, prof=None, waves=0, nblocks=0, dead=None, line_stats=None, gr_export=None,
+                      dict_in=None):
+        """k_stage_analyze_wave; ``dict_in`` = (moff, bits, words) device arrays or None each
+        (docproc.h DictIn: the word sources of dictionary-script documents); ``line_stats`` (uint32, >= 4 * (total bytes / 8 + 16 ndocs) + 16): the
         C4 line export (docproc.h StageOut::line_stats), document d at 4 * (off[d] / 8 + 16 d).
         ``gr_export`` (zeroed, >= nblocks descriptors): split mode, every launched document exports
         its word arrays and gr_split_wave finishes its n-gram orders."""
@@ -187,7 +197,7 @@ class Kernels:
             self.stream(), plan.data_ptr(), stage.data_ptr(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs,
             scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
             t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof), waves, nblocks,
-            _ptr(dead), _ptr(line_stats), _ptr(gr_export))
+            _ptr(dead), _ptr(line_stats), _ptr(gr_export), *_dict_ptrs(dict_in))
         _check(rc, "tb_stage_analyze")
 
     def gr_export_wave_bytes(self, n_docs: int) -> int:
@@ -214,7 +224,7 @@ class Kernels:
 
     def stage_analyze_blk(self, plan, stage, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n,
                           rec, flags, lds_bytes=0, prof=None, dead=None, gr_export=None, n_split=0, split_bytes=0,
-                          threads=512, line_stats=None, pre=None, n_pre=0):
+                          threads=512, line_stats=None, pre=None, n_pre=0, dict_in=None):
         """k_stage_analyze_blk; ``gr_export`` (zeroed, >= n_split descriptors): the first n_split
         launch positions longer than ``split_bytes`` export their word arrays (split mode)."""
         t = self.tabs
@@ -227,7 +237,7 @@ class Kernels:
             nlong, ndocs, scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(),
             t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof),
             _ptr(dead), _ptr(gr_export), n_split if gr_export is not None else 0, split_bytes, int(threads),
-            _ptr(line_stats), _ptr(pre), int(n_pre) if pre is not None else 0)
+            _ptr(line_stats), _ptr(pre), int(n_pre) if pre is not None else 0, *_dict_ptrs(dict_in))
         _check(rc, "tb_stage_analyze_blk")
 
     def pre_decode(self, bytes_, off, perm_pre, npre, dead, pre, tiles_max, cnt):
@@ -269,13 +279,14 @@ class Kernels:
         _check(rc, "tb_gr_dup_split")
 
     def c4_pass_a_blk(self, c4, bytes_, off, perm_long, nlong, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags,
-                      lds_bytes=0, prof=None, dead=None, line_stats=None):
+                      lds_bytes=0, prof=None, dead=None, line_stats=None, c4_words=None, dict_lines=None):
         t = self.tabs
+        dl = dict_lines or (None, None)
         rc = self.lib.tb_c4_pass_a_blk(
             self.stream(), c4.data_ptr(), bytes_.data_ptr(), off.data_ptr(), perm_long.data_ptr(), nlong, ndocs,
             scratch.data_ptr(), scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(),
             t[2].data_ptr(), t[3].data_ptr(), rec.data_ptr(), src.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof),
-            _ptr(dead), _ptr(line_stats))
+            _ptr(dead), _ptr(line_stats), _ptr(c4_words), _ptr(dl[0]), _ptr(dl[1]))
         _check(rc, "tb_c4_pass_a_blk")
 
     def badwords_match(self, bytes_, off, ndocs, table, fold, matched, root=None, cjk=None, root0=-1, cjk0=0,
@@ -359,16 +370,20 @@ class Kernels:
         _check(rc, "tb_langid_mfma")
 
     def c4_pass_a(self, c4, bytes_, off, perm, ndocs, scratch, scratch_off, pw, pw_n, rec, src, flags, lds_bytes=0,
-                  prof=None, nblocks=0, dead=None, line_stats=None):
+                  prof=None, nblocks=0, dead=None, line_stats=None, c4_words=None, dict_lines=None):
         """k_c4_pass_a; ``line_stats``: the line export of a stage over the same content version
         (trimmed spans, word counts and longest words of the Rust lines: documents without a
-        citation skip decode, lines and words when split_paragraph is set)."""
+        citation skip decode, lines and words when split_paragraph is set). ``c4_words`` (uint32
+        per document, preset to 0xFFFFFFFF): the rewrite's word count on the export path.
+        ``dict_lines`` = (offsets int64, data uint32): host ICU line statistics of dictionary-script
+        documents (docproc.h DictLines)."""
         t = self.tabs
+        dl = dict_lines or (None, None)
         rc = self.lib.tb_c4_pass_a(
             self.stream(), c4.data_ptr(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs, scratch.data_ptr(),
             scratch_off.data_ptr(), pw.data_ptr(), pw_n, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
             t[3].data_ptr(), rec.data_ptr(), src.data_ptr(), flags.data_ptr(), lds_bytes, _ptr(prof), nblocks,
-            _ptr(dead), _ptr(line_stats))
+            _ptr(dead), _ptr(line_stats), _ptr(c4_words), _ptr(dl[0]), _ptr(dl[1]))
         _check(rc, "tb_c4_pass_a")
 
     def c4_pass_b(self, bytes_, off, ndocs, scratch, scratch_off, src, new_off, out):

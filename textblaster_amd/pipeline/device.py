@@ -154,6 +154,19 @@ def trailing_token_counters(plan: ExecPlan) -> List[int]:
     return out[::-1]
 
 
+def dict_marks_wanted(plan: ExecPlan, steps_native) -> bool:
+    """Does a stage over the original text segment words (GopherQuality / GopherRepetition /
+    FineWeb)? Then the host computes ICU word marks for the dictionary-script documents of every
+    batch (text.h dict_word_marks) and they stay on the device (TB_DICT_MARKS=0: CPU path)."""
+    import os
+
+    if os.environ.get("TB_DICT_MARKS", "1") in ("", "0"):
+        return False
+    kinds = ("GopherQualityFilter", "GopherRepetitionFilter", "FineWebQualityFilter")
+    return any(plan.stage_version[s] == 0 and any(plan.steps[i].type in kinds for i in idx)
+               for s, idx in enumerate(plan.stages))
+
+
 def resolve_entries(plan: ExecPlan, stage_layout):
     """K16 plan: (entries, c4_versions) over every pipeline step in order — entries are (step,
     record slot, prefix) with slots = [stage 0 .. stage S-1, C4 step 0 ..] — or None when a step
@@ -407,12 +420,16 @@ class DeviceRunner:
     DEFAULT_PRE_DOC_BYTES = 262144
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None, max_batch_bytes: int = 384 << 20,
-                 token_counters=None, slots: Optional[int] = None):
+                 token_counters=None, slots: Optional[int] = None, host_threads: int = 8):
         import os
 
         from ..ops import hiprt
 
         self.rt = hiprt
+        self.host_threads = max(1, int(host_threads))
+        # dictionary-script documents: word marks from the host's ICU segmentation (stage kernels
+        # of the original text) instead of the CPU path for the whole document
+        self.dict_marks = dict_marks_wanted(plan, steps_native)
         with tracing.trace_range("tb.init.hip_context"):
             self.device = hiprt.parse_device(device)
             if self.device >= hiprt.device_count():
@@ -905,12 +922,34 @@ class DeviceRunner:
             sd, si = bw_segments(lens, self.c4_growth * v, BW_SEG_BYTES)
             if len(sd):
                 bw_arrays += [((v, "seg_doc"), sd), ((v, "seg_idx"), si)]
+        dict_arrays = []
+        dict_c4_keys = []  # C4 steps with host line statistics (their two arrays follow the marks)
+        if self.dict_marks and ndocs:
+            with tracing.trace_range("tb.dict_marks"):
+                moff, mbits = h.dict_word_marks(data, off, self.host_threads)
+            if len(mbits):
+                dict_arrays = [moff, mbits]
+                metrics.DICT_MARKED_DOCS_TOTAL.inc(int(np.count_nonzero(moff >= 0)))
+                # C4 steps on the original text: the per-line ICU word statistics of the marked
+                # documents that may hold a citation (their C4 pass segments processed lines)
+                for i in self.plan.c4_steps:
+                    if self.plan.steps[i].version_in == 0:
+                        lo, ld = h.dict_c4_lines(data, off, moff, bool(self.steps[i].remove_citations),
+                                                 self.host_threads)
+                        if len(ld):
+                            dict_c4_keys.append(i)
+                            dict_arrays += [lo, ld]
         with tracing.trace_range("tb.stage_h2d"):
             staged_views, staged = self._stage_inputs(
                 slot, [data if len(data) else np.zeros(1, np.uint8), off, perm, scratch_off]
-                + [np.ascontiguousarray(a) for _, a in bw_arrays], direct_keep)
+                + [np.ascontiguousarray(a) for _, a in bw_arrays] + dict_arrays, direct_keep)
         d_bytes, d_off, d_perm, d_soff = staged_views[:4]
-        bw_dev = {key: d for (key, _), d in zip(bw_arrays, staged_views[4:])}
+        bw_dev = {key: d for (key, _), d in zip(bw_arrays, staged_views[4:4 + len(bw_arrays)])}
+        # per content version: the word sources of its dictionary-script documents (DictIn)
+        nd_arr = len(dict_arrays)
+        dv = staged_views[len(staged_views) - nd_arr:] if nd_arr else []
+        dict_in = {0: (dv[0], dv[1], None)} if nd_arr else {}
+        dict_lines = {i: (dv[2 + 2 * k], dv[3 + 2 * k]) for k, i in enumerate(dict_c4_keys)}
         scratch = self._scratch_for(slot, int(scratch_off[-1]))
         # grows (new tensor, on this slot's stream) only for documents over 2 MB; the batch keeps a
         # reference to the table it used, so the other slot's kernels never see it freed
@@ -1004,7 +1043,8 @@ class DeviceRunner:
                                                      self.lds_bytes_blk, prof, skip,
                                                      gx[a0 * esz:] if (gx is not None and ns) else None, ns,
                                                      self.split_doc_bytes, thr, ls_out,
-                                                     pre if with_pre else None, a1 - a0 if with_pre else 0)
+                                                     pre if with_pre else None, a1 - a0 if with_pre else 0,
+                                                     dict_in.get(ver))
                         if n_split:
                             gr_pos, n_tasks = self.gr_split[s]
                             cur = rt.empty(1, np.uint32)
@@ -1033,7 +1073,8 @@ class DeviceRunner:
                     with self._ktimed(keep, f"stage{s}"):
                         self.k.stage_analyze(self.plan_t, self.stage_ts[s], vb, vo, d_perm[n_long:], ndocs,
                                              scratch, d_soff[n_long:], pw, pw_n, rec, flags,
-                                             self.lds_bytes, prof, self.stage_waves, nw, skip, ls_out, gxw)
+                                             self.lds_bytes, prof, self.stage_waves, nw, skip, ls_out, gxw,
+                                             dict_in.get(ver))
                         if gxw is not None:
                             gr_pos, n_tasks = self.gr_split[s]
                             # wave documents longer than ngram_big_bytes (a prefix: perm is longest
@@ -1060,6 +1101,13 @@ class DeviceRunner:
                 rec = rt.zeros(7 * ndocs, np.int64)
                 src = rt.zeros(2 * ndocs, np.int64)
                 new_off = rt.zeros(ndocs + 1, np.int64)
+                # the rewrite's word count per document (kNoWords unless C4 pass A's export path
+                # set it): the word source of the next version's dictionary-script documents
+                c4w = None
+                if self.dict_marks and ver in dict_in:
+                    c4w = rt.empty(ndocs, np.uint32).fill_(0xFF)
+                    keep.append(c4w)
+                    dict_in[ver + 1] = (None, None, c4w)
                 cap = vlen + self.c4_growth * ndocs + 16  # device rewrites never grow more (kC4MaxGrowth)
                 out = rt.empty(cap, np.uint8)
                 ev_main = self._record(main)
@@ -1077,14 +1125,14 @@ class DeviceRunner:
                     with rt.stream(slot.s_c4blk):
                         self.k.c4_pass_a_blk(self.c4_ts[i], vb, vo, d_perm[:n_long], n_long, ndocs, c4_scratch,
                                              d_soff, pw, pw_n, rec, src, flags, self.lds_bytes_blk, prof, skip,
-                                             lstats)
+                                             lstats, c4w, dict_lines.get(i))
                         ev_c4blk = self._record(slot.s_c4blk)
                         keep.append(ev_c4blk)
                 with rt.stream(slot.s_c4), self._ktimed(keep, f"c4_step{i}"):
                     if n_long < ndocs:
                         self.k.c4_pass_a(self.c4_ts[i], vb, vo, d_perm[n_long:], ndocs, c4_scratch, d_soff[n_long:], pw,
                                          pw_n, rec, src, flags, self.lds_bytes_c4, prof, ndocs - n_long, skip,
-                                         lstats)
+                                         lstats, c4w, dict_lines.get(i))
                     if ev_c4blk is not None:
                         slot.s_c4.wait_event(ev_c4blk)
                     rt.scan_strided_i64(src[1:], 2, ndocs, new_off[1:])
@@ -1220,6 +1268,7 @@ class EmulatedRunner:
         self.bpe = []
         if self.resolve_blob is not None and os.environ.get("TB_DEVICE_TOKENS", "1") not in ("", "0"):
             self.bpe = list(token_counters or [])
+        self.dict_marks = dict_marks_wanted(plan, steps_native)
 
     def run(self, data: np.ndarray, off: np.ndarray, bw: Optional[Dict[int, BwInput]] = None) -> DeviceResult:
         import time
@@ -1234,6 +1283,20 @@ class EmulatedRunner:
         dead = np.zeros(ndocs, dtype=np.uint8) if self.gates else None
         lid_rec = {}
         lstats = {}  # content version -> the C4 line export buffer (as on the device)
+        # content version -> the word sources of its dictionary-script documents (DeviceRunner)
+        dict_in = {}
+        if self.dict_marks and ndocs:
+            moff, mbits = h.dict_word_marks(data, off, self.nthreads)
+            if len(mbits):
+                dict_in[0] = dict(dict_moff=moff, dict_bits=mbits)
+        dict_lines = {}
+        if 0 in dict_in:
+            for i in self.plan.c4_steps:
+                if self.plan.steps[i].version_in == 0:
+                    lo, ld = h.dict_c4_lines(data, off, dict_in[0]["dict_moff"], bool(self.steps[i].remove_citations),
+                                             self.nthreads)
+                    if len(ld):
+                        dict_lines[i] = dict(dict_loff=lo, dict_ldata=ld)
         for p, (kind, x) in enumerate(self.passes):
             skip = dead if p > 0 else None
             if kind == "lid":
@@ -1253,16 +1316,21 @@ class EmulatedRunner:
                 if self.line_stats_stage.get(sv) == x:
                     ls = lstats[sv] = np.empty(h.line_stats_words(vo), dtype=np.uint32)
                 rec, fl = h.emulate_stage(self.steps, self.plan.stages[x], vd, vo, self.nthreads, self.lid, 0, skip,
-                                          line_stats=ls)
+                                          line_stats=ls, **dict_in.get(sv, {}))
                 if x in lid_rec:
                     for k, width, prefix in self.stage_layout[x][1]:
                         if k == KIND_LANGID:
                             rec[prefix * ndocs:(prefix + width) * ndocs] = lid_rec[x][prefix * ndocs:(prefix + width) * ndocs]
                 stage_recs[x] = rec
             else:
-                vd, vo = versions[self.plan.steps[x].version_in]
+                vin = self.plan.steps[x].version_in
+                vd, vo = versions[vin]
+                c4w = None
+                if vin in dict_in:
+                    c4w = np.full(ndocs, 0xFFFFFFFF, dtype=np.uint32)
+                    dict_in[self.plan.steps[x].version_out] = dict(dict_words=c4w)
                 rec, nd, no, fl = h.emulate_c4(self.steps[x], vd, vo, self.nthreads, 0, skip,
-                                               line_stats=lstats.get(self.plan.steps[x].version_in))
+                                               line_stats=lstats.get(vin), c4_words=c4w, **dict_lines.get(x, {}))
                 c4_recs[x] = rec
                 versions[self.plan.steps[x].version_out] = (nd, no)
             flags |= fl

@@ -194,7 +194,7 @@ class Engine:
             with tracing.trace_range("tb.init.device_runner"):
                 self.device_runner = DeviceRunner(self.steps, self.plan, device or "cuda", self.langid,
                                                   max_batch_bytes=self.max_batch_bytes, token_counters=token_counters,
-                                                  slots=slots)
+                                                  slots=slots, host_threads=self.nthreads)
 
     # ------------------------------------------------------------------------------------------
     def process(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None,

@@ -68,6 +68,9 @@ GPU_KERNEL_SECONDS = Histogram("tb_gpu_kernel_seconds", "Per-batch device time o
 DELEGATED_DOCS_TOTAL = Counter("tb_cpu_delegated_docs_total",
                                "Documents recomputed on the CPU oracle path (dictionary scripts, collisions).",
                                registry=REGISTRY)
+DICT_MARKED_DOCS_TOTAL = Counter("tb_dict_marked_docs_total",
+                                 "Dictionary-script documents kept on the device with host ICU word marks.",
+                                 registry=REGISTRY)
 BATCH_FAILURES_TOTAL = Counter("tb_batch_failures_total", "Batches whose device work failed (then recovered).",
                                ["error"], registry=REGISTRY)
 CPU_FALLBACK_DOCS_TOTAL = Counter("tb_cpu_fallback_docs_total",

@@ -112,17 +112,26 @@ def test_device_gate_matches_host_gate(host, corpus, runner_parts):
     assert len(diff) <= max(2, len(corpus) // 500), diff[:10]
 
 
-def test_dictionary_scripts_are_flagged(host, runner_parts):
-    """A dictionary-script document goes to the CPU path only when it reaches a segmentation pass:
-    the CJK document fails the language gate on the device (exact records, not delegated), the
-    Danish document with a CJK snippet passes it and is flagged by the stage kernel's decode."""
-    _, _, _, runner, _ = runner_parts
+def test_dictionary_scripts_are_flagged(host, runner_parts, monkeypatch):
+    """A dictionary-script document leaves the device only when it reaches a segmentation pass
+    without host word marks: the CJK document fails the language gate on the device (exact records,
+    not delegated); the Danish document with a CJK snippet passes it and stays on the device with
+    the host's ICU marks of its snippet line, or (TB_DICT_MARKS=0) is flagged by the stage
+    kernel's decode."""
+    from textblaster_amd.pipeline.device import DeviceRunner
+
+    _, steps, plan, runner, lid = runner_parts
     rng = np.random.default_rng(5)
     dan = synth.make_doc(rng, "dan", 1500)
     data, off = synth.pack(["日本語のテキストです。", "plain english text here.", dan[:200] + " 日本語 " + dan[200:]])
     res = runner.run(data, off)
     assert res.flags[0] == 0 and res.dead[0] != 0
     assert res.flags[1] == 0
+    assert res.flags[2] == 0 and runner.dict_marks
+    monkeypatch.setenv("TB_DICT_MARKS", "0")
+    nomarks = DeviceRunner(steps, plan, runner.device, lid)
+    res = nomarks.run(data, off)
+    assert res.flags[0] == 0 and res.flags[1] == 0
     assert res.flags[2] != 0
 
 
@@ -294,6 +303,9 @@ def test_pre_decoded_long_documents_match_host(host, runner_parts, monkeypatch):
     from textblaster_amd.pipeline.device import DeviceRunner
 
     cfg, steps, plan, _, lid = runner_parts
+    # (the pre-pass documents take no host word marks: compare both runs with the CPU path for
+    # dictionary scripts)
+    monkeypatch.setenv("TB_DICT_MARKS", "0")
     rng = np.random.default_rng(3)
     langs = ["eng", "dan", "swe", "nob", "nno"]
     texts = [synth.make_doc(rng, langs[k % 5], int(s)) for k, s in enumerate(np.geomspace(66000, 400000, 8))]

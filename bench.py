@@ -74,6 +74,9 @@ def main():
     ap.add_argument("--backend", default="cuda", choices=["cuda", "cpu", "emulate"])
     ap.add_argument("--segmentation", default="icu", help="CPU backend segmentation (icu|rules)")
     ap.add_argument("--threads", type=int, default=None)
+    ap.add_argument("--ar1-every", type=int, default=1,
+                    help="all-reduce the counter vector every N steps (0: only the final totals)")
+    ap.add_argument("--ar1-window", type=int, default=4, help="outstanding async all-reduces before a wait")
     args = ap.parse_args()
     if args.steps < 1 or args.warmup < 0 or args.docs_per_step < 1 or args.gpus < 1:
         ap.error("--steps must be >= 1, --warmup >= 0, --docs-per-step >= 1 and --gpus >= 1")
@@ -167,9 +170,9 @@ def main():
     t0 = time.perf_counter()
     n_done = 0
     tsum: dict = {}
-    # AR1 every TB_AR1_EVERY steps (default every step; 0: only the final totals reduction)
-    ar1_every = int(os.environ.get("TB_AR1_EVERY", "1"))
-    ar1_window = int(os.environ.get("TB_AR1_WINDOW", "4"))
+    # AR1 every --ar1-every steps (default every step; 0: only the final totals reduction)
+    ar1_every = args.ar1_every
+    ar1_window = args.ar1_window
     ar1s = collections.deque()
     for res in eng.process_many(feed(args.steps, args.warmup)):
         step = np.asarray([res.n_docs, res.n_kept, res.n_excluded, len(res.error_rows)], dtype=np.int64)
@@ -178,7 +181,7 @@ def main():
         step_filtered += np.bincount(fs, minlength=nsteps)[:nsteps]
         # AR1 once per step: the global counter vector (what rank 0's /metrics serves), reduced
         # over RCCL while the next steps run; the main thread (which also assembles outputs)
-        # only waits once more than TB_AR1_WINDOW reductions are outstanding
+        # only waits once more than --ar1-window reductions are outstanding
         if ar1_every and n_done % ar1_every == 0:
             ar1s.append(ctx.all_reduce_sum_async(step))
         while ar1s and (len(ar1s) > ar1_window or ar1s[0].done()):

@@ -1805,7 +1805,7 @@ TB_HD void gr_dup_one_order(DocCtx<P>& x, const DevStep& ds, int t, const GrExpo
 // byte, as decode() defines them) of the first kLidMaxCps code points, plus the virtual end
 // position, emits the 1..4-grams ending there (lid_grams_at); their int16 logit rows are summed
 // exactly. Neighbouring letters are found by stepping back to the previous lead bytes, so no
-// per-code-point arrays are needed. The device runs its own kernel for this (k_langid_features,
+// per-code-point arrays are needed. The device runs its own kernel for this (k_langid_mfma,
 // same sums); this version runs inside the stage emulation on the host.
 template <class P, int D>
 TB_HD void langid_sums(DocCtx<P>& x, const uint8_t* b, uint32_t n, const LidTables& lt, int64_t* sums) {
@@ -1836,8 +1836,7 @@ TB_HD void langid_sums(DocCtx<P>& x, const uint8_t* b, uint32_t n, const LidTabl
         const int64_t p3 = p2 >= 0 ? prev_lead(b, p2) : -1;
         part[D - 1] += lid_grams_n(lid_letter(ucd, b, n, p3), lid_letter(ucd, b, n, p2),
                                    lid_letter(ucd, b, n, p1), l0, [&](uint32_t g, int order) {
-                                     if (lt.E) lid_add_emb(lt.E, g, order, part);
-                                     else lid_add_row(lt.P, g, part);
+                                     lid_add_emb(lt.E, g, order, part);
                                    });
       },
       tmp, sums);
@@ -1846,26 +1845,19 @@ TB_HD void langid_sums(DocCtx<P>& x, const uint8_t* b, uint32_t n, const LidTabl
 
 // Language-id record straight from the UTF-8 bytes: every code point position (a UTF-8 lead
 // byte, as decode() defines them) of the first kLidMaxCps code points, plus the virtual end
-// position, emits the 1..4-grams ending there (lid_grams_at); their rows (v2: int16 logit rows,
-// v3: int8 embedding rows) are summed exactly, then decided (v3: lid_record_v3, the same integers
-// as the device's MFMA tile). Neighbouring letters are found by stepping back to the previous lead
+// position, emits the 1..4-grams ending there (lid_grams_at); their int8 embedding rows are summed
+// exactly, then decided (lid_record_v3, the same integers as the device's MFMA tile). Neighbouring letters are found by stepping back to the previous lead
 // bytes, so no per-code-point arrays are needed. The device runs its own kernel for this
-// (k_langid_features / k_langid_mfma, same records); this version runs inside the stage
+// (k_langid_mfma, same records); this version runs inside the stage
 // emulation on the host.
 template <class P>
 TB_HD void langid_record(DocCtx<P>& x, const uint8_t* b, uint32_t n, const LidTables& lt, int64_t* r) {
   const auto mark = x.mark();
   int64_t* sums = x.template alloc_hot<int64_t>(kLidDim + 1);  // shared by the lanes
   if (x.overflow) return;
-  if (lt.E) {
-    langid_sums<P, kLidDim + 1>(x, b, n, lt, sums);
-    if (x.overflow) return;
-    x.par.single([&]() { lid_record_v3(sums, sums[kLidDim], lt, r); });
-  } else {
-    langid_sums<P, kLidLangs + 1>(x, b, n, lt, sums);
-    if (x.overflow) return;
-    x.par.single([&]() { lid_decide(sums, sums[kLidLangs], lt.bias, r); });
-  }
+  langid_sums<P, kLidDim + 1>(x, b, n, lt, sums);
+  if (x.overflow) return;
+  x.par.single([&]() { lid_record_v3(sums, sums[kLidDim], lt, r); });
   x.par.sync();
   x.reset(mark);
 }
@@ -2600,7 +2592,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
       if constexpr (kWithLid) {
         for (int s = 0; s < st.n_steps; ++s) {
           const DevStep& ds = st.steps[s];
-          if (ds.kind == DK_LANGID && (lid.P || lid.E))
+          if (ds.kind == DK_LANGID && lid.E)
             langid_record(x, b, n, lid, out.rec + (int64_t)ds.rec_prefix * out.ndocs + (int64_t)out.doc * ds.width);
         }
       }
@@ -2749,9 +2741,9 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
       x.reset(mark);
       x.stamp(PH_FW);
     } else if (ds.kind == DK_LANGID) {
-      // on the device this runs as a separate kernel (k_langid_features): lid.P == nullptr
+      // on the device this runs as a separate kernel (k_langid_mfma): lid.E == nullptr
       if constexpr (kWithLid)
-        if (lid.P || lid.E) langid_record(x, b, n, lid, r);
+        if (lid.E) langid_record(x, b, n, lid, r);
       x.stamp(PH_LID);
     }
     if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }

@@ -1,7 +1,6 @@
 // Character n-gram language identifier that stands in for lingua (reference
-// src/pipeline/filters/language_filter.rs:35-93; survey H5). Two models share the featurizer:
-//
-// v3 (default, "fastText + bf16 MFMA head"): a document vector of kLidDim = 32 dims, the
+// src/pipeline/filters/language_filter.rs:35-93; survey H5), "fastText + bf16 MFMA head":
+// a document vector of kLidDim = 32 dims, the
 // concatenation of two 16-dim bags over one int8 embedding table of kLidRowDim = 16 values per
 // bucket (16 bytes per n-gram gather): the 1- and 2-grams are summed into the lower half, the 3-
 // and 4-grams into the upper half. A document's rows are summed exactly (int32), the mean doc
@@ -12,10 +11,7 @@
 // below 2^24, so the MFMA's fp32 result is exact in any summation order and the host computes the
 // same integers: logits = C * w_scale * 2^-e + b, softmax, confidence = top probability.
 //
-// v2 (opt-in): the head folded into the table offline, P[bucket][8] int16 fixed-point logit
-// contributions (scale kLidScale): logits = (sum of the document's rows) / #grams / kLidScale + b.
-//
-// Both decide with lid_exp (a fixed polynomial with explicit fma), so host and device agree on the
+// The decision uses lid_exp (a fixed polynomial with explicit fma), so host and device agree on the
 // confidence bits, not only on the integer sums.
 //
 // N-grams: the text is scanned as code points (first kLidMaxCps only); letters (Alphabetic) are
@@ -29,13 +25,12 @@
 namespace tb {
 
 constexpr int kLidLangs = 5;
-constexpr int kLidRow = 8;  // int16 per bucket (languages 0..4, zero padding): one 16-byte load
+constexpr int kLidRow = 8;  // bias floats (languages 0..4, zero padding)
 constexpr int kLidBucketsLog2 = 16;
 constexpr uint32_t kLidBuckets = 1u << kLidBucketsLog2;
 constexpr int kLidMaxCps = 4096;
 constexpr int kLidMaxGrams = 4;  // n-grams emitted per code point position, at most
 constexpr uint32_t kLidBoundary = 0x20;
-constexpr double kLidScale = 1024.0;  // P = int16 / 1024 (|P| < 32)
 constexpr int kLidDim = 32;           // v3 doc-vector dims = the MFMA K
 constexpr int kLidRowDim = 16;        // v3 stored dims per bucket (half of the doc vector)
 constexpr int kLidHeadCols = 16;      // v3 head columns (5 languages, zero padded to the MFMA N)
@@ -82,13 +77,6 @@ TB_HD int lid_grams_at(uint32_t lm3, uint32_t lm2, uint32_t lm1, uint32_t l0, F&
   return lid_grams_n(lm3, lm2, lm1, l0, [&](uint32_t g, int) { emit(g); });
 }
 
-// Adds the int16 row of bucket g to the 5 language sums.
-TB_HD void lid_add_row(const int16_t* P, uint32_t g, int32_t* acc) {
-  const int16_t* r = P + (size_t)g * kLidRow;
-#pragma unroll
-  for (int l = 0; l < kLidLangs; ++l) acc[l] += r[l];
-}
-
 // exp(x) for x <= 0 with the same bits on host and device: range reduction by ln 2 and a
 // degree-13 Taylor polynomial on |r| <= 0.35 (truncation error < 4e-18), every multiply-add an
 // explicit fma (correctly rounded on both sides; no contraction choices left to the compiler).
@@ -119,19 +107,6 @@ TB_HD void lid_softmax_decide(const double* logit, int64_t* r) {
   r[1] = u.i;
 }
 
-// v2 decision from the exact sums: r[0] = language index (-1: no n-gram), r[1] = confidence bits.
-TB_HD void lid_decide(const int64_t* sums, int64_t cnt, const float* bias, int64_t* r) {
-  if (cnt <= 0) {
-    r[0] = -1;
-    r[1] = 0;
-    return;
-  }
-  double logit[kLidLangs];
-  for (int l = 0; l < kLidLangs; ++l) logit[l] = (double)sums[l] / (double)cnt / kLidScale + (double)bias[l];
-  lid_softmax_decide(logit, r);
-}
-
-// ---- v3 -----------------------------------------------------------------------------------
 // Block exponent of a document: the largest e in [0, 30] with max|S| * 2^e <= 255 * cnt, so every
 // a[k] = round(S[k] * 2^e / cnt) satisfies |a[k]| <= 255.
 TB_HD int lid_block_exp(int64_t smax, int64_t cnt) {
@@ -192,19 +167,18 @@ TB_HD int64_t prev_lead(const uint8_t* b, int64_t s) {
   return k;
 }
 
-// The model's tables as the kernels see them (v2: P; v3: E, W, w_scale).
+// The model's tables as the kernels see them (E == nullptr: no model).
 struct LidTables {
-  const int16_t* P;    // v2: [kLidBuckets * kLidRow]
-  const float* bias;   // [kLidRow]
-  const int8_t* E = nullptr;   // v3: [kLidBuckets * kLidRowDim] int8 embedding rows
-  const int16_t* W = nullptr;  // v3: [kLidDim * kLidLangs] integer head (|W| <= 255)
-  double w_scale = 0;          // v3: logit units per head unit at e = 0
+  const float* bias = nullptr;  // [kLidRow]
+  const int8_t* E = nullptr;    // [kLidBuckets * kLidRowDim] int8 embedding rows
+  const int16_t* W = nullptr;   // [kLidDim * kLidLangs] integer head (|W| <= 255)
+  double w_scale = 0;           // logit units per head unit at e = 0
 };
 
 // Dims of the doc vector that an n-gram of order n feeds: [lid_half(n), lid_half(n) + 16).
 TB_HD int lid_half(int n) { return n >= 3 ? kLidRowDim : 0; }
 
-// Adds the int8 embedding row of bucket g (an n-gram of order n) to its half of the sums (v3).
+// Adds the int8 embedding row of bucket g (an n-gram of order n) to its half of the sums.
 TB_HD void lid_add_emb(const int8_t* E, uint32_t g, int n, int32_t* acc) {
   const int8_t* r = E + (size_t)g * kLidRowDim;
   int32_t* a = acc + lid_half(n);
@@ -212,7 +186,7 @@ TB_HD void lid_add_emb(const int8_t* E, uint32_t g, int n, int32_t* acc) {
   for (int d = 0; d < kLidRowDim; ++d) a[d] += r[d];
 }
 
-// v3 record from the exact embedding sums S[kLidDim] and the n-gram count (host reference of the
+// Record from the exact embedding sums S[kLidDim] and the n-gram count (host reference of the
 // device's MFMA tile: the same integers).
 TB_HD void lid_record_v3(const int64_t* S, int64_t cnt, const LidTables& lt, int64_t* r) {
   if (cnt <= 0) {

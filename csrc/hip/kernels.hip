@@ -9,7 +9,6 @@
 //
 //  tb_stage_analyze   : decode + UAX#29 words + lines + hashes -> Gopher/FineWeb records
 //  tb_langid_mfma     : fastText int8 embedding bag + bf16 MFMA head (16 docs per tile) -> language records
-//  tb_langid_features : (v2 model) hashed 1..4-gram int16 logit rows summed per document -> language records
 //  tb_c4_pass_a       : C4 line filtering, citation removal, rewritten text into scratch
 //  tb_c4_pass_b       : compaction of the rewritten texts into the next content version
 #include <hip/hip_runtime.h>
@@ -119,7 +118,7 @@ __device__ __forceinline__ void c4_src_absolute(DocCtx<P>& x, int64_t* src, int6
     if (line_stats) out.line_stats = line_stats + line_stats_base(off[doc], doc);                     \
     if (gr_export) { out.gr_export = gr_export + blockIdx.x; out.b_global = bytes + off[doc]; }       \
     out.dict = dict;                                                                                  \
-    analyze_stage<WavePar, false>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out); /* LD: own kernel */ \
+    analyze_stage<WavePar, false>(x, *stage, *plan, LidTables{}, b, n, out); /* LD: own kernel */ \
   }
 
 #ifndef TB_STAGE_WPE
@@ -177,7 +176,7 @@ __device__ __forceinline__ void stage_blk_body(
   // split documents (the first n_split launch positions, longer than split_bytes) export their
   // word arrays; k_gr_dup_split finishes their duplicated n-gram orders
   if (gr_export && (int)blockIdx.x < n_split && n > split_bytes) out.gr_export = gr_export + blockIdx.x;
-  analyze_stage<BlockPar<NT>, false, kPre>(x, *stage, *plan, LidTables{nullptr, nullptr}, b, n, out);
+  analyze_stage<BlockPar<NT>, false, kPre>(x, *stage, *plan, LidTables{}, b, n, out);
 }
 
 #define TB_STAGE_BLK_KERNEL(NAME, NT, PRE)                                                             \
@@ -687,144 +686,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
   if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
 }
 
-// Language ID, one wave per document (csrc/common/langid.h): every lane takes one byte position
-// of a 64-byte chunk; a code point position emits the 1..4-grams ending there, and each gram
-// costs one 16-byte gather of its int16 logit row (the model's table is 1 MB: L2-resident).
-// The letters of the three previous code points come from registers: a ballot of the chunk's
-// lead bytes gives every lane the lanes of its previous code points (highest set bits below it),
-// whose letters are read with shuffles, and the last three letters of the previous chunk are
-// carried in registers for the first lanes. The next chunk's byte is loaded before the current
-// chunk is processed, so the byte load is off the critical path. Only a non-ASCII letter reads
-// the rest of its code point from memory. Same exact integer sums as the host
-// (langid_record / LangidModel::sums).
-__device__ __forceinline__ void lid_add_row16(const int16_t* __restrict__ P, uint32_t g, int32_t* acc) {
-  const uint4 w = *(const uint4*)(P + (size_t)g * kLidRow);
-  acc[0] += (int32_t)(int16_t)(w.x & 0xffffu);
-  acc[1] += (int32_t)w.x >> 16;
-  acc[2] += (int32_t)(int16_t)(w.y & 0xffffu);
-  acc[3] += (int32_t)w.y >> 16;
-  acc[4] += (int32_t)(int16_t)(w.z & 0xffffu);
-}
-
 // index of the highest set bit of m (m != 0)
 __device__ __forceinline__ int lid_top(uint64_t m) { return 63 - __clzll((long long)m); }
-
-__device__ __forceinline__ void langid_coop(DocCtx<WavePar>& x, const uint8_t* b, uint32_t n, const LidTables lt,
-                                            int64_t* r) {
-  const UcdView ucd = x.ucd;
-  const auto mark = x.mark();
-  uint32_t* limb = x.template alloc_hot<uint32_t>(1);
-  if (x.overflow) return;
-  x.par.single([&]() { *limb = n; });
-  x.par.sync();
-  if (n > (uint32_t)kLidMaxCps) {
-    x.par.template compact<int>(
-        n, [&](uint32_t i, int&) { return utf8_is_lead(b[i]); },
-        [&](uint32_t i, uint32_t k, int&) { if (k == (uint32_t)kLidMaxCps) *limb = i; });
-    x.par.sync();
-  }
-  const uint32_t lim = *limb;
-  const int lane = (int)x.par.lane;
-  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  // a lane adds at most 4 rows (|P| <= 2^15) per chunk of <= 257 chunks: int32 cannot overflow
-  int32_t acc[kLidLangs] = {0, 0, 0, 0, 0};
-  uint32_t cnt = 0;
-  uint32_t c1 = 0, c2 = 0, c3 = 0;  // letters of the last three code points before the chunk
-  uint8_t cur = (uint32_t)lane < lim ? b[lane] : (uint8_t)0;
-  for (uint32_t base = 0; base <= lim; base += 64) {  // wave-uniform trip count
-    const uint32_t s = base + (uint32_t)lane;
-    const uint8_t nxt = s + 64 < lim ? b[s + 64] : (uint8_t)0;  // prefetch of the next chunk
-    const bool lead = s < lim && utf8_is_lead(cur);
-    const uint32_t l0 = lead ? (cur < 0x80u ? ((cur | 0x20u) - 'a' < 26u ? (cur | 0x20u) : 0u)
-                                            : lid_letter(ucd, b, n, s))
-                             : 0u;
-    const uint64_t M = __ballot(lead);
-    // previous code points: lanes of the highest lead bits below this one (every lane shuffles,
-    // from a lead lane or itself), then the carry from the previous chunk
-    uint64_t m = M & below;
-    uint32_t lm[3];
-    bool have[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      have[k] = m != 0;
-      const int j = have[k] ? lid_top(m) : lane;
-      if (have[k]) m &= ~(1ull << j);
-      lm[k] = (uint32_t)__shfl((int)l0, j);
-    }
-    if (lead || s == lim) {
-      // the slots without a lane in this chunk are a suffix: fill it from the carry, newest first
-      if (!have[0]) {
-        lm[0] = c1; lm[1] = c2; lm[2] = c3;
-      } else if (!have[1]) {
-        lm[1] = c1; lm[2] = c2;
-      } else if (!have[2]) {
-        lm[2] = c1;
-      }
-      cnt += (uint32_t)lid_grams_at(lm[2], lm[1], lm[0], l0, [&](uint32_t g) { lid_add_row16(lt.P, g, acc); });
-    }
-    // carry: letters of this chunk's last three code points (then the older carry); M is
-    // wave-uniform, so these shuffles run in uniform control flow
-    if (M) {
-      uint64_t mm = M;
-      const int j0 = lid_top(mm);
-      mm &= ~(1ull << j0);
-      const uint32_t x0 = (uint32_t)__shfl((int)l0, j0);
-      if (!mm) {
-        c3 = c2; c2 = c1; c1 = x0;
-      } else {
-        const int j1 = lid_top(mm);
-        mm &= ~(1ull << j1);
-        const uint32_t x1 = (uint32_t)__shfl((int)l0, j1);
-        if (!mm) {
-          c3 = c1; c2 = x1; c1 = x0;
-        } else {
-          const uint32_t x2 = (uint32_t)__shfl((int)l0, lid_top(mm));
-          c3 = x2; c2 = x1; c1 = x0;
-        }
-      }
-    }
-    cur = nxt;
-  }
-  int64_t sums[kLidLangs];
-#pragma unroll
-  for (int l = 0; l < kLidLangs; ++l) {
-    int64_t v = acc[l];
-    for (int o = 1; o < 64; o <<= 1) v += pardetail::shfl_t(v, lane ^ o);
-    sums[l] = v;
-  }
-  for (int o = 1; o < 64; o <<= 1) cnt += (uint32_t)__shfl_xor((int)cnt, o);
-  if (x.par.leader()) lid_decide(sums, (int64_t)cnt, lt.bias, r);
-  x.par.sync();
-  x.reset(mark);
-}
-
-// Language ID of one document per wave (own kernel: it would otherwise set the register budget,
-// and so the occupancy, of the whole stage kernel). Writes the step's record (language, conf).
-__global__ __launch_bounds__(64) void k_langid_features(
-    const uint8_t* __restrict__ bytes, const int64_t* __restrict__ off, const int32_t* __restrict__ perm,
-    int32_t ndocs, char* scratch, const int64_t* __restrict__ scratch_off, DevTables tabs, LidTables lt,
-    int64_t* rec, int32_t width, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
-  const int doc = perm ? perm[blockIdx.x] : (int)blockIdx.x;
-  if (doc >= ndocs) return;
-  DocCtx<WavePar> x = make_ctx(tabs, nullptr, 0, scratch, scratch_off, doc, (int)blockIdx.x, flags, lds_bytes, prof);
-  const uint8_t* b = bytes + off[doc];
-  const uint32_t n = (uint32_t)(off[doc + 1] - off[doc]);
-  x.stamp(PH_START);
-  langid_coop(x, b, n, lt, rec + (int64_t)doc * width);
-  // (no dictionary-script flag: the language records are exact for every script; a document
-  // with such code points goes to the CPU path only if it reaches a segmentation pass, whose
-  // decode flags it)
-  x.stamp(PH_LID);
-  if (x.overflow) x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW);
-}
 
 // Language ID v3 (csrc/common/langid.h): two fastText bags + bf16 MFMA head, 16 documents per
 // 256-thread workgroup: wave w gathers documents w, w + 4, w + 8, w + 12 of the tile one after
 // another (launch positions blockIdx.x * 16 + ...; the length-sorted order keeps a tile's
 // documents alike in size). Per 64-byte chunk every lane finds the n-grams ending at its code
-// point (the chunked walk and register letter carry of langid_coop; at most one gram per order
+// point (a chunked walk with the previous letters carried in registers; at most one gram per order
 // n = 1..4, so each order has a fixed slot) and loads each gram's 16-byte embedding row with one
-// dwordx4 (the bytes of the v2 table). Rows are added SWAR-style: the table holds E + 128 as
+// dwordx4. Rows are added SWAR-style: the table holds E + 128 as
 // unsigned bytes, even and odd bytes go to the two 16-bit halves of a register, the 1-/2-gram
 // slots into one set of 8 packed registers (dims 0..15), the 3-/4-gram slots into another (dims
 // 16..31) — no lane-dependent selects. Every 64 chunks (and at the end) a butterfly over the
@@ -1967,12 +1838,9 @@ int tb_gr_dup_split(hipStream_t stream, const void* stage, int32_t gr_step, cons
           hipSuccess || per_cu <= 0)
     per_cu = 1;
   const int64_t total = (int64_t)n_split * n_tasks;
-  // TB_SPLIT_GRID=full: one workgroup per task (the hardware dispatcher orders them instead)
-  static const bool full = [] {
-    const char* e = std::getenv("TB_SPLIT_GRID");
-    return e && std::string(e) == "full";
-  }();
-  const int grid = (int)std::min<int64_t>(total, full ? total : (int64_t)cus * per_cu);
+  // persistent: one resident wave of workgroups pulls tasks from the cursor (one workgroup per
+  // task, ordered by the hardware dispatcher instead, measured slower: profiles/r8_c5/)
+  const int grid = (int)std::min<int64_t>(total, (int64_t)cus * per_cu);
   (void)hipMemsetAsync(cursor, 0, sizeof(uint32_t), stream);
   hipLaunchKernelGGL(k_gr_dup_split, dim3((uint32_t)grid), dim3(kBlockThreads), lds_bytes, stream,
                      (const DevStage*)stage, gr_step, perm, n_split, n_tasks, ndocs, (const GrExport*)gr_export, pw,
@@ -2062,21 +1930,6 @@ int tb_badwords_match(hipStream_t stream, const uint8_t* bytes, const int64_t* o
   hipLaunchKernelGGL(k_badwords_match, dim3((nitems + kBwWaves - 1) / kBwWaves), dim3(64 * kBwWaves), 0, stream, bytes,
                      off, nitems, root, cjk, root0, cjk0, dead, dead_max, bt, t, fold, matched, seg_doc, seg_idx,
                      seg_bytes);
-  return (int)hipGetLastError();
-}
-
-int tb_langid_features(hipStream_t stream, const uint8_t* bytes, const int64_t* off, const int32_t* perm,
-                       int32_t ndocs, char* scratch, const int64_t* scratch_off, const uint16_t* s1,
-                       const uint32_t* s2, const uint16_t* l1, const int32_t* l2, const int16_t* P, const float* bias,
-                       int64_t* rec, int32_t width, uint32_t* flags, uint32_t lds_bytes, uint64_t* prof) {
-  if (ndocs <= 0) return 0;
-  if (lds_bytes > kMaxLdsPerDoc || !P || !bias || !rec || width < 2) return (int)hipErrorInvalidValue;
-  DevTables t{s1, s2, l1, l2};
-  if (lds_bytes > 65536)
-    (void)hipFuncSetAttribute((const void*)k_langid_features, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds_bytes);
-  hipLaunchKernelGGL(k_langid_features, dim3(ndocs), dim3(64), lds_bytes, stream, bytes, off, perm, ndocs, scratch,
-                     scratch_off, t, LidTables{P, bias}, rec, width, flags, lds_bytes, prof);
   return (int)hipGetLastError();
 }
 
@@ -2192,7 +2045,7 @@ int tb_pow_table(hipStream_t stream, uint64_t* pw, uint32_t n) {
 int tb_phase_slots() { return kPhaseSlots; }
 int tb_stage_waves() { return TB_STAGE_WPE; }  // waves per SIMD the wave stage kernel is built for
 
-int tb_abi_version() { return 23; }
+int tb_abi_version() { return 24; }
 size_t tb_sizeof_plan() { return sizeof(DevPlan); }
 size_t tb_sizeof_stage() { return sizeof(DevStage); }
 size_t tb_sizeof_c4() { return sizeof(DevC4); }

@@ -380,7 +380,7 @@ void emulate_stage(const std::vector<StepCfg>& steps, const std::vector<int>& id
       if (line_stats) out.line_stats = line_stats + line_stats_base(off[i], i);
       GrExport ex{};
       if (split_tasks > 0 && gr_pos >= 0) out.gr_export = &ex;
-      analyze_stage(x, st, *plan, lid ? lid->tables() : LidTables{nullptr, nullptr}, (const uint8_t*)data + off[i], n, out);
+      analyze_stage(x, st, *plan, lid ? lid->tables() : LidTables{}, (const uint8_t*)data + off[i], n, out);
       if (x.overflow) continue;
       if (!out.gr_export || !ex.valid) {
         note_scratch(x.peak, n);

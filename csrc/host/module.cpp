@@ -510,18 +510,9 @@ PYBIND11_MODULE(_tbhost, m) {
 
   // ---- language id (CPU) ----
   py::class_<LangidModel, std::shared_ptr<LangidModel>>(m, "LangidModel")
-      .def(py::init([](py::array_t<int16_t, py::array::c_style> P, py::array_t<float, py::array::c_style> b) {
-        // v2: folded int16 logit table
-        auto mdl = std::make_shared<LangidModel>();
-        if ((size_t)P.size() != (size_t)kLidBuckets * kLidRow) throw std::invalid_argument("P shape");
-        if ((size_t)b.size() != (size_t)kLidRow) throw std::invalid_argument("b shape");
-        mdl->P.assign(P.data(), P.data() + P.size());
-        mdl->b.assign(b.data(), b.data() + b.size());
-        return mdl;
-      }))
       .def(py::init([](py::array_t<int8_t, py::array::c_style> E, py::array_t<int16_t, py::array::c_style> W,
                        double w_scale, py::array_t<float, py::array::c_style> b) {
-        // v3: int8 embedding rows + integer head (the MFMA tile's operands)
+        // int8 embedding rows + integer head (the MFMA tile's operands)
         auto mdl = std::make_shared<LangidModel>();
         if ((size_t)E.size() != (size_t)kLidBuckets * kLidRowDim) throw std::invalid_argument("E shape");
         if ((size_t)W.size() != (size_t)kLidDim * kLidLangs) throw std::invalid_argument("W shape");
@@ -529,7 +520,6 @@ PYBIND11_MODULE(_tbhost, m) {
         for (py::ssize_t i = 0; i < W.size(); ++i)
           if (W.data()[i] > kLidQMax || W.data()[i] < -kLidQMax) throw std::invalid_argument("W out of range");
         if (!(w_scale > 0)) throw std::invalid_argument("w_scale must be > 0");
-        mdl->version = 3;
         mdl->E.assign(E.data(), E.data() + E.size());
         mdl->W.assign(W.data(), W.data() + W.size());
         mdl->w_scale = w_scale;
@@ -584,7 +574,6 @@ PYBIND11_MODULE(_tbhost, m) {
   m.attr("LID_ROW") = kLidRow;
   m.attr("LID_LANGS") = kLidLangs;
   m.attr("LID_BUCKETS") = kLidBuckets;
-  m.attr("LID_SCALE") = kLidScale;
   m.attr("LID_DIM") = kLidDim;
   m.attr("LID_ROW_DIM") = kLidRowDim;
   m.attr("LID_QMAX") = kLidQMax;

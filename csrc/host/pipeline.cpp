@@ -170,8 +170,7 @@ int64_t LangidModel::sums(std::string_view text, int64_t* out) const {
   uint32_t lm3 = 0, lm2 = 0, lm1 = 0;
   int ncp = 0;
   auto emit = [&](uint32_t g, int order) {
-    if (version == 3) lid_add_emb(E.data(), g, order, part);
-    else lid_add_row(P.data(), g, part);
+    lid_add_emb(E.data(), g, order, part);
     for (int l = 0; l < D; ++l) { out[l] += part[l]; part[l] = 0; }
   };
   uint32_t i = 0;
@@ -191,8 +190,7 @@ int64_t LangidModel::sums(std::string_view text, int64_t* out) const {
 }
 
 void LangidModel::record(const int64_t* s, int64_t cnt, int64_t* r) const {
-  if (version == 3) lid_record_v3(s, cnt, tables(), r);
-  else lid_decide(s, cnt, b.data(), r);
+  lid_record_v3(s, cnt, tables(), r);
 }
 
 int LangidModel::detect(std::string_view text, double* conf) const {

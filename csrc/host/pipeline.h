@@ -38,27 +38,25 @@ struct PoolTag {
 std::vector<std::pair<std::string, double>> pool_cpu_stats();
 
 struct LangidModel {
-  int version = 2;         // 2: folded int16 logit table (P); 3: int8 embeddings + MFMA head (E, W)
-  std::vector<int16_t> P;  // v2: [kLidBuckets * kLidRow] fixed-point logit rows (csrc/common/langid.h)
+  int version = 3;         // int8 embeddings + MFMA head (csrc/common/langid.h)
   std::vector<float> b;    // [kLidRow]
-  std::vector<int8_t> E;   // v3: [kLidBuckets * kLidRowDim] embedding rows (block-sparse halves)
-  std::vector<int16_t> W;  // v3: [kLidDim * kLidLangs] integer head
-  double w_scale = 0;      // v3
+  std::vector<int8_t> E;   // [kLidBuckets * kLidRowDim] embedding rows (block-sparse halves)
+  std::vector<int16_t> W;  // [kLidDim * kLidLangs] integer head
+  double w_scale = 0;
   // Detect the language of `text`: returns lang index or -1, confidence in *conf.
   int detect(std::string_view text, double* conf) const;
-  // Exact sums of the text's n-gram rows (out[sum_width()]: v2 per-language sums, v3 embedding
-  // dims); returns the n-gram count.
+  // Exact sums of the text's n-gram rows (out[sum_width()]: embedding dims); returns the
+  // n-gram count.
   int64_t sums(std::string_view text, int64_t* out) const;
-  int sum_width() const { return version == 3 ? kLidDim : kLidLangs; }
+  int sum_width() const { return kLidDim; }
   // The language record (r[0] language or -1, r[1] confidence bits) from sums() output.
   void record(const int64_t* s, int64_t cnt, int64_t* r) const;
   LidTables tables() const {
-    LidTables t{version == 2 ? P.data() : nullptr, b.data()};
-    if (version == 3) {
-      t.E = E.data();
-      t.W = W.data();
-      t.w_scale = w_scale;
-    }
+    LidTables t;
+    t.bias = b.data();
+    t.E = E.data();
+    t.W = W.data();
+    t.w_scale = w_scale;
     return t;
   }
 };

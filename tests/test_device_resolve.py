@@ -42,7 +42,7 @@ def test_device_resolve_outputs_equal_host_assembly(monkeypatch):
     before = metrics.DEVICE_RESOLVE_FALLBACK_TOTAL._value.get()
     a = Engine(cfg, backend="emulate", nthreads=4, keep_reasons=True).process(data, off)
     assert metrics.DEVICE_RESOLVE_FALLBACK_TOTAL._value.get() == before  # fast path taken
-    monkeypatch.setenv("TB_DEVICE_RESOLVE", "0")
+    monkeypatch.setenv("TB_TUNE", "device_resolve=0")
     b = Engine(cfg, backend="emulate", nthreads=4, keep_reasons=True).process(data, off)
     c = Engine(cfg, backend="cpu", segmentation="icu", nthreads=4, keep_reasons=True).process(data, off)
     for x in (b, c):

@@ -258,14 +258,10 @@ def test_dynamic_schedule_balances_a_straggler(tmp_path, monkeypatch):
     outputs are identical to the one-rank run either way."""
     inp = _corpus_groups(tmp_path)
     _, o1, e1 = _cli(tmp_path, inp, "one", "--unit-rows", "20")
-    monkeypatch.setenv("TB_READ_THREADS", "1")
-    monkeypatch.setenv("TB_CLAIM_AHEAD", "1")
-    monkeypatch.setenv("TB_SCHEDULE", "static")
-    r_s, o_s, e_s = _cli(tmp_path, inp, "static", "--gpus", "2", "--unit-rows", "20", "--fault-inject",
-                         "slow@0.03:1")
-    monkeypatch.setenv("TB_SCHEDULE", "dynamic")
-    r_d, o_d, e_d = _cli(tmp_path, inp, "dyn", "--gpus", "2", "--unit-rows", "20", "--fault-inject",
-                         "slow@0.03:1")
+    flags = ("--gpus", "2", "--unit-rows", "20", "--read-threads", "1", "--claim-ahead", "1",
+             "--fault-inject", "slow@0.03:1")
+    r_s, o_s, e_s = _cli(tmp_path, inp, "static", *flags, "--schedule", "static")
+    r_d, o_d, e_d = _cli(tmp_path, inp, "dyn", *flags, "--schedule", "dynamic")
     for o, e in ((o_s, e_s), (o_d, e_d)):
         assert pq.read_table(o).equals(pq.read_table(o1)) and pq.read_table(e).equals(pq.read_table(e1))
     su, sb = _rank_stats(r_s.stdout)
@@ -280,15 +276,13 @@ def test_dynamic_schedule_balances_a_straggler(tmp_path, monkeypatch):
 
 
 def test_claim_gate_of_one_with_many_reader_threads(tmp_path, monkeypatch):
-    """TB_CLAIM_AHEAD=1 (the reference's basic_qos prefetch of 1) with 4 reader threads: the
+    """--claim-ahead 1 (the reference's basic_qos prefetch of 1) with 4 reader threads: the
     reader takes the next group only after yielding the previous one, so a gate smaller than its
     decode window cannot starve it; the outputs equal the one-rank run."""
     inp = _corpus_groups(tmp_path)
     _, o1, e1 = _cli(tmp_path, inp, "one", "--unit-rows", "20")
-    monkeypatch.setenv("TB_READ_THREADS", "4")
-    monkeypatch.setenv("TB_CLAIM_AHEAD", "1")
-    monkeypatch.setenv("TB_SCHEDULE", "dynamic")
-    r, o, e = _cli(tmp_path, inp, "gate1", "--gpus", "2", "--unit-rows", "20")
+    r, o, e = _cli(tmp_path, inp, "gate1", "--gpus", "2", "--unit-rows", "20", "--read-threads", "4",
+                   "--claim-ahead", "1", "--schedule", "dynamic")
     assert pq.read_table(o).equals(pq.read_table(o1)) and pq.read_table(e).equals(pq.read_table(e1))
     units, _ = _rank_stats(r.stdout)
     assert sum(units) == 160

@@ -142,10 +142,10 @@ def test_gopher_repetition_records_equal_oracle_on_repetitive_text(host):
 
 def test_mixed_script_delegation_is_overlapped_and_exact(monkeypatch):
     """Dictionary-script documents (5 % with a CJK / Thai snippet, 1 % CJK) without host word marks
-    (TB_DICT_MARKS=0): process_many recomputes the delegated ones on the engine's delegation thread
+    (TB_TUNE dict_marks=0): process_many recomputes the delegated ones on the engine's delegation thread
     while later batches are resolved; the merged results equal the CPU oracle batch for batch, and
     documents the language gate already filtered (the CJK ones) are not delegated."""
-    monkeypatch.setenv("TB_DICT_MARKS", "0")
+    monkeypatch.setenv("TB_TUNE", "dict_marks=0")
     cfg = load_pipeline_config("config/bench_pipeline.yaml")
     batches = [synth.pack(synth.make_corpus(600, 800, seed=40 + s, mixed_script=True)) for s in range(3)]
     emu = Engine(cfg, backend="emulate", nthreads=4)
@@ -221,7 +221,7 @@ def test_language_id_after_c4_is_recomputed_for_delegated_documents(tmp_path, mo
         "  - {type: LanguageDetectionFilter, min_confidence: 0.5, allowed_languages: [dan, eng, swe, nob, nno]}\n"
     p = tmp_path / "lid_after_c4.yaml"
     p.write_text(cfg_text)
-    monkeypatch.setenv("TB_DICT_MARKS", "0")  # dictionary-script documents go to the CPU path
+    monkeypatch.setenv("TB_TUNE", "dict_marks=0")  # dictionary-script documents go to the CPU path
     cfg = load_pipeline_config(str(p))
     assert [s.type for s in cfg.pipeline][-1] == "LanguageDetectionFilter"
     texts = synth.make_corpus(900, 800, seed=77, mixed_script=True)

@@ -81,7 +81,7 @@ def test_device_resolve_fast_path_equals_host_assembly(monkeypatch):
     assert eng.device_runner.resolve_t is not None
     a = eng.process(data, off)
     assert metrics.DEVICE_RESOLVE_FALLBACK_TOTAL._value.get() == before
-    monkeypatch.setenv("TB_DEVICE_RESOLVE", "0")
+    monkeypatch.setenv("TB_TUNE", "device_resolve=0")
     b = Engine(cfg, backend="cuda").process(data, off)
     np.testing.assert_array_equal(a.status, b.status)
     np.testing.assert_array_equal(a.fail_step, b.fail_step)
@@ -128,10 +128,9 @@ def test_device_equals_icu_oracle_on_hard_corpus(monkeypatch, mode):
     from test_emulated_device_path import outputs
 
     if mode == "split":
-        monkeypatch.setenv("TB_SPLIT_DOC_BYTES", "4096")
+        monkeypatch.setenv("TB_TUNE", "split_doc_bytes=4096")
     if mode == "pre":
-        monkeypatch.setenv("TB_PRE_DOC_BYTES", "65536")
-        monkeypatch.setenv("TB_SPLIT_DOC_BYTES", "20000")
+        monkeypatch.setenv("TB_TUNE", "pre_doc_bytes=65536,split_doc_bytes=20000")
     cfg = load_pipeline_config(CFG)
     texts = _hard_corpus()
     data, off = synth.pack(texts)

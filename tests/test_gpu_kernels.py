@@ -116,7 +116,7 @@ def test_dictionary_scripts_are_flagged(host, runner_parts, monkeypatch):
     """A dictionary-script document leaves the device only when it reaches a segmentation pass
     without host word marks: the CJK document fails the language gate on the device (exact records,
     not delegated); the Danish document with a CJK snippet passes it and stays on the device with
-    the host's ICU marks of its snippet line, or (TB_DICT_MARKS=0) is flagged by the stage
+    the host's ICU marks of its snippet line, or (TB_TUNE dict_marks=0) is flagged by the stage
     kernel's decode."""
     from textblaster_amd.pipeline.device import DeviceRunner
 
@@ -128,7 +128,7 @@ def test_dictionary_scripts_are_flagged(host, runner_parts, monkeypatch):
     assert res.flags[0] == 0 and res.dead[0] != 0
     assert res.flags[1] == 0
     assert res.flags[2] == 0 and runner.dict_marks
-    monkeypatch.setenv("TB_DICT_MARKS", "0")
+    monkeypatch.setenv("TB_TUNE", "dict_marks=0")
     nomarks = DeviceRunner(steps, plan, runner.device, lid)
     res = nomarks.run(data, off)
     assert res.flags[0] == 0 and res.flags[1] == 0
@@ -157,7 +157,7 @@ def test_langid_records_match_host(host, corpus, runner_parts):
     """k_langid_mfma (v3: int8 embedding bag, bf16 MFMA head over 16-document tiles) vs. the host
     model on the corpus: same exact sums and head integers, so the same language and confidence."""
     _, _, _, runner, lid = runner_parts
-    assert lid.version == 3 and runner.lid_version == 3
+    assert lid.version == 3 and runner.lid_E is not None
     texts = corpus[:517]  # not a multiple of the 16-document tile
     data, off = synth.pack(texts)
     res = runner.run(data, off)
@@ -199,21 +199,6 @@ def test_langid_mfma_head_vs_fp32_reference(host, corpus, runner_parts):
             continue
         assert abs(got - float(p.max())) < 0.015, (i, got, float(p.max()))
     assert near <= 2
-
-
-def test_langid_v2_table_records_match_host(host, corpus, runner_parts):
-    """The opt-in v2 model (folded int16 table, k_langid_features) still runs and matches."""
-    from textblaster_amd.models.langid import TABLE_WEIGHTS, load
-    from textblaster_amd.pipeline.device import DeviceRunner
-
-    cfg, steps, plan, _, _ = runner_parts
-    lid2 = load(TABLE_WEIGHTS)
-    runner = DeviceRunner(steps, plan, "cuda:0", lid2)
-    assert runner.lid_version == 2
-    texts = corpus[:256]
-    data, off = synth.pack(texts)
-    res = runner.run(data, off)
-    _assert_langid_equal(texts, _langid_records(runner, res, len(texts)), lid2.native())
 
 
 def test_langid_edge_cases_bit_exact(host, runner_parts):
@@ -265,7 +250,7 @@ def test_split_documents_match_host_emulation(host, corpus, runner_parts, monkey
     from textblaster_amd.pipeline.device import KIND_GOPHER_REP, DeviceRunner
 
     cfg, steps, plan, _, lid = runner_parts
-    monkeypatch.setenv("TB_SPLIT_DOC_BYTES", "1")  # clamped to the long-document threshold
+    monkeypatch.setenv("TB_TUNE", "split_doc_bytes=1")  # clamped to the long-document threshold
     runner = DeviceRunner(steps, plan, "cuda:0", lid)
     assert runner.gr_split and runner.split_doc_bytes == runner.long_doc_bytes
     data, off = synth.pack(corpus)
@@ -305,7 +290,7 @@ def test_pre_decoded_long_documents_match_host(host, runner_parts, monkeypatch):
     cfg, steps, plan, _, lid = runner_parts
     # (the pre-pass documents take no host word marks: compare both runs with the CPU path for
     # dictionary scripts)
-    monkeypatch.setenv("TB_DICT_MARKS", "0")
+    monkeypatch.setenv("TB_TUNE", "dict_marks=0")
     rng = np.random.default_rng(3)
     langs = ["eng", "dan", "swe", "nob", "nno"]
     texts = [synth.make_doc(rng, langs[k % 5], int(s)) for k, s in enumerate(np.geomspace(66000, 400000, 8))]
@@ -319,7 +304,7 @@ def test_pre_decoded_long_documents_match_host(host, runner_parts, monkeypatch):
     lens = np.diff(off)
     res = {}
     for pre in ("65536", "0"):
-        monkeypatch.setenv("TB_PRE_DOC_BYTES", pre)
+        monkeypatch.setenv("TB_TUNE", f"dict_marks=0,pre_doc_bytes={pre}")
         runner = DeviceRunner(steps, plan, "cuda:0", lid)
         assert runner.pre_doc_bytes == (65536 if pre != "0" else 0)
         res[pre] = runner.run(data, off)

@@ -27,7 +27,7 @@ DEFAULT_CFG = os.path.join(REPO, "config", "pipeline_config.yaml")
 def _run(tmp_path, inp, tag, *extra, env_extra=None):
     out, exc = str(tmp_path / f"{tag}.o.parquet"), str(tmp_path / f"{tag}.e.parquet")
     env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="2", TB_MASTER_PORT=str(free_port()),
-               TB_MAX_BATCH_BYTES=str(256 << 10), HSA_ENABLE_IPC_MODE_LEGACY="0")
+               TB_TUNE=f"batch_bytes={256 << 10}", HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.update(env_extra or {})
     cmd = [sys.executable, "-m", "textblaster_amd", "run", "-i", inp, "-o", out, "-e", exc, "-c", DEFAULT_CFG,
            "--backend", "cuda", "--unit-rows", "400", "--tokenizer-dir", TOK,

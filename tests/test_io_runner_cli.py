@@ -300,19 +300,3 @@ def test_daily_log_handler_rolls_over(tmp_path):
     assert open(tmp_path / "producer.log.2026-10-17").read() == "b\nc\n"
 
 
-def test_reader_decodes_into_host_buffers(tmp_path):
-    """With a batch-buffer allocator set (the GPU engine's pinned host_buffer), batches of 1 MB and
-    more carry their text in buffers from it, byte-identical to the plain read."""
-    texts = synth.make_corpus(3000, 600, seed=31) + ["a &amp; b &lt;c&gt;"]
-    p = str(tmp_path / "in.parquet")
-    pq.write_table(pa.table({"id": [f"d{i}" for i in range(len(texts))], "text": texts}), p)
-    plain = list(ParquetReader(ParquetInputConfig(p, "text", "id")).iter_batches(batch_rows=4096))
-    given = []
-    r = ParquetReader(ParquetInputConfig(p, "text", "id"))
-    r.host_buffer = lambda n: given.append(np.empty(n, np.uint8)) or given[-1]
-    mine = list(r.iter_batches(batch_rows=4096))
-    assert given and len(plain) == len(mine)
-    for a, b in zip(plain, mine):
-        np.testing.assert_array_equal(a.text[1], b.text[1])
-        assert bytes(a.text[0]) == bytes(b.text[0])
-    assert any(b.text[0] is g for b in mine for g in given)

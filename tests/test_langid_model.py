@@ -1,6 +1,6 @@
 """Language-ID models (csrc/common/langid.h): the stage emulation's record (langid_record, the
 device algorithm run on the host) equals the host model's decision for every document (v3
-fastText + MFMA head, and the v2 folded table), the v3 integer head agrees with a plain fp32/f64
+fastText + MFMA head), the v3 integer head agrees with a plain fp32/f64
 reference of the same model, the deterministic exp matches libm, the featurizer emits the
 documented 1..4-grams, and model files are validated on load."""
 import math
@@ -10,7 +10,7 @@ import pytest
 
 from textblaster_amd import native
 from textblaster_amd.config import load_pipeline_config_str
-from textblaster_amd.models.langid import LANGS, TABLE_WEIGHTS, load, load_default
+from textblaster_amd.models.langid import LANGS, load, load_default
 from textblaster_amd.pipeline.plan import build_plan
 from textblaster_amd.utils import synth
 
@@ -18,11 +18,10 @@ EDGE = ["", "1234 !!!", "a", "ab", "abc", "Å", "ø ø øø øøø øøøø", "x
         "blåbærgrød og æblegrød", "The quick brown fox.", "Hvorfor kjem du ikkje?", "ΣΑΣ ΣΑΣ."]
 
 
-@pytest.mark.parametrize("version", [3, 2])
-def test_stage_emulation_record_equals_host_model(version):
+def test_stage_emulation_record_equals_host_model():
     h = native.host()
-    lid = load_default() if version == 3 else load(TABLE_WEIGHTS)
-    assert lid.version == version
+    lid = load_default()
+    assert lid.version == 3
     cfg = load_pipeline_config_str(
         "pipeline:\n  - {type: LanguageDetectionFilter, min_confidence: 0.65, allowed_languages: [dan]}\n")
     steps = [h.make_step(s.native_dict()) for s in cfg.pipeline]
@@ -135,14 +134,12 @@ def test_lid_exp_matches_libm():
 
 def test_model_file_validation(tmp_path):
     h = native.host()
-    good = load(TABLE_WEIGHTS)
+    good = load_default()
     p = tmp_path / "bad.npz"
-    np.savez(p, P=good.P, b=good.b[:3])
+    np.savez(p, E=good.E, W=good.W, w_scale=good.w_scale, b=good.b[:3])
     with pytest.raises(ValueError):
         load(str(p))
-    P = good.P.copy().reshape(-1, h.LID_ROW)
-    P[5, h.LID_LANGS] = 1  # padding column must stay zero
-    np.savez(p, P=P.reshape(-1), b=good.b)
+    np.savez(p, P=np.zeros(8 << 16, np.int16), b=good.b)  # the removed v2 (folded table) format
     with pytest.raises(ValueError):
         load(str(p))
     np.savez(p, emb=np.zeros(4, np.uint16), w=np.zeros(4, np.uint16), b=good.b)  # the round-2 format

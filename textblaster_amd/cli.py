@@ -148,6 +148,9 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("--claim-ahead", type=int, default=None,
                        help="row groups a rank may claim ahead of its main loop (reference prefetch_count "
                             "semantics; default readers + 3)")
+        p.add_argument("--schedule", choices=("dynamic", "static"), default="dynamic",
+                       help="row groups across ranks: a shared claim cursor (dynamic) or byte-balanced "
+                            "contiguous ranges (static)")
         p.add_argument("--resume", action="store_true", help="skip units recorded in the work dir manifest")
         p.add_argument("--checkpoint", action="store_true", help="write per-unit parts + manifest (resumable)")
         p.add_argument("--work-dir", default=None, help="checkpoint dir (default <output-file>.work)")
@@ -246,7 +249,7 @@ def run_cmd(args, argv: List[str]) -> int:
         compression=args.compression, tokenizer_dir=args.tokenizer_dir, badwords_dir=args.badwords_dir,
         html_decode=args.html_decode, metrics_port=args.metrics_port, tokenizer_file=args.tokenizer_file,
         fault_inject=args.fault_inject, read_threads=args.read_threads, write_threads=args.write_threads,
-        batch_bytes=args.batch_bytes, slots=args.slots, claim_ahead=args.claim_ahead)
+        batch_bytes=args.batch_bytes, slots=args.slots, claim_ahead=args.claim_ahead, schedule=args.schedule)
     try:
         stats = run(rc, ctx)
     except RankFailure as e:

@@ -151,9 +151,6 @@ class ParquetReader:
         self.html_threads = html_threads
         # optional device decoder (ops.html.HtmlDecoder, K17); default: the host C++ decoder
         self.html_decoder = html_decoder
-        # optional allocator of page-locked batch buffers (Engine.host_buffer), set once the
-        # engine exists: batches read after that carry their text in pinned memory
-        self.host_buffer = None
         self._pf_obj = None
 
     @property
@@ -239,13 +236,6 @@ class ParquetReader:
                                                   self.html_threads)
         if dec is not None:
             data, off = dec
-        hb = self.host_buffer
-        if hb is not None and len(data) >= (1 << 20):
-            # decoded text into a page-locked batch buffer (Engine.host_buffer): the device upload
-            # DMAs straight from it, no staging copy on the submitting thread
-            buf = hb(len(data))
-            native.host().parallel_copy(buf, 0, np.ascontiguousarray(data), 1)
-            data = buf
         if not (pa.types.is_string(ids.type) or pa.types.is_large_string(ids.type)):
             ids = pc.cast(ids, pa.string())
         if self.has_source:

@@ -1,9 +1,7 @@
 """Language identification model (stands in for lingua; reference language_filter.rs:35-93).
 
-Two models share one featurizer: hashed character 1..4-grams of lowercased letter runs
-(csrc/common/langid.h), 65536 buckets.
-
-* **v3 (default, ``langid_v3.npz``)**: fastText with a D = 32 document vector made of two 16-dim
+Featurizer: hashed character 1..4-grams of lowercased letter runs (csrc/common/langid.h), 65536
+buckets. Model (``langid_v3.npz``): fastText with a D = 32 document vector made of two 16-dim
   bags over one int8 embedding table (16 values per bucket, so a gather moves 16 bytes): the
   1- and 2-grams are summed into dims 0..15, the 3- and 4-grams into dims 16..31; a document's
   rows are summed exactly, the mean doc vector is quantised to
@@ -11,10 +9,8 @@ Two models share one featurizer: hashed character 1..4-grams of lowercased lette
   the 32 -> 5 linear head runs on the matrix cores as ``v_mfma_f32_16x16x32_bf16`` tiles of 16
   documents (k_langid_mfma) with integer bf16 weights. Every product and partial sum is an
   integer below 2^24, so the MFMA's fp32 output is exact and the CPU path computes the same
-  records bit for bit.
-* **v2 (opt-in, ``langid_v2.npz``)**: the head folded into the table, P[bucket] = int16 logit
-  contributions (scale 1/1024): logits = mean of the document's rows + b
-  (k_langid_features: one 16-byte gather per n-gram, no matrix-core work).
+  records bit for bit. (Round 5's folded int16 logit table, "v2", lost its A/B to this model
+  and was removed.)
 
 Softmax over {English, Danish, Swedish, Nynorsk, Bokmal}; the confidence is the top probability.
 Weights are produced offline by ``tools/train_langid.py`` from ``models/data/langid_corpus`` and
@@ -32,7 +28,6 @@ from .. import native
 
 DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
 DEFAULT_WEIGHTS = os.path.join(DATA_DIR, "langid_v3.npz")
-TABLE_WEIGHTS = os.path.join(DATA_DIR, "langid_v2.npz")
 LANGS = ("eng", "dan", "swe", "nno", "nob")
 NAMES = ("English", "Danish", "Swedish", "Nynorsk", "Bokmal")
 QMAX = 255  # |integer| of the v3 doc vectors and head weights: exact in bf16
@@ -41,35 +36,29 @@ QMAX = 255  # |integer| of the v3 doc vectors and head weights: exact in bf16
 @dataclasses.dataclass
 class LangidWeights:
     b: np.ndarray                      # float32 [8] bias
-    P: Optional[np.ndarray] = None     # v2: int16 [BUCKETS * ROW] fixed-point logit rows
-    E: Optional[np.ndarray] = None     # v3: int8 [BUCKETS * ROW_DIM] embedding rows (both bags)
-    W: Optional[np.ndarray] = None     # v3: int16 [DIM * LANGS] integer head, |W| <= 255
-    w_scale: float = 0.0               # v3: logit units per head unit
+    E: np.ndarray                      # int8 [BUCKETS * ROW_DIM] embedding rows (both bags)
+    W: np.ndarray                      # int16 [DIM * LANGS] integer head, |W| <= 255
+    w_scale: float                     # logit units per head unit
     _native: Optional[object] = None
 
     @property
     def version(self) -> int:
-        return 3 if self.E is not None else 2
+        return 3
 
     @property
     def description(self) -> str:
-        if self.version == 3:
-            return ("fastText int8 EmbeddingBag(65536 x 16) x 2 bags (1-2 / 3-4-grams) -> 32-dim doc vector -> "
-                    "bf16 MFMA head (v_mfma_f32_16x16x32_bf16)")
-        return "hashed 1-4-gram int16 logit table"
+        return ("fastText int8 EmbeddingBag(65536 x 16) x 2 bags (1-2 / 3-4-grams) -> 32-dim doc vector -> "
+                "bf16 MFMA head (v_mfma_f32_16x16x32_bf16)")
 
     @property
     def dtype(self) -> str:
         """Compute dtype of the model's math on the device (bench.py reports it)."""
-        return "bf16" if self.version == 3 else "int16"
+        return "bf16"
 
     def native(self):
         if self._native is None:
             h = native.host()
-            if self.version == 3:
-                self._native = h.LangidModel(self.E, self.W, float(self.w_scale), self.b)
-            else:
-                self._native = h.LangidModel(self.P, self.b)
+            self._native = h.LangidModel(self.E, self.W, float(self.w_scale), self.b)
         return self._native
 
     def detect(self, text: str):
@@ -119,25 +108,17 @@ def load(path: str) -> LangidWeights:
     h = native.host()
     with np.load(path, allow_pickle=False) as z:
         files = set(z.files)
-        if {"E", "W", "w_scale", "b"} <= files:
-            E = np.ascontiguousarray(z["E"], dtype=np.int8).reshape(-1)
-            W = np.ascontiguousarray(z["W"], dtype=np.int16).reshape(-1)
-            w_scale = float(np.asarray(z["w_scale"]).reshape(()))
-            b = np.ascontiguousarray(z["b"], dtype=np.float32).reshape(-1)
-            if E.size != h.LID_BUCKETS * h.LID_ROW_DIM or W.size != h.LID_DIM * h.LID_LANGS or b.size != h.LID_ROW:
-                raise ValueError(f"language model {path} has the wrong shape")
-            if np.any(np.abs(W.astype(np.int32)) > QMAX) or not w_scale > 0:
-                raise ValueError(f"language model {path}: head out of range")
-            return LangidWeights(b=b, E=E, W=W, w_scale=w_scale)
-        if not {"P", "b"} <= files:
-            raise ValueError(f"language model {path} is neither a v3 (E, W, w_scale, b) nor a v2 (P, b) model")
-        P = np.ascontiguousarray(z["P"], dtype=np.int16).reshape(-1)
+        if not {"E", "W", "w_scale", "b"} <= files:
+            raise ValueError(f"language model {path} is not a fastText model (E, W, w_scale, b)")
+        E = np.ascontiguousarray(z["E"], dtype=np.int8).reshape(-1)
+        W = np.ascontiguousarray(z["W"], dtype=np.int16).reshape(-1)
+        w_scale = float(np.asarray(z["w_scale"]).reshape(()))
         b = np.ascontiguousarray(z["b"], dtype=np.float32).reshape(-1)
-    if P.size != h.LID_BUCKETS * h.LID_ROW or b.size != h.LID_ROW:
+    if E.size != h.LID_BUCKETS * h.LID_ROW_DIM or W.size != h.LID_DIM * h.LID_LANGS or b.size != h.LID_ROW:
         raise ValueError(f"language model {path} has the wrong shape")
-    if np.any(P.reshape(-1, h.LID_ROW)[:, h.LID_LANGS:] != 0):
-        raise ValueError(f"language model {path}: padding columns must be zero")
-    return LangidWeights(b=b, P=P)
+    if np.any(np.abs(W.astype(np.int32)) > QMAX) or not w_scale > 0:
+        raise ValueError(f"language model {path}: head out of range")
+    return LangidWeights(b=b, E=E, W=W, w_scale=w_scale)
 
 
 _default: Optional[LangidWeights] = None
@@ -147,8 +128,6 @@ def load_default() -> LangidWeights:
     global _default
     if _default is None:
         path = os.environ.get("TB_LANGID_MODEL", DEFAULT_WEIGHTS)
-        if path == "table":
-            path = TABLE_WEIGHTS
         if not os.path.exists(path):
             raise FileNotFoundError(
                 f"language-id weights not found at {path}; run `python tools/train_langid.py`")

@@ -20,7 +20,6 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
-import os
 import threading
 from typing import Iterator, Optional
 
@@ -142,8 +141,14 @@ class Stream:
         return ev
 
 
-# host waits on events sleep instead of spinning (TB_EVENT_BLOCKING=0: spin, HIP's default)
-_BLOCKING_EVENTS = os.environ.get("TB_EVENT_BLOCKING", "1") not in ("", "0")
+# host waits on events sleep instead of spinning (TB_TUNE event_blocking=0: spin, HIP's default;
+# DeviceRunner sets it from its tuning)
+_BLOCKING_EVENTS = True
+
+
+def set_blocking_events(on: bool) -> None:
+    global _BLOCKING_EVENTS
+    _BLOCKING_EVENTS = bool(on)
 
 
 class Event:

@@ -22,7 +22,7 @@ _SZ = ctypes.c_size_t
 
 # Bumped with every change of an entry point's signature in the table below: a stale
 # libtbhip.so with an older argument list would otherwise be called with the wrong arguments.
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 _SIGS = {
     "tb_stage_analyze": [_P, _P, _P, _P, _P, _P, _I32, _P, _P, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _P, _I32, _I32, _P,
@@ -46,7 +46,6 @@ _SIGS = {
     "tb_block_threads": [],
     "tb_badwords_match": [_P, _P, _P, _I32, _P, _P, _I32, _I32, _P, _U32, _P, _U32, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                           _U32],
-    "tb_langid_features": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _U32, _P],
     "tb_langid_mfma": [_P, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P, ctypes.c_double, _P, _P, _I32, _P],
     "tb_langid_prepare": [_P, _P, _P],
     "tb_pre_wcanon": [_P, _P, _P, _P, _I32, _P, _P, _U32, _P, _U32, _P],
@@ -316,23 +315,6 @@ class Kernels:
                 t[2].data_ptr(), t[3].data_ptr(), f1.data_ptr(), f2.data_ptr(), matched.data_ptr(), _ptr(sd), _ptr(si),
                 int(seg_bytes))
             _check(rc, "tb_badwords_match")
-
-    def langid_features(self, bytes_, off, perm, ndocs, scratch, scratch_off, P, bias, rec, width, flags, lds_bytes=0,
-                        prof=None):
-        """k_langid_features: the language record (language, confidence bits) of every document into
-        ``rec`` (document d at rec[d * width]); ``P``: int16 [buckets * 8] logit rows, ``bias``:
-        float32 [8] (csrc/common/langid.h)."""
-        from .. import native
-
-        h = native.host()
-        t = self.tabs
-        if P.numel() != h.LID_BUCKETS * h.LID_ROW or bias.numel() != h.LID_ROW or width < 2 or rec.numel() < ndocs * width:
-            raise DeviceError("langid_features: operand shapes")
-        rc = self.lib.tb_langid_features(
-            self.stream(), bytes_.data_ptr(), off.data_ptr(), _ptr(perm), ndocs, scratch.data_ptr(),
-            scratch_off.data_ptr(), t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), P.data_ptr(),
-            bias.data_ptr(), rec.data_ptr(), width, flags.data_ptr(), lds_bytes, _ptr(prof))
-        _check(rc, "tb_langid_features")
 
     def langid_prepare(self, E):
         """The pair table of k_langid_mfma (orders 1 + 2 of every position over a 32-letter alphabet,

@@ -9,7 +9,6 @@ once at the end of the batch.
 from __future__ import annotations
 
 import dataclasses
-import os
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -19,6 +18,8 @@ from ..errors import DeviceError
 from ..ops.kernels import PRE_DOC, PRE_TILE, PRE_WCHUNK
 from ..utils import metrics, tracing
 from .plan import ExecPlan
+from . import tuning
+from .tuning import DeviceTuning
 
 SCRATCH_ALIGN = 256
 
@@ -154,13 +155,11 @@ def trailing_token_counters(plan: ExecPlan) -> List[int]:
     return out[::-1]
 
 
-def dict_marks_wanted(plan: ExecPlan, steps_native) -> bool:
+def dict_marks_wanted(plan: ExecPlan, steps_native, tune: Optional[DeviceTuning] = None) -> bool:
     """Does a stage over the original text segment words (GopherQuality / GopherRepetition /
     FineWeb)? Then the host computes ICU word marks for the dictionary-script documents of every
-    batch (text.h dict_word_marks) and they stay on the device (TB_DICT_MARKS=0: CPU path)."""
-    import os
-
-    if os.environ.get("TB_DICT_MARKS", "1") in ("", "0"):
+    batch (text.h dict_word_marks) and they stay on the device (TB_TUNE dict_marks=0: CPU path)."""
+    if not (tune or tuning.from_env()).dict_marks:
         return False
     kinds = ("GopherQualityFilter", "GopherRepetitionFilter", "FineWebQualityFilter")
     return any(plan.stage_version[s] == 0 and any(plan.steps[i].type in kinds for i in idx)
@@ -314,13 +313,13 @@ KIND_GOPHER_QUALITY = 1
 KIND_FINEWEB = 3
 
 
-def line_stats_stages(plan: ExecPlan, stage_layout) -> Dict[int, int]:
+def line_stats_stages(plan: ExecPlan, stage_layout, tune: Optional[DeviceTuning] = None) -> Dict[int, int]:
     """C4 line export (docproc.h export_line_stats): per content version read by a C4 pass, the
     first stage of that version that segments words and Rust lines (GopherQuality / FineWeb);
     it exports every line's trimmed span, word count and longest word, and the C4 pass reads them
-    instead of decoding and segmenting the text again. TB_C4_LINE_STATS=0 turns it off."""
+    instead of decoding and segmenting the text again. TB_TUNE c4_line_stats=0 turns it off."""
     out: Dict[int, int] = {}
-    if os.environ.get("TB_C4_LINE_STATS", "1") == "0":
+    if not (tune or tuning.from_env()).c4_line_stats:
         return out
     c4_versions = {plan.steps[i].version_in for i in plan.c4_steps}
     for si, sv in enumerate(plan.stage_version):
@@ -404,32 +403,20 @@ def bw_dead_max(plan: ExecPlan, passes, pass_of_step: Dict[int, int]) -> Dict[in
 
 class DeviceRunner:
     N_SLOTS = 2
-    # per-wave LDS slices: the stage kernel is built for W waves/SIMD (tb_stage_waves: 8 -> 64
-    # VGPRs; 6 -> 80 cost 10 % more stage time, profiles/r8_wpe/) = 4 W waves/CU, so 160 KB / 4 W
-    # each costs no occupancy (5 KB at 8); the C4 kernel
-    # (7 waves/SIMD) only keeps per-line arrays there
-    DEFAULT_LDS_BYTES_C4 = 2560
-    DEFAULT_LONG_DOC_BYTES = 4096  # with the 3-per-CU workgroup kernel (profiles/r2_c5/long_doc_threshold.txt)
-    DEFAULT_LDS_BYTES_BLK = 49152
-    DEFAULT_SPLIT_DOC_BYTES = 32768  # config 5 A/B: 147.6 K (64 KiB) -> 151.5-152.5 K docs/s (profiles/r8_c5/)
-    # documents of at least this size get their code points and word-break marks from
-    # the multi-workgroup pre-pass (k_pre_*) before their stage workgroup runs; 0 disables. Never
-    # below 64 KiB (smaller documents use the packed code point layout). ~1 MB documents: 1,001 ->
-    # 1,136 docs/s; at 64 KiB the pre-pass costs config 5 (~50 KB documents) 10 %, at 256 KiB
-    # nothing (profiles/r5_pre/)
-    DEFAULT_PRE_DOC_BYTES = 262144
 
     def __init__(self, steps_native, plan: ExecPlan, device, langid=None, max_batch_bytes: int = 384 << 20,
-                 token_counters=None, slots: Optional[int] = None, host_threads: int = 8):
-        import os
-
+                 token_counters=None, slots: Optional[int] = None, host_threads: int = 8,
+                 tune: Optional[DeviceTuning] = None):
         from ..ops import hiprt
 
+        # operating points (pipeline/tuning.py: defaults with their A/B evidence, TB_TUNE overrides)
+        self.tune = tu = (tune or tuning.from_env()).replace(slots=slots or None)
         self.rt = hiprt
+        hiprt.set_blocking_events(tu.event_blocking)
         self.host_threads = max(1, int(host_threads))
         # dictionary-script documents: word marks from the host's ICU segmentation (stage kernels
         # of the original text) instead of the CPU path for the whole document
-        self.dict_marks = dict_marks_wanted(plan, steps_native)
+        self.dict_marks = dict_marks_wanted(plan, steps_native, tu)
         with tracing.trace_range("tb.init.hip_context"):
             self.device = hiprt.parse_device(device)
             if self.device >= hiprt.device_count():
@@ -446,21 +433,17 @@ class DeviceRunner:
         # slots, which carry only DMA copies. Measured on the 1-GPU bench (profiles/r2_streams/):
         # 6 -> 44.5 ms/step, 13 (5 per slot + copies, the round-1 layout) -> 45-47.5,
         # 4 (copies folded into the slot streams) -> 50, 5 (one shared copy stream) -> 55: an
-        # upload must never queue behind a download. TB_STREAMS selects a layout for A/B runs;
-        # TB_SERIAL_STREAMS=1 puts everything on one stream (exclusive kernel timings).
-        blk_prio = int(os.environ.get("TB_BLK_PRIORITY", "-1"))
-        serial = os.environ.get("TB_SERIAL_STREAMS", "") not in ("", "0")
-        self.stream_layout = "serial" if serial else os.environ.get("TB_STREAMS", "6")
-        if self.stream_layout not in ("serial", "4", "4c", "4f", "5", "6", "13"):
-            raise DeviceError("TB_STREAMS must be one of 4, 4c, 4f, 5, 6, 13")
+        # upload must never queue behind a download. The other layouts lost their A/Bs and were
+        # removed; TB_TUNE streams=serial puts everything on one stream (exclusive kernel timings).
+        blk_prio = tu.blk_priority
+        self.stream_layout = tu.streams
         # Batches in flight on the device. Each slot holds its own scratch arena (<= 176 B per text
         # byte, x1.25 headroom): three slots keep the GPU fed (interleaved A/B, 20-step headline
         # bench: 35.3 vs 38.6 ms/step, profiles/r2_slots/ab.txt) and fit 288 GB of HBM with
-        # 384 MB device batches; a smaller device gets two. `slots` (run --slots) or TB_SLOTS
-        # overrides.
-        env_slots = slots or os.environ.get("TB_SLOTS")
-        if env_slots:
-            self.N_SLOTS = max(1, int(env_slots))
+        # 384 MB device batches; a smaller device gets two. `slots` (run --slots) or TB_TUNE
+        # slots=N overrides.
+        if tu.slots:
+            self.N_SLOTS = max(1, int(tu.slots))
         else:
             try:
                 _, total = hiprt.mem_info()
@@ -473,42 +456,11 @@ class DeviceRunner:
             one = hiprt.Stream()
             for sl in self.slots:
                 sl.main = sl.s_lid = sl.s_blk = sl.s_c4 = sl.s_c4blk = sl.s_h2d = sl.s_d2h = one
-        elif self.stream_layout == "4":
-            for sl in self.slots:
-                sl.main = sl.s_c4 = sl.s_d2h = hiprt.Stream()
-                sl.s_blk = sl.s_lid = sl.s_c4blk = sl.s_h2d = hiprt.Stream(priority=blk_prio)
-        elif self.stream_layout == "4c":
-            side, copy = hiprt.Stream(priority=blk_prio), hiprt.Stream()
-            for sl in self.slots:
-                sl.main = sl.s_c4 = hiprt.Stream()
-                sl.s_blk = sl.s_lid = sl.s_c4blk = side
-                sl.s_h2d = sl.s_d2h = copy
-        elif self.stream_layout == "4f":
-            # per slot: compute + side; the side stream also carries the slot's copies in both
-            # directions (D2H after the batch's completion event)
-            for sl in self.slots:
-                sl.main = sl.s_c4 = hiprt.Stream()
-                sl.s_blk = sl.s_lid = sl.s_c4blk = sl.s_h2d = sl.s_d2h = hiprt.Stream(priority=blk_prio)
-        elif self.stream_layout == "5":
-            copy = hiprt.Stream()
-            for sl in self.slots:
-                sl.main = sl.s_c4 = hiprt.Stream()
-                sl.s_blk = sl.s_lid = sl.s_c4blk = hiprt.Stream(priority=blk_prio)
-                sl.s_h2d = sl.s_d2h = copy
-        elif self.stream_layout == "6":
-            h2d, d2h = hiprt.Stream(), hiprt.Stream()
-            for sl in self.slots:
-                sl.main = sl.s_c4 = hiprt.Stream()
-                sl.s_blk = sl.s_lid = sl.s_c4blk = hiprt.Stream(priority=blk_prio)
-                sl.s_h2d, sl.s_d2h = h2d, d2h
         else:
             h2d, d2h = hiprt.Stream(), hiprt.Stream()
             for sl in self.slots:
-                sl.main = hiprt.Stream()
-                sl.s_lid = hiprt.Stream()
-                sl.s_blk = hiprt.Stream(priority=blk_prio)
-                sl.s_c4 = hiprt.Stream()
-                sl.s_c4blk = hiprt.Stream(priority=blk_prio)
+                sl.main = sl.s_c4 = hiprt.Stream()
+                sl.s_blk = sl.s_lid = sl.s_c4blk = hiprt.Stream(priority=blk_prio)
                 sl.s_h2d, sl.s_d2h = h2d, d2h
         init = self.slots[0].main
         with hiprt.stream(init):
@@ -523,79 +475,71 @@ class DeviceRunner:
             self.c4_ts = {i: self._to_dev(h.build_c4(steps_native[i])) for i in plan.c4_steps}
             self.has_lid = any(steps_native[i].kind == h.StepKind.LanguageDetection
                                for st in plan.stages for i in st)
-            self.lid_P = self.lid_b = self.lid_E = self.lid_WT = None
-            self.lid_version = 0
+            self.lid_b = self.lid_E = self.lid_WT = None
             self.lid_w_scale = 0.0
             if self.has_lid:
                 if langid is None:
                     raise DeviceError("LanguageDetectionFilter needs a language-id model")
-                self.lid_version = langid.version
                 self.lid_b = hiprt.to_device(np.ascontiguousarray(langid.b, dtype=np.float32))
-                if langid.version == 3:
-                    # v3: int8 embedding rows, biased to E + 128 as bytes for the kernel's SWAR sums
-                    # (2 MB, L2-resident), + the bf16 MFMA head operand
-                    self.lid_E = hiprt.to_device((langid.E.astype(np.int16) + 128).astype(np.uint8))
-                    self.lid_aux = self.k.langid_prepare(self.lid_E)  # 1-/2-gram pair table
-                    self.lid_WT = hiprt.to_device(np.ascontiguousarray(langid.head_bf16_t()).reshape(-1))
-                    self.lid_w_scale = float(langid.w_scale)
-                else:
-                    # v2: int16 logit rows of the hashed n-grams (1 MB, L2-resident)
-                    self.lid_P = hiprt.to_device(np.ascontiguousarray(langid.P, dtype=np.int16))
+                # int8 embedding rows, biased to E + 128 as bytes for the kernel's SWAR sums
+                # (2 MB, L2-resident), + the bf16 MFMA head operand
+                self.lid_E = hiprt.to_device((langid.E.astype(np.int16) + 128).astype(np.uint8))
+                self.lid_aux = self.k.langid_prepare(self.lid_E)  # 1-/2-gram pair table
+                self.lid_WT = hiprt.to_device(np.ascontiguousarray(langid.head_bf16_t()).reshape(-1))
+                self.lid_w_scale = float(langid.w_scale)
             self.c4_growth = int(h.C4_MAX_GROWTH)
-            # TB_GATE=0 disables step gating (every pass runs over every document)
-            self.gating = os.environ.get("TB_GATE", "1") not in ("", "0")
+            # gate=0 disables step gating (every pass runs over every document)
+            self.gating = tu.gate
             self.passes, self.pass_of_step, gates = plan_passes(
-                plan, self.stage_layout, steps_native, self.gating,
-                os.environ.get("TB_LID_GATE", "1") not in ("", "0") and self.has_lid)
+                plan, self.stage_layout, steps_native, self.gating, tu.lid_gate and self.has_lid)
             self.gate_ts = {p: self._to_dev(b) for p, (b, _) in gates.items()}
             self.bw_dead_max = bw_dead_max(plan, self.passes, self.pass_of_step)
             self.gate_need = {p: need for p, (_, need) in gates.items()}
             # K16: device resolve + output compaction when every step runs on the device
             self.resolve_t = None
-            if os.environ.get("TB_DEVICE_RESOLVE", "1") not in ("", "0"):
+            if tu.device_resolve:
                 blob = build_resolve(plan, self.stage_layout, steps_native)
                 if blob is not None:
                     self.resolve_t = self._to_dev(blob)
                     # int64 fields per document read from each record buffer (launch-time check)
                     self.resolve_need = [w for w, _ in self.stage_layout] + [7] * len(plan.c4_steps)
             # trailing TokenCounter steps with a byte-level BPE tokenizer: counted on the device
-            # after K16 (token_counters: [(step, BpeSpec)]; TB_DEVICE_TOKENS=0 leaves them to the host)
+            # after K16 (token_counters: [(step, BpeSpec)]; device_tokens=0 leaves them to the host)
             self.bpe = []
-            if self.resolve_t is not None and os.environ.get("TB_DEVICE_TOKENS", "1") not in ("", "0"):
+            if self.resolve_t is not None and tu.device_tokens:
                 self.bpe = [(i, self.k.bpe_tables(sp)) for i, sp in (token_counters or [])]
             # B^k for the hashes, shared read-only by both slots: allocated once (longer spans
             # fall back to powmod61 in the kernels)
             with tracing.trace_range("tb.init.pow_table"):
                 self.k.pow_table(1 << 22)
             init.synchronize()  # uploads and the table are complete before any slot stream reads them
-        # LDS arena per document (one wave per workgroup); TB_LDS_BYTES overrides for tuning
-        # the stage kernel's register budget (the one variant built, kernels.hip TB_STAGE_WPE)
+        # LDS arena per document (one wave per workgroup): the stage kernel is built for W
+        # waves/SIMD (tb_stage_waves) = 4 W waves/CU, so 160 KB / 4 W each costs no occupancy
         self.stage_waves = int(self.k.lib.tb_stage_waves())
-        self.lds_bytes = int(os.environ.get("TB_LDS_BYTES", str((163840 // (4 * self.stage_waves)) & ~255)))
-        self.lds_bytes_c4 = int(os.environ.get("TB_LDS_BYTES_C4", str(self.DEFAULT_LDS_BYTES_C4)))
-        if not 0 <= self.lds_bytes_c4 <= 131072:
-            raise DeviceError("TB_LDS_BYTES_C4 must be in [0, 131072]")
+        self.lds_bytes = tu.lds_bytes or (163840 // (4 * self.stage_waves)) & ~255
+        self.lds_bytes_c4 = tu.lds_bytes_c4
         # documents longer than this run one workgroup (4 waves) each instead of one wave
-        self.long_doc_bytes = int(os.environ.get("TB_LONG_DOC_BYTES", str(self.DEFAULT_LONG_DOC_BYTES)))
-        if not 0 <= self.lds_bytes <= 131072:
-            raise DeviceError("TB_LDS_BYTES must be in [0, 131072]")
-        # 48 KB: three long-document workgroups per CU (with the 6-wave register budget of
-        # k_stage_analyze_blk, csrc/hip/kernels.hip TB_BLK_WPE)
-        self.lds_bytes_blk = int(os.environ.get("TB_LDS_BYTES_BLK", str(self.DEFAULT_LDS_BYTES_BLK)))
+        self.long_doc_bytes = tu.long_doc_bytes
+        # three long-document workgroups per CU (with the register budget of k_stage_analyze_blk,
+        # csrc/hip/kernels.hip TB_BLK_WPE)
+        self.lds_bytes_blk = tu.lds_bytes_blk
         self.block_threads = int(self.k.lib.tb_block_threads())  # threads of the long-document workgroups
-        # LDS slice of the split-order workgroups (k_gr_dup_split); TB_LDS_BYTES_DUP for tuning
-        self.lds_bytes_dup = int(os.environ.get("TB_LDS_BYTES_DUP", str(self.lds_bytes_blk)))
+        # LDS slice of the split-order workgroups (k_gr_dup_split)
+        self.lds_bytes_dup = tu.lds_bytes_dup or self.lds_bytes_blk
         # SURVEY 5.7 split: documents longer than this finish their duplicated n-gram orders in one
         # workgroup per order (k_gr_dup_split) instead of one after another in their stage
         # workgroup; 0 disables. Never below the long-document threshold (wave documents cannot
         # export: their arrays may live in LDS).
-        self.split_doc_bytes = int(os.environ.get("TB_SPLIT_DOC_BYTES", str(self.DEFAULT_SPLIT_DOC_BYTES)))
+        self.split_doc_bytes = tu.split_doc_bytes
         if self.split_doc_bytes > 0:
             self.split_doc_bytes = max(self.split_doc_bytes, self.long_doc_bytes)
-        self.pre_doc_bytes = int(os.environ.get("TB_PRE_DOC_BYTES", str(self.DEFAULT_PRE_DOC_BYTES)))
-        # TB_PRE_WCANON=0: the pre-pass documents' word hashing and canonicalisation stay in their
+        # documents of at least this size get their code points and word-break marks
+        # from the multi-workgroup pre-pass (k_pre_*) before their stage workgroup runs; 0
+        # disables. Never below 64 KiB (smaller documents use the packed code point layout).
+        self.pre_doc_bytes = tu.pre_doc_bytes
+        # pre_wcanon=0: the pre-pass documents' word hashing and canonicalisation stay in their
         # stage workgroup (gopher_rep_record) instead of k_pre_wcanon's many workgroups
-        self.pre_wcanon = os.environ.get("TB_PRE_WCANON", "1") not in ("", "0")
+        self.pre_wcanon = tu.pre_wcanon
         if self.pre_doc_bytes > 0:
             self.pre_doc_bytes = max(self.pre_doc_bytes, 65536, self.long_doc_bytes)
         # per stage: (position of its GopherRepetition step, number of split tasks = its duplicated
@@ -607,44 +551,25 @@ class DeviceRunner:
                 st = steps_native[idx[grs[0]]]
                 if st.n_dup + st.n_top > 0:
                     self.gr_split[si] = (grs[0], st.n_dup + st.n_top + 2)
-        self.line_stats_stage = line_stats_stages(plan, self.stage_layout)
-        # wave documents finish their n-gram orders in one wave per (document, order)
-        # (k_gr_split_wave, LDS slice TB_LDS_BYTES_SPLIT); TB_WAVE_SPLIT=0 keeps them in the stage
-        self.wave_split = os.environ.get("TB_WAVE_SPLIT", "1") not in ("", "0")
-        # scratch bytes per text byte (one pass, split documents): devplan.h; TB_SCRATCH_RATE=a,b (or axb)
+        self.line_stats_stage = line_stats_stages(plan, self.stage_layout, tu)
+        # scratch bytes per text byte (one pass, split documents): devplan.h; scratch_rate=a:b
         # overrides for A/B runs (larger only: smaller slices send documents to the CPU path)
-        self.scratch_rates = (int(h.SCRATCH_PER_BYTE), int(h.SCRATCH_PER_BYTE_SPLIT))
-        if os.environ.get("TB_SCRATCH_RATE"):
-            a, b = (int(v) for v in os.environ["TB_SCRATCH_RATE"].replace("x", ",").split(","))
-            self.scratch_rates = (max(a, self.scratch_rates[0]), max(b, self.scratch_rates[1]))
-        # (5 KB = 8 waves/SIMD: 2.68 ms/step vs 2.80 at 6 KB and 3.44 at 4 KB, profiles/r8_wpe/;
-        # round-5 start: 6 KB beat 4 and 8, profiles/r7_ngram/ab_occupancy.txt)
-        self.lds_bytes_split = int(os.environ.get("TB_LDS_BYTES_SPLIT", "5120"))
-        self.ngram_block = os.environ.get("TB_NGRAM_BLOCK", "1") not in ("", "0")
-        # wave documents longer than this take one wave per n-gram order (k_gr_split_wave), the
-        # shorter ones one workgroup per document (k_gr_ngrams: 256 words, ~5.5 bytes per word on
-        # natural text; a document with more words runs the generic code in that workgroup)
-        self.ngram_big_bytes = int(os.environ.get("TB_NGRAM_BIG_BYTES", "1200"))
-        if not 0 <= self.lds_bytes_split <= 65536:
-            raise DeviceError("TB_LDS_BYTES_SPLIT must be in [0, 65536]")
-        if not 0 <= self.lds_bytes_blk <= 131072:
-            # the workgroup kernels also hold static LDS (cross-wave exchange buffers): a 160 KB
-            # dynamic slice does not fit the CU's 160 KB and the launch fails with
-            # HSA_STATUS_ERROR_INVALID_ALLOCATION (measured), so cap it here
-            raise DeviceError("TB_LDS_BYTES_BLK must be in [0, 131072]")
-        # pinned inputs DMA'd in place (no host staging copy); TB_ZERO_COPY=0 forces the copy
-        self.zero_copy = os.environ.get("TB_ZERO_COPY", "1") != "0"
-        # the cooperative-gather bag keeps its sums in registers; LDS holds only the cut offset
-        self.lds_bytes_lid = int(os.environ.get("TB_LDS_BYTES_LID", "256"))
-        if self.lds_bytes_lid < 16:
-            # the language-id kernel runs concurrently with the stage kernels and must not touch
-            # their HBM scratch arena: its working set has to fit its LDS slice
-            raise DeviceError("TB_LDS_BYTES_LID must be >= 16")
-        # TB_PHASE_PROF=1: per-document phase cycle counters (s_memtime stamps) for profiling
-        self.phase_prof = os.environ.get("TB_PHASE_PROF", "") not in ("", "0")
+        self.scratch_rates = (max(int(h.SCRATCH_PER_BYTE), tu.scratch_rate[0]),
+                              max(int(h.SCRATCH_PER_BYTE_SPLIT), tu.scratch_rate[1]))
+        # wave documents finish their n-gram orders in one wave per (document, order)
+        # (k_gr_split_wave) or, below ngram_big_bytes, one workgroup per document (k_gr_ngrams:
+        # 256 words, ~5.5 bytes per word on natural text; a document with more words runs the
+        # generic code in that workgroup)
+        self.lds_bytes_split = tu.lds_bytes_split
+        self.ngram_block = tu.ngram_block
+        self.ngram_big_bytes = tu.ngram_big_bytes
+        # pinned inputs DMA'd in place (no host staging copy); zero_copy=0 forces the copy
+        self.zero_copy = tu.zero_copy
+        # phase_prof=1: per-document phase cycle counters (s_memtime stamps) for profiling
+        self.phase_prof = tu.phase_prof
         self.phase_totals: Dict[str, np.ndarray] = {}
         self.phase_docs: Dict[str, int] = {}
-        self.copy_threads = int(os.environ.get("TB_COPY_THREADS", "8"))
+        self.copy_threads = tu.copy_threads
         self._next_slot = 0
         self._bw_table = None  # (gen, device copy) of the hashed bad-words trie table
         self._bw_fold = None
@@ -798,14 +723,10 @@ class DeviceRunner:
         return d_pre, n_pre
 
     def _langid(self, vb, vo, d_perm, ndocs, scratch, d_soff, rec, width, flags, prof):
-        """Language-id records of a content version: k_langid_mfma (v3: embedding bag + bf16 MFMA
-        head) or k_langid_features (v2: folded logit table)."""
-        if self.lid_version == 3:
-            self.k.langid_mfma(vb, vo, d_perm, ndocs, self.lid_E, self.lid_aux, self.lid_WT, self.lid_w_scale,
-                               self.lid_b, rec, width, prof)
-        else:
-            self.k.langid_features(vb, vo, d_perm, ndocs, scratch, d_soff, self.lid_P, self.lid_b, rec, width, flags,
-                                   self.lds_bytes_lid, prof)
+        """Language-id records of a content version: k_langid_mfma (embedding bag + bf16 MFMA
+        head, one 16-document tile per workgroup; no scratch)."""
+        self.k.langid_mfma(vb, vo, d_perm, ndocs, self.lid_E, self.lid_aux, self.lid_WT, self.lid_w_scale,
+                           self.lid_b, rec, width, prof)
 
     def _scratch_for(self, slot: _Slot, nbytes: int, which: str = "stage"):
         attr = "scratch" if which == "stage" else "scratch_c4"
@@ -897,8 +818,7 @@ class DeviceRunner:
             split = np.zeros(ndocs, bool)
             if self.split_doc_bytes > 0:
                 split |= is_long & (lens > self.split_doc_bytes)
-            if self.wave_split:
-                split |= ~is_long & (lens > self.ngram_big_bytes)
+            split |= ~is_long & (lens > self.ngram_big_bytes)
             rate[split] = r_split
         per_doc = 4096 + rate * (lens + 64)
         per_doc = (per_doc + SCRATCH_ALIGN - 1) // SCRATCH_ALIGN * SCRATCH_ALIGN
@@ -996,7 +916,7 @@ class DeviceRunner:
                     # below skip the documents it filters
                     slot.s_lid.wait_event(ev_pre)
                     with rt.stream(slot.s_lid):
-                        with self._ktimed(keep, "langid_features"):
+                        with self._ktimed(keep, "langid"):
                             for width, prefix in lid_at:
                                 self._langid(vb, vo, d_perm, ndocs, scratch, d_soff, rec[prefix * ndocs:], width,
                                              flags, self._prof_buf(ndocs, keep, f"langid{s}"))
@@ -1056,7 +976,7 @@ class DeviceRunner:
                 if lid_at and not lid_pass:
                     # language ID next to the stage kernels: it writes only its own record columns
                     slot.s_lid.wait_event(ev_pre)
-                    with rt.stream(slot.s_lid), self._ktimed(keep, "langid_features"):
+                    with rt.stream(slot.s_lid), self._ktimed(keep, "langid"):
                         for width, prefix in lid_at:
                             self._langid(vb, vo, d_perm, ndocs, scratch, d_soff, rec[prefix * ndocs:], width,
                                          flags, self._prof_buf(ndocs, keep, f"langid{s}"))
@@ -1065,7 +985,7 @@ class DeviceRunner:
                 if n_long < ndocs:
                     nw = ndocs - n_long
                     gxw = None
-                    if s in self.gr_split and self.wave_split:
+                    if s in self.gr_split:
                         # split mode: the wave documents' n-gram orders run one wave per (document,
                         # order) after the stage kernel (k_gr_split_wave)
                         gxw = rt.zeros(self.k.gr_export_wave_bytes(nw), np.uint8)
@@ -1243,9 +1163,7 @@ class EmulatedRunner:
     the host side of the device pipeline."""
 
     def __init__(self, steps_native, plan: ExecPlan, langid=None, nthreads: int = 8, gating: Optional[bool] = None,
-                 gate_corrupt: int = 0, token_counters=None):
-        import os
-
+                 gate_corrupt: int = 0, token_counters=None, tune: Optional[DeviceTuning] = None):
         h = native.host()
         self.steps = steps_native
         self.plan = plan
@@ -1253,22 +1171,23 @@ class EmulatedRunner:
         self.lid = langid.native() if langid is not None else None
         _, stage_bs = h.build_device_plan(steps_native, plan.stages)
         self.stage_layout = [h.stage_layout(b) for b in stage_bs]
+        tu = tune or tuning.from_env()
         if gating is None:
-            gating = os.environ.get("TB_GATE", "1") not in ("", "0")
+            gating = tu.gate
         self.passes, self.pass_of_step, self.gates = plan_passes(
-            plan, self.stage_layout, steps_native, gating, os.environ.get("TB_LID_GATE", "1") not in ("", "0"))
+            plan, self.stage_layout, steps_native, gating, tu.lid_gate)
         self.bw_dead_max = bw_dead_max(plan, self.passes, self.pass_of_step)
-        self.line_stats_stage = line_stats_stages(plan, self.stage_layout)
+        self.line_stats_stage = line_stats_stages(plan, self.stage_layout, tu)
         # test hook: additionally mark every k-th document dead after the first pass (a wrong
         # device gate), to exercise the resolver's recovery path
         self.gate_corrupt = gate_corrupt
         self.resolve_blob = None
-        if os.environ.get("TB_DEVICE_RESOLVE", "1") not in ("", "0"):
+        if tu.device_resolve:
             self.resolve_blob = build_resolve(plan, self.stage_layout, steps_native)
         self.bpe = []
-        if self.resolve_blob is not None and os.environ.get("TB_DEVICE_TOKENS", "1") not in ("", "0"):
+        if self.resolve_blob is not None and tu.device_tokens:
             self.bpe = list(token_counters or [])
-        self.dict_marks = dict_marks_wanted(plan, steps_native)
+        self.dict_marks = dict_marks_wanted(plan, steps_native, tu)
 
     def run(self, data: np.ndarray, off: np.ndarray, bw: Optional[Dict[int, BwInput]] = None) -> DeviceResult:
         import time

@@ -30,6 +30,8 @@ from ..config.pipeline import PipelineConfig
 from ..errors import ConfigError, DeviceError, Unexpected
 from ..utils import tracing
 from .plan import ExecPlan, build_plan
+from . import tuning
+from .tuning import DeviceTuning
 
 # per-document device flag bits (csrc/common/docproc.h DocFlag)
 DOC_NEEDS_CPU = 1
@@ -113,7 +115,8 @@ class Engine:
                  tokenizer_dir: Optional[str] = None, badwords_dir: Optional[str] = None,
                  keep_reasons: bool = False, tokenizer_file: Optional[str] = None,
                  fault_inject: Optional[str] = None, tokenizers=None, badwords=None,
-                 max_batch_bytes: Optional[int] = None, slots: Optional[int] = None):
+                 max_batch_bytes: Optional[int] = None, slots: Optional[int] = None,
+                 tune: Optional[DeviceTuning] = None):
         self.cfg = cfg
         self._cpu_engine = None
         self._n_submitted = 0
@@ -125,11 +128,13 @@ class Engine:
         # batches' resolve / assembly on the consumer thread (the native pools do the heavy part)
         self._deleg_pool = None
         self._async_delegation = False
-        # process_many on the GPU backend submits from a helper thread (TB_PREFETCH_THREAD=0: off)
-        self.prefetch_threads = os.environ.get("TB_PREFETCH_THREAD", "1") not in ("", "0")
+        # device operating points (pipeline/tuning.py; TB_TUNE, run --batch-bytes / --slots)
+        self.tune = (tune or tuning.from_env()).replace(batch_bytes=max_batch_bytes or None, slots=slots or None)
+        # process_many on the GPU backend submits from a helper thread (prefetch_thread=0: off)
+        self.prefetch_threads = self.tune.prefetch_thread
         # text bytes per device batch (scratch 80-176 B per text byte per in-flight slot: 384 MB of
         # text -> at most ~85 GB of HBM per slot, three slots in flight on a 288 GB MI355X)
-        self.max_batch_bytes = int(max_batch_bytes or os.environ.get("TB_MAX_BATCH_BYTES", str(384 << 20)))
+        self.max_batch_bytes = int(self.tune.batch_bytes)
         self.h = native.host()
         self.plan: ExecPlan = build_plan(cfg)
         self.steps = [self.h.make_step(s.native_dict()) for s in cfg.pipeline]
@@ -183,7 +188,7 @@ class Engine:
             from .device import EmulatedRunner
 
             self.device_runner = EmulatedRunner(self.steps, self.plan, self.langid, self.nthreads,
-                                                token_counters=token_counters)
+                                                token_counters=token_counters, tune=self.tune)
         if backend == "cuda":
             for st in self.steps:
                 ok, why = self.h.device_supported(st)
@@ -194,7 +199,7 @@ class Engine:
             with tracing.trace_range("tb.init.device_runner"):
                 self.device_runner = DeviceRunner(self.steps, self.plan, device or "cuda", self.langid,
                                                   max_batch_bytes=self.max_batch_bytes, token_counters=token_counters,
-                                                  slots=slots, host_threads=self.nthreads)
+                                                  host_threads=self.nthreads, tune=self.tune)
 
     # ------------------------------------------------------------------------------------------
     def process(self, data: np.ndarray, off: np.ndarray, meta: Optional[Tuple] = None,

@@ -10,7 +10,7 @@ Work decomposition
   competing-consumer equivalent of the reference's work queue (worker_logic.rs:241-283,
   utils/common.rs:91-94 ``basic_qos``): a rank whose documents cost more per byte (very long
   documents run at a fraction of the short-document rate on the GPU) or whose GPU is busier
-  takes fewer groups, so the ranks finish together. ``TB_SCHEDULE=static`` restores contiguous
+  takes fewer groups, so the ranks finish together. ``run --schedule static`` restores contiguous
   ranges balanced by bytes (``parallel.dist.shard_ranges``). Documents never cross GPUs.
 
 Per rank, four stages overlap (bounded queues, the heavy native calls release the GIL):
@@ -86,16 +86,15 @@ class RunConfig:
     metrics_port: Optional[int] = None
     progress_interval: float = 1.0
     tokenizer_file: Optional[str] = None
-    # row groups decoded / units encoded concurrently; None: TB_READ_THREADS / TB_WRITE_THREADS,
-    # else the rank's thread budget when it is pinned to a CPU set (parallel/placement.py), else 8 / 4
+    # row groups decoded / units encoded concurrently; None: the rank's thread budget when it is pinned to a CPU set (parallel/placement.py), else 8 / 4
     read_threads: Optional[int] = None
     write_threads: Optional[int] = None
     claim_ahead: Optional[int] = None    # groups a rank may hold ahead of its main loop (default readers + 3)
-    batch_bytes: Optional[int] = None    # device batch bytes (default 384 MB; TB_MAX_BATCH_BYTES)
-    slots: Optional[int] = None          # device batches in flight (default: auto, 3 when HBM allows; TB_SLOTS)
+    batch_bytes: Optional[int] = None    # device batch bytes (default 384 MB; TB_TUNE batch_bytes)
+    slots: Optional[int] = None          # device batches in flight (default: auto, 3 when HBM allows; TB_TUNE slots)
     fault_inject: Optional[str] = None   # debug: "kernel@N" / "oom@N" (N = 1-based batch), "rank@N[:R]",
                                          # "slow@SECONDS[:R]" (rank R sleeps after every unit)
-    schedule: str = os.environ.get("TB_SCHEDULE", "dynamic")  # dynamic (shared cursor) | static (ranges)
+    schedule: str = "dynamic"            # dynamic (shared cursor) | static (byte-balanced ranges)
 
 
 @dataclasses.dataclass
@@ -592,8 +591,8 @@ def _sort_by_row(tbl: pa.Table, rows: np.ndarray) -> pa.Table:
 
 
 def resolve_threads(rc: RunConfig):
-    """(pool, readers, writers) of this rank: explicit settings first (RunConfig, then the
-    TB_THREADS / TB_READ_THREADS / TB_WRITE_THREADS env), then the thread budget of the CPU set
+    """(pool, readers, writers) of this rank: explicit settings first (RunConfig / the CLI, and
+    TB_THREADS for the pool), then the thread budget of the CPU set
     the rank is pinned to (placement.thread_budget: all three within its CPUs), else the
     one-rank defaults (pool = the process's CPU share, 8 readers, 4 writers)."""
     from .parallel import placement
@@ -605,14 +604,14 @@ def resolve_threads(rc: RunConfig):
     def pick(v, env, dflt):
         if v is not None:
             return int(v)
-        e = os.environ.get(env)
+        e = os.environ.get(env) if env else None
         if e and e.isdigit() and int(e) > 0:
             return int(e)
         return dflt
 
     pool = pick(rc.threads, "TB_THREADS", bud.pool if bud else default_threads())
-    read = pick(rc.read_threads, "TB_READ_THREADS", bud.read if bud else 8)
-    write = pick(rc.write_threads, "TB_WRITE_THREADS", bud.write if bud else 4)
+    read = pick(rc.read_threads, None, bud.read if bud else 8)
+    write = pick(rc.write_threads, None, bud.write if bud else 4)
     return pool, read, write
 
 
@@ -678,7 +677,7 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     claimed: List[int] = []
     # groups a rank may hold ahead of its main loop: enough for the decode threads and the
     # engine's batches in flight
-    ahead = rc.claim_ahead if rc.claim_ahead is not None else int(os.environ.get("TB_CLAIM_AHEAD", "0") or 0)
+    ahead = rc.claim_ahead or 0
     gate = _ClaimGate(ahead if ahead > 0 else rc.read_threads + 3)
     if rc.schedule == "static":
         groups_it = unit_groups([u for u in mine if u.index not in done])
@@ -725,11 +724,6 @@ def run(rc: RunConfig, ctx: Optional[DistContext] = None, cfg: Optional[Pipeline
     except BaseException:
         source.close()
         raise
-    # TB_PINNED_READ=1: readers copy each decoded batch into a pinned engine buffer (zero-copy
-    # upload). Off by default: the reader threads are this path's bottleneck and the extra copy
-    # there costs more than the staging copy it saves (profiles/r8_e2e/ab_pinned_read.txt)
-    if engine.backend == "cuda" and os.environ.get("TB_PINNED_READ", "0") not in ("", "0"):
-        reader.host_buffer = engine.host_buffer
     log.info("rank %d/%d: schedule=%s, %d units already done, backend=%s, CPUs %s, threads: pool %d, "
              "readers %d, writers %d", rank, world, rc.schedule, local.units_skipped, engine.backend,
              os.environ.get("TB_CPU_SET", "(not pinned)"), engine.nthreads, rc.read_threads, rc.write_threads)

@@ -65,7 +65,7 @@ def reliability(model, gran="sentence"):
 
 def report(res, rel=None) -> str:
     lines = ["# Language-id evaluation (held-out set)", "",
-             "Model: `textblaster_amd/models/data/langid_v2.npz` (hashed char 1-4-gram int16 logit table),",
+             "Model: `textblaster_amd/models/data/langid_v3.npz` (fastText int8 two-bag embedding + bf16 MFMA head),",
              "trained by `tools/train_langid.py` on `models/data/langid_corpus/` (~260-300 hand-written lines",
              "per language, ~20-25 KB each). Evaluation text: `textblaster_amd/models/data/langid_eval/`",
              "(110 parallel sentences per language, no overlap with the training corpus, not generated from",

@@ -9,10 +9,11 @@
 #   tests=K     pytest -m gpu -k K (a subset)                                    -> pytest.log
 #   bench       bench.py --steps $STEPS --warmup $WARMUP $BENCH_ARGS (the driver's 20 / 5)  -> bench.json
 #   prof        serialized-stream kernel trace (exclusive kernel times, tools/prof_summary.py)
-#               + TB_PHASE_PROF=1 per-phase wave cycles                          -> kernels_serialized.txt, phase_cycles.txt
+#               + TB_TUNE=phase_prof=1 per-phase wave cycles                         -> kernels_serialized.txt, phase_cycles.txt
 #   pmc         PMC counter passes (one rocprofv3 run per counter group, no tracing) -> pmc_per_kernel.txt
-#   ab          interleaved A/B of env settings: AB="A1=x,A2=y B1=z" (space-separated settings,
-#               comma-separated assignments), REPS repetitions, serialized kernel stats + bench each
+#   ab          interleaved A/B of env settings: AB="TB_TUNE=slots=2,streams=6;TB_HIP_LIB=x.so TB_TUNE=slots=3"
+#               (space-separated settings, ';'-separated env assignments), REPS repetitions,
+#               serialized kernel stats + bench each
 #   timeline    kernel + memory-copy trace of a few steps (tools/prof_summary.py per-step timeline)
 #   e2e         Parquet -> Parquet end to end (tools/e2e_bench.py $E2E_ARGS)   -> e2e.json
 # env: OUT (default r), STEPS (bench steps, 20), WARMUP (5), BENCH_ARGS (extra bench.py args, also used by
@@ -27,8 +28,11 @@ STEPS=${STEPS:-20}
 WARMUP=${WARMUP:-5}
 
 kstats() {  # kstats <dir> <log> [env...]: serialized kernel trace of a short bench
-  local dir=$1 log=$2; shift 2
-  (cd /tmp && export TMPDIR=/tmp && env "$@" TB_SERIAL_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+  local dir=$1 log=$2 a tune="" envs=(); shift 2
+  for a in "$@"; do  # one stream for everything (exclusive kernel times) on top of the setting's TB_TUNE
+    if [[ $a == TB_TUNE=* ]]; then tune=${a#TB_TUNE=}; else envs+=("$a"); fi
+  done
+  (cd /tmp && export TMPDIR=/tmp && env "${envs[@]}" TB_TUNE="streams=serial${tune:+,$tune}" timeout -k 10 300 rocprofv3 --kernel-trace --stats \
     --output-format csv -d "$dir" -o k -- python3 "$REPO/bench.py" --steps 4 --warmup 1 $BENCH_ARGS) > "$log" 2>&1
 }
 
@@ -64,7 +68,7 @@ step_prof() {
   python3 tools/prof_summary.py "$(find "$D/serial" -name '*kernel_trace.csv' | head -1)" > "$D/kernels_serialized.txt" 2>&1
   find "$D/serial" -name '*kernel_trace.csv' -delete
   head -14 "$D/kernels_serialized.txt"
-  TB_PHASE_PROF=1 timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 $BENCH_ARGS > "$D/phase_bench.json" \
+  TB_TUNE=phase_prof=1 timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 $BENCH_ARGS > "$D/phase_bench.json" \
     2> "$D/phase_cycles.txt" || { tail -5 "$D/phase_cycles.txt"; return 1; }
   grep -v amdgpu.ids "$D/phase_cycles.txt" | head -30
 }
@@ -97,7 +101,7 @@ step_ab() {
     for S in $AB; do
       i=$((i + 1))
       local E
-      E=$(echo "$S" | tr ',' ' ')
+      E=$(echo "$S" | tr ';' ' ')
       kstats "$D/ab_r${rep}_$i" "$D/ab_r${rep}_$i.log" $E || { tail -5 "$D/ab_r${rep}_$i.log"; return 1; }
       local T
       T=$(find "$D/ab_r${rep}_$i" -name '*kernel_trace.csv' | head -1)

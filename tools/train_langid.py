@@ -5,7 +5,7 @@ fastText classifier. Hashed character 1..4-grams (65536 buckets) -> a D = 32 mea
 vector: two 16-dim bags over one int8 embedding table of 16 values per bucket (16 bytes per
 gather), the 1- and 2-grams summed into dims 0..15, the 3- and 4-grams into dims 16..31 ->
 linear head 32 -> 5 languages -> softmax. Training: (1) the convex problem first — the
-mean-mode table T of per-bucket logits (the head folded in, = the v2 model in float); (2)
+mean-mode table T of per-bucket logits (the head folded in); (2)
 lifted to D = 32: a seeded Gaussian head W0 = [W_lo; W_hi] (each 16 x 5) and the minimum-norm
 E[g] with E[g] W_lo = E[g] W_hi = T[g] (16 unknowns, 10 equations: [W_lo W_hi] has full column
 rank), so every gram's row maps back to its logits exactly whichever half it feeds;
@@ -18,7 +18,6 @@ partial sum is an integer below 2^24, so the MFMA's fp32 result is exact and the
 reproduces it bit for bit.
 
     python tools/train_langid.py [--epochs 12] [--n 10000] [--out path]
-    python tools/train_langid.py --table      # the v2 folded int16 logit table (langid_v2.npz)
 
 Training text: the hand-written sentences in models/data/langid_corpus/<lang>.txt (whole
 sentences, runs of sentences and sentence fragments). The held-out evaluation
@@ -80,7 +79,7 @@ def train_folded(feats, labels, h, epochs):
     bias = torch.nn.Parameter(torch.zeros(len(LANGS)))
     opt = torch.optim.Adam(list(table.parameters()) + [bias], lr=0.02)
     lossf = torch.nn.CrossEntropyLoss(label_smoothing=0.1)
-    lim = 32767.0 / h.LID_SCALE
+    lim = 32767.0 / 1024.0  # |logit contribution| bound of the folded table (int16 / 1024)
     for ep in range(epochs):
         tot = 0.0
         for idx, flat, offs in batches(feats, labels, 256, torch.randperm(len(feats))):
@@ -93,16 +92,6 @@ def train_folded(feats, labels, h, epochs):
             tot += loss.item() * len(idx)
         print(f"epoch {ep} loss {tot / len(feats):.4f}", flush=True)
     return table.weight.detach().numpy().astype(np.float64), bias.detach().numpy().astype(np.float64)
-
-
-def train_table(feats, labels, h, epochs):
-    """v2: the folded table exported as int16 fixed point (scale 1/1024) + bias."""
-    T, b0 = train_folded(feats, labels, h, epochs)
-    P = np.zeros((h.LID_BUCKETS, h.LID_ROW), dtype=np.int16)
-    P[:, :len(LANGS)] = np.clip(np.rint(T * h.LID_SCALE), -32767, 32767).astype(np.int16)
-    b = np.zeros(h.LID_ROW, dtype=np.float32)
-    b[:len(LANGS)] = b0
-    return {"P": P.reshape(-1), "b": b}
 
 
 def train_fasttext(feats, labels, h, epochs, dim, finetune_epochs=0, seed=7):
@@ -122,7 +111,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--epochs", type=int, default=12)
     ap.add_argument("--n", type=int, default=10000)
-    ap.add_argument("--table", action="store_true", help="train the v2 folded int16 logit table instead")
     ap.add_argument("--out", default=None)
     ap.add_argument("--vocab-share", type=float, default=0.0,
                     help="fraction of samples drawn from the synthetic benchmark vocabulary (default 0)")
@@ -135,12 +123,8 @@ def main():
     keep = [i for i, f in enumerate(feats) if len(f)]
     feats = [feats[i] for i in keep]
     labels = torch.tensor([train[i][1] for i in keep])
-    if args.table:
-        arrays = train_table(feats, labels, h, args.epochs)
-        out = args.out or os.path.join(DATA_DIR, "langid_v2.npz")
-    else:
-        arrays = train_fasttext(feats, labels, h, args.epochs, h.LID_DIM)
-        out = args.out or os.path.join(DATA_DIR, "langid_v3.npz")
+    arrays = train_fasttext(feats, labels, h, args.epochs, h.LID_DIM)
+    out = args.out or os.path.join(DATA_DIR, "langid_v3.npz")
     np.savez(out, **arrays)
     print("saved", out, os.path.getsize(out))
 

@@ -785,19 +785,64 @@ std::vector<std::unique_ptr<CharBuf>>* g_charbufs = new std::vector<std::unique_
 
 // Every metadata key a step decision can write (filters.cpp decide_t, step_meta): an input key
 // outside this list cannot be overwritten by a step.
-static bool meta_collides(const FlatMeta& fm) {
+static bool is_step_key(std::string_view k) {
   static const std::string_view kStepKeys[] = {
       "gopher_quality_filter_status", "gopher_quality_filter_reasons", "gopher_repetition_filter_status",
       "gopher_repetition_filter_reasons", "gopher_repetition_filter_reason", "c4_filter_status",
       "c4_filter_reasons", "line-filter-too_long_word", "line-filter-no_terminal_punc",
       "line-filter-too_few_words", "fineweb_filter_status", "fineweb_filter_reason", "Detected language",
       "Detected language confidence", "token_count", "c4_badwords_filter_status", "c4_badwords_filter_reason"};
-  for (const auto& e : fm.e) {
-    const std::string_view k = fm.key(e);
-    for (const auto& sk : kStepKeys)
-      if (k == sk) return true;
-  }
+  for (const auto& sk : kStepKeys)
+    if (k == sk) return true;
   return false;
+}
+
+static bool meta_collides(const FlatMeta& fm) {
+  for (const auto& e : fm.e)
+    if (is_step_key(fm.key(e))) return true;
+  return false;
+}
+
+// Is `s` an input metadata object whose text is already its own canonical serialization: no
+// whitespace, only string members, no byte that json_escape_append would escape (no '\\', no
+// control character), at most 16 members with distinct keys none of which a step writes? Then
+// parse_meta_json + append_json would reproduce `s` byte for byte, and the output metadata is
+// `s` without its closing brace followed by the steps' members. `inner` = the members' text.
+static bool canonical_meta(std::string_view s, std::string_view& inner) {
+  const size_t n = s.size();
+  if (n < 2 || s[0] != '{' || s[n - 1] != '}') return false;
+  inner = s.substr(1, n - 2);
+  if (n == 2) return true;
+  std::string_view keys[16];
+  int nk = 0;
+  size_t i = 1;
+  // one quoted string without escapes at s[i]; returns its contents
+  auto str = [&](std::string_view& out) -> bool {
+    if (i >= n || s[i] != '"') return false;
+    const size_t a = ++i;
+    while (i < n) {
+      const unsigned char c = (unsigned char)s[i];
+      if (c == '"') break;
+      if (c < 0x20 || c == '\\') return false;
+      ++i;
+    }
+    if (i >= n) return false;
+    out = s.substr(a, i - a);
+    ++i;
+    return true;
+  };
+  while (true) {
+    std::string_view k, v;
+    if (!str(k) || i >= n || s[i] != ':') return false;
+    ++i;
+    if (!str(v) || nk == 16 || is_step_key(k)) return false;
+    for (int j = 0; j < nk; ++j)
+      if (keys[j] == k) return false;
+    keys[nk++] = k;
+    if (i == n - 1) return true;  // the closing brace
+    if (s[i] != ',') return false;
+    ++i;
+  }
 }
 
 static std::unique_ptr<CharBuf> take_charbuf() {
@@ -876,6 +921,27 @@ void BatchState::assemble(const std::vector<int64_t>& idx, RawBuf& text_data, st
             meta_valid[k] = 1;
           }
           continue;
+        }
+        if (has_input && fast_meta) {
+          std::string_view inner;
+          const std::string_view raw(meta_data_ + meta_off_[i], (size_t)(meta_off_[i + 1] - meta_off_[i]));
+          if (canonical_meta(raw, inner)) {
+            // the input members as they are (their text is canonical), then the steps' members
+            const size_t before = md.size();
+            md.push_back('{');
+            md.append(inner.data(), inner.size());
+            bool first = inner.empty();
+            for (int s = 0; s <= last; ++s) step_meta_json(i, s, md, first);
+            if (first) {
+              md.resize(before);
+              meta_off[k + 1] = 0;
+            } else {
+              md.push_back('}');
+              meta_off[k + 1] = (int64_t)(md.size() - before);
+              meta_valid[k] = 1;
+            }
+            continue;
+          }
         }
         if (has_input) {
           if (!input_meta(i, fm)) meta_fail_.fetch_add(1, std::memory_order_relaxed);

@@ -69,7 +69,11 @@ def test_direct_json_metadata_with_input_metadata(monkeypatch):
     texts = synth.make_corpus(600, 600, seed=22)
     data, off = synth.pack(texts)
     kinds = ['{"url":"https://example.com/%d"}', '{}', 'not json', '{"c4_filter_status":"x","a":"b"}',
-             '{"Detected language":"xx"}', '{"k\\"q":"v\\\\n\\u00e6 \\u4e2d"}', '{"a":"1","b":"2","c":"3"}', None]
+             '{"Detected language":"xx"}', '{"k\\"q":"v\\\\n\\u00e6 \\u4e2d"}', '{"a":"1","b":"2","c":"3"}', None,
+             # the canonical-text splice must fall back for every non-canonical form
+             '{ "a": "1" }', '{"a":"1","a":"2"}', '{"a":1}', '{"a":"æ 中 ü","b":""}', '{"a":"x\ty"}', '{"a":"1",}',
+             '{"":""}', '{"a":"1"}}', '{"a":"1","token_count":"3"}', "{" + ",".join(f'"k{j}":"v"' for j in range(17)) + "}",
+             "{" + ",".join(f'"k{j}":"v"' for j in range(16)) + "}"]
     metas = [kinds[i % len(kinds)] for i in range(len(texts))]
     enc = [(m % i if "%d" in m else m).encode() if m is not None else b"" for i, m in enumerate(metas)]
     mo = np.zeros(len(enc) + 1, dtype=np.int64)

@@ -29,6 +29,8 @@ enum : int {
   PH_START = 0, PH_DECODE, PH_DICT, PH_PREFIX_HASH, PH_WORDS, PH_LINES, PH_GQ, PH_GR_LINES, PH_GR_WORDS,
   PH_GR_TOP, PH_GR_DUP, PH_FW, PH_LID, PH_GR_DUP_WALK, PH_GR_DUP_CANON, PH_GR_TOP_CANON,
   PH_C4_LOREM = 16, PH_C4_DECODE, PH_C4_LINES, PH_C4_CITE, PH_C4_WORDS, PH_C4_CODES, PH_C4_JOIN, PH_C4_SENT,
+  // sub-phases of the stage kernel's GopherRepetition / GopherQuality work
+  PH_GR_NL = 24, PH_GR_LINE_DUP, PH_GR_WH, PH_GR_WCANON, PH_GQ_WORDS, PH_GQ_BYTES,
   kPhaseSlots = 32
 };
 
@@ -293,6 +295,37 @@ struct DocCtx {
 };
 
 TB_HD bool is_ws(uint32_t p) { return (p & P_WS) != 0; }
+
+// [tcs, tce): the code points of [0, C) without leading / trailing whitespace (tcs >= tce: all
+// whitespace). One wave searches chunk by chunk from each end and stops at the first chunk with a
+// non-whitespace code point (usually the first and the last chunk) instead of reducing over all
+// code points.
+template <class P, class PA>
+TB_HD void trim_span(DocCtx<P>& x, const PA& prop, uint32_t C, uint32_t& tcs, uint32_t& tce) {
+#if defined(__HIPCC__)
+  if constexpr (P::kWaves == 1) {
+    const uint32_t lane = x.par.lane;
+    tcs = C;
+    for (uint32_t base = 0; base < C; base += 64) {
+      const uint32_t j = base + lane;
+      const uint64_t m = __ballot(j < C && !is_ws(prop[j]));
+      if (m) { tcs = base + (uint32_t)__builtin_ctzll(m); break; }
+    }
+    tce = 0;
+    if (tcs < C) {
+      for (uint32_t base = (C - 1) & ~63u;; base -= 64) {
+        const uint32_t j = base + lane;
+        const uint64_t m = __ballot(j < C && !is_ws(prop[j]));
+        if (m) { tce = base + (uint32_t)(64 - __clzll((long long)m)); break; }
+        if (base == 0) break;
+      }
+    }
+    return;
+  }
+#endif
+  tcs = x.par.template min<uint32_t>(C, C, [&](uint32_t i) { return is_ws(prop[i]) ? C : i; });
+  tce = x.par.template max<uint32_t>(C, 0u, [&](uint32_t i) { return is_ws(prop[i]) ? 0u : i + 1; });
+}
 // Wave documents with fewer words than this keep n-gram canonical ids in 16 bits (every
 // canonicalisation slot index < 1.5 n + 2 fits); more words send the document to the CPU path.
 constexpr uint32_t kWave16 = 43000;
@@ -424,17 +457,12 @@ TB_HD bool word_mark(const PropArr& prop, uint32_t C, uint32_t i) {
 // words() for one wave (WavePar), in one pass over the code points instead of a mark pass and a
 // scan pass: each chunk's packed entries are loaded once (the next chunk's while this one is
 // processed, so the load is off the critical path), the neighbours the break rules look at come
-// from DPP lane moves (wave_shr / wave_shl) plus a two-entry carry, and the word's byte span
-// travels in the scan element, so the emit has no dependent offset loads. Same words as the
-// generic version (word_mark + the WSeg scan).
-struct WSeg5 {
-  uint32_t bits, first, last, fo, lo;  // WSeg + byte offsets of `first` / `last`
+// from DPP lane moves (wave_shr / wave_shl) plus a two-entry carry, and each word's extent comes
+// from bit operations on the chunk's ballots (no segmented scan). Same words as the generic
+// version (word_mark + the WSeg scan).
+struct WSeg5 {  // the segment still open at a chunk's end
+  uint32_t bits, first, last, fo, lo;  // WSeg bits + byte offsets of `first` / `last`
 };
-__device__ __forceinline__ WSeg5 wseg5_op(const WSeg5& a, const WSeg5& b) {
-  if (b.bits & 1u) return b;
-  return WSeg5{a.bits | (b.bits & 6u), a.first < b.first ? a.first : b.first, a.last > b.last ? a.last : b.last,
-               a.fo < b.fo ? a.fo : b.fo, a.lo > b.lo ? a.lo : b.lo};
-}
 __device__ __forceinline__ uint32_t lane_prev(uint32_t v) {  // lane l gets lane l-1 (lane 0: v)
   return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x138, 0xF, 0xF, false);
 }
@@ -500,30 +528,63 @@ __device__ Words words_wave(DocCtx<P>& x, const Cps& c, const uint32_t* marks) {
       if (j < C && ((hm[j >> 5] >> (j & 31)) & 1u)) mk = ((marks[j >> 5] >> (j & 31)) & 1u) != 0;
       if (i64 < C && ((hm[i64 >> 5] >> (i64 & 31)) & 1u)) mk64 = ((marks[i64 >> 5] >> (i64 & 31)) & 1u) != 0;
     }
-    const uint64_t M = __ballot(mk);
-    const bool mnext = lane == 63 ? mk64 : (((M >> (lane + 1)) & 1ull) != 0 || j + 1 >= C);
+    // Segment aggregates from ballots instead of a scan: a lane's segment runs from the last mark
+    // at or below it (or, with none, from an earlier chunk: the carry); its first / last
+    // non-whitespace code point and its word-character / alphabetic bits are bit operations on
+    // the chunk's masks, the byte offsets two lane reads (ds_bpermute).
+    const bool valid = j < C;
     const bool ws = is_ws(cp);
-    WSeg5 e;
-    e.bits = (mk ? 1u : 0u) | ((!(cp & P_PUNCT) && !ws) ? 2u : 0u) | ((cp & P_ALPHA) ? 4u : 0u);
-    e.first = ws ? kNone : j;
-    e.last = ws ? 0u : j + 1;
-    e.fo = ws ? kNone : co;
-    e.lo = ws ? 0u : on;
-    if (j >= C) e = WSeg5{0u, kNone, 0u, kNone, 0u};
-    const WSeg5 xs = pardetail::wave_incl_scan(e, lane, wseg5_op);
-    const WSeg5 incl = wseg5_op(carry, xs);
-    const bool sel = j < C && mnext && (incl.bits & 2u);
+    const uint64_t M = __ballot(mk);  // (mk implies j < C)
+    const uint64_t NW = __ballot(valid && !ws);
+    const uint64_t WC = __ballot(valid && !ws && !(cp & P_PUNCT));
+    const uint64_t AL = __ballot(valid && (cp & P_ALPHA));
+    const bool mnext = lane == 63 ? mk64 : (((M >> (lane + 1)) & 1ull) != 0 || j + 1 >= C);
+    const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes 0 .. lane
+    const uint64_t mb = M & le;
+    const bool fc = mb == 0;  // the segment began in an earlier chunk
+    const uint64_t seg = fc ? le : (le & (~0ull << (63 - __clzll((long long)mb))));
+    const uint64_t nws = NW & seg;
+    const bool hasw = (WC & seg) != 0 || (fc && (carry.bits & 2u));
+    const int f = nws ? __builtin_ctzll(nws) : 0;
+    const int l = nws ? 63 - __clzll((long long)nws) : 0;
+    const uint32_t fo_l = (uint32_t)__shfl((int)co, f);
+    const uint32_t lo_l = (uint32_t)__shfl((int)on, l);
+    const bool sel = valid && mnext && hasw;
     const uint64_t sm = __ballot(sel);
     if (sel) {
       const uint32_t q = k + (uint32_t)__popcll(sm & lt);
-      cs[q] = incl.first;
-      ce[q] = incl.last;
-      bs[q] = incl.fo;
-      be[q] = incl.lo;
-      al[q] = (incl.bits & 4u) ? 1 : 0;
+      const bool cf = fc && carry.first != kNone;
+      cs[q] = cf ? carry.first : base + (uint32_t)f;
+      bs[q] = cf ? carry.fo : fo_l;
+      ce[q] = nws ? base + (uint32_t)l + 1u : carry.last;
+      be[q] = nws ? lo_l : carry.lo;
+      al[q] = ((AL & seg) != 0 || (fc && (carry.bits & 4u))) ? 1 : 0;
     }
     k += (uint32_t)__popcll(sm);
-    carry = wseg5_op(carry, pardetail::bcast63(xs));
+    {  // carry: the segment open at the chunk's end (uniform)
+      const bool rs = M != 0;
+      const uint64_t sg = rs ? (~0ull << (63 - __clzll((long long)M))) : ~0ull;
+      const uint64_t nwc = NW & sg;
+      const uint32_t keep = rs ? 0u : carry.bits;
+      carry.bits = (keep & 6u) | ((WC & sg) ? 2u : 0u) | ((AL & sg) ? 4u : 0u);
+      if (rs || carry.first == kNone) {
+        if (nwc) {
+          const int f2 = __builtin_ctzll(nwc);
+          carry.first = base + (uint32_t)f2;
+          carry.fo = (uint32_t)__builtin_amdgcn_readlane((int)co, f2);
+        } else {
+          carry.first = kNone;
+        }
+      }
+      if (nwc) {
+        const int l2 = 63 - __clzll((long long)nwc);
+        carry.last = base + (uint32_t)l2 + 1u;
+        carry.lo = (uint32_t)__builtin_amdgcn_readlane((int)on, l2);
+      } else if (rs) {
+        carry.last = 0u;
+        carry.lo = 0u;
+      }
+    }
     c2 = l62;
     c1 = l63;
     cp = np;
@@ -898,13 +959,15 @@ TB_HD void lower_bytes(const UcdView& ucd, const Cps& cv, uint32_t s, uint32_t e
   }
 }
 
-TB_HD bool is_stop_word(const UcdView& ucd, const DevStopSet& ss, const Cps& cv, uint32_t s, uint32_t e) {
+// [s, e): the word's code points, [b0, b1): its bytes (Words::bs / be: no offset loads)
+TB_HD bool is_stop_word(const UcdView& ucd, const DevStopSet& ss, const Cps& cv, uint32_t s, uint32_t e,
+                        uint32_t b0, uint32_t b1) {
   // every code point lowercases to at least one byte
   if (ss.n == 0 || (int32_t)(e - s) > ss.max_len) return false;
   if (ss.lite_nslots > 0) {
     // ASCII word of <= 7 bytes (as many bytes as code points): its lowercase bytes are the key
     // of the set's fast table, which holds every ASCII entry of <= 7 bytes (devplan.h)
-    const uint32_t b0 = cv.o(s), nb = cv.o(e) - b0;
+    const uint32_t nb = b1 - b0;
     if (nb <= 7u && nb == e - s) {
       uint64_t key = (uint64_t)nb << 56;
       for (uint32_t k = 0; k < nb; ++k) {
@@ -1280,13 +1343,13 @@ template <class P>
 TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, const Cps& c,
                              const PHView& ph, const Words& w, int64_t* r, bool release_props = false,
                              GrExport* ex = nullptr, const PreDoc* pre = nullptr,
-                             const uint8_t* b_export = nullptr) {
+                             const uint8_t* b_export = nullptr, Lines lines = Lines{}) {
   const uint32_t C = c.n;
   const PropArr prop = c.props();
   const OffArr off = c.offs();
   const int width = ds.width;
-  const uint32_t tcs = x.par.template min<uint32_t>(C, C, [&](uint32_t i) { return is_ws(prop[i]) ? C : i; });
-  const uint32_t tce = x.par.template max<uint32_t>(C, 0u, [&](uint32_t i) { return is_ws(prop[i]) ? 0u : i + 1; });
+  uint32_t tcs, tce;
+  trim_span(x, prop, C, tcs, tce);
   if (tcs >= tce) {
     x.par.single([&]() {
       for (int k = 0; k < width; ++k) r[k] = 0;
@@ -1306,6 +1369,32 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     rs = pre->nl_pos + a;
     rl = pre->nl_len + a;
     NR = e - a;
+  } else if (lines.n > 0) {
+    // From the stage's Rust lines (`lines`: their starts, ls[k] = one past a '\n' for k >= 1):
+    // the line feeds are exactly the code points ls[k] - 1, and a run continues while the next
+    // line is empty (ls[k + 1] == ls[k] + 1). The runs inside the trimmed span [tcs, tce) are
+    // whole (its ends are not whitespace), and the '\n' a text may end with is outside it. One
+    // compaction over the lines instead of one over the code points.
+    const uint32_t* ls = lines.ls;
+    const uint32_t NL = lines.n;
+    // (workgroup documents: HBM, so that split mode can hand them to k_gr_dup_split)
+    rs = P::kWaves == 1 ? x.template alloc_hot<uint32_t>(NL + 1) : x.template alloc<uint32_t>(NL + 1);
+    rl = P::kWaves == 1 ? x.template alloc_hot<uint32_t>(NL + 1) : x.template alloc<uint32_t>(NL + 1);
+    if (x.overflow) return;
+    NR = x.par.template compact<int>(
+        NL,
+        [&](uint32_t k, int&) {
+          if (k == 0) return false;
+          const uint32_t p = ls[k] - 1;
+          return p >= tcs && p < tce && (k == 1 || ls[k - 1] != p);
+        },
+        [&](uint32_t k, uint32_t q, int&) {
+          uint32_t e = k;
+          while (e + 1 < NL && ls[e + 1] == ls[e] + 1) ++e;
+          rs[q] = ls[k] - 1;
+          rl[q] = e - k + 1;
+        });
+    x.par.sync();
   } else {
     rs = x.template alloc<uint32_t>(span + 1);
     rl = x.template alloc<uint32_t>(span + 1);
@@ -1324,7 +1413,8 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
         });
     x.par.sync();
   }
-  uint32_t* prs = x.template alloc<uint32_t>(span + 1);
+  x.stamp(PH_GR_NL);
+  uint32_t* prs = x.template alloc<uint32_t>(NR + 1);
   if (x.overflow) return;
   int64_t line_dup = 0, line_dup_b = 0, para_dup = 0, para_dup_b = 0;
   // split mode: the duplicated line / paragraph statistics go to k_gr_dup_split when everything
@@ -1340,6 +1430,7 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     dup_spans(x, b, ph, NR + 1,
               [&](uint32_t k, uint32_t& s0, uint32_t& e0) { gr_line_span(rs, rl, off, tcs, tce, NR, k, s0, e0); },
               &line_dup, &line_dup_b);
+  x.stamp(PH_GR_LINE_DUP);
   const uint32_t NPR = x.par.template compact<int>(
       NR, [&](uint32_t k, int&) { return rl[k] >= 2; }, [&](uint32_t k, uint32_t q, int&) { prs[q] = k; });
   x.par.sync();
@@ -1407,9 +1498,11 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     if (x.overflow) return;
     x.par.for_n(W, [&](uint32_t k) { wh[k] = span_hash8(x, ph, w.bs[k], w.be[k]); });
     x.par.sync();
+    x.stamp(PH_GR_WH);
     canonicalize(
         x, W, [&](uint32_t k) { return dev_key(wh[k], w.be[k] - w.bs[k]); },
         [&](uint32_t i, uint32_t j) { return bytes_eq<P>(b, w.bs[i], w.be[i], w.bs[j], w.be[j]); }, wid);
+    x.stamp(PH_GR_WCANON);
     const uint32_t totl = x.par.template scan<uint32_t>(
         W, 0u, [](uint32_t a, uint32_t c2) { return a + c2; },
         [&](uint32_t k) { return w.be[k] - w.bs[k]; }, [&](uint32_t k, uint32_t e) { WL[k] = e; });
@@ -2014,8 +2107,8 @@ TB_HD void c4_finish(DocCtx<P>& x, const DevC4& c4, uint32_t n, uint8_t* Jb, uin
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
   const uint32_t JC = jc.n;
   const PropArr jprop = jc.props();
-  const uint32_t tcs = x.par.template min<uint32_t>(JC, JC, [&](uint32_t i) { return is_ws(jprop[i]) ? JC : i; });
-  const uint32_t tce = x.par.template max<uint32_t>(JC, 0u, [&](uint32_t i) { return is_ws(jprop[i]) ? 0u : i + 1; });
+  uint32_t tcs, tce;
+  trim_span(x, jprop, JC, tcs, tce);
   uint32_t nsent = 0, bstart = 0, blen = 0;
   if (tcs < tce) {
     const uint32_t lim = c4.min_num_sentences > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)c4.min_num_sentences;
@@ -2263,8 +2356,8 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
       lb[k] = e;
     });
   } else {
-    const uint32_t tcs = x.par.template min<uint32_t>(C, C, [&](uint32_t i) { return is_ws(prop[i]) ? C : i; });
-    const uint32_t tce = x.par.template max<uint32_t>(C, 0u, [&](uint32_t i) { return is_ws(prop[i]) ? 0u : i + 1; });
+    uint32_t tcs, tce;
+    trim_span(x, prop, C, tcs, tce);
     if (tcs < tce) {
       const uint32_t m = tce - tcs;
       uint32_t* st = x.template alloc<uint32_t>(m + 1);
@@ -2639,7 +2732,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
       const uint64_t as = x.par.template sum<uint64_t>(W, [&](uint32_t k) {
         const uint32_t a = w.cs[k], e = w.ce[k];
         return ((uint64_t)(e - a) << 32) | ((uint64_t)w.alpha[k] << 16) |
-               (uint64_t)is_stop_word(ucd, ss, c, a, e);
+               (uint64_t)is_stop_word(ucd, ss, c, a, e, w.bs[k], w.be[k]);
       });
       // fields: chars (bits 32..63, <= C), alphabetic words (16..31) and stop words (0..15), both
       // <= W; documents with 2^16 words or more are counted field by field
@@ -2652,9 +2745,10 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
         sum_chars = x.par.template sum<int64_t>(W, [&](uint32_t k) { return (int64_t)(w.ce[k] - w.cs[k]); });
         alpha = x.par.template sum<int64_t>(W, [&](uint32_t k) { return (int64_t)w.alpha[k]; });
         stop = x.par.template sum<int64_t>(W, [&](uint32_t k) {
-          return (int64_t)is_stop_word(ucd, ss, c, w.cs[k], w.ce[k]);
+          return (int64_t)is_stop_word(ucd, ss, c, w.cs[k], w.ce[k], w.bs[k], w.be[k]);
         });
       }
+      x.stamp(PH_GQ_WORDS);
 #if TB_GQ_BYTES
       // the same counts over the bytes ('#' and '.' are ASCII, U+2026 is E2 80 A6 and E2 is
       // always a lead byte): no code point offset loads
@@ -2678,6 +2772,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
         return (uint64_t)((j - i) / 3);
       });
 #endif
+      x.stamp(PH_GQ_BYTES);
       const int64_t nhash = hi32(he), nell = lo32(he);
       const uint64_t be = x.par.template sum<uint64_t>(L.n, [&](uint32_t k) {
         const uint32_t ls = L.ls[k], le = L.le[k];
@@ -2705,7 +2800,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
     } else if (ds.kind == DK_GOPHER_REP) {
       ++gr_seen;
       gopher_rep_record(x, ds, b, c, ph, w, r, kHotProps && gr_seen == n_gr, n_gr == 1 ? out.gr_export : nullptr,
-                        kPre ? out.pre : nullptr, out.b_global);
+                        kPre ? out.pre : nullptr, out.b_global, L);
     } else if (ds.kind == DK_FINEWEB) {
       const auto mark = x.mark();
       uint32_t* nb = x.template alloc<uint32_t>(L.n + 1);

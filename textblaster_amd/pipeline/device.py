@@ -777,7 +777,9 @@ class DeviceRunner:
         names = {0: "start", 1: "decode", 2: "dict", 3: "prefix_hash", 4: "words", 5: "lines", 6: "gopher_quality",
                  7: "gr_lines_paras", 8: "gr_word_hash", 9: "gr_top_ngrams", 10: "gr_dup_ngrams", 11: "fineweb",
                  12: "langid", 13: "gr_dup_walk", 14: "gr_dup_canon", 15: "gr_top_canon", 16: "c4_lorem", 17: "c4_decode", 18: "c4_lines", 19: "c4_cite", 20: "c4_words",
-                 21: "c4_codes", 22: "c4_join", 23: "c4_sentences"}
+                 21: "c4_codes", 22: "c4_join", 23: "c4_sentences",
+                 24: "gr_nl_runs", 25: "gr_line_dup", 26: "gr_word_hash8", 27: "gr_word_canon", 28: "gq_words",
+                 29: "gq_bytes"}
         lines = []
         for k, tot in self.phase_totals.items():
             nd = max(1, self.phase_docs[k])

@@ -30,7 +30,7 @@ enum : int {
   PH_GR_TOP, PH_GR_DUP, PH_FW, PH_LID, PH_GR_DUP_WALK, PH_GR_DUP_CANON, PH_GR_TOP_CANON,
   PH_C4_LOREM = 16, PH_C4_DECODE, PH_C4_LINES, PH_C4_CITE, PH_C4_WORDS, PH_C4_CODES, PH_C4_JOIN, PH_C4_SENT,
   // sub-phases of the stage kernel's GopherRepetition / GopherQuality work
-  PH_GR_NL = 24, PH_GR_LINE_DUP, PH_GR_WH, PH_GR_WCANON, PH_GQ_WORDS, PH_GQ_BYTES,
+  PH_GR_NL = 24, PH_GR_LINE_DUP, PH_GR_WH, PH_GR_WCANON, PH_GQ_WORDS, PH_GQ_BYTES, PH_RUST_LINES,
   kPhaseSlots = 32
 };
 
@@ -490,8 +490,12 @@ __device__ Words words_wave(DocCtx<P>& x, const Cps& c, const uint32_t* marks) {
   const PropArr prop = c.props();
   const uint32_t lane = x.par.lane;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  uint32_t *cs = w.cs, *ce = w.ce, *bs = w.bs, *be = w.be;
-  uint8_t* al = w.alpha;
+  // The word arrays are in the HBM arena (alloc): typed as global, their stores are global_store
+  // (vmcnt only) instead of flat stores, which the next chunk's flat loads would have to wait for.
+  typedef __attribute__((address_space(1))) uint32_t g32;
+  typedef __attribute__((address_space(1))) uint8_t g8;
+  g32 *cs = (g32*)w.cs, *ce = (g32*)w.ce, *bs = (g32*)w.bs, *be = (g32*)w.be;
+  g8* al = (g8*)w.alpha;
   constexpr uint32_t kNone = 0xFFFFFFFFu;
   // entry i <= C: property (entry C: 0) and byte offset (entry C: the byte length)
   uint32_t cp = 0, co = 0, np = 0, no = 0;
@@ -554,11 +558,14 @@ __device__ Words words_wave(DocCtx<P>& x, const Cps& c, const uint32_t* marks) {
     if (sel) {
       const uint32_t q = k + (uint32_t)__popcll(sm & lt);
       const bool cf = fc && carry.first != kNone;
-      cs[q] = cf ? carry.first : base + (uint32_t)f;
-      bs[q] = cf ? carry.fo : fo_l;
-      ce[q] = nws ? base + (uint32_t)l + 1u : carry.last;
-      be[q] = nws ? lo_l : carry.lo;
-      al[q] = ((AL & seg) != 0 || (fc && (carry.bits & 4u))) ? 1 : 0;
+      const uint32_t w0 = cf ? carry.first : base + (uint32_t)f, w1 = nws ? base + (uint32_t)l + 1u : carry.last;
+      const uint32_t b0 = cf ? carry.fo : fo_l, b1 = nws ? lo_l : carry.lo;
+      const bool alpha = (AL & seg) != 0 || (fc && (carry.bits & 4u));
+      cs[q] = w0;
+      bs[q] = b0;
+      ce[q] = w1;
+      be[q] = b1;
+      al[q] = alpha ? 1 : 0;
     }
     k += (uint32_t)__popcll(sm);
     {  // carry: the segment open at the chunk's end (uniform)
@@ -1493,11 +1500,17 @@ TB_HD void gopher_rep_record(DocCtx<P>& x, const DevStep& ds, const uint8_t* b, 
     WL = ex ? x.template alloc<uint32_t>(W + 1) : x.template alloc_hot_keep<uint32_t>(W + 1, tab_bytes);
     K = ex ? x.template alloc<uint64_t>(W + 1) : x.template alloc_hot_keep<uint64_t>(W + 1, tab_bytes);
     PB = ex ? x.template alloc<uint64_t>(W + 1) : x.template alloc_hot_keep<uint64_t>(W + 1, tab_bytes);
+    // One-wave documents export these arrays and read neither the code point arrays nor the prefix
+    // hashes (the top of the LDS slice) after the word hashes: the slice's top is released right
+    // there, so the word canonicalisation table lands in the LDS (it was in HBM for most ~1 KB
+    // documents) and the hashes go to the bottom.
+    const bool early = P::kWaves == 1 && release_props && ex != nullptr;
     const auto mw = x.mark();
-    uint64_t* wh = x.template alloc_hot_hi<uint64_t>(W + 1);
+    uint64_t* wh = early ? x.template alloc_hot<uint64_t>(W + 1) : x.template alloc_hot_hi<uint64_t>(W + 1);
     if (x.overflow) return;
     x.par.for_n(W, [&](uint32_t k) { wh[k] = span_hash8(x, ph, w.bs[k], w.be[k]); });
     x.par.sync();
+    if (early) x.release_hi();
     x.stamp(PH_GR_WH);
     canonicalize(
         x, W, [&](uint32_t k) { return dev_key(wh[k], w.be[k] - w.bs[k]); },
@@ -2705,6 +2718,7 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
   Lines L;
   if (need_lines) L = rust_lines(x, c);
   if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return; }
+  x.stamp(PH_RUST_LINES);
   if (out.line_stats && need_words && need_lines) export_line_stats(x, c, w, L, n, out.line_stats);
   x.stamp(PH_LINES);
   const uint32_t W = w.n;

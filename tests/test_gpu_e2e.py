@@ -192,3 +192,48 @@ def test_device_dictionary_scripts_equal_oracle(cfg_name):
     np.testing.assert_array_equal(a.fail_step, b.fail_step)
     assert a.reasons == b.reasons
     assert outputs(a) == outputs(b)
+
+
+def test_device_equals_icu_oracle_on_megabyte_documents(monkeypatch, tmp_path):
+    """The long-document bench shape (~1 MB documents: multi-workgroup pre-pass, split n-gram
+    orders in the persistent k_gr_dup_split) against the CPU ICU oracle: two documents of 1-2 MB
+    (one with a 60,000-type Zipf vocabulary, so the n-gram tables are large) among short ones.
+    The word cap and the lorem / curly gates are lifted so that both pass GopherRepetition and
+    GopherQuality, get rewritten by C4 and fail FineWeb with a ratio in the reason (an exact check
+    of the device's FineWeb record of the 1-2 MB rewrites). Same decisions, rewritten text and
+    metadata byte for byte."""
+    import json
+
+    import numpy as np
+
+    from textblaster_amd.config import load_pipeline_config
+    from textblaster_amd.pipeline.engine import Engine
+
+    from test_emulated_device_path import outputs
+
+    monkeypatch.setenv("TB_TUNE", "pre_doc_bytes=65536,split_doc_bytes=32768")
+    rng = np.random.default_rng(29)
+    texts = [synth.make_doc(rng, "dan", 1_100_000), synth.make_doc(rng, "eng", 1_900_000, vocab_kind="zipf")]
+    texts += synth.make_corpus(64, 1024, seed=31)
+    data, off = synth.pack(texts)
+    assert np.count_nonzero(np.diff(off) >= 1_000_000) == 2
+    yml = open(CFG).read().replace("max_doc_words: 100000", "max_doc_words: 10000000")
+    yml = yml.replace("filter_lorem_ipsum: true", "filter_lorem_ipsum: false")
+    yml = yml.replace("filter_curly_bracket: true", "filter_curly_bracket: false")
+    (tmp_path / "mb.yaml").write_text(yml)
+    cfg = load_pipeline_config(str(tmp_path / "mb.yaml"))
+    eng = Engine(cfg, backend="cuda", keep_reasons=True)
+    assert eng.device_runner.pre_doc_bytes == 65536
+    a = eng.process(data, off)
+    b = Engine(cfg, backend="cpu", segmentation="icu", keep_reasons=True).process(data, off)
+    assert a.n_delegated == 0
+    assert list(b.fail_step[:2]) == [4, 4]  # both reach FineWeb (step 4) on the oracle
+    np.testing.assert_array_equal(a.status, b.status)
+    np.testing.assert_array_equal(a.fail_step, b.fail_step)
+    assert a.reasons == b.reasons
+    oa, ob = outputs(a), outputs(b)
+    assert oa.keys() == ob.keys()
+    for k in oa:
+        (ka, ta, ma), (kb, tb, mb) = oa[k], ob[k]
+        assert (ka, ta) == (kb, tb), (k, len(texts[k]))
+        assert (ma is None) == (mb is None) and (ma is None or json.loads(ma) == json.loads(mb)), k

@@ -779,7 +779,7 @@ class DeviceRunner:
                  12: "langid", 13: "gr_dup_walk", 14: "gr_dup_canon", 15: "gr_top_canon", 16: "c4_lorem", 17: "c4_decode", 18: "c4_lines", 19: "c4_cite", 20: "c4_words",
                  21: "c4_codes", 22: "c4_join", 23: "c4_sentences",
                  24: "gr_nl_runs", 25: "gr_line_dup", 26: "gr_word_hash8", 27: "gr_word_canon", 28: "gq_words",
-                 29: "gq_bytes"}
+                 29: "gq_bytes", 30: "rust_lines"}
         lines = []
         for k, tot in self.phase_totals.items():
             nd = max(1, self.phase_docs[k])

@@ -2039,6 +2039,67 @@ TB_HD uint32_t c4_phrases_at(const DevC4& c4, const uint8_t* b, uint32_t n, uint
   return bits;
 }
 
+// Bytes of v equal to c: bit 7 of each such byte set (exact, no carries between bytes).
+TB_HD uint32_t swar_eq_mask(uint32_t v, uint32_t c) {
+  const uint32_t t = v ^ (c * 0x01010101u);
+  return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+}
+
+// GopherQuality's byte counts of b[0, n): '#' bytes (high half) and ellipses (low half: every
+// U+2026 plus len / 3 for each maximal run of '.'). Items are groups of four aligned dwords (one
+// dword of look-behind and one of look-ahead, issued together); a dword without '.' or 0xE2 costs
+// three SWAR compares and a popcount. Same counts as the per-byte definition.
+template <class P>
+TB_HD uint64_t gq_byte_counts(DocCtx<P>& x, const uint8_t* b, uint32_t n) {
+  const uintptr_t a0 = (uintptr_t)b & ~(uintptr_t)3;
+  const uint32_t head = (uint32_t)((uintptr_t)b - a0);
+  const uint32_t nd = (head + n + 3) >> 2;
+  const uint32_t* w = (const uint32_t*)a0;
+  auto dw = [&](int64_t k) -> uint32_t {  // dword k of the aligned stream, bytes outside the text zero
+    if (k < 0 || k >= (int64_t)nd) return 0u;
+    const int64_t e = 4 * k + 4 - head;
+    if (e <= (int64_t)n && 4 * k >= (int64_t)head) return w[k];
+    uint32_t v = 0;
+    for (uint32_t j = 0; j < 4; ++j) {
+      const int64_t sj = 4 * k + j - head;
+      if (sj >= 0 && sj < (int64_t)n) v |= (uint32_t)b[sj] << (8 * j);
+    }
+    return v;
+  };
+  return x.par.template sum<uint64_t>((nd + 3) >> 2, [&](uint32_t g) {
+    uint32_t d[6];  // d[0]: dword 4g - 1, d[1..4]: the group, d[5]: dword 4g + 4
+#pragma unroll
+    for (uint32_t i = 0; i < 6; ++i) d[i] = dw((int64_t)4 * g + i - 1);
+    uint64_t acc = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint32_t v = d[i + 1];
+      acc += (uint64_t)__builtin_popcount(swar_eq_mask(v, '#')) << 32;
+      const uint32_t dots = swar_eq_mask(v, '.'), e2 = swar_eq_mask(v, 0xE2);
+      if ((dots | e2) == 0) continue;
+      const uint64_t v64 = (uint64_t)v | ((uint64_t)d[i + 2] << 32);
+      for (uint32_t r = 0; r < 4; ++r) {
+        const uint32_t c0 = (v >> (8 * r)) & 0xFFu;
+        if (c0 == 0xE2) {
+          acc += ((v64 >> (8 * r + 8)) & 0xFFFFu) == 0xA680u ? 1u : 0u;
+          continue;
+        }
+        if (c0 != '.') continue;
+        const uint32_t prev = r ? (v >> (8 * r - 8)) & 0xFFu : d[i] >> 24;
+        if (prev == '.') continue;  // not the start of its run
+        uint32_t len = 1;
+        while (r + len < 8 && ((v64 >> (8 * (r + len))) & 0xFFu) == '.') ++len;
+        if (r + len == 8) {  // the run goes past the window: the rest byte by byte
+          int64_t j = 4 * ((int64_t)4 * g + i) + r + len - head;
+          while (j < (int64_t)n && b[j] == '.') { ++j; ++len; }
+        }
+        acc += len / 3;
+      }
+    }
+    return acc;
+  });
+}
+
 // ASCII 'A'..'Z' -> 'a'..'z' in all 8 bytes of v (other bytes unchanged).
 TB_HD uint64_t swar_lower8(uint64_t v) {
   constexpr uint64_t k7F = 0x7F7F7F7F7F7F7F7Full, k80 = 0x8080808080808080ull;
@@ -2635,9 +2696,6 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
 #ifndef TB_HOT_PROPS
 #define TB_HOT_PROPS 1
 #endif
-#ifndef TB_GQ_BYTES
-#define TB_GQ_BYTES 1
-#endif
 constexpr bool kHotProps = TB_HOT_PROPS != 0;
 
 // kPre: the document comes with its pre-pass (StageOut::pre: code points, words, runs of '\n');
@@ -2763,10 +2821,10 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
         });
       }
       x.stamp(PH_GQ_WORDS);
-#if TB_GQ_BYTES
       // the same counts over the bytes ('#' and '.' are ASCII, U+2026 is E2 80 A6 and E2 is
-      // always a lead byte): no code point offset loads
-      const uint64_t he = x.par.template sum<uint64_t>(n, [&](uint32_t i) {
+      // always a lead byte): no code point offset loads, four bytes per SWAR test
+      // (workgroup documents: the per-byte form, the SWAR groups cost their kernels ~50 spilled VGPRs)
+      const uint64_t he = P::kWaves <= 1 ? gq_byte_counts(x, b, n) : x.par.template sum<uint64_t>(n, [&](uint32_t i) {
         const uint32_t c0 = b[i];
         if (c0 == '#') return (uint64_t)1 << 32;
         if (c0 == 0xE2) return (uint64_t)(i + 2 < n && b[i + 1] == 0x80 && b[i + 2] == 0xA6);
@@ -2775,17 +2833,6 @@ TB_HD void analyze_stage(DocCtx<P>& x, const DevStage& st, const DevPlan& plan,
         while (j < n && b[j] == '.') ++j;
         return (uint64_t)((j - i) / 3);
       });
-#else
-      const uint64_t he = x.par.template sum<uint64_t>(C, [&](uint32_t i) {
-        const uint32_t c0 = c.lead(i);
-        if (c0 == '#') return (uint64_t)1 << 32;
-        if (c0 == 0xE2) return (uint64_t)(c.cp(i) == 0x2026);
-        if (c0 != '.' || (i > 0 && c.lead(i - 1) == '.')) return (uint64_t)0;
-        uint32_t j = i;
-        while (j < C && c.lead(j) == '.') ++j;
-        return (uint64_t)((j - i) / 3);
-      });
-#endif
       x.stamp(PH_GQ_BYTES);
       const int64_t nhash = hi32(he), nell = lo32(he);
       const uint64_t be = x.par.template sum<uint64_t>(L.n, [&](uint32_t k) {

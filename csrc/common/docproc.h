@@ -447,7 +447,11 @@ TB_HD bool word_mark(const PropArr& prop, uint32_t C, uint32_t i) {
   if (TB_WB_CTX) {
     const uint32_t pm2 = i >= 2 ? prop[i - 2] : 0xFFFFFFFFu;
     const uint32_t pp1 = i + 1 < C ? prop[i + 1] : 0xFFFFFFFFu;
+#if defined(__HIP_DEVICE_COMPILE__)
     const int r = wb_break_ctx(pm2, prop[i - 1], prop[i], pp1);
+#else
+    const int r = wb_break_ctx_tab(pm2, prop[i - 1], prop[i], pp1);  // (the table form the wave kernels use)
+#endif
     if (r != 2) return r != 0;
   }
   return wb_break(CpsAcc{prop}, (int)C, (int)i);
@@ -469,11 +473,22 @@ __device__ __forceinline__ uint32_t lane_prev(uint32_t v) {  // lane l gets lane
 __device__ __forceinline__ uint32_t lane_next(uint32_t v) {  // lane l gets lane l+1 (lane 63: v)
   return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x130, 0xF, 0xF, false);
 }
-// word_mark from the four properties around position i (sentinel 0xFFFFFFFF outside [0, C))
+// the word-break pair table (uax29.h kWbPairTab) in constant memory: each wave loads it into one
+// register (lane k holds dword k) and reads a pair's dword from the lane that holds it
+static __constant__ WbPairTab g_wb_pair_tab = kWbPairTab;
+// The pair table dword of the pair (pm1, p0): read from the lane that holds it, by every lane of
+// the wave at once (a lane read from a lane outside EXEC returns nothing useful, so this is never
+// done under divergent control flow).
+__device__ __forceinline__ uint32_t wb_pair_dword(uint32_t wbt, uint32_t pm1, uint32_t p0) {
+  const uint32_t i = (pm1 & P_WB_MASK) * kWbClasses + (p0 & P_WB_MASK);
+  return (uint32_t)__shfl((int)wbt, (int)(i >> 3));
+}
+// word_mark from the four properties around position i (sentinel 0xFFFFFFFF outside [0, C));
+// tw: the pair table dword of (pm1, p0) (wb_pair_dword)
 __device__ __forceinline__ bool word_mark4(const PropArr& prop, uint32_t C, uint32_t i, uint32_t pm2, uint32_t pm1,
-                                           uint32_t p0, uint32_t pp1) {
+                                           uint32_t p0, uint32_t pp1, uint32_t tw) {
   if (i == 0 || i >= C) return true;
-  const int r = wb_break_ctx(pm2, pm1, p0, pp1);
+  const int r = wb_break_ctx_tab(pm2, pm1, p0, pp1, [&](uint32_t) { return tw; });
   if (r != 2) return r != 0;
   return wb_break(CpsAcc{prop}, (int)C, (int)i);
 }
@@ -500,6 +515,7 @@ __device__ Words words_wave(DocCtx<P>& x, const Cps& c, const uint32_t* marks) {
   // entry i <= C: property (entry C: 0) and byte offset (entry C: the byte length)
   uint32_t cp = 0, co = 0, np = 0, no = 0;
   if (lane <= C) { cp = c.p(lane); co = c.o(lane); }
+  const uint32_t wbt = lane < (uint32_t)kWbTabWords ? g_wb_pair_tab.w[lane] : 0u;
   uint32_t c1 = kNone, c2 = kNone;  // properties of the two code points before the chunk
   WSeg5 carry{0u, kNone, 0u, kNone, 0u};
   uint32_t k = 0;
@@ -525,8 +541,9 @@ __device__ Words words_wave(DocCtx<P>& x, const Cps& c, const uint32_t* marks) {
     const uint32_t l62 = (uint32_t)__builtin_amdgcn_readlane((int)cp, 62);
     const uint32_t l63 = (uint32_t)__builtin_amdgcn_readlane((int)cp, 63);
     const uint32_t i64 = base + 64;
-    bool mk = j < C && word_mark4(prop, C, j, pm2s, pm1, cp, pp1s);
-    bool mk64 = i64 >= C || word_mark4(prop, C, i64, l62, l63, n0p, i64 + 1 < C ? n1p : kNone);
+    const uint32_t tw = wb_pair_dword(wbt, pm1, cp), tw64 = wb_pair_dword(wbt, l63, n0p);  // (all lanes)
+    bool mk = j < C && word_mark4(prop, C, j, pm2s, pm1, cp, pp1s, tw);
+    bool mk64 = i64 >= C || word_mark4(prop, C, i64, l62, l63, n0p, i64 + 1 < C ? n1p : kNone, tw64);
     if (marks) {  // host record: ICU marks (first bitmap) where its mask (second bitmap) is set
       const uint32_t* hm = marks + mask_words(C + 1);
       if (j < C && ((hm[j >> 5] >> (j & 31)) & 1u)) mk = ((marks[j >> 5] >> (j & 31)) & 1u) != 0;

@@ -13,11 +13,11 @@
 
 namespace tb {
 
-TB_HD bool wb_ign(int c) { return c == WB_Extend || c == WB_Format || c == WB_ZWJ; }
-TB_HD bool wb_nl(int c) { return c == WB_CR || c == WB_LF || c == WB_Newline; }
-TB_HD bool wb_ah(int c) { return c == WB_ALetter || c == WB_Hebrew; }
-TB_HD bool wb_midletq(int c) { return c == WB_MidLetter || c == WB_MidNumLet || c == WB_SQ; }
-TB_HD bool wb_midnumq(int c) { return c == WB_MidNum || c == WB_MidNumLet || c == WB_SQ; }
+constexpr TB_HD bool wb_ign(int c) { return c == WB_Extend || c == WB_Format || c == WB_ZWJ; }
+constexpr TB_HD bool wb_nl(int c) { return c == WB_CR || c == WB_LF || c == WB_Newline; }
+constexpr TB_HD bool wb_ah(int c) { return c == WB_ALetter || c == WB_Hebrew; }
+constexpr TB_HD bool wb_midletq(int c) { return c == WB_MidLetter || c == WB_MidNumLet || c == WB_SQ; }
+constexpr TB_HD bool wb_midnumq(int c) { return c == WB_MidNum || c == WB_MidNumLet || c == WB_SQ; }
 
 // Effective previous code point index for WB4: the nearest index < i that is not
 // Extend/Format/ZWJ. Returns -1 if the run of ignorables reaches sot.
@@ -101,7 +101,7 @@ TB_HD bool wb_break(const A& a, int n, int i) {
 // out of range), for positions whose window holds no Extend/Format/ZWJ/RI: then the effective
 // left contexts are i-1 and i-2 and the effective right context is i+1, so every rule is decided
 // from registers. Returns 0 / 1, or 2 when the window needs the general look-around.
-TB_HD int wb_break_ctx(uint32_t pm2, uint32_t pm1, uint32_t p0, uint32_t pp1) {
+constexpr TB_HD int wb_break_ctx(uint32_t pm2, uint32_t pm1, uint32_t p0, uint32_t pp1) {
   const int L0 = wb_of(pm1), R = wb_of(p0);
   if (L0 == WB_ALetter) {  // the common pairs first (as wb_break)
     if (R == WB_ALetter) return 0;
@@ -136,6 +136,113 @@ TB_HD int wb_break_ctx(uint32_t pm2, uint32_t pm1, uint32_t p0, uint32_t pp1) {
     return 0;                                                           // WB13a
   if (L == WB_ExtendNumLet && (wb_ah(R) || R == WB_Numeric || R == WB_Katakana)) return 0;  // WB13b
   return 1;                                                             // WB999
+}
+
+// The same decision from a table of the class pairs (L, R) = (i-1, i): once no Extend / Format /
+// ZWJ / RI is in the window, every rule of wb_break_ctx either decides a pair outright or asks
+// whether one context class (RR = i+1 for WB6 / 7b / 12, LL = i-2 for WB7 / 7c / 11) lies in a
+// set (AHLetter, Hebrew or Numeric). The table holds that per pair as a 4-bit code, 8 pairs per
+// dword; it is generated at compile time from wb_break_ctx itself (wb_pair_code), so the two agree
+// by construction, and tools/host_selftest.cpp checks them against each other on every window.
+// On the device one wave keeps the 46 table dwords in one register (lane k: dword k) and looks a
+// pair up with one lane read (ds_bpermute): a handful of VALU instructions instead of the rule
+// chain, which every lane of a wave runs through when its lanes hold different classes.
+enum : uint32_t {
+  WBC_NB = 0, WBC_BR = 1, WBC_RR_AH = 2, WBC_RR_HEB = 3, WBC_RR_NUM = 4, WBC_LL_AH = 5, WBC_LL_HEB = 6,
+  WBC_LL_NUM = 7, WBC_BAD = 15
+};
+constexpr int kWbClasses = 19;
+constexpr int kWbTabWords = (kWbClasses * kWbClasses + 7) / 8;  // 46
+constexpr uint32_t kWbSpecial = (1u << WB_Extend) | (1u << WB_Format) | (1u << WB_ZWJ) | (1u << WB_RI);
+constexpr uint32_t kWbSetAH = (1u << WB_ALetter) | (1u << WB_Hebrew);
+constexpr uint32_t kWbSetHeb = 1u << WB_Hebrew;
+constexpr uint32_t kWbSetNum = 1u << WB_Numeric;
+
+constexpr uint32_t wb_pair_code(int L, int R) {
+  if ((kWbSpecial >> L) & 1u || (kWbSpecial >> R) & 1u) return WBC_BR;  // (never looked up)
+  int ctx[kWbClasses + 1] = {};  // -1 (no code point) and the classes that are not special
+  int nc = 0;
+  ctx[nc++] = -1;
+  for (int c = 0; c < kWbClasses; ++c)
+    if (!((kWbSpecial >> c) & 1u)) ctx[nc++] = c;
+  auto r = [&](int ll, int rr) {
+    return wb_break_ctx(ll < 0 ? 0xFFFFFFFFu : (uint32_t)ll, (uint32_t)L, (uint32_t)R, rr < 0 ? 0xFFFFFFFFu : (uint32_t)rr);
+  };
+  const int r0 = r(-1, -1);
+  bool dep_ll = false, dep_rr = false;
+  for (int a = 0; a < nc; ++a)
+    for (int b = 0; b < nc; ++b) {
+      if (r(ctx[a], -1) != r0) dep_ll = true;
+      if (r(-1, ctx[b]) != r0) dep_rr = true;
+    }
+  if (!dep_ll && !dep_rr) {
+    for (int a = 0; a < nc; ++a)
+      for (int b = 0; b < nc; ++b)
+        if (r(ctx[a], ctx[b]) != r0) return WBC_BAD;
+    return r0 == 0 ? WBC_NB : (r0 == 1 ? WBC_BR : WBC_BAD);
+  }
+  if (dep_ll && dep_rr) return WBC_BAD;
+  // one side decides: the set of its classes with no break, everything else breaks
+  uint32_t set = 0;
+  for (int a = 1; a < nc; ++a) {
+    const int v = dep_rr ? r(-1, ctx[a]) : r(ctx[a], -1);
+    if (v == 0) set |= 1u << ctx[a];
+    else if (v != 1) return WBC_BAD;
+  }
+  if (r0 != 1) return WBC_BAD;
+  for (int a = 0; a < nc; ++a)  // the other side changes nothing
+    for (int b = 0; b < nc; ++b) {
+      const int v = dep_rr ? r(ctx[a], ctx[b]) : r(ctx[b], ctx[a]);
+      const int want = ctx[b] >= 0 && ((set >> ctx[b]) & 1u) ? 0 : 1;
+      if (v != want) return WBC_BAD;
+    }
+  const uint32_t base = dep_rr ? WBC_RR_AH : WBC_LL_AH;
+  if (set == kWbSetAH) return base;
+  if (set == kWbSetHeb) return base + 1;
+  if (set == kWbSetNum) return base + 2;
+  return WBC_BAD;
+}
+struct WbPairTab {
+  uint32_t w[kWbTabWords];
+};
+constexpr WbPairTab make_wb_pair_tab() {
+  WbPairTab t{};
+  for (int L = 0; L < kWbClasses; ++L)
+    for (int R = 0; R < kWbClasses; ++R) {
+      const int i = L * kWbClasses + R;
+      t.w[i >> 3] |= wb_pair_code(L, R) << ((i & 7) * 4);
+    }
+  return t;
+}
+constexpr bool wb_pair_tab_ok(const WbPairTab& t) {
+  for (int i = 0; i < kWbClasses * kWbClasses; ++i)
+    if (((t.w[i >> 3] >> ((i & 7) * 4)) & 0xFu) == WBC_BAD) return false;
+  return true;
+}
+inline constexpr WbPairTab kWbPairTab = make_wb_pair_tab();
+static_assert(wb_pair_tab_ok(kWbPairTab), "a word-break pair needs a context the table cannot encode");
+
+// wb_break_ctx by the pair table; lookup(i) returns dword i >> 3 of kWbPairTab (any source).
+template <class Lookup>
+TB_HD int wb_break_ctx_tab(uint32_t pm2, uint32_t pm1, uint32_t p0, uint32_t pp1, Lookup&& lookup) {
+  const uint32_t L = pm1 & P_WB_MASK, R = p0 & P_WB_MASK;
+  if (((1u << L) | (1u << R)) & kWbSpecial) return 2;
+  const uint32_t i = L * kWbClasses + R;
+  const uint32_t code = (lookup(i >> 3) >> ((i & 7u) * 4u)) & 0xFu;
+  // a pair decided outright does not look past i-1 and i (an ignorable at i-2 or i+1 only changes
+  // the effective contexts further out); a context rule reads the effective i-2 / i+1, which the
+  // window holds unless it is ignorable or RI (then the general walk)
+  if (code <= WBC_BR) return (int)code;
+  const uint32_t bLL = pm2 == 0xFFFFFFFFu ? 0u : 1u << (pm2 & P_WB_MASK);
+  const uint32_t bRR = pp1 == 0xFFFFFFFFu ? 0u : 1u << (pp1 & P_WB_MASK);
+  const uint32_t ctx = code <= WBC_RR_NUM ? bRR : bLL;
+  if (ctx & kWbSpecial) return 2;
+  const uint32_t set = (code == WBC_RR_AH || code == WBC_LL_AH) ? kWbSetAH
+                       : (code == WBC_RR_HEB || code == WBC_LL_HEB) ? kWbSetHeb : kWbSetNum;
+  return (ctx & set) ? 0 : 1;
+}
+TB_HD int wb_break_ctx_tab(uint32_t pm2, uint32_t pm1, uint32_t p0, uint32_t pp1) {
+  return wb_break_ctx_tab(pm2, pm1, p0, pp1, [](uint32_t k) { return kWbPairTab.w[k]; });
 }
 
 // ---------------------------------------------------------------------------------------------

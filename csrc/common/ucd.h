@@ -53,7 +53,7 @@ struct UcdView {
   }
 };
 
-TB_HD int wb_of(uint32_t p) { return (int)(p & P_WB_MASK); }
+constexpr TB_HD int wb_of(uint32_t p) { return (int)(p & P_WB_MASK); }
 TB_HD int sb_of(uint32_t p) { return (int)((p >> P_SB_SHIFT) & 0xF); }
 
 // Decode one UTF-8 code point starting at s[i] (input is valid UTF-8: Arrow Utf8 guarantees it).

@@ -132,7 +132,8 @@ def build_hip(verbose: bool = False, force: bool = False) -> str:
     os.makedirs(os.path.join(BUILD_DIR, "hip"), exist_ok=True)
     # no -ffast-math: the language-id decision (langid.h: explicit-fma exp, IEEE f64 division) and
     # the exact integer / bf16 MFMA paths must match the host bit for bit
-    flags = [f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-fPIC", "-fno-gpu-rdc"]
+    # (constexpr-steps: the word-break pair table of uax29.h is generated at compile time)
+    flags = [f"--offload-arch={GPU_ARCH}", "-O3", "-std=c++17", "-fPIC", "-fno-gpu-rdc", "-fconstexpr-steps=200000000"]
     objs = []
 
     def compile_one(src: str) -> str:

@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 name=$1; shift
 mkdir -p build/variants
 python3 -c "from textblaster_amd import native; native.build_hip()" > /dev/null
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-gpu-rdc "$@" -c csrc/hip/kernels.hip \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-gpu-rdc -fconstexpr-steps=200000000 "$@" -c csrc/hip/kernels.hip \
   -o build/variants/kernels_$name.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o textblaster_amd/libtbhip_$name.so build/variants/kernels_$name.o \
   $(ls build/hip/*.o | grep -v kernels.hip.o)

@@ -20,6 +20,7 @@
 #include "../csrc/host/json.h"
 #include "../csrc/host/pipeline.h"
 #include "../csrc/host/text.h"
+#include "../csrc/common/uax29.h"
 
 using namespace tb;
 
@@ -104,7 +105,40 @@ static std::vector<StepCfg> steps() {
   return v;
 }
 
+// Every window (i-2, i-1, i, i+1) of word-break classes, i-2 / i+1 possibly absent: the pair-table
+// rule (uax29.h wb_break_ctx_tab, the wave kernels' form) decides like the rule chain it was built
+// from wherever that decides, and like the general walk (wb_break over the window as a text)
+// wherever it decides without the walk.
+struct WinAcc {
+  const uint32_t* v;
+  uint32_t p(int i) const { return v[i]; }
+};
+static void check_wb_pair_table() {
+  int decided = 0;
+  for (uint32_t a = 0; a <= (uint32_t)kWbClasses; ++a)
+    for (uint32_t b = 0; b < (uint32_t)kWbClasses; ++b)
+      for (uint32_t c = 0; c < (uint32_t)kWbClasses; ++c)
+        for (uint32_t d = 0; d <= (uint32_t)kWbClasses; ++d) {
+          const uint32_t pm2 = a == (uint32_t)kWbClasses ? 0xFFFFFFFFu : a;
+          const uint32_t pp1 = d == (uint32_t)kWbClasses ? 0xFFFFFFFFu : d;
+          const int x = wb_break_ctx(pm2, b, c, pp1), y = wb_break_ctx_tab(pm2, b, c, pp1);
+          if (y == 2) continue;
+          ++decided;
+          uint32_t v[4];
+          int n = 0;
+          if (pm2 != 0xFFFFFFFFu) v[n++] = pm2;
+          const int i = n + 1;
+          v[n++] = b;
+          v[n++] = c;
+          if (pp1 != 0xFFFFFFFFu) v[n++] = pp1;
+          CHECK(x == 2 || x == y, "wb pair table vs rules: %u %u %u %u", a, b, c, d);
+          CHECK((int)wb_break(WinAcc{v}, n, i) == y, "wb pair table vs walk: %u %u %u %u", a, b, c, d);
+        }
+  CHECK(decided > 60000, "wb pair table decided %d windows", decided);
+}
+
 int main(int argc, char** argv) {
+  check_wb_pair_table();
   const int ndocs = argc > 1 ? std::atoi(argv[1]) : 400;
   std::mt19937_64 rng(12345);
   std::vector<std::string> docs;

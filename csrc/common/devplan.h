@@ -66,6 +66,10 @@ struct DevStopSet {
   // stop_fast_slot (lite_nslots entries, 0 = empty). An ASCII word of <= 7 bytes is a stop word
   // iff its lowercase key is here (no other entry can equal it), so those need no byte compare.
   uint64_t fast_keys[kStopLiteMaxSlots];
+  // 1: every entry is ASCII of <= 7 bytes (all of them are in fast_keys). A word outside the fast
+  // path then matches only if it lowercases to ASCII, which needs U+212A KELVIN SIGN (-> 'k', the
+  // only non-ASCII code point with an ASCII lowercase; its UTF-8 starts with E2)
+  int32_t all_ascii7;
 };
 
 TB_HD uint32_t stop_fast_slot(uint64_t key, uint32_t nslots) {

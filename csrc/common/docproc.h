@@ -1008,6 +1008,11 @@ TB_HD bool is_stop_word(const UcdView& ucd, const DevStopSet& ss, const Cps& cv,
         slot = (slot + 1) & (ns - 1);
       }
     }
+    if (ss.all_ascii7) {  // (devplan.h) no lowercase of this word is in the set without a Kelvin sign
+      bool e2 = false;
+      for (uint32_t k = b0; k < b1; ++k) e2 |= cv.b[k] == 0xE2;
+      if (!e2) return false;
+    }
   }
   uint64_t h = 0;
   uint32_t len = 0;

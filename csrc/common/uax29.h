@@ -158,45 +158,24 @@ constexpr uint32_t kWbSetAH = (1u << WB_ALetter) | (1u << WB_Hebrew);
 constexpr uint32_t kWbSetHeb = 1u << WB_Hebrew;
 constexpr uint32_t kWbSetNum = 1u << WB_Numeric;
 
+// (the decision of every window against the rule chain and the general walk is checked by
+// tools/host_selftest.cpp; here only which side, if any, a pair depends on)
 constexpr uint32_t wb_pair_code(int L, int R) {
   if ((kWbSpecial >> L) & 1u || (kWbSpecial >> R) & 1u) return WBC_BR;  // (never looked up)
-  int ctx[kWbClasses + 1] = {};  // -1 (no code point) and the classes that are not special
-  int nc = 0;
-  ctx[nc++] = -1;
-  for (int c = 0; c < kWbClasses; ++c)
-    if (!((kWbSpecial >> c) & 1u)) ctx[nc++] = c;
   auto r = [&](int ll, int rr) {
     return wb_break_ctx(ll < 0 ? 0xFFFFFFFFu : (uint32_t)ll, (uint32_t)L, (uint32_t)R, rr < 0 ? 0xFFFFFFFFu : (uint32_t)rr);
   };
   const int r0 = r(-1, -1);
-  bool dep_ll = false, dep_rr = false;
-  for (int a = 0; a < nc; ++a)
-    for (int b = 0; b < nc; ++b) {
-      if (r(ctx[a], -1) != r0) dep_ll = true;
-      if (r(-1, ctx[b]) != r0) dep_rr = true;
-    }
-  if (!dep_ll && !dep_rr) {
-    for (int a = 0; a < nc; ++a)
-      for (int b = 0; b < nc; ++b)
-        if (r(ctx[a], ctx[b]) != r0) return WBC_BAD;
-    return r0 == 0 ? WBC_NB : (r0 == 1 ? WBC_BR : WBC_BAD);
+  uint32_t set_ll = 0, set_rr = 0;  // context classes that change the decision
+  for (int c = 0; c < kWbClasses; ++c) {
+    if ((kWbSpecial >> c) & 1u) continue;
+    if (r(c, -1) != r0) set_ll |= 1u << c;
+    if (r(-1, c) != r0) set_rr |= 1u << c;
   }
-  if (dep_ll && dep_rr) return WBC_BAD;
-  // one side decides: the set of its classes with no break, everything else breaks
-  uint32_t set = 0;
-  for (int a = 1; a < nc; ++a) {
-    const int v = dep_rr ? r(-1, ctx[a]) : r(ctx[a], -1);
-    if (v == 0) set |= 1u << ctx[a];
-    else if (v != 1) return WBC_BAD;
-  }
-  if (r0 != 1) return WBC_BAD;
-  for (int a = 0; a < nc; ++a)  // the other side changes nothing
-    for (int b = 0; b < nc; ++b) {
-      const int v = dep_rr ? r(ctx[a], ctx[b]) : r(ctx[b], ctx[a]);
-      const int want = ctx[b] >= 0 && ((set >> ctx[b]) & 1u) ? 0 : 1;
-      if (v != want) return WBC_BAD;
-    }
-  const uint32_t base = dep_rr ? WBC_RR_AH : WBC_LL_AH;
+  if (!set_ll && !set_rr) return r0 == 0 ? WBC_NB : (r0 == 1 ? WBC_BR : WBC_BAD);
+  if ((set_ll && set_rr) || r0 != 1) return WBC_BAD;
+  const uint32_t set = set_ll | set_rr;
+  const uint32_t base = set_rr ? WBC_RR_AH : WBC_LL_AH;
   if (set == kWbSetAH) return base;
   if (set == kWbSetHeb) return base + 1;
   if (set == kWbSetNum) return base + 2;

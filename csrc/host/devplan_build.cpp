@@ -73,6 +73,7 @@ static int add_stop_set(DevPlan& plan, const std::vector<std::string>& words) {
     uint32_t ns = 16;
     while (ns < 4u * (uint32_t)ss.n) ns <<= 1;
     ss.lite_nslots = (int32_t)ns;
+    ss.all_ascii7 = 1;
     for (size_t i = 0; i < uniq.size(); ++i) {
       uint32_t h = kStopLiteHash0;
       for (unsigned char c : uniq[i]) h = stop_lite_hash_push(h, c);
@@ -82,6 +83,7 @@ static int add_stop_set(DevPlan& plan, const std::vector<std::string>& words) {
       const std::string& w = uniq[i];
       bool ascii = !w.empty() && w.size() <= 7;
       for (unsigned char c : w) ascii = ascii && c < 0x80;
+      if (!ascii) ss.all_ascii7 = 0;
       if (ascii) {
         uint64_t key = (uint64_t)w.size() << 56;
         for (size_t k = 0; k < w.size(); ++k) key |= (uint64_t)(unsigned char)w[k] << (8 * k);

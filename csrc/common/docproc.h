@@ -442,15 +442,21 @@ TB_HD WSeg wseg_op(const WSeg& a, const WSeg& b) {
 #ifndef TB_WB_CTX
 #define TB_WB_CTX 1
 #endif
+#if defined(__HIPCC__)
+// the word-break pair table (uax29.h kWbPairTab) in constant memory: the one-wave words() loads it
+// into one register (lane k holds dword k) and reads a pair's dword from the lane that holds it;
+// word_mark() on the device reads it directly
+static __constant__ WbPairTab g_wb_pair_tab = kWbPairTab;
+#endif
 TB_HD bool word_mark(const PropArr& prop, uint32_t C, uint32_t i) {
   if (i == 0 || i == C) return true;
   if (TB_WB_CTX) {
     const uint32_t pm2 = i >= 2 ? prop[i - 2] : 0xFFFFFFFFu;
     const uint32_t pp1 = i + 1 < C ? prop[i + 1] : 0xFFFFFFFFu;
 #if defined(__HIP_DEVICE_COMPILE__)
-    const int r = wb_break_ctx(pm2, prop[i - 1], prop[i], pp1);
+    const int r = wb_break_ctx_tab(pm2, prop[i - 1], prop[i], pp1, [](uint32_t k) { return g_wb_pair_tab.w[k]; });
 #else
-    const int r = wb_break_ctx_tab(pm2, prop[i - 1], prop[i], pp1);  // (the table form the wave kernels use)
+    const int r = wb_break_ctx_tab(pm2, prop[i - 1], prop[i], pp1);
 #endif
     if (r != 2) return r != 0;
   }
@@ -473,9 +479,6 @@ __device__ __forceinline__ uint32_t lane_prev(uint32_t v) {  // lane l gets lane
 __device__ __forceinline__ uint32_t lane_next(uint32_t v) {  // lane l gets lane l+1 (lane 63: v)
   return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x130, 0xF, 0xF, false);
 }
-// the word-break pair table (uax29.h kWbPairTab) in constant memory: each wave loads it into one
-// register (lane k holds dword k) and reads a pair's dword from the lane that holds it
-static __constant__ WbPairTab g_wb_pair_tab = kWbPairTab;
 // The pair table dword of the pair (pm1, p0): read from the lane that holds it, by every lane of
 // the wave at once (a lane read from a lane outside EXEC returns nothing useful, so this is never
 // done under divergent control flow).

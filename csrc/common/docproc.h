@@ -2395,6 +2395,219 @@ TB_HD void c4_pass_a_export(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uin
   c4_plain_tail(x, c4, b, n, NLn, lbs, lbe, nw, mx, phrase_bits, r, src, wout);
 }
 
+// The byte past a citation starting at b[i] == '[' inside [i, e) (a trimmed line), 0 when none
+// starts there, 0xFFFFFFFF when the match depends on a non-ASCII byte (a Unicode digit or space).
+TB_HD uint32_t c4_cite_end_bytes(const UcdView& ucd, const uint8_t* b, uint32_t i, uint32_t e) {
+  uint32_t p = i + 1;
+  if (p >= e) return 0;
+  if (b[p] >= 0x80) return 0xFFFFFFFFu;
+  if (b[p] < '0' || b[p] > '9') return 0;
+  while (p < e && b[p] >= '0' && b[p] <= '9') ++p;
+  while (true) {
+    if (p < e && b[p] >= 0x80) return 0xFFFFFFFFu;  // a non-ASCII digit could continue \d+
+    if (!(p < e && b[p] == ',')) break;
+    uint32_t q = p + 1;
+    while (q < e && b[q] < 0x80 && (ucd.props(b[q]) & P_WS)) ++q;
+    if (q < e && b[q] >= 0x80) return 0xFFFFFFFFu;  // Unicode whitespace or digit
+    if (!(q < e && b[q] >= '0' && b[q] <= '9')) break;
+    while (q < e && b[q] >= '0' && b[q] <= '9') ++q;
+    p = q;
+  }
+  return (p < e && b[p] == ']') ? p + 1 : 0;
+}
+
+// C4 pass A for a one-wave document with a possible citation, from the stage's line export: the
+// citations (reference CITATION_REGEX, c4_filters.rs:33, applied to each trimmed line) are found on
+// the bytes of the exported trimmed line spans, the processed lines Pb are built byte-parallel
+// (a removed-byte bitmap and its prefix popcounts give every kept byte's place), and only the lines
+// that lost a citation are segmented again; no decode, no Rust lines, no per-code-point line ids.
+// Returns false without writing anything when a candidate needs Unicode classes (a non-ASCII byte
+// where \d or \s could continue the match): the general path runs then.
+template <class P>
+TB_HD bool c4_pass_a_cite_export(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n, const uint32_t* region,
+                                 uint32_t NLn, int64_t* r, int64_t* src) {
+  const LineStat* ls = (const LineStat*)(region + 4);
+  const auto mark0 = x.mark();
+  const uint32_t nwd = (n + 31) / 32 + 1;
+  uint32_t* lbs = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* lbe = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* nw = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* mx = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* plen = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint32_t* poff = x.template alloc_hot<uint32_t>(NLn + 1);
+  uint8_t* code = x.template alloc_hot<uint8_t>(NLn + 1);    // 1: the line lost a citation (then the codes)
+  uint32_t* pf = x.template alloc_hot<uint32_t>(NLn + 1);    // pattern flags per line
+  uint32_t* rmb = x.template alloc_hot<uint32_t>(nwd);       // removed bytes
+  uint32_t* wr = x.template alloc_hot<uint32_t>(nwd + 1);    // exclusive popcount prefix of rmb
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return true; }
+  x.par.for_n(NLn, [&](uint32_t k) {
+    const LineStat e = ls[k];
+    lbs[k] = e.bs; lbe[k] = e.be; nw[k] = e.nw; mx[k] = e.mx; code[k] = 0; pf[k] = 0;
+  });
+  x.par.for_n(nwd, [&](uint32_t w) { rmb[w] = 0; });
+  x.par.single([&]() { lbs[NLn] = 0xFFFFFFFFu; });
+  x.par.sync();
+  auto line_of_byte = [&](uint32_t bs) {  // last line with byte start <= bs
+    uint32_t lo = 0, hi = NLn;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (lbs[mid] <= bs) lo = mid; else hi = mid;
+    }
+    return lo;
+  };
+  uint32_t bad = 0;
+  x.par.for_n(n, [&](uint32_t i) {
+    if (b[i] != '[') return;
+    const uint32_t k = line_of_byte(i), e = lbe[k];
+    if (i < lbs[k] || i >= e) return;
+    const uint32_t ce = c4_cite_end_bytes(x.ucd, b, i, e);
+    if (ce == 0xFFFFFFFFu) { bad = 1; return; }
+    if (ce == 0) return;
+    for (uint32_t q = i; q < ce; ++q) P::or32(&rmb[q >> 5], 1u << (q & 31));
+    code[k] = 1;
+  });
+  x.par.sync();
+  if (x.par.reduce_or(bad)) {
+    x.reset(mark0);
+    return false;
+  }
+  x.par.template scan<uint32_t>(
+      nwd, 0u, [](uint32_t a, uint32_t c2) { return a + c2; }, [&](uint32_t w) { return (uint32_t)__builtin_popcount(rmb[w]); },
+      [&](uint32_t w, uint32_t e) { wr[w] = e; });
+  x.par.sync();
+  auto rank = [&](uint32_t i) {  // removed bytes before byte i
+    return wr[i >> 5] + (uint32_t)__builtin_popcount(rmb[i >> 5] & ((1u << (i & 31)) - 1u));
+  };
+  auto removed = [&](uint32_t i) { return (rmb[i >> 5] >> (i & 31)) & 1u; };
+  x.par.for_n(NLn, [&](uint32_t k) { plen[k] = (lbe[k] - lbs[k]) - (rank(lbe[k]) - rank(lbs[k])); });
+  x.par.sync();
+  const uint32_t Ptot = x.par.template scan<uint32_t>(
+      NLn, 0u, [](uint32_t a, uint32_t c2) { return a + c2; }, [&](uint32_t k) { return plen[k] + 1u; },
+      [&](uint32_t k, uint32_t e) { poff[k] = e; });
+  uint8_t* Pb = x.template alloc<uint8_t>(Ptot + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return true; }
+  x.par.sync();
+  x.par.for_n(n, [&](uint32_t i) {
+    const uint32_t k = line_of_byte(i);
+    if (i < lbs[k] || i >= lbe[k] || removed(i)) return;
+    Pb[poff[k] + (i - lbs[k]) - (rank(i) - rank(lbs[k]))] = b[i];
+  });
+  x.par.for_n(NLn, [&](uint32_t k) { Pb[poff[k] + plen[k]] = '\n'; });
+  x.par.single([&]() { poff[NLn] = Ptot; });
+  x.par.sync();
+  x.stamp(PH_C4_CITE);
+  auto line_of_p = [&](uint32_t bs) {  // last line with poff <= bs
+    uint32_t lo = 0, hi = NLn;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (poff[mid] <= bs) lo = mid; else hi = mid;
+    }
+    return lo;
+  };
+  // words of the lines that lost a citation (joined with '\n', so no word spans two lines)
+  {
+    uint32_t* coff = x.template alloc_hot<uint32_t>(NLn + 1);
+    if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return true; }
+    const uint32_t Ctot = x.par.template scan<uint32_t>(
+        NLn, 0u, [](uint32_t a, uint32_t c2) { return a + c2; },
+        [&](uint32_t k) { return code[k] ? plen[k] + 1 : 0u; }, [&](uint32_t k, uint32_t e) { coff[k] = e; });
+    x.par.for_n(NLn, [&](uint32_t k) { if (code[k]) { nw[k] = 0; mx[k] = 0; } });
+    x.par.sync();
+    if (Ctot > 0) {
+      const auto mc = x.mark();
+      uint8_t* Pc = x.template alloc<uint8_t>(Ctot + 1);
+      if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return true; }
+      x.par.for_n(Ptot, [&](uint32_t i) {
+        const uint32_t k = line_of_p(i);
+        if (code[k] && i - poff[k] <= plen[k]) Pc[coff[k] + (i - poff[k])] = Pb[i];  // (its '\n' too)
+      });
+      x.par.sync();
+      uint32_t dict = 0;
+      Cps cc = decode(x, Pc, Ctot, false, &dict);
+      if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return true; }
+      if (dict) {  // dictionary-script text in a cited line: its words need ICU
+        x.set_flag(DOC_NEEDS_CPU);
+        return true;
+      }
+      Words cw = words(x, cc);
+      if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return true; }
+      x.par.for_n(cw.n, [&](uint32_t q) {
+        const uint32_t bs = cw.bs[q];
+        uint32_t lo = 0, hi = NLn;  // last line with coff <= bs: the cited line holding the word
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (coff[mid] <= bs) lo = mid; else hi = mid;
+        }
+        P::add32(&nw[lo], 1u);
+        P::max32(&mx[lo], cw.ce[q] - cw.cs[q]);
+      });
+      x.par.sync();
+      x.reset(mc);
+    }
+  }
+  x.stamp(PH_C4_WORDS);
+  if (c4.filter_javascript || c4.filter_policy) {
+    scan_bytes16(x, Pb, Ptot, [&](uint32_t s, uint32_t, uint32_t, uint32_t l3) {
+      if (!c4_phrase_prefix(l3)) return;
+      const uint32_t bits = c4_phrases_at(c4, Pb, Ptot, s);
+      if (bits) P::or32(&pf[line_of_p(s)], bits);
+    });
+  }
+  x.par.sync();
+  x.par.for_n(NLn, [&](uint32_t k) {
+    const uint8_t* lp = Pb + poff[k];
+    const uint32_t ln = plen[k];
+    uint8_t cd = 0;
+    if (c4.max_word_length > 0 && (int64_t)mx[k] > c4.max_word_length) {
+      cd = 1;
+    } else if (c4.filter_no_terminal_punct) {
+      bool term = false;
+      if (ln > 0) {
+        uint32_t st = ln - 1;
+        while (st > 0 && (lp[st] & 0xC0) == 0x80) --st;
+        int len;
+        term = end_punct(utf8_decode(lp, st, ln, &len));
+      }
+      const bool ell = ln >= 3 && lp[ln - 1] == '.' && lp[ln - 2] == '.' && lp[ln - 3] == '.';
+      if (!term || ell) cd = 2;
+    }
+    if (cd == 0 && c4.min_words_per_line > 0 && (int64_t)nw[k] < c4.min_words_per_line) cd = 3;
+    if (cd == 0 && c4.filter_javascript && (pf[k] & C4F_JS)) cd = 4;
+    if (cd == 0 && c4.filter_policy && (pf[k] & C4F_POLICY)) cd = 5;
+    code[k] = cd;
+  });
+  x.par.sync();
+  const uint64_t s12 = x.par.template sum<uint64_t>(NLn, [&](uint32_t k) {
+    return (uint64_t)(code[k] == 1) | ((uint64_t)(code[k] == 2) << 32);
+  });
+  const int64_t s_long = (int64_t)(s12 & 0xFFFFFFFFull), s_punct = (int64_t)(s12 >> 32);
+  const int64_t s_few = x.par.template sum<int64_t>(NLn, [&](uint32_t k) { return (int64_t)(code[k] == 3); });
+  x.stamp(PH_C4_CODES);
+  // ---- joined kept lines (HBM: read back by pass B), copied from Pb ----
+  uint32_t* joff = x.template alloc_hot<uint32_t>(NLn + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return true; }
+  uint32_t Jtot = x.par.template scan<uint32_t>(
+      NLn, 0u, [](uint32_t a, uint32_t b2) { return a + b2; },
+      [&](uint32_t k) { return code[k] == 0 ? plen[k] + 1 : 0u; }, [&](uint32_t k, uint32_t e) { joff[k] = e; });
+  if (Jtot > 0) Jtot -= 1;
+  uint8_t* Jb = x.template alloc_global<uint8_t>(Jtot + 1);
+  if (x.overflow) { x.set_flag(DOC_NEEDS_CPU | DOC_OVERFLOW); return true; }
+  x.par.sync();
+  x.par.for_n(Ptot, [&](uint32_t i) {
+    const uint32_t k = line_of_p(i);
+    const uint32_t j = i - poff[k];
+    if (code[k] != 0 || j >= plen[k]) return;
+    Jb[joff[k] + j] = Pb[i];
+  });
+  x.par.for_n(NLn, [&](uint32_t k) {
+    if (code[k] == 0 && joff[k] + plen[k] < Jtot) Jb[joff[k] + plen[k]] = '\n';
+  });
+  x.par.sync();
+  x.stamp(PH_C4_JOIN);
+  c4_finish(x, c4, n, Jb, Jtot, s_long, s_punct, s_few, r, src);
+  return true;
+}
+
 // `wout` (optional): the rewrite's word count when it comes from the stage's line export (the
 // only path a dictionary-script document takes here; kNoWords stays otherwise)
 // `hls` (optional): a dictionary-script document's per-line word statistics from the host (ICU,
@@ -2419,11 +2632,16 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
   // A citation needs a '[' followed by a digit: without one (the common case) every processed
   // line is its trimmed original line and the plain path runs on the original bytes.
   const bool maybe_cite = c4.remove_citations != 0 && (scan & C4S_CITE);
-  if (TB_C4_PLAIN && !maybe_cite && line_stats && c4.split_paragraph) {
+  if (TB_C4_PLAIN && line_stats && c4.split_paragraph) {
     const uint32_t NL = line_stats[0];  // the stage kernel of this content version wrote it
     if (NL != kLineStatsNone) {
-      c4_pass_a_export(x, c4, b, n, line_stats, NL, r, src, scan, wout);
-      return;
+      if (!maybe_cite) {
+        c4_pass_a_export(x, c4, b, n, line_stats, NL, r, src, scan, wout);
+        return;
+      }
+      // (one-wave documents without host line statistics: dictionary-script lines take the
+      // general path, which has the ICU statistics of every processed line)
+      if (P::kWaves <= 1 && !hls && NL > 0 && c4_pass_a_cite_export(x, c4, b, n, line_stats, NL, r, src)) return;
     }
   }
   uint32_t dict = 0;

@@ -2416,7 +2416,7 @@ TB_HD uint32_t c4_cite_end_bytes(const UcdView& ucd, const uint8_t* b, uint32_t 
   return (p < e && b[p] == ']') ? p + 1 : 0;
 }
 
-// C4 pass A for a one-wave document with a possible citation, from the stage's line export: the
+// C4 pass A for a document with a possible citation, from the stage's line export: the
 // citations (reference CITATION_REGEX, c4_filters.rs:33, applied to each trimmed line) are found on
 // the bytes of the exported trimmed line spans, the processed lines Pb are built byte-parallel
 // (a removed-byte bitmap and its prefix popcounts give every kept byte's place), and only the lines
@@ -2639,9 +2639,10 @@ TB_HD void c4_pass_a(DocCtx<P>& x, const DevC4& c4, const uint8_t* b, uint32_t n
         c4_pass_a_export(x, c4, b, n, line_stats, NL, r, src, scan, wout);
         return;
       }
-      // (one-wave documents without host line statistics: dictionary-script lines take the
-      // general path, which has the ICU statistics of every processed line)
-      if (P::kWaves <= 1 && !hls && NL > 0 && c4_pass_a_cite_export(x, c4, b, n, line_stats, NL, r, src)) return;
+      // (documents with host line statistics, i.e. dictionary-script lines, take the general
+      // path, which has the ICU statistics of every processed line; workgroup documents too:
+      // k_c4_pass_a_blk 1.09 -> 0.57 ms/step, profiles/r10_ab_citeblk)
+      if (!hls && NL > 0 && c4_pass_a_cite_export(x, c4, b, n, line_stats, NL, r, src)) return;
     }
   }
   uint32_t dict = 0;

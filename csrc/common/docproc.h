@@ -184,7 +184,7 @@ struct DocCtx {
   const uint64_t* pw = nullptr;  // pw[k] = B^k, k <= pw_n; followed by ipw
   const uint64_t* ipw = nullptr; // ipw[k] = B^-k, k <= pw_n
   uint32_t pw_n = 0;
-  const uint32_t* asc = nullptr; // UCD properties of code points < 128 (LDS copy), or null
+  const uint16_t* asc = nullptr; // compact UCD properties of code points < 256 (LDS copy), or null
   char* scr = nullptr;       // global (HBM) scratch arena of this document
   uint64_t cap = 0;
   uint64_t used = 0;
@@ -348,7 +348,7 @@ TB_HD Cps decode(DocCtx<P>& x, const uint8_t* b, uint32_t n, bool hot = false, u
   }
   if (x.overflow) return c;
   const UcdView ucd = x.ucd;
-  const uint32_t* asc = x.asc;
+  const uint16_t* asc = x.asc;
   uint32_t* ent = c.ent;
   uint32_t* off = c.off;
   uint16_t* pra = c.prop;
@@ -356,21 +356,24 @@ TB_HD Cps decode(DocCtx<P>& x, const uint8_t* b, uint32_t n, bool hot = false, u
   c.n = x.par.template compact<int>(
       n, [&](uint32_t i, int&) { return utf8_is_lead(b[i]); },
       [&](uint32_t i, uint32_t k, int&) {
-        uint32_t p;
-        if (b[i] < 0x80 && asc) {
-          p = asc[b[i]];
+        uint16_t cpk;
+        const uint32_t c0 = b[i];
+        // U+0000..U+00FF (ASCII, and C2 / C3 leads: Latin-1, e.g. æ ø å ä ö é) from the LDS table,
+        // decoded inline; none of them is a dictionary script
+        if (asc && (c0 < 0x80 || (c0 & 0xFEu) == 0xC2u)) {
+          cpk = asc[c0 < 0x80 ? c0 : (((c0 & 0x1Fu) << 6) | (b[i + 1] & 0x3Fu))];
         } else {
           int len;
-          p = ucd.props(utf8_decode(b, i, n, &len));
+          const uint32_t p = ucd.props(utf8_decode(b, i, n, &len));
+          cpk = compact_prop(p);
+          dl |= (p & P_DICT) ? 1u : 0u;
         }
-        const uint16_t cpk = compact_prop(p);
         if (packed) {
           ent[k] = i | ((uint32_t)cpk << 16);
         } else {
           off[k] = i;
           pra[k] = cpk;
         }
-        dl |= (p & P_DICT) ? 1u : 0u;
       });
   const uint32_t cn = c.n;
   x.par.single([&]() {

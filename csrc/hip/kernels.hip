@@ -62,16 +62,17 @@ __device__ __forceinline__ DocCtx<P> make_ctx(const DevTables& t, const uint64_t
   return x;
 }
 
-// Per-wave LDS copies that turn the hottest global reads into LDS reads: the UCD properties of
-// the 128 ASCII code points (every decode looks one up) and, for wave-path documents, the text
+// Per-wave LDS copies that turn the hottest global reads into LDS reads: the compact UCD properties
+// of U+0000..U+00FF (every decode looks up ASCII and Latin-1 letters there instead of the two-level
+// global table) and, for wave-path documents, the text
 // itself (read by every pass: lead bytes, decoding, hashing, byte verification). The text copy
 // moves whole dwords (the batch buffers are padded, so the up to 3 bytes read past a document's
 // end stay inside the allocation).
 template <class P>
 __device__ __forceinline__ void lds_ascii_props(DocCtx<P>& x) {
-  uint32_t* asc = x.template try_lds<uint32_t>(128);
+  uint16_t* asc = x.template try_lds<uint16_t>(256);
   if (!asc) return;
-  x.par.for_n(128, [&](uint32_t c) { asc[c] = x.ucd.props(c); });
+  x.par.for_n(256, [&](uint32_t c) { asc[c] = compact_prop(x.ucd.props(c)); });
   x.par.sync();
   x.asc = asc;
 }
